@@ -1,0 +1,199 @@
+/*
+ * go1_mi355x.h -- C ABI of the MI355X-native Go1 trajectory-tracking step.
+ *
+ * This library replaces, for the hot path of Daffan/legged_tracking, the Isaac
+ * Gym calls inside LeggedRobot.step() and the PyTorch post-physics code around
+ * them (reference: go1_gym/envs/base/legged_robot_trajectory_tracking.py):
+ *
+ *   go1_step()        <- LeggedRobot.step                      :64-112
+ *                         (_compute_torques :957-996, eval_actuator_network
+ *                          :1311-1320, gym.set_dof_actuation_force_tensor /
+ *                          simulate / fetch_results / refresh_dof_state_tensor
+ *                          :82-88, post_physics_step :114-169)
+ *   go1_reset_envs()  <- LeggedRobot.reset_idx                 :218-296
+ *                         (+ gym.set_*_tensor_indexed :1011-1013, :1050-1052)
+ *   go1_set_terrain() <- Terrain env_height_samples / env_terrain_origin
+ *                         (_get_env_origins :1808-1847)
+ *
+ * All device pointers are owned by the caller (PyTorch tensors); the library
+ * never allocates or frees them.  Every call is asynchronous on the caller's
+ * stream (hipStream_t passed as void*), never synchronises the host, and
+ * returns 0 on success or a negative GO1_E* code; go1_last_error() returns a
+ * thread-local message.  No C++ exceptions cross this boundary.
+ * One host thread per handle.
+ */
+#ifndef GO1_MI355X_H
+#define GO1_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GO1_ABI_VERSION 1
+
+#define GO1_NUM_DOF 12
+#define GO1_NUM_BODIES 17
+#define GO1_NUM_TERMS 10
+#define GO1_NUM_SUMS 13
+#define GO1_NUM_OBS 261
+#define GO1_NUM_PRIV 2
+#define GO1_LAG_SLOTS 7
+#define GO1_U_PER_ENV 308
+#define GO1_MODEL_FLOATS 175
+#define GO1_ACTUATOR_FLOATS 1313 /* w1[32][6] b1[32] w2[32][32] b2[32] w3[32] b3[1] */
+#define GO1_GRID_X 21
+#define GO1_GRID_Y 11
+
+enum {
+  GO1_OK = 0,
+  GO1_E_ARG = -1,     /* bad argument / shape */
+  GO1_E_HIP = -2,     /* HIP runtime error */
+  GO1_E_STATE = -3,   /* call order: bind/terrain missing */
+};
+
+/* Static configuration, fixed for the life of a handle.  Values come from the
+ * reference Cfg after config_go1() and scripts/train.py (see
+ * legged_tracking_amd/config.py for the mapping and citations). */
+typedef struct go1_config {
+  int32_t n_envs;
+  int32_t terrain_kind;        /* 0 plane (legged_robot_trajectory_tracking.py:1928-1932), 1 tunnel tiles */
+  int32_t camera_zero;         /* Cfg.env.camera_zero (:400-404) */
+  int32_t measure_front_half;  /* Cfg.terrain.measure_front_half (:395-399) */
+  int32_t add_noise;           /* Cfg.noise.add_noise (:472-473) */
+  int32_t use_terminal_body_height; /* (:205-209) */
+  int32_t custom_origins;      /* trimesh origins draw x/y init noise (:1023-1033) */
+  int32_t decimation;          /* 4 (go1_crawling.py:37) */
+  int32_t n_internal;          /* physics sub-steps per sim step (native integrator) */
+  int32_t rand_interval;       /* ceil(rand_interval_s / dt) (:1873) */
+  int32_t hf_nx, hf_ny;        /* tile pixels: 80 x 40 for single_path */
+  int32_t pad0, pad1;
+  float sim_dt;                /* 0.005 (config.py:355) */
+  float dt;                    /* decimation * sim_dt */
+  float action_scale;          /* 0.25 */
+  float hip_scale_reduction;   /* 0.5 */
+  float clip_actions;          /* 10 (train.py:241) */
+  float clip_obs;              /* 100 */
+  float horizontal_scale;      /* 0.05 */
+  float max_episode_length;    /* ceil(episode_length_s / dt) = 500 */
+  float terminal_body_height;  /* 0.0 */
+  float switch_dist;           /* 0.3 (train.py:169) */
+  float base_height_target;    /* 0.28 */
+  float tracking_sigma_lin;    /* 0.05 */
+  float tracking_sigma_ang;    /* 0.5 */
+  float target_lin_vel;        /* 0.25 */
+  float target_ang_vel;        /* pi/2 */
+  float lin_reaching_criterion;/* 0.3 */
+  float ang_reaching_criterion;/* pi/20 */
+  float t_reach;               /* 0 */
+  float ceiling_height;        /* used when !camera_zero (:406-409) */
+  float obs_scale_dof_pos, obs_scale_dof_vel, obs_scale_heights;
+  float noise_gravity, noise_dof_pos, noise_dof_vel; /* noise_vec entries (:1086-1166) */
+  float camera_offset_x;       /* 0.12 (:1224) */
+  float camera_offset_norm;    /* torch.norm(camera_offset) in f32 */
+  float priv_friction_shift, priv_friction_scale, priv_rest_shift, priv_rest_scale;
+  float strength_range, strength_lo;   /* torch: rand*(max-min)+min, as f32 */
+  float offset_range, offset_lo;
+  float reset_dof_range, reset_dof_lo; /* torch_rand_float(0.5, 1.5) */
+  float reset_vel_range, reset_vel_lo; /* torch_rand_float(-0.5, 0.5) */
+  float x_init_range2, x_init_lo, y_init_range2, y_init_lo, yaw_range2, yaw_lo;
+  float x_init_offset, y_init_offset;
+  float base_init_state[13];
+  float traj_base_x, traj_base_y, traj_base_z, traj_roll, traj_pitch, traj_yaw;
+  float default_dof_pos[12];
+  float dof_pos_limits[24];    /* soft limits (lo, hi) per dof (:702-706) */
+  float torque_limits[12];
+  float hard_limits[24];       /* URDF limits for the native joint-limit model */
+  float height_grid_x[GO1_GRID_X], height_grid_y[GO1_GRID_Y];
+  /* native contact / joint-limit model (no reference equivalent: PhysX is closed) */
+  float contact_stiffness, contact_damping, friction_damping, limit_stiffness, limit_damping;
+  float model[GO1_MODEL_FLOATS];
+  float actuator[GO1_ACTUATOR_FLOATS];
+} go1_config;
+
+/* Per-env state, SoA planes, each row-major (n_envs, width).  f32 unless noted. */
+typedef struct go1_state {
+  float* root;             /* 13: pos3, quat xyzw, lin vel3 (world), ang vel3 (world) */
+  float* dof_pos;          /* 12 */
+  float* dof_vel;          /* 12 */
+  float* last_actions;     /* 12 */
+  float* last_dof_vel;     /* 12 */
+  float* lag;              /* 84: 7 slots x 12, slot 0 oldest (:973-974) */
+  float* pos_err_hist;     /* 24: joint_pos_err_last, _last_last (:985-986) */
+  float* vel_hist;         /* 24: joint_vel_last, _last_last */
+  float* motor_strength;   /* 12 */
+  float* motor_offset;     /* 12 */
+  float* friction;         /* 1 */
+  float* restitution;      /* 1 */
+  float* payload;          /* 1 */
+  int32_t* episode_length; /* 1 */
+  int32_t* curr_pose_index;/* 1 */
+  float* trajectory;       /* 6: x y z roll pitch yaw (traj_length = 1) */
+  float* base_rotation;    /* 3: rpy from the previous step (:929) */
+  int32_t* collision_count;/* 1 */
+  float* episode_sums;     /* 13 (layout.SUM_KEYS) */
+  float* joint_pos_target; /* 12 */
+} go1_state;
+
+/* Terrain: unique tiles (n_tiles, 2, hf_nx, hf_ny) f32 [layer 0 ceiling, 1 floor],
+ * env -> tile index, env terrain origin (n_envs,3) and env origin (n_envs,3). */
+typedef struct go1_terrain {
+  const float* tiles;
+  const int32_t* env_tile;
+  const float* env_terrain_origin;
+  const float* env_origins;
+  int32_t n_tiles;
+  int32_t pad;
+} go1_terrain;
+
+/* Per-call arguments of go1_step. */
+typedef struct go1_step_args {
+  const float* actions;        /* (n_envs, 12) */
+  float gravity_vec[3];        /* normalized gravity used for projected_gravity (:134, :658) */
+  float sim_gravity[3];        /* gravity applied by the integrator (:657-660) */
+  float reward_scales[GO1_NUM_TERMS]; /* already x dt, decayed (:1380-1385, :171-182) */
+  uint64_t rng_seed;
+  uint64_t rng_step;           /* Philox counter: one value per call */
+  const float* uniforms;       /* parity mode: (n_envs, GO1_U_PER_ENV); NULL -> Philox */
+  /* parity mode: injected post-physics state instead of the native integrator */
+  const float* inj_dof;        /* (decimation, n_envs, 12, 2) pos, vel after each sim step */
+  const float* inj_root;       /* (n_envs, 13) after the last sim step */
+  const float* inj_contact;    /* (n_envs, 17, 3) net contact forces */
+  /* outputs */
+  float* obs;                  /* (n_envs, 261) */
+  float* priv;                 /* (n_envs, 2) */
+  float* rew;                  /* (n_envs) */
+  uint8_t* reset;              /* (n_envs) bool */
+  uint8_t* time_out;           /* (n_envs) bool */
+  uint8_t* extras_time_outs;   /* (n_envs) bool, rebound only on steps with a reset (:289-291) */
+  int32_t* any_reset;          /* 1 int, scratch, zeroed by the library */
+  float* contact_forces;       /* (n_envs, 17, 3) or NULL */
+  /* optional debug outputs (NULL = not written) */
+  float* dbg_torques;          /* (decimation, n_envs, 12) */
+  float* dbg_heights;          /* (n_envs, 2, 21, 11) measured heights before camera_zero */
+  float* dbg_terms;            /* (n_envs, 10) unscaled reward terms */
+  float* dbg_commands;         /* (n_envs, 2) */
+  uint8_t* dbg_reached;        /* (n_envs) */
+} go1_step_args;
+
+typedef struct go1_handle go1_handle;
+
+int go1_abi_version(void);
+const char* go1_last_error(void);
+int go1_create(const go1_config* cfg, go1_handle** out);
+int go1_bind(go1_handle* h, const go1_state* state);
+int go1_set_terrain(go1_handle* h, const go1_terrain* terrain);
+int go1_step(go1_handle* h, const go1_step_args* args, void* stream);
+/* Reset envs whose mask[e] != 0: reset_idx semantics (:218-296) incl. DR draws;
+ * uniforms NULL -> Philox(rng_seed, rng_step). */
+int go1_reset_envs(go1_handle* h, const uint8_t* mask, const float* uniforms, uint64_t rng_seed,
+                   uint64_t rng_step, void* stream);
+/* Actuator-net torques for (n_rows, 6) inputs -> (n_rows) (eval_actuator_network :1311-1320). */
+int go1_actuator_net(go1_handle* h, const float* x, float* out, int32_t n_rows, void* stream);
+int go1_destroy(go1_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GO1_MI355X_H */

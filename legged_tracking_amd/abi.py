@@ -1,0 +1,97 @@
+"""ctypes mirror of include/go1_mi355x.h (the C ABI).  Pure host code.
+
+The struct layouts here must match the header field for field; tests/test_abi.py
+checks sizes and offsets against the compiled library's expectations.
+"""
+import ctypes as C
+
+GO1_NUM_DOF = 12
+GO1_NUM_BODIES = 17
+GO1_NUM_TERMS = 10
+GO1_NUM_SUMS = 13
+GO1_NUM_OBS = 261
+GO1_NUM_PRIV = 2
+GO1_LAG_SLOTS = 7
+GO1_U_PER_ENV = 308
+GO1_MODEL_FLOATS = 175
+GO1_ACTUATOR_FLOATS = 1313
+GO1_GRID_X = 21
+GO1_GRID_Y = 11
+
+F = C.c_float
+I32 = C.c_int32
+P = C.c_void_p
+
+
+class Go1Config(C.Structure):
+    _fields_ = [
+        ("n_envs", I32), ("terrain_kind", I32), ("camera_zero", I32), ("measure_front_half", I32),
+        ("add_noise", I32), ("use_terminal_body_height", I32), ("custom_origins", I32), ("decimation", I32),
+        ("n_internal", I32), ("rand_interval", I32), ("hf_nx", I32), ("hf_ny", I32), ("pad0", I32), ("pad1", I32),
+        ("sim_dt", F), ("dt", F), ("action_scale", F), ("hip_scale_reduction", F), ("clip_actions", F),
+        ("clip_obs", F), ("horizontal_scale", F), ("max_episode_length", F), ("terminal_body_height", F),
+        ("switch_dist", F), ("base_height_target", F), ("tracking_sigma_lin", F), ("tracking_sigma_ang", F),
+        ("target_lin_vel", F), ("target_ang_vel", F), ("lin_reaching_criterion", F),
+        ("ang_reaching_criterion", F), ("t_reach", F), ("ceiling_height", F),
+        ("obs_scale_dof_pos", F), ("obs_scale_dof_vel", F), ("obs_scale_heights", F),
+        ("noise_gravity", F), ("noise_dof_pos", F), ("noise_dof_vel", F),
+        ("camera_offset_x", F), ("camera_offset_norm", F),
+        ("priv_friction_shift", F), ("priv_friction_scale", F), ("priv_rest_shift", F), ("priv_rest_scale", F),
+        ("strength_range", F), ("strength_lo", F), ("offset_range", F), ("offset_lo", F),
+        ("reset_dof_range", F), ("reset_dof_lo", F), ("reset_vel_range", F), ("reset_vel_lo", F),
+        ("x_init_range2", F), ("x_init_lo", F), ("y_init_range2", F), ("y_init_lo", F), ("yaw_range2", F),
+        ("yaw_lo", F), ("x_init_offset", F), ("y_init_offset", F),
+        ("base_init_state", F * 13),
+        ("traj_base_x", F), ("traj_base_y", F), ("traj_base_z", F), ("traj_roll", F), ("traj_pitch", F),
+        ("traj_yaw", F),
+        ("default_dof_pos", F * 12), ("dof_pos_limits", F * 24), ("torque_limits", F * 12),
+        ("hard_limits", F * 24), ("height_grid_x", F * GO1_GRID_X), ("height_grid_y", F * GO1_GRID_Y),
+        ("contact_stiffness", F), ("contact_damping", F), ("friction_damping", F), ("limit_stiffness", F),
+        ("limit_damping", F),
+        ("model", F * GO1_MODEL_FLOATS), ("actuator", F * GO1_ACTUATOR_FLOATS),
+    ]
+
+
+class Go1State(C.Structure):
+    _fields_ = [(n, P) for n in (
+        "root", "dof_pos", "dof_vel", "last_actions", "last_dof_vel", "lag", "pos_err_hist", "vel_hist",
+        "motor_strength", "motor_offset", "friction", "restitution", "payload", "episode_length",
+        "curr_pose_index", "trajectory", "base_rotation", "collision_count", "episode_sums",
+        "joint_pos_target")]
+
+
+class Go1Terrain(C.Structure):
+    _fields_ = [("tiles", P), ("env_tile", P), ("env_terrain_origin", P), ("env_origins", P),
+                ("n_tiles", I32), ("pad", I32)]
+
+
+class Go1StepArgs(C.Structure):
+    _fields_ = [
+        ("actions", P), ("gravity_vec", F * 3), ("sim_gravity", F * 3), ("reward_scales", F * GO1_NUM_TERMS),
+        ("rng_seed", C.c_uint64), ("rng_step", C.c_uint64), ("uniforms", P),
+        ("inj_dof", P), ("inj_root", P), ("inj_contact", P),
+        ("obs", P), ("priv", P), ("rew", P), ("reset", P), ("time_out", P), ("extras_time_outs", P),
+        ("any_reset", P), ("contact_forces", P),
+        ("dbg_torques", P), ("dbg_heights", P), ("dbg_terms", P), ("dbg_commands", P), ("dbg_reached", P),
+    ]
+
+
+# state field widths and dtypes (must match go1_state order)
+STATE_SPEC = (
+    ("root", 13, "f32"), ("dof_pos", 12, "f32"), ("dof_vel", 12, "f32"), ("last_actions", 12, "f32"),
+    ("last_dof_vel", 12, "f32"), ("lag", 84, "f32"), ("pos_err_hist", 24, "f32"), ("vel_hist", 24, "f32"),
+    ("motor_strength", 12, "f32"), ("motor_offset", 12, "f32"), ("friction", 1, "f32"),
+    ("restitution", 1, "f32"), ("payload", 1, "f32"), ("episode_length", 1, "i32"),
+    ("curr_pose_index", 1, "i32"), ("trajectory", 6, "f32"), ("base_rotation", 3, "f32"),
+    ("collision_count", 1, "i32"), ("episode_sums", GO1_NUM_SUMS, "f32"), ("joint_pos_target", 12, "f32"),
+)
+assert tuple(n for n, _, _ in STATE_SPEC) == tuple(n for n, _ in Go1State._fields_)
+
+
+def ptr(a):
+    """Raw address of a numpy array or a torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data

@@ -1,0 +1,689 @@
+"""Config contract of the reference (Cfg / config_go1) and its mapping onto the C ABI.
+
+`Cfg` mirrors go1_gym/envs/base/legged_robot_trajectory_tracking_config.py:6-373
+(the attributes the trajectory-tracking step reads); `config_go1` mirrors
+go1_gym/envs/go1/go1_crawling.py:8-106.  Both are plain mutable classes so that
+scripts/train.py:46-241 can mutate them exactly as it mutates the reference's
+params_proto classes.  `vars(Cfg.x)` returns a new dict of public attributes in
+definition order (the reading of params_proto 2.10.5's Meta.__dict__ used by
+the survey; params_proto itself is absent offline).
+
+`build_abi_config()` turns a mutated Cfg into the go1_config struct, computing
+every constant the way torch would (f32 scalars, same operation order).
+"""
+import math
+
+import numpy as np
+
+from . import abi, layout as L, model as M
+
+_TYPE_DICT = type.__dict__["__dict__"]
+
+
+class _Meta(type):
+    """vars(cls) -> fresh dict of public non-callable class attributes."""
+
+    @property
+    def __dict__(cls):
+        out = {}
+        for k, v in _TYPE_DICT.__get__(cls).items():
+            if k.startswith("_") or isinstance(v, (type, staticmethod, classmethod, property)) or callable(v):
+                continue
+            out[k] = v
+        return out
+
+
+class PrefixProto(metaclass=_Meta):
+    def __init_subclass__(cls, **kwargs):
+        pass
+
+
+ParamsProto = PrefixProto
+
+
+def make_cfg():
+    """A fresh Cfg class tree with the reference's defaults (config.py:6-373)."""
+
+    class Cfg(PrefixProto, cli=False):
+        class env(PrefixProto, cli=False):
+            num_envs = 4096
+            num_observations = 235
+            num_scalar_observations = 42
+            num_privileged_obs = 6
+            privileged_future_horizon = 1
+            num_actions = 12
+            num_observation_history = 15
+            env_spacing = 3.
+            send_timeouts = True
+            episode_length_s = 20
+            observe_heights = True
+            observe_vel = True
+            observe_only_ang_vel = False
+            observe_only_lin_vel = False
+            observe_yaw = False
+            observe_contact_states = False
+            observe_command = True
+            observe_height_command = True
+            observe_gait_commands = False
+            observe_timing_parameter = False
+            observe_clock_inputs = False
+            observe_two_prev_actions = False
+            observe_imu = False
+            record_video = True
+            recording_width_px = 360
+            recording_height_px = 240
+            recording_mode = "COLOR"
+            num_recording_envs = 1
+            debug_viz = False
+            all_agents_share = False
+            look_from_back = False
+            priv_observe_friction = True
+            priv_observe_friction_indep = True
+            priv_observe_ground_friction = False
+            priv_observe_ground_friction_per_foot = False
+            priv_observe_restitution = True
+            priv_observe_base_mass = True
+            priv_observe_com_displacement = True
+            priv_observe_motor_strength = False
+            priv_observe_motor_offset = False
+            priv_observe_joint_friction = True
+            priv_observe_Kp_factor = True
+            priv_observe_Kd_factor = True
+            priv_observe_contact_forces = False
+            priv_observe_contact_states = False
+            priv_observe_body_velocity = False
+            priv_observe_foot_height = False
+            priv_observe_body_height = False
+            priv_observe_gravity = False
+            priv_observe_terrain_type = False
+            priv_observe_clock_inputs = False
+            priv_observe_doubletime_clock_inputs = False
+            priv_observe_halftime_clock_inputs = False
+            priv_observe_desired_contact_states = False
+            priv_observe_dummy_variable = False
+            terminate_end_of_trajectory = False
+            use_terminal_body_rotation = False
+            rotate_camera = False
+            camera_zero = True
+            command_xy_only = True
+            viewer_look_at_robot = False
+
+        class terrain(PrefixProto, cli=False):
+            mesh_type = 'trimesh'
+            terrain_type = 'random_pyramid'
+            valid_tunnel_only = False
+            ceiling_height = 0.5
+            start_loc = 0.4
+            x_init_range = 0.
+            y_init_range = 0.
+            x_init_offset = 0.
+            y_init_offset = 0.
+            yaw_init_range = 0.
+            static_friction = 1.0
+            dynamic_friction = 1.0
+            restitution = 0.
+            terrain_ratio_x = 0.5
+            terrain_ratio_y = 0.5
+            terrain_length = 8.0
+            terrain_width = 3.6
+            terrain_border_ratio_x = 0.9
+            terrain_border_ratio_y = 0.5
+            num_rows = 1
+            num_cols = 1
+            horizontal_scale = 0.05
+            vertical_scale = 0.005
+            measured_points_x = np.linspace(-1, 1, 21)
+            measured_points_y = np.linspace(-0.5, 0.5, 11)
+            measure_front_half = True
+            terminate_end_of_trajectory = False
+
+        class commands(PrefixProto, cli=False):
+            switch_upon_reach = True
+            switch_interval = 0.5
+            traj_function = "fixed_target"
+            traj_length = 1
+            num_interpolation = 1
+            base_x = 5.0
+            base_y = 0.0
+            base_z = 0.34
+            base_roll = 0.0
+            base_pitch = 0.0
+            base_yaw = 0.0
+            x_range = 0.4
+            y_range = 0.5
+            z_range = 0.1
+            roll_range = 30 * np.pi / 180
+            pitch_range = 30 * np.pi / 180
+            yaw_range = 180 * np.pi / 180
+            x_mean = 3.6
+            y_mean = 3.6
+            y_eang = 0.4
+            global_reference = False
+            switch_dist = 0.05
+            switch_yaw = 0.5
+            sampling_based_planning = False
+            plan_interval = 10
+
+        class curriculum_thresholds(PrefixProto, cli=False):
+            cl_fix_target = False
+            cl_start_target_dist = 0.5
+            cl_goal_target_dist = 3.6
+            cl_switch_delta = 0.5
+            cl_switch_threshold = 1.0
+
+        class init_state(PrefixProto, cli=False):
+            pos = [0.0, 0.0, 1.]
+            rot = [0.0, 0.0, 0.0, 1.0]
+            lin_vel = [0.0, 0.0, 0.0]
+            ang_vel = [0.0, 0.0, 0.0]
+            default_joint_angles = {"joint_a": 0., "joint_b": 0.}
+
+        class control(PrefixProto, cli=False):
+            control_type = 'actuator_net'
+            stiffness = {'joint_a': 10.0, 'joint_b': 15.}
+            damping = {'joint_a': 1.0, 'joint_b': 1.5}
+            action_scale = 0.5
+            hip_scale_reduction = 1.0
+            decimation = 4
+
+        class asset(PrefixProto, cli=False):
+            file = ""
+            foot_name = "None"
+            penalize_contacts_on = []
+            terminate_after_contacts_on = []
+            disable_gravity = False
+            collapse_fixed_joints = True
+            fix_base_link = False
+            default_dof_drive_mode = 3
+            self_collisions = 0
+            replace_cylinder_with_capsule = True
+            flip_visual_attachments = True
+            density = 0.001
+            angular_damping = 0.
+            linear_damping = 0.
+            max_angular_velocity = 1000.
+            max_linear_velocity = 1000.
+            armature = 0.
+            thickness = 0.01
+
+        class domain_rand(PrefixProto, cli=False):
+            rand_interval_s = 10
+            randomize_motor_strength = False
+            randomize_motor_offset = True
+            motor_offset_range = [-0.02, 0.02]
+            randomize_rigids_after_start = True
+            randomize_friction = True
+            friction_range = [0.5, 1.25]
+            randomize_restitution = False
+            restitution_range = [0, 1.0]
+            randomize_base_mass = False
+            added_mass_range = [-1., 1.]
+            randomize_com_displacement = False
+            com_displacement_range = [-0.15, 0.15]
+            motor_strength_range = [0.9, 1.1]
+            randomize_Kp_factor = False
+            Kp_factor_range = [0.8, 1.3]
+            randomize_Kd_factor = False
+            Kd_factor_range = [0.5, 1.5]
+            gravity_rand_interval_s = 7
+            gravity_impulse_duration = 1.0
+            randomize_gravity = False
+            gravity_range = [-1.0, 1.0]
+            push_robots = True
+            push_interval_s = 15
+            max_push_vel_xy = 1.
+            randomize_lag_timesteps = True
+            lag_timesteps = 6
+
+        class rewards(PrefixProto, cli=False):
+            only_positive_rewards = True
+            only_positive_rewards_ji22_style = False
+            sigma_rew_neg = 5
+            reward_container_name = "RewardsCrawling"
+            target_lin_vel = 0.5
+            lin_reaching_criterion = 0.1
+            tracking_sigma_lin = 0.10
+            target_ang_vel = np.pi / 2.0
+            ang_reaching_criterion = np.pi / 20.
+            tracking_sigma_ang = 0.5
+            use_terminal_body_height = True
+            terminal_body_height = 0.1
+
+        class reward_scales(ParamsProto, cli=False):
+            torques = -0.00001
+            dof_acc = -2.5e-7
+            collision = -1.
+            action_rate = -0.01
+            reaching_linear_vel = 0.0
+            reaching_z = 0.0
+            reaching_yaw = 0.0
+
+        class normalization(PrefixProto, cli=False):
+            clip_observations = 100.
+            clip_actions = 100.
+            friction_range = [0.05, 4.5]
+            ground_friction_range = [0.05, 4.5]
+            restitution_range = [0, 1.0]
+            added_mass_range = [-1., 3.]
+            com_displacement_range = [-0.1, 0.1]
+            motor_strength_range = [0.9, 1.1]
+            motor_offset_range = [-0.05, 0.05]
+            Kp_factor_range = [0.8, 1.3]
+            Kd_factor_range = [0.5, 1.5]
+            joint_friction_range = [0.0, 0.7]
+            contact_force_range = [0.0, 50.0]
+            contact_state_range = [0.0, 1.0]
+            body_velocity_range = [-6.0, 6.0]
+            foot_height_range = [0.0, 0.15]
+            body_height_range = [0.0, 0.60]
+            gravity_range = [-1.0, 1.0]
+            motion = [-0.01, 0.01]
+
+        class obs_scales(PrefixProto, cli=False):
+            lin_vel = 2.0
+            ang_vel = 0.25
+            dof_pos = 1.0
+            dof_vel = 0.05
+            imu = 0.1
+            height_measurements = 0.1
+            friction_measurements = 1.0
+
+        class noise(PrefixProto, cli=False):
+            add_noise = True
+            noise_level = 1.0
+
+        class noise_scales(PrefixProto, cli=False):
+            dof_pos = 0.01
+            dof_vel = 1.5
+            lin_vel = 0.1
+            ang_vel = 0.2
+            imu = 0.1
+            gravity = 0.05
+            contact_states = 0.05
+            height_measurements = 0.1
+            friction_measurements = 0.0
+
+        class viewer(PrefixProto, cli=False):
+            ref_env = 0
+            pos = [10, 0, 6]
+            lookat = [11., 5, 3.]
+
+        class sim(PrefixProto, cli=False):
+            dt = 0.005
+            substeps = 1
+            gravity = [0., 0., -9.81]
+            up_axis = 1
+            use_gpu_pipeline = True
+
+            class physx(PrefixProto, cli=False):
+                num_threads = 10
+                solver_type = 1
+                num_position_iterations = 4
+                num_velocity_iterations = 0
+                contact_offset = 0.01
+                rest_offset = 0.0
+                bounce_threshold_velocity = 0.5
+                max_depenetration_velocity = 1.0
+                max_gpu_contact_pairs = 2 ** 23
+                default_buffer_size_multiplier = 5
+                contact_collection = 2
+
+    return Cfg
+
+
+Cfg = make_cfg()
+
+
+def config_go1(Cnfg):
+    """go1_gym/envs/go1/go1_crawling.py:8-106 (values only)."""
+    _ = Cnfg.init_state
+    _.pos = [0.0, 0.0, 0.34]
+    _.default_joint_angles = {n: v for n, v in zip(L.DOF_NAMES, L.DEFAULT_DOF_POS)}
+    _ = Cnfg.control
+    _.control_type = 'P'
+    _.stiffness = {'joint': 20.}
+    _.damping = {'joint': 0.5}
+    _.action_scale = 0.25
+    _.hip_scale_reduction = 0.5
+    _.decimation = 4
+    _ = Cnfg.asset
+    _.file = '{MINI_GYM_ROOT_DIR}/resources/robots/go1/urdf/go1.urdf'
+    _.foot_name = "foot"
+    _.penalize_contacts_on = ["thigh", "calf"]
+    _.terminate_after_contacts_on = ["base"]
+    _.self_collisions = 0
+    _.flip_visual_attachments = False
+    _.fix_base_link = False
+    _ = Cnfg.rewards
+    _.soft_dof_pos_limit = 0.9
+    _.base_height_target = 0.34
+    _ = Cnfg.reward_scales
+    _.torques = -0.0001
+    _.action_rate = -0.01
+    _.dof_pos_limits = -10.0
+    _.orientation = -5.
+    _.base_height = -30.
+    _ = Cnfg.terrain
+    _.mesh_type = 'trimesh'
+    _.measure_heights = False
+    _.terrain_noise_magnitude = 0.0
+    _.teleport_robots = True
+    _.border_size = 50
+    _.terrain_proportions = [0, 0, 0, 0, 0, 0, 0, 0, 1.0]
+    _.curriculum = False
+    _ = Cnfg.env
+    _.num_observations = 42
+    _.observe_vel = False
+    _.num_envs = 4000
+    _ = Cnfg.commands
+    _.heading_command = False
+    _.resampling_time = 10.0
+    _.command_curriculum = True
+    _.num_lin_vel_bins = 30
+    _.num_ang_vel_bins = 30
+    _.lin_vel_x = [-0.6, 0.6]
+    _.lin_vel_y = [-0.6, 0.6]
+    _.ang_vel_yaw = [-1, 1]
+    _ = Cnfg.domain_rand
+    _.randomize_base_mass = True
+    _.added_mass_range = [-1, 3]
+    _.push_robots = False
+    _.max_push_vel_xy = 0.5
+    _.randomize_friction = True
+    _.friction_range = [0.05, 4.5]
+    _.randomize_restitution = True
+    _.restitution_range = [0.0, 1.0]
+    _.restitution = 0.5
+    _.randomize_com_displacement = True
+    _.com_displacement_range = [-0.1, 0.1]
+    _.randomize_motor_strength = True
+    _.motor_strength_range = [0.9, 1.1]
+    _.randomize_Kp_factor = False
+    _.randomize_Kd_factor = False
+    _.rand_interval_s = 6
+
+
+def readme_config(n_envs=4096, terrain="single_path", rows=32, cols=32, camera_zero=None, domain_rand=True):
+    """Cfg as scripts/train.py:46-241 builds it for the README command
+    (--terrain single_path --measure_front_half --camera_zero --old_ppo
+    --penalty_scaler 1.0 --strategy e2e --terminal_body_height 0.0), with
+    num_envs / terrain grid overridable (train.py:128-130 hard-codes 1024/32/32)."""
+    C = make_cfg()
+    config_go1(C)
+    if camera_zero is None:
+        camera_zero = terrain != "plane"  # plane + camera_zero crashes in the reference (:402)
+    C.env.observe_heights = True
+    C.env.command_type = "xy"
+    C.env.num_observations = 261
+    C.env.num_scalar_observations = 261
+    C.env.num_privileged_obs = 2
+    C.env.num_observation_history = 1
+    C.env.look_from_back = True
+    C.env.terminate_end_of_trajectory = False
+    C.env.record_all_envs = False
+    C.env.episode_length_s = 20
+    C.env.rotate_camera = False
+    C.env.camera_zero = camera_zero
+    C.env.timestep_in_obs = False
+    C.terrain.measure_front_half = True
+    C.asset.penalize_contacts_on = ["thigh", "calf", "base"]
+    C.asset.terminate_after_contacts_on = []
+    C.rewards.small_vel_threshold = 0.1
+    C.rewards.lin_reaching_criterion = 0.3
+    C.rewards.ang_reaching_criterion = np.pi / 20.0
+    C.rewards.only_positive_rewards = False
+    C.rewards.use_terminal_body_height = True
+    C.rewards.terminal_body_height = 0.0
+    C.rewards.lin_vel_form = "exp"
+    C.rewards.tracking_sigma_lin = 0.05
+    C.rewards.base_height_target = 0.28
+    C.rewards.target_lin_vel = 0.25
+    p = 1.0
+    C.reward_scales.dof_acc = -2.5e-7 * p
+    C.reward_scales.torques = -1e-5 * p
+    C.reward_scales.action_rate = -1e-3 * p
+    C.reward_scales.dof_pos_limits = -10.0 * p
+    C.reward_scales.collision = -5.0 * p
+    C.reward_scales.base_height = -20.0 * p
+    C.reward_scales.orientation = -0.0 * p
+    C.reward_scales.ang_vel_xy = -0.001 * p
+    C.reward_scales.large_vel = -0.0 * p
+    C.reward_scales.reaching_z = 0.0
+    C.reward_scales.reaching_roll = 0.0
+    C.reward_scales.reaching_pitch = 0.0
+    C.reward_scales.e2e = 1.0
+    C.rewards.T_reach = 0
+    C.rewards.exploration_steps = 2500
+    C.reward_scales.exploration_lin = 1.0
+    C.reward_scales.exploration_yaw = 0.4
+    C.env.num_envs = n_envs
+    C.terrain.num_cols = cols
+    C.terrain.num_rows = rows
+    if terrain == "plane":
+        C.terrain.mesh_type = 'plane'
+    elif terrain == "single_path":
+        C.terrain.terrain_type = "single_path"
+        C.terrain.terrain_length = 4.0
+        C.terrain.terrain_width = 2.0
+        C.terrain.terrain_ratio_x = 0.9
+        C.terrain.terrain_ratio_y = 0.5
+        C.terrain.ceiling_height = 0.8
+        C.terrain.start_loc = 0.32
+        C.terrain.p_flat = 0.9
+        C.terrain.p_double = 0.6
+        C.env.episode_length_s = 10.0
+        C.commands.sampling_based_planning = False
+    else:
+        raise ValueError(f"terrain {terrain!r}: only plane and single_path are on this path")
+    C.commands.traj_function = "fixed_target"
+    C.commands.traj_length = 1
+    C.commands.num_interpolation = 1
+    C.commands.switch_dist = 0.3
+    C.commands.base_x = C.terrain.terrain_length * C.terrain.terrain_ratio_x - 1.0
+    C.domain_rand.lag_timesteps = 6
+    C.domain_rand.randomize_lag_timesteps = True
+    C.control.control_type = "actuator_net"
+    C.domain_rand.randomize_rigids_after_start = False
+    C.domain_rand.randomize_friction = domain_rand
+    C.env.priv_observe_friction = True
+    C.domain_rand.friction_range = [0.1, 3.0]
+    C.domain_rand.randomize_restitution = domain_rand
+    C.env.priv_observe_restitution = True
+    C.domain_rand.restitution_range = [0.0, 0.4]
+    C.domain_rand.randomize_base_mass = domain_rand
+    C.env.priv_observe_base_mass = False
+    C.domain_rand.added_mass_range = [-1.0, 3.0]
+    C.domain_rand.randomize_gravity = domain_rand
+    C.domain_rand.gravity_range = [-1.0, 1.0]
+    C.domain_rand.gravity_rand_interval_s = 8.0
+    C.domain_rand.gravity_impulse_duration = 0.99
+    C.env.priv_observe_gravity = False
+    C.domain_rand.randomize_com_displacement = False
+    C.env.priv_observe_com_displacement = False
+    C.domain_rand.randomize_motor_strength = domain_rand
+    C.domain_rand.motor_strength_range = [0.9, 1.1]
+    C.domain_rand.randomize_motor_offset = domain_rand
+    C.domain_rand.motor_offset_range = [-0.02, 0.02]
+    C.domain_rand.push_robots = False
+    C.env.priv_observe_motor_strength = False
+    C.env.priv_observe_motor_offset = False
+    C.env.priv_observe_body_velocity = False
+    C.env.priv_observe_body_height = False
+    C.env.priv_observe_desired_contact_states = False
+    C.normalization.friction_range = [0, 1]
+    C.normalization.ground_friction_range = [0, 1]
+    C.normalization.clip_actions = 10.0
+    return C
+
+
+# ------------------------------------------------------------------ derived values
+def derived(cfg):
+    """Values LeggedRobot._parse_cfg computes (legged_robot_trajectory_tracking.py:1860-1878)."""
+    dt = cfg.control.decimation * cfg.sim.dt
+    out = dict(dt=dt, max_episode_length=float(np.ceil(cfg.env.episode_length_s / dt)),
+               rand_interval=int(np.ceil(cfg.domain_rand.rand_interval_s / dt)),
+               gravity_rand_interval=int(np.ceil(cfg.domain_rand.gravity_rand_interval_s / dt)))
+    out["gravity_rand_duration"] = int(np.ceil(out["gravity_rand_interval"] * cfg.domain_rand.gravity_impulse_duration))
+    scales = {}
+    for k, v in vars(cfg.reward_scales).items():
+        if v != 0:
+            scales[k] = v * dt
+    out["reward_scales"] = scales
+    return out
+
+
+def soft_dof_limits(soft=0.9):
+    """_process_dof_props soft limits (:702-706) computed in f32 like torch."""
+    lim = np.zeros((12, 2), np.float32)
+    for i in range(12):
+        lo, hi = L.JOINT_LIMITS[i % 3]
+        lo, hi = np.float32(lo), np.float32(hi)
+        m = (lo + hi) / np.float32(2)
+        r = hi - lo
+        half = np.float32(0.5) * r * np.float32(soft)
+        lim[i, 0] = m - half
+        lim[i, 1] = m + half
+    return lim
+
+
+def f32(x):
+    return float(np.float32(x))
+
+
+# Native physics constants (no reference counterpart: PhysX is closed)
+PHYSICS = dict(contact_stiffness=2.0e4, contact_damping=250.0, friction_damping=150.0,
+               limit_stiffness=150.0, limit_damping=2.0, n_internal=2)
+
+
+def build_abi_config(cfg, n_envs=None, physics=None, actuator=None, hf_shape=(80, 40)):
+    """go1_config for the C ABI from a (mutated) Cfg."""
+    physics = dict(PHYSICS, **(physics or {}))
+    d = derived(cfg)
+    c = abi.Go1Config()
+    n = n_envs if n_envs is not None else cfg.env.num_envs
+    plane = cfg.terrain.mesh_type == "plane"
+    c.n_envs = n
+    c.terrain_kind = 0 if plane else 1
+    c.camera_zero = int(bool(cfg.env.camera_zero))
+    if plane and cfg.env.camera_zero:
+        raise AttributeError("'LeggedRobot' object has no attribute 'camera_pitch_angle' "
+                             "(plane terrain + camera_zero fails in the reference, :402)")
+    c.measure_front_half = int(bool(cfg.terrain.measure_front_half))
+    c.add_noise = int(bool(cfg.noise.add_noise))
+    c.use_terminal_body_height = int(bool(cfg.rewards.use_terminal_body_height))
+    c.custom_origins = 0 if plane else 1
+    c.decimation = cfg.control.decimation
+    c.n_internal = physics["n_internal"]
+    c.rand_interval = d["rand_interval"]
+    c.hf_nx, c.hf_ny = hf_shape
+    c.sim_dt = f32(cfg.sim.dt)
+    c.dt = f32(d["dt"])
+    c.action_scale = f32(cfg.control.action_scale)
+    c.hip_scale_reduction = f32(cfg.control.hip_scale_reduction)
+    c.clip_actions = f32(cfg.normalization.clip_actions)
+    c.clip_obs = f32(cfg.normalization.clip_observations)
+    c.horizontal_scale = f32(cfg.terrain.horizontal_scale)
+    c.max_episode_length = f32(d["max_episode_length"])
+    c.terminal_body_height = f32(cfg.rewards.terminal_body_height)
+    c.switch_dist = f32(cfg.commands.switch_dist)
+    c.base_height_target = f32(cfg.rewards.base_height_target)
+    c.tracking_sigma_lin = f32(cfg.rewards.tracking_sigma_lin)
+    c.tracking_sigma_ang = f32(cfg.rewards.tracking_sigma_ang)
+    c.target_lin_vel = f32(cfg.rewards.target_lin_vel)
+    c.target_ang_vel = f32(cfg.rewards.target_ang_vel)
+    c.lin_reaching_criterion = f32(cfg.rewards.lin_reaching_criterion)
+    c.ang_reaching_criterion = f32(cfg.rewards.ang_reaching_criterion)
+    c.t_reach = f32(getattr(cfg.rewards, "T_reach", 0))
+    c.ceiling_height = f32(cfg.terrain.ceiling_height)
+    c.obs_scale_dof_pos = f32(cfg.obs_scales.dof_pos)
+    c.obs_scale_dof_vel = f32(cfg.obs_scales.dof_vel)
+    c.obs_scale_heights = f32(cfg.obs_scales.height_measurements)
+    # noise_vec (:1110-1117): torch.ones(k) * scale * level (* obs scale), f32 left to right
+    lvl = cfg.noise.noise_level
+    ns = cfg.noise_scales
+    c.noise_gravity = f32(np.float32(np.float32(1.0) * np.float32(ns.gravity)) * np.float32(lvl))
+    c.noise_dof_pos = f32(np.float32(np.float32(np.float32(1.0) * np.float32(ns.dof_pos)) * np.float32(lvl))
+                          * np.float32(cfg.obs_scales.dof_pos))
+    c.noise_dof_vel = f32(np.float32(np.float32(np.float32(1.0) * np.float32(ns.dof_vel)) * np.float32(lvl))
+                          * np.float32(cfg.obs_scales.dof_vel))
+    c.camera_offset_x = f32(0.12)
+    c.camera_offset_norm = f32(np.sqrt(np.float32(0.12) * np.float32(0.12)))
+    fr = cfg.normalization.friction_range
+    rr = cfg.normalization.restitution_range
+    c.priv_friction_scale = f32(2.0 / (fr[1] - fr[0]))
+    c.priv_friction_shift = f32((fr[1] + fr[0]) / 2.0)
+    c.priv_rest_scale = f32(2.0 / (rr[1] - rr[0]))
+    c.priv_rest_shift = f32((rr[1] + rr[0]) / 2.0)
+    dr = cfg.domain_rand
+    lo, hi = dr.motor_strength_range
+    c.strength_range, c.strength_lo = f32(hi - lo), f32(lo)
+    lo, hi = dr.motor_offset_range
+    c.offset_range, c.offset_lo = f32(hi - lo), f32(lo)
+    if not dr.randomize_motor_strength:
+        c.strength_range, c.strength_lo = 0.0, 1.0
+    if not dr.randomize_motor_offset:
+        c.offset_range, c.offset_lo = 0.0, 0.0
+    c.reset_dof_range, c.reset_dof_lo = f32(1.5 - 0.5), f32(0.5)
+    c.reset_vel_range, c.reset_vel_lo = f32(0.5 - (-0.5)), f32(-0.5)
+    t = cfg.terrain
+    c.x_init_range2, c.x_init_lo = f32(t.x_init_range - (-t.x_init_range)), f32(-t.x_init_range)
+    c.y_init_range2, c.y_init_lo = f32(t.y_init_range - (-t.y_init_range)), f32(-t.y_init_range)
+    c.yaw_range2, c.yaw_lo = f32(t.yaw_init_range - (-t.yaw_init_range)), f32(-t.yaw_init_range)
+    c.x_init_offset, c.y_init_offset = f32(t.x_init_offset), f32(t.y_init_offset)
+    init = list(cfg.init_state.pos) + list(cfg.init_state.rot) + list(cfg.init_state.lin_vel) + \
+        list(cfg.init_state.ang_vel)
+    for i, v in enumerate(init):
+        c.base_init_state[i] = f32(v)
+    cm = cfg.commands
+    c.traj_base_x, c.traj_base_y, c.traj_base_z = f32(cm.base_x), f32(cm.base_y), f32(cm.base_z)
+    c.traj_roll, c.traj_pitch, c.traj_yaw = f32(cm.base_roll), f32(cm.base_pitch), 0.0
+    for i, nme in enumerate(L.DOF_NAMES):
+        c.default_dof_pos[i] = f32(cfg.init_state.default_joint_angles[nme])
+    soft = soft_dof_limits(getattr(cfg.rewards, "soft_dof_pos_limit", 1.0))
+    for i in range(12):
+        c.dof_pos_limits[2 * i] = float(soft[i, 0])
+        c.dof_pos_limits[2 * i + 1] = float(soft[i, 1])
+        c.torque_limits[i] = f32(L.TORQUE_LIMIT)
+        lo, hi = L.JOINT_LIMITS[i % 3]
+        c.hard_limits[2 * i], c.hard_limits[2 * i + 1] = f32(lo), f32(hi)
+    for i, v in enumerate(np.asarray(t.measured_points_x, np.float64)):
+        c.height_grid_x[i] = f32(v)
+    for i, v in enumerate(np.asarray(t.measured_points_y, np.float64)):
+        c.height_grid_y[i] = f32(v)
+    for k in ("contact_stiffness", "contact_damping", "friction_damping", "limit_stiffness", "limit_damping"):
+        setattr(c, k, float(physics[k]))
+    for i, v in enumerate(M.model_block()):
+        c.model[i] = float(v)
+    w = actuator if actuator is not None else load_actuator()
+    for i, v in enumerate(w):
+        c.actuator[i] = float(v)
+    return c
+
+
+def load_actuator():
+    """Flat f32 actuator weights (GO1_ACTUATOR_FLOATS), from data/actuator_go1.npz."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "data", "actuator_go1.npz"))
+    flat = np.concatenate([d["w1"].ravel(), d["b1"], d["w2"].ravel(), d["b2"], d["w3"].ravel(), d["b3"]])
+    assert flat.shape == (abi.GO1_ACTUATOR_FLOATS,)
+    return flat.astype(np.float32)
+
+
+def reward_scale_vector(scales: dict):
+    """f32 vector in layout.REWARD_KEYS order."""
+    return np.array([np.float32(scales.get(k, 0.0)) for k in L.REWARD_KEYS], np.float32)
+
+
+def _fmaf(a, b, c):
+    return np.float32(np.float64(a) * np.float64(b) + np.float64(c))
+
+
+def gravity_state(gravities):
+    """_randomize_gravity (:656-660): sim gravity and normalized gravity_vec, f32.
+    torch.norm of a 3-vector is sqrt(fma(z, z, fma(y, y, x*x))) on the CPU."""
+    g = np.asarray(gravities, np.float32) + np.array([0, 0, -9.8], np.float32)
+    s = np.float32(g[0] * g[0])
+    s = _fmaf(g[1], g[1], s)
+    s = _fmaf(g[2], g[2], s)
+    n = np.sqrt(np.float32(s))
+    return g.astype(np.float32), (g / n).astype(np.float32)

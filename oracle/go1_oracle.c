@@ -1,0 +1,1035 @@
+/*
+ * go1_oracle.c -- CPU ORACLE of the Go1 trajectory-tracking step.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or the timed CPU baseline) -- never as the thing measured or shipped.
+ *
+ * It restates, in plain C, the reference algorithm of
+ *   go1_gym/envs/base/legged_robot_trajectory_tracking.py  (cited :line below)
+ *   go1_gym/envs/rewards/reward_crawling.py               (RewardsCrawling)
+ *   go1_gym/envs/trajectories/trajectory_function.py      (_traj_fn_fixed_target)
+ *   go1_gym/utils/math_utils.py                            (quat_apply_yaw_inverse, wrap_to_pi, ...)
+ *   isaacgym.torch_utils (absent; published formulas restated)
+ * with every f32 operation in the order torch evaluates it, so that integer /
+ * boolean outputs (height-scan indices, termination and reset masks) are
+ * bit-exact.  Parity pinned by the tests/golden npz fixtures, generated from the
+ * reference's own code (tests/golden/make_golden.py).
+ *
+ * The rigid-body dynamics (PhysX in the reference, a closed binary that is not
+ * available) is replaced by this build's own floating-base articulated-body
+ * algorithm + heightfield contact, restated here in f64 as the oracle for the
+ * f32 HIP integrator.  Physics parity with PhysX is UNPINNED.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/go1_mi355x.h"
+#include "portable_math.h"
+
+#define NDOF 12
+#define NB 17
+#define PI_F 3.14159265358979323846f
+#define TWO_PI_F ((float)(2.0 * 3.14159265358979323846))
+
+/* ------------------------------------------------------------------ Philox */
+/* Philox4x32-10 (Salmon et al., SC'11).  counter = (env, slot/4, step lo, step hi),
+ * key = seed.  u = (x >> 8) * 2^-24 in [0, 1). */
+static void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = l1; c[2] = n2; c[3] = l0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+float go1o_uniform(uint64_t seed, uint64_t step, uint32_t env, uint32_t slot) {
+  uint32_t c[4] = {env, slot >> 2, (uint32_t)step, (uint32_t)(step >> 32)};
+  philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return (float)(c[slot & 3] >> 8) * (1.0f / 16777216.0f);
+}
+
+static float draw(const go1_step_args* a, const float* U, int n_envs, int e, int slot) {
+  (void)n_envs;
+  if (U) return U[(size_t)e * GO1_U_PER_ENV + slot];
+  return go1o_uniform(a->rng_seed, a->rng_step, (uint32_t)e, (uint32_t)slot);
+}
+
+/* ------------------------------------------------------------ actuator net */
+/* eval_actuator_network (:1311-1320): Linear(6,32) softsign Linear(32,32) softsign
+ * Linear(32,1), each output an fmaf chain over k in increasing order seeded with
+ * the bias (= what an f32-input MFMA computes bit for bit). */
+float go1o_actuator_eval(const float* W, const float x[6]) {
+  const float *w1 = W, *b1 = W + 192, *w2 = W + 224, *b2 = W + 1248, *w3 = W + 1280, *b3 = W + 1312;
+  float h1[32], h2[32];
+  for (int k = 0; k < 32; ++k) {
+    float acc = b1[k];
+    for (int i = 0; i < 6; ++i) acc = fmaf(w1[k * 6 + i], x[i], acc);
+    h1[k] = acc / (fabsf(acc) + 1.0f);
+  }
+  for (int k = 0; k < 32; ++k) {
+    float acc = b2[k];
+    for (int i = 0; i < 32; ++i) acc = fmaf(w2[k * 32 + i], h1[i], acc);
+    h2[k] = acc / (fabsf(acc) + 1.0f);
+  }
+  float acc = b3[0];
+  for (int i = 0; i < 32; ++i) acc = fmaf(w3[i], h2[i], acc);
+  return acc;
+}
+
+void go1o_actuator_batch(const float* W, const float* x, float* out, int n) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) out[i] = go1o_actuator_eval(W, x + (size_t)i * 6);
+}
+
+/* ------------------------------------------------------- torch-order quats */
+/* isaacgym.torch_utils.quat_rotate_inverse, q = (x, y, z, w) */
+static void quat_rotate_inverse_f(const float* q, const float* v, float* out) {
+  float qw = q[3];
+  float s = 2.0f * (qw * qw) - 1.0f;
+  float a0 = v[0] * s, a1 = v[1] * s, a2 = v[2] * s;
+  float c0 = q[1] * v[2] - q[2] * v[1];
+  float c1 = q[2] * v[0] - q[0] * v[2];
+  float c2 = q[0] * v[1] - q[1] * v[0];
+  float b0 = c0 * qw * 2.0f, b1 = c1 * qw * 2.0f, b2 = c2 * qw * 2.0f;
+  float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+  float e0 = q[0] * d * 2.0f, e1 = q[1] * d * 2.0f, e2 = q[2] * d * 2.0f;
+  out[0] = a0 - b0 + e0;
+  out[1] = a1 - b1 + e1;
+  out[2] = a2 - b2 + e2;
+}
+
+/* math_utils.quat_apply_yaw_inverse: zero x,y of q, normalize, rotate inverse */
+static void quat_apply_yaw_inverse_f(const float* q, const float* v, float* out) {
+  float qy[4] = {0.0f, 0.0f, q[2], q[3]};
+  float n2 = fmaf(qy[3], qy[3], fmaf(qy[2], qy[2], fmaf(qy[1], qy[1], qy[0] * qy[0])));
+  float n = sqrtf(n2);
+  if (n < 1e-9f) n = 1e-9f;
+  for (int i = 0; i < 4; ++i) qy[i] = qy[i] / n;
+  quat_rotate_inverse_f(qy, v, out);
+}
+
+/* torch.remainder for f32 divisor b > 0 */
+static float remainder_f(float a, float b) {
+  float m = fmodf(a, b);
+  if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
+  return m;
+}
+
+/* math_utils.wrap_to_pi (in place, :20-24) */
+static float wrap_to_pi_f(float a) {
+  a = remainder_f(a, TWO_PI_F);
+  if (a > PI_F) a = a - TWO_PI_F;
+  return a;
+}
+
+/* quaternion_to_roll_pitch_yaw = wrap_to_pi(get_euler_xyz(q)) (math_utils.py:42-48) */
+static void quat_to_rpy_f(const float* q, float* rpy) {
+  float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+  float sinr = 2.0f * (qw * qx + qy * qz);
+  float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
+  float roll = pm_atan2f(sinr, cosr);
+  float sinp = 2.0f * (qw * qy - qz * qx);
+  float pitch = fabsf(sinp) >= 1.0f ? copysignf(PM_PIO2, sinp) : pm_asinf(sinp);
+  float siny = 2.0f * (qw * qz + qx * qy);
+  float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
+  float yaw = pm_atan2f(siny, cosy);
+  rpy[0] = wrap_to_pi_f(remainder_f(roll, TWO_PI_F));
+  rpy[1] = wrap_to_pi_f(remainder_f(pitch, TWO_PI_F));
+  rpy[2] = wrap_to_pi_f(remainder_f(yaw, TWO_PI_F));
+}
+
+static float norm2_f(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
+static float norm3_f(float x, float y, float z) { return sqrtf(fmaf(z, z, fmaf(y, y, x * x))); }
+static float sq_f(float x) { return x * x; }
+
+/* ====================================================================== */
+/*                      native physics, f64 restatement                    */
+/* ====================================================================== */
+typedef struct { double m[6][6]; } M6;
+
+typedef struct {
+  double mass, com[3], I[3][3]; /* inertia about COM */
+} Body;
+
+typedef struct {
+  Body base;
+  Body leg[4][3];
+  double origin[4][3][3]; /* joint origins in parent frame */
+  double foot[3], foot_r, trunk_half[3], thigh_r, calf_r;
+} Model;
+
+static void load_model(const go1_config* c, Model* M) {
+  const float* p = c->model;
+  int k = 0;
+  Body* bodies[13];
+  bodies[0] = &M->base;
+  for (int l = 0; l < 4; ++l)
+    for (int j = 0; j < 3; ++j) bodies[1 + l * 3 + j] = &M->leg[l][j];
+  for (int b = 0; b < 13; ++b) {
+    Body* B = bodies[b];
+    B->mass = p[k++];
+    for (int i = 0; i < 3; ++i) B->com[i] = p[k++];
+    double xx = p[k++], xy = p[k++], xz = p[k++], yy = p[k++], yz = p[k++], zz = p[k++];
+    B->I[0][0] = xx; B->I[0][1] = xy; B->I[0][2] = xz;
+    B->I[1][0] = xy; B->I[1][1] = yy; B->I[1][2] = yz;
+    B->I[2][0] = xz; B->I[2][1] = yz; B->I[2][2] = zz;
+  }
+  for (int l = 0; l < 4; ++l)
+    for (int j = 0; j < 3; ++j)
+      for (int i = 0; i < 3; ++i) M->origin[l][j][i] = p[k++];
+  for (int i = 0; i < 3; ++i) M->foot[i] = p[k++];
+  M->foot_r = p[k++];
+  for (int i = 0; i < 3; ++i) M->trunk_half[i] = p[k++];
+  M->thigh_r = p[k++];
+  M->calf_r = p[k++];
+}
+
+static void cross3(const double* a, const double* b, double* o) {
+  double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+/* rigid spatial inertia about the body frame origin: [[Ic + m(c.c 1 - c c^T), m c~], [m c~^T, m 1]] */
+static void rigid_inertia(const Body* B, double mass_scale, M6* I) {
+  double m = B->mass * mass_scale;
+  const double* c = B->com;
+  double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+  memset(I, 0, sizeof(*I));
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) I->m[i][j] = B->I[i][j] * mass_scale + m * ((i == j ? cc : 0.0) - c[i] * c[j]);
+  double cx[3][3] = {{0, -c[2], c[1]}, {c[2], 0, -c[0]}, {-c[1], c[0], 0}};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      I->m[i][3 + j] = m * cx[i][j];
+      I->m[3 + j][i] = m * cx[i][j];
+    }
+  for (int i = 0; i < 3; ++i) I->m[3 + i][3 + i] = m;
+}
+
+static void m6_vec(const M6* A, const double* v, double* o) {
+  for (int i = 0; i < 6; ++i) {
+    double s = 0;
+    for (int j = 0; j < 6; ++j) s += A->m[i][j] * v[j];
+    o[i] = s;
+  }
+}
+
+/* spatial force cross product v x* f, v = (w, v), f = (n, f) */
+static void crf(const double* v, const double* f, double* o) {
+  double a[3], b[3], c[3];
+  cross3(v, f, a);
+  cross3(v + 3, f + 3, b);
+  cross3(v, f + 3, c);
+  for (int i = 0; i < 3; ++i) { o[i] = a[i] + b[i]; o[3 + i] = c[i]; }
+}
+
+/* rotation matrix E (parent->child coords) of a revolute joint about unit axis ax by q:
+ * E = Rot(ax, q)^T */
+static void joint_E(int ax, double q, double E[3][3]) {
+  double c = cos(q), s = sin(q);
+  memset(E, 0, sizeof(double) * 9);
+  if (ax == 0) {
+    E[0][0] = 1; E[1][1] = c; E[1][2] = s; E[2][1] = -s; E[2][2] = c;
+  } else {
+    E[1][1] = 1; E[0][0] = c; E[0][2] = -s; E[2][0] = s; E[2][2] = c;
+  }
+}
+
+/* motion transform parent -> child: (w, v) -> (E w, E (v - r x w)) */
+static void xform_motion(double E[3][3], const double* r, const double* vin, double* vout) {
+  double rw[3], t[3];
+  cross3(r, vin, rw);
+  for (int i = 0; i < 3; ++i) t[i] = vin[3 + i] - rw[i];
+  for (int i = 0; i < 3; ++i) {
+    vout[i] = E[i][0] * vin[0] + E[i][1] * vin[1] + E[i][2] * vin[2];
+    vout[3 + i] = E[i][0] * t[0] + E[i][1] * t[1] + E[i][2] * t[2];
+  }
+}
+
+/* force transform child -> parent: (n, f) -> (E^T n + r x E^T f, E^T f) */
+static void xform_force_T(double E[3][3], const double* r, const double* fin, double* fout) {
+  double n[3], f[3], rf[3];
+  for (int i = 0; i < 3; ++i) {
+    n[i] = E[0][i] * fin[0] + E[1][i] * fin[1] + E[2][i] * fin[2];
+    f[i] = E[0][i] * fin[3] + E[1][i] * fin[4] + E[2][i] * fin[5];
+  }
+  cross3(r, f, rf);
+  for (int i = 0; i < 3; ++i) { fout[i] = n[i] + rf[i]; fout[3 + i] = f[i]; }
+}
+
+/* X^T A X for X = motion transform (E, r) */
+static void xform_inertia_T(double E[3][3], const double* r, const M6* A, M6* out) {
+  /* build X explicitly: X = [[E, 0], [-E r~, E]] */
+  double X[6][6];
+  memset(X, 0, sizeof(X));
+  double rx[3][3] = {{0, -r[2], r[1]}, {r[2], 0, -r[0]}, {-r[1], r[0], 0}};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      X[i][j] = E[i][j];
+      X[3 + i][3 + j] = E[i][j];
+      double s = 0;
+      for (int k = 0; k < 3; ++k) s += E[i][k] * rx[k][j];
+      X[3 + i][j] = -s;
+    }
+  double T[6][6];
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) {
+      double s = 0;
+      for (int k = 0; k < 6; ++k) s += A->m[i][k] * X[k][j];
+      T[i][j] = s;
+    }
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) {
+      double s = 0;
+      for (int k = 0; k < 6; ++k) s += X[k][i] * T[k][j];
+      out->m[i][j] = s;
+    }
+}
+
+/* solve SPD 6x6 A x = b (Cholesky) */
+static void solve6(const M6* A, const double* b, double* x) {
+  double L[6][6] = {{0}};
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = A->m[i][j];
+      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+      if (i == j) L[i][i] = sqrt(s > 1e-300 ? s : 1e-300);
+      else L[i][j] = s / L[j][j];
+    }
+  double y[6];
+  for (int i = 0; i < 6; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+}
+
+static void quat_to_R(const double* q, double R[3][3]) {
+  double x = q[0], y = q[1], z = q[2], w = q[3];
+  R[0][0] = 1 - 2 * (y * y + z * z); R[0][1] = 2 * (x * y - z * w); R[0][2] = 2 * (x * z + y * w);
+  R[1][0] = 2 * (x * y + z * w); R[1][1] = 1 - 2 * (x * x + z * z); R[1][2] = 2 * (y * z - x * w);
+  R[2][0] = 2 * (x * z - y * w); R[2][1] = 2 * (y * z + x * w); R[2][2] = 1 - 2 * (x * x + y * y);
+}
+
+/* ---- terrain queries (tile layer 0 ceiling, 1 floor), bilinear at pixel corners */
+typedef struct {
+  const float* tile; /* (2, nx, ny) or NULL for plane */
+  int nx, ny;
+  double ox, oy, hs;
+} TerrainView;
+
+static double tile_at(const TerrainView* T, int layer, int i, int j) {
+  if (i < 0) i = 0;
+  if (i > T->nx - 1) i = T->nx - 1;
+  if (j < 0) j = 0;
+  if (j > T->ny - 1) j = T->ny - 1;
+  return (double)T->tile[((size_t)layer * T->nx + i) * T->ny + j];
+}
+
+/* height and gradient of layer at world (x, y) */
+static void height_query(const TerrainView* T, int layer, double x, double y, double* h, double* gx, double* gy) {
+  if (!T->tile) {
+    *h = layer == 1 ? 0.0 : 1e9;
+    *gx = *gy = 0.0;
+    return;
+  }
+  double u = (x - T->ox) / T->hs, v = (y - T->oy) / T->hs;
+  double fu = floor(u), fv = floor(v);
+  int i = (int)fu, j = (int)fv;
+  double a = u - fu, b = v - fv;
+  double h00 = tile_at(T, layer, i, j), h10 = tile_at(T, layer, i + 1, j);
+  double h01 = tile_at(T, layer, i, j + 1), h11 = tile_at(T, layer, i + 1, j + 1);
+  *h = (1 - a) * (1 - b) * h00 + a * (1 - b) * h10 + (1 - a) * b * h01 + a * b * h11;
+  *gx = ((1 - b) * (h10 - h00) + b * (h11 - h01)) / T->hs;
+  *gy = ((1 - a) * (h01 - h00) + a * (h11 - h10)) / T->hs;
+}
+
+typedef struct {
+  double k, d, kf, mu;
+} ContactParams;
+
+/* penalty contact of a sphere (centre p, velocity pv, radius r) against floor and
+ * ceiling; returns world force F */
+static void sphere_contact(const TerrainView* T, const ContactParams* C, const double* p, const double* pv, double r,
+                           double* F) {
+  F[0] = F[1] = F[2] = 0.0;
+  for (int layer = 1; layer >= 0; --layer) {
+    double h, gx, gy;
+    height_query(T, layer, p[0], p[1], &h, &gx, &gy);
+    double n[3], dv;
+    if (layer == 1) { /* floor, normal up */
+      dv = h + r - p[2];
+      n[0] = -gx; n[1] = -gy; n[2] = 1.0;
+    } else {
+      dv = p[2] + r - h;
+      n[0] = gx; n[1] = gy; n[2] = -1.0;
+    }
+    if (dv <= 0.0) continue;
+    double inv = 1.0 / sqrt(n[0] * n[0] + n[1] * n[1] + 1.0);
+    for (int i = 0; i < 3; ++i) n[i] *= inv;
+    double depth = dv * inv;
+    double vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
+    double fn = C->k * depth - C->d * vn;
+    if (fn <= 0.0) continue;
+    double vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
+    double vtn = sqrt(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
+    double ft = C->kf * vtn, fmax = C->mu * fn;
+    if (ft > fmax) ft = fmax;
+    double s = vtn > 1e-9 ? ft / vtn : 0.0;
+    for (int i = 0; i < 3; ++i) F[i] += fn * n[i] - s * vt[i];
+  }
+}
+
+/* Contact points per leg, in the frame of their link:
+ *   thigh: (0,0,-0.071), (0,0,-0.142), knee (0,0,-0.213)   radius thigh_r
+ *   calf : (0,0,-0.071), (0,0,-0.142)                     radius calf_r
+ *   foot : foot offset (calf frame)                        radius foot_r
+ * Trunk: the 8 corners of the collision box (radius 0). */
+#define N_THIGH_PTS 3
+#define N_CALF_PTS 2
+static const double THIGH_PTS_Z[N_THIGH_PTS] = {-0.071, -0.142, -0.213};
+static const double CALF_PTS_Z[N_CALF_PTS] = {-0.071, -0.142};
+
+typedef struct {
+  double pos[3], quat[4], v[3], w[3];
+  double q[NDOF], qd[NDOF];
+} PhysState;
+
+/* world pose/velocity of a point given body pose (Rb, pb) and body spatial velocity
+ * (w, v) in body coords at body origin */
+static void point_kin(double Rb[3][3], const double* pb, const double* vb, const double* lp, double* pw, double* vw) {
+  double wl[3], vl[3];
+  cross3(vb, lp, wl);
+  for (int i = 0; i < 3; ++i) vl[i] = vb[3 + i] + wl[i];
+  for (int i = 0; i < 3; ++i) {
+    pw[i] = pb[i] + Rb[i][0] * lp[0] + Rb[i][1] * lp[1] + Rb[i][2] * lp[2];
+    vw[i] = Rb[i][0] * vl[0] + Rb[i][1] * vl[1] + Rb[i][2] * vl[2];
+  }
+}
+
+/* world force F at local point lp -> body-coords spatial force (n, f) at origin */
+static void point_force(double Rb[3][3], const double* lp, const double* F, double* fs) {
+  double f[3];
+  for (int i = 0; i < 3; ++i) f[i] = Rb[0][i] * F[0] + Rb[1][i] * F[1] + Rb[2][i] * F[2];
+  double n[3];
+  cross3(lp, f, n);
+  for (int i = 0; i < 3; ++i) { fs[i] += n[i]; fs[3 + i] += f[i]; }
+}
+
+/* One integrator step of length h with torques tau.  Writes net contact forces
+ * per reported body (17 x 3, world) into cf (may be NULL). */
+static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, const double* tau, double h,
+                         const double* g, double friction, double payload, const TerrainView* T, double* cf) {
+  ContactParams C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
+  double R[3][3];
+  quat_to_R(S->quat, R);
+  double vb[6]; /* base spatial velocity, body coords */
+  for (int i = 0; i < 3; ++i) {
+    vb[i] = R[0][i] * S->w[0] + R[1][i] * S->w[1] + R[2][i] * S->w[2];
+    vb[3 + i] = R[0][i] * S->v[0] + R[1][i] * S->v[1] + R[2][i] * S->v[2];
+  }
+  double gb[3];
+  for (int i = 0; i < 3; ++i) gb[i] = R[0][i] * g[0] + R[1][i] * g[1] + R[2][i] * g[2];
+  if (cf) memset(cf, 0, sizeof(double) * NB * 3);
+
+  /* base rigid inertia (payload added to the trunk, inertia scaled by mass ratio) */
+  double mscale = (M->base.mass + payload) / M->base.mass;
+  M6 IA0;
+  rigid_inertia(&M->base, mscale, &IA0);
+  double pA0[6], hmom[6];
+  m6_vec(&IA0, vb, hmom);
+  crf(vb, hmom, pA0);
+  {
+    double fext[6] = {0}, fg[3], cg[3];
+    double m = M->base.mass * mscale;
+    for (int i = 0; i < 3; ++i) fg[i] = m * gb[i];
+    cross3(M->base.com, fg, cg);
+    for (int i = 0; i < 3; ++i) { fext[i] += cg[i]; fext[3 + i] += fg[i]; }
+    for (int cx = 0; cx < 8; ++cx) {
+      double lp[3] = {(cx & 1) ? M->trunk_half[0] : -M->trunk_half[0], (cx & 2) ? M->trunk_half[1] : -M->trunk_half[1],
+                      (cx & 4) ? M->trunk_half[2] : -M->trunk_half[2]};
+      double pw[3], vw[3], F[3];
+      point_kin(R, S->pos, vb, lp, pw, vw);
+      sphere_contact(T, &C, pw, vw, 0.0, F);
+      point_force(R, lp, F, fext);
+      if (cf) for (int i = 0; i < 3; ++i) cf[i] += F[i];
+    }
+    for (int i = 0; i < 6; ++i) pA0[i] -= fext[i];
+  }
+
+  /* per-leg quantities kept for the forward pass */
+  double E[4][3][3][3], vj[4][3][6], cj[4][3][6], U[4][3][6], D[4][3], u[4][3];
+  for (int l = 0; l < 4; ++l) {
+    double Rp[3][3], pp[3], vp[6];
+    memcpy(Rp, R, sizeof(Rp));
+    memcpy(pp, S->pos, sizeof(pp));
+    memcpy(vp, vb, sizeof(vp));
+    M6 IA[3];
+    double pA[3][6], Rw[3][3][3], pw_[3][3];
+    for (int j = 0; j < 3; ++j) {
+      int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
+      const double* r = M->origin[l][j];
+      joint_E(ax, S->q[dof], E[l][j]);
+      xform_motion(E[l][j], r, vp, vj[l][j]);
+      vj[l][j][ax] += S->qd[dof];
+      /* c = v x (S qd) */
+      double sq[3] = {0, 0, 0};
+      sq[ax] = S->qd[dof];
+      cross3(vj[l][j], sq, cj[l][j]);
+      cross3(vj[l][j] + 3, sq, cj[l][j] + 3);
+      /* world pose of the link */
+      double rw[3];
+      for (int i = 0; i < 3; ++i) rw[i] = Rp[i][0] * r[0] + Rp[i][1] * r[1] + Rp[i][2] * r[2];
+      for (int i = 0; i < 3; ++i) {
+        pw_[j][i] = pp[i] + rw[i];
+        for (int k = 0; k < 3; ++k)
+          Rw[j][i][k] = Rp[i][0] * E[l][j][k][0] + Rp[i][1] * E[l][j][k][1] + Rp[i][2] * E[l][j][k][2];
+      }
+      memcpy(Rp, Rw[j], sizeof(Rp));
+      memcpy(pp, pw_[j], sizeof(pp));
+      memcpy(vp, vj[l][j], sizeof(vp));
+    }
+    /* rigid inertias, bias forces, gravity and contact */
+    for (int j = 0; j < 3; ++j) {
+      const Body* B = &M->leg[l][j];
+      rigid_inertia(B, 1.0, &IA[j]);
+      double hm[6];
+      m6_vec(&IA[j], vj[l][j], hm);
+      crf(vj[l][j], hm, pA[j]);
+      double gl[3], fext[6] = {0}, fg[3], cg[3];
+      for (int i = 0; i < 3; ++i) gl[i] = Rw[j][0][i] * g[0] + Rw[j][1][i] * g[1] + Rw[j][2][i] * g[2];
+      for (int i = 0; i < 3; ++i) fg[i] = B->mass * gl[i];
+      cross3(B->com, fg, cg);
+      for (int i = 0; i < 3; ++i) { fext[i] += cg[i]; fext[3 + i] += fg[i]; }
+      int body_idx = 1 + l * 4 + j; /* hip, thigh, calf */
+      if (j == 1) {
+        for (int p = 0; p < N_THIGH_PTS; ++p) {
+          double lp[3] = {0, 0, THIGH_PTS_Z[p]}, pw[3], vw[3], F[3];
+          point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
+          sphere_contact(T, &C, pw, vw, M->thigh_r, F);
+          point_force(Rw[j], lp, F, fext);
+          if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
+        }
+      } else if (j == 2) {
+        for (int p = 0; p < N_CALF_PTS + 1; ++p) {
+          double lp[3], r = p < N_CALF_PTS ? M->calf_r : M->foot_r;
+          if (p < N_CALF_PTS) { lp[0] = 0; lp[1] = 0; lp[2] = CALF_PTS_Z[p]; }
+          else { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
+          double pw[3], vw[3], F[3];
+          point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
+          sphere_contact(T, &C, pw, vw, r, F);
+          point_force(Rw[j], lp, F, fext);
+          int bi = p < N_CALF_PTS ? body_idx : body_idx + 1; /* foot body reported separately */
+          if (cf) for (int i = 0; i < 3; ++i) cf[bi * 3 + i] += F[i];
+        }
+      }
+      for (int i = 0; i < 6; ++i) pA[j][i] -= fext[i];
+    }
+    /* backward pass calf -> hip */
+    for (int j = 2; j >= 0; --j) {
+      int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
+      double t = tau[dof];
+      /* native joint-limit spring-damper at the URDF limits */
+      double lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1];
+      if (S->q[dof] > hi) t -= cfg->limit_stiffness * (S->q[dof] - hi) + cfg->limit_damping * S->qd[dof];
+      else if (S->q[dof] < lo) t -= cfg->limit_stiffness * (S->q[dof] - lo) + cfg->limit_damping * S->qd[dof];
+      for (int i = 0; i < 6; ++i) U[l][j][i] = IA[j].m[i][ax];
+      D[l][j] = IA[j].m[ax][ax];
+      u[l][j] = t - pA[j][ax];
+      M6 Ia;
+      double pa[6], Iac[6];
+      for (int a = 0; a < 6; ++a)
+        for (int b = 0; b < 6; ++b) Ia.m[a][b] = IA[j].m[a][b] - U[l][j][a] * U[l][j][b] / D[l][j];
+      m6_vec(&Ia, cj[l][j], Iac);
+      for (int i = 0; i < 6; ++i) pa[i] = pA[j][i] + Iac[i] + U[l][j][i] * u[l][j] / D[l][j];
+      M6 Ip;
+      double pp2[6];
+      xform_inertia_T(E[l][j], M->origin[l][j], &Ia, &Ip);
+      xform_force_T(E[l][j], M->origin[l][j], pa, pp2);
+      if (j > 0) {
+        for (int a = 0; a < 6; ++a) for (int b = 0; b < 6; ++b) IA[j - 1].m[a][b] += Ip.m[a][b];
+        for (int i = 0; i < 6; ++i) pA[j - 1][i] += pp2[i];
+      } else {
+        for (int a = 0; a < 6; ++a) for (int b = 0; b < 6; ++b) IA0.m[a][b] += Ip.m[a][b];
+        for (int i = 0; i < 6; ++i) pA0[i] += pp2[i];
+      }
+    }
+  }
+  /* base acceleration */
+  double a0[6], mp[6];
+  for (int i = 0; i < 6; ++i) mp[i] = -pA0[i];
+  solve6(&IA0, mp, a0);
+  double qdd[NDOF];
+  for (int l = 0; l < 4; ++l) {
+    double ap[6];
+    memcpy(ap, a0, sizeof(ap));
+    for (int j = 0; j < 3; ++j) {
+      int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
+      double aj[6];
+      xform_motion(E[l][j], M->origin[l][j], ap, aj);
+      for (int i = 0; i < 6; ++i) aj[i] += cj[l][j][i];
+      double Ua = 0;
+      for (int i = 0; i < 6; ++i) Ua += U[l][j][i] * aj[i];
+      qdd[dof] = (u[l][j] - Ua) / D[l][j];
+      aj[ax] += qdd[dof];
+      memcpy(ap, aj, sizeof(ap));
+    }
+  }
+  /* semi-implicit Euler: classical accelerations of the base in world coords */
+  double wv[3], alin_b[3], aw[3], al[3];
+  cross3(vb, vb + 3, wv);
+  for (int i = 0; i < 3; ++i) alin_b[i] = a0[3 + i] + wv[i];
+  for (int i = 0; i < 3; ++i) {
+    aw[i] = R[i][0] * a0[0] + R[i][1] * a0[1] + R[i][2] * a0[2];
+    al[i] = R[i][0] * alin_b[0] + R[i][1] * alin_b[1] + R[i][2] * alin_b[2];
+  }
+  for (int i = 0; i < 3; ++i) {
+    S->w[i] += h * aw[i];
+    S->v[i] += h * al[i];
+    S->pos[i] += h * S->v[i];
+  }
+  {
+    /* q <- exp(h w / 2) (x) q, world-frame angular velocity */
+    double th = 0.5 * h * sqrt(S->w[0] * S->w[0] + S->w[1] * S->w[1] + S->w[2] * S->w[2]);
+    double sc = th > 1e-12 ? sin(th) / (th / (0.5 * h)) : 0.5 * h;
+    double dq[4] = {S->w[0] * sc, S->w[1] * sc, S->w[2] * sc, cos(th)};
+    double* q = S->quat;
+    double nq[4];
+    nq[3] = dq[3] * q[3] - dq[0] * q[0] - dq[1] * q[1] - dq[2] * q[2];
+    nq[0] = dq[3] * q[0] + dq[0] * q[3] + dq[1] * q[2] - dq[2] * q[1];
+    nq[1] = dq[3] * q[1] - dq[0] * q[2] + dq[1] * q[3] + dq[2] * q[0];
+    nq[2] = dq[3] * q[2] + dq[0] * q[1] - dq[1] * q[0] + dq[2] * q[3];
+    double n = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+    for (int i = 0; i < 4; ++i) q[i] = nq[i] / n;
+  }
+  for (int d = 0; d < NDOF; ++d) {
+    S->qd[d] += h * qdd[d];
+    S->q[d] += h * S->qd[d];
+  }
+}
+
+/* exposed for the physics invariant tests: run n substeps of length h on a
+ * state given as doubles; tiles may be NULL (plane) */
+void go1o_physics(const go1_config* cfg, double* pos, double* quat, double* v, double* w, double* q, double* qd,
+                  const double* tau, int n_sub, double h, const double* g, double friction, double payload,
+                  const float* tile, double ox, double oy, double* cf_out) {
+  Model M;
+  load_model(cfg, &M);
+  PhysState S;
+  memcpy(S.pos, pos, 24); memcpy(S.quat, quat, 32); memcpy(S.v, v, 24); memcpy(S.w, w, 24);
+  memcpy(S.q, q, 96); memcpy(S.qd, qd, 96);
+  TerrainView T = {tile, cfg->hf_nx, cfg->hf_ny, ox, oy, cfg->horizontal_scale};
+  for (int i = 0; i < n_sub; ++i) phys_substep(&M, cfg, &S, tau, h, g, friction, payload, &T, cf_out);
+  memcpy(pos, S.pos, 24); memcpy(quat, S.quat, 32); memcpy(v, S.v, 24); memcpy(w, S.w, 24);
+  memcpy(q, S.q, 96); memcpy(qd, S.qd, 96);
+}
+
+/* ====================================================================== */
+/*                              the step                                   */
+/* ====================================================================== */
+static void compute_torques(const go1_config* c, const go1_state* st, int e, const float* act, float* torque) {
+  float* lag = st->lag + (size_t)e * 84;
+  float* eh = st->pos_err_hist + (size_t)e * 24;
+  float* vh = st->vel_hist + (size_t)e * 24;
+  const float* dp = st->dof_pos + (size_t)e * NDOF;
+  const float* dv = st->dof_vel + (size_t)e * NDOF;
+  /* actions_scaled (:969-970); lag push (:973-974) */
+  float scaled[NDOF];
+  for (int d = 0; d < NDOF; ++d) {
+    scaled[d] = act[d] * c->action_scale;
+    if (d % 3 == 0) scaled[d] = scaled[d] * c->hip_scale_reduction;
+  }
+  memmove(lag, lag + NDOF, sizeof(float) * NDOF * (GO1_LAG_SLOTS - 1));
+  memcpy(lag + NDOF * (GO1_LAG_SLOTS - 1), scaled, sizeof(scaled));
+  for (int d = 0; d < NDOF; ++d) {
+    float tgt = lag[d] + c->default_dof_pos[d];
+    st->joint_pos_target[(size_t)e * NDOF + d] = tgt;
+    float err = dp[d] - tgt + st->motor_offset[(size_t)e * NDOF + d];
+    float x[6] = {err, eh[d], eh[NDOF + d], dv[d], vh[d], vh[NDOF + d]};
+    float t = go1o_actuator_eval(c->actuator, x);
+    eh[NDOF + d] = eh[d];
+    eh[d] = err;
+    vh[NDOF + d] = vh[d];
+    vh[d] = dv[d];
+    t = t * st->motor_strength[(size_t)e * NDOF + d];
+    float lim = c->torque_limits[d];
+    torque[d] = t < -lim ? -lim : (t > lim ? lim : t);
+  }
+}
+
+/* _reset_idx for one env (:218-296): DR, dofs, root, trajectory, buffers */
+static void reset_env(const go1_config* c, const go1_state* st, const go1_terrain* ter, int e, const go1_step_args* a,
+                      const float* U) {
+  int n = c->n_envs;
+  /* _randomize_dof_props (:744-754) */
+  float us = draw(a, U, n, e, 0);
+  float s = us * c->strength_range + c->strength_lo;
+  for (int d = 0; d < NDOF; ++d) {
+    st->motor_strength[(size_t)e * NDOF + d] = s;
+    float uo = draw(a, U, n, e, 1 + d);
+    st->motor_offset[(size_t)e * NDOF + d] = uo * c->offset_range + c->offset_lo;
+  }
+  /* _reset_dofs (:998-1008) */
+  for (int d = 0; d < NDOF; ++d) {
+    float u = draw(a, U, n, e, 13 + d);
+    float f = c->reset_dof_range * u + c->reset_dof_lo;
+    st->dof_pos[(size_t)e * NDOF + d] = c->default_dof_pos[d] * f;
+    st->dof_vel[(size_t)e * NDOF + d] = 0.0f;
+  }
+  /* _reset_root_states (:1015-1052) */
+  float* r = st->root + (size_t)e * 13;
+  for (int i = 0; i < 13; ++i) r[i] = c->base_init_state[i];
+  const float* eo = ter->env_origins + (size_t)e * 3;
+  r[0] = r[0] + eo[0];
+  r[1] = r[1] + eo[1];
+  r[2] = r[2] + eo[2];
+  if (c->custom_origins) {
+    float ux = draw(a, U, n, e, 25), uy = draw(a, U, n, e, 26);
+    r[0] = r[0] + (c->x_init_range2 * ux + c->x_init_lo);
+    r[1] = r[1] + (c->y_init_range2 * uy + c->y_init_lo);
+    r[0] = r[0] + c->x_init_offset;
+    r[1] = r[1] + c->y_init_offset;
+  }
+  float yaw = c->yaw_range2 * draw(a, U, n, e, 27) + c->yaw_lo;
+  /* quat_from_angle_axis(yaw, z) then quat_unit */
+  float th = yaw / 2.0f;
+  float sth, cth;
+  pm_sincosf(th, &sth, &cth);
+  float qv[4] = {0.0f * sth, 0.0f * sth, 1.0f * sth, cth};
+  float qn = sqrtf(fmaf(qv[3], qv[3], fmaf(qv[2], qv[2], fmaf(qv[1], qv[1], qv[0] * qv[0]))));
+  if (qn < 1e-9f) qn = 1e-9f;
+  for (int i = 0; i < 4; ++i) r[3 + i] = qv[i] / qn;
+  for (int i = 0; i < 6; ++i) r[7 + i] = c->reset_vel_range * draw(a, U, n, e, 28 + i) + c->reset_vel_lo;
+  /* _resample_trajectory + _traj_fn_fixed_target (trajectory_function.py:14-26) */
+  st->curr_pose_index[e] = 0;
+  float* tr = st->trajectory + (size_t)e * 6;
+  tr[0] = c->traj_base_x + r[0];
+  tr[1] = c->traj_base_y + r[1];
+  tr[2] = c->traj_base_z;
+  tr[3] = c->traj_roll;
+  tr[4] = c->traj_pitch;
+  tr[5] = c->traj_yaw;
+  /* buffers (:246-254, :262, :273, :295-296) */
+  for (int d = 0; d < NDOF; ++d) {
+    st->last_actions[(size_t)e * NDOF + d] = 0.0f;
+    st->last_dof_vel[(size_t)e * NDOF + d] = 0.0f;
+  }
+  st->episode_length[e] = 0;
+  for (int k = 0; k < GO1_NUM_SUMS; ++k) st->episode_sums[(size_t)e * GO1_NUM_SUMS + k] = 0.0f;
+  st->collision_count[e] = 0;
+  for (int i = 0; i < 84; ++i) st->lag[(size_t)e * 84 + i] = 0.0f;
+}
+
+int go1o_reset_envs(const go1_config* c, const go1_state* st, const go1_terrain* ter, const uint8_t* mask,
+                    const float* U, uint64_t seed, uint64_t step) {
+  go1_step_args a;
+  memset(&a, 0, sizeof(a));
+  a.rng_seed = seed;
+  a.rng_step = step;
+  for (int e = 0; e < c->n_envs; ++e)
+    if (mask[e]) reset_env(c, st, ter, e, &a, U);
+  return 0;
+}
+
+/* Full step for env e.  Returns nothing; writes outputs. */
+static void step_env(const go1_config* c, const Model* M, const go1_state* st, const go1_terrain* ter,
+                     const go1_step_args* a, int e) {
+  const int n = c->n_envs;
+  const float* U = a->uniforms;
+  float act[NDOF];
+  for (int d = 0; d < NDOF; ++d) {
+    float x = a->actions[(size_t)e * NDOF + d];
+    act[d] = x < -c->clip_actions ? -c->clip_actions : (x > c->clip_actions ? c->clip_actions : x);
+  }
+  float* root = st->root + (size_t)e * 13;
+  float* dp = st->dof_pos + (size_t)e * NDOF;
+  float* dv = st->dof_vel + (size_t)e * NDOF;
+  float torque[NDOF];
+  float cf[NB * 3];
+  memset(cf, 0, sizeof(cf));
+  const float* tile = NULL;
+  double ox = 0, oy = 0;
+  if (c->terrain_kind == 1) {
+    tile = ter->tiles + (size_t)ter->env_tile[e] * 2 * c->hf_nx * c->hf_ny;
+    ox = ter->env_terrain_origin[(size_t)e * 3];
+    oy = ter->env_terrain_origin[(size_t)e * 3 + 1];
+  }
+  PhysState S;
+  if (!a->inj_dof) {
+    for (int i = 0; i < 3; ++i) {
+      S.pos[i] = root[i]; S.v[i] = root[7 + i]; S.w[i] = root[10 + i];
+    }
+    for (int i = 0; i < 4; ++i) S.quat[i] = root[3 + i];
+    for (int d = 0; d < NDOF; ++d) { S.q[d] = dp[d]; S.qd[d] = dv[d]; }
+  }
+  for (int sub = 0; sub < c->decimation; ++sub) {
+    compute_torques(c, st, e, act, torque);
+    if (a->dbg_torques)
+      for (int d = 0; d < NDOF; ++d) a->dbg_torques[((size_t)sub * n + e) * NDOF + d] = torque[d];
+    if (a->inj_dof) {
+      const float* id = a->inj_dof + ((size_t)sub * n + e) * NDOF * 2;
+      for (int d = 0; d < NDOF; ++d) { dp[d] = id[2 * d]; dv[d] = id[2 * d + 1]; }
+    } else {
+      double tau[NDOF], g[3] = {a->sim_gravity[0], a->sim_gravity[1], a->sim_gravity[2]};
+      double cfd[NB * 3];
+      for (int d = 0; d < NDOF; ++d) tau[d] = torque[d];
+      TerrainView T = {tile, c->hf_nx, c->hf_ny, ox, oy, c->horizontal_scale};
+      double h = (double)c->sim_dt / c->n_internal;
+      for (int k = 0; k < c->n_internal; ++k)
+        phys_substep(M, c, &S, tau, h, g, st->friction[e], st->payload[e], &T, cfd);
+      for (int d = 0; d < NDOF; ++d) { dp[d] = (float)S.q[d]; dv[d] = (float)S.qd[d]; }
+      for (int i = 0; i < NB * 3; ++i) cf[i] = (float)cfd[i];
+    }
+  }
+  if (a->inj_dof) {
+    for (int i = 0; i < 13; ++i) root[i] = a->inj_root[(size_t)e * 13 + i];
+    for (int i = 0; i < NB * 3; ++i) cf[i] = a->inj_contact[(size_t)e * NB * 3 + i];
+  } else {
+    for (int i = 0; i < 3; ++i) {
+      root[i] = (float)S.pos[i]; root[7 + i] = (float)S.v[i]; root[10 + i] = (float)S.w[i];
+    }
+    for (int i = 0; i < 4; ++i) root[3 + i] = (float)S.quat[i];
+  }
+  if (a->contact_forces)
+    for (int i = 0; i < NB * 3; ++i) a->contact_forces[(size_t)e * NB * 3 + i] = cf[i];
+
+  /* ---------------- post_physics_step (:114-169) */
+  int ep = st->episode_length[e] + 1;
+  st->episode_length[e] = ep;
+  float q[4] = {root[3], root[4], root[5], root[6]};
+  float blv[3], bav[3], pg[3];
+  quat_rotate_inverse_f(q, root + 7, blv);
+  quat_rotate_inverse_f(q, root + 10, bav);
+  quat_rotate_inverse_f(q, a->gravity_vec, pg);
+
+  /* _get_heights (:1918-1965), camera pitch = previous step's base_rotation */
+  float* brot = st->base_rotation + (size_t)e * 3;
+  float cam_pitch = brot[1];
+  float heights[2][GO1_GRID_X][GO1_GRID_Y];
+  if (c->terrain_kind == 1) {
+    const float* eto = ter->env_terrain_origin + (size_t)e * 3;
+    float cos_p = pm_cosf(cam_pitch);
+    float camx = c->camera_offset_x * cos_p;
+    float camy = 0.0f * cos_p;
+    for (int i = 0; i < GO1_GRID_X; ++i)
+      for (int j = 0; j < GO1_GRID_Y; ++j) {
+        float px = c->height_grid_x[i] + root[0];
+        float py = c->height_grid_y[j] + root[1];
+        if (c->camera_zero) { px = px + camx; py = py + camy; }
+        px = px - eto[0];
+        py = py - eto[1];
+        long ix = (long)(px / c->horizontal_scale);
+        long iy = (long)(py / c->horizontal_scale);
+        if (ix < 0) ix = 0;
+        if (ix > c->hf_nx - 2) ix = c->hf_nx - 2;
+        if (iy < 0) iy = 0;
+        if (iy > c->hf_ny - 2) iy = c->hf_ny - 2;
+        for (int layer = 0; layer < 2; ++layer)
+          heights[layer][i][j] = tile[((size_t)layer * c->hf_nx + ix) * c->hf_ny + iy];
+      }
+  } else {
+    for (int i = 0; i < GO1_GRID_X; ++i)
+      for (int j = 0; j < GO1_GRID_Y; ++j) { heights[0][i][j] = 1.0f; heights[1][i][j] = 0.0f; }
+  }
+  if (a->dbg_heights) memcpy(a->dbg_heights + (size_t)e * 2 * GO1_GRID_X * GO1_GRID_Y, heights, sizeof(heights));
+
+  /* _plan_target_pose / _compute_relative_target_pose (:850-932) */
+  float* tr = st->trajectory + (size_t)e * 6;
+  float rel_in[3] = {tr[0] - root[0], tr[1] - root[1], tr[2] - root[2]};
+  float rel_lin[3];
+  quat_apply_yaw_inverse_f(q, rel_in, rel_lin);
+  float rpy[3];
+  quat_to_rpy_f(q, rpy);
+  float rel_rot[3];
+  for (int i = 0; i < 3; ++i) rel_rot[i] = wrap_to_pi_f(tr[3 + i] - rpy[i]);
+  for (int i = 0; i < 3; ++i) brot[i] = rpy[i];
+  float cmd[2] = {rel_lin[0], rel_lin[1]}; /* command_type "xy" (:801-802) */
+
+  /* DR every rand_interval (:822-824) */
+  if (ep % c->rand_interval == 0) {
+    float us = draw(a, U, n, e, 34);
+    float s = us * c->strength_range + c->strength_lo;
+    for (int d = 0; d < NDOF; ++d) {
+      st->motor_strength[(size_t)e * NDOF + d] = s;
+      st->motor_offset[(size_t)e * NDOF + d] = draw(a, U, n, e, 35 + d) * c->offset_range + c->offset_lo;
+    }
+  }
+  /* switch / reached (:836-844), traj_length = 1 */
+  float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
+  int switched = rel_norm < c->switch_dist;
+  int idx = st->curr_pose_index[e];
+  if (switched) { idx += 1; if (idx > 0) idx = 0; }
+  st->curr_pose_index[e] = idx;
+  int reached = switched && idx == 0;
+  if (a->dbg_reached) a->dbg_reached[e] = (uint8_t)reached;
+  /* collision_count (:848): thigh x4, calf x4, base */
+  static const int PEN[9] = {2, 6, 10, 14, 3, 7, 11, 15, 0};
+  float coll = 0.0f;
+  for (int k = 0; k < 9; ++k) {
+    const float* f = cf + PEN[k] * 3;
+    if (norm3_f(f[0], f[1], f[2]) > 0.1f) coll += 1.0f;
+  }
+  st->collision_count[e] += (int)coll;
+
+  /* check_termination (:198-216) */
+  int time_out = (float)ep > c->max_episode_length;
+  int reset = time_out;
+  if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = 1;
+
+  /* compute_reward (:320-355) with RewardsCrawling terms */
+  float terms[GO1_NUM_TERMS];
+  {
+    float s = 0.0f;
+    for (int d = 0; d < NDOF; ++d) s += sq_f(torque[d]);
+    terms[0] = s;
+    const float* ldv = st->last_dof_vel + (size_t)e * NDOF;
+    s = 0.0f;
+    for (int d = 0; d < NDOF; ++d) s += sq_f((ldv[d] - dv[d]) / c->dt);
+    terms[1] = s;
+    terms[2] = coll;
+    const float* la = st->last_actions + (size_t)e * NDOF;
+    s = 0.0f;
+    for (int d = 0; d < NDOF; ++d) s += sq_f(la[d] - act[d]);
+    terms[3] = s;
+    s = 0.0f;
+    for (int d = 0; d < NDOF; ++d) {
+      float lo = dp[d] - c->dof_pos_limits[2 * d];
+      float hi = dp[d] - c->dof_pos_limits[2 * d + 1];
+      float o = -(lo < 0.0f ? lo : 0.0f);
+      o = o + (hi > 0.0f ? hi : 0.0f);
+      s += o;
+    }
+    terms[4] = s;
+    terms[5] = sq_f(root[2] - c->base_height_target);
+    terms[6] = sq_f(bav[0]) + sq_f(bav[1]);
+    /* e2e (reward_crawling.py:61-77) */
+    float mag = norm2_f(rel_lin[0], rel_lin[1]);
+    float lerr = sq_f(blv[0]) + sq_f(blv[1]);
+    float r_e2e = expf(-lerr / c->tracking_sigma_lin);
+    terms[7] = r_e2e * (mag < c->switch_dist ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
+    /* exploration_lin (:79-94) */
+    float tx = rel_lin[0] / (mag + 1e-6f) * c->target_lin_vel;
+    float ty = rel_lin[1] / (mag + 1e-6f) * c->target_lin_vel;
+    float gate = mag > c->lin_reaching_criterion ? 1.0f : 0.0f;
+    tx = tx * gate;
+    ty = ty * gate;
+    float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
+    terms[8] = expf(-le / c->tracking_sigma_lin);
+    /* exploration_yaw (:110-120) */
+    float ta = rel_rot[2];
+    float m = fabsf(ta);
+    ta = ta / (m + 1e-6f) * c->target_ang_vel;
+    ta = ta * (m > c->ang_reaching_criterion ? 1.0f : 0.0f);
+    float ae = sq_f(ta - bav[2]);
+    terms[9] = expf(-ae / c->tracking_sigma_ang);
+  }
+  if (a->dbg_terms) memcpy(a->dbg_terms + (size_t)e * GO1_NUM_TERMS, terms, sizeof(terms));
+  float rew = 0.0f, pos = 0.0f, neg = 0.0f;
+  float* sums = st->episode_sums + (size_t)e * GO1_NUM_SUMS;
+  for (int k = 0; k < GO1_NUM_TERMS; ++k) {
+    float r = terms[k] * a->reward_scales[k];
+    rew = rew + r;
+    /* sign of torch.sum(rew) == sign of the scale for these sign-definite terms */
+    if (a->reward_scales[k] >= 0.0f) pos = pos + r; else neg = neg + r;
+    sums[k] = sums[k] + r;
+  }
+  sums[10] = sums[10] + rew;
+  sums[11] = sums[11] + pos;
+  sums[12] = sums[12] + neg;
+
+  /* reset_idx (:218-296) for this env.  self.commands is a VIEW of
+   * local_relative_linear[:, :2] (:802), which reset_idx zeroes in place (:252),
+   * so a reset env observes a zero command this step. */
+  if (reset) {
+    reset_env(c, st, ter, e, a, U);
+    cmd[0] = 0.0f;
+    cmd[1] = 0.0f;
+  }
+  if (a->dbg_commands) { a->dbg_commands[e * 2] = cmd[0]; a->dbg_commands[e * 2 + 1] = cmd[1]; }
+
+  /* compute_observations (:357-475) -- post-reset dof/root, pre-reset gravity/cmd/heights */
+  float* o = a->obs + (size_t)e * GO1_NUM_OBS;
+  o[0] = pg[0]; o[1] = pg[1]; o[2] = pg[2];
+  o[3] = cmd[0] * 1.0f; o[4] = cmd[1] * 1.0f;
+  for (int d = 0; d < NDOF; ++d) {
+    o[5 + d] = (dp[d] - c->default_dof_pos[d]) * c->obs_scale_dof_pos;
+    o[17 + d] = dv[d] * c->obs_scale_dof_vel;
+    o[29 + d] = act[d];
+  }
+  int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
+  int k = 41;
+  float zroot = root[2];
+  float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
+  for (int layer = 0; layer < 2; ++layer)
+    for (int i = x_start; i < GO1_GRID_X; ++i)
+      for (int j = 0; j < GO1_GRID_Y; ++j) {
+        float h = heights[layer][i][j];
+        if (c->camera_zero) {
+          h = h - zroot;
+          h = h - cam_z;
+          h = h < -0.3f ? -0.3f : (h > 0.3f ? 0.3f : h);
+        } else {
+          h = h < 0.0f ? 0.0f : (h > c->ceiling_height ? c->ceiling_height : h);
+          h = h / c->ceiling_height;
+          h = h - 0.5f;
+        }
+        o[k++] = h * c->obs_scale_heights;
+      }
+  if (c->add_noise) {
+    for (int i = 0; i < GO1_NUM_OBS; ++i) {
+      float nv = 0.0f;
+      if (i < 3) nv = c->noise_gravity;
+      else if (i >= 5 && i < 17) nv = c->noise_dof_pos;
+      else if (i >= 17 && i < 29) nv = c->noise_dof_vel;
+      float u = draw(a, U, n, e, 47 + i);
+      o[i] = o[i] + (2.0f * u - 1.0f) * nv;
+    }
+  }
+  for (int i = 0; i < GO1_NUM_OBS; ++i) {
+    float v = o[i];
+    o[i] = v < -c->clip_obs ? -c->clip_obs : (v > c->clip_obs ? c->clip_obs : v);
+  }
+  float* pv = a->priv + (size_t)e * GO1_NUM_PRIV;
+  pv[0] = (st->friction[e] - c->priv_friction_shift) * c->priv_friction_scale;
+  pv[1] = (st->restitution[e] - c->priv_rest_shift) * c->priv_rest_scale;
+  for (int i = 0; i < 2; ++i) pv[i] = pv[i] < -c->clip_obs ? -c->clip_obs : (pv[i] > c->clip_obs ? c->clip_obs : pv[i]);
+
+  /* epilogue (:148-153) */
+  for (int d = 0; d < NDOF; ++d) {
+    st->last_actions[(size_t)e * NDOF + d] = act[d];
+    st->last_dof_vel[(size_t)e * NDOF + d] = dv[d];
+  }
+  a->rew[e] = rew;
+  a->reset[e] = (uint8_t)reset;
+  a->time_out[e] = (uint8_t)time_out;
+}
+
+int go1o_step(const go1_config* c, const go1_state* st, const go1_terrain* ter, const go1_step_args* a) {
+  Model M;
+  load_model(c, &M);
+  int any = 0;
+#pragma omp parallel for schedule(static) reduction(| : any)
+  for (int e = 0; e < c->n_envs; ++e) {
+    step_env(c, &M, st, ter, a, e);
+    any |= a->reset[e];
+  }
+  if (a->extras_time_outs && any)
+    for (int e = 0; e < c->n_envs; ++e) a->extras_time_outs[e] = a->time_out[e];
+  return 0;
+}
+
+int go1o_abi_version(void) { return GO1_ABI_VERSION; }

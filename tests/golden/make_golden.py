@@ -1,0 +1,571 @@
+"""Generate golden fixtures by running the REFERENCE's own Python in this container.
+
+Container-only test infrastructure: imports /root/reference (read-only, never
+copied) behind offline stand-ins for Isaac Gym / params_proto / gym / wandb
+(tests/golden/refstubs).  Never runs on the GPU box; the .npz files it writes
+are committed under tests/golden/ and travel instead.
+
+What runs is the reference's real code:
+  * scripts/train.py:train_go1  -- builds Cfg exactly as the README command does
+    (scripts/train.py:46-241); we intercept TrajectoryTrackingEnv construction to
+    capture that Cfg, then shrink num_envs and the terrain grid;
+  * go1_gym/envs/go1/trajectory_tracking/__init__.py TrajectoryTrackingEnv and
+    go1_gym/envs/base/legged_robot_trajectory_tracking.py LeggedRobot -- step(),
+    post_physics_step(), reset_idx(), compute_observations(), rewards, terrain.
+
+Isaac Gym itself is absent (isaacgym==1.0rc4).  A fake gym hands out plain torch
+tensors for root/dof/contact/rigid-body state; its simulate() writes a
+synthetic post-physics state chosen by this harness (a seeded random walk), so
+the fixtures pin everything AROUND the physics: actuator-net torques, height
+scan, targets, rewards, terminations, resets, observations.  Every torch RNG
+draw the reference makes is recorded and scattered into the canonical per-env
+uniform layout the oracle and the HIP kernel consume (legged_tracking_amd/layout.py).
+
+The actuator network is NOT loaded with torch.jit.load (that would execute code
+from a file shipped in the reference); torch.jit.load is patched to return an
+equivalent torch module built from weights extracted as raw data
+(tests/golden/extract_actuator.py).
+
+Usage: python tests/golden/make_golden.py  (writes tests/golden/*.npz)
+"""
+import argparse
+import inspect
+import os
+import sys
+import types
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+sys.dont_write_bytecode = True  # the reference tree is read-only
+os.environ.setdefault("MPLBACKEND", "Agg")
+sys.path.insert(0, os.path.join(HERE, "refstubs"))
+sys.path.insert(1, REF)
+sys.path.insert(2, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from legged_tracking_amd import layout as L  # noqa: E402
+
+# ---------------------------------------------------------------- actuator net
+_W = np.load(os.path.join(REPO, "legged_tracking_amd", "data", "actuator_go1.npz"))
+
+
+class _Softsign(torch.nn.Module):
+    def forward(self, x):
+        return torch.nn.functional.softsign(x)
+
+
+def _actuator_module():
+    m = torch.nn.Sequential(torch.nn.Linear(6, 32), _Softsign(), torch.nn.Linear(32, 32), _Softsign(),
+                            torch.nn.Linear(32, 1))
+    with torch.no_grad():
+        m[0].weight.copy_(torch.from_numpy(_W["w1"]))
+        m[0].bias.copy_(torch.from_numpy(_W["b1"]))
+        m[2].weight.copy_(torch.from_numpy(_W["w2"]))
+        m[2].bias.copy_(torch.from_numpy(_W["b2"]))
+        m[4].weight.copy_(torch.from_numpy(_W["w3"]))
+        m[4].bias.copy_(torch.from_numpy(_W["b3"]))
+    m.requires_grad_(False)
+    return m
+
+
+def _jit_load(path, *a, **k):
+    assert path.endswith("unitree_go1.pt"), path
+    return _actuator_module()
+
+
+torch.jit.load = _jit_load
+
+# ---------------------------------------------------------------- robot asset
+BODY_NAMES = L.BODY_NAMES
+DOF_NAMES = L.DOF_NAMES
+
+
+def _dof_props():
+    dt = np.dtype([("lower", "f4"), ("upper", "f4"), ("velocity", "f4"), ("effort", "f4")])
+    p = np.zeros(12, dtype=dt)
+    for i in range(12):
+        lo, hi = L.JOINT_LIMITS[i % 3]
+        p[i] = (lo, hi, L.JOINT_VEL_LIMIT[i % 3], L.TORQUE_LIMIT)
+    return p
+
+
+class _Props:
+    def __init__(self, **k):
+        self.__dict__.update(k)
+
+
+class FakeGym:
+    """Hands the reference plain torch tensors; simulate() calls the harness hook."""
+
+    hook = None
+
+    def __init__(self):
+        self.n_envs = 0
+        self.tensors = {}
+        self.gravity = None
+        self.torque_log = []
+
+    # --- sim / assets
+    def create_sim(self, *a):
+        return "sim"
+
+    def load_asset(self, sim, root, fname, opts):
+        return "robot" if fname.endswith("go1.urdf") else "arrow"
+
+    def create_box(self, *a):
+        return "box"
+
+    def get_asset_dof_count(self, asset):
+        return 12 if asset == "robot" else 0
+
+    def get_asset_rigid_body_count(self, asset):
+        return 17 if asset == "robot" else 1
+
+    def get_asset_dof_properties(self, asset):
+        return _dof_props()
+
+    def get_asset_rigid_shape_properties(self, asset):
+        return [_Props(friction=1.0, restitution=0.0) for _ in range(17)]
+
+    def get_asset_rigid_body_names(self, asset):
+        return list(BODY_NAMES)
+
+    def get_asset_dof_names(self, asset):
+        return list(DOF_NAMES)
+
+    def create_env(self, *a):
+        self.n_envs += 1
+        return self.n_envs - 1
+
+    def create_actor(self, env, asset, *a):
+        return 0 if asset == "robot" else 1
+
+    def get_actor_rigid_body_properties(self, env, actor):
+        return [_Props(mass=L.BODY_MASS_PHYSX[i], com=None) for i in range(17)]
+
+    def find_actor_rigid_body_handle(self, env, actor, name):
+        return BODY_NAMES.index(name)
+
+    def get_sim_params(self, sim):
+        return _Props(gravity=None)
+
+    def set_sim_params(self, sim, p):
+        g = p.gravity
+        self.gravity = (float(g.x), float(g.y), float(g.z))
+
+    def prepare_sim(self, sim):
+        n = self.n_envs
+        self.tensors = {
+            "root": torch.zeros(2 * n, 13),
+            "dof": torch.zeros(12 * n, 2),
+            "contact": torch.zeros(18 * n, 3),
+            "rigid": torch.zeros(18 * n, 13),
+        }
+
+    def acquire_actor_root_state_tensor(self, sim):
+        return self.tensors["root"]
+
+    def acquire_dof_state_tensor(self, sim):
+        return self.tensors["dof"]
+
+    def acquire_net_contact_force_tensor(self, sim):
+        return self.tensors["contact"]
+
+    def acquire_rigid_body_state_tensor(self, sim):
+        return self.tensors["rigid"]
+
+    def set_dof_actuation_force_tensor(self, sim, t):
+        self.torque_log.append(t.detach().clone())
+
+    def simulate(self, sim):
+        FakeGym.hook(self)
+
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        return lambda *a, **k: None
+
+
+from isaacgym import gymapi  # noqa: E402
+
+gymapi._FACTORY = FakeGym
+
+# ---------------------------------------------------------------- RNG recorder
+_rand_log = []
+_orig_rand, _orig_rand_like, _orig_randint = torch.rand, torch.rand_like, torch.randint
+
+
+def _caller():
+    for fr in inspect.stack()[2:8]:
+        if fr.function in ("_randomize_dof_props", "_reset_dofs", "_reset_root_states", "compute_observations",
+                           "_randomize_gravity", "_randomize_rigid_body_props", "_create_envs", "reset",
+                           "_push_robots", "learn", "act", "mini_batch_generator"):
+            return fr.function
+    return "other"
+
+
+def _rand(*a, **k):
+    out = _orig_rand(*a, **k)
+    _rand_log.append((_caller(), out.clone()))
+    return out
+
+
+def _rand_like(*a, **k):
+    out = _orig_rand_like(*a, **k)
+    _rand_log.append((_caller(), out.clone()))
+    return out
+
+
+def _randint(*a, **k):
+    out = _orig_randint(*a, **k)
+    _rand_log.append((_caller() + ":randint", out.clone()))
+    return out
+
+
+torch.rand, torch.rand_like, torch.randint = _rand, _rand_like, _randint
+
+
+# ---------------------------------------------------------------- Cfg capture
+class _Captured(Exception):
+    pass
+
+
+def capture_cfg(argv):
+    """Run scripts/train.py:train_go1 up to env construction; return its Cfg."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_train", os.path.join(REF, "scripts", "train.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    import go1_gym.envs.go1.trajectory_tracking as tt
+    real = tt.TrajectoryTrackingEnv
+    captured = {}
+
+    class _Intercept:
+        def __init__(self, sim_device, headless, cfg=None, **k):
+            captured["cfg"] = cfg
+            raise _Captured()
+
+    tt.TrajectoryTrackingEnv = _Intercept
+    p = argparse.ArgumentParser()
+    # flag set of scripts/train.py:287-338 (defaults are the reference's)
+    for name, kw in [("--headless", dict(action="store_true")), ("--wandb", dict(action="store_true")),
+                     ("--name", dict(type=str, default="velocity_tracking")), ("--resume", dict(type=str, default="")),
+                     ("--freeze_model", dict(action="store_true")), ("--device", dict(default=0, type=int)),
+                     ("--logdir", dict(type=str, default="/tmp/ref_logs")),
+                     ("--strategy", dict(default="vel")), ("--old_ppo", dict(action="store_true")),
+                     ("--gru", dict(action="store_true")), ("--cnn", dict(action="store_true")),
+                     ("--learning_rate", dict(type=float, default=1e-3)), ("--gamma", dict(type=float, default=0.99)),
+                     ("--exploration_steps", dict(type=int, default=2500)),
+                     ("--normalize_obs", dict(action="store_true")),
+                     ("--num_steps_per_env", dict(type=int, default=24)), ("--command_type", dict(default="xy")),
+                     ("--timestep_in_obs", dict(action="store_true")), ("--num_history", dict(type=int, default=1)),
+                     ("--measure_front_half", dict(action="store_true")),
+                     ("--rotate_camera", dict(action="store_true")), ("--camera_zero", dict(action="store_true")),
+                     ("--blind", dict(action="store_true")),
+                     ("--terminal_body_height", dict(type=float, default=0.0)),
+                     ("--terrain", dict(default="single_path")), ("--no_domain_rand", dict(action="store_true")),
+                     ("--empty_tunnel", dict(action="store_true")), ("--random_target", dict(action="store_true")),
+                     ("--terminate_after_reach", dict(action="store_true")),
+                     ("--lin_vel_form", dict(default="exp")), ("--r_explore_lin", dict(type=float, default=1.0)),
+                     ("--r_explore_yaw", dict(type=float, default=0.4)),
+                     ("--penalty_scaler", dict(type=float, default=1.0)),
+                     ("--only_positive", dict(action="store_true")),
+                     ("--r_orientation", dict(type=float, default=0.0)),
+                     ("--r_base_height", dict(type=float, default=20.0)),
+                     ("--r_ang_vel", dict(type=float, default=0.001)), ("--t_reach", dict(type=int, default=0)),
+                     ("--r_task", dict(type=float, default=1.0)), ("--r_collision", dict(type=float, default=5.0)),
+                     ("--r_large_vel", dict(type=float, default=0.0))]:
+        p.add_argument(name, **kw)
+    mod.args = p.parse_args(argv)
+    try:
+        mod.train_go1(mod.args)
+    except _Captured:
+        pass
+    tt.TrajectoryTrackingEnv = real
+    return captured["cfg"], real
+
+
+# ---------------------------------------------------------------- physics stand-in
+class RandomWalkPhysics:
+    """Seeded synthetic post-physics state (NOT dynamics): a bounded random walk."""
+
+    def __init__(self, env, seed):
+        self.env = env
+        self.g = np.random.default_rng(seed)
+        self.log = []  # per substep: dict of injected tensors
+
+    def __call__(self, gym):
+        T = gym.tensors
+        n = gym.n_envs
+        g = self.g
+        dof = T["dof"].view(n, 12, 2)
+        dof[..., 0] += torch.from_numpy(g.normal(0, 0.05, (n, 12)).astype(np.float32))
+        dof[..., 1] = torch.from_numpy(g.normal(0, 1.5, (n, 12)).astype(np.float32))
+        root = T["root"].view(n, 2, 13)[:, 0]
+        root[:, 0:2] += torch.from_numpy(g.normal(0.01, 0.02, (n, 2)).astype(np.float32))
+        root[:, 2] += torch.from_numpy(g.normal(-0.002, 0.03, (n,)).astype(np.float32))
+        q = root[:, 3:7] + torch.from_numpy(g.normal(0, 0.05, (n, 4)).astype(np.float32))
+        root[:, 3:7] = q / q.norm(dim=1, keepdim=True)
+        root[:, 7:13] = torch.from_numpy(g.normal(0, 0.4, (n, 6)).astype(np.float32))
+        cf = torch.from_numpy(g.normal(0, 2.0, (n, 18, 3)).astype(np.float32))
+        cf *= torch.from_numpy((g.random((n, 18, 1)) < 0.3).astype(np.float32))
+        cf[:, 17] = 0
+        T["contact"].view(n, 18, 3)[:] = cf
+        rb = T["rigid"].view(n, 18, 13)
+        rb[:, :17, 0:3] = root[:, None, 0:3] + torch.from_numpy(g.normal(0, 0.15, (n, 17, 3)).astype(np.float32))
+        self.log.append({"dof": T["dof"].clone(), "root": T["root"].view(n, 2, 13)[:, 0].clone(),
+                         "contact": T["contact"].view(n, 18, 3)[:, :17].clone(),
+                         "feet": rb[:, [4, 8, 12, 16], 0:3].clone()})
+
+
+# ---------------------------------------------------------------- state extraction
+def env_state(env):
+    """Canonical per-env state (legged_tracking_amd/layout.py) read off the reference env."""
+    n = env.num_envs
+    rs = env.root_states[::env.num_actor]
+    s = {
+        "root": rs[:, 0:13].clone(),
+        "dof_pos": env.dof_pos.clone(),
+        "dof_vel": env.dof_vel.clone(),
+        "last_actions": env.last_actions.clone(),
+        "last_dof_vel": env.last_dof_vel.clone(),
+        "lag": torch.stack([b.clone() for b in env.lag_buffer], 1),  # (n, 7, 12), slot 0 oldest
+        "pos_err_hist": torch.stack([env.joint_pos_err_last, env.joint_pos_err_last_last], 1),
+        "vel_hist": torch.stack([env.joint_vel_last, env.joint_vel_last_last], 1),
+        "motor_strength": env.motor_strengths.clone(),
+        "motor_offset": env.motor_offsets.clone(),
+        "friction": env.friction_coeffs[:, 0].clone(),
+        "restitution": env.restitutions[:, 0].clone(),
+        "payload": env.payloads.clone(),
+        "episode_length": env.episode_length_buf.clone(),
+        "curr_pose_index": env.curr_pose_index.clone(),
+        "trajectory": env.trajectories[:, 0, :].clone(),
+        "base_rotation": env.base_rotation.clone(),
+        "collision_count": env.collision_count.clone(),
+        "episode_sums": torch.stack([env.episode_sums[k] for k in L.SUM_KEYS], 1),
+        "joint_pos_target": env.joint_pos_target.clone(),
+    }
+    return {k: v.detach().cpu().numpy() for k, v in s.items()}
+
+
+def scatter_draws(env, log):
+    """Map the recorded torch draws of ONE step onto the canonical per-env layout."""
+    n = env.num_envs
+    u = np.full((n, L.U_PER_ENV), np.nan, dtype=np.float32)
+    ug = np.full((3,), np.nan, dtype=np.float32)
+    ids = scatter_draws.ids  # env ids per call, pushed by the patched reset/dr hooks
+    it = iter(ids)
+    for tag, t in log:
+        a = t.detach().cpu().numpy().astype(np.float32)
+        if tag == "compute_observations":
+            u[:, L.U_NOISE:L.U_NOISE + a.shape[1]] = a
+        elif tag == "_randomize_gravity":
+            ug[:] = a
+        elif tag == "_randomize_dof_props":
+            kind, e = next(it)
+            base = L.U_RESET_STRENGTH if kind == "reset" else L.U_DR_STRENGTH
+            if a.ndim == 1:
+                u[e, base] = a
+            else:
+                u[e, base + 1:base + 13] = a
+        elif tag == "_reset_dofs":
+            kind, e = next(it)
+            u[e, L.U_RESET_DOF:L.U_RESET_DOF + 12] = a
+        elif tag == "_reset_root_states":
+            kind, e = next(it)
+            j = scatter_draws.root_k
+            if a.shape[1] == 6:
+                u[e, L.U_RESET_VEL:L.U_RESET_VEL + 6] = a
+            else:
+                u[e, L.U_RESET_XY + j] = a[:, 0]
+            scatter_draws.root_k = j + 1
+        else:
+            raise RuntimeError(f"unexpected RNG draw in step from {tag}")
+    return u, ug
+
+
+def install_id_tracking(env):
+    """Wrap the reference's own DR/reset helpers to learn which env ids each draw covers."""
+    cls = type(env)
+    orig_dr, orig_dofs, orig_root = cls._randomize_dof_props, cls._reset_dofs, cls._reset_root_states
+    state = {"in_reset": False}
+    orig_reset_idx = cls.reset_idx
+
+    def reset_idx(self, env_ids):
+        state["in_reset"] = True
+        try:
+            return orig_reset_idx(self, env_ids)
+        finally:
+            state["in_reset"] = False
+
+    def dr(self, env_ids, cfg):
+        e = env_ids.cpu().numpy()
+        kind = "reset" if state["in_reset"] else "dr"
+        if len(e):
+            scatter_draws.ids.extend([(kind, e), (kind, e)])
+        return orig_dr(self, env_ids, cfg)
+
+    def dofs(self, env_ids, cfg):
+        scatter_draws.ids.append(("reset", env_ids.cpu().numpy()))
+        return orig_dofs(self, env_ids, cfg)
+
+    def root(self, env_ids, cfg):
+        e = env_ids.cpu().numpy()
+        k = 4 if self.custom_origins else 2
+        scatter_draws.ids.extend([("reset", e)] * k)
+        if not self.custom_origins:
+            scatter_draws.root_k = 2
+        return orig_root(self, env_ids, cfg)
+
+    cls.reset_idx, cls._randomize_dof_props, cls._reset_dofs, cls._reset_root_states = reset_idx, dr, dofs, root
+
+
+scatter_draws.ids = []
+scatter_draws.root_k = 0
+
+
+def build_env(terrain, n_envs, rows, seed, extra_argv=()):
+    argv = ["--terrain", terrain, "--measure_front_half", "--old_ppo", "--penalty_scaler", "1.0",
+            "--strategy", "e2e", "--terminal_body_height", "0.0", *extra_argv]
+    if terrain != "plane":
+        argv.append("--camera_zero")
+    cfg, Env = capture_cfg(argv)
+    cfg.env.num_envs = n_envs
+    cfg.terrain.num_rows = rows
+    cfg.terrain.num_cols = rows
+    # seeding as scripts/train.py:33-40 does
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    env = Env(sim_device="cpu", headless=True, cfg=cfg)
+    return env, cfg
+
+
+def run(terrain, n_envs, rows, n_steps, seed, out, extra_argv=(), actions_scale=1.0, counter_start=None):
+    env, cfg = build_env(terrain, n_envs, rows, seed, extra_argv)
+    install_id_tracking(env)
+    term_log = {}
+
+    def _wrap(name, fn):
+        def w():
+            out = fn()
+            term_log[name] = out.detach().clone()
+            return out
+        return w
+
+    env.reward_functions = [_wrap(nm, fn) for nm, fn in zip(env.reward_names, env.reward_functions)]
+    # measured_heights is later modified in place by the camera_zero branch of
+    # compute_observations (:399-403); record _get_heights' own output
+    orig_gh = env._get_heights
+
+    def _gh(env_ids):
+        out = orig_gh(env_ids)
+        term_log["heights"] = out.detach().clone()
+        return out
+
+    env._get_heights = _gh
+    assert tuple(env.reward_names) == L.REWARD_KEYS, env.reward_names
+    gym = env.gym
+    phys = RandomWalkPhysics(env, seed + 1)
+    FakeGym.hook = phys
+    n = env.num_envs
+    rec = {"static": {}, "steps": []}
+    st = rec["static"]
+    st["env_height_samples"] = (env.env_height_samples.numpy() if terrain != "plane"
+                                else np.zeros((n, 2, 1, 1), np.float32))
+    st["env_terrain_origin"] = (env.env_terrain_origin.numpy() if terrain != "plane" else np.zeros((n, 3), np.float32))
+    st["env_origins"] = env.env_origins.numpy()
+    st["default_dof_pos"] = env.default_dof_pos.numpy()[0]
+    st["dof_pos_limits"] = env.dof_pos_limits.numpy()
+    st["torque_limits"] = env.torque_limits.numpy()
+    st["max_episode_length"] = np.float64(env.max_episode_length)
+    st["reward_scales"] = np.array([env.reward_scales[k] for k in L.REWARD_KEYS], np.float64)
+    st["reward_keys"] = np.array(list(env.reward_scales.keys()))
+    st["gravities"] = env.gravities.numpy()[0]
+
+    # reset() as the reference's TrajectoryTrackingEnv.reset (trajectory_tracking/__init__.py:46-55)
+    _rand_log.clear()
+    scatter_draws.ids.clear()
+    env.reset()
+    rec["after_reset"] = env_state(env)
+    rec["after_reset_obs"] = env.obs_buf.numpy().copy()
+    if counter_start is not None:
+        env.common_step_counter = counter_start
+    g = np.random.default_rng(seed + 2)
+    for t in range(n_steps):
+        pre = env_state(env)
+        pre_counter = env.common_step_counter
+        pre_scales = np.array([env.reward_scales[k] for k in L.REWARD_KEYS], np.float64)
+        pre_grav = env.gravities.numpy()[0].copy()
+        pre_gvec = env.gravity_vec.numpy()[0].copy()
+        pre_simg = np.array(gym.gravity, np.float32)
+        actions = torch.from_numpy((g.normal(0, 1.0, (n, 12)) * actions_scale).astype(np.float32))
+        if t % 7 == 3:  # exercise the +/-10 action clip (scripts/train.py:241)
+            actions[:4] *= 20.0
+        _rand_log.clear()
+        scatter_draws.ids.clear()
+        scatter_draws.root_k = 0
+        phys.log.clear()
+        gym.torque_log.clear()
+        obs, rew, reset, extras = env.step(actions)
+        u, ug = scatter_draws(env, list(_rand_log))
+        step = {
+            "pre": pre, "post": env_state(env), "actions": actions.numpy(),
+            "common_step_counter": np.int64(pre_counter), "reward_scales": pre_scales, "gravity": pre_grav,
+            "gravity_after": env.gravities.numpy()[0].copy(),
+            "gravity_vec": pre_gvec, "sim_gravity": pre_simg,
+            "uniforms": u, "uniforms_gravity": ug,
+            "inj_dof": np.stack([p["dof"].view(n, 12, 2).numpy() for p in phys.log]),  # (4, n, 12, 2)
+            "inj_root": phys.log[-1]["root"].numpy(), "inj_contact": phys.log[-1]["contact"].numpy(),
+            "inj_feet": phys.log[-1]["feet"].numpy(),
+            "torques": np.stack([x.view(n, 12).numpy() for x in gym.torque_log]),  # (4, n, 12)
+            "obs": obs.numpy().copy(), "priv": extras["privileged_obs"].numpy().copy(),
+            "rew": rew.numpy().copy(), "reset": reset.numpy().copy(),
+            "time_out": env.time_out_buf.numpy().copy(),
+            "extras_time_outs": (extras["time_outs"].numpy().copy() if "time_outs" in extras
+                                 else np.zeros(0, bool)),
+            "measured_heights": term_log["heights"].numpy().copy(),
+            "rew_terms": np.stack([term_log[k].float().numpy() for k in L.REWARD_KEYS], 1),
+            "arrow_root": env.root_states[1::2, 0:7].numpy().copy(),
+            "reached": env.reached_buf.numpy().copy(),
+            "commands": env.commands.numpy().copy(),
+        }
+        rec["steps"].append(step)
+    flat = {}
+    for k, v in rec["static"].items():
+        flat["static/" + k] = v
+    for k, v in rec["after_reset"].items():
+        flat["after_reset/" + k] = v
+    flat["after_reset_obs"] = rec["after_reset_obs"]
+    for t, s in enumerate(rec["steps"]):
+        for k, v in s.items():
+            if isinstance(v, dict):
+                for kk, vv in v.items():
+                    flat[f"s{t}/{k}/{kk}"] = vv
+            else:
+                flat[f"s{t}/{k}"] = v
+    flat["meta/n_steps"] = np.int64(n_steps)
+    flat["meta/terrain"] = np.array(terrain)
+    np.savez_compressed(out, **flat)
+    print("wrote", out, len(flat), "arrays")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--which", default="all")
+    a = ap.parse_args()
+    if a.which == "all":
+        # one fresh process per fixture: the reference mutates its module-level Cfg
+        import subprocess
+        for w in ("single_path", "plane"):
+            subprocess.run([sys.executable, __file__, "--steps", str(a.steps), "--which", w], check=True)
+    elif a.which == "single_path":
+        # gravity zeroing at counter 396 and resampling at 400 fall inside the window
+        run("single_path", 64, 4, a.steps, 11, os.path.join(HERE, "step_single_path.npz"), counter_start=393)
+    elif a.which == "plane":
+        # plane (no camera_zero: the reference raises with it, :402); exploration decay after 2500
+        run("plane", 64, 4, a.steps, 12, os.path.join(HERE, "step_plane.npz"), counter_start=2497)
