@@ -175,11 +175,17 @@ typedef struct go1_step_args {
   float* dbg_terms;            /* (n_envs, 10) unscaled reward terms */
   float* dbg_commands;         /* (n_envs, 2) */
   uint8_t* dbg_reached;        /* (n_envs) */
+  /* optional hipEvent_t pair recorded around the fused step kernel alone (NULL = none) */
+  void* ev_begin;
+  void* ev_end;
 } go1_step_args;
 
 typedef struct go1_handle go1_handle;
 
 int go1_abi_version(void);
+/* sizeof(go1_config), sizeof(go1_state), sizeof(go1_terrain), sizeof(go1_step_args):
+ * lets a foreign binding (ctypes / cgo / JNI) verify its struct mirrors. */
+void go1_abi_sizes(int64_t out[4]);
 const char* go1_last_error(void);
 int go1_create(const go1_config* cfg, go1_handle** out);
 int go1_bind(go1_handle* h, const go1_state* state);

@@ -551,7 +551,7 @@ def f32(x):
 
 
 # Native physics constants (no reference counterpart: PhysX is closed)
-PHYSICS = dict(contact_stiffness=2.0e4, contact_damping=250.0, friction_damping=150.0,
+PHYSICS = dict(contact_stiffness=2.0e4, contact_damping=80.0, friction_damping=60.0,
                limit_stiffness=150.0, limit_damping=2.0, n_internal=2)
 
 

@@ -1,0 +1,106 @@
+/*
+ * pmath.h -- deterministic f32 transcendentals for the HIP kernels (product copy).
+ *
+ * Deterministic f32 sin/cos/asin/atan2 built only from IEEE-exact operations
+ * (+ - * / sqrt, fmaf, rintf, fabsf, copysignf), so these kernels and the CPU
+ * oracle (which carries its own copy, oracle/portable_math.h) produce
+ * bit-identical height-scan inputs and rpy angles.  Algorithms: Cody-Waite reduction by pi/2 and
+ * the single-precision minimax polynomials of the Cephes library (sinf/cosf,
+ * asinf, atanf).  Accuracy ~1-2 ulp vs the correctly rounded value; torch's
+ * own f32 functions differ from either at the ulp level, which the parity
+ * tests absorb in their stated float tolerance.
+ *
+ * Compile with -ffp-contract=off: every a*b+c written below without fmaf must
+ * stay two roundings.
+ */
+#ifndef GO1_PMATH_H
+#define GO1_PMATH_H
+#include <hip/hip_runtime.h>
+#define PM_FN __device__ __forceinline__
+
+#define PM_PIO2_HI 1.5703125f
+#define PM_PIO2_MID 4.837512969970703125e-4f
+#define PM_PIO2_LO 7.54978995489188216e-8f
+#define PM_2_PI 0.636619772367581343f
+#define PM_PIO2 1.57079632679489661923f
+#define PM_PIO4 0.785398163397448309616f
+#define PM_PI 3.14159265358979323846f
+
+PM_FN float pm_sin_poly(float r) {
+  float z = r * r;
+  float p = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  return fmaf(p * z, r, r);
+}
+
+PM_FN float pm_cos_poly(float r) {
+  float z = r * r;
+  float p = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+  return fmaf(p * z, z, fmaf(-0.5f, z, 1.0f));
+}
+
+/* sin and cos of x, |x| <= ~1e3 */
+PM_FN void pm_sincosf(float x, float* s, float* c) {
+  float j = rintf(x * PM_2_PI);
+  float r = fmaf(-j, PM_PIO2_HI, x);
+  r = fmaf(-j, PM_PIO2_MID, r);
+  r = fmaf(-j, PM_PIO2_LO, r);
+  int q = ((int)j) & 3;
+  float sp = pm_sin_poly(r), cp = pm_cos_poly(r);
+  switch (q) {
+    case 0: *s = sp; *c = cp; break;
+    case 1: *s = cp; *c = -sp; break;
+    case 2: *s = -sp; *c = -cp; break;
+    default: *s = -cp; *c = sp; break;
+  }
+}
+
+PM_FN float pm_sinf(float x) { float s, c; pm_sincosf(x, &s, &c); return s; }
+PM_FN float pm_cosf(float x) { float s, c; pm_sincosf(x, &s, &c); return c; }
+
+PM_FN float pm_asinf(float x) {
+  float a = fabsf(x), z, s;
+  int big = a > 0.5f;
+  if (big) {
+    z = 0.5f * (1.0f - a);
+    s = sqrtf(z);
+  } else {
+    z = a * a;
+    s = a;
+  }
+  float p = fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
+                      7.4953002686e-2f), z, 1.6666752422e-1f);
+  float r = fmaf(p * z, s, s);
+  if (big) r = PM_PIO2 - (r + r);
+  return copysignf(r, x);
+}
+
+PM_FN float pm_atanf(float x) {
+  float a = fabsf(x), y0, t;
+  if (a > 2.414213562373095f) {
+    y0 = PM_PIO2;
+    t = -1.0f / a;
+  } else if (a > 0.4142135623730950f) {
+    y0 = PM_PIO4;
+    t = (a - 1.0f) / (a + 1.0f);
+  } else {
+    y0 = 0.0f;
+    t = a;
+  }
+  float z = t * t;
+  float p = fmaf(fmaf(fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f), z,
+                 -3.33329491539e-1f);
+  float r = y0 + fmaf(p * z, t, t);
+  return copysignf(r, x);
+}
+
+PM_FN float pm_atan2f(float y, float x) {
+  if (x == 0.0f) {
+    if (y == 0.0f) return __builtin_signbit(x) ? copysignf(PM_PI, y) : copysignf(0.0f, y);
+    return copysignf(PM_PIO2, y);
+  }
+  float r = pm_atanf(y / x);
+  if (x < 0.0f) r = (y < 0.0f || (y == 0.0f && __builtin_signbit(y))) ? r - PM_PI : r + PM_PI;
+  return r;
+}
+
+#endif

@@ -1,0 +1,174 @@
+"""Thin host binding of the HIP C ABI (include/go1_mi355x.h) over PyTorch-ROCm tensors.
+
+torch provides device memory and the stream; every computation of the step runs
+in the HIP library legged_tracking_amd/_build/libgo1_mi355x.so.  If that library
+is missing or the GPU is absent this module raises -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import torch
+
+from . import abi, layout as L
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libgo1_mi355x.so")
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the HIP library (fails loudly; build with __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"HIP extension missing: {LIB_PATH} (run python -c 'import __graft_entry__ as g; g.build()')")
+    l = C.CDLL(LIB_PATH)
+    l.go1_abi_version.restype = C.c_int
+    l.go1_last_error.restype = C.c_char_p
+    l.go1_create.argtypes = [C.POINTER(abi.Go1Config), C.POINTER(C.c_void_p)]
+    l.go1_bind.argtypes = [C.c_void_p, C.POINTER(abi.Go1State)]
+    l.go1_set_terrain.argtypes = [C.c_void_p, C.POINTER(abi.Go1Terrain)]
+    l.go1_step.argtypes = [C.c_void_p, C.POINTER(abi.Go1StepArgs), C.c_void_p]
+    l.go1_reset_envs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
+    l.go1_actuator_net.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    l.go1_destroy.argtypes = [C.c_void_p]
+    if l.go1_abi_version() != 1:
+        raise NativeError("ABI version mismatch")
+    _lib = l
+    return l
+
+
+def _check(rc):
+    if rc != 0:
+        raise NativeError(lib().go1_last_error().decode())
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class StateTensors:
+    """go1_state planes as torch tensors on the device (SoA, row-major (n, width))."""
+
+    def __init__(self, n, device):
+        self.n = n
+        self.t = {}
+        for name, w, dt in abi.STATE_SPEC:
+            self.t[name] = torch.zeros((n, w), dtype=torch.float32 if dt == "f32" else torch.int32, device=device)
+
+    def struct(self):
+        return abi.Go1State(**{k: v.data_ptr() for k, v in self.t.items()})
+
+    def __getitem__(self, k):
+        return self.t[k]
+
+    def load(self, arrays: dict):
+        for k, v in arrays.items():
+            if k in self.t:
+                self.t[k].copy_(torch.as_tensor(np.asarray(v)).reshape(self.t[k].shape).to(self.t[k].dtype))
+
+    def numpy(self):
+        return {k: v.cpu().numpy() for k, v in self.t.items()}
+
+
+class Go1Native:
+    """Owns one go1_handle and the device buffers the C ABI writes."""
+
+    def __init__(self, cfg: abi.Go1Config, device="cuda:0"):
+        if not torch.cuda.is_available():
+            raise NativeError("no GPU visible: the MI355X step has no CPU fallback")
+        self.device = torch.device(device)
+        self.cfg = cfg
+        self.n = n = cfg.n_envs
+        self.h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _check(lib().go1_create(C.byref(cfg), C.byref(self.h)))
+            self.state = StateTensors(n, self.device)
+            _check(lib().go1_bind(self.h, C.byref(self.state.struct())))
+            dev = self.device
+            self.obs = torch.zeros((n, abi.GO1_NUM_OBS), device=dev)
+            self.priv = torch.zeros((n, abi.GO1_NUM_PRIV), device=dev)
+            self.rew = torch.zeros(n, device=dev)
+            self.reset = torch.zeros(n, dtype=torch.bool, device=dev)
+            self.time_out = torch.zeros(n, dtype=torch.bool, device=dev)
+            self.extras_time_outs = torch.zeros(n, dtype=torch.bool, device=dev)
+            self.contact_forces = torch.zeros((n, 17, 3), device=dev)
+        self._terrain_keep = None
+
+    def set_terrain(self, tiles, env_tile, env_terrain_origin, env_origins):
+        d = self.device
+        t = [torch.as_tensor(np.ascontiguousarray(tiles, np.float32)).to(d),
+             torch.as_tensor(np.ascontiguousarray(env_tile, np.int32)).to(d),
+             torch.as_tensor(np.ascontiguousarray(env_terrain_origin, np.float32)).to(d),
+             torch.as_tensor(np.ascontiguousarray(env_origins, np.float32)).to(d)]
+        self._terrain_keep = t
+        s = abi.Go1Terrain(tiles=t[0].data_ptr(), env_tile=t[1].data_ptr(), env_terrain_origin=t[2].data_ptr(),
+                           env_origins=t[3].data_ptr(), n_tiles=int(t[0].shape[0]))
+        _check(lib().go1_set_terrain(self.h, C.byref(s)))
+
+    def step(self, actions, gravity_vec, sim_gravity, reward_scales, rng_seed=0, rng_step=0, uniforms=None,
+             inj=None, debug=None, events=None):
+        """One fused LeggedRobot.step on the current stream.  `debug` is an optional dict
+        of preallocated tensors (torques, heights, terms, commands, reached)."""
+        a = abi.Go1StepArgs()
+        assert actions.is_contiguous() and actions.dtype == torch.float32 and actions.shape == (self.n, 12)
+        a.actions = actions.data_ptr()
+        for i in range(3):
+            a.gravity_vec[i] = float(gravity_vec[i])
+            a.sim_gravity[i] = float(sim_gravity[i])
+        for i in range(abi.GO1_NUM_TERMS):
+            a.reward_scales[i] = float(reward_scales[i])
+        a.rng_seed, a.rng_step = int(rng_seed), int(rng_step)
+        if uniforms is not None:
+            assert uniforms.is_contiguous() and uniforms.shape == (self.n, abi.GO1_U_PER_ENV)
+            a.uniforms = uniforms.data_ptr()
+        if inj is not None:
+            a.inj_dof, a.inj_root, a.inj_contact = (inj[k].data_ptr() for k in ("dof", "root", "contact"))
+        a.obs, a.priv, a.rew = self.obs.data_ptr(), self.priv.data_ptr(), self.rew.data_ptr()
+        a.reset, a.time_out = self.reset.data_ptr(), self.time_out.data_ptr()
+        a.extras_time_outs = self.extras_time_outs.data_ptr()
+        a.contact_forces = self.contact_forces.data_ptr()
+        if debug:
+            for k, fld in (("torques", "dbg_torques"), ("heights", "dbg_heights"), ("terms", "dbg_terms"),
+                           ("commands", "dbg_commands"), ("reached", "dbg_reached")):
+                if k in debug:
+                    setattr(a, fld, debug[k].data_ptr())
+        if events is not None:  # (hipEvent_t begin, hipEvent_t end) as ints
+            a.ev_begin, a.ev_end = events
+        _check(lib().go1_step(self.h, C.byref(a), _stream()))
+
+    def reset_envs(self, mask, uniforms=None, rng_seed=0, rng_step=0):
+        m = mask.to(torch.uint8).contiguous()
+        _check(lib().go1_reset_envs(self.h, m.data_ptr(), None if uniforms is None else uniforms.data_ptr(),
+                                    int(rng_seed), int(rng_step), _stream()))
+        return m  # keep alive until the stream passes it
+
+    def actuator(self, x):
+        x = x.contiguous()
+        out = torch.empty(x.shape[0], device=x.device)
+        _check(lib().go1_actuator_net(self.h, x.data_ptr(), out.data_ptr(), x.shape[0], _stream()))
+        return out
+
+    def close(self):
+        if self.h:
+            lib().go1_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def debug_buffers(n, decimation, device):
+    return dict(torques=torch.zeros((decimation, n, 12), device=device),
+                heights=torch.zeros((n, 2, 21, 11), device=device),
+                terms=torch.zeros((n, 10), device=device), commands=torch.zeros((n, 2), device=device),
+                reached=torch.zeros(n, dtype=torch.uint8, device=device))

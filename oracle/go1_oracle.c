@@ -151,6 +151,15 @@ static float norm2_f(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
 static float norm3_f(float x, float y, float z) { return sqrtf(fmaf(z, z, fmaf(y, y, x * x))); }
 static float sq_f(float x) { return x * x; }
 
+/* sum over the 12 dofs in the grouping the HIP kernel uses (one leg per lane:
+ * ((x0+x1)+x2) per leg, then (leg0+leg1)+(leg2+leg3)).  torch's own CPU order
+ * is not specified; the parity tests use a float tolerance against it. */
+static float sum12_legs(const float* x) {
+  float s[4];
+  for (int l = 0; l < 4; ++l) s[l] = (x[3 * l] + x[3 * l + 1]) + x[3 * l + 2];
+  return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
 /* ====================================================================== */
 /*                      native physics, f64 restatement                    */
 /* ====================================================================== */
@@ -893,27 +902,23 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   /* compute_reward (:320-355) with RewardsCrawling terms */
   float terms[GO1_NUM_TERMS];
   {
-    float s = 0.0f;
-    for (int d = 0; d < NDOF; ++d) s += sq_f(torque[d]);
-    terms[0] = s;
+    float x[NDOF];
+    for (int d = 0; d < NDOF; ++d) x[d] = sq_f(torque[d]);
+    terms[0] = sum12_legs(x);
     const float* ldv = st->last_dof_vel + (size_t)e * NDOF;
-    s = 0.0f;
-    for (int d = 0; d < NDOF; ++d) s += sq_f((ldv[d] - dv[d]) / c->dt);
-    terms[1] = s;
+    for (int d = 0; d < NDOF; ++d) x[d] = sq_f((ldv[d] - dv[d]) / c->dt);
+    terms[1] = sum12_legs(x);
     terms[2] = coll;
     const float* la = st->last_actions + (size_t)e * NDOF;
-    s = 0.0f;
-    for (int d = 0; d < NDOF; ++d) s += sq_f(la[d] - act[d]);
-    terms[3] = s;
-    s = 0.0f;
+    for (int d = 0; d < NDOF; ++d) x[d] = sq_f(la[d] - act[d]);
+    terms[3] = sum12_legs(x);
     for (int d = 0; d < NDOF; ++d) {
       float lo = dp[d] - c->dof_pos_limits[2 * d];
       float hi = dp[d] - c->dof_pos_limits[2 * d + 1];
       float o = -(lo < 0.0f ? lo : 0.0f);
-      o = o + (hi > 0.0f ? hi : 0.0f);
-      s += o;
+      x[d] = o + (hi > 0.0f ? hi : 0.0f);
     }
-    terms[4] = s;
+    terms[4] = sum12_legs(x);
     terms[5] = sq_f(root[2] - c->base_height_target);
     terms[6] = sq_f(bav[0]) + sq_f(bav[1]);
     /* e2e (reward_crawling.py:61-77) */

@@ -444,7 +444,8 @@ def build_env(terrain, n_envs, rows, seed, extra_argv=()):
     return env, cfg
 
 
-def run(terrain, n_envs, rows, n_steps, seed, out, extra_argv=(), actions_scale=1.0, counter_start=None):
+def run(terrain, n_envs, rows, n_steps, seed, out, extra_argv=(), actions_scale=1.0, counter_start=None,
+        events=False):
     env, cfg = build_env(terrain, n_envs, rows, seed, extra_argv)
     install_id_tracking(env)
     term_log = {}
@@ -494,6 +495,13 @@ def run(terrain, n_envs, rows, n_steps, seed, out, extra_argv=(), actions_scale=
     rec["after_reset_obs"] = env.obs_buf.numpy().copy()
     if counter_start is not None:
         env.common_step_counter = counter_start
+    if events:
+        # drive rarely-hit branches: DR at episode_length % rand_interval == 0
+        # (:822-824), waypoint switch/reached (:836-844), timeouts (:203)
+        env.episode_length_buf[:8] = int(env.cfg.domain_rand.rand_interval) - 2
+        env.episode_length_buf[8:12] = int(env.max_episode_length) - 1
+        rs = env.root_states[::env.num_actor]
+        env.trajectories[12:28, 0, 0:2] = rs[12:28, 0:2] + torch.linspace(-0.3, 0.3, 16)[:, None]
     g = np.random.default_rng(seed + 2)
     for t in range(n_steps):
         pre = env_state(env)
@@ -561,11 +569,14 @@ if __name__ == "__main__":
     if a.which == "all":
         # one fresh process per fixture: the reference mutates its module-level Cfg
         import subprocess
-        for w in ("single_path", "plane"):
+        for w in ("single_path", "plane", "events"):
             subprocess.run([sys.executable, __file__, "--steps", str(a.steps), "--which", w], check=True)
     elif a.which == "single_path":
         # gravity zeroing at counter 396 and resampling at 400 fall inside the window
         run("single_path", 64, 4, a.steps, 11, os.path.join(HERE, "step_single_path.npz"), counter_start=393)
+    elif a.which == "events":
+        run("single_path", 64, 4, 5, 13, os.path.join(HERE, "step_single_path_events.npz"), counter_start=398,
+            events=True)
     elif a.which == "plane":
         # plane (no camera_zero: the reference raises with it, :402); exploration decay after 2500
         run("plane", 64, 4, a.steps, 12, os.path.join(HERE, "step_plane.npz"), counter_start=2497)

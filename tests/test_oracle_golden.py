@@ -8,7 +8,7 @@ import pytest
 from oracle import oracle as O
 from tests import golden_io as G
 
-FIXTURES = ["step_single_path.npz", "step_plane.npz"]
+FIXTURES = ["step_single_path.npz", "step_plane.npz", "step_single_path_events.npz"]
 RTOL, ATOL = 2e-5, 2e-5
 
 
