@@ -169,7 +169,8 @@ def main():
         hp.hipEventElapsedTime(C.byref(ms), evs[2 * k], evs[2 * k + 1])
         kt.append(ms.value)
     kernel_ms = float(np.mean(kt))
-    assert torch.isfinite(g.obs).all(), "non-finite observations"
+    if not os.environ.get("GO1_BENCH_ALLOW_NONFINITE"):
+        assert torch.isfinite(g.obs).all(), "non-finite observations"
     if dist:
         t = torch.tensor([elapsed, kernel_ms], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -75,32 +75,82 @@ __device__ __forceinline__ float qsum(float v) {
 }
 
 // ---------------------------------------------------------------- actuator net
-// Bit-identical to go1o_actuator_eval: every output is an fmaf chain over k in
-// increasing order seeded with the bias; softsign x / (|x| + 1) in IEEE division.
-__device__ __forceinline__ float actuator_eval(const float* __restrict__ W, float x0, float x1, float x2, float x3,
-                                               float x4, float x5) {
-  float h1[32];
+// eval_actuator_network (:1311-1320) on the matrix cores.  One "group" = 16
+// (env, joint) items; each item is carried by the 4 lanes {i, 16+i, 32+i, 48+i}
+// of a wave (i = lane & 15, q = lane >> 4), exactly the v_mfma_f32_16x16x4_f32
+// B-operand layout (B[k = q][item i]) and C/D layout (rows 4q..4q+3, column i).
+//   layer 1: D = W1pad(32x8) . X(8x16): 2 M-tiles x 2 K-steps = 4 MFMA
+//   layer 2: D = W2(32x32) . H1(32x16): each lane's layer-1 rows ARE its layer-2
+//            B operand when the K-steps run over (m, r) with k = 16 m + 4 q + r,
+//            so no data moves between the layers: 2 M-tiles x 8 K-steps = 16 MFMA
+//   layer 3: per-lane fma over its 8 rows, then two xor-shuffles (16, 32).
+// f32-input MFMA is bit-for-bit a k-ordered fmaf chain, and the oracle uses the
+// same k order (oracle/go1_oracle.c go1o_actuator_eval): torques are bit-identical.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+struct MlpFrag {
+  float w1[2][2];  // [mo][s] = W1[16 mo + i][4 s + q]  (0 for k >= 6)
+  float w2[2][8];  // [mo][4 m + r] = W2[16 mo + i][16 m + 4 q + r]
+  f4 b1[2], b2[2]; // rows 4 q + r of tile mo
+  float w3[2][4];  // w3[16 mo + 4 q + r]
+  float b3;
+};
+
+__device__ __forceinline__ void mlp_load(const float* __restrict__ W, int lane, MlpFrag& F) {
+  const int i = lane & 15, q = lane >> 4;
 #pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    float acc = W[192 + k];
-    acc = fmaf(W[k * 6 + 0], x0, acc);
-    acc = fmaf(W[k * 6 + 1], x1, acc);
-    acc = fmaf(W[k * 6 + 2], x2, acc);
-    acc = fmaf(W[k * 6 + 3], x3, acc);
-    acc = fmaf(W[k * 6 + 4], x4, acc);
-    acc = fmaf(W[k * 6 + 5], x5, acc);
-    h1[k] = acc / (fabsf(acc) + 1.0f);
+  for (int mo = 0; mo < 2; ++mo) {
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const int k = 4 * sk + q;
+      F.w1[mo][sk] = k < 6 ? W[(16 * mo + i) * 6 + k] : 0.0f;
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) F.w2[mo][4 * m + r] = W[224 + (16 * mo + i) * 32 + 16 * m + 4 * q + r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      F.b1[mo][r] = W[192 + 16 * mo + 4 * q + r];
+      F.b2[mo][r] = W[1248 + 16 * mo + 4 * q + r];
+      F.w3[mo][r] = W[1280 + 16 * mo + 4 * q + r];
+    }
   }
-  float out = W[1312];
+  F.b3 = W[1312];
+}
+
+__device__ __forceinline__ float softsign(float x) { return x / (fabsf(x) + 1.0f); }
+
+// b0 = X[k = q][item], b1v = X[k = 4 + q][item] (0 for q >= 2).  Returns the torque
+// of item (lane & 15) in all four lanes of the item.  Needs all 64 lanes active.
+__device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v) {
+  f4 a1[2];
 #pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    float acc = W[1248 + k];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) acc = fmaf(W[224 + k * 32 + i], h1[i], acc);
-    float h2 = acc / (fabsf(acc) + 1.0f);
-    out = fmaf(W[1280 + k], h2, out);
+  for (int mo = 0; mo < 2; ++mo) {
+    a1[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][0], b0, F.b1[mo], 0, 0, 0);
+    a1[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][1], b1v, a1[mo], 0, 0, 0);
   }
-  return out;
+  float h1[2][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h1[m][r] = softsign(a1[m][r]);
+  f4 a2[2] = {F.b2[0], F.b2[1]};
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mo = 0; mo < 2; ++mo)
+        a2[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w2[mo][4 * m + r], h1[m][r], a2[mo], 0, 0, 0);
+  float p = 0.0f;
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p = fmaf(F.w3[mo][r], softsign(a2[mo][r]), p);
+  p = p + __shfl_xor(p, 16);
+  p = p + __shfl_xor(p, 32);
+  return p + F.b3;
 }
 
 // ---------------------------------------------------------------- torch-order f32 math
@@ -227,12 +277,26 @@ __device__ __forceinline__ void crf(const float* v, const float* f, float* o) {
   o[3] = c[0]; o[4] = c[1]; o[5] = c[2];
 }
 
-// revolute joint about coordinate axis ax (0 = x, 1 = y): E = Rot(ax, q)^T
-__device__ __forceinline__ void joint_E(int ax, float c, float s, float E[9]) {
+// Revolute joint about coordinate axis ax (0 = x, 1 = y) by q: E = Rot(ax, q)^T maps
+// parent coordinates to child coordinates.  Only (c, s) is kept; every product with E
+// mixes two components.
+__device__ __forceinline__ void rE(int ax, float c, float s, const float* v, float* o) {  // o = E v
   if (ax == 0) {
-    E[0] = 1; E[1] = 0; E[2] = 0; E[3] = 0; E[4] = c; E[5] = s; E[6] = 0; E[7] = -s; E[8] = c;
+    float y = c * v[1] + s * v[2], z = c * v[2] - s * v[1];
+    o[0] = v[0]; o[1] = y; o[2] = z;
   } else {
-    E[0] = c; E[1] = 0; E[2] = -s; E[3] = 0; E[4] = 1; E[5] = 0; E[6] = s; E[7] = 0; E[8] = c;
+    float x = c * v[0] - s * v[2], z = s * v[0] + c * v[2];
+    o[0] = x; o[1] = v[1]; o[2] = z;
+  }
+}
+
+__device__ __forceinline__ void rET(int ax, float c, float s, const float* v, float* o) {  // o = E^T v
+  if (ax == 0) {
+    float y = c * v[1] - s * v[2], z = s * v[1] + c * v[2];
+    o[0] = v[0]; o[1] = y; o[2] = z;
+  } else {
+    float x = c * v[0] + s * v[2], z = c * v[2] - s * v[0];
+    o[0] = x; o[1] = v[1]; o[2] = z;
   }
 }
 
@@ -250,121 +314,77 @@ __device__ __forceinline__ void mat3T_vec(const float* E, const float* v, float*
   o[0] = x; o[1] = y; o[2] = z;
 }
 
-// motion transform parent -> child
-__device__ __forceinline__ void xm(const float* E, const float* r, const float* vin, float* vout) {
+// motion transform parent -> child: (w, v) -> (E w, E (v - r x w))
+__device__ __forceinline__ void xm(int ax, float c, float s, const float* r, const float* vin, float* vout) {
   float rw[3], t[3];
   cross3(r, vin, rw);
   t[0] = vin[3] - rw[0]; t[1] = vin[4] - rw[1]; t[2] = vin[5] - rw[2];
-  float w[3], v[3];
-  mat3_vec(E, vin, w);
-  mat3_vec(E, t, v);
-  vout[0] = w[0]; vout[1] = w[1]; vout[2] = w[2]; vout[3] = v[0]; vout[4] = v[1]; vout[5] = v[2];
+  rE(ax, c, s, vin, vout);
+  rE(ax, c, s, t, vout + 3);
 }
 
-// force transform child -> parent
-__device__ __forceinline__ void xfT(const float* E, const float* r, const float* fin, float* fout) {
+// force transform child -> parent: (n, f) -> (E^T n + r x E^T f, E^T f)
+__device__ __forceinline__ void xfT(int ax, float c, float s, const float* r, const float* fin, float* fout) {
   float n[3], f[3], rf[3];
-  mat3T_vec(E, fin, n);
-  mat3T_vec(E, fin + 3, f);
+  rET(ax, c, s, fin, n);
+  rET(ax, c, s, fin + 3, f);
   cross3(r, f, rf);
   fout[0] = n[0] + rf[0]; fout[1] = n[1] + rf[1]; fout[2] = n[2] + rf[2];
   fout[3] = f[0]; fout[4] = f[1]; fout[5] = f[2];
 }
 
-// X^T Ia X for X = [[E, 0], [-E r~, E]]: rotate blocks by E^T(.)E, then translate by r.
-__device__ __forceinline__ void xform_inertia(const float* E, const float* r, const SI& In, SI& Out) {
-  float A[9], B[9], C[9], T[9];
-  // A' = E^T A E
+// Q = E^T M E for a full 3x3 M (row-major): rows of M E are E^T(row of M), then E^T per column.
+__device__ __forceinline__ void rot_congruence(int ax, float c, float s, const float* M, float* Q) {
+  float N[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) rET(ax, c, s, M + 3 * i, N + 3 * i);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float col[3] = {N[j], N[3 + j], N[6 + j]}, out[3];
+    rET(ax, c, s, col, out);
+    Q[j] = out[0]; Q[3 + j] = out[1]; Q[6 + j] = out[2];
+  }
+}
+
+// X^T Ia X for X = [[E, 0], [-E r~, E]]: rotate the blocks by E^T(.)E, then translate by r:
+//   A'' = A' + r~ B'^T - B' r~ - r~ C' r~ ,  B'' = B' + r~ C' ,  C'' = C'.
+__device__ __forceinline__ void xform_inertia(int ax, float cq, float sq, const float* r, const SI& In, SI& Out) {
+  float M[9], A[9], B[9], C[9];
+  M[0] = In.a[0]; M[1] = In.a[1]; M[2] = In.a[2]; M[3] = In.a[1]; M[4] = In.a[3]; M[5] = In.a[4];
+  M[6] = In.a[2]; M[7] = In.a[4]; M[8] = In.a[5];
+  rot_congruence(ax, cq, sq, M, A);
+  rot_congruence(ax, cq, sq, In.b, B);
+  M[0] = In.c[0]; M[1] = In.c[1]; M[2] = In.c[2]; M[3] = In.c[1]; M[4] = In.c[3]; M[5] = In.c[4];
+  M[6] = In.c[2]; M[7] = In.c[4]; M[8] = In.c[5];
+  rot_congruence(ax, cq, sq, M, C);
+  const float rx[9] = {0.0f, -r[2], r[1], r[2], 0.0f, -r[0], -r[1], r[0], 0.0f};
+  float RC[9], RBt[9], BR[9];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      float s = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s += S3(In.a, i, k) * E[k * 3 + j];
-      T[i * 3 + j] = s;
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s += E[k * 3 + i] * T[k * 3 + j];
-      A[i * 3 + j] = s;
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s += In.b[i * 3 + k] * E[k * 3 + j];
-      T[i * 3 + j] = s;
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s += E[k * 3 + i] * T[k * 3 + j];
-      B[i * 3 + j] = s;
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s += S3(In.c, i, k) * E[k * 3 + j];
-      T[i * 3 + j] = s;
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s += E[k * 3 + i] * T[k * 3 + j];
-      C[i * 3 + j] = s;
-    }
-  // translate: A'' = A' + r~ B'^T - B' r~ - r~ C' r~ ; B'' = B' + r~ C'
-  float rx[9] = {0.0f, -r[2], r[1], r[2], 0.0f, -r[0], -r[1], r[0], 0.0f};
-  float RC[9], RBt[9], BR[9], RCR[9];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = 0.0f, t = 0.0f, u = 0.0f;
+      float s0 = 0.0f, t0 = 0.0f, u0 = 0.0f;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        s += rx[i * 3 + k] * C[k * 3 + j];
-        t += rx[i * 3 + k] * B[j * 3 + k];
-        u += B[i * 3 + k] * rx[k * 3 + j];
+        s0 += rx[i * 3 + k] * C[k * 3 + j];
+        t0 += rx[i * 3 + k] * B[j * 3 + k];
+        u0 += B[i * 3 + k] * rx[k * 3 + j];
       }
-      RC[i * 3 + j] = s;
-      RBt[i * 3 + j] = t;
-      BR[i * 3 + j] = u;
+      RC[i * 3 + j] = s0;
+      RBt[i * 3 + j] = t0;
+      BR[i * 3 + j] = u0;
     }
+  // upper triangle of A'' only (symmetric)
+  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) s += RC[i * 3 + k] * rx[k * 3 + j];
-      RCR[i * 3 + j] = s;
-    }
-  float Af[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Af[i] = A[i] + RBt[i] - BR[i] - RCR[i];
-  Out.a[0] = Af[0]; Out.a[1] = 0.5f * (Af[1] + Af[3]); Out.a[2] = 0.5f * (Af[2] + Af[6]);
-  Out.a[3] = Af[4]; Out.a[4] = 0.5f * (Af[5] + Af[7]); Out.a[5] = Af[8];
+  for (int t = 0; t < 6; ++t) {
+    const int i = II[t], j = JJ[t];
+    float rcr = RC[i * 3 + 0] * rx[0 * 3 + j] + RC[i * 3 + 1] * rx[1 * 3 + j] + RC[i * 3 + 2] * rx[2 * 3 + j];
+    Out.a[t] = A[i * 3 + j] + RBt[i * 3 + j] - BR[i * 3 + j] - rcr;
+    Out.c[t] = C[i * 3 + j];
+  }
 #pragma unroll
   for (int i = 0; i < 9; ++i) Out.b[i] = B[i] + RC[i];
-  Out.c[0] = C[0]; Out.c[1] = 0.5f * (C[1] + C[3]); Out.c[2] = 0.5f * (C[2] + C[6]);
-  Out.c[3] = C[4]; Out.c[4] = 0.5f * (C[5] + C[7]); Out.c[5] = C[8];
 }
 
 __device__ __forceinline__ void si_add(SI& A, const SI& B) {
@@ -413,10 +433,17 @@ __device__ __forceinline__ void quat_to_R(const float* q, float* R) {
   R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
 }
 
+// Terrain view of one env.  `patch` is an LDS copy of the PSZ x PSZ cells around
+// the env's base at the start of the step, floor and ceiling interleaved, filled
+// once per step by the whole block; the integrator's contact queries hit it and
+// fall back to the HBM tile outside it (identical values: a pure cache).
+#define PSZ 22
 struct Terr {
   const float* tile;  // (2, nx, ny) or nullptr
   int nx, ny;
   float ox, oy, hs;
+  const float2* patch;  // LDS, PSZ x PSZ (floor, ceiling) or nullptr
+  int pi0, pj0;
 };
 
 __device__ __forceinline__ float tile_at(const Terr& T, int layer, int i, int j) {
@@ -425,22 +452,37 @@ __device__ __forceinline__ float tile_at(const Terr& T, int layer, int i, int j)
   return T.tile[((size_t)layer * T.nx + i) * T.ny + j];
 }
 
-__device__ __forceinline__ void height_query(const Terr& T, int layer, float x, float y, float& h, float& gx,
-                                             float& gy) {
+// floor (layer 1) and ceiling (layer 0) heights and gradients at world (x, y), bilinear
+__device__ __forceinline__ void height_query2(const Terr& T, float x, float y, float* hf, float* hc) {
   if (!T.tile) {
-    h = layer == 1 ? 0.0f : 1e9f;
-    gx = gy = 0.0f;
+    hf[0] = 0.0f; hf[1] = 0.0f; hf[2] = 0.0f;
+    hc[0] = 1e9f; hc[1] = 0.0f; hc[2] = 0.0f;
     return;
   }
-  float u = (x - T.ox) / T.hs, v = (y - T.oy) / T.hs;
-  float fu = floorf(u), fv = floorf(v);
-  int i = (int)fu, j = (int)fv;
-  float a = u - fu, b = v - fv;
-  float h00 = tile_at(T, layer, i, j), h10 = tile_at(T, layer, i + 1, j);
-  float h01 = tile_at(T, layer, i, j + 1), h11 = tile_at(T, layer, i + 1, j + 1);
-  h = (1 - a) * (1 - b) * h00 + a * (1 - b) * h10 + (1 - a) * b * h01 + a * b * h11;
-  gx = ((1 - b) * (h10 - h00) + b * (h11 - h01)) / T.hs;
-  gy = ((1 - a) * (h01 - h00) + a * (h11 - h10)) / T.hs;
+  // bounded before the float -> int conversions (a diverged pose must not index memory)
+  const float u = fminf(fmaxf((x - T.ox) / T.hs, -4.0f), (float)(T.nx + 4));
+  const float v = fminf(fmaxf((y - T.oy) / T.hs, -4.0f), (float)(T.ny + 4));
+  const float fu = floorf(u), fv = floorf(v);
+  const int i = (int)fu, j = (int)fv;
+  const float a = u - fu, b = v - fv;
+  float2 c00, c10, c01, c11;
+  const int li = i - T.pi0, lj = j - T.pj0;
+  if (T.patch && li >= 0 && li < PSZ - 1 && lj >= 0 && lj < PSZ - 1) {
+    const float2* pp = T.patch + li * PSZ + lj;
+    c00 = pp[0]; c01 = pp[1]; c10 = pp[PSZ]; c11 = pp[PSZ + 1];
+  } else {
+    c00 = make_float2(tile_at(T, 1, i, j), tile_at(T, 0, i, j));
+    c10 = make_float2(tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j));
+    c01 = make_float2(tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1));
+    c11 = make_float2(tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1));
+  }
+  const float inv = 1.0f / T.hs;
+  hf[0] = (1 - a) * (1 - b) * c00.x + a * (1 - b) * c10.x + (1 - a) * b * c01.x + a * b * c11.x;
+  hf[1] = ((1 - b) * (c10.x - c00.x) + b * (c11.x - c01.x)) * inv;
+  hf[2] = ((1 - a) * (c01.x - c00.x) + a * (c11.x - c10.x)) * inv;
+  hc[0] = (1 - a) * (1 - b) * c00.y + a * (1 - b) * c10.y + (1 - a) * b * c01.y + a * b * c11.y;
+  hc[1] = ((1 - b) * (c10.y - c00.y) + b * (c11.y - c01.y)) * inv;
+  hc[2] = ((1 - a) * (c01.y - c00.y) + a * (c11.y - c10.y)) * inv;
 }
 
 struct CP {
@@ -450,10 +492,11 @@ struct CP {
 __device__ __forceinline__ void sphere_contact(const Terr& T, const CP& C, const float* p, const float* pv, float r,
                                                float* F) {
   F[0] = F[1] = F[2] = 0.0f;
+  float hq[2][3];
+  height_query2(T, p[0], p[1], hq[1], hq[0]);
 #pragma unroll
   for (int layer = 1; layer >= 0; --layer) {
-    float h, gx, gy;
-    height_query(T, layer, p[0], p[1], h, gx, gy);
+    const float h = hq[layer][0], gx = hq[layer][1], gy = hq[layer][2];
     float n[3], dv;
     if (layer == 1) {
       dv = h + r - p[2];
@@ -463,19 +506,19 @@ __device__ __forceinline__ void sphere_contact(const Terr& T, const CP& C, const
       n[0] = gx; n[1] = gy; n[2] = -1.0f;
     }
     if (dv <= 0.0f) continue;
-    float inv = 1.0f / sqrtf(n[0] * n[0] + n[1] * n[1] + 1.0f);
+    const float inv = 1.0f / sqrtf(n[0] * n[0] + n[1] * n[1] + 1.0f);
     n[0] *= inv; n[1] *= inv; n[2] *= inv;
-    float depth = dv * inv;
-    float vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
-    float fn = C.k * depth - C.d * vn;
+    const float depth = dv * inv;
+    const float vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
+    const float fn = C.k * depth - C.d * vn;
     if (fn <= 0.0f) continue;
-    float vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
-    float vtn = sqrtf(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
-    float ft = fminf(C.kf * vtn, C.mu * fn);
-    float s = vtn > 1e-9f ? ft / vtn : 0.0f;
-    F[0] += fn * n[0] - s * vt[0];
-    F[1] += fn * n[1] - s * vt[1];
-    F[2] += fn * n[2] - s * vt[2];
+    const float vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
+    const float vtn = sqrtf(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
+    const float ft = fminf(C.kf * vtn, C.mu * fn);
+    const float sc = vtn > 1e-9f ? ft / vtn : 0.0f;
+    F[0] += fn * n[0] - sc * vt[0];
+    F[1] += fn * n[1] - sc * vt[1];
+    F[2] += fn * n[2] - sc * vt[2];
   }
 }
 
@@ -503,42 +546,29 @@ struct Phys {
   float q[3], qd[3];                   // this leg's joints
 };
 
-// One integrator step of length h.  cf: this lane's reported contact forces
-// (thigh, calf, foot of its leg; base from the quad sum), written when cf_out.
+// One integrator step of length h for the env of this lane's quad.  Each lane
+// handles its leg (kinematics, contacts, ABA backward/forward pass) and two of
+// the eight trunk corners; base quantities are replicated across the quad.
+// cf_out: write this lane's reported contact forces (thigh, calf, foot of its
+// leg; the base from the quad sum).
 __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const float* tau, float h, const float* g,
                              float friction, float payload, const Terr& T, int leg, bool cf_out, float* cf_leg,
                              float* cf_base) {
 #pragma clang fp contract(fast)
   const float* model = cfg->model;
-  CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
+  const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
   float R[9];
   quat_to_R(S.quat, R);
   float vb[6];
   mat3T_vec(R, S.w, vb);
   mat3T_vec(R, S.v, vb + 3);
-  // ---- base rigid body (every lane of the quad, identical)
-  const float* bb = model;  // base body block
-  float mscale = (bb[0] + payload) / bb[0];
-  SI I0;
-  rigid_si(bb, mscale, I0);
-  float p0[6], hm[6];
-  si_mul(I0, vb, hm);
-  crf(vb, hm, p0);
-  // gravity on the base is applied once (lane-independent); trunk corners split 2 per lane
-  float fbase[6] = {0, 0, 0, 0, 0, 0};
-  {
-    float gb[3];
-    mat3T_vec(R, g, gb);
-    float m = bb[0] * mscale;
-    float fg[3] = {m * gb[0], m * gb[1], m * gb[2]}, cg[3];
-    cross3(bb + 1, fg, cg);
-    p0[0] -= cg[0]; p0[1] -= cg[1]; p0[2] -= cg[2]; p0[3] -= fg[0]; p0[4] -= fg[1]; p0[5] -= fg[2];
-  }
+  // ---- trunk corners (two per lane) -> base external force, body coords
   const float* th = model + 13 * 10 + 4 * 9 + 3 + 1;  // trunk half extents
+  float fbase[6] = {0, 0, 0, 0, 0, 0};
   float Fb[3] = {0, 0, 0};
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    int cx = leg * 2 + k;
+    const int cx = leg * 2 + k;
     float lp[3] = {(cx & 1) ? th[0] : -th[0], (cx & 2) ? th[1] : -th[1], (cx & 4) ? th[2] : -th[2]};
     float pw[3], vw[3], F[3];
     point_kin(R, S.pos, vb, lp, pw, vw);
@@ -546,9 +576,14 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
     point_force(R, lp, F, fbase);
     Fb[0] += F[0]; Fb[1] += F[1]; Fb[2] += F[2];
   }
-  // ---- this leg: kinematics
+  // ---- this leg: kinematics, rigid bias forces, gravity and contacts (hip -> calf)
   const float* origin = model + 13 * 10 + leg * 9;
-  float E[3][9], vj[3][6], cj[3][6], Rw[3][9], pw_[3][3];
+  const float* foot = model + 13 * 10 + 4 * 9;
+  const float foot_r = foot[3];
+  const float thigh_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3];
+  const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
+  float cs[3][2], cj[3][6], pA[3][6];
+  float cfl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // thigh, calf, foot
   {
     float Rp[9], pp[3], vp[6];
 #pragma unroll
@@ -560,128 +595,133 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
     for (int j = 0; j < 3; ++j) {
       const int ax = j == 0 ? 0 : 1;
       const float* r = origin + j * 3;
-      float s, c;
-      sincosf(S.q[j], &s, &c);
-      joint_E(ax, c, s, E[j]);
-      xm(E[j], r, vp, vj[j]);
-      vj[j][ax] += S.qd[j];
-      float sq[3] = {0, 0, 0};
-      sq[ax] = S.qd[j];
-      cross3(vj[j], sq, cj[j]);
-      cross3(vj[j] + 3, sq, cj[j] + 3);
+      float sn, cn;
+      pm_sincosf(S.q[j], &sn, &cn);
+      cs[j][0] = cn; cs[j][1] = sn;
+      float vj[6];
+      xm(ax, cn, sn, r, vp, vj);
+      vj[ax] += S.qd[j];
+      // c_j = v_j x (S qd): S = unit axis ax
+      {
+        float sq[3] = {0, 0, 0};
+        sq[ax] = S.qd[j];
+        cross3(vj, sq, cj[j]);
+        cross3(vj + 3, sq, cj[j] + 3);
+      }
+      // world pose of link j: p = pp + Rp r ; Rw rows = E (rows of Rp)
       float rw[3];
       mat3_vec(Rp, r, rw);
-      pw_[j][0] = pp[0] + rw[0]; pw_[j][1] = pp[1] + rw[1]; pw_[j][2] = pp[2] + rw[2];
-      // Rw = Rp E^T
+      pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];
 #pragma unroll
-      for (int a = 0; a < 3; ++a)
+      for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
+      // rigid inertia about the link origin, bias force v x* I v
+      const float* B = model + 10 * (1 + leg * 3 + j);
+      SI I;
+      rigid_si(B, 1.0f, I);
+      float hm[6];
+      si_mul(I, vj, hm);
+      crf(vj, hm, pA[j]);
+      float gl[3], fext[6];
+      mat3T_vec(Rp, g, gl);
+      float fg[3] = {B[0] * gl[0], B[0] * gl[1], B[0] * gl[2]}, cg[3];
+      cross3(B + 1, fg, cg);
+      fext[0] = cg[0]; fext[1] = cg[1]; fext[2] = cg[2]; fext[3] = fg[0]; fext[4] = fg[1]; fext[5] = fg[2];
+      if (j == 1) {
 #pragma unroll
-        for (int b = 0; b < 3; ++b)
-          Rw[j][a * 3 + b] = Rp[a * 3 + 0] * E[j][b * 3 + 0] + Rp[a * 3 + 1] * E[j][b * 3 + 1] +
-                             Rp[a * 3 + 2] * E[j][b * 3 + 2];
+        for (int p = 0; p < 3; ++p) {
+          const float lp[3] = {0.0f, 0.0f, p == 0 ? -0.071f : (p == 1 ? -0.142f : -0.213f)};
+          float pw[3], vw[3], F[3];
+          point_kin(Rp, pp, vj, lp, pw, vw);
+          sphere_contact(T, C, pw, vw, thigh_r, F);
+          point_force(Rp, lp, F, fext);
+          cfl[0] += F[0]; cfl[1] += F[1]; cfl[2] += F[2];
+        }
+      } else if (j == 2) {
 #pragma unroll
-      for (int i = 0; i < 9; ++i) Rp[i] = Rw[j][i];
-      pp[0] = pw_[j][0]; pp[1] = pw_[j][1]; pp[2] = pw_[j][2];
+        for (int p = 0; p < 3; ++p) {
+          float lp[3], rr;
+          if (p < 2) { lp[0] = 0.0f; lp[1] = 0.0f; lp[2] = p == 0 ? -0.071f : -0.142f; rr = calf_r; }
+          else { lp[0] = foot[0]; lp[1] = foot[1]; lp[2] = foot[2]; rr = foot_r; }
+          float pw[3], vw[3], F[3];
+          point_kin(Rp, pp, vj, lp, pw, vw);
+          sphere_contact(T, C, pw, vw, rr, F);
+          point_force(Rp, lp, F, fext);
+          const int slot = p < 2 ? 3 : 6;
+          cfl[slot] += F[0]; cfl[slot + 1] += F[1]; cfl[slot + 2] += F[2];
+        }
+      }
 #pragma unroll
-      for (int i = 0; i < 6; ++i) vp[i] = vj[j][i];
+      for (int i = 0; i < 6; ++i) { pA[j][i] -= fext[i]; vp[i] = vj[i]; }
     }
   }
-  // ---- rigid inertias, bias and external forces
-  SI IA[3];
-  float pA[3][6];
-  const float* foot = model + 13 * 10 + 4 * 9;
-  const float foot_r = foot[3];
-  const float thigh_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3];
-  const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
-  float cfl[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};  // thigh, calf, foot
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const float* B = model + 10 * (1 + leg * 3 + j);
-    rigid_si(B, 1.0f, IA[j]);
-    float hmj[6];
-    si_mul(IA[j], vj[j], hmj);
-    crf(vj[j], hmj, pA[j]);
-    float gl[3], fext[6] = {0, 0, 0, 0, 0, 0};
-    mat3T_vec(Rw[j], g, gl);
-    float fg[3] = {B[0] * gl[0], B[0] * gl[1], B[0] * gl[2]}, cg[3];
-    cross3(B + 1, fg, cg);
-    fext[0] = cg[0]; fext[1] = cg[1]; fext[2] = cg[2]; fext[3] = fg[0]; fext[4] = fg[1]; fext[5] = fg[2];
-    if (j == 1) {
-      const float zs[3] = {-0.071f, -0.142f, -0.213f};
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        float lp[3] = {0.0f, 0.0f, zs[p]}, pw[3], vw[3], F[3];
-        point_kin(Rw[j], pw_[j], vj[j], lp, pw, vw);
-        sphere_contact(T, C, pw, vw, thigh_r, F);
-        point_force(Rw[j], lp, F, fext);
-        cfl[0][0] += F[0]; cfl[0][1] += F[1]; cfl[0][2] += F[2];
-      }
-    } else if (j == 2) {
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        float lp[3], rr;
-        if (p < 2) { lp[0] = 0.0f; lp[1] = 0.0f; lp[2] = p == 0 ? -0.071f : -0.142f; rr = calf_r; }
-        else { lp[0] = foot[0]; lp[1] = foot[1]; lp[2] = foot[2]; rr = foot_r; }
-        float pw[3], vw[3], F[3];
-        point_kin(Rw[j], pw_[j], vj[j], lp, pw, vw);
-        sphere_contact(T, C, pw, vw, rr, F);
-        point_force(Rw[j], lp, F, fext);
-        int slot = p < 2 ? 1 : 2;
-        cfl[slot][0] += F[0]; cfl[slot][1] += F[1]; cfl[slot][2] += F[2];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) pA[j][i] -= fext[i];
-  }
-  // ---- backward pass calf -> hip
+  // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
   float U[3][6], D[3], u[3];
   SI Ip;
   float pp6[6];
+  {
+    SI IA;
+    rigid_si(model + 10 * (1 + leg * 3 + 2), 1.0f, IA);
 #pragma unroll
-  for (int j = 2; j >= 0; --j) {
-    const int ax = j == 0 ? 0 : 1;
-    const int dof = leg * 3 + j;
-    float t = tau[j];
-    float lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1];
-    if (S.q[j] > hi) t -= cfg->limit_stiffness * (S.q[j] - hi) + cfg->limit_damping * S.qd[j];
-    else if (S.q[j] < lo) t -= cfg->limit_stiffness * (S.q[j] - lo) + cfg->limit_damping * S.qd[j];
+    for (int j = 2; j >= 0; --j) {
+      const int ax = j == 0 ? 0 : 1;
+      const int dof = leg * 3 + j;
+      float t = tau[j];
+      const float lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1];
+      if (S.q[j] > hi) t -= cfg->limit_stiffness * (S.q[j] - hi) + cfg->limit_damping * S.qd[j];
+      else if (S.q[j] < lo) t -= cfg->limit_stiffness * (S.q[j] - lo) + cfg->limit_damping * S.qd[j];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) U[j][i] = si_get(IA[j], i, ax);
-    D[j] = si_get(IA[j], ax, ax);
-    u[j] = t - pA[j][ax];
-    float invD = 1.0f / D[j];
-    SI Ia;
-    // Ia = IA - U U^T / D
-    float Ua[3] = {U[j][0], U[j][1], U[j][2]}, Ul[3] = {U[j][3], U[j][4], U[j][5]};
-    Ia.a[0] = IA[j].a[0] - Ua[0] * Ua[0] * invD; Ia.a[1] = IA[j].a[1] - Ua[0] * Ua[1] * invD;
-    Ia.a[2] = IA[j].a[2] - Ua[0] * Ua[2] * invD; Ia.a[3] = IA[j].a[3] - Ua[1] * Ua[1] * invD;
-    Ia.a[4] = IA[j].a[4] - Ua[1] * Ua[2] * invD; Ia.a[5] = IA[j].a[5] - Ua[2] * Ua[2] * invD;
+      for (int i = 0; i < 6; ++i) U[j][i] = si_get(IA, i, ax);
+      D[j] = si_get(IA, ax, ax);
+      u[j] = t - pA[j][ax];
+      const float invD = 1.0f / D[j];
+      const float Ua[3] = {U[j][0], U[j][1], U[j][2]}, Ul[3] = {U[j][3], U[j][4], U[j][5]};
+      SI Ia;
+      Ia.a[0] = IA.a[0] - Ua[0] * Ua[0] * invD; Ia.a[1] = IA.a[1] - Ua[0] * Ua[1] * invD;
+      Ia.a[2] = IA.a[2] - Ua[0] * Ua[2] * invD; Ia.a[3] = IA.a[3] - Ua[1] * Ua[1] * invD;
+      Ia.a[4] = IA.a[4] - Ua[1] * Ua[2] * invD; Ia.a[5] = IA.a[5] - Ua[2] * Ua[2] * invD;
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
+      for (int a = 0; a < 3; ++a)
 #pragma unroll
-      for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA[j].b[a * 3 + b] - Ua[a] * Ul[b] * invD;
-    Ia.c[0] = IA[j].c[0] - Ul[0] * Ul[0] * invD; Ia.c[1] = IA[j].c[1] - Ul[0] * Ul[1] * invD;
-    Ia.c[2] = IA[j].c[2] - Ul[0] * Ul[2] * invD; Ia.c[3] = IA[j].c[3] - Ul[1] * Ul[1] * invD;
-    Ia.c[4] = IA[j].c[4] - Ul[1] * Ul[2] * invD; Ia.c[5] = IA[j].c[5] - Ul[2] * Ul[2] * invD;
-    float Iac[6], pa[6];
-    si_mul(Ia, cj[j], Iac);
+        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Ua[a] * Ul[b] * invD;
+      Ia.c[0] = IA.c[0] - Ul[0] * Ul[0] * invD; Ia.c[1] = IA.c[1] - Ul[0] * Ul[1] * invD;
+      Ia.c[2] = IA.c[2] - Ul[0] * Ul[2] * invD; Ia.c[3] = IA.c[3] - Ul[1] * Ul[1] * invD;
+      Ia.c[4] = IA.c[4] - Ul[1] * Ul[2] * invD; Ia.c[5] = IA.c[5] - Ul[2] * Ul[2] * invD;
+      float Iac[6], pa[6], pt[6];
+      si_mul(Ia, cj[j], Iac);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) pa[i] = pA[j][i] + Iac[i] + U[j][i] * u[j] * invD;
-    SI It;
-    float pt[6];
-    xform_inertia(E[j], origin + j * 3, Ia, It);
-    xfT(E[j], origin + j * 3, pa, pt);
-    if (j > 0) {
-      si_add(IA[j - 1], It);
+      for (int i = 0; i < 6; ++i) pa[i] = pA[j][i] + Iac[i] + U[j][i] * u[j] * invD;
+      SI It;
+      xform_inertia(ax, cs[j][0], cs[j][1], origin + j * 3, Ia, It);
+      xfT(ax, cs[j][0], cs[j][1], origin + j * 3, pa, pt);
+      if (j > 0) {
+        rigid_si(model + 10 * (1 + leg * 3 + j - 1), 1.0f, IA);
+        si_add(IA, It);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) pA[j - 1][i] += pt[i];
-    } else {
-      Ip = It;
+        for (int i = 0; i < 6; ++i) pA[j - 1][i] += pt[i];
+      } else {
+        Ip = It;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) pp6[i] = pt[i];
+        for (int i = 0; i < 6; ++i) pp6[i] = pt[i];
+      }
     }
   }
-  // ---- quad reduction: sum of the four legs' contributions and the trunk corners
+  // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
+  const float* bb = model;
+  const float mscale = (bb[0] + payload) / bb[0];
+  SI I0;
+  rigid_si(bb, mscale, I0);
+  float p0[6];
+  {
+    float hm[6];
+    si_mul(I0, vb, hm);
+    crf(vb, hm, p0);
+    float gb[3];
+    mat3T_vec(R, g, gb);
+    const float m = bb[0] * mscale;
+    float fg[3] = {m * gb[0], m * gb[1], m * gb[2]}, cg[3];
+    cross3(bb + 1, fg, cg);
+    p0[0] -= cg[0]; p0[1] -= cg[1]; p0[2] -= cg[2]; p0[3] -= fg[0]; p0[4] -= fg[1]; p0[5] -= fg[2];
+  }
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     Ip.a[i] = qsum(Ip.a[i]);
@@ -705,7 +745,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
     for (int j = 0; j < 3; ++j) {
       const int ax = j == 0 ? 0 : 1;
       float aj[6];
-      xm(E[j], origin + j * 3, ap, aj);
+      xm(ax, cs[j][0], cs[j][1], origin + j * 3, ap, aj);
 #pragma unroll
       for (int i = 0; i < 6; ++i) aj[i] += cj[j][i];
       float Ua = 0.0f;
@@ -730,19 +770,19 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
     S.pos[i] += h * S.v[i];
   }
   {
-    float wn = sqrtf(S.w[0] * S.w[0] + S.w[1] * S.w[1] + S.w[2] * S.w[2]);
-    float thh = 0.5f * h * wn;
+    const float wn = sqrtf(S.w[0] * S.w[0] + S.w[1] * S.w[1] + S.w[2] * S.w[2]);
+    const float thh = 0.5f * h * wn;
     float sth, cth;
-    sincosf(thh, &sth, &cth);
-    float sc = thh > 1e-12f ? sth / wn : 0.5f * h;
-    float dq[4] = {S.w[0] * sc, S.w[1] * sc, S.w[2] * sc, cth};
+    pm_sincosf(thh, &sth, &cth);
+    const float sc = thh > 1e-12f ? sth / wn : 0.5f * h;
+    const float dq[4] = {S.w[0] * sc, S.w[1] * sc, S.w[2] * sc, cth};
     float* q = S.quat;
     float nq[4];
     nq[3] = dq[3] * q[3] - dq[0] * q[0] - dq[1] * q[1] - dq[2] * q[2];
     nq[0] = dq[3] * q[0] + dq[0] * q[3] + dq[1] * q[2] - dq[2] * q[1];
     nq[1] = dq[3] * q[1] - dq[0] * q[2] + dq[1] * q[3] + dq[2] * q[0];
     nq[2] = dq[3] * q[2] + dq[0] * q[1] - dq[1] * q[0] + dq[2] * q[3];
-    float inv = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+    const float inv = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = nq[i] * inv;
   }
@@ -753,7 +793,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
   }
   if (cf_out) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) cf_leg[i] = (&cfl[0][0])[i];
+    for (int i = 0; i < 9; ++i) cf_leg[i] = cfl[i];
     cf_base[0] = qsum(Fb[0]);
     cf_base[1] = qsum(Fb[1]);
     cf_base[2] = qsum(Fb[2]);
@@ -824,39 +864,62 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const go1_step_args& A = K.a;
   const int n = c->n_envs;
   const int leg = threadIdx.x & 3;
-  const int e = blockIdx.x * EPB + (threadIdx.x >> 2);
-  if (e >= n) return;  // whole quads exit together
+  const int lane = threadIdx.x & 63, lq = lane >> 4;
+  const int e = blockIdx.x * EPB + (threadIdx.x >> 2);  // n % EPB == 0 (go1_create): every wave is full
+  (void)n;
+  MlpFrag F;
+  mlp_load(c->actuator, lane, F);
   const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e};
   const size_t d0 = (size_t)e * NDOF + leg * 3;
+  const float* lag_in = st.lag + (size_t)e * 84 + leg * 3;
 
   // ---------------- load
-  float act[3], root[13], q[3], qd[3], lag[GO1_LAG_SLOTS][3], eh[2][3], vh[2][3], strength[3], offset[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) act[j] = clampf(A.actions[d0 + j], -c->clip_actions, c->clip_actions);
-#pragma unroll
-  for (int i = 0; i < 13; ++i) root[i] = st.root[(size_t)e * 13 + i];
+  float act[3], q[3], qd[3], eh[2][3], vh[2][3], strength[3], offset[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
+    act[j] = clampf(A.actions[d0 + j], -c->clip_actions, c->clip_actions);
     q[j] = st.dof_pos[d0 + j];
     qd[j] = st.dof_vel[d0 + j];
     strength[j] = st.motor_strength[d0 + j];
     offset[j] = st.motor_offset[d0 + j];
-#pragma unroll
-    for (int s = 0; s < GO1_LAG_SLOTS; ++s) lag[s][j] = st.lag[(size_t)e * 84 + s * 12 + leg * 3 + j];
     eh[0][j] = st.pos_err_hist[(size_t)e * 24 + leg * 3 + j];
     eh[1][j] = st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j];
     vh[0][j] = st.vel_hist[(size_t)e * 24 + leg * 3 + j];
     vh[1][j] = st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j];
   }
   const float friction = st.friction[e], payload = st.payload[e];
-  Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale};
+  Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
+  __shared__ float2 s_patch[EPB][PSZ * PSZ];
+  __shared__ int s_patch_meta[EPB][3];
   if (c->terrain_kind == 1) {
-    T.tile = K.ter.tiles + (size_t)K.ter.env_tile[e] * 2 * c->hf_nx * c->hf_ny;
+    const int tix = K.ter.env_tile[e];
+    T.tile = K.ter.tiles + (size_t)tix * 2 * c->hf_nx * c->hf_ny;
     T.ox = K.ter.env_terrain_origin[(size_t)e * 3];
     T.oy = K.ter.env_terrain_origin[(size_t)e * 3 + 1];
+    if (!INJ) {
+      // patch centred on the base at the start of the step
+      const float bx = st.root[(size_t)e * 13], by = st.root[(size_t)e * 13 + 1];
+      T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(c->hf_nx + 64))) - PSZ / 2;
+      T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(c->hf_ny + 64))) - PSZ / 2;
+      T.patch = &s_patch[threadIdx.x >> 2][0];
+      if (leg == 0) {
+        s_patch_meta[threadIdx.x >> 2][0] = tix;
+        s_patch_meta[threadIdx.x >> 2][1] = T.pi0;
+        s_patch_meta[threadIdx.x >> 2][2] = T.pj0;
+      }
+      __syncthreads();
+      const int nx = c->hf_nx, ny = c->hf_ny;
+      for (int idx = threadIdx.x; idx < EPB * PSZ * PSZ; idx += TPB) {
+        const int el = idx / (PSZ * PSZ), cell = idx - el * (PSZ * PSZ);
+        const int ci = cell / PSZ, cj = cell - ci * PSZ;
+        const int gi = min(max(s_patch_meta[el][1] + ci, 0), nx - 1);
+        const int gj = min(max(s_patch_meta[el][2] + cj, 0), ny - 1);
+        const float* tl = K.ter.tiles + (size_t)s_patch_meta[el][0] * 2 * nx * ny;
+        s_patch[el][cell] = make_float2(tl[((size_t)nx + gi) * ny + gj], tl[(size_t)gi * ny + gj]);
+      }
+      __syncthreads();
+    }
   }
-
-  // ---------------- decimation loop (:82-88)
   float scaled[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -864,39 +927,70 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (j == 0) scaled[j] = scaled[j] * c->hip_scale_reduction;
   }
   Phys P;
+  if (!INJ) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    P.pos[i] = root[i]; P.v[i] = root[7 + i]; P.w[i] = root[10 + i];
+    for (int i = 0; i < 3; ++i) {
+      P.pos[i] = st.root[(size_t)e * 13 + i];
+      P.v[i] = st.root[(size_t)e * 13 + 7 + i];
+      P.w[i] = st.root[(size_t)e * 13 + 10 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) P.quat[i] = root[3 + i];
+
+  // ---------------- decimation loop (:82-88)
+  // The lag ring is pushed once per sim sub-step with the same scaled action
+  // (:973), so sub-step s reads the slot s+1 of the incoming ring and the ring
+  // leaves the step as [old4, old5, old6, scaled x 4].
   float torque[3], tgt[3];
   float cf_leg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_base[3] = {0, 0, 0};
   const int dec = c->decimation;
   for (int sub = 0; sub < dec; ++sub) {
-    // _compute_torques (:957-996).  The weight pointer is laundered each sub-step so the
-    // 1313 weights are re-read through the scalar cache instead of being hoisted into
-    // (and spilled from) SGPRs for the whole loop.
-    const float* W = c->actuator;
-    asm volatile("" : "+s"(W));
-#pragma unroll
-    for (int s = 0; s < GO1_LAG_SLOTS - 1; ++s)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) lag[s][j] = lag[s + 1][j];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) lag[GO1_LAG_SLOTS - 1][j] = scaled[j];
+    // _compute_torques (:957-996): inputs of this lane's three joints ...
+    const int slot = sub + 1;
+    float xin[3][6];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int d = leg * 3 + j;
-      tgt[j] = lag[0][j] + c->default_dof_pos[d];
-      float err = q[j] - tgt[j] + offset[j];
-      float t = actuator_eval(W, err, eh[0][j], eh[1][j], qd[j], vh[0][j], vh[1][j]);
+      const float lg = slot < GO1_LAG_SLOTS ? lag_in[slot * 12 + j] : scaled[j];
+      tgt[j] = lg + c->default_dof_pos[d];
+      const float err = q[j] - tgt[j] + offset[j];
+      xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
+      xin[j][3] = qd[j]; xin[j][4] = vh[0][j]; xin[j][5] = vh[1][j];
+    }
+    // ... -> 12 MFMA groups per wave: group (joint j, lane row qq) holds the items of
+    // envs 4qq..4qq+3 x legs, whose owner lanes are 16 qq + (lane & 15).
+    float tq[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int src = 16 * qq + (lane & 15);
+        float y[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) y[k] = __shfl(xin[j][k], src);
+        const float b0 = lq == 0 ? y[0] : (lq == 1 ? y[1] : (lq == 2 ? y[2] : y[3]));
+        const float b1v = lq == 0 ? y[4] : (lq == 1 ? y[5] : 0.0f);
+#ifdef GO1_ABL_NO_MLP
+        const float t = 0.0f * (b0 + b1v);  // ablation build only: no actuator net
+#else
+        const float t = mlp_group(F, b0, b1v);
+#endif
+        if (lq == qq) tq[j] = t;
+      }
+#ifdef GO1_ABL_NO_MLP
+#pragma unroll
+    for (int j = 0; j < 3; ++j) tq[j] += -20.0f * xin[j][0] - 0.5f * xin[j][3];  // PD stand-in
+#endif
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int d = leg * 3 + j;
       eh[1][j] = eh[0][j];
-      eh[0][j] = err;
+      eh[0][j] = xin[j][0];
       vh[1][j] = vh[0][j];
       vh[0][j] = qd[j];
-      t = t * strength[j];
-      float lim = c->torque_limits[d];
+      const float t = tq[j] * strength[j];
+      const float lim = c->torque_limits[d];
       torque[j] = clampf(t, -lim, lim);
       if (A.dbg_torques) A.dbg_torques[((size_t)sub * n + e) * NDOF + d] = torque[j];
     }
@@ -912,14 +1006,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int j = 0; j < 3; ++j) { P.q[j] = q[j]; P.qd[j] = qd[j]; }
       for (int k = 0; k < c->n_internal; ++k) {
-        bool last = (sub == dec - 1) && (k == c->n_internal - 1);
+        const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
+#ifndef GO1_ABL_NO_PHYS
         phys_substep(c, P, torque, h, A.sim_gravity, friction, payload, T, leg, last, cf_leg, cf_base);
+#else
+        (void)last; (void)h;
+        P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];
+#endif
       }
 #pragma unroll
       for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }
     }
   }
-  float cf[NB * 3];  // only the entries this lane needs: base + its leg
+  float root[13];
   if (INJ) {
 #pragma unroll
     for (int i = 0; i < 13; ++i) root[i] = A.inj_root[(size_t)e * 13 + i];
@@ -938,7 +1037,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 4; ++i) root[3 + i] = P.quat[i];
   }
-  (void)cf;
   if (A.contact_forces) {
     float* o = A.contact_forces + (size_t)e * NB * 3;
     if (leg == 0) { o[0] = cf_base[0]; o[1] = cf_base[1]; o[2] = cf_base[2]; }
@@ -949,103 +1047,105 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 
   // ================= post_physics_step (:114-169), contraction off =================
-  int ep = st.episode_length[e] + 1;
-  float qb[4] = {root[3], root[4], root[5], root[6]};
-  float blv[3], bav[3], pg[3];
-  quat_rotate_inverse_f(qb, root + 7, blv);
-  quat_rotate_inverse_f(qb, root + 10, bav);
-  quat_rotate_inverse_f(qb, A.gravity_vec, pg);
-  float brot_prev[3] = {st.base_rotation[(size_t)e * 3], st.base_rotation[(size_t)e * 3 + 1],
-                        st.base_rotation[(size_t)e * 3 + 2]};
-  const float cam_pitch = brot_prev[1];
-
-  // _plan_target_pose / _compute_relative_target_pose (:850-932)
-  float traj[6];
+  const int ep = st.episode_length[e] + 1;
+  float blv[3], bav[3], pg[3], rpy[3], rel_lin[3], rel_rot[3];
+  {
+    const float qb[4] = {root[3], root[4], root[5], root[6]};
+    quat_rotate_inverse_f(qb, root + 7, blv);
+    quat_rotate_inverse_f(qb, root + 10, bav);
+    quat_rotate_inverse_f(qb, A.gravity_vec, pg);
+    // _plan_target_pose / _compute_relative_target_pose (:850-932)
+    const float* tr = st.trajectory + (size_t)e * 6;
+    const float rel_in[3] = {tr[0] - root[0], tr[1] - root[1], tr[2] - root[2]};
+    quat_apply_yaw_inverse_f(qb, rel_in, rel_lin);
+    quat_to_rpy_f(qb, rpy);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) traj[i] = st.trajectory[(size_t)e * 6 + i];
-  float rel_in[3] = {traj[0] - root[0], traj[1] - root[1], traj[2] - root[2]};
-  float rel_lin[3], rpy[3], rel_rot[3];
-  quat_apply_yaw_inverse_f(qb, rel_in, rel_lin);
-  quat_to_rpy_f(qb, rpy);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) rel_rot[i] = wrap_to_pi_f(traj[3 + i] - rpy[i]);
+    for (int i = 0; i < 3; ++i) rel_rot[i] = wrap_to_pi_f(tr[3 + i] - rpy[i]);
+  }
+  const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
   float cmd[2] = {rel_lin[0], rel_lin[1]};
 
   // DR every rand_interval (:822-824)
   if (ep % c->rand_interval == 0) {
-    float s = rng(34) * c->strength_range + c->strength_lo;
+    const float sv = rng(34) * c->strength_range + c->strength_lo;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      strength[j] = s;
+      strength[j] = sv;
       offset[j] = rng(35 + leg * 3 + j) * c->offset_range + c->offset_lo;
     }
   }
-  float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
-  bool switched = rel_norm < c->switch_dist;
+  const float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
+  const bool switched = rel_norm < c->switch_dist;
   int idx = st.curr_pose_index[e];
   if (switched) { idx += 1; if (idx > 0) idx = 0; }
-  bool reached = switched && idx == 0;
+  const bool reached = switched && idx == 0;
   // collision count (:848): this lane's thigh + calf, base on lane 0
   float coll_l = (norm3_f(cf_leg[0], cf_leg[1], cf_leg[2]) > 0.1f ? 1.0f : 0.0f) +
                  (norm3_f(cf_leg[3], cf_leg[4], cf_leg[5]) > 0.1f ? 1.0f : 0.0f);
   if (leg == 0 && norm3_f(cf_base[0], cf_base[1], cf_base[2]) > 0.1f) coll_l += 1.0f;
-  float coll = qsum(coll_l);
+  const float coll = qsum(coll_l);
 
   // check_termination (:198-216)
-  bool time_out = (float)ep > c->max_episode_length;
+  const bool time_out = (float)ep > c->max_episode_length;
   bool reset = time_out;
   if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = true;
+  if (!INJ) {
+    // native-integrator divergence guard (no reference counterpart: PhysX does not
+    // return non-finite states): an env whose state is not finite is reset
+    bool finite = true;
+#pragma unroll
+    for (int i = 0; i < 13; ++i) finite = finite && isfinite(root[i]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) finite = finite && isfinite(q[j]) && isfinite(qd[j]);
+    finite = qsum(finite ? 0.0f : 1.0f) == 0.0f;
+    if (!finite) reset = true;
+  }
 
   // rewards (:320-355, reward_crawling.py)
-  const float* ldv = st.last_dof_vel + d0;
-  const float* la = st.last_actions + d0;
-  float t_tq = 0.0f, t_acc = 0.0f, t_ar = 0.0f, t_lim = 0.0f;
+  float terms[GO1_NUM_TERMS];
   {
+    const float* ldv = st.last_dof_vel + d0;
+    const float* la = st.last_actions + d0;
     float x[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) x[j] = sq_f(torque[j]);
-    t_tq = qsum((x[0] + x[1]) + x[2]);
+    terms[0] = qsum((x[0] + x[1]) + x[2]);
 #pragma unroll
     for (int j = 0; j < 3; ++j) x[j] = sq_f((ldv[j] - qd[j]) / c->dt);
-    t_acc = qsum((x[0] + x[1]) + x[2]);
+    terms[1] = qsum((x[0] + x[1]) + x[2]);
+    terms[2] = coll;
 #pragma unroll
     for (int j = 0; j < 3; ++j) x[j] = sq_f(la[j] - act[j]);
-    t_ar = qsum((x[0] + x[1]) + x[2]);
+    terms[3] = qsum((x[0] + x[1]) + x[2]);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int d = leg * 3 + j;
-      float lo = q[j] - c->dof_pos_limits[2 * d];
-      float hi = q[j] - c->dof_pos_limits[2 * d + 1];
-      float o = -(lo < 0.0f ? lo : 0.0f);
+      const float lo = q[j] - c->dof_pos_limits[2 * d];
+      const float hi = q[j] - c->dof_pos_limits[2 * d + 1];
+      const float o = -(lo < 0.0f ? lo : 0.0f);
       x[j] = o + (hi > 0.0f ? hi : 0.0f);
     }
-    t_lim = qsum((x[0] + x[1]) + x[2]);
+    terms[4] = qsum((x[0] + x[1]) + x[2]);
   }
-  float terms[GO1_NUM_TERMS];
-  terms[0] = t_tq;
-  terms[1] = t_acc;
-  terms[2] = coll;
-  terms[3] = t_ar;
-  terms[4] = t_lim;
   terms[5] = sq_f(root[2] - c->base_height_target);
   terms[6] = sq_f(bav[0]) + sq_f(bav[1]);
   {
-    float mag = norm2_f(rel_lin[0], rel_lin[1]);
-    float lerr = sq_f(blv[0]) + sq_f(blv[1]);
-    float r_e2e = expf(-lerr / c->tracking_sigma_lin);
+    const float mag = norm2_f(rel_lin[0], rel_lin[1]);
+    const float lerr = sq_f(blv[0]) + sq_f(blv[1]);
+    const float r_e2e = expf(-lerr / c->tracking_sigma_lin);
     terms[7] = r_e2e * (mag < c->switch_dist ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
     float tx = rel_lin[0] / (mag + 1e-6f) * c->target_lin_vel;
     float ty = rel_lin[1] / (mag + 1e-6f) * c->target_lin_vel;
-    float gate = mag > c->lin_reaching_criterion ? 1.0f : 0.0f;
+    const float gate = mag > c->lin_reaching_criterion ? 1.0f : 0.0f;
     tx = tx * gate;
     ty = ty * gate;
-    float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
+    const float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
     terms[8] = expf(-le / c->tracking_sigma_lin);
     float ta = rel_rot[2];
-    float m = fabsf(ta);
+    const float m = fabsf(ta);
     ta = ta / (m + 1e-6f) * c->target_ang_vel;
     ta = ta * (m > c->ang_reaching_criterion ? 1.0f : 0.0f);
-    float ae = sq_f(ta - bav[2]);
+    const float ae = sq_f(ta - bav[2]);
     terms[9] = expf(-ae / c->tracking_sigma_ang);
   }
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
@@ -1054,7 +1154,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = st.episode_sums[(size_t)e * GO1_NUM_SUMS + k];
 #pragma unroll
   for (int k = 0; k < GO1_NUM_TERMS; ++k) {
-    float r = terms[k] * A.reward_scales[k];
+    const float r = terms[k] * A.reward_scales[k];
     rew = rew + r;
     if (A.reward_scales[k] >= 0.0f) pos = pos + r; else neg = neg + r;
     sums[k] = sums[k] + r;
@@ -1066,63 +1166,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int k = 0; k < GO1_NUM_TERMS; ++k) A.dbg_terms[(size_t)e * GO1_NUM_TERMS + k] = terms[k];
 
-  // ---- height scan (:1918-1965): uses the pre-reset root and the previous pitch
-  const int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
-  const int n_rows = GO1_GRID_X - x_start;
-  const int n_pts = n_rows * GO1_GRID_Y;
-  float hvals[2][28];  // this lane's points p = leg + 4 k, k < 28  (n_pts <= 231 needs debug path)
-  const bool plane = c->terrain_kind == 0;
-  float camx = 0.0f, camy = 0.0f;
-  if (!plane) {
-    float cos_p = pm_cosf(cam_pitch);
-    camx = c->camera_offset_x * cos_p;
-    camy = 0.0f * cos_p;
-  }
-  auto sample = [&](int i, int j, float& h0, float& h1) {
-    if (plane) { h0 = 1.0f; h1 = 0.0f; return; }
-    float px = c->height_grid_x[i] + root[0];
-    float py = c->height_grid_y[j] + root[1];
-    if (c->camera_zero) { px = px + camx; py = py + camy; }
-    px = px - T.ox;
-    py = py - T.oy;
-    long ix = (long)(px / c->horizontal_scale);
-    long iy = (long)(py / c->horizontal_scale);
-    ix = ix < 0 ? 0 : (ix > c->hf_nx - 2 ? c->hf_nx - 2 : ix);
-    iy = iy < 0 ? 0 : (iy > c->hf_ny - 2 ? c->hf_ny - 2 : iy);
-    h0 = T.tile[(size_t)ix * c->hf_ny + iy];
-    h1 = T.tile[((size_t)c->hf_nx + ix) * c->hf_ny + iy];
-  };
-#pragma unroll
-  for (int k = 0; k < 28; ++k) {
-    int p = leg + 4 * k;
-    if (p < n_pts && k < 28) {
-      int i = x_start + p / GO1_GRID_Y, j = p % GO1_GRID_Y;
-      sample(i, j, hvals[0][k], hvals[1][k]);
-    }
-  }
-  if (A.dbg_heights) {
-    float* o = A.dbg_heights + (size_t)e * 2 * GO1_GRID_X * GO1_GRID_Y;
-    for (int p = leg; p < GO1_GRID_X * GO1_GRID_Y; p += 4) {
-      float h0, h1;
-      sample(p / GO1_GRID_Y, p % GO1_GRID_Y, h0, h1);
-      o[p] = h0;
-      o[GO1_GRID_X * GO1_GRID_Y + p] = h1;
-    }
-  }
-
-  // ---- reset_idx (:218-296)
+  // ---- reset_idx (:218-296); the height scan below still samples at the pre-reset pose
+  const float scan_x = root[0], scan_y = root[1];
   float traj_new[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) traj_new[i] = traj[i];
+  for (int i = 0; i < 6; ++i) traj_new[i] = st.trajectory[(size_t)e * 6 + i];
   if (reset) {
     reset_env(c, K.ter, rng, e, leg, root, q, qd, strength, offset, traj_new);
     idx = 0;
 #pragma unroll
     for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < GO1_LAG_SLOTS; ++s)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) lag[s][j] = 0.0f;
     cmd[0] = 0.0f;  // commands is a view of local_relative_linear, zeroed by reset_idx (:252, :802)
     cmd[1] = 0.0f;
   }
@@ -1149,27 +1202,61 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     put(17 + d, qd[j] * c->obs_scale_dof_vel, c->noise_dof_vel, true);
     put(29 + d, act[j], 0.0f, false);
   }
+  // height scan (:1918-1965) fused with the height observations (:395-411)
   {
-    const float zroot = root[2];
+    const bool plane = c->terrain_kind == 0;
+    float camx = 0.0f, camy = 0.0f;
+    if (!plane) {
+      const float cos_p = pm_cosf(cam_pitch);
+      camx = c->camera_offset_x * cos_p;
+      camy = 0.0f * cos_p;
+    }
+    auto sample = [&](int i, int j, float& h0, float& h1) {
+      if (plane) { h0 = 1.0f; h1 = 0.0f; return; }
+      float px = c->height_grid_x[i] + scan_x;
+      float py = c->height_grid_y[j] + scan_y;
+      if (c->camera_zero) { px = px + camx; py = py + camy; }
+      px = px - T.ox;
+      py = py - T.oy;
+      // .long() truncation then clip (:1948-1952); the float is bounded first so that a
+      // non-finite pose cannot turn the conversion into undefined behaviour
+      const float fx = fminf(fmaxf(px / c->horizontal_scale, -1.0f), (float)c->hf_nx);
+      const float fy = fminf(fmaxf(py / c->horizontal_scale, -1.0f), (float)c->hf_ny);
+      int ix = (int)fx, iy = (int)fy;
+      ix = ix < 0 ? 0 : (ix > c->hf_nx - 2 ? c->hf_nx - 2 : ix);
+      iy = iy < 0 ? 0 : (iy > c->hf_ny - 2 ? c->hf_ny - 2 : iy);
+      h0 = T.tile[(size_t)ix * c->hf_ny + iy];
+      h1 = T.tile[((size_t)c->hf_nx + ix) * c->hf_ny + iy];
+    };
+    const int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
+    const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
+    const float zroot = root[2];  // post-reset (:401)
     const float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
+    for (int p = leg; p < n_pts; p += 4) {
+      float hv[2];
+      sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[0], hv[1]);
 #pragma unroll
-    for (int k = 0; k < 28; ++k) {
-      int p = leg + 4 * k;
-      if (p < n_pts) {
-#pragma unroll
-        for (int layer = 0; layer < 2; ++layer) {
-          float h = hvals[layer][k];
-          if (c->camera_zero) {
-            h = h - zroot;
-            h = h - cam_z;
-            h = clampf(h, -0.3f, 0.3f);
-          } else {
-            h = clampf(h, 0.0f, c->ceiling_height);
-            h = h / c->ceiling_height;
-            h = h - 0.5f;
-          }
-          o[41 + layer * n_pts + p] = clampf(h * c->obs_scale_heights, -clip, clip);
+      for (int layer = 0; layer < 2; ++layer) {
+        float hh = hv[layer];
+        if (c->camera_zero) {
+          hh = hh - zroot;
+          hh = hh - cam_z;
+          hh = clampf(hh, -0.3f, 0.3f);
+        } else {
+          hh = clampf(hh, 0.0f, c->ceiling_height);
+          hh = hh / c->ceiling_height;
+          hh = hh - 0.5f;
         }
+        o[41 + layer * n_pts + p] = clampf(hh * c->obs_scale_heights, -clip, clip);
+      }
+    }
+    if (A.dbg_heights) {
+      float* od = A.dbg_heights + (size_t)e * 2 * GO1_GRID_X * GO1_GRID_Y;
+      for (int p = leg; p < GO1_GRID_X * GO1_GRID_Y; p += 4) {
+        float h0, h1;
+        sample(p / GO1_GRID_Y, p % GO1_GRID_Y, h0, h1);
+        od[p] = h0;
+        od[GO1_GRID_X * GO1_GRID_Y + p] = h1;
       }
     }
   }
@@ -1180,6 +1267,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 
   // ---------------- write back (epilogue :148-153)
+  float lag_out[GO1_LAG_SLOTS][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int s2 = 0; s2 < GO1_LAG_SLOTS; ++s2) {
+      const int src = s2 + dec;  // slot after `dec` pushes
+      lag_out[s2][j] = reset ? 0.0f : (src < GO1_LAG_SLOTS ? lag_in[src * 12 + j] : scaled[j]);
+    }
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     st.dof_pos[d0 + j] = q[j];
@@ -1190,7 +1285,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     st.motor_offset[d0 + j] = offset[j];
     st.joint_pos_target[d0 + j] = tgt[j];
 #pragma unroll
-    for (int s = 0; s < GO1_LAG_SLOTS; ++s) st.lag[(size_t)e * 84 + s * 12 + leg * 3 + j] = lag[s][j];
+    for (int s2 = 0; s2 < GO1_LAG_SLOTS; ++s2) st.lag[(size_t)e * 84 + s2 * 12 + leg * 3 + j] = lag_out[s2][j];
     st.pos_err_hist[(size_t)e * 24 + leg * 3 + j] = eh[0][j];
     st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j] = eh[1][j];
     st.vel_hist[(size_t)e * 24 + leg * 3 + j] = vh[0][j];
@@ -1215,7 +1310,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (A.dbg_reached) A.dbg_reached[e] = reached;
   }
   // one atomic per wave when any env of the wave reset (extras["time_outs"] rebinding, :289-291)
-  if (__ballot(reset && leg == 0) != 0ull && threadIdx.x == 0) atomicOr(K.any_reset, 1);
+  if (__ballot(reset && leg == 0) != 0ull && (threadIdx.x & 63) == 0) atomicOr(K.any_reset, 1);
 }
 
 // extras["time_outs"] is rebound to time_out_buf only on steps where reset_idx ran.
@@ -1261,12 +1356,21 @@ __global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __rest
   }
 }
 
-__global__ void go1_actuator_kernel(const go1_config* __restrict__ c, const float* __restrict__ x,
-                                    float* __restrict__ out, int n) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float* r = x + (size_t)i * 6;
-  out[i] = actuator_eval(c->actuator, r[0], r[1], r[2], r[3], r[4], r[5]);
+__global__ __launch_bounds__(64) void go1_actuator_kernel(const go1_config* __restrict__ c,
+                                                         const float* __restrict__ x, float* __restrict__ out,
+                                                         int n) {
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  MlpFrag F;
+  mlp_load(c->actuator, lane, F);
+  const int n_groups = (n + 15) / 16;
+  for (int g = blockIdx.x; g < n_groups; g += gridDim.x) {  // uniform per wave: all lanes stay active
+    const int row = g * 16 + (lane & 15);
+    const float* r = x + (size_t)min(row, n - 1) * 6;
+    const float b0 = r[q];
+    const float b1v = q < 2 ? r[4 + q] : 0.0f;
+    const float t = mlp_group(F, b0, b1v);
+    if (q == 0 && row < n) out[row] = t;
+  }
 }
 
 // =====================================================================
@@ -1314,6 +1418,8 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   if (cfg->decimation <= 0 || cfg->n_internal <= 0) return fail(GO1_E_ARG, "go1_create: decimation/n_internal");
   if (cfg->terrain_kind == 1 && (cfg->hf_nx < 2 || cfg->hf_ny < 2)) return fail(GO1_E_ARG, "go1_create: tile shape");
   if (cfg->rand_interval <= 0) return fail(GO1_E_ARG, "go1_create: rand_interval");
+  if (cfg->n_envs % EPB != 0)
+    return fail(GO1_E_ARG, "go1_create: n_envs must be a multiple of 16 (one wave = 16 envs x 4 legs)");
   if (!cfg->measure_front_half)
     return fail(GO1_E_ARG, "go1_create: only the 261-wide front-half height scan is on this path "
                            "(Cfg.terrain.measure_front_half, scripts/train.py:53)");
@@ -1401,8 +1507,9 @@ int go1_reset_envs(go1_handle* h, const uint8_t* mask, const float* uniforms, ui
 int go1_actuator_net(go1_handle* h, const float* x, float* out, int32_t n_rows, void* stream) {
   if (!h || !x || !out || n_rows < 0) return fail(GO1_E_ARG, "go1_actuator_net: bad argument");
   if (n_rows == 0) return GO1_OK;
-  hipLaunchKernelGGL(go1_actuator_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->d_cfg,
-                     x, out, n_rows);
+  const int groups = (n_rows + 15) / 16;
+  hipLaunchKernelGGL(go1_actuator_kernel, dim3(groups < 4096 ? groups : 4096), dim3(64), 0, (hipStream_t)stream,
+                     h->d_cfg, x, out, n_rows);
   HIP_TRY(hipGetLastError());
   return GO1_OK;
 }

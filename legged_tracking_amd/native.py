@@ -13,7 +13,7 @@ import torch
 from . import abi, layout as L
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libgo1_mi355x.so")
+LIB_PATH = os.environ.get("GO1_LIB_OVERRIDE") or os.path.join(HERE, "_build", "libgo1_mi355x.so")
 _lib = None
 
 

@@ -65,24 +65,44 @@ static float draw(const go1_step_args* a, const float* U, int n_envs, int e, int
 
 /* ------------------------------------------------------------ actuator net */
 /* eval_actuator_network (:1311-1320): Linear(6,32) softsign Linear(32,32) softsign
- * Linear(32,1), each output an fmaf chain over k in increasing order seeded with
- * the bias (= what an f32-input MFMA computes bit for bit). */
+ * Linear(32,1).  The accumulation ORDER is the one the HIP kernel's f32 MFMA
+ * tiles produce (v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain), so the two
+ * are bit-identical; torch's own order is unspecified (tests use a tolerance):
+ *   layer 1, unit u : acc = b1[u]; k = 0..7 ascending (inputs padded 6 -> 8 with zeros)
+ *   layer 2, unit v : acc = b2[v]; k = 16 m + 4 q + r for m in 0..1, r in 0..3, q in 0..3
+ *   layer 3         : p_q = fma chain over u = 16 m + 4 q + r (m, r ascending) from 0;
+ *                     out = ((p0 + p1) + (p2 + p3)) + b3
+ */
 float go1o_actuator_eval(const float* W, const float x[6]) {
   const float *w1 = W, *b1 = W + 192, *w2 = W + 224, *b2 = W + 1248, *w3 = W + 1280, *b3 = W + 1312;
+  float xp[8] = {x[0], x[1], x[2], x[3], x[4], x[5], 0.0f, 0.0f};
   float h1[32], h2[32];
-  for (int k = 0; k < 32; ++k) {
-    float acc = b1[k];
-    for (int i = 0; i < 6; ++i) acc = fmaf(w1[k * 6 + i], x[i], acc);
-    h1[k] = acc / (fabsf(acc) + 1.0f);
+  for (int u = 0; u < 32; ++u) {
+    float acc = b1[u];
+    for (int k = 0; k < 8; ++k) acc = fmaf(k < 6 ? w1[u * 6 + k] : 0.0f, xp[k], acc);
+    h1[u] = acc / (fabsf(acc) + 1.0f);
   }
-  for (int k = 0; k < 32; ++k) {
-    float acc = b2[k];
-    for (int i = 0; i < 32; ++i) acc = fmaf(w2[k * 32 + i], h1[i], acc);
-    h2[k] = acc / (fabsf(acc) + 1.0f);
+  for (int v = 0; v < 32; ++v) {
+    float acc = b2[v];
+    for (int m = 0; m < 2; ++m)
+      for (int r = 0; r < 4; ++r)
+        for (int q = 0; q < 4; ++q) {
+          int k = 16 * m + 4 * q + r;
+          acc = fmaf(w2[v * 32 + k], h1[k], acc);
+        }
+    h2[v] = acc / (fabsf(acc) + 1.0f);
   }
-  float acc = b3[0];
-  for (int i = 0; i < 32; ++i) acc = fmaf(w3[i], h2[i], acc);
-  return acc;
+  float p[4];
+  for (int q = 0; q < 4; ++q) {
+    float a = 0.0f;
+    for (int m = 0; m < 2; ++m)
+      for (int r = 0; r < 4; ++r) {
+        int u = 16 * m + 4 * q + r;
+        a = fmaf(w3[u], h2[u], a);
+      }
+    p[q] = a;
+  }
+  return ((p[0] + p[1]) + (p[2] + p[3])) + b3[0];
 }
 
 void go1o_actuator_batch(const float* W, const float* x, float* out, int n) {
@@ -356,7 +376,7 @@ static void height_query(const TerrainView* T, int layer, double x, double y, do
     *gx = *gy = 0.0;
     return;
   }
-  double u = (x - T->ox) / T->hs, v = (y - T->oy) / T->hs;
+  double u = fmin(fmax((x - T->ox) / T->hs, -4.0), T->nx + 4.0), v = fmin(fmax((y - T->oy) / T->hs, -4.0), T->ny + 4.0);
   double fu = floor(u), fv = floor(v);
   int i = (int)fu, j = (int)fv;
   double a = u - fu, b = v - fv;
@@ -841,8 +861,10 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
         if (c->camera_zero) { px = px + camx; py = py + camy; }
         px = px - eto[0];
         py = py - eto[1];
-        long ix = (long)(px / c->horizontal_scale);
-        long iy = (long)(py / c->horizontal_scale);
+        float fx = fminf(fmaxf(px / c->horizontal_scale, -1.0f), (float)c->hf_nx);
+        float fy = fminf(fmaxf(py / c->horizontal_scale, -1.0f), (float)c->hf_ny);
+        long ix = (long)fx;
+        long iy = (long)fy;
         if (ix < 0) ix = 0;
         if (ix > c->hf_nx - 2) ix = c->hf_nx - 2;
         if (iy < 0) iy = 0;
@@ -898,6 +920,12 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   int time_out = (float)ep > c->max_episode_length;
   int reset = time_out;
   if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = 1;
+  if (!a->inj_dof) { /* native-integrator divergence guard (see the HIP kernel) */
+    int finite = 1;
+    for (int i = 0; i < 13; ++i) finite = finite && isfinite(root[i]);
+    for (int d = 0; d < NDOF; ++d) finite = finite && isfinite(dp[d]) && isfinite(dv[d]);
+    if (!finite) reset = 1;
+  }
 
   /* compute_reward (:320-355) with RewardsCrawling terms */
   float terms[GO1_NUM_TERMS];

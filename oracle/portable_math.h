@@ -43,7 +43,8 @@ static inline void pm_sincosf(float x, float* s, float* c) {
   float r = fmaf(-j, PM_PIO2_HI, x);
   r = fmaf(-j, PM_PIO2_MID, r);
   r = fmaf(-j, PM_PIO2_LO, r);
-  int q = ((int)j) & 3;
+  /* bounded before the conversion: a NaN / huge argument must not be undefined behaviour */
+  int q = ((int)fminf(fmaxf(j, -1.0e6f), 1.0e6f)) & 3;
   float sp = pm_sin_poly(r), cp = pm_cos_poly(r);
   switch (q) {
     case 0: *s = sp; *c = cp; break;

@@ -178,3 +178,29 @@ def test_philox_streams_match_oracle():
     O.reset_envs(c, st, ter, mask.astype(np.uint8), rng_seed=123456789012345, rng_step=2 ** 40 + 7)
     np.testing.assert_array_equal(g.state["dof_pos"].cpu().numpy(), st["dof_pos"])
     np.testing.assert_array_equal(g.state["root"].cpu().numpy(), st["root"])
+
+
+def test_diverged_envs_reset_without_faulting():
+    """Non-finite or absurd states (a diverged integrator) must neither fault the GPU
+    nor poison other envs: the divergence guard resets them."""
+    n = 64
+    cfg, c, td, ter, st, rng = _sim_setup(n)
+    bad = np.array([3, 17, 40, 63])
+    st["root"][3, 0] = np.nan
+    st["root"][17, 2] = np.inf
+    st["root"][40, 0:2] = 1e30
+    st["dof_pos"][63, 4] = -np.inf
+    g = native.Go1Native(c, DEV)
+    g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    g.state.load(st.arrays)
+    grav, gvec = CF.gravity_state([0.0, 0.0, 0.0])
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    for t in range(2):
+        g.step(_dev(np.zeros((n, 12), np.float32)), gvec, grav, scales, rng_seed=1, rng_step=t)
+        torch.cuda.synchronize()
+        if t == 0:
+            assert g.reset.cpu().numpy()[bad].all()
+    gs = g.state.numpy()
+    assert np.isfinite(gs["root"]).all() and np.isfinite(gs["dof_pos"]).all()
+    good = np.setdiff1d(np.arange(n), bad)
+    assert np.isfinite(g.obs.cpu().numpy()[good]).all()
