@@ -220,6 +220,11 @@ struct SI {
   float a[6], b[9], c[6];
 };
 
+// Integrator-only fast math (hardware v_rcp_f32 / v_rsq_f32, ~1 ulp): the f32
+// integrator is compared with the f64 oracle within a tolerance, never bitwise.
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+
 #define S3(m, i, j) m[((i) == 0 ? ((j) == 0 ? 0 : (j) == 1 ? 1 : 2) : (i) == 1 ? ((j) == 0 ? 1 : (j) == 1 ? 3 : 4) : ((j) == 0 ? 2 : (j) == 1 ? 4 : 5))]
 
 __device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
@@ -405,8 +410,8 @@ __device__ __forceinline__ void solve6(const SI& M, const float* b, float* x) {
       float s = si_get(M, i, j);
 #pragma unroll
       for (int k = 0; k < j; ++k) s -= LI(i, k) * LI(j, k);
-      if (i == j) LI(i, i) = sqrtf(fmaxf(s, 1e-30f));
-      else LI(i, j) = s / LI(j, j);
+      if (i == j) LI(i, i) = frsq(fmaxf(s, 1e-30f));  // holds 1 / L_ii
+      else LI(i, j) = s * LI(j, j);
     }
   float y[6];
 #pragma unroll
@@ -414,14 +419,14 @@ __device__ __forceinline__ void solve6(const SI& M, const float* b, float* x) {
     float s = b[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) s -= LI(i, k) * y[k];
-    y[i] = s / LI(i, i);
+    y[i] = s * LI(i, i);
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     float s = y[i];
 #pragma unroll
     for (int k = i + 1; k < 6; ++k) s -= LI(k, i) * x[k];
-    x[i] = s / LI(i, i);
+    x[i] = s * LI(i, i);
   }
 #undef LI
 }
@@ -437,7 +442,7 @@ __device__ __forceinline__ void quat_to_R(const float* q, float* R) {
 // the env's base at the start of the step, floor and ceiling interleaved, filled
 // once per step by the whole block; the integrator's contact queries hit it and
 // fall back to the HBM tile outside it (identical values: a pure cache).
-#define PSZ 22
+#define PSZ 16
 struct Terr {
   const float* tile;  // (2, nx, ny) or nullptr
   int nx, ny;
@@ -460,8 +465,9 @@ __device__ __forceinline__ void height_query2(const Terr& T, float x, float y, f
     return;
   }
   // bounded before the float -> int conversions (a diverged pose must not index memory)
-  const float u = fminf(fmaxf((x - T.ox) / T.hs, -4.0f), (float)(T.nx + 4));
-  const float v = fminf(fmaxf((y - T.oy) / T.hs, -4.0f), (float)(T.ny + 4));
+  const float ihs = frcp(T.hs);
+  const float u = fminf(fmaxf((x - T.ox) * ihs, -4.0f), (float)(T.nx + 4));
+  const float v = fminf(fmaxf((y - T.oy) * ihs, -4.0f), (float)(T.ny + 4));
   const float fu = floorf(u), fv = floorf(v);
   const int i = (int)fu, j = (int)fv;
   const float a = u - fu, b = v - fv;
@@ -476,7 +482,7 @@ __device__ __forceinline__ void height_query2(const Terr& T, float x, float y, f
     c01 = make_float2(tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1));
     c11 = make_float2(tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1));
   }
-  const float inv = 1.0f / T.hs;
+  const float inv = ihs;
   hf[0] = (1 - a) * (1 - b) * c00.x + a * (1 - b) * c10.x + (1 - a) * b * c01.x + a * b * c11.x;
   hf[1] = ((1 - b) * (c10.x - c00.x) + b * (c11.x - c01.x)) * inv;
   hf[2] = ((1 - a) * (c01.x - c00.x) + a * (c11.x - c10.x)) * inv;
@@ -506,16 +512,18 @@ __device__ __forceinline__ void sphere_contact(const Terr& T, const CP& C, const
       n[0] = gx; n[1] = gy; n[2] = -1.0f;
     }
     if (dv <= 0.0f) continue;
-    const float inv = 1.0f / sqrtf(n[0] * n[0] + n[1] * n[1] + 1.0f);
+    const float inv = frsq(n[0] * n[0] + n[1] * n[1] + 1.0f);
     n[0] *= inv; n[1] *= inv; n[2] *= inv;
     const float depth = dv * inv;
     const float vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
     const float fn = C.k * depth - C.d * vn;
     if (fn <= 0.0f) continue;
     const float vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
-    const float vtn = sqrtf(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
+    const float vt2 = vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2];
+    const float ivt = frsq(fmaxf(vt2, 1e-18f));
+    const float vtn = vt2 * ivt;
     const float ft = fminf(C.kf * vtn, C.mu * fn);
-    const float sc = vtn > 1e-9f ? ft / vtn : 0.0f;
+    const float sc = vtn > 1e-9f ? ft * ivt : 0.0f;
     F[0] += fn * n[0] - sc * vt[0];
     F[1] += fn * n[1] - sc * vt[1];
     F[2] += fn * n[2] - sc * vt[2];
@@ -673,7 +681,8 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
       for (int i = 0; i < 6; ++i) U[j][i] = si_get(IA, i, ax);
       D[j] = si_get(IA, ax, ax);
       u[j] = t - pA[j][ax];
-      const float invD = 1.0f / D[j];
+      const float invD = frcp(D[j]);
+      D[j] = invD;  // the forward pass only needs 1 / D
       const float Ua[3] = {U[j][0], U[j][1], U[j][2]}, Ul[3] = {U[j][3], U[j][4], U[j][5]};
       SI Ia;
       Ia.a[0] = IA.a[0] - Ua[0] * Ua[0] * invD; Ia.a[1] = IA.a[1] - Ua[0] * Ua[1] * invD;
@@ -707,7 +716,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
   }
   // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
   const float* bb = model;
-  const float mscale = (bb[0] + payload) / bb[0];
+  const float mscale = (bb[0] + payload) * frcp(bb[0]);
   SI I0;
   rigid_si(bb, mscale, I0);
   float p0[6];
@@ -751,7 +760,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
       float Ua = 0.0f;
 #pragma unroll
       for (int i = 0; i < 6; ++i) Ua += U[j][i] * aj[i];
-      qdd[j] = (u[j] - Ua) / D[j];
+      qdd[j] = (u[j] - Ua) * D[j];
       aj[ax] += qdd[j];
 #pragma unroll
       for (int i = 0; i < 6; ++i) ap[i] = aj[i];
@@ -770,11 +779,13 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
     S.pos[i] += h * S.v[i];
   }
   {
-    const float wn = sqrtf(S.w[0] * S.w[0] + S.w[1] * S.w[1] + S.w[2] * S.w[2]);
+    const float wn2 = S.w[0] * S.w[0] + S.w[1] * S.w[1] + S.w[2] * S.w[2];
+    const float iwn = frsq(fmaxf(wn2, 1e-30f));
+    const float wn = wn2 * iwn;
     const float thh = 0.5f * h * wn;
     float sth, cth;
     pm_sincosf(thh, &sth, &cth);
-    const float sc = thh > 1e-12f ? sth / wn : 0.5f * h;
+    const float sc = thh > 1e-12f ? sth * iwn : 0.5f * h;
     const float dq[4] = {S.w[0] * sc, S.w[1] * sc, S.w[2] * sc, cth};
     float* q = S.quat;
     float nq[4];
@@ -782,7 +793,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
     nq[0] = dq[3] * q[0] + dq[0] * q[3] + dq[1] * q[2] - dq[2] * q[1];
     nq[1] = dq[3] * q[1] - dq[0] * q[2] + dq[1] * q[3] + dq[2] * q[0];
     nq[2] = dq[3] * q[2] + dq[0] * q[1] - dq[1] * q[0] + dq[2] * q[3];
-    const float inv = 1.0f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+    const float inv = frsq(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = nq[i] * inv;
   }
@@ -909,13 +920,22 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       __syncthreads();
       const int nx = c->hf_nx, ny = c->hf_ny;
-      for (int idx = threadIdx.x; idx < EPB * PSZ * PSZ; idx += TPB) {
-        const int el = idx / (PSZ * PSZ), cell = idx - el * (PSZ * PSZ);
-        const int ci = cell / PSZ, cj = cell - ci * PSZ;
-        const int gi = min(max(s_patch_meta[el][1] + ci, 0), nx - 1);
-        const int gj = min(max(s_patch_meta[el][2] + cj, 0), ny - 1);
-        const float* tl = K.ter.tiles + (size_t)s_patch_meta[el][0] * 2 * nx * ny;
-        s_patch[el][cell] = make_float2(tl[((size_t)nx + gi) * ny + gj], tl[(size_t)gi * ny + gj]);
+      // 2 envs x 256 cells per pass: 8 cells (16 loads) in flight per lane
+#pragma unroll 1
+      for (int el0 = 0; el0 < EPB; el0 += 2) {
+        float2 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int el = el0 + (k >> 2);
+          const int cell = threadIdx.x + 64 * (k & 3);  // PSZ * PSZ = 256 = 4 x 64
+          const int ci = cell >> 4, cj = cell & 15;
+          const int gi = min(max(s_patch_meta[el][1] + ci, 0), nx - 1);
+          const int gj = min(max(s_patch_meta[el][2] + cj, 0), ny - 1);
+          const float* tl = K.ter.tiles + (size_t)s_patch_meta[el][0] * 2 * nx * ny;
+          v[k] = make_float2(tl[((size_t)nx + gi) * ny + gj], tl[(size_t)gi * ny + gj]);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s_patch[el0 + (k >> 2)][threadIdx.x + 64 * (k & 3)] = v[k];
       }
       __syncthreads();
     }
@@ -1232,22 +1252,32 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
     const float zroot = root[2];  // post-reset (:401)
     const float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
-    for (int p = leg; p < n_pts; p += 4) {
-      float hv[2];
-      sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[0], hv[1]);
+    // 28 points per lane (n_pts <= 112 for the front half): indices first, then all
+    // loads in flight together, then the observation arithmetic
+    float hv[28][2];
 #pragma unroll
-      for (int layer = 0; layer < 2; ++layer) {
-        float hh = hv[layer];
-        if (c->camera_zero) {
-          hh = hh - zroot;
-          hh = hh - cam_z;
-          hh = clampf(hh, -0.3f, 0.3f);
-        } else {
-          hh = clampf(hh, 0.0f, c->ceiling_height);
-          hh = hh / c->ceiling_height;
-          hh = hh - 0.5f;
+    for (int k = 0; k < 28; ++k) {
+      const int p = min(leg + 4 * k, n_pts - 1);
+      sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[k][0], hv[k][1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 28; ++k) {
+      const int p = leg + 4 * k;
+      if (p < n_pts) {
+#pragma unroll
+        for (int layer = 0; layer < 2; ++layer) {
+          float hh = hv[k][layer];
+          if (c->camera_zero) {
+            hh = hh - zroot;
+            hh = hh - cam_z;
+            hh = clampf(hh, -0.3f, 0.3f);
+          } else {
+            hh = clampf(hh, 0.0f, c->ceiling_height);
+            hh = hh / c->ceiling_height;
+            hh = hh - 0.5f;
+          }
+          o[41 + layer * n_pts + p] = clampf(hh * c->obs_scale_heights, -clip, clip);
         }
-        o[41 + layer * n_pts + p] = clampf(hh * c->obs_scale_heights, -clip, clip);
       }
     }
     if (A.dbg_heights) {

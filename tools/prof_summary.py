@@ -1,0 +1,87 @@
+"""Condense a tools/profile.sh output directory into the files committed under profiles/.
+
+  python tools/prof_summary.py gpurun_out/prof_r01 profiles/r01 [tag]
+
+Writes <tag>_kernel_stats.csv (the rocprofv3 --stats rows of this repo's kernels)
+and <tag>_counters.json (per-dispatch means of every PMC counter collected, for
+the fused step kernel, plus the HBM traffic per launch derived from them).
+
+Counter units / corrections (MI355X_MICROARCH.md, "HBM"): FETCH_SIZE and
+WRITE_SIZE are in KiB per dispatch.  FETCH_SIZE reads exactly half of the bytes
+of wide (16 B/lane) coalesced loads; the step kernel's loads are 4 B/lane SoA
+rows, an uncalibrated width, so the raw value is reported and the doubled value
+is given as the upper bound.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+OURS = ("go1_", "mlp", "gae", "ppo", "rollout")
+
+
+def kernel_stats(src):
+    rows = []
+    for f in glob.glob(os.path.join(src, "trace", "*kernel_stats.csv")):
+        with open(f) as fh:
+            r = csv.DictReader(fh)
+            for row in r:
+                if any(k in row["Name"] for k in OURS):
+                    rows.append(row)
+    return rows
+
+
+def counters(src, match="go1_step_kernel"):
+    acc = defaultdict(list)
+    for f in glob.glob(os.path.join(src, "*", "*counter_collection.csv")):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if match in row["Kernel_Name"]:
+                    acc[(row["Dispatch_Id"], row["Counter_Name"])].append(float(row["Counter_Value"]))
+    per = defaultdict(list)
+    meta = {}
+    for (disp, name), vals in acc.items():
+        per[name].append(sum(vals))  # sum over XCD / SE instances of one dispatch
+    for f in glob.glob(os.path.join(src, "*", "*counter_collection.csv")):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if match in row["Kernel_Name"]:
+                    meta = {k: row[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                                "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count")}
+                    break
+        if meta:
+            break
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}, meta
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    tag = sys.argv[3] if len(sys.argv) > 3 else "step"
+    os.makedirs(dst, exist_ok=True)
+    rows = kernel_stats(src)
+    if rows:
+        with open(os.path.join(dst, f"{tag}_kernel_stats.csv"), "w", newline="") as fh:
+            w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
+            w.writeheader()
+            w.writerows(rows)
+    means, counts, meta = counters(src)
+    out = {"kernel": "go1_step_kernel<false>", "dispatches": counts, "per_dispatch_mean": means, "resources": meta}
+    if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
+        fetch = means["FETCH_SIZE"] * 1024
+        write = means["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = {"fetch": fetch, "write": write, "traffic": fetch + write,
+                                       "traffic_upper_fetch_doubled": 2 * fetch + write}
+    if "SQ_WAVES" in means and means["SQ_WAVES"]:
+        w = means["SQ_WAVES"]
+        out["per_wave"] = {k: means[k] / w for k in means if k.startswith("SQ_") and k != "SQ_WAVES"}
+    with open(os.path.join(dst, f"{tag}_counters.json"), "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+    for r in rows:
+        print(r["Name"][:60], r["Calls"], r["AverageNs"])
+    print(json.dumps(out.get("hbm_bytes_per_launch"), indent=1))
+
+
+if __name__ == "__main__":
+    main()

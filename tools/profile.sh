@@ -1,0 +1,20 @@
+#!/bin/bash
+# rocprofv3 passes for the bench (run under gpurun).  Counters are collected in
+# their own passes (never combined with tracing), per the pool's rules.
+ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
+TAG=${1:-r01}
+OUT="$ROOT/gpurun_out/prof_$TAG"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+B="$ROOT/bench.py --steps 100 --warmup 10 --no-cpu-baseline"
+set -o pipefail
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- python3 $B > "$OUT/trace.log" 2>&1 || { echo "trace rc=$?"; exit 1; }
+echo trace ok
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o fetch -- python3 $B > "$OUT/fetch.log" 2>&1 || { echo "fetch rc=$?"; exit 1; }
+echo fetch ok
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o write -- python3 $B > "$OUT/write.log" 2>&1 || { echo "write rc=$?"; exit 1; }
+echo write ok
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sq" -o sq -- python3 $B > "$OUT/sq.log" 2>&1 || { echo "sq rc=$?"; tail -20 "$OUT/sq.log"; }
+echo sq done
+timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1; echo list rc=$?
+find "$OUT" -name "*.csv" | head -20
