@@ -45,6 +45,8 @@ extern "C" {
 #define GO1_ACTUATOR_FLOATS 1313 /* w1[32][6] b1[32] w2[32][32] b2[32] w3[32] b3[1] */
 #define GO1_GRID_X 21
 #define GO1_GRID_Y 11
+#define GO1_EPISODE_LOG 16 /* 13 episode sums, episode length, reached, goal distance */
+#define GO1_AUX 32         /* base lin vel 3, base ang vel 3, commands 2, foot pos 12, torques 12 */
 
 enum {
   GO1_OK = 0,
@@ -68,7 +70,8 @@ typedef struct go1_config {
   int32_t n_internal;          /* physics sub-steps per sim step (native integrator) */
   int32_t rand_interval;       /* ceil(rand_interval_s / dt) (:1873) */
   int32_t hf_nx, hf_ny;        /* tile pixels: 80 x 40 for single_path */
-  int32_t pad0, pad1;
+  int32_t env_id_offset;       /* global id of local env 0 (rank * n_envs): keys the Philox streams */
+  int32_t pad1;
   float sim_dt;                /* 0.005 (config.py:355) */
   float dt;                    /* decimation * sim_dt */
   float action_scale;          /* 0.25 */
@@ -175,6 +178,13 @@ typedef struct go1_step_args {
   float* dbg_terms;            /* (n_envs, 10) unscaled reward terms */
   float* dbg_commands;         /* (n_envs, 2) */
   uint8_t* dbg_reached;        /* (n_envs) */
+  /* optional host-facing outputs (NULL = not written) */
+  float* episode_log;          /* (n_envs, GO1_EPISODE_LOG): rows of envs reset this step hold the
+                                  reset_idx logging of extras["train/episode"] (:256-271); every
+                                  other row gets only column 13 (episode length) = 0 */
+  float* aux;                  /* (n_envs, GO1_AUX): base_lin_vel, base_ang_vel, commands (post-reset),
+                                  foot positions (world), torques of the last sim step: the
+                                  TrajectoryTrackingEnv.step extras (trajectory_tracking/__init__.py:25-41) */
   /* optional hipEvent_t pair recorded around the fused step kernel alone (NULL = none) */
   void* ev_begin;
   void* ev_end;

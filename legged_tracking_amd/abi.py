@@ -17,6 +17,8 @@ GO1_MODEL_FLOATS = 175
 GO1_ACTUATOR_FLOATS = 1313
 GO1_GRID_X = 21
 GO1_GRID_Y = 11
+GO1_EPISODE_LOG = 16
+GO1_AUX = 32
 
 F = C.c_float
 I32 = C.c_int32
@@ -27,7 +29,7 @@ class Go1Config(C.Structure):
     _fields_ = [
         ("n_envs", I32), ("terrain_kind", I32), ("camera_zero", I32), ("measure_front_half", I32),
         ("add_noise", I32), ("use_terminal_body_height", I32), ("custom_origins", I32), ("decimation", I32),
-        ("n_internal", I32), ("rand_interval", I32), ("hf_nx", I32), ("hf_ny", I32), ("pad0", I32), ("pad1", I32),
+        ("n_internal", I32), ("rand_interval", I32), ("hf_nx", I32), ("hf_ny", I32), ("env_id_offset", I32), ("pad1", I32),
         ("sim_dt", F), ("dt", F), ("action_scale", F), ("hip_scale_reduction", F), ("clip_actions", F),
         ("clip_obs", F), ("horizontal_scale", F), ("max_episode_length", F), ("terminal_body_height", F),
         ("switch_dist", F), ("base_height_target", F), ("tracking_sigma_lin", F), ("tracking_sigma_ang", F),
@@ -73,7 +75,7 @@ class Go1StepArgs(C.Structure):
         ("obs", P), ("priv", P), ("rew", P), ("reset", P), ("time_out", P), ("extras_time_outs", P),
         ("any_reset", P), ("contact_forces", P),
         ("dbg_torques", P), ("dbg_heights", P), ("dbg_terms", P), ("dbg_commands", P), ("dbg_reached", P),
-        ("ev_begin", P), ("ev_end", P),
+        ("episode_log", P), ("aux", P), ("ev_begin", P), ("ev_end", P),
     ]
 
 

@@ -58,10 +58,11 @@ __device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t 
 struct Rng {
   const float* U;  // parity-mode uniforms or nullptr
   uint64_t seed, step;
-  int e;
+  int e;    // local env index (parity-mode uniforms)
+  int gid;  // global env id (Philox counter): local index + go1_config.env_id_offset
   __device__ float operator()(int slot) const {
     if (U) return U[(size_t)e * GO1_U_PER_ENV + slot];
-    uint32_t c[4] = {(uint32_t)e, (uint32_t)slot >> 2, (uint32_t)step, (uint32_t)(step >> 32)};
+    uint32_t c[4] = {(uint32_t)gid, (uint32_t)slot >> 2, (uint32_t)step, (uint32_t)(step >> 32)};
     philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     return (float)(c[slot & 3] >> 8) * (1.0f / 16777216.0f);
   }
@@ -549,6 +550,28 @@ __device__ __forceinline__ void point_force(const float* Rb, const float* lp, co
 }
 
 // Physical state of one env as held by one lane of its quad.
+// World position of this leg's foot body origin (rigid_body_state[:, feet, 0:3] after
+// the last sim step), the kinematic chain of phys_substep without velocities.
+__device__ void foot_world(const float* __restrict__ model, const float* root, const float* q, int leg, float* out) {
+  float Rp[9], pp[3] = {root[0], root[1], root[2]};
+  quat_to_R(root + 3, Rp);
+  const float* origin = model + 13 * 10 + leg * 9;
+  const float* foot = model + 13 * 10 + 4 * 9;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int ax = j == 0 ? 0 : 1;
+    float rw[3], sn, cn;
+    mat3_vec(Rp, origin + j * 3, rw);
+    pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];
+    pm_sincosf(q[j], &sn, &cn);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
+  }
+  float fw[3];
+  mat3_vec(Rp, foot, fw);
+  out[0] = pp[0] + fw[0]; out[1] = pp[1] + fw[1]; out[2] = pp[2] + fw[2];
+}
+
 struct Phys {
   float pos[3], quat[4], v[3], w[3];  // base (replicated in the quad)
   float q[3], qd[3];                   // this leg's joints
@@ -880,7 +903,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   (void)n;
   MlpFrag F;
   mlp_load(c->actuator, lane, F);
-  const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e};
+  const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset};
   const size_t d0 = (size_t)e * NDOF + leg * 3;
   const float* lag_in = st.lag + (size_t)e * 84 + leg * 3;
 
@@ -1191,6 +1214,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float traj_new[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) traj_new[i] = st.trajectory[(size_t)e * 6 + i];
+  if (A.episode_log && leg == 0 && !reset) A.episode_log[(size_t)e * GO1_EPISODE_LOG + 13] = 0.0f;
+  if (reset && A.episode_log && leg == 0) {
+    // reset_idx logging (:256-271): pre-reset sums, episode length, reached, goal distance
+    float* lg = A.episode_log + (size_t)e * GO1_EPISODE_LOG;
+#pragma unroll
+    for (int k = 0; k < GO1_NUM_SUMS; ++k) lg[k] = sums[k];
+    lg[13] = (float)ep;
+    lg[14] = reached ? 1.0f : 0.0f;
+    lg[15] = norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+  }
   if (reset) {
     reset_env(c, K.ter, rng, e, leg, root, q, qd, strength, offset, traj_new);
     idx = 0;
@@ -1296,6 +1329,21 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     pv[1] = clampf((st.restitution[e] - c->priv_rest_shift) * c->priv_rest_scale, -clip, clip);
   }
 
+  if (A.aux) {
+    // TrajectoryTrackingEnv.step extras (trajectory_tracking/__init__.py:25-41), post-reset state
+    float* ax = A.aux + (size_t)e * GO1_AUX;
+    if (leg == 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { ax[i] = blv[i]; ax[3 + i] = bav[i]; }
+      ax[6] = cmd[0];
+      ax[7] = cmd[1];
+    }
+    float fp[3];
+    foot_world(c->model, root, q, leg, fp);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { ax[8 + leg * 3 + i] = fp[i]; ax[20 + leg * 3 + i] = torque[i]; }
+  }
+
   // ---------------- write back (epilogue :148-153)
   float lag_out[GO1_LAG_SLOTS][3];
 #pragma unroll
@@ -1358,7 +1406,7 @@ __global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __rest
   const int leg = threadIdx.x & 3;
   const int e = blockIdx.x * EPB + (threadIdx.x >> 2);
   if (e >= c->n_envs || !mask[e]) return;
-  const Rng rng = {U, seed, step, e};
+  const Rng rng = {U, seed, step, e, e + c->env_id_offset};
   float root[13], q[3], qd[3], strength[3], offset[3], traj[6];
   reset_env(c, ter, rng, e, leg, root, q, qd, strength, offset, traj);
   const size_t d0 = (size_t)e * NDOF + leg * 3;

@@ -1,0 +1,512 @@
+"""Drop-in host side of the trajectory-tracking env over the HIP step.
+
+Mirrors the reference's env API for the hot path:
+
+  LeggedRobot            <- go1_gym/envs/base/legged_robot_trajectory_tracking.py:24-362
+  TrajectoryTrackingEnv  <- go1_gym/envs/go1/trajectory_tracking/__init__.py:11-55
+  HistoryWrapper         <- go1_gym/envs/wrappers/history_wrapper.py:6-41
+
+Everything per-env runs in the fused HIP kernel (legged_tracking_amd/csrc/go1_step.hip)
+through the C ABI (include/go1_mi355x.h); this module keeps only what the
+reference keeps on the host or as global state:
+
+  * common_step_counter, the global gravity schedule (_randomize_gravity :645-660,
+    resampled every gravity_rand_interval steps and zeroed gravity_rand_duration
+    later, :826-830) and the init quirk that projected_gravity uses [0, 0, -1]
+    until the first resample (:1221 runs after create_sim's draw at :1574);
+  * the exploration-scale decay of update_curriculum (:171-182), in float64 like
+    the reference's Python floats;
+  * extras: "train/episode" / "timeouts" are filled from the kernel's episode
+    log lazily (one device->host copy when read, or every EPISODE_RING steps);
+    the TrajectoryTrackingEnv.step numpy extras (:25-41) are computed on read.
+
+Output tensors (obs, priv, rew, reset, time_out) rotate through OUT_RING buffers
+so that a tensor returned by step() stays valid for OUT_RING-1 further steps
+(the reference rebinds them every step; Runner / PPO hold the previous step's
+observations across one env.step).
+
+Differences from the reference, all documented in DESIGN.md:
+  * root_states is (num_envs, 13) (the reference's also interleaves the arrow
+    actors, num_actor = 2); the arrow actor is visual only;
+  * extras["time_outs"] exists from the first step (all False until the first
+    reset), which is numerically identical for PPO's bootstrapping (adds 0);
+  * eval envs (eval_cfg), curriculum (cl_fix_target), push_robots and
+    randomize_rigids_after_start are not on this path and raise.
+"""
+import math
+from collections import defaultdict, deque
+
+import numpy as np
+import torch
+
+from . import abi, config as CF, layout as L, terrain as T
+
+OUT_RING = 4
+EPISODE_RING = 64
+_LAZY = object()
+
+
+def _dist_info():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+    except Exception:
+        pass
+    return 0, 1
+
+
+class StepExtras(dict):
+    """The env's `extras` dict: device-backed entries are materialised on read."""
+
+    def __init__(self, env):
+        super().__init__()
+        self._env = env
+        self._lazy = {}
+
+    def set_lazy(self, key, fn):
+        self._lazy[key] = fn
+        dict.__setitem__(self, key, _LAZY)
+
+    def __getitem__(self, key):
+        if key in ("train/episode", "eval/episode", "timeouts"):
+            self._env._flush_episode_log()
+        v = dict.__getitem__(self, key)
+        return self._lazy[key]() if v is _LAZY else v
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def items(self):
+        return [(k, self[k]) for k in list(self.keys())]
+
+    def values(self):
+        return [self[k] for k in list(self.keys())]
+
+
+def _episode_dicts():
+    return defaultdict(lambda: deque([], 4000)), defaultdict(lambda: deque([], 4000)), deque([], 4000)
+
+
+class LeggedRobot:
+    """LeggedRobot (:24-362) for the README configuration, backed by the HIP step."""
+
+    def __init__(self, cfg, sim_params=None, physics_engine="SIM_PHYSX", sim_device="cuda:0", headless=True,
+                 eval_cfg=None, initial_dynamics_dict=None, *, seed=1, rank=None, world_size=None, backend=None,
+                 physics=None):
+        if eval_cfg is not None:
+            raise NotImplementedError("eval envs (eval_cfg) are not on the accelerated path")
+        if cfg.curriculum_thresholds.cl_fix_target:
+            raise NotImplementedError("cl_fix_target curriculum is not on the accelerated path")
+        dr = cfg.domain_rand
+        if getattr(dr, "push_robots", False) or getattr(dr, "randomize_rigids_after_start", False):
+            raise NotImplementedError("push_robots / randomize_rigids_after_start are not on the accelerated path")
+        self.cfg = cfg
+        self.eval_cfg = None
+        self.sim_device = sim_device
+        self.headless = headless
+        if rank is None or world_size is None:
+            r, w = _dist_info()
+            rank = r if rank is None else rank
+            world_size = w if world_size is None else world_size
+        self.rank, self.world_size = rank, world_size
+        self.num_obs = cfg.env.num_observations
+        self.num_privileged_obs = cfg.env.num_privileged_obs
+        self.num_actions = cfg.env.num_actions
+        self.num_envs = self.num_train_envs = cfg.env.num_envs
+        self.num_eval_envs = 0
+        self.seed = int(seed)
+        d = CF.derived(cfg)
+        self.dt = d["dt"]
+        self.max_episode_length_s = cfg.env.episode_length_s
+        self.max_episode_length = d["max_episode_length"]
+        self.reward_scales = dict(d["reward_scales"])
+        unknown = set(self.reward_scales) - set(L.REWARD_KEYS)
+        if unknown:
+            raise NotImplementedError(f"reward terms not on the accelerated path: {sorted(unknown)}")
+        self.reward_names = list(self.reward_scales)
+        self._gravity_interval = d["gravity_rand_interval"]
+        self._gravity_duration = d["gravity_rand_duration"]
+        n, n_global = self.num_envs, self.num_envs * world_size
+        self._abi_cfg = CF.build_abi_config(cfg, n_envs=n, physics=physics)
+        self._abi_cfg.env_id_offset = rank * n
+        # terrain: the global grid is built identically on every rank (same seed), each
+        # rank binds the slice of global env ids it owns (_get_env_origins :1808-1847)
+        td = T.build(cfg, n_global, np.random.RandomState(self.seed))
+        sl = slice(rank * n, (rank + 1) * n)
+        self.terrain = td
+        if backend is None:  # the HIP library (no CPU fallback); tests inject a factory
+            from . import native
+            backend = lambda c: native.Go1Native(c, sim_device)  # noqa: E731
+        self._sim = backend(self._abi_cfg)
+        self.device = self._sim.device
+        self._sim.set_terrain(td.tiles, td.env_tile[sl], td.env_terrain_origin[sl], td.env_origins[sl])
+        self.env_origins = torch.as_tensor(td.env_origins[sl], device=self.device)
+        dev = self.device
+        # output rings
+        self._obs = torch.zeros((OUT_RING, n, self.num_obs), device=dev)
+        self._priv = torch.zeros((OUT_RING, n, self.num_privileged_obs), device=dev)
+        self._rew = torch.zeros((OUT_RING, n), device=dev)
+        self._reset = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
+        self._time_out = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
+        self._slot = 0
+        self._elog = torch.zeros((EPISODE_RING, n, abi.GO1_EPISODE_LOG), device=dev)
+        self._elog_pending = []
+        self._elog_k = 0
+        self._aux = torch.zeros((n, abi.GO1_AUX), device=dev)
+        self._reset_mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+        # host RNG for the global gravity draws: identical on every rank
+        self._host_rng = np.random.default_rng(self.seed)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(self.seed * 1000003 + rank)
+        self._gen = gen
+        # _init_custom_buffers__ / _randomize_rigid_body_props (:1329-1350, :710-733)
+        st = self._sim.state
+        if dr.randomize_friction:
+            lo, hi = dr.friction_range
+            st["friction"].copy_(torch.rand((n, 1), generator=gen, device=dev) * (hi - lo) + lo)
+        else:
+            st["friction"].fill_(1.0)
+        if dr.randomize_restitution:
+            lo, hi = dr.restitution_range
+            st["restitution"].copy_(torch.rand((n, 1), generator=gen, device=dev) * (hi - lo) + lo)
+        if dr.randomize_base_mass:
+            lo, hi = dr.added_mass_range
+            st["payload"].copy_(torch.rand((n, 1), generator=gen, device=dev) * (hi - lo) + lo)
+        st["motor_strength"].fill_(1.0)
+        # gravity (:1574 then :1221): sim gravity drawn, projection vector reset to -z
+        self.common_step_counter = 0
+        self.gravities = np.zeros(3, np.float32)
+        self._randomize_gravity()
+        self._gravity_vec = np.array([0.0, 0.0, -1.0], np.float32)
+        self.extras = StepExtras(self)
+        self._train_ep, self._eval_ep, self._timeouts = _episode_dicts()
+        self._install_extras()
+        self._rng_step = 0
+
+    # ------------------------------------------------------------------ host state
+    def _randomize_gravity(self, external_force=None):
+        """_randomize_gravity (:645-660): one global draw shared by every env (and rank)."""
+        if external_force is not None:
+            self.gravities[:] = np.asarray(external_force, np.float32)
+        elif self.cfg.domain_rand.randomize_gravity:
+            lo, hi = self.cfg.domain_rand.gravity_range
+            u = self._host_rng.random(3).astype(np.float32)
+            self.gravities[:] = u * np.float32(hi - lo) + np.float32(lo)
+        self._sim_gravity, self._gravity_vec = CF.gravity_state(self.gravities)
+
+    @property
+    def gravity_vec(self):
+        return torch.as_tensor(self._gravity_vec, device=self.device).repeat(self.num_envs, 1)
+
+    def _scale_vector(self):
+        return CF.reward_scale_vector(self.reward_scales)
+
+    def _install_extras(self):
+        ex = self.extras
+        dict.__setitem__(ex, "train/episode", self._train_ep)
+        dict.__setitem__(ex, "eval/episode", self._eval_ep)
+        dict.__setitem__(ex, "timeouts", self._timeouts)
+        dict.__setitem__(ex, "time_outs", torch.zeros(self.num_train_envs, dtype=torch.bool, device=self.device))
+
+    # ------------------------------------------------------------------ views
+    @property
+    def state(self):
+        return self._sim.state
+
+    @property
+    def obs_buf(self):
+        return self._obs[(self._slot - 1) % OUT_RING]
+
+    @property
+    def privileged_obs_buf(self):
+        return self._priv[(self._slot - 1) % OUT_RING]
+
+    @property
+    def rew_buf(self):
+        return self._rew[(self._slot - 1) % OUT_RING]
+
+    @property
+    def reset_buf(self):
+        return self._reset[(self._slot - 1) % OUT_RING]
+
+    @property
+    def time_out_buf(self):
+        return self._time_out[(self._slot - 1) % OUT_RING]
+
+    @property
+    def episode_length_buf(self):
+        return self._sim.state["episode_length"][:, 0]
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, v):
+        self._sim.state["episode_length"][:, 0].copy_(torch.as_tensor(v, device=self.device))
+
+    @property
+    def root_states(self):
+        return self._sim.state["root"]
+
+    @property
+    def base_pos(self):
+        return self._sim.state["root"][:, 0:3]
+
+    @property
+    def base_quat(self):
+        return self._sim.state["root"][:, 3:7]
+
+    @property
+    def dof_pos(self):
+        return self._sim.state["dof_pos"]
+
+    @property
+    def dof_vel(self):
+        return self._sim.state["dof_vel"]
+
+    @property
+    def last_actions(self):
+        return self._sim.state["last_actions"]
+
+    @property
+    def joint_pos_target(self):
+        return self._sim.state["joint_pos_target"]
+
+    @property
+    def contact_forces(self):
+        return self._sim.contact_forces
+
+    @property
+    def torques(self):
+        return self._aux[:, 20:32]
+
+    @property
+    def base_lin_vel(self):
+        return self._aux[:, 0:3]
+
+    @property
+    def base_ang_vel(self):
+        return self._aux[:, 3:6]
+
+    @property
+    def commands(self):
+        return self._aux[:, 6:8]
+
+    @property
+    def foot_positions(self):
+        return self._aux[:, 8:20].view(-1, 4, 3)
+
+    @property
+    def episode_sums(self):
+        s = self._sim.state["episode_sums"]
+        return {k: s[:, i] for i, k in enumerate(L.SUM_KEYS)}
+
+    def get_observations(self):
+        return self.obs_buf
+
+    def get_privileged_observations(self):
+        return self.privileged_obs_buf
+
+    # ------------------------------------------------------------------ step
+    def step(self, actions):
+        """LeggedRobot.step (:64-112): returns obs, privileged_obs, rew, reset, extras."""
+        a = torch.as_tensor(actions)
+        if a.device != self.device or a.dtype != torch.float32:
+            a = a.to(self.device, torch.float32)
+        a = a.detach().contiguous()
+        if a.shape != (self.num_envs, self.num_actions):
+            raise ValueError(f"actions must be ({self.num_envs}, {self.num_actions}), got {tuple(a.shape)}")
+        s = self._slot
+        out = dict(obs=self._obs[s], priv=self._priv[s], rew=self._rew[s], reset=self._reset[s],
+                   time_out=self._time_out[s])
+        k = self._elog_k
+        if len(self._elog_pending) == EPISODE_RING:
+            self._flush_episode_log()
+        self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
+                       rng_step=self._rng_step, out=out, episode_log=self._elog[k], aux=self._aux)
+        self._rng_step += 1
+        self._elog_pending.append(k)
+        self._elog_k = (k + 1) % EPISODE_RING
+        self._slot = (s + 1) % OUT_RING
+        dict.__setitem__(self.extras, "time_outs", self._sim.extras_time_outs)
+        # post-physics host bookkeeping (:126, :826-830, :171-182)
+        self.common_step_counter += 1
+        c = self.common_step_counter
+        if c % int(self._gravity_interval) == 0:
+            self._randomize_gravity()
+        if int(c - self._gravity_duration) % int(self._gravity_interval) == 0:
+            self._randomize_gravity(np.zeros(3, np.float32))
+        self.update_curriculum()
+        return out["obs"], out["priv"], out["rew"], out["reset"], self.extras
+
+    def update_curriculum(self):
+        """update_curriculum (:171-182): exploration scales decay after exploration_steps."""
+        rw = self.cfg.rewards
+        for key in ("exploration_lin", "exploration_yaw"):
+            if key in self.reward_scales:
+                if self.common_step_counter > rw.exploration_steps:
+                    self.reward_scales[key] -= getattr(self.cfg.reward_scales, key) * self.dt / rw.exploration_steps
+                    self.reward_scales[key] = max(self.reward_scales[key], 0)
+                self._train_ep[key] = self.reward_scales[key]
+
+    def reset_idx(self, env_ids):
+        """reset_idx (:218-296) for explicit ids (the step resets its own envs in the kernel)."""
+        env_ids = torch.as_tensor(env_ids, device=self.device).long().flatten()
+        if env_ids.numel() == 0:
+            return
+        self._flush_episode_log()
+        st = self._sim.state
+        sums = st["episode_sums"][env_ids].cpu().numpy()
+        ep = st["episode_length"][env_ids, 0].float().cpu().numpy()
+        for i, key in enumerate(L.SUM_KEYS):
+            self._train_ep["rew_" + key].extend(sums[:, i])
+        self._train_ep["episode_length"].extend(ep)
+        mask = self._reset_mask
+        mask.zero_()
+        mask[env_ids] = 1
+        self._sim.reset_envs(mask, rng_seed=self.seed, rng_step=(1 << 62) + self._rng_step)
+        self._rng_step += 1
+        tb = self.time_out_buf[: self.num_train_envs]
+        self._timeouts.extend(tb.cpu().numpy())
+        self._sim.extras_time_outs.copy_(tb)  # extras["time_outs"] rebinding (:289-291)
+
+    def reset(self):
+        """BaseTask.reset (base_task.py:93-99)."""
+        self.reset_idx(torch.arange(self.num_envs, device=self.device))
+        obs, privileged_obs, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
+        return obs, privileged_obs
+
+    # ------------------------------------------------------------------ episode log
+    def _flush_episode_log(self):
+        """Move pending reset_idx logging (kernel episode_log rows) into the deques, in step order."""
+        if not self._elog_pending:
+            return
+        ks = torch.as_tensor(self._elog_pending, device=self.device)
+        self._elog_pending = []
+        logs = self._elog.index_select(0, ks)                      # (k, n, 16)
+        m = logs[:, : self.num_train_envs, 13] > 0                  # reset rows of train envs
+        idx = m.nonzero()
+        rows = logs[idx[:, 0], idx[:, 1]].cpu().numpy()
+        step_of_row = idx[:, 0].cpu().numpy()
+        any_k = m.any(1).cpu().numpy()
+        tmax = np.float32(self.max_episode_length)
+        ep_all = logs[:, : self.num_train_envs, 13].cpu().numpy() if any_k.any() else None
+        for j in range(len(any_k)):
+            if not any_k[j]:
+                continue
+            r = rows[step_of_row == j]
+            for i, key in enumerate(L.SUM_KEYS):
+                self._train_ep["rew_" + key].extend(r[:, i])
+            self._train_ep["episode_length"].extend(r[:, 13])
+            self._train_ep["reached"].extend(r[:, 14] > 0)
+            self._train_ep["goal_distance"].extend(r[:, 15])
+            self._timeouts.extend(ep_all[j] > tmax)
+
+    # ------------------------------------------------------------------ misc API
+    def start_recording(self):
+        pass
+
+    def pause_recording(self):
+        pass
+
+    def start_recording_eval(self):
+        pass
+
+    def pause_recording_eval(self):
+        pass
+
+    def get_complete_frames(self):
+        return []
+
+    def get_complete_frames_eval(self):
+        return []
+
+    def render(self, mode="rgb_array"):
+        return None
+
+    def close(self):
+        self._sim.close()
+
+
+class TrajectoryTrackingEnv(LeggedRobot):
+    """TrajectoryTrackingEnv (trajectory_tracking/__init__.py:11-55)."""
+
+    def __init__(self, sim_device="cuda:0", headless=True, num_envs=None, prone=False, deploy=False, cfg=None,
+                 eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", **kw):
+        if cfg is None:
+            cfg = CF.readme_config(n_envs=num_envs or 4096)
+        if num_envs is not None:
+            cfg.env.num_envs = num_envs
+        super().__init__(cfg, None, physics_engine, sim_device, headless, eval_cfg, initial_dynamics_dict, **kw)
+        n = self.num_envs
+        ex = self.extras
+        ex.set_lazy("joint_pos", lambda: self.dof_pos.cpu().numpy())
+        ex.set_lazy("joint_vel", lambda: self.dof_vel.cpu().numpy())
+        ex.set_lazy("joint_pos_target", lambda: self.joint_pos_target.cpu().numpy())
+        dict.__setitem__(ex, "joint_vel_target", torch.zeros(12))
+        ex.set_lazy("body_linear_vel", lambda: self.base_lin_vel.cpu().numpy())
+        ex.set_lazy("body_angular_vel", lambda: self.base_ang_vel.cpu().numpy())
+        ex.set_lazy("body_linear_vel_cmd", lambda: self.commands.cpu().numpy())
+        ex.set_lazy("body_angular_vel_cmd", lambda: np.zeros((n, 0), np.float32))
+        ex.set_lazy("contact_states",
+                    lambda: (self.contact_forces[:, list(L.FEET_INDICES), 2] > 1.0).cpu().numpy().copy())
+        ex.set_lazy("foot_positions", lambda: self.foot_positions.cpu().numpy().copy())
+        ex.set_lazy("body_pos", lambda: self.base_pos.cpu().numpy())
+        ex.set_lazy("torques", lambda: self.torques.cpu().numpy())
+
+    def step(self, actions):
+        obs, priv, rew, reset, extras = super().step(actions)
+        dict.__setitem__(extras, "privileged_obs", priv)
+        return obs, rew, reset, extras
+
+    def reset(self):
+        self.reset_idx(torch.arange(self.num_envs, device=self.device))
+        self.episode_length_buf = torch.randint(int(self.max_episode_length), (self.num_envs,), device=self.device,
+                                                generator=self._gen, dtype=torch.int32)
+        self._train_ep, self._eval_ep, self._timeouts = _episode_dicts()
+        self._elog_pending = []
+        self._install_extras()
+        obs, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
+        return obs
+
+
+class HistoryWrapper:
+    """HistoryWrapper (history_wrapper.py:6-41): dict observations with an obs history."""
+
+    def __init__(self, env):
+        self.env = env
+        self.obs_history_length = self.env.cfg.env.num_observation_history
+        self.num_obs_history = self.obs_history_length * self.env.num_obs
+        self.obs_history = torch.zeros(self.env.num_envs, self.num_obs_history, dtype=torch.float,
+                                       device=self.env.device)
+        self.num_privileged_obs = self.env.num_privileged_obs
+
+    def __getattr__(self, name):
+        return getattr(self.env, name)
+
+    def _push(self, obs):
+        if self.obs_history_length == 1:
+            self.obs_history = obs.clone()
+        else:
+            self.obs_history = torch.cat((self.obs_history[:, self.env.num_obs:], obs), dim=-1)
+
+    def step(self, action):
+        obs, rew, done, info = self.env.step(action)
+        privileged_obs = info["privileged_obs"]
+        self._push(obs)
+        return {"obs": obs, "privileged_obs": privileged_obs, "obs_history": self.obs_history}, rew, done, info
+
+    def get_observations(self):
+        obs = self.env.get_observations()
+        privileged_obs = self.env.get_privileged_observations()
+        self._push(obs)
+        return {"obs": obs, "privileged_obs": privileged_obs, "obs_history": self.obs_history}
+
+    def reset_idx(self, env_ids):
+        ret = self.env.reset_idx(env_ids)
+        self.obs_history[env_ids, :] = 0
+        return ret
+
+    def reset(self):
+        ret = self.env.reset()
+        privileged_obs = self.env.get_privileged_observations()
+        self.obs_history[:, :] = 0
+        return {"obs": ret, "privileged_obs": privileged_obs, "obs_history": self.obs_history}

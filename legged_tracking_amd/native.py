@@ -113,9 +113,10 @@ class Go1Native:
         _check(lib().go1_set_terrain(self.h, C.byref(s)))
 
     def step(self, actions, gravity_vec, sim_gravity, reward_scales, rng_seed=0, rng_step=0, uniforms=None,
-             inj=None, debug=None, events=None):
+             inj=None, debug=None, events=None, episode_log=None, aux=None, out=None):
         """One fused LeggedRobot.step on the current stream.  `debug` is an optional dict
-        of preallocated tensors (torques, heights, terms, commands, reached)."""
+        of preallocated tensors (torques, heights, terms, commands, reached); `out` may
+        replace the default output buffers (obs, priv, rew, reset, time_out)."""
         a = abi.Go1StepArgs()
         assert actions.is_contiguous() and actions.dtype == torch.float32 and actions.shape == (self.n, 12)
         a.actions = actions.data_ptr()
@@ -130,8 +131,14 @@ class Go1Native:
             a.uniforms = uniforms.data_ptr()
         if inj is not None:
             a.inj_dof, a.inj_root, a.inj_contact = (inj[k].data_ptr() for k in ("dof", "root", "contact"))
-        a.obs, a.priv, a.rew = self.obs.data_ptr(), self.priv.data_ptr(), self.rew.data_ptr()
-        a.reset, a.time_out = self.reset.data_ptr(), self.time_out.data_ptr()
+        o = dict(obs=self.obs, priv=self.priv, rew=self.rew, reset=self.reset, time_out=self.time_out)
+        if out:
+            for k, v in out.items():
+                assert k in o and v.shape == o[k].shape and v.dtype == o[k].dtype and v.is_contiguous(), k
+                assert v.device == self.device, k
+                o[k] = v
+        a.obs, a.priv, a.rew = o["obs"].data_ptr(), o["priv"].data_ptr(), o["rew"].data_ptr()
+        a.reset, a.time_out = o["reset"].data_ptr(), o["time_out"].data_ptr()
         a.extras_time_outs = self.extras_time_outs.data_ptr()
         a.contact_forces = self.contact_forces.data_ptr()
         if debug:
@@ -139,6 +146,12 @@ class Go1Native:
                            ("commands", "dbg_commands"), ("reached", "dbg_reached")):
                 if k in debug:
                     setattr(a, fld, debug[k].data_ptr())
+        if episode_log is not None:
+            assert episode_log.is_contiguous() and episode_log.shape == (self.n, abi.GO1_EPISODE_LOG)
+            a.episode_log = episode_log.data_ptr()
+        if aux is not None:
+            assert aux.is_contiguous() and aux.shape == (self.n, abi.GO1_AUX)
+            a.aux = aux.data_ptr()
         if events is not None:  # (hipEvent_t begin, hipEvent_t end) as ints
             a.ev_begin, a.ev_end = events
         _check(lib().go1_step(self.h, C.byref(a), _stream()))

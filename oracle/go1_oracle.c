@@ -57,10 +57,10 @@ float go1o_uniform(uint64_t seed, uint64_t step, uint32_t env, uint32_t slot) {
   return (float)(c[slot & 3] >> 8) * (1.0f / 16777216.0f);
 }
 
-static float draw(const go1_step_args* a, const float* U, int n_envs, int e, int slot) {
-  (void)n_envs;
+/* parity mode: caller uniforms of local env e; otherwise Philox keyed by the GLOBAL env id */
+static float draw(const go1_step_args* a, const float* U, int env_id_offset, int e, int slot) {
   if (U) return U[(size_t)e * GO1_U_PER_ENV + slot];
-  return go1o_uniform(a->rng_seed, a->rng_step, (uint32_t)e, (uint32_t)slot);
+  return go1o_uniform(a->rng_seed, a->rng_step, (uint32_t)(e + env_id_offset), (uint32_t)slot);
 }
 
 /* ------------------------------------------------------------ actuator net */
@@ -703,18 +703,17 @@ static void compute_torques(const go1_config* c, const go1_state* st, int e, con
 /* _reset_idx for one env (:218-296): DR, dofs, root, trajectory, buffers */
 static void reset_env(const go1_config* c, const go1_state* st, const go1_terrain* ter, int e, const go1_step_args* a,
                       const float* U) {
-  int n = c->n_envs;
   /* _randomize_dof_props (:744-754) */
-  float us = draw(a, U, n, e, 0);
+  float us = draw(a, U, c->env_id_offset, e, 0);
   float s = us * c->strength_range + c->strength_lo;
   for (int d = 0; d < NDOF; ++d) {
     st->motor_strength[(size_t)e * NDOF + d] = s;
-    float uo = draw(a, U, n, e, 1 + d);
+    float uo = draw(a, U, c->env_id_offset, e, 1 + d);
     st->motor_offset[(size_t)e * NDOF + d] = uo * c->offset_range + c->offset_lo;
   }
   /* _reset_dofs (:998-1008) */
   for (int d = 0; d < NDOF; ++d) {
-    float u = draw(a, U, n, e, 13 + d);
+    float u = draw(a, U, c->env_id_offset, e, 13 + d);
     float f = c->reset_dof_range * u + c->reset_dof_lo;
     st->dof_pos[(size_t)e * NDOF + d] = c->default_dof_pos[d] * f;
     st->dof_vel[(size_t)e * NDOF + d] = 0.0f;
@@ -727,13 +726,13 @@ static void reset_env(const go1_config* c, const go1_state* st, const go1_terrai
   r[1] = r[1] + eo[1];
   r[2] = r[2] + eo[2];
   if (c->custom_origins) {
-    float ux = draw(a, U, n, e, 25), uy = draw(a, U, n, e, 26);
+    float ux = draw(a, U, c->env_id_offset, e, 25), uy = draw(a, U, c->env_id_offset, e, 26);
     r[0] = r[0] + (c->x_init_range2 * ux + c->x_init_lo);
     r[1] = r[1] + (c->y_init_range2 * uy + c->y_init_lo);
     r[0] = r[0] + c->x_init_offset;
     r[1] = r[1] + c->y_init_offset;
   }
-  float yaw = c->yaw_range2 * draw(a, U, n, e, 27) + c->yaw_lo;
+  float yaw = c->yaw_range2 * draw(a, U, c->env_id_offset, e, 27) + c->yaw_lo;
   /* quat_from_angle_axis(yaw, z) then quat_unit */
   float th = yaw / 2.0f;
   float sth, cth;
@@ -742,7 +741,7 @@ static void reset_env(const go1_config* c, const go1_state* st, const go1_terrai
   float qn = sqrtf(fmaf(qv[3], qv[3], fmaf(qv[2], qv[2], fmaf(qv[1], qv[1], qv[0] * qv[0]))));
   if (qn < 1e-9f) qn = 1e-9f;
   for (int i = 0; i < 4; ++i) r[3 + i] = qv[i] / qn;
-  for (int i = 0; i < 6; ++i) r[7 + i] = c->reset_vel_range * draw(a, U, n, e, 28 + i) + c->reset_vel_lo;
+  for (int i = 0; i < 6; ++i) r[7 + i] = c->reset_vel_range * draw(a, U, c->env_id_offset, e, 28 + i) + c->reset_vel_lo;
   /* _resample_trajectory + _traj_fn_fixed_target (trajectory_function.py:14-26) */
   st->curr_pose_index[e] = 0;
   float* tr = st->trajectory + (size_t)e * 6;
@@ -772,6 +771,25 @@ int go1o_reset_envs(const go1_config* c, const go1_state* st, const go1_terrain*
   for (int e = 0; e < c->n_envs; ++e)
     if (mask[e]) reset_env(c, st, ter, e, &a, U);
   return 0;
+}
+
+/* World position of leg l's foot body origin (rigid_body_state[:, feet, 0:3]) */
+static void foot_world(const Model* M, const float* root, const float* dp, int l, float* out) {
+  double qd4[4] = {root[3], root[4], root[5], root[6]};
+  double R[3][3], Rp[3][3], pp[3] = {root[0], root[1], root[2]};
+  quat_to_R(qd4, R);
+  memcpy(Rp, R, sizeof(Rp));
+  for (int j = 0; j < 3; ++j) {
+    double E[3][3], Rw[3][3];
+    const double* r = M->origin[l][j];
+    for (int i = 0; i < 3; ++i) pp[i] += Rp[i][0] * r[0] + Rp[i][1] * r[1] + Rp[i][2] * r[2];
+    joint_E(j == 0 ? 0 : 1, dp[l * 3 + j], E);
+    for (int i = 0; i < 3; ++i)
+      for (int k = 0; k < 3; ++k) Rw[i][k] = Rp[i][0] * E[k][0] + Rp[i][1] * E[k][1] + Rp[i][2] * E[k][2];
+    memcpy(Rp, Rw, sizeof(Rp));
+  }
+  for (int i = 0; i < 3; ++i)
+    out[i] = (float)(pp[i] + Rp[i][0] * M->foot[0] + Rp[i][1] * M->foot[1] + Rp[i][2] * M->foot[2]);
 }
 
 /* Full step for env e.  Returns nothing; writes outputs. */
@@ -892,11 +910,11 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
 
   /* DR every rand_interval (:822-824) */
   if (ep % c->rand_interval == 0) {
-    float us = draw(a, U, n, e, 34);
+    float us = draw(a, U, c->env_id_offset, e, 34);
     float s = us * c->strength_range + c->strength_lo;
     for (int d = 0; d < NDOF; ++d) {
       st->motor_strength[(size_t)e * NDOF + d] = s;
-      st->motor_offset[(size_t)e * NDOF + d] = draw(a, U, n, e, 35 + d) * c->offset_range + c->offset_lo;
+      st->motor_offset[(size_t)e * NDOF + d] = draw(a, U, c->env_id_offset, e, 35 + d) * c->offset_range + c->offset_lo;
     }
   }
   /* switch / reached (:836-844), traj_length = 1 */
@@ -987,6 +1005,14 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   /* reset_idx (:218-296) for this env.  self.commands is a VIEW of
    * local_relative_linear[:, :2] (:802), which reset_idx zeroes in place (:252),
    * so a reset env observes a zero command this step. */
+  if (a->episode_log && !reset) a->episode_log[(size_t)e * GO1_EPISODE_LOG + 13] = 0.0f;
+  if (reset && a->episode_log) { /* reset_idx logging (:256-271) */
+    float* lg = a->episode_log + (size_t)e * GO1_EPISODE_LOG;
+    for (int k2 = 0; k2 < GO1_NUM_SUMS; ++k2) lg[k2] = sums[k2];
+    lg[13] = (float)ep;
+    lg[14] = reached ? 1.0f : 0.0f;
+    lg[15] = norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+  }
   if (reset) {
     reset_env(c, st, ter, e, a, U);
     cmd[0] = 0.0f;
@@ -1028,7 +1054,7 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
       if (i < 3) nv = c->noise_gravity;
       else if (i >= 5 && i < 17) nv = c->noise_dof_pos;
       else if (i >= 17 && i < 29) nv = c->noise_dof_vel;
-      float u = draw(a, U, n, e, 47 + i);
+      float u = draw(a, U, c->env_id_offset, e, 47 + i);
       o[i] = o[i] + (2.0f * u - 1.0f) * nv;
     }
   }
@@ -1040,6 +1066,15 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   pv[0] = (st->friction[e] - c->priv_friction_shift) * c->priv_friction_scale;
   pv[1] = (st->restitution[e] - c->priv_rest_shift) * c->priv_rest_scale;
   for (int i = 0; i < 2; ++i) pv[i] = pv[i] < -c->clip_obs ? -c->clip_obs : (pv[i] > c->clip_obs ? c->clip_obs : pv[i]);
+
+  if (a->aux) { /* TrajectoryTrackingEnv.step extras (trajectory_tracking/__init__.py:25-41) */
+    float* ax = a->aux + (size_t)e * GO1_AUX;
+    for (int i = 0; i < 3; ++i) { ax[i] = blv[i]; ax[3 + i] = bav[i]; }
+    ax[6] = cmd[0];
+    ax[7] = cmd[1];
+    for (int l = 0; l < 4; ++l) foot_world(M, root, dp, l, ax + 8 + 3 * l);
+    for (int d = 0; d < NDOF; ++d) ax[20 + d] = torque[d];
+  }
 
   /* epilogue (:148-153) */
   for (int d = 0; d < NDOF; ++d) {

@@ -88,7 +88,9 @@ def step(cfg, state, terrain, actions, gravity_vec, sim_gravity, reward_scales, 
     if debug:
         out.update(torques=np.zeros((cfg.decimation, n, 12), np.float32),
                    heights=np.zeros((n, 2, 21, 11), np.float32), terms=np.zeros((n, 10), np.float32),
-                   commands=np.zeros((n, 2), np.float32), reached=np.zeros(n, np.uint8))
+                   commands=np.zeros((n, 2), np.float32), reached=np.zeros(n, np.uint8),
+                   episode_log=np.full((n, abi.GO1_EPISODE_LOG), np.nan, np.float32),
+                   aux=np.zeros((n, abi.GO1_AUX), np.float32))
     actions = np.ascontiguousarray(actions, np.float32)
     keep = [actions]
     a = abi.Go1StepArgs()
@@ -114,6 +116,7 @@ def step(cfg, state, terrain, actions, gravity_vec, sim_gravity, reward_scales, 
         a.dbg_torques, a.dbg_heights, a.dbg_terms = abi.ptr(out["torques"]), abi.ptr(out["heights"]), abi.ptr(
             out["terms"])
         a.dbg_commands, a.dbg_reached = abi.ptr(out["commands"]), abi.ptr(out["reached"])
+        a.episode_log, a.aux = abi.ptr(out["episode_log"]), abi.ptr(out["aux"])
     st = state.struct()
     ts = terrain.struct()
     rc = lib().go1o_step(C.byref(cfg), C.byref(st), C.byref(ts), C.byref(a))

@@ -518,8 +518,16 @@ def run(terrain, n_envs, rows, n_steps, seed, out, extra_argv=(), actions_scale=
         scatter_draws.root_k = 0
         phys.log.clear()
         gym.torque_log.clear()
+        ep_before = {k: len(v) for k, v in env.extras["train/episode"].items() if hasattr(v, "__len__")}
+        to_before = len(env.extras["timeouts"])
         obs, rew, reset, extras = env.step(actions)
         u, ug = scatter_draws(env, list(_rand_log))
+        ep_new = {}
+        for k, v in extras["train/episode"].items():
+            if hasattr(v, "__len__"):
+                ep_new["episode/" + k] = np.asarray(list(v)[ep_before.get(k, 0):], np.float64)
+            else:
+                ep_new["episode_scalar/" + k] = np.float64(v)
         step = {
             "pre": pre, "post": env_state(env), "actions": actions.numpy(),
             "common_step_counter": np.int64(pre_counter), "reward_scales": pre_scales, "gravity": pre_grav,
@@ -540,6 +548,12 @@ def run(terrain, n_envs, rows, n_steps, seed, out, extra_argv=(), actions_scale=
             "arrow_root": env.root_states[1::2, 0:7].numpy().copy(),
             "reached": env.reached_buf.numpy().copy(),
             "commands": env.commands.numpy().copy(),
+            "x_body_linear_vel": np.asarray(extras["body_linear_vel"]).copy(),
+            "x_body_angular_vel": np.asarray(extras["body_angular_vel"]).copy(),
+            "x_body_linear_vel_cmd": np.asarray(extras["body_linear_vel_cmd"]).copy(),
+            "x_torques": np.asarray(extras["torques"]).copy(),
+            "x_timeouts_new": np.array([bool(x) for x in list(extras["timeouts"])[to_before:]], bool),
+            **ep_new,
         }
         rec["steps"].append(step)
     flat = {}

@@ -43,3 +43,26 @@ def step_inputs(d, t):
     scales = d[f"s{t}/reward_scales"].astype(np.float32)
     return dict(actions=d[f"s{t}/actions"], gravity_vec=d[f"s{t}/gravity_vec"], sim_gravity=d[f"s{t}/sim_gravity"],
                 reward_scales=scales, uniforms=d[f"s{t}/uniforms"], inj=inj)
+
+
+def check_episode_log_and_extras(d, t, episode_log, aux, rtol=2e-5, atol=2e-5):
+    """Rows of envs reset at step t vs the reference's extras["train/episode"] additions
+    (reset_idx :256-271, ascending env id), and the TrajectoryTrackingEnv.step extras
+    (trajectory_tracking/__init__.py:25-41) vs the aux block."""
+    from legged_tracking_amd import layout as L
+    rs = d[f"s{t}/reset"].astype(bool)
+    rows = episode_log[rs]
+    if f"s{t}/episode/episode_length" not in d.files:  # no reset has logged yet: the deques do not exist
+        assert not rs.any()
+    if rs.any():
+        for i, k in enumerate(L.SUM_KEYS):
+            np.testing.assert_allclose(rows[:, i], d[f"s{t}/episode/rew_{k}"], rtol=1e-4, atol=1e-6, err_msg=k)
+        np.testing.assert_array_equal(rows[:, 13], d[f"s{t}/episode/episode_length"])
+        np.testing.assert_array_equal(rows[:, 14], d[f"s{t}/episode/reached"])
+        np.testing.assert_allclose(rows[:, 15], d[f"s{t}/episode/goal_distance"], rtol=rtol, atol=atol)
+    elif f"s{t}/episode/episode_length" in d.files:
+        assert d[f"s{t}/episode/episode_length"].size == 0
+    np.testing.assert_allclose(aux[:, 0:3], d[f"s{t}/x_body_linear_vel"], rtol=rtol, atol=atol)
+    np.testing.assert_allclose(aux[:, 3:6], d[f"s{t}/x_body_angular_vel"], rtol=rtol, atol=atol)
+    np.testing.assert_allclose(aux[:, 6:8], d[f"s{t}/x_body_linear_vel_cmd"], rtol=rtol, atol=atol)
+    np.testing.assert_allclose(aux[:, 20:32], d[f"s{t}/x_torques"], rtol=rtol, atol=atol)

@@ -60,14 +60,17 @@ def test_fused_step_replays_reference_fixture(name):
     g = native.Go1Native(c, DEV)
     g.set_terrain(ter.tiles, ter.env_tile, ter.eto, ter.eo)
     dbg = native.debug_buffers(n, c.decimation, DEV)
+    elog = torch.full((n, 16), float("nan"), device=DEV)
+    aux = torch.zeros((n, 32), device=DEV)
     for t in range(int(d["meta/n_steps"])):
         st = G.state_at(d, t, "pre")
         g.state.load(st.arrays)
         inp = G.step_inputs(d, t)
         inj = {k: _dev(v, torch.float32) for k, v in inp["inj"].items()}
         u = _dev(np.nan_to_num(inp["uniforms"], nan=0.5), torch.float32)
+        elog.fill_(float("nan"))
         g.step(_dev(inp["actions"]), inp["gravity_vec"], inp["sim_gravity"], inp["reward_scales"], uniforms=u,
-               inj=inj, debug=dbg)
+               inj=inj, debug=dbg, episode_log=elog, aux=aux)
         torch.cuda.synchronize()
         # oracle on the same inputs
         ost = st.copy()
@@ -85,6 +88,17 @@ def test_fused_step_replays_reference_fixture(name):
         np.testing.assert_array_equal(obs, oo["obs"])
         np.testing.assert_array_equal(g.priv.cpu().numpy(), oo["priv"])
         np.testing.assert_allclose(g.rew.cpu().numpy(), oo["rew"], rtol=2e-6, atol=1e-9)
+        # reset_idx logging rows (NaN elsewhere) and the step extras
+        rs = d[f"s{t}/reset"].astype(bool)
+        el = elog.cpu().numpy()
+        assert (el[~rs][:, 13] == 0).all()
+        np.testing.assert_array_equal(el[rs][:, 13:15], oo["episode_log"][rs][:, 13:15])
+        np.testing.assert_allclose(el[rs], oo["episode_log"][rs], rtol=2e-6, atol=1e-8)
+        ax = aux.cpu().numpy()
+        np.testing.assert_array_equal(ax[:, :8], oo["aux"][:, :8])
+        np.testing.assert_array_equal(ax[:, 20:], oo["aux"][:, 20:])
+        np.testing.assert_allclose(ax[:, 8:20], oo["aux"][:, 8:20], rtol=0, atol=2e-5)
+        G.check_episode_log_and_extras(d, t, el, ax)
         gs = g.state.numpy()
         for k in ("episode_length", "curr_pose_index", "collision_count"):
             np.testing.assert_array_equal(gs[k].ravel(), d[f"s{t}/post/{k}"].ravel(), err_msg=k)
@@ -204,3 +218,50 @@ def test_diverged_envs_reset_without_faulting():
     assert np.isfinite(gs["root"]).all() and np.isfinite(gs["dof_pos"]).all()
     good = np.setdiff1d(np.arange(n), bad)
     assert np.isfinite(g.obs.cpu().numpy()[good]).all()
+
+
+def test_env_api_on_gpu_matches_oracle_backend():
+    """TrajectoryTrackingEnv + HistoryWrapper over the HIP library: first steps agree with
+    the same env driven by the CPU oracle (integrator tolerance), extras materialise."""
+    from legged_tracking_amd import env as E
+    from tests.cpu_backend import OracleBackend
+    n = 256
+
+    def mk(dev, backend):
+        cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=4, cols=4)
+        return E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device=dev, cfg=cfg, seed=3, rank=0, world_size=1,
+                                                        backend=backend))
+
+    g = mk(DEV, None)
+    c = mk("cpu", OracleBackend)
+    assert g.env._sim.__class__.__name__ == "Go1Native"
+    g.reset()
+    c.reset()
+    # identical DR draws on both sides (torch generators differ between devices)
+    for k in ("friction", "restitution", "payload", "episode_length"):
+        c.env.state[k].copy_(g.env.state[k].cpu())
+    for k in ("root", "dof_pos", "dof_vel", "motor_strength", "motor_offset", "trajectory", "lag"):
+        c.env.state[k].copy_(g.env.state[k].cpu())
+    rng = np.random.default_rng(0)
+    for t in range(3):
+        a = rng.normal(0, 1, (n, 12)).astype(np.float32)
+        og, rg, dg, ig = g.step(torch.from_numpy(a).to(DEV))
+        oc, rc, dc, ic = c.step(torch.from_numpy(a))
+        torch.cuda.synchronize()
+        err = np.abs(og["obs"].cpu().numpy()[:, :41] - oc["obs"].numpy()[:, :41])
+        assert np.percentile(err, 99) < 5e-2, np.percentile(err, 99)
+        assert (dg.cpu().numpy() == dc.numpy()).mean() > 0.98
+        for k in ("joint_pos", "body_linear_vel", "foot_positions", "torques", "contact_states"):
+            assert ig[k].shape == ic[k].shape, k
+        for key in ("state",):
+            pass
+        # continue both from the GPU state so each comparison is one step
+        for k in ("root", "dof_pos", "dof_vel", "last_actions", "last_dof_vel", "lag", "pos_err_hist", "vel_hist",
+                  "motor_strength", "motor_offset", "episode_length", "episode_sums", "collision_count",
+                  "trajectory", "base_rotation", "curr_pose_index"):
+            c.env.state[k].copy_(g.env.state[k].cpu())
+    for _ in range(100):
+        g.step(torch.randn(n, 12, device=DEV))
+    ep = g.extras["train/episode"]
+    assert len(ep["episode_length"]) == len(ep["rew_total"]) and len(g.extras["timeouts"]) % n == 0
+    assert torch.isfinite(g.env.obs_buf).all()

@@ -59,5 +59,6 @@ def test_oracle_replays_reference_steps(name):
                 continue
             np.testing.assert_allclose(st[k].reshape(d[f"s{t}/post/{k}"].shape), d[f"s{t}/post/{k}"], rtol=1e-4,
                                        atol=2e-5, err_msg=f"step {t} state {k}")
+        G.check_episode_log_and_extras(d, t, out["episode_log"], out["aux"])
         n_resets += int(d[f"s{t}/reset"].sum())
     assert n_resets > 0, "fixture should exercise reset_idx"
