@@ -1,0 +1,60 @@
+/*
+ * go1_rollout.h -- C ABI of the MI355X PPO rollout kernels (legged_tracking_amd/csrc/rollout.hip).
+ *
+ * Replaces, for the rollout half of the hot path (go1_gym_learn/ppo_cse):
+ *   go1_record_transition()  <- RolloutStorage.add_transitions     rollout_storage.py:57-71
+ *                               + PPO.process_env_step bootstrap    ppo.py:79-92
+ *   go1_gae()                <- RolloutStorage.compute_returns      rollout_storage.py:76-87
+ *   go1_adv_normalize()      <- rollout_storage.py:89-90 (global normalisation; the
+ *                               caller may all-reduce the 2 f64 statistics across ranks
+ *                               between the two calls)
+ *
+ * All pointers are device pointers owned by the caller; every call is
+ * asynchronous on the given HIP stream and returns 0 or a negative code.
+ */
+#ifndef GO1_ROLLOUT_H
+#define GO1_ROLLOUT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GO1_OK_RT 0
+#define GO1_RT_E_ARG -1
+#define GO1_RT_E_HIP -2
+
+/* One transition (rows of n_envs) and the storage slot it goes to. */
+typedef struct go1_transition {
+  const float* obs;               /* (n, num_obs) */
+  const float* privileged_obs;    /* (n, num_priv) */
+  const float* obs_history;       /* (n, num_obs_history) */
+  const float* actions;           /* (n, num_actions) */
+  const float* mu;                /* (n, num_actions) action mean */
+  const float* sigma;             /* (n, num_actions) action std */
+  const float* actions_log_prob;  /* (n) */
+  const float* values;            /* (n) */
+  const float* rewards;           /* (n) env rewards before bootstrapping */
+  const uint8_t* dones;           /* (n) bool */
+  const uint8_t* time_outs;       /* (n) bool or NULL (no bootstrap) */
+  float *st_obs, *st_privileged_obs, *st_obs_history, *st_actions, *st_mu, *st_sigma, *st_actions_log_prob;
+  float *st_values, *st_rewards;
+  uint8_t* st_dones;
+  int32_t num_obs, num_priv, num_obs_history, num_actions;
+} go1_transition;
+
+const char* go1_rollout_last_error(void);
+int go1_record_transition(const go1_transition* tr, int32_t n_envs, float gamma, void* stream);
+/* rewards/values/returns/advantages: (T, n) f32; dones (T, n) u8; last_values (n);
+ * stats: 2 f64 (sum, sum of squares of the raw advantages), overwritten. */
+int go1_gae(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
+            float* returns, float* advantages, double* stats, int32_t T, int32_t n_envs, float gamma, float lam,
+            void* stream);
+/* advantages <- (a - mean) / (std + 1e-8); count = number of samples the stats cover (all ranks). */
+int go1_adv_normalize(float* advantages, const double* stats, double count, int64_t total, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GO1_ROLLOUT_H */

@@ -1,30 +1,45 @@
-"""Build the HIP C-ABI library for gfx950 in-tree (legged_tracking_amd/_build)."""
+"""Build the HIP C-ABI libraries for gfx950 in-tree (legged_tracking_amd/_build)."""
 import os
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "go1_step.hip")
-OUT = os.path.join(HERE, "_build", "libgo1_mi355x.so")
+INC = os.path.join(HERE, "..", "include")
+BUILD = os.path.join(HERE, "_build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off"]
 
+# name -> (source, extra dependencies)
+LIBS = {
+    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", os.path.join(INC, "go1_mi355x.h")]),
+    "libgo1_rollout.so": ("rollout.hip", [os.path.join(INC, "go1_rollout.h")]),
+}
+OUT = os.path.join(BUILD, "libgo1_mi355x.so")  # the step library (kept for callers of build())
 
-def needs_build():
-    if not os.path.exists(OUT):
+
+def _paths(name):
+    src, deps = LIBS[name]
+    src = os.path.join(HERE, "csrc", src)
+    return src, [src] + [d if os.path.isabs(d) else os.path.join(HERE, "csrc", d) for d in deps]
+
+
+def needs_build(name):
+    out = os.path.join(BUILD, name)
+    if not os.path.exists(out):
         return True
-    deps = [SRC, os.path.join(HERE, "csrc", "pmath.h"), os.path.join(HERE, "..", "include", "go1_mi355x.h")]
-    return any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in deps)
+    return any(os.path.getmtime(d) > os.path.getmtime(out) for d in _paths(name)[1])
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC, *FLAGS, "-o", OUT, SRC]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+def build(force=False, verbose=False, names=None):
+    os.makedirs(BUILD, exist_ok=True)
+    for name in names or LIBS:
+        if not force and not needs_build(name):
+            continue
+        src, _ = _paths(name)
+        cmd = [HIPCC, *FLAGS, "-o", os.path.join(BUILD, name), src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
     return OUT
 
 

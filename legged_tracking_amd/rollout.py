@@ -1,0 +1,586 @@
+"""PPO rollout over the HIP env step: the go1_gym_learn.ppo_cse API the training script uses.
+
+Mirrors, with the same public names, constructor arguments and parameter names (so
+the reference's `ac_weights.pt` state dicts load unchanged):
+
+  AC_Args, ActorCritic     <- go1_gym_learn/ppo_cse/actor_critic.py:9-178
+  PPO_Args, PPO            <- go1_gym_learn/ppo_cse/ppo.py:13-206
+  RolloutStorage           <- go1_gym_learn/ppo_cse/rollout_storage.py:5-138
+  RunnerArgs, Runner       <- go1_gym_learn/ppo_cse/__init__.py:46-357
+
+MI355X mapping: the policy / value / adaptation MLPs are plain GEMM chains on
+hipBLASLt (through torch); the per-step transition copy, the GAE scan and the
+advantage normalisation are HIP kernels (csrc/rollout.hip, C ABI
+include/go1_rollout.h).  With torch.distributed initialised (one process per GPU,
+RCCL), the advantage statistics, the gradients and the KL estimate are
+all-reduced so that every rank follows the same optimisation trajectory as one
+large-batch run.
+"""
+import copy
+import ctypes as C
+import os
+import time
+from collections import deque
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.distributions import Normal
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GO1_ROLLOUT_LIB_OVERRIDE") or os.path.join(HERE, "_build", "libgo1_rollout.so")
+
+
+# ----------------------------------------------------------------------------- args
+class _Args:
+    """Plain mutable argument holder (scripts/train.py assigns attributes)."""
+
+
+class AC_Args(_Args):
+    init_noise_std = 1.0
+    actor_hidden_dims = [512, 256, 128]
+    critic_hidden_dims = [512, 256, 128]
+    activation = "elu"
+    adaptation_module_branch_hidden_dims = [256, 128]
+    use_decoder = False
+    normalize_obs = False
+
+
+class PPO_Args(_Args):
+    value_loss_coef = 1.0
+    use_clipped_value_loss = True
+    clip_param = 0.2
+    entropy_coef = 0.01
+    num_learning_epochs = 5
+    num_mini_batches = 4
+    learning_rate = 1.0e-3
+    adaptation_module_learning_rate = 1.0e-3
+    num_adaptation_module_substeps = 1
+    schedule = "adaptive"
+    gamma = 0.99
+    lam = 0.95
+    desired_kl = 0.01
+    max_grad_norm = 1.0
+    selective_adaptation_module_loss = False
+
+
+class RunnerArgs(_Args):
+    algorithm_class_name = "RMA"
+    num_steps_per_env = 24
+    max_iterations = 1500
+    save_interval = 400
+    save_video_interval = 100
+    log_freq = 10
+    resume = False
+    load_run = -1
+    checkpoint = -1
+    resume_path = None
+    resume_curriculum = True
+
+
+# ----------------------------------------------------------------------------- native kernels
+class _Transition(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("obs", "privileged_obs", "obs_history", "actions", "mu", "sigma",
+                                          "actions_log_prob", "values", "rewards", "dones", "time_outs",
+                                          "st_obs", "st_privileged_obs", "st_obs_history", "st_actions", "st_mu",
+                                          "st_sigma", "st_actions_log_prob", "st_values", "st_rewards",
+                                          "st_dones")] + [
+        ("num_obs", C.c_int32), ("num_priv", C.c_int32), ("num_obs_history", C.c_int32), ("num_actions", C.c_int32)]
+
+
+class HipRolloutKernels:
+    """ctypes binding of libgo1_rollout.so; raises when the library or the GPU is missing."""
+
+    def __init__(self):
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP rollout library missing: {LIB_PATH} (run __graft_entry__.build())")
+        if not torch.cuda.is_available():
+            raise RuntimeError("no GPU visible: the rollout kernels have no CPU fallback")
+        lib = C.CDLL(LIB_PATH)
+        lib.go1_rollout_last_error.restype = C.c_char_p
+        lib.go1_record_transition.argtypes = [C.POINTER(_Transition), C.c_int32, C.c_float, C.c_void_p]
+        lib.go1_gae.argtypes = [C.c_void_p] * 7 + [C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_void_p]
+        lib.go1_adv_normalize.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_int64, C.c_void_p]
+        self.lib = lib
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise RuntimeError(self.lib.go1_rollout_last_error().decode())
+
+    @staticmethod
+    def _s():
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def record(self, st, step, tr, gamma):
+        t = _Transition()
+        src = dict(obs=tr["observations"], privileged_obs=tr["privileged_observations"],
+                   obs_history=tr["observation_histories"], actions=tr["actions"], mu=tr["action_mean"],
+                   sigma=tr["action_sigma"], actions_log_prob=tr["actions_log_prob"], values=tr["values"],
+                   rewards=tr["rewards"], dones=tr["dones"], time_outs=tr.get("time_outs"))
+        keep = []
+        for k, v in src.items():
+            if v is None:
+                continue
+            v = v.detach()
+            if v.dtype == torch.bool:
+                v = v.view(torch.uint8)
+            v = v.contiguous()
+            keep.append(v)
+            setattr(t, k, v.data_ptr())
+        for k, buf in (("st_obs", st.observations), ("st_privileged_obs", st.privileged_observations),
+                       ("st_obs_history", st.observation_histories), ("st_actions", st.actions),
+                       ("st_mu", st.mu), ("st_sigma", st.sigma), ("st_actions_log_prob", st.actions_log_prob),
+                       ("st_values", st.values), ("st_rewards", st.rewards), ("st_dones", st.dones)):
+            setattr(t, k, buf[step].data_ptr())
+        t.num_obs, t.num_priv = st.observations.shape[-1], st.privileged_observations.shape[-1]
+        t.num_obs_history, t.num_actions = st.observation_histories.shape[-1], st.actions.shape[-1]
+        self._chk(self.lib.go1_record_transition(C.byref(t), st.num_envs, gamma, self._s()))
+        return keep
+
+    def gae(self, st, last_values, gamma, lam):
+        lv = last_values.detach().contiguous()
+        self._chk(self.lib.go1_gae(st.rewards.data_ptr(), st.dones.data_ptr(), st.values.data_ptr(), lv.data_ptr(),
+                                   st.returns.data_ptr(), st.advantages.data_ptr(), st.adv_stats.data_ptr(),
+                                   st.num_transitions_per_env, st.num_envs, gamma, lam, self._s()))
+
+    def normalize(self, st, count):
+        self._chk(self.lib.go1_adv_normalize(st.advantages.data_ptr(), st.adv_stats.data_ptr(), float(count),
+                                             st.advantages.numel(), self._s()))
+
+
+# ----------------------------------------------------------------------------- model
+def get_activation(name):
+    acts = dict(elu=nn.ELU, selu=nn.SELU, relu=nn.ReLU, crelu=nn.ReLU, lrelu=nn.LeakyReLU, tanh=nn.Tanh,
+                sigmoid=nn.Sigmoid)
+    if name not in acts:
+        raise ValueError(f"invalid activation function {name!r}")
+    return acts[name]()
+
+
+def _mlp(sizes, act):
+    layers = []
+    for i in range(len(sizes) - 1):
+        layers.append(nn.Linear(sizes[i], sizes[i + 1]))
+        if i < len(sizes) - 2:
+            layers.append(act)
+    return nn.Sequential(*layers)
+
+
+class ActorCritic(nn.Module):
+    """Student/teacher actor-critic (actor_critic.py:21-156): adaptation module
+    obs_history -> latent (privileged estimate), actor (obs_history, latent) -> action
+    mean, critic (obs_history, privileged_obs) -> value, state-independent std."""
+
+    is_recurrent = False
+
+    def __init__(self, num_obs, num_privileged_obs, num_obs_history, num_actions, **kwargs):
+        super().__init__()
+        self.decoder = AC_Args.use_decoder
+        self.num_obs_history = num_obs_history
+        self.num_privileged_obs = num_privileged_obs
+        act = get_activation(AC_Args.activation)
+        self.adaptation_module = _mlp([num_obs_history, *AC_Args.adaptation_module_branch_hidden_dims,
+                                       num_privileged_obs], act)
+        self.actor_body = _mlp([num_privileged_obs + num_obs_history, *AC_Args.actor_hidden_dims, num_actions], act)
+        self.critic_body = _mlp([num_privileged_obs + num_obs_history, *AC_Args.critic_hidden_dims, 1], act)
+        self.std = nn.Parameter(AC_Args.init_noise_std * torch.ones(num_actions))
+        self.distribution = None
+        self.normalize_obs = AC_Args.normalize_obs
+        if self.normalize_obs:
+            raise NotImplementedError("normalize_obs is off in the README configuration and not on this path")
+
+    def reset(self, dones=None):
+        pass
+
+    @property
+    def action_mean(self):
+        return self.distribution.mean
+
+    @property
+    def action_std(self):
+        return self.distribution.stddev
+
+    @property
+    def entropy(self):
+        return self.distribution.entropy().sum(dim=-1)
+
+    def update_distribution(self, observation_history):
+        latent = self.adaptation_module(observation_history)
+        mean = self.actor_body(torch.cat((observation_history, latent), dim=-1))
+        self.distribution = Normal(mean, mean * 0.0 + self.std, validate_args=False)
+
+    def act(self, observation_history, **kwargs):
+        self.update_distribution(observation_history)
+        return self.distribution.sample()
+
+    def get_actions_log_prob(self, actions):
+        return self.distribution.log_prob(actions).sum(dim=-1)
+
+    def act_expert(self, ob, policy_info={}):
+        return self.act_teacher(ob["obs_history"], ob["privileged_obs"])
+
+    def act_inference(self, ob, policy_info={}):
+        return self.act_student(ob["obs_history"], policy_info=policy_info)
+
+    def act_student(self, observation_history, policy_info={}):
+        latent = self.adaptation_module(observation_history)
+        policy_info["latents"] = latent.detach().cpu().numpy()
+        return self.actor_body(torch.cat((observation_history, latent), dim=-1))
+
+    def act_teacher(self, observation_history, privileged_info, policy_info={}):
+        policy_info["latents"] = privileged_info
+        return self.actor_body(torch.cat((observation_history, privileged_info), dim=-1))
+
+    def evaluate(self, observation_history, privileged_observations, **kwargs):
+        return self.critic_body(torch.cat((observation_history, privileged_observations), dim=-1))
+
+    def get_student_latent(self, observation_history):
+        return self.adaptation_module(observation_history)
+
+
+# ----------------------------------------------------------------------------- storage
+class RolloutStorage:
+    """Device-resident (T, n, ...) rollout buffers (rollout_storage.py:24-56)."""
+
+    class Transition:
+        def __init__(self):
+            self.observations = None
+            self.privileged_observations = None
+            self.observation_histories = None
+            self.critic_observations = None
+            self.actions = None
+            self.rewards = None
+            self.dones = None
+            self.values = None
+            self.actions_log_prob = None
+            self.action_mean = None
+            self.action_sigma = None
+            self.env_bins = None
+            self.time_outs = None
+
+        def clear(self):
+            self.__init__()
+
+    def __init__(self, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape, obs_history_shape,
+                 actions_shape, device="cpu", kernels=None):
+        self.device = device
+        T, n = num_transitions_per_env, num_envs
+        z = lambda *s: torch.zeros(T, n, *s, device=device)  # noqa: E731
+        self.obs_shape, self.privileged_obs_shape = obs_shape, privileged_obs_shape
+        self.obs_history_shape, self.actions_shape = obs_history_shape, actions_shape
+        self.observations = z(*obs_shape)
+        self.privileged_observations = z(*privileged_obs_shape)
+        self.observation_histories = z(*obs_history_shape)
+        self.rewards = z(1)
+        self.actions = z(*actions_shape)
+        self.dones = z(1).byte()
+        self.actions_log_prob = z(1)
+        self.values = z(1)
+        self.returns = z(1)
+        self.advantages = z(1)
+        self.mu = z(*actions_shape)
+        self.sigma = z(*actions_shape)
+        self.env_bins = z(1)
+        self.adv_stats = torch.zeros(2, dtype=torch.float64, device=device)
+        self.num_transitions_per_env, self.num_envs = T, n
+        self.step = 0
+        self.kernels = kernels if kernels is not None else HipRolloutKernels()
+        self._keep = None
+
+    def add_transitions(self, transition, gamma=0.0):
+        if self.step >= self.num_transitions_per_env:
+            raise AssertionError("Rollout buffer overflow")
+        tr = {k: getattr(transition, k) for k in ("observations", "privileged_observations", "observation_histories",
+                                                  "actions", "action_mean", "action_sigma", "actions_log_prob",
+                                                  "values", "rewards", "dones", "time_outs")}
+        self._keep = self.kernels.record(self, self.step, tr, gamma)
+        self.step += 1
+
+    def clear(self):
+        self.step = 0
+
+    def compute_returns(self, last_values, gamma, lam):
+        """GAE (rollout_storage.py:76-90); global normalisation across ranks."""
+        self.kernels.gae(self, last_values, gamma, lam)
+        count = float(self.advantages.numel())
+        if torch.distributed.is_available() and torch.distributed.is_initialized() and \
+                torch.distributed.get_world_size() > 1:
+            torch.distributed.all_reduce(self.adv_stats)
+            count *= torch.distributed.get_world_size()
+        self.kernels.normalize(self, count)
+
+    def get_statistics(self):
+        done = self.dones.clone()
+        done[-1] = 1
+        flat_dones = done.permute(1, 0, 2).reshape(-1, 1)
+        done_indices = torch.cat((flat_dones.new_tensor([-1], dtype=torch.int64),
+                                  flat_dones.nonzero(as_tuple=False)[:, 0]))
+        return (done_indices[1:] - done_indices[:-1]).float().mean(), self.rewards.mean()
+
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8, generator=None):
+        batch_size = self.num_envs * self.num_transitions_per_env
+        mb = batch_size // num_mini_batches
+        indices = torch.randperm(num_mini_batches * mb, device=self.device, generator=generator)
+        flat = [x.flatten(0, 1) for x in (self.observations, self.observations, self.privileged_observations,
+                                         self.observation_histories, self.actions, self.values, self.advantages,
+                                         self.returns, self.actions_log_prob, self.mu, self.sigma)]
+        bins = self.env_bins.flatten(0, 1)
+        for _ in range(num_epochs):
+            for i in range(num_mini_batches):
+                idx = indices[i * mb:(i + 1) * mb]
+                b = [x[idx] for x in flat]
+                yield (*b, None, bins[idx])
+
+
+# ----------------------------------------------------------------------------- PPO
+def _world():
+    d = torch.distributed
+    if d.is_available() and d.is_initialized():
+        return d.get_world_size()
+    return 1
+
+
+class PPO:
+    """PPO with the adaptation-module regression (ppo.py:33-206)."""
+
+    def __init__(self, actor_critic, device="cpu", kernels=None):
+        self.device = device
+        self.actor_critic = actor_critic.to(device)
+        self.storage = None
+        self.kernels = kernels
+        self.optimizer = torch.optim.Adam(self.actor_critic.parameters(), lr=PPO_Args.learning_rate)
+        self.adaptation_module_optimizer = torch.optim.Adam(self.actor_critic.parameters(),
+                                                            lr=PPO_Args.adaptation_module_learning_rate)
+        self.transition = RolloutStorage.Transition()
+        self.learning_rate = PPO_Args.learning_rate
+        if _world() > 1:  # every rank starts from rank 0's weights
+            for p in self.actor_critic.parameters():
+                torch.distributed.broadcast(p.data, 0)
+
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, privileged_obs_shape,
+                     obs_history_shape, action_shape):
+        self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, privileged_obs_shape,
+                                      obs_history_shape, action_shape, self.device, kernels=self.kernels)
+
+    def test_mode(self):
+        self.actor_critic.eval()
+
+    def train_mode(self):
+        self.actor_critic.train()
+
+    def act(self, obs, privileged_obs, obs_history):
+        ac = self.actor_critic
+        t = self.transition
+        t.actions = ac.act(obs_history).detach()
+        t.values = ac.evaluate(obs_history, privileged_obs).detach()
+        t.actions_log_prob = ac.get_actions_log_prob(t.actions).detach()
+        t.action_mean = ac.action_mean.detach()
+        t.action_sigma = ac.action_std.detach()
+        t.observations = obs
+        t.critic_observations = obs
+        t.privileged_observations = privileged_obs
+        t.observation_histories = obs_history
+        return t.actions
+
+    def process_env_step(self, rewards, dones, infos):
+        """Records the transition; the time-out bootstrap r += gamma * V * time_outs
+        (ppo.py:85-87) is applied inside the record kernel."""
+        t = self.transition
+        t.rewards = rewards
+        t.dones = dones
+        t.time_outs = infos["time_outs"] if "time_outs" in infos else None
+        self.storage.add_transitions(t, gamma=PPO_Args.gamma)
+        t.clear()
+        self.actor_critic.reset(dones)
+
+    def compute_returns(self, last_critic_obs, last_critic_privileged_obs):
+        last_values = self.actor_critic.evaluate(last_critic_obs, last_critic_privileged_obs).detach()
+        self.storage.compute_returns(last_values, PPO_Args.gamma, PPO_Args.lam)
+
+    def _allreduce_grads(self):
+        w = _world()
+        if w == 1:
+            return
+        params = [p for p in self.actor_critic.parameters() if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        torch.distributed.all_reduce(flat)
+        flat /= w
+        off = 0
+        for p in params:
+            k = p.numel()
+            p.grad.copy_(flat[off:off + k].view_as(p.grad))
+            off += k
+
+    def update(self):
+        A = PPO_Args
+        ac = self.actor_critic
+        mean_value_loss = mean_surrogate_loss = mean_adapt = mean_adapt_test = 0.0
+        gen = self.storage.mini_batch_generator(A.num_mini_batches, A.num_learning_epochs)
+        for (obs_b, critic_obs_b, priv_b, hist_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b,
+             old_sigma_b, masks_b, bins_b) in gen:
+            ac.act(hist_b, masks=masks_b)
+            logp_b = ac.get_actions_log_prob(act_b)
+            value_b = ac.evaluate(hist_b, priv_b, masks=masks_b)
+            mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
+            if A.desired_kl is not None and A.schedule == "adaptive":
+                with torch.inference_mode():
+                    kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.0e-5) +
+                                   (torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) /
+                                   (2.0 * torch.square(sigma_b)) - 0.5, axis=-1)
+                    kl_mean = torch.mean(kl)
+                    if _world() > 1:
+                        kl_mean = kl_mean.clone()
+                        torch.distributed.all_reduce(kl_mean)
+                        kl_mean /= _world()
+                    kl_mean = float(kl_mean)
+                    if kl_mean > A.desired_kl * 2.0:
+                        self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+                    elif A.desired_kl / 2.0 > kl_mean > 0.0:
+                        self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+                    for g in self.optimizer.param_groups:
+                        g["lr"] = self.learning_rate
+            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+            surrogate = -torch.squeeze(adv_b) * ratio
+            surrogate_clipped = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - A.clip_param, 1.0 + A.clip_param)
+            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+            if A.use_clipped_value_loss:
+                value_clipped = target_v_b + (value_b - target_v_b).clamp(-A.clip_param, A.clip_param)
+                value_loss = torch.max((value_b - ret_b).pow(2), (value_clipped - ret_b).pow(2)).mean()
+            else:
+                value_loss = (ret_b - value_b).pow(2).mean()
+            loss = surrogate_loss + A.value_loss_coef * value_loss - A.entropy_coef * entropy_b.mean()
+            self.optimizer.zero_grad()
+            loss.backward()
+            self._allreduce_grads()
+            nn.utils.clip_grad_norm_(ac.parameters(), A.max_grad_norm)
+            self.optimizer.step()
+            mean_value_loss += value_loss.item()
+            mean_surrogate_loss += surrogate_loss.item()
+            num_train = int(priv_b.shape[0] // 5 * 4)
+            for _ in range(A.num_adaptation_module_substeps):
+                pred = ac.adaptation_module(hist_b)
+                with torch.no_grad():
+                    target = priv_b
+                sel = torch.linspace(0, pred.shape[1] - 1, steps=pred.shape[1], dtype=torch.long)
+                if A.selective_adaptation_module_loss:
+                    sel = 0
+                adapt_loss = F.mse_loss(pred[:num_train, sel], target[:num_train, sel])
+                adapt_test = F.mse_loss(pred[num_train:, sel], target[num_train:, sel])
+                self.adaptation_module_optimizer.zero_grad()
+                adapt_loss.backward()
+                self._allreduce_grads()
+                self.adaptation_module_optimizer.step()
+                mean_adapt += adapt_loss.item()
+                mean_adapt_test += adapt_test.item()
+        n_up = A.num_learning_epochs * A.num_mini_batches
+        n_ad = n_up * A.num_adaptation_module_substeps
+        self.storage.clear()
+        return (mean_value_loss / n_up, mean_surrogate_loss / n_up, mean_adapt / n_ad, 0.0, 0.0,
+                mean_adapt_test / n_ad, 0.0, 0.0)
+
+
+# ----------------------------------------------------------------------------- runner
+class Runner:
+    """Runner (ppo_cse/__init__.py:66-357): rollout of num_steps_per_env env steps per
+    iteration, GAE, PPO update, checkpoints (ac_weights.pt + TorchScript adaptation
+    module and actor body, the formats scripts/eval.py and the deploy stack read)."""
+
+    def __init__(self, env, device="cpu", runner_args=RunnerArgs, ac_args=AC_Args, log_wandb=False, kernels=None,
+                 save_dir="last_run/checkpoints"):
+        self.device = device
+        self.env = env
+        self.runner_args = runner_args
+        self.log_wandb = log_wandb
+        self.save_dir = save_dir
+        ac = ActorCritic(env.num_obs, env.num_privileged_obs, env.num_obs_history, env.num_actions).to(device)
+        if runner_args.resume:
+            ac.load_state_dict(torch.load(runner_args.resume, map_location=device, weights_only=True))
+        self.alg = PPO(ac, device=device, kernels=kernels)
+        self.num_steps_per_env = runner_args.num_steps_per_env
+        self.alg.init_storage(env.num_train_envs, self.num_steps_per_env, [env.num_obs], [env.num_privileged_obs],
+                              [env.num_obs_history], [env.num_actions])
+        self.tot_timesteps = 0
+        self.tot_time = 0
+        self.current_learning_iteration = 0
+        self.last_recording_it = -1000
+        self.env.reset()
+
+    def rollout(self, obs, privileged_obs, obs_history, update_model=True, eval_expert=False):
+        """One iteration's rollout (ppo_cse/__init__.py:164-214)."""
+        n_train = self.env.num_train_envs
+        rewards = dones = infos = None
+        for _ in range(self.num_steps_per_env):
+            actions = self.alg.act(obs[:n_train], privileged_obs[:n_train], obs_history[:n_train])
+            if n_train < self.env.num_envs:
+                ac = self.alg.actor_critic
+                extra = ac.act_teacher(obs_history[n_train:], privileged_obs[n_train:]) if eval_expert else \
+                    ac.act_student(obs_history[n_train:])
+                actions = torch.cat((actions, extra), dim=0)
+            obs_dict, rewards, dones, infos = self.env.step(actions)
+            obs, privileged_obs, obs_history = obs_dict["obs"], obs_dict["privileged_obs"], obs_dict["obs_history"]
+            if update_model:
+                self.alg.process_env_step(rewards[:n_train], dones[:n_train], infos)
+            if "train/episode" in infos and self.log_wandb:
+                import wandb
+                info = infos["train/episode"]
+                wandb.log({"train": {k: np.mean(v) for k, v in info.items()}})
+        return obs, privileged_obs, obs_history, infos
+
+    def learn(self, num_learning_iterations, init_at_random_ep_len=False, eval_freq=100, curriculum_dump_freq=500,
+              eval_expert=False, update_model=True):
+        n_train = self.env.num_train_envs
+        obs_dict = self.env.get_observations()
+        obs, privileged_obs, obs_history = (obs_dict[k].to(self.device) for k in ("obs", "privileged_obs",
+                                                                                  "obs_history"))
+        self.alg.actor_critic.train()
+        if init_at_random_ep_len:
+            # as in the reference, this lands on the HistoryWrapper, not the env
+            self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
+                                                             high=int(self.env.max_episode_length))
+        for it in range(num_learning_iterations):
+            start = time.time()
+            with torch.inference_mode():
+                obs, privileged_obs, obs_history, infos = self.rollout(obs, privileged_obs, obs_history,
+                                                                       update_model, eval_expert)
+                if update_model:
+                    self.alg.compute_returns(obs_history[:n_train], privileged_obs[:n_train])
+            if update_model:
+                losses = self.alg.update()
+            else:
+                losses = (0.0,) * 8
+            if self.log_wandb:
+                import wandb
+                keys = ("mean_value_loss", "mean_surrogate_loss", "adaptation_loss", "mean_decoder_loss",
+                        "mean_decoder_loss_student", "mean_adaptation_module_test_loss", "mean_decoder_test_loss",
+                        "mean_decoder_test_loss_student")
+                wandb.log({"metrics": dict(zip(keys, losses))})
+            self.tot_timesteps += self.num_steps_per_env * self.env.num_envs
+            self.tot_time += time.time() - start
+            self.current_learning_iteration = it
+            if it % self.runner_args.save_interval == 0:
+                self.save(self.save_dir)
+        self.save(self.save_dir)
+
+    def save(self, save_path):
+        """ac_weights.pt + adaptation_module_latest.jit + body_latest.jit (__init__.py:274-319)."""
+        if _world() > 1 and torch.distributed.get_rank() != 0:
+            return
+        os.makedirs(save_path, exist_ok=True)
+        ac = self.alg.actor_critic
+        torch.save(ac.state_dict(), os.path.join(save_path, "ac_weights.pt"))
+        torch.jit.script(copy.deepcopy(ac.adaptation_module).to("cpu")).save(
+            os.path.join(save_path, "adaptation_module_latest.jit"))
+        torch.jit.script(copy.deepcopy(ac.actor_body).to("cpu")).save(os.path.join(save_path, "body_latest.jit"))
+
+    def get_inference_policy(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.act_inference
+
+    def get_expert_policy(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.act_expert

@@ -1,0 +1,179 @@
+"""PPO rollout half of the path against the reference's own outputs
+(tests/golden/ppo_rollout.npz from tests/golden/make_golden_ppo.py).
+
+CPU tests drive the host logic with the torch restatement of the rollout kernels
+(tests/rollout_ref.py); the HIP kernels are checked in the gpu-marked tests:
+returns / raw advantages / bootstrapped rewards bit-exact (same f32 op order),
+normalised advantages within 2e-6 (f64 statistics vs torch's f32 reductions).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from legged_tracking_amd import rollout as R
+from tests import golden_io as G
+from tests.rollout_ref import TorchRolloutKernels
+
+
+def _fixture():
+    return G.load("ppo_rollout.npz")
+
+
+def _ac(d, device="cpu"):
+    ac = R.ActorCritic(261, 2, 261, 12)
+    sd = {k[3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("sd/")}
+    ac.load_state_dict(sd)  # the reference's parameter names load unchanged
+    return ac.to(device)
+
+
+def test_actor_critic_matches_reference():
+    d = _fixture()
+    ac = _ac(d)
+    hist, priv, acts = (torch.from_numpy(d[k]) for k in ("in/hist", "in/priv", "in/actions"))
+    with torch.no_grad():
+        ac.update_distribution(hist)
+        np.testing.assert_allclose(ac.adaptation_module(hist).numpy(), d["ac/latent"], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(ac.action_mean.numpy(), d["ac/mean"], rtol=1e-6, atol=1e-6)
+        np.testing.assert_array_equal(ac.action_std.numpy(), d["ac/std"])
+        np.testing.assert_allclose(ac.get_actions_log_prob(acts).numpy(), d["ac/log_prob"], rtol=1e-6, atol=1e-5)
+        np.testing.assert_allclose(ac.entropy.numpy(), d["ac/entropy"], rtol=1e-6)
+        np.testing.assert_allclose(ac.evaluate(hist, priv).numpy(), d["ac/value"], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(ac.act_teacher(hist, priv).numpy(), d["ac/teacher_mean"], rtol=1e-6, atol=1e-6)
+
+
+def _storage_from_fixture(d, kernels, device="cpu"):
+    T, n = d["gae/rewards_in"].shape
+    st = R.RolloutStorage(n, T, [261], [2], [261], [12], device, kernels=kernels)
+    tr = R.RolloutStorage.Transition()
+    for t in range(T):
+        tr.observations = torch.zeros(n, 261, device=device)
+        tr.privileged_observations = torch.zeros(n, 2, device=device)
+        tr.observation_histories = torch.zeros(n, 261, device=device)
+        tr.actions = torch.zeros(n, 12, device=device)
+        tr.action_mean = torch.zeros(n, 12, device=device)
+        tr.action_sigma = torch.ones(n, 12, device=device)
+        tr.actions_log_prob = torch.zeros(n, device=device)
+        tr.values = torch.from_numpy(d["gae/values"][t][:, None]).to(device)
+        tr.rewards = torch.from_numpy(d["gae/rewards_in"][t]).to(device)
+        tr.dones = torch.from_numpy(d["gae/dones"][t]).to(device)
+        tr.time_outs = torch.from_numpy(d["gae/time_outs"][t]).to(device)
+        st.add_transitions(tr, gamma=float(d["gae/gamma"]))
+    return st
+
+
+def _check_gae(d, st):
+    np.testing.assert_array_equal(st.rewards.cpu().numpy()[..., 0], d["gae/rewards_boot"])
+    last_v = torch.from_numpy(d["gae/last_values"][:, None]).to(st.device)
+    st.compute_returns(last_v, float(d["gae/gamma"]), float(d["gae/lam"]))
+    np.testing.assert_array_equal(st.returns.cpu().numpy()[..., 0], d["gae/returns"])
+    np.testing.assert_allclose(st.advantages.cpu().numpy()[..., 0], d["gae/advantages"], rtol=2e-6, atol=2e-6)
+
+
+def test_gae_restatement_matches_reference():
+    d = _fixture()
+    _check_gae(d, _storage_from_fixture(d, TorchRolloutKernels()))
+
+
+@pytest.mark.gpu
+def test_hip_rollout_kernels_match_reference():
+    d = _fixture()
+    st = _storage_from_fixture(d, R.HipRolloutKernels(), device="cuda:0")
+    # raw advantages before normalisation are bit-exact too
+    k = st.kernels
+    last_v = torch.from_numpy(d["gae/last_values"][:, None]).cuda()
+    k.gae(st, last_v, float(d["gae/gamma"]), float(d["gae/lam"]))
+    np.testing.assert_array_equal(st.advantages.cpu().numpy()[..., 0], d["gae/raw_advantages"])
+    _check_gae(d, st)
+
+
+def _runner(tmp_path, n=16, steps=4, kernels=None):
+    from legged_tracking_amd import env as E
+    from tests.test_env_host import make_env
+    R.RunnerArgs.num_steps_per_env = steps
+    R.PPO_Args.num_learning_epochs = 1
+    R.PPO_Args.num_mini_batches = 2
+    env = E.HistoryWrapper(make_env(n=n))
+    return R.Runner(env, device="cpu", kernels=kernels or TorchRolloutKernels(),
+                    save_dir=str(tmp_path / "checkpoints"))
+
+
+def test_runner_learns_and_writes_reference_checkpoints(tmp_path):
+    torch.manual_seed(0)
+    try:
+        runner = _runner(tmp_path)
+        before = {k: v.clone() for k, v in runner.alg.actor_critic.state_dict().items()}
+        runner.learn(2, init_at_random_ep_len=True)
+    finally:
+        R.RunnerArgs.num_steps_per_env, R.PPO_Args.num_learning_epochs, R.PPO_Args.num_mini_batches = 24, 5, 4
+    after = runner.alg.actor_critic.state_dict()
+    assert any(not torch.equal(before[k], after[k]) for k in before)
+    ck = tmp_path / "checkpoints"
+    sd = torch.load(ck / "ac_weights.pt", weights_only=True)
+    assert set(sd) == set(after)
+    body = torch.jit.load(str(ck / "body_latest.jit"))
+    adapt = torch.jit.load(str(ck / "adaptation_module_latest.jit"))
+    x = torch.randn(3, 261)
+    with torch.no_grad():
+        lat = adapt(x)
+        np.testing.assert_allclose(body(torch.cat([x, lat], 1)).numpy(),
+                                   runner.alg.actor_critic.act_student(x).numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _ddp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        d = _fixture()
+        T, n = d["gae/rewards_in"].shape
+        half = n // world
+        # global advantage normalisation: each rank holds half of the envs
+        sl = slice(rank * half, (rank + 1) * half)
+        st = R.RolloutStorage(half, T, [261], [2], [261], [12], "cpu", kernels=TorchRolloutKernels())
+        st.rewards[..., 0] = torch.from_numpy(d["gae/rewards_boot"][:, sl])
+        st.dones[..., 0] = torch.from_numpy(d["gae/dones"][:, sl].astype(np.uint8))
+        st.values[..., 0] = torch.from_numpy(d["gae/values"][:, sl])
+        st.compute_returns(torch.from_numpy(d["gae/last_values"][sl, None]), float(d["gae/gamma"]),
+                           float(d["gae/lam"]))
+        ok_adv = np.allclose(st.advantages.numpy()[..., 0], d["gae/advantages"][:, sl], rtol=2e-6, atol=2e-6)
+        # gradient all-reduce: ranks with different data end with identical weights
+        torch.manual_seed(123)  # same init on both ranks is not required: PPO broadcasts rank 0's
+        if rank == 1:
+            torch.manual_seed(999)
+        ac = R.ActorCritic(261, 2, 261, 12)
+        alg = R.PPO(ac, "cpu", kernels=TorchRolloutKernels())
+        alg.storage = st
+        g = np.random.default_rng(rank)
+        for name in ("observations", "privileged_observations", "observation_histories", "actions", "mu"):
+            getattr(st, name).copy_(torch.from_numpy(g.normal(0, 1, getattr(st, name).shape).astype(np.float32)))
+        st.sigma.fill_(1.0)
+        st.actions_log_prob.copy_(torch.from_numpy(g.normal(-15, 1, st.actions_log_prob.shape).astype(np.float32)))
+        R.PPO_Args.num_learning_epochs, R.PPO_Args.num_mini_batches = 1, 2
+        alg.update()
+        flat = torch.cat([p.detach().reshape(-1) for p in ac.parameters()])
+        other = flat.clone()
+        dist.broadcast(other, 0)
+        lr = torch.tensor([alg.learning_rate])
+        lr0 = lr.clone()
+        dist.broadcast(lr0, 0)
+        q.put((rank, bool(ok_adv), bool(torch.equal(flat, other)), bool(torch.equal(lr, lr0))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_normalisation_and_gradients_gloo():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 1000
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs)
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    for rank, ok_adv, same_w, same_lr in res:
+        assert ok_adv and same_w and same_lr, res
