@@ -46,6 +46,22 @@ BYTES_PER_ENV_STEP = 1936 + 2279
 FLOPS_PER_ENV_STEP = 12 * 4 * 2688
 
 
+# PMC-measured HBM bytes per launch of the step kernel (tools/profile.sh + tools/prof_summary.py;
+# FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  Re-collected whenever the kernel changes.
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01", "step_counters.json")
+
+
+def pmc_traffic(n_envs):
+    try:
+        with open(TRAFFIC_FILE) as f:
+            d = json.load(f)
+        if int(d["resources"]["Grid_Size"]) != 4 * n_envs:
+            return None, None
+        return d["hbm_bytes_per_launch"]["traffic"], os.path.relpath(TRAFFIC_FILE, REPO)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def hip():
     h = C.CDLL("libamdhip64.so")
     h.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
@@ -94,6 +110,45 @@ def cpu_baseline(n_envs, budget_s=12.0, max_steps=400):
                       f"{dt:.1f} s on {threads} threads of {cores} visible ({model})"}
 
 
+def rollout_rate(n, dev, steps, warmup):
+    """Secondary line (SURVEY 8(d) "report both env-only and rollout (act + step) rates"):
+    the Runner's rollout loop -- ActorCritic.act + value (hipBLASLt GEMMs), env.step
+    through TrajectoryTrackingEnv/HistoryWrapper, transition record kernel -- at n envs."""
+    import torch
+    from legged_tracking_amd import config as CF, env as E, rollout as R
+    cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=32, cols=32)
+    env = E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device=str(dev), cfg=cfg, seed=11, rank=0, world_size=1))
+    ac = R.ActorCritic(env.num_obs, env.num_privileged_obs, env.num_obs_history, env.num_actions).to(dev)
+    alg = R.PPO(ac, device=dev)
+    T = 24
+    alg.init_storage(n, T, [env.num_obs], [env.num_privileged_obs], [env.num_obs_history], [env.num_actions])
+    env.reset()
+    od = env.get_observations()
+    obs, priv, hist = od["obs"], od["privileged_obs"], od["obs_history"]
+
+    def one():
+        nonlocal obs, priv, hist
+        if alg.storage.step == T:
+            alg.storage.clear()
+        a = alg.act(obs, priv, hist)
+        od, rew, done, info = env.step(a)
+        obs, priv, hist = od["obs"], od["privileged_obs"], od["obs_history"]
+        alg.process_env_step(rew, done, info)
+
+    with torch.inference_mode():
+        for _ in range(warmup):
+            one()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+            "what": "PPO.act (policy+value GEMMs, Normal sample) + TrajectoryTrackingEnv.step + HistoryWrapper + "
+                    "process_env_step record kernel, 1 GPU"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,6 +157,7 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-rollout", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -180,6 +236,7 @@ def main():
         value = n_global * args.steps / elapsed
         achieved_gbs = BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
         achieved_tf = FLOPS_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic(n)
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -189,11 +246,14 @@ def main():
                        "envs_per_gpu": n, "global_envs": n_global, "decimation": c.decimation,
                        "integrator_substeps": c.n_internal, "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * n,
                          "kernel": "go1_step_kernel<false>", "kernel_ms": kernel_ms,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP,
                          "fp32_tflops_actuator_only": achieved_tf, "fp32_frac_actuator_only": achieved_tf / FP32_PEAK_TFLOPS},
         }
+        if not args.no_rollout:
+            line["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24))
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(n, budget_s=args.cpu_budget)
         print(json.dumps(line), flush=True)

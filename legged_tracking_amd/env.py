@@ -92,7 +92,7 @@ class LeggedRobot:
     """LeggedRobot (:24-362) for the README configuration, backed by the HIP step."""
 
     def __init__(self, cfg, sim_params=None, physics_engine="SIM_PHYSX", sim_device="cuda:0", headless=True,
-                 eval_cfg=None, initial_dynamics_dict=None, *, seed=1, rank=None, world_size=None, backend=None,
+                 eval_cfg=None, initial_dynamics_dict=None, *, seed=11, rank=None, world_size=None, backend=None,
                  physics=None):
         if eval_cfg is not None:
             raise NotImplementedError("eval envs (eval_cfg) are not on the accelerated path")
