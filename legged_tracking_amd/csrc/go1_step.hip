@@ -36,10 +36,25 @@
 
 #pragma clang fp contract(off)
 
+#ifdef GO1_ISA_MARKS  // section markers for static instruction accounting (tools/isa_sections.py)
+#define MARK(x) asm volatile("; MARK " #x)
+#else
+#define MARK(x)
+#endif
+#ifndef GO1_MLP_UNROLL_N
+#define GO1_MLP_UNROLL_N 4
+#endif
+#ifndef GO1_CONTACT_ROLL
+#define GO1_CONTACT_ROLL 0
+#endif
+#ifndef GO1_TRUNK_PTS
+#define GO1_TRUNK_PTS 2
+#endif
 #define NDOF 12
 #define NB 17
-#define EPB 16          // envs per block
-#define TPB (EPB * 4)   // one wave
+#define EPB 16          // envs per block of the reset kernel (4 lanes per env)
+#define TPB 64          // one wave per block
+#define SEPB 4          // envs per wave of the step kernel (16 lanes per env: 4 roles x 4 legs)
 #define PI_F 3.14159265358979323846f
 #define TWO_PI_F 6.28318548202514648438f  // (float)(2*pi), torch's f32 scalar
 
@@ -69,10 +84,33 @@ struct Rng {
 };
 
 // ---------------------------------------------------------------- quad helpers
+#ifndef GO1_DPP
+#define GO1_DPP 1
+#endif
+// sum over the quad (lanes xor 1, 2) in the order (l0 + l1) + (l2 + l3); DPP quad_perm
+// moves stay in the VALU (no LDS round trip)
 __device__ __forceinline__ float qsum(float v) {
+#if GO1_DPP
+  v = v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  v = v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+#else
   v = v + __shfl_xor(v, 1);
   v = v + __shfl_xor(v, 2);
+#endif
   return v;
+}
+
+// sum over the four 16-lane rows, (r0 + r1) + (r2 + r3): gfx950 v_permlane16/32_swap
+__device__ __forceinline__ float rowsum4(float p) {
+#if GO1_DPP
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+  p = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+#else
+  p = p + __shfl_xor(p, 16);
+  return p + __shfl_xor(p, 32);
+#endif
 }
 
 // ---------------------------------------------------------------- actuator net
@@ -120,7 +158,26 @@ __device__ __forceinline__ void mlp_load(const float* __restrict__ W, int lane, 
   F.b3 = W[1312];
 }
 
-__device__ __forceinline__ float softsign(float x) { return x / (fabsf(x) + 1.0f); }
+#ifndef GO1_FAST_SOFTSIGN
+#define GO1_FAST_SOFTSIGN 1
+#endif
+// x / (|x| + 1).  The fast form (hardware reciprocal + one FMA residual correction)
+// equals the IEEE quotient for every finite |x| < 2^126 (exhaustive check over all
+// 2^32 inputs on gfx950: tools/probes/softsign_div.hip); for |x| >= 2^24 the IEEE
+// quotient is exactly +-1 (|x| + 1 rounds to |x|), and inf gives NaN, as IEEE.
+__device__ __forceinline__ float softsign(float x) {
+#if GO1_FAST_SOFTSIGN
+  const float ax = fabsf(x);
+  const float d = ax + 1.0f;
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float q0 = x * r;
+  const float q = fmaf(fmaf(-q0, d, x), r, q0);
+  const float big = ax == __builtin_inff() ? __builtin_nanf("") : copysignf(1.0f, x);
+  return ax >= 16777216.0f ? big : q;
+#else
+  return x / (fabsf(x) + 1.0f);
+#endif
+}
 
 // b0 = X[k = q][item], b1v = X[k = 4 + q][item] (0 for q >= 2).  Returns the torque
 // of item (lane & 15) in all four lanes of the item.  Needs all 64 lanes active.
@@ -149,9 +206,7 @@ __device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v
   for (int mo = 0; mo < 2; ++mo)
 #pragma unroll
     for (int r = 0; r < 4; ++r) p = fmaf(F.w3[mo][r], softsign(a2[mo][r]), p);
-  p = p + __shfl_xor(p, 16);
-  p = p + __shfl_xor(p, 32);
-  return p + F.b3;
+  return rowsum4(p) + F.b3;
 }
 
 // ---------------------------------------------------------------- torch-order f32 math
@@ -573,48 +628,44 @@ __device__ void foot_world(const float* __restrict__ model, const float* root, c
 }
 
 struct Phys {
-  float pos[3], quat[4], v[3], w[3];  // base (replicated in the quad)
-  float q[3], qd[3];                   // this leg's joints
+  float pos[3], quat[4], v[3], w[3];  // base (replicated on the 16 lanes of the env)
+  float q[3], qd[3];                   // this lane's leg
 };
 
-// One integrator step of length h for the env of this lane's quad.  Each lane
-// handles its leg (kinematics, contacts, ABA backward/forward pass) and two of
-// the eight trunk corners; base quantities are replicated across the quad.
-// cf_out: write this lane's reported contact forces (thigh, calf, foot of its
-// leg; the base from the quad sum).
+// sum over the 4 roles of a leg (lanes xor 4, 8), bitwise identical on every lane
+__device__ __forceinline__ float rsum(float v) {
+  v = v + __shfl_xor(v, 4);
+  v = v + __shfl_xor(v, 8);
+  return v;
+}
+
+// One integrator step of length h for the env of this lane.  Lane layout (16 per
+// env): lane = 16 env + 4 role + leg.  The four roles of a leg compute the leg's
+// kinematics and ABA passes redundantly (base quantities on all 16 lanes), and
+// split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
+// two per lane, so each wave has four envs and the whole grid fills every SIMD.
+// cf_out: this lane's reported contact forces (thigh, calf, foot of its leg; base).
 __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const float* tau, float h, const float* g,
-                             float friction, float payload, const Terr& T, int leg, bool cf_out, float* cf_leg,
-                             float* cf_base) {
+                             float friction, float payload, const Terr& T, int leg, int role, bool cf_out,
+                             float* cf_leg, float* cf_base) {
 #pragma clang fp contract(fast)
   const float* model = cfg->model;
+  MARK(phys_begin);
   const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
   float R[9];
   quat_to_R(S.quat, R);
   float vb[6];
   mat3T_vec(R, S.w, vb);
   mat3T_vec(R, S.v, vb + 3);
-  // ---- trunk corners (two per lane) -> base external force, body coords
   const float* th = model + 13 * 10 + 4 * 9 + 3 + 1;  // trunk half extents
-  float fbase[6] = {0, 0, 0, 0, 0, 0};
-  float Fb[3] = {0, 0, 0};
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int cx = leg * 2 + k;
-    float lp[3] = {(cx & 1) ? th[0] : -th[0], (cx & 2) ? th[1] : -th[1], (cx & 4) ? th[2] : -th[2]};
-    float pw[3], vw[3], F[3];
-    point_kin(R, S.pos, vb, lp, pw, vw);
-    sphere_contact(T, C, pw, vw, 0.0f, F);
-    point_force(R, lp, F, fbase);
-    Fb[0] += F[0]; Fb[1] += F[1]; Fb[2] += F[2];
-  }
-  // ---- this leg: kinematics, rigid bias forces, gravity and contacts (hip -> calf)
+  // ---- this leg: kinematics, rigid bias forces and gravity (hip -> calf)
   const float* origin = model + 13 * 10 + leg * 9;
   const float* foot = model + 13 * 10 + 4 * 9;
   const float foot_r = foot[3];
   const float thigh_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3];
   const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
   float cs[3][2], cj[3][6], pA[3][6];
-  float cfl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // thigh, calf, foot
+  float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
   {
     float Rp[9], pp[3], vp[6];
 #pragma unroll
@@ -645,46 +696,79 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
       pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];
 #pragma unroll
       for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
-      // rigid inertia about the link origin, bias force v x* I v
+      // rigid inertia about the link origin, bias force v x* I v, minus gravity
       const float* B = model + 10 * (1 + leg * 3 + j);
       SI I;
       rigid_si(B, 1.0f, I);
       float hm[6];
       si_mul(I, vj, hm);
       crf(vj, hm, pA[j]);
-      float gl[3], fext[6];
+      float gl[3];
       mat3T_vec(Rp, g, gl);
       float fg[3] = {B[0] * gl[0], B[0] * gl[1], B[0] * gl[2]}, cg[3];
       cross3(B + 1, fg, cg);
-      fext[0] = cg[0]; fext[1] = cg[1]; fext[2] = cg[2]; fext[3] = fg[0]; fext[4] = fg[1]; fext[5] = fg[2];
-      if (j == 1) {
+      pA[j][0] -= cg[0]; pA[j][1] -= cg[1]; pA[j][2] -= cg[2];
+      pA[j][3] -= fg[0]; pA[j][4] -= fg[1]; pA[j][5] -= fg[2];
+      if (j > 0) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const float lp[3] = {0.0f, 0.0f, p == 0 ? -0.071f : (p == 1 ? -0.142f : -0.213f)};
-          float pw[3], vw[3], F[3];
-          point_kin(Rp, pp, vj, lp, pw, vw);
-          sphere_contact(T, C, pw, vw, thigh_r, F);
-          point_force(Rp, lp, F, fext);
-          cfl[0] += F[0]; cfl[1] += F[1]; cfl[2] += F[2];
-        }
-      } else if (j == 2) {
+        for (int i = 0; i < 9; ++i) Rl[j - 1][i] = Rp[i];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          float lp[3], rr;
-          if (p < 2) { lp[0] = 0.0f; lp[1] = 0.0f; lp[2] = p == 0 ? -0.071f : -0.142f; rr = calf_r; }
-          else { lp[0] = foot[0]; lp[1] = foot[1]; lp[2] = foot[2]; rr = foot_r; }
-          float pw[3], vw[3], F[3];
-          point_kin(Rp, pp, vj, lp, pw, vw);
-          sphere_contact(T, C, pw, vw, rr, F);
-          point_force(Rp, lp, F, fext);
-          const int slot = p < 2 ? 3 : 6;
-          cfl[slot] += F[0]; cfl[slot + 1] += F[1]; cfl[slot + 2] += F[2];
-        }
+        for (int i = 0; i < 3; ++i) pl[j - 1][i] = pp[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) vl[j - 1][i] = vj[i];
       }
 #pragma unroll
-      for (int i = 0; i < 6; ++i) { pA[j][i] -= fext[i]; vp[i] = vj[i]; }
+      for (int i = 0; i < 6; ++i) vp[i] = vj[i];
     }
   }
+  MARK(leg_kin_done);
+  // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
+  //      corner 2 leg, corner 2 leg + 1]; forces in the body frame of the point's body
+  float fth[6] = {0, 0, 0, 0, 0, 0}, fca[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
+  float Fth[3] = {0, 0, 0}, Fca[3] = {0, 0, 0}, Fft[3] = {0, 0, 0}, Fb[3] = {0, 0, 0};
+#pragma unroll
+  for (int sidx = 0; sidx < 2; ++sidx) {
+    const int p = 2 * role + sidx;
+    const bool on_thigh = p < 3, on_calf = p >= 3 && p < 6, on_base = p >= 6;
+    float Rs[9], ps[3], vs[6];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rs[i] = on_thigh ? Rl[0][i] : (on_calf ? Rl[1][i] : R[i]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ps[i] = on_thigh ? pl[0][i] : (on_calf ? pl[1][i] : S.pos[i]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) vs[i] = on_thigh ? vl[0][i] : (on_calf ? vl[1][i] : vb[i]);
+    const int cx = leg * 2 + (p - 6);
+    const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
+    float lp[3];
+    lp[0] = on_base ? ((cx & 1) ? th[0] : -th[0]) : (p == 5 ? foot[0] : 0.0f);
+    lp[1] = on_base ? ((cx & 2) ? th[1] : -th[1]) : (p == 5 ? foot[1] : 0.0f);
+    lp[2] = on_base ? ((cx & 4) ? th[2] : -th[2]) : (p == 5 ? foot[2] : lz);
+    const float rr = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
+    float pw[3], vw[3], F[3], f6[6] = {0, 0, 0, 0, 0, 0};
+    point_kin(Rs, ps, vs, lp, pw, vw);
+    sphere_contact(T, C, pw, vw, rr, F);
+    point_force(Rs, lp, F, f6);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      fth[i] += on_thigh ? f6[i] : 0.0f;
+      fca[i] += on_calf ? f6[i] : 0.0f;
+      fbase[i] += on_base ? f6[i] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      Fth[i] += on_thigh ? F[i] : 0.0f;
+      Fca[i] += (p == 3 || p == 4) ? F[i] : 0.0f;
+      Fft[i] += p == 5 ? F[i] : 0.0f;
+      Fb[i] += on_base ? F[i] : 0.0f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    pA[1][i] -= rsum(fth[i]);
+    pA[2][i] -= rsum(fca[i]);
+    fbase[i] = rsum(fbase[i]);
+  }
+  MARK(leg_kin_contacts_done);
   // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
   float U[3][6], D[3], u[3];
   SI Ip;
@@ -737,6 +821,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
       }
     }
   }
+  MARK(backward_done);
   // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
   const float* bb = model;
   const float mscale = (bb[0] + payload) * frcp(bb[0]);
@@ -767,6 +852,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
 #pragma unroll
   for (int i = 0; i < 6; ++i) rhs[i] = -(p0[i] + pp6[i]);
   solve6(I0, rhs, a0);
+  MARK(base_solve_done);
   // ---- forward pass
   float qdd[3];
   {
@@ -789,6 +875,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
       for (int i = 0; i < 6; ++i) ap[i] = aj[i];
     }
   }
+  MARK(forward_done);
   // ---- semi-implicit Euler (base identical in the quad)
   float wv[3], alb[3], aw[3], al[3];
   cross3(vb, vb + 3, wv);
@@ -825,12 +912,15 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
     S.qd[j] += h * qdd[j];
     S.q[j] += h * S.qd[j];
   }
+  MARK(integrate_done);
   if (cf_out) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) cf_leg[i] = cfl[i];
-    cf_base[0] = qsum(Fb[0]);
-    cf_base[1] = qsum(Fb[1]);
-    cf_base[2] = qsum(Fb[2]);
+    for (int i = 0; i < 3; ++i) {
+      cf_leg[i] = rsum(Fth[i]);
+      cf_leg[3 + i] = rsum(Fca[i]);
+      cf_leg[6 + i] = rsum(Fft[i]);
+      cf_base[i] = qsum(rsum(Fb[i]));
+    }
   }
 }
 
@@ -899,7 +989,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int n = c->n_envs;
   const int leg = threadIdx.x & 3;
   const int lane = threadIdx.x & 63, lq = lane >> 4;
-  const int e = blockIdx.x * EPB + (threadIdx.x >> 2);  // n % EPB == 0 (go1_create): every wave is full
+  const int role = (lane >> 2) & 3, el = lane >> 4, sub16 = lane & 15;
+  const bool owner = role == 0;  // the lane of a leg that stores its per-leg outputs
+  const int e = blockIdx.x * SEPB + el;  // n % 16 == 0 (go1_create): every wave is full
   (void)n;
   MlpFrag F;
   mlp_load(c->actuator, lane, F);
@@ -923,8 +1015,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const float friction = st.friction[e], payload = st.payload[e];
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
-  __shared__ float2 s_patch[EPB][PSZ * PSZ];
-  __shared__ int s_patch_meta[EPB][3];
+  __shared__ float2 s_patch[SEPB][PSZ * PSZ];
+  __shared__ int s_patch_meta[SEPB][3];
   if (c->terrain_kind == 1) {
     const int tix = K.ter.env_tile[e];
     T.tile = K.ter.tiles + (size_t)tix * 2 * c->hf_nx * c->hf_ny;
@@ -935,17 +1027,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const float bx = st.root[(size_t)e * 13], by = st.root[(size_t)e * 13 + 1];
       T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(c->hf_nx + 64))) - PSZ / 2;
       T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(c->hf_ny + 64))) - PSZ / 2;
-      T.patch = &s_patch[threadIdx.x >> 2][0];
-      if (leg == 0) {
-        s_patch_meta[threadIdx.x >> 2][0] = tix;
-        s_patch_meta[threadIdx.x >> 2][1] = T.pi0;
-        s_patch_meta[threadIdx.x >> 2][2] = T.pj0;
+      T.patch = &s_patch[el][0];
+      if (sub16 == 0) {
+        s_patch_meta[el][0] = tix;
+        s_patch_meta[el][1] = T.pi0;
+        s_patch_meta[el][2] = T.pj0;
       }
       __syncthreads();
       const int nx = c->hf_nx, ny = c->hf_ny;
       // 2 envs x 256 cells per pass: 8 cells (16 loads) in flight per lane
 #pragma unroll 1
-      for (int el0 = 0; el0 < EPB; el0 += 2) {
+      for (int el0 = 0; el0 < SEPB; el0 += 2) {
         float2 v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -1001,30 +1093,31 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
       xin[j][3] = qd[j]; xin[j][4] = vh[0][j]; xin[j][5] = vh[1][j];
     }
-    // ... -> 12 MFMA groups per wave: group (joint j, lane row qq) holds the items of
-    // envs 4qq..4qq+3 x legs, whose owner lanes are 16 qq + (lane & 15).
+    // ... -> 3 MFMA groups per wave: group j holds joint j of the 16 (env, leg) items of
+    // the wave, item i = 4 env + leg (owner lane 16 env + leg); the torque of item i
+    // comes back from lane i.
+    MARK(mlp_begin);
     float tq[3] = {0.0f, 0.0f, 0.0f};
+    const int src = 16 * (sub16 >> 2) + (sub16 & 3);
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < 3; ++j) {
+      float y[6];
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int src = 16 * qq + (lane & 15);
-        float y[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) y[k] = __shfl(xin[j][k], src);
-        const float b0 = lq == 0 ? y[0] : (lq == 1 ? y[1] : (lq == 2 ? y[2] : y[3]));
-        const float b1v = lq == 0 ? y[4] : (lq == 1 ? y[5] : 0.0f);
+      for (int k = 0; k < 6; ++k) y[k] = __shfl(xin[j][k], src);
+      const float b0 = lq == 0 ? y[0] : (lq == 1 ? y[1] : (lq == 2 ? y[2] : y[3]));
+      const float b1v = lq == 0 ? y[4] : (lq == 1 ? y[5] : 0.0f);
 #ifdef GO1_ABL_NO_MLP
-        const float t = 0.0f * (b0 + b1v);  // ablation build only: no actuator net
+      const float t = 0.0f * (b0 + b1v);  // ablation build only: no actuator net
 #else
-        const float t = mlp_group(F, b0, b1v);
+      const float t = mlp_group(F, b0, b1v);
 #endif
-        if (lq == qq) tq[j] = t;
-      }
+      tq[j] = __shfl(t, 4 * el + leg);
+    }
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
     for (int j = 0; j < 3; ++j) tq[j] += -20.0f * xin[j][0] - 0.5f * xin[j][3];  // PD stand-in
 #endif
+    MARK(mlp_done);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int d = leg * 3 + j;
@@ -1035,7 +1128,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const float t = tq[j] * strength[j];
       const float lim = c->torque_limits[d];
       torque[j] = clampf(t, -lim, lim);
-      if (A.dbg_torques) A.dbg_torques[((size_t)sub * n + e) * NDOF + d] = torque[j];
+      if (A.dbg_torques && owner) A.dbg_torques[((size_t)sub * n + e) * NDOF + d] = torque[j];
     }
     if (INJ) {
       const float* id = A.inj_dof + ((size_t)sub * n + e) * NDOF * 2;
@@ -1051,7 +1144,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
 #ifndef GO1_ABL_NO_PHYS
-        phys_substep(c, P, torque, h, A.sim_gravity, friction, payload, T, leg, last, cf_leg, cf_base);
+        phys_substep(c, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_leg, cf_base);
 #else
         (void)last; (void)h;
         P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];
@@ -1080,7 +1173,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 4; ++i) root[3 + i] = P.quat[i];
   }
-  if (A.contact_forces) {
+  if (A.contact_forces && owner) {
     float* o = A.contact_forces + (size_t)e * NB * 3;
     if (leg == 0) { o[0] = cf_base[0]; o[1] = cf_base[1]; o[2] = cf_base[2]; }
     float* ol = o + (1 + leg * 4) * 3;
@@ -1089,6 +1182,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int i = 0; i < 9; ++i) ol[3 + i] = cf_leg[i];
   }
 
+  MARK(post_begin);
   // ================= post_physics_step (:114-169), contraction off =================
   const int ep = st.episode_length[e] + 1;
   float blv[3], bav[3], pg[3], rpy[3], rel_lin[3], rel_rot[3];
@@ -1108,6 +1202,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
   float cmd[2] = {rel_lin[0], rel_lin[1]};
 
+  MARK(post_kin_done);
   // DR every rand_interval (:822-824)
   if (ep % c->rand_interval == 0) {
     const float sv = rng(34) * c->strength_range + c->strength_lo;
@@ -1144,6 +1239,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (!finite) reset = true;
   }
 
+  MARK(termination_done);
   // rewards (:320-355, reward_crawling.py)
   float terms[GO1_NUM_TERMS];
   {
@@ -1205,17 +1301,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   sums[10] = sums[10] + rew;
   sums[11] = sums[11] + pos;
   sums[12] = sums[12] + neg;
-  if (A.dbg_terms && leg == 0)
+  if (A.dbg_terms && owner && leg == 0)
 #pragma unroll
     for (int k = 0; k < GO1_NUM_TERMS; ++k) A.dbg_terms[(size_t)e * GO1_NUM_TERMS + k] = terms[k];
 
+  MARK(rewards_done);
   // ---- reset_idx (:218-296); the height scan below still samples at the pre-reset pose
   const float scan_x = root[0], scan_y = root[1];
   float traj_new[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) traj_new[i] = st.trajectory[(size_t)e * 6 + i];
-  if (A.episode_log && leg == 0 && !reset) A.episode_log[(size_t)e * GO1_EPISODE_LOG + 13] = 0.0f;
-  if (reset && A.episode_log && leg == 0) {
+  if (A.episode_log && owner && leg == 0 && !reset) A.episode_log[(size_t)e * GO1_EPISODE_LOG + 13] = 0.0f;
+  if (reset && A.episode_log && owner && leg == 0) {
     // reset_idx logging (:256-271): pre-reset sums, episode length, reached, goal distance
     float* lg = A.episode_log + (size_t)e * GO1_EPISODE_LOG;
 #pragma unroll
@@ -1234,6 +1331,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const int coll_count = reset ? 0 : st.collision_count[e] + (int)coll;
 
+  MARK(reset_done);
   // ---- compute_observations (:357-475)
   float* o = A.obs + (size_t)e * GO1_NUM_OBS;
   const float clip = c->clip_obs;
@@ -1241,20 +1339,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (noisy && c->add_noise) v = v + (2.0f * rng(47 + i) - 1.0f) * nv;
     o[i] = clampf(v, -clip, clip);
   };
-  if (leg == 0) {
+  // role r < 3 writes joint r of its leg; role 3 of leg 0 writes gravity and commands
+  if (role == 3 && leg == 0) {
     put(0, pg[0], c->noise_gravity, true);
     put(1, pg[1], c->noise_gravity, true);
     put(2, pg[2], c->noise_gravity, true);
     put(3, cmd[0] * 1.0f, 0.0f, false);
     put(4, cmd[1] * 1.0f, 0.0f, false);
   }
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int d = leg * 3 + j;
-    put(5 + d, (q[j] - c->default_dof_pos[d]) * c->obs_scale_dof_pos, c->noise_dof_pos, true);
-    put(17 + d, qd[j] * c->obs_scale_dof_vel, c->noise_dof_vel, true);
-    put(29 + d, act[j], 0.0f, false);
+  if (role < 3) {
+    const int j = role, d = leg * 3 + role;
+    const float qj = j == 0 ? q[0] : (j == 1 ? q[1] : q[2]);
+    const float qdj = j == 0 ? qd[0] : (j == 1 ? qd[1] : qd[2]);
+    const float aj = j == 0 ? act[0] : (j == 1 ? act[1] : act[2]);
+    put(5 + d, (qj - c->default_dof_pos[d]) * c->obs_scale_dof_pos, c->noise_dof_pos, true);
+    put(17 + d, qdj * c->obs_scale_dof_vel, c->noise_dof_vel, true);
+    put(29 + d, aj, 0.0f, false);
   }
+  MARK(obs_props_done);
   // height scan (:1918-1965) fused with the height observations (:395-411)
   {
     const bool plane = c->terrain_kind == 0;
@@ -1285,17 +1387,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
     const float zroot = root[2];  // post-reset (:401)
     const float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
-    // 28 points per lane (n_pts <= 112 for the front half): indices first, then all
-    // loads in flight together, then the observation arithmetic
-    float hv[28][2];
+    // the env's 16 lanes take points sub16 + 16 k (n_pts <= 112 for the front half):
+    // indices first, then all loads in flight together, then the observation arithmetic
+    constexpr int KPTS = 7;
+    float hv[KPTS][2];
 #pragma unroll
-    for (int k = 0; k < 28; ++k) {
-      const int p = min(leg + 4 * k, n_pts - 1);
+    for (int k = 0; k < KPTS; ++k) {
+      const int p = min(sub16 + 16 * k, n_pts - 1);
       sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[k][0], hv[k][1]);
     }
 #pragma unroll
-    for (int k = 0; k < 28; ++k) {
-      const int p = leg + 4 * k;
+    for (int k = 0; k < KPTS; ++k) {
+      const int p = sub16 + 16 * k;
       if (p < n_pts) {
 #pragma unroll
         for (int layer = 0; layer < 2; ++layer) {
@@ -1313,9 +1416,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
     }
+    MARK(heights_done);
     if (A.dbg_heights) {
       float* od = A.dbg_heights + (size_t)e * 2 * GO1_GRID_X * GO1_GRID_Y;
-      for (int p = leg; p < GO1_GRID_X * GO1_GRID_Y; p += 4) {
+      for (int p = sub16; p < GO1_GRID_X * GO1_GRID_Y; p += 16) {
         float h0, h1;
         sample(p / GO1_GRID_Y, p % GO1_GRID_Y, h0, h1);
         od[p] = h0;
@@ -1323,53 +1427,60 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
   }
-  if (leg == 0) {
+  if (sub16 == 0) {
     float* pv = A.priv + (size_t)e * GO1_NUM_PRIV;
     pv[0] = clampf((friction - c->priv_friction_shift) * c->priv_friction_scale, -clip, clip);
     pv[1] = clampf((st.restitution[e] - c->priv_rest_shift) * c->priv_rest_scale, -clip, clip);
   }
 
+  MARK(priv_done);
   if (A.aux) {
     // TrajectoryTrackingEnv.step extras (trajectory_tracking/__init__.py:25-41), post-reset state
     float* ax = A.aux + (size_t)e * GO1_AUX;
-    if (leg == 0) {
+    if (role == 2 && leg == 0) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) { ax[i] = blv[i]; ax[3 + i] = bav[i]; }
       ax[6] = cmd[0];
       ax[7] = cmd[1];
     }
-    float fp[3];
-    foot_world(c->model, root, q, leg, fp);
+    if (role == 1) {
+      float fp[3];
+      foot_world(c->model, root, q, leg, fp);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { ax[8 + leg * 3 + i] = fp[i]; ax[20 + leg * 3 + i] = torque[i]; }
+      for (int i = 0; i < 3; ++i) ax[8 + leg * 3 + i] = fp[i];
+    }
+    if (owner)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ax[20 + leg * 3 + i] = torque[i];
   }
 
-  // ---------------- write back (epilogue :148-153)
-  float lag_out[GO1_LAG_SLOTS][3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
+  MARK(aux_done);
+  // ---------------- write back (epilogue :148-153): role r < 3 stores joint r of its
+  // leg, role 3 of leg 0 stores the env-level state
+  if (role < 3) {
+    const int j = role;
+    auto pick = [&](const float* v3) { return j == 0 ? v3[0] : (j == 1 ? v3[1] : v3[2]); };
+    const size_t dj = d0 + j;
+    st.dof_pos[dj] = pick(q);
+    st.dof_vel[dj] = pick(qd);
+    st.last_actions[dj] = pick(act);
+    st.last_dof_vel[dj] = pick(qd);
+    st.motor_strength[dj] = pick(strength);
+    st.motor_offset[dj] = pick(offset);
+    st.joint_pos_target[dj] = pick(tgt);
+    const float sj = pick(scaled);
 #pragma unroll
     for (int s2 = 0; s2 < GO1_LAG_SLOTS; ++s2) {
       const int src = s2 + dec;  // slot after `dec` pushes
-      lag_out[s2][j] = reset ? 0.0f : (src < GO1_LAG_SLOTS ? lag_in[src * 12 + j] : scaled[j]);
+      const float v = reset ? 0.0f : (src < GO1_LAG_SLOTS ? lag_in[src * 12 + j] : sj);
+      st.lag[(size_t)e * 84 + s2 * 12 + leg * 3 + j] = v;
     }
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    st.dof_pos[d0 + j] = q[j];
-    st.dof_vel[d0 + j] = qd[j];
-    st.last_actions[d0 + j] = act[j];
-    st.last_dof_vel[d0 + j] = qd[j];
-    st.motor_strength[d0 + j] = strength[j];
-    st.motor_offset[d0 + j] = offset[j];
-    st.joint_pos_target[d0 + j] = tgt[j];
-#pragma unroll
-    for (int s2 = 0; s2 < GO1_LAG_SLOTS; ++s2) st.lag[(size_t)e * 84 + s2 * 12 + leg * 3 + j] = lag_out[s2][j];
-    st.pos_err_hist[(size_t)e * 24 + leg * 3 + j] = eh[0][j];
-    st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j] = eh[1][j];
-    st.vel_hist[(size_t)e * 24 + leg * 3 + j] = vh[0][j];
-    st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j] = vh[1][j];
+    st.pos_err_hist[(size_t)e * 24 + leg * 3 + j] = pick(eh[0]);
+    st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j] = pick(eh[1]);
+    st.vel_hist[(size_t)e * 24 + leg * 3 + j] = pick(vh[0]);
+    st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j] = pick(vh[1]);
   }
-  if (leg == 0) {
+  if (role == 3 && leg == 0) {
 #pragma unroll
     for (int i = 0; i < 13; ++i) st.root[(size_t)e * 13 + i] = root[i];
 #pragma unroll
@@ -1559,7 +1670,7 @@ int go1_step(go1_handle* h, const go1_step_args* a, void* stream) {
   K.ter = h->ter;
   K.a = *a;
   K.any_reset = flag;
-  dim3 grid((n + EPB - 1) / EPB), block(TPB);
+  dim3 grid(n / SEPB), block(TPB);
   if (a->ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_begin, s));
   if (inj) hipLaunchKernelGGL(go1_step_kernel<true>, grid, block, 0, s, h->d_cfg, K);
   else hipLaunchKernelGGL(go1_step_kernel<false>, grid, block, 0, s, h->d_cfg, K);

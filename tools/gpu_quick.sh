@@ -1,0 +1,11 @@
+#!/bin/bash
+# Quick GPU iteration: parity tests, then the bench without the CPU / rollout legs.
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python bench.py --steps 500 --warmup 50 --no-cpu-baseline --no-rollout > gpurun_out/bench_quick.log 2>&1 || exit $?
+python -c "import json; d=json.loads(open('gpurun_out/bench_quick.log').read().strip().splitlines()[-1]); print('value', round(d['value']/1e6,2), 'M env-steps/s; ms/step', round(d['ms_per_step'],4), 'kernel ms', round(d['roofline']['kernel_ms'],4))"
+for x in "$@"; do echo "== $x"; timeout -k 10 120 $x || exit $?; done

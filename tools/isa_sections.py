@@ -1,0 +1,50 @@
+"""Static instruction counts between MARK() section markers of the step kernel.
+
+  python tools/isa_sections.py   (compiles go1_step.hip with -DGO1_ISA_MARKS into /tmp)
+
+Straight-line sections inside the sub-step loop run decimation x n_internal
+times per step, so static counts x trip counts ~ the dynamic SQ_INSTS_VALU."""
+import os
+import re
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = "/tmp/go1_isa"
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    src = os.path.join(REPO, "legged_tracking_amd", "csrc", "go1_step.hip")
+    extra = sys.argv[1:]
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "-DGO1_ISA_MARKS", *extra, "-c", "--save-temps", "-o", os.path.join(OUT, "k.o"), src],
+                   cwd=OUT, check=True)
+    s = open(os.path.join(OUT, "go1_step-hip-amdgcn-amd-amdhsa-gfx950.s")).read().splitlines()
+    start = next(i for i, l in enumerate(s) if l.startswith("_Z15go1_step_kernelILb0EE"))
+    end = next(i for i in range(start, len(s)) if s[i].startswith(".Lfunc_end"))
+    cur, counts = "prologue", {}
+    for l in s[start:end]:
+        m = re.search(r"; MARK (\w+)", l)
+        if m:
+            cur = m.group(1)
+            continue
+        t = l.strip()
+        c = counts.setdefault(cur, [0, 0, 0, 0, 0])
+        if t.startswith("v_"):
+            c[0] += 1
+            if "mfma" in t:
+                c[1] += 1
+        elif t.startswith(("global_", "buffer_")):
+            c[2] += 1
+        elif t.startswith("ds_"):
+            c[3] += 1
+        elif t.startswith("s_"):
+            c[4] += 1
+    print(f"{'section (code after marker)':32s} {'VALU':>6s} {'MFMA':>5s} {'VMEM':>5s} {'LDS':>5s} {'SALU':>5s}")
+    for k, (v, mf, vm, ld, sa) in counts.items():
+        print(f"{k:32s} {v:6d} {mf:5d} {vm:5d} {ld:5d} {sa:5d}")
+
+
+if __name__ == "__main__":
+    main()
