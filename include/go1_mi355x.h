@@ -170,7 +170,7 @@ typedef struct go1_step_args {
   uint8_t* reset;              /* (n_envs) bool */
   uint8_t* time_out;           /* (n_envs) bool */
   uint8_t* extras_time_outs;   /* (n_envs) bool, rebound only on steps with a reset (:289-291) */
-  int32_t* any_reset;          /* 1 int, scratch, zeroed by the library */
+  int32_t* any_reset;          /* reserved (the library keeps its own flag words) */
   float* contact_forces;       /* (n_envs, 17, 3) or NULL */
   /* optional debug outputs (NULL = not written) */
   float* dbg_torques;          /* (decimation, n_envs, 12) */
