@@ -632,15 +632,11 @@ struct Phys {
   float q[3], qd[3];                   // this lane's leg
 };
 
-// sum over the 4 roles of a leg (lanes xor 4, 8), bitwise identical on every lane
-__device__ __forceinline__ float rsum(float v) {
-  v = v + __shfl_xor(v, 4);
-  v = v + __shfl_xor(v, 8);
-  return v;
-}
+// sum over the 4 roles of a leg (the four 16-lane rows), bitwise identical on every lane
+__device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 
 // One integrator step of length h for the env of this lane.  Lane layout (16 per
-// env): lane = 16 env + 4 role + leg.  The four roles of a leg compute the leg's
+// env): lane = 16 role + 4 env + leg.  The four roles of a leg compute the leg's
 // kinematics and ABA passes redundantly (base quantities on all 16 lanes), and
 // split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
 // two per lane, so each wave has four envs and the whole grid fills every SIMD.
@@ -989,7 +985,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int n = c->n_envs;
   const int leg = threadIdx.x & 3;
   const int lane = threadIdx.x & 63, lq = lane >> 4;
-  const int role = (lane >> 2) & 3, el = lane >> 4, sub16 = lane & 15;
+  // lane = 16 role + 4 env + leg: the four roles of an (env, leg) form one column of
+  // the 16 x 4 MFMA B operand, so the actuator-net inputs and outputs never move
+  const int role = lane >> 4, el = (lane >> 2) & 3, sub16 = 4 * role + leg;
   const bool owner = role == 0;  // the lane of a leg that stores its per-leg outputs
   const int e = blockIdx.x * SEPB + el;  // n % 16 == 0 (go1_create): every wave is full
   (void)n;
@@ -1093,17 +1091,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
       xin[j][3] = qd[j]; xin[j][4] = vh[0][j]; xin[j][5] = vh[1][j];
     }
-    // ... -> 3 MFMA groups per wave: group j holds joint j of the 16 (env, leg) items of
-    // the wave, item i = 4 env + leg (owner lane 16 env + leg); the torque of item i
-    // comes back from lane i.
+    // ... -> 3 MFMA groups per wave: group j holds joint j of the 16 (env, leg) items
+    // of the wave in column 4 env + leg; row (= role) q supplies inputs q and 4 + q of
+    // its own leg and receives the item's torque in place.
     MARK(mlp_begin);
     float tq[3] = {0.0f, 0.0f, 0.0f};
-    const int src = 16 * (sub16 >> 2) + (sub16 & 3);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      float y[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) y[k] = __shfl(xin[j][k], src);
+      const float* y = xin[j];
       const float b0 = lq == 0 ? y[0] : (lq == 1 ? y[1] : (lq == 2 ? y[2] : y[3]));
       const float b1v = lq == 0 ? y[4] : (lq == 1 ? y[5] : 0.0f);
 #ifdef GO1_ABL_NO_MLP
@@ -1111,7 +1106,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #else
       const float t = mlp_group(F, b0, b1v);
 #endif
-      tq[j] = __shfl(t, 4 * el + leg);
+      tq[j] = t;
     }
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
