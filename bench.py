@@ -52,14 +52,17 @@ TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01", "step_counters.json")
 
 
 def pmc_traffic(n_envs):
+    """(HBM bytes per launch, VALU issue fraction, source) from the committed PMC summary."""
     try:
         with open(TRAFFIC_FILE) as f:
             d = json.load(f)
-        if int(d["resources"]["Grid_Size"]) != 4 * n_envs:
-            return None, None
-        return d["hbm_bytes_per_launch"]["traffic"], os.path.relpath(TRAFFIC_FILE, REPO)
-    except (OSError, KeyError, ValueError):
-        return None, None
+        if int(d["resources"]["Grid_Size"]) != 16 * n_envs:  # 16 lanes per env
+            return None, None, None
+        pw = d.get("per_wave", {})
+        valu = pw["SQ_ACTIVE_INST_VALU"] / pw["SQ_WAVE_CYCLES"] if "SQ_ACTIVE_INST_VALU" in pw else None
+        return d["hbm_bytes_per_launch"]["traffic"], valu, os.path.relpath(TRAFFIC_FILE, REPO)
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None, None, None
 
 
 def hip():
@@ -236,7 +239,7 @@ def main():
         value = n_global * args.steps / elapsed
         achieved_gbs = BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
         achieved_tf = FLOPS_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic(n)
+        traffic, valu_frac, traffic_src = pmc_traffic(n)
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -250,7 +253,9 @@ def main():
                          "traffic_source": traffic_src, "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * n,
                          "kernel": "go1_step_kernel<false>", "kernel_ms": kernel_ms,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP,
-                         "fp32_tflops_actuator_only": achieved_tf, "fp32_frac_actuator_only": achieved_tf / FP32_PEAK_TFLOPS},
+                         "fp32_tflops_actuator_only": achieved_tf, "fp32_frac_actuator_only": achieved_tf / FP32_PEAK_TFLOPS,
+                         "valu_issue_frac_pmc": valu_frac,
+                         "note": "latency/VALU-issue bound, not HBM bound: see DESIGN.md section 5"},
         }
         if not args.no_rollout:
             line["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24))

@@ -418,30 +418,26 @@ __device__ __forceinline__ void xform_inertia(int ax, float cq, float sq, const 
   M[0] = In.c[0]; M[1] = In.c[1]; M[2] = In.c[2]; M[3] = In.c[1]; M[4] = In.c[3]; M[5] = In.c[4];
   M[6] = In.c[2]; M[7] = In.c[4]; M[8] = In.c[5];
   rot_congruence(ax, cq, sq, M, C);
-  const float rx[9] = {0.0f, -r[2], r[1], r[2], 0.0f, -r[0], -r[1], r[0], 0.0f};
-  float RC[9], RBt[9], BR[9];
+  // translation, with (M r~) row i = (row i of M) x r and r~ B'^T = -(B' r~)^T
+  float RC[9], BR[9], RCR[9];
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+  for (int j = 0; j < 3; ++j) {  // r~ C': column j = r x C'[:, j]
+    const float col[3] = {C[j], C[3 + j], C[6 + j]};
+    float t[3];
+    cross3(r, col, t);
+    RC[j] = t[0]; RC[3 + j] = t[1]; RC[6 + j] = t[2];
+  }
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float s0 = 0.0f, t0 = 0.0f, u0 = 0.0f;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        s0 += rx[i * 3 + k] * C[k * 3 + j];
-        t0 += rx[i * 3 + k] * B[j * 3 + k];
-        u0 += B[i * 3 + k] * rx[k * 3 + j];
-      }
-      RC[i * 3 + j] = s0;
-      RBt[i * 3 + j] = t0;
-      BR[i * 3 + j] = u0;
-    }
-  // upper triangle of A'' only (symmetric)
+  for (int i = 0; i < 3; ++i) {
+    cross3(B + 3 * i, r, BR + 3 * i);    // B' r~
+    cross3(RC + 3 * i, r, RCR + 3 * i);  // r~ C' r~
+  }
+  // upper triangle of A'' = A' - BR^T - BR - RCR (symmetric)
   const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
   for (int t = 0; t < 6; ++t) {
     const int i = II[t], j = JJ[t];
-    float rcr = RC[i * 3 + 0] * rx[0 * 3 + j] + RC[i * 3 + 1] * rx[1 * 3 + j] + RC[i * 3 + 2] * rx[2 * 3 + j];
-    Out.a[t] = A[i * 3 + j] + RBt[i * 3 + j] - BR[i * 3 + j] - rcr;
+    Out.a[t] = A[i * 3 + j] - BR[j * 3 + i] - BR[i * 3 + j] - RCR[i * 3 + j];
     Out.c[t] = C[i * 3 + j];
   }
 #pragma unroll

@@ -34,25 +34,25 @@ def kernel_stats(src):
 
 
 def counters(src, match="go1_step_kernel"):
-    acc = defaultdict(list)
-    for f in glob.glob(os.path.join(src, "*", "*counter_collection.csv")):
-        with open(f) as fh:
-            for row in csv.DictReader(fh):
-                if match in row["Kernel_Name"]:
-                    acc[(row["Dispatch_Id"], row["Counter_Name"])].append(float(row["Counter_Value"]))
+    """Per-dispatch means of every counter: instances (XCD / SE) of one dispatch are
+    summed, then averaged over dispatches; a counter collected in several passes is
+    averaged over the passes."""
     per = defaultdict(list)
     meta = {}
-    for (disp, name), vals in acc.items():
-        per[name].append(sum(vals))  # sum over XCD / SE instances of one dispatch
-    for f in glob.glob(os.path.join(src, "*", "*counter_collection.csv")):
+    for f in sorted(glob.glob(os.path.join(src, "*", "*counter_collection.csv"))):
+        acc = defaultdict(float)
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if match in row["Kernel_Name"]:
-                    meta = {k: row[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
-                                                "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count")}
-                    break
-        if meta:
-            break
+                    acc[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
+                    if not meta:
+                        meta = {k: row[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                                    "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count")}
+        by_name = defaultdict(list)
+        for (disp, name), v in acc.items():
+            by_name[name].append(v)
+        for name, vals in by_name.items():
+            per[name].append(sum(vals) / len(vals))
     return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}, meta
 
 
@@ -67,7 +67,8 @@ def main():
             w.writeheader()
             w.writerows(rows)
     means, counts, meta = counters(src)
-    out = {"kernel": "go1_step_kernel<false>", "dispatches": counts, "per_dispatch_mean": means, "resources": meta}
+    out = {"kernel": "go1_step_kernel<false>", "passes_per_counter": counts, "per_dispatch_mean": means,
+           "resources": meta}
     if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
         fetch = means["FETCH_SIZE"] * 1024
         write = means["WRITE_SIZE"] * 1024

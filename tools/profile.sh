@@ -6,7 +6,7 @@ TAG=${1:-r01}
 OUT="$ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="$ROOT/bench.py --steps 100 --warmup 10 --no-cpu-baseline"
+B="$ROOT/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-rollout"
 set -o pipefail
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- python3 $B > "$OUT/trace.log" 2>&1 || { echo "trace rc=$?"; exit 1; }
 echo trace ok
@@ -16,5 +16,6 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write"
 echo write ok
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sq" -o sq -- python3 $B > "$OUT/sq.log" 2>&1 || { echo "sq rc=$?"; tail -20 "$OUT/sq.log"; }
 echo sq done
-timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1; echo list rc=$?
+timeout -k 10 300 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY --output-format csv -d "$OUT/sq2" -o sq2 -- python3 $B > "$OUT/sq2.log" 2>&1 || { echo "sq2 rc=$?"; tail -20 "$OUT/sq2.log"; }
+echo sq2 done
 find "$OUT" -name "*.csv" | head -20
