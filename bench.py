@@ -113,7 +113,7 @@ def cpu_baseline(n_envs, budget_s=12.0, max_steps=400):
                       f"{dt:.1f} s on {threads} threads of {cores} visible ({model})"}
 
 
-def rollout_rate(n, dev, steps, warmup):
+def rollout_rate(n, dev, steps, warmup, prof=None):
     """Secondary line (SURVEY 8(d) "report both env-only and rollout (act + step) rates"):
     the Runner's rollout loop -- ActorCritic.act + value (hipBLASLt GEMMs), env.step
     through TrajectoryTrackingEnv/HistoryWrapper, transition record kernel -- at n envs."""
@@ -142,14 +142,19 @@ def rollout_rate(n, dev, steps, warmup):
         for _ in range(warmup):
             one()
         torch.cuda.synchronize()
+        if prof is not None:
+            prof.enable()
         t0 = time.perf_counter()
         for _ in range(steps):
             one()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if prof is not None:
+            prof.disable()
     return {"value": n * steps / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
-            "what": "PPO.act (policy+value GEMMs, Normal sample) + TrajectoryTrackingEnv.step + HistoryWrapper + "
-                    "process_env_step record kernel, 1 GPU"}
+            "what": "PPO.act (fused MFMA adaptation+actor+critic kernel, Normal sample) + TrajectoryTrackingEnv.step "
+                    "+ HistoryWrapper + process_env_step record kernel, 1 GPU",
+            "fused_policy": alg.fused is not None}
 
 
 def main():
@@ -161,9 +166,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rollout", action="store_true")
+    ap.add_argument("--rollout-only", action="store_true", help="profile helper: time only the rollout loop")
     args = ap.parse_args()
 
     import torch
+    if args.rollout_only:
+        print(json.dumps(rollout_rate(args.envs_per_gpu, torch.device("cuda", 0), args.steps, args.warmup)))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

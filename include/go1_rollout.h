@@ -44,7 +44,35 @@ typedef struct go1_transition {
   int32_t num_obs, num_priv, num_obs_history, num_actions;
 } go1_transition;
 
+/* Fused policy inference (ActorCritic.act / evaluate, actor_critic.py:121-150) for the
+ * default AC_Args architecture: adaptation 261 -> 256 -> 128 -> 2, actor
+ * [hist, latent] -> 512 -> 256 -> 128 -> num_actions, critic [hist, priv] -> 512 -> 256
+ * -> 128 -> 1, ELU.  Weights packed by legged_tracking_amd/rollout.py (fragment order,
+ * layers: a1 a2 a3 p1 p2 p3 p4 c1 c2 c3 c4). */
+#define GO1_POLICY_LAYERS 11
+typedef struct go1_policy_layer {
+  const float* w; /* [n/16][k/4][64], n and k padded to 16 / 4 */
+  const float* b; /* [n padded to 16] */
+} go1_policy_layer;
+typedef struct go1_policy_args {
+  const float* obs_history;    /* (n, hist_dim) */
+  const float* privileged_obs; /* (n, 2) */
+  float* action_mean;          /* (n, num_actions) */
+  float* value;                /* (n) */
+  float* latent;               /* (n, 2) or NULL */
+  /* optional in-kernel Normal(mean, std).sample() + log_prob (NULL actions = skip) */
+  const float* std;            /* (num_actions) */
+  float* actions;              /* (n, num_actions) */
+  float* action_sigma;         /* (n, num_actions) */
+  float* log_prob;             /* (n) */
+  uint64_t rng_seed, rng_step; /* Philox key / counter, one counter value per call */
+  int32_t env_id_offset;       /* global id of row 0 (rank * n) */
+  int32_t n_envs, hist_dim, num_actions;
+  go1_policy_layer layers[GO1_POLICY_LAYERS];
+} go1_policy_args;
+
 const char* go1_rollout_last_error(void);
+int go1_policy_forward(const go1_policy_args* args, void* stream);
 int go1_record_transition(const go1_transition* tr, int32_t n_envs, float gamma, void* stream);
 /* rewards/values/returns/advantages: (T, n) f32; dones (T, n) u8; last_values (n);
  * stats: 2 f64 (sum, sum of squares of the raw advantages), overwritten. */

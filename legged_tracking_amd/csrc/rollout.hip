@@ -20,6 +20,23 @@
 
 namespace {
 
+typedef float f4_t __attribute__((ext_vector_type(4)));
+
+// Philox4x32-10 (Salmon et al. 2011), as in the env step kernel
+__device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& m) {
@@ -130,6 +147,205 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
   }
 }
 
+// ------------------------------------------------------------------ policy inference
+// ActorCritic.act / evaluate (actor_critic.py:121-150) for 16 envs per workgroup of 4
+// waves, every layer on v_mfma_f32_16x16x4_f32 with weights as the A operand
+// (16 output features x 4 k) and activations as B (4 k x 16 envs):
+//   adaptation: hist(261) -> 256 -> 128 -> 2 (latent)
+//   actor:      [hist, latent](263) -> 512 -> 256 -> 128 -> 12 (action mean)
+//   critic:     [hist, priv](263)   -> 512 -> 256 -> 128 -> 1  (value)
+// ELU between layers.  Activations stay in LDS as [feature][env] (B-fragment reads are
+// conflict-free rows of 16 floats); weights are pre-packed on the host into fragment
+// order (one coalesced 256 B load per MFMA, L2-resident: 2.8 MB for all three nets).
+constexpr int PIN = 272;  // 261 / 263 inputs padded to a multiple of 16
+
+typedef go1_policy_layer PolicyLayer;  // w packed [n/16][k/4][64], b [n padded to 16]
+
+__device__ __forceinline__ float elu(float x) { return x > 0.0f ? x : expm1f(x); }
+
+// NT output tiles (tile indices tile0 + i * tstride) of one layer for the 16 envs:
+// acc = b + W x, then ELU (act) and store to dst[feature][env].  Weights are packed
+// [tile][k/16][lane][4]: one 16-byte load per lane feeds four K-steps of one tile, and
+// the next group's loads are issued before the current group's MFMAs (double buffer).
+template <int NT, int NL>
+__device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const float (*const* src)[16], int tile0,
+                                             int tstride, float (*const* dst)[16], bool act, int lane) {
+  // NL layers (the actor and the critic at the same depth) advance together: 2 x NT
+  // independent accumulators keep the MFMA pipe busy while the next weights load
+  const int q = lane >> 4, c = lane & 15;
+  const int G = S >> 2;  // groups of four K-steps (K padded to a multiple of 16)
+  f4_t acc[NL][NT], wa[NL][NT], wb[NL][NT];
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const int t = tile0 + i * tstride;
+      acc[l][i] = *reinterpret_cast<const f4_t*>(L[l].b + 16 * t + 4 * q);
+      wa[l][i] = reinterpret_cast<const f4_t*>(L[l].w)[((size_t)t * G + 0) * 64 + lane];
+    }
+  for (int g = 0; g < G; ++g) {
+    if (g + 1 < G) {
+#pragma unroll
+      for (int l = 0; l < NL; ++l)
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+          wb[l][i] = reinterpret_cast<const f4_t*>(L[l].w)[((size_t)(tile0 + i * tstride) * G + g + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      float bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bv[u] = src[l][16 * g + 4 * u + q][c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+          acc[l][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[l][i][u], bv[u], acc[l][i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) wa[l][i] = wb[l][i];
+  }
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const int t = tile0 + i * tstride;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[l][16 * t + 4 * q + r][c] = act ? elu(acc[l][i][r]) : acc[l][i][r];
+    }
+}
+
+__global__ __launch_bounds__(256) void policy_kernel(go1_policy_args P) {
+  __shared__ float xa[PIN][16], xc[PIN][16];  // actor / critic inputs (adaptation uses xa)
+  __shared__ float h1[2][512][16];             // layer-1 outputs (actor, critic); layer 3 reuses it
+  __shared__ float h2[2][256][16];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int e0 = blockIdx.x * 16;
+  const int ne = min(16, P.n_envs - e0);
+  for (int idx = tid; idx < 16 * PIN; idx += 256) {
+    const int e = idx / PIN, k = idx - e * PIN;
+    float v = 0.0f;
+    if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
+    xa[k][e] = v;
+    xc[k][e] = (e < ne && k >= P.hist_dim && k < P.hist_dim + 2) ? P.privileged_obs[(size_t)(e0 + e) * 2 + (k - P.hist_dim)] : v;
+  }
+  __syncthreads();
+  const PolicyLayer* Ls = P.layers;
+  // adaptation module (xa rows >= hist_dim are still zero)
+  {
+    const float(*s0[1])[16] = {xa};
+    float(*d0[1])[16] = {h1[0]};
+    policy_tiles<4, 1>(Ls + 0, PIN / 4, s0, wave, 4, d0, true, lane);  // 256
+  }
+  __syncthreads();
+  {
+    const float(*s0[1])[16] = {h1[0]};
+    float(*d0[1])[16] = {h2[0]};
+    policy_tiles<2, 1>(Ls + 1, 256 / 4, s0, wave, 4, d0, true, lane);  // 128
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const int q = lane >> 4, c = lane & 15;
+    f4_t acc = *reinterpret_cast<const f4_t*>(Ls[2].b + 4 * q);
+    const f4_t* W = reinterpret_cast<const f4_t*>(Ls[2].w);
+    for (int g = 0; g < 128 / 16; ++g) {
+      const f4_t w = W[g * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u], h2[0][16 * g + 4 * u + q][c], acc, 0, 0, 0);
+    }
+    if (q == 0) {  // features 0, 1: the latent, also the actor's inputs hist_dim, hist_dim + 1
+      xa[P.hist_dim][c] = acc[0];
+      xa[P.hist_dim + 1][c] = acc[1];
+      if (c < ne && P.latent) {
+        P.latent[(size_t)(e0 + c) * 2] = acc[0];
+        P.latent[(size_t)(e0 + c) * 2 + 1] = acc[1];
+      }
+    }
+  }
+  __syncthreads();
+  // actor and critic, layer by layer; wave w takes tiles w, w + 4, ... of both nets
+  const PolicyLayer LA1[2] = {Ls[3], Ls[7]}, LA2[2] = {Ls[4], Ls[8]}, LA3[2] = {Ls[5], Ls[9]};
+  {
+    const float(*s1[2])[16] = {xa, xc};
+    float(*d1[2])[16] = {h1[0], h1[1]};
+    policy_tiles<8, 2>(LA1, PIN / 4, s1, wave, 4, d1, true, lane);  // 512
+  }
+  __syncthreads();
+  {
+    const float(*s2[2])[16] = {h1[0], h1[1]};
+    float(*d2[2])[16] = {h2[0], h2[1]};
+    policy_tiles<4, 2>(LA2, 512 / 4, s2, wave, 4, d2, true, lane);  // 256
+  }
+  __syncthreads();
+  {
+    const float(*s3[2])[16] = {h2[0], h2[1]};
+    float(*d3[2])[16] = {h1[0], h1[1]};
+    policy_tiles<2, 2>(LA3, 256 / 4, s3, wave, 4, d3, true, lane);  // 128
+  }
+  __syncthreads();
+  if (wave < 2) {
+    const int q = lane >> 4, c = lane & 15;
+    const PolicyLayer L = Ls[wave == 0 ? 6 : 10];
+    f4_t acc = *reinterpret_cast<const f4_t*>(L.b + 4 * q);
+    const f4_t* W = reinterpret_cast<const f4_t*>(L.w);
+    for (int g = 0; g < 128 / 16; ++g) {
+      const f4_t w = W[g * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u], h1[wave][16 * g + 4 * u + q][c], acc, 0, 0, 0);
+    }
+    if (wave == 0 && P.actions) {
+      // Normal(mean, std).sample() and its log_prob summed over the actions
+      // (actor_critic.py:137-145), Box-Muller on Philox4x32-10 uniforms keyed by
+      // (global env, action, step): row q, element r is action f = 4 q + r of env c
+      float lp = 0.0f;
+      f4_t a4, s4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 4 * q + r;
+        const bool real = f < P.num_actions;
+        const float sd = real ? P.std[f] : 1.0f;
+        uint32_t ctr[4] = {(uint32_t)(e0 + c + P.env_id_offset), (uint32_t)f, (uint32_t)P.rng_step,
+                           (uint32_t)(P.rng_step >> 32)};
+        philox4x32(ctr, (uint32_t)P.rng_seed, (uint32_t)(P.rng_seed >> 32));
+        const float u1 = ((float)(ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+        const float u2 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);
+        const float z = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+        a4[r] = acc[r] + sd * z;
+        s4[r] = sd;
+        if (real) lp += -0.5f * z * z - logf(sd) - 0.91893853320467274f;  // log sqrt(2 pi)
+      }
+      // sum over the four rows (actions 0-3, 4-7, 8-11, 12-15 of the env)
+      auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(lp), __float_as_uint(lp), false, false);
+      lp = __uint_as_float(x[0]) + __uint_as_float(x[1]);
+      auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(lp), __float_as_uint(lp), false, false);
+      lp = __uint_as_float(y[0]) + __uint_as_float(y[1]);
+      if (c < ne) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * q + r;
+          if (f < P.num_actions) {
+            P.actions[(size_t)(e0 + c) * P.num_actions + f] = a4[r];
+            P.action_sigma[(size_t)(e0 + c) * P.num_actions + f] = s4[r];
+          }
+        }
+        if (q == 0) P.log_prob[e0 + c] = lp;
+      }
+    }
+    if (c < ne) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 4 * q + r;
+        if (wave == 0 && f < P.num_actions) P.action_mean[(size_t)(e0 + c) * P.num_actions + f] = acc[r];
+        if (wave == 1 && f == 0) P.value[e0 + c] = acc[r];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -157,6 +373,20 @@ int go1_gae(const float* rewards, const uint8_t* dones, const float* values, con
   RT_TRY(hipMemsetAsync(stats, 0, 2 * sizeof(double), s));
   hipLaunchKernelGGL(gae_kernel, dim3((n_envs + 255) / 256), dim3(256), 0, s, rewards, dones, values, last_values,
                      returns, advantages, stats, T, n_envs, gamma, lam);
+  RT_TRY(hipGetLastError());
+  return GO1_OK_RT;
+}
+
+int go1_policy_forward(const go1_policy_args* args, void* stream) {
+  if (!args || args->n_envs <= 0 || !args->obs_history || !args->privileged_obs || !args->action_mean ||
+      !args->value)
+    return fail(GO1_RT_E_ARG, "go1_policy_forward: bad argument");
+  if (args->hist_dim + 2 > PIN || args->num_actions > 16)
+    return fail(GO1_RT_E_ARG, "go1_policy_forward: input / action width outside the compiled architecture");
+  for (int i = 0; i < GO1_POLICY_LAYERS; ++i)
+    if (!args->layers[i].w || !args->layers[i].b) return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer");
+  go1_policy_args P = *args;
+  hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(256), 0, (hipStream_t)stream, P);
   RT_TRY(hipGetLastError());
   return GO1_OK_RT;
 }

@@ -84,6 +84,92 @@ class StepExtras(dict):
         return [self[k] for k in list(self.keys())]
 
 
+class EpisodeLogRing:
+    """Device ring of the kernel's per-step episode log (go1_step_args.episode_log) and its
+    asynchronous trip to the host.
+
+    Two halves of EPISODE_RING steps.  When a half fills, a side stream copies it to
+    pinned host memory while the next half is written; the copy is turned into deque
+    entries on the host one half later (long finished, no wait), so the rollout never
+    blocks on logging.  Reading extras["train/episode"] / ["timeouts"] drains everything
+    synchronously.  Deques keep their last 4000 entries (deque(maxlen=4000), as the
+    reference), so only the newest 4000 values per key are materialised."""
+
+    def __init__(self, env, n, device):
+        self.env = env
+        self.dev = device
+        self.buf = torch.zeros((2, EPISODE_RING, n, abi.GO1_EPISODE_LOG), device=device)
+        self.half, self.slot, self.done = 0, 0, 0  # write position; slots of this half already drained
+        self.cuda = device.type == "cuda"
+        if self.cuda:
+            self.host = torch.zeros((2, EPISODE_RING, n, abi.GO1_EPISODE_LOG), pin_memory=True)
+            self.side = torch.cuda.Stream(device)
+            self.copied = [None, None]  # event per half: host copy finished
+        self.inflight = None  # (half, first slot) copied to host, not yet turned into deque entries
+
+    def next_slot(self):
+        """Buffer the kernel writes this step's log into."""
+        if self.slot == 0 and self.cuda and self.copied[self.half] is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self.copied[self.half])  # half free again
+        return self.buf[self.half, self.slot]
+
+    def advance(self):
+        self.slot += 1
+        if self.slot == EPISODE_RING:
+            h, first = self.half, self.done
+            self.half, self.slot, self.done = h ^ 1, 0, 0
+            if self.cuda:
+                self._drain_inflight()
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.dev))
+                self.side.wait_event(ev)
+                with torch.cuda.stream(self.side):
+                    self.host[h].copy_(self.buf[h], non_blocking=True)
+                    done = torch.cuda.Event()
+                    done.record(self.side)
+                self.copied[h] = done
+                self.inflight = (h, first)
+            else:
+                self._process(self.buf[h, first:].numpy())
+
+    def _drain_inflight(self):
+        if self.inflight is not None:
+            h, first = self.inflight
+            self.inflight = None
+            self.copied[h].synchronize()
+            self._process(self.host[h, first:].numpy())
+
+    def drain(self):
+        """Everything logged so far, synchronously (extras read)."""
+        if self.cuda:
+            self._drain_inflight()
+        if self.slot > self.done:
+            self._process(self.buf[self.half, self.done:self.slot].cpu().numpy())
+            self.done = self.slot
+
+    def reset(self):
+        if self.cuda:
+            self._drain_inflight()
+        self.done = self.slot
+
+    def _process(self, logs):
+        env = self.env
+        ntr = env.num_train_envs
+        col = logs[:, :ntr, 13]                              # episode length, 0 = no reset
+        steps, envs = np.nonzero(col > 0)                    # by step, then env
+        if steps.size == 0:
+            return
+        rows = logs[steps, envs][-4000:]
+        reset_steps = np.unique(steps)
+        timeouts = (col[reset_steps] > np.float32(env.max_episode_length)).reshape(-1)[-4000:]
+        env._timeouts.extend(timeouts)
+        for i, key in enumerate(L.SUM_KEYS):
+            env._train_ep["rew_" + key].extend(rows[:, i])
+        env._train_ep["episode_length"].extend(rows[:, 13])
+        env._train_ep["reached"].extend(rows[:, 14] > 0)
+        env._train_ep["goal_distance"].extend(rows[:, 15])
+
+
 def _episode_dicts():
     return defaultdict(lambda: deque([], 4000)), defaultdict(lambda: deque([], 4000)), deque([], 4000)
 
@@ -150,9 +236,7 @@ class LeggedRobot:
         self._reset = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
         self._time_out = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
         self._slot = 0
-        self._elog = torch.zeros((EPISODE_RING, n, abi.GO1_EPISODE_LOG), device=dev)
-        self._elog_pending = []
-        self._elog_k = 0
+        self._elog = EpisodeLogRing(self, n, dev)
         self._aux = torch.zeros((n, abi.GO1_AUX), device=dev)
         self._reset_mask = torch.zeros(n, dtype=torch.uint8, device=dev)
         # host RNG for the global gravity draws: identical on every rank
@@ -308,23 +392,22 @@ class LeggedRobot:
     # ------------------------------------------------------------------ step
     def step(self, actions):
         """LeggedRobot.step (:64-112): returns obs, privileged_obs, rew, reset, extras."""
-        a = torch.as_tensor(actions)
+        a = actions if isinstance(actions, torch.Tensor) else torch.as_tensor(actions)
         if a.device != self.device or a.dtype != torch.float32:
             a = a.to(self.device, torch.float32)
-        a = a.detach().contiguous()
+        if a.requires_grad:
+            a = a.detach()
+        if not a.is_contiguous():
+            a = a.contiguous()
         if a.shape != (self.num_envs, self.num_actions):
             raise ValueError(f"actions must be ({self.num_envs}, {self.num_actions}), got {tuple(a.shape)}")
         s = self._slot
         out = dict(obs=self._obs[s], priv=self._priv[s], rew=self._rew[s], reset=self._reset[s],
                    time_out=self._time_out[s])
-        k = self._elog_k
-        if len(self._elog_pending) == EPISODE_RING:
-            self._flush_episode_log()
         self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
-                       rng_step=self._rng_step, out=out, episode_log=self._elog[k], aux=self._aux)
+                       rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux)
         self._rng_step += 1
-        self._elog_pending.append(k)
-        self._elog_k = (k + 1) % EPISODE_RING
+        self._elog.advance()
         self._slot = (s + 1) % OUT_RING
         dict.__setitem__(self.extras, "time_outs", self._sim.extras_time_outs)
         # post-physics host bookkeeping (:126, :826-830, :171-182)
@@ -376,29 +459,7 @@ class LeggedRobot:
 
     # ------------------------------------------------------------------ episode log
     def _flush_episode_log(self):
-        """Move pending reset_idx logging (kernel episode_log rows) into the deques, in step order."""
-        if not self._elog_pending:
-            return
-        ks = torch.as_tensor(self._elog_pending, device=self.device)
-        self._elog_pending = []
-        logs = self._elog.index_select(0, ks)                      # (k, n, 16)
-        m = logs[:, : self.num_train_envs, 13] > 0                  # reset rows of train envs
-        idx = m.nonzero()
-        rows = logs[idx[:, 0], idx[:, 1]].cpu().numpy()
-        step_of_row = idx[:, 0].cpu().numpy()
-        any_k = m.any(1).cpu().numpy()
-        tmax = np.float32(self.max_episode_length)
-        ep_all = logs[:, : self.num_train_envs, 13].cpu().numpy() if any_k.any() else None
-        for j in range(len(any_k)):
-            if not any_k[j]:
-                continue
-            r = rows[step_of_row == j]
-            for i, key in enumerate(L.SUM_KEYS):
-                self._train_ep["rew_" + key].extend(r[:, i])
-            self._train_ep["episode_length"].extend(r[:, 13])
-            self._train_ep["reached"].extend(r[:, 14] > 0)
-            self._train_ep["goal_distance"].extend(r[:, 15])
-            self._timeouts.extend(ep_all[j] > tmax)
+        self._elog.drain()
 
     # ------------------------------------------------------------------ misc API
     def start_recording(self):
@@ -462,7 +523,7 @@ class TrajectoryTrackingEnv(LeggedRobot):
         self.episode_length_buf = torch.randint(int(self.max_episode_length), (self.num_envs,), device=self.device,
                                                 generator=self._gen, dtype=torch.int32)
         self._train_ep, self._eval_ep, self._timeouts = _episode_dicts()
-        self._elog_pending = []
+        self._elog.reset()
         self._install_extras()
         obs, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
         return obs

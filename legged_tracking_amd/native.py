@@ -100,6 +100,9 @@ class Go1Native:
             self.extras_time_outs = torch.zeros(n, dtype=torch.bool, device=dev)
             self.contact_forces = torch.zeros((n, 17, 3), device=dev)
         self._terrain_keep = None
+        self._args = None
+        self._consts = None
+        self._lib_step = lib().go1_step
 
     def set_terrain(self, tiles, env_tile, env_terrain_origin, env_origins):
         d = self.device
@@ -116,45 +119,57 @@ class Go1Native:
              inj=None, debug=None, events=None, episode_log=None, aux=None, out=None):
         """One fused LeggedRobot.step on the current stream.  `debug` is an optional dict
         of preallocated tensors (torques, heights, terms, commands, reached); `out` may
-        replace the default output buffers (obs, priv, rew, reset, time_out)."""
-        a = abi.Go1StepArgs()
-        assert actions.is_contiguous() and actions.dtype == torch.float32 and actions.shape == (self.n, 12)
+        replace the default output buffers (obs, priv, rew, reset, time_out).
+
+        The go1_step_args struct is kept between calls (the rollout calls this every
+        few hundred microseconds); only the fields that change are rewritten."""
+        a = self._args
+        if a is None:
+            a = self._args = abi.Go1StepArgs()
+            a.contact_forces = self.contact_forces.data_ptr()
+            a.extras_time_outs = self.extras_time_outs.data_ptr()
+        if actions.dtype != torch.float32 or actions.shape != (self.n, 12) or not actions.is_contiguous() or \
+                actions.device != self.device:
+            raise NativeError("actions must be a contiguous (n_envs, 12) float32 tensor on the env's device")
         a.actions = actions.data_ptr()
-        for i in range(3):
-            a.gravity_vec[i] = float(gravity_vec[i])
-            a.sim_gravity[i] = float(sim_gravity[i])
-        for i in range(abi.GO1_NUM_TERMS):
-            a.reward_scales[i] = float(reward_scales[i])
+        key = (tuple(gravity_vec), tuple(sim_gravity), tuple(reward_scales))
+        if key != self._consts:
+            self._consts = key
+            a.gravity_vec[:] = [float(x) for x in gravity_vec]
+            a.sim_gravity[:] = [float(x) for x in sim_gravity]
+            a.reward_scales[:] = [float(x) for x in reward_scales]
         a.rng_seed, a.rng_step = int(rng_seed), int(rng_step)
+        a.uniforms = None
         if uniforms is not None:
             assert uniforms.is_contiguous() and uniforms.shape == (self.n, abi.GO1_U_PER_ENV)
             a.uniforms = uniforms.data_ptr()
         if inj is not None:
             a.inj_dof, a.inj_root, a.inj_contact = (inj[k].data_ptr() for k in ("dof", "root", "contact"))
-        o = dict(obs=self.obs, priv=self.priv, rew=self.rew, reset=self.reset, time_out=self.time_out)
+        else:
+            a.inj_dof = a.inj_root = a.inj_contact = None
         if out:
-            for k, v in out.items():
-                assert k in o and v.shape == o[k].shape and v.dtype == o[k].dtype and v.is_contiguous(), k
-                assert v.device == self.device, k
-                o[k] = v
-        a.obs, a.priv, a.rew = o["obs"].data_ptr(), o["priv"].data_ptr(), o["rew"].data_ptr()
-        a.reset, a.time_out = o["reset"].data_ptr(), o["time_out"].data_ptr()
-        a.extras_time_outs = self.extras_time_outs.data_ptr()
-        a.contact_forces = self.contact_forces.data_ptr()
-        if debug:
-            for k, fld in (("torques", "dbg_torques"), ("heights", "dbg_heights"), ("terms", "dbg_terms"),
-                           ("commands", "dbg_commands"), ("reached", "dbg_reached")):
-                if k in debug:
-                    setattr(a, fld, debug[k].data_ptr())
+            for k in ("obs", "priv", "rew", "reset", "time_out"):
+                v = out.get(k)
+                if v is None:
+                    v = getattr(self, k)
+                elif v.device != self.device or not v.is_contiguous() or v.shape != getattr(self, k).shape or \
+                        v.dtype != getattr(self, k).dtype:
+                    raise NativeError(f"output buffer {k!r} does not match the expected shape / dtype / device")
+                setattr(a, k, v.data_ptr())
+        else:
+            a.obs, a.priv, a.rew = self.obs.data_ptr(), self.priv.data_ptr(), self.rew.data_ptr()
+            a.reset, a.time_out = self.reset.data_ptr(), self.time_out.data_ptr()
+        for k, fld in (("torques", "dbg_torques"), ("heights", "dbg_heights"), ("terms", "dbg_terms"),
+                       ("commands", "dbg_commands"), ("reached", "dbg_reached")):
+            setattr(a, fld, debug[k].data_ptr() if debug and k in debug else None)
         if episode_log is not None:
             assert episode_log.is_contiguous() and episode_log.shape == (self.n, abi.GO1_EPISODE_LOG)
-            a.episode_log = episode_log.data_ptr()
+        a.episode_log = episode_log.data_ptr() if episode_log is not None else None
         if aux is not None:
             assert aux.is_contiguous() and aux.shape == (self.n, abi.GO1_AUX)
-            a.aux = aux.data_ptr()
-        if events is not None:  # (hipEvent_t begin, hipEvent_t end) as ints
-            a.ev_begin, a.ev_end = events
-        _check(lib().go1_step(self.h, C.byref(a), _stream()))
+        a.aux = aux.data_ptr() if aux is not None else None
+        a.ev_begin, a.ev_end = events if events is not None else (None, None)  # hipEvent_t pair as ints
+        _check(self._lib_step(self.h, C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
 
     def reset_envs(self, mask, uniforms=None, rng_seed=0, rng_step=0):
         m = mask.to(torch.uint8).contiguous()

@@ -89,6 +89,106 @@ class _Transition(C.Structure):
         ("num_obs", C.c_int32), ("num_priv", C.c_int32), ("num_obs_history", C.c_int32), ("num_actions", C.c_int32)]
 
 
+class _PolicyLayer(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("b", C.c_void_p)]
+
+
+class _PolicyArgs(C.Structure):
+    _fields_ = [("obs_history", C.c_void_p), ("privileged_obs", C.c_void_p), ("action_mean", C.c_void_p),
+                ("value", C.c_void_p), ("latent", C.c_void_p), ("std", C.c_void_p), ("actions", C.c_void_p),
+                ("action_sigma", C.c_void_p), ("log_prob", C.c_void_p), ("rng_seed", C.c_uint64),
+                ("rng_step", C.c_uint64), ("env_id_offset", C.c_int32), ("n_envs", C.c_int32),
+                ("hist_dim", C.c_int32), ("num_actions", C.c_int32), ("layers", _PolicyLayer * 11)]
+
+
+def _pack_linear(lin):
+    """nn.Linear -> (weights in MFMA A-fragment order, bias padded to 16).
+
+    Packed [n/16][k/16][lane = 16 q + m][u] = W[16 t + m][16 g + 4 u + q]: lane (m, q)
+    of output tile t reads one float4 per group g of four K-steps (k = 16 g + 4 u + q)."""
+    W, b = lin.weight.detach(), lin.bias.detach()
+    n, k = W.shape
+    npad, kpad = -(-n // 16) * 16, -(-k // 16) * 16
+    Wp = torch.zeros(npad, kpad, device=W.device, dtype=torch.float32)
+    Wp[:n, :k] = W
+    bp = torch.zeros(npad, device=W.device, dtype=torch.float32)
+    bp[:n] = b
+    # [t, m, g, u, q] -> [t, g, q, m, u]
+    return Wp.view(npad // 16, 16, kpad // 16, 4, 4).permute(0, 2, 4, 1, 3).contiguous(), bp
+
+
+class FusedPolicy:
+    """ActorCritic forward for the rollout (act + evaluate) in one HIP kernel
+    (csrc/rollout.hip policy_kernel).  Re-pack after every optimiser step."""
+
+    def __init__(self, ac, lib):
+        self.ac = ac
+        self.lib = lib
+        self.packed = None
+
+    @staticmethod
+    def supported(ac):
+        try:
+            a, p, c = ac.adaptation_module, ac.actor_body, ac.critic_body
+            shapes = [tuple(m.weight.shape) for m in (a[0], a[2], a[4], p[0], p[2], p[4], p[6], c[0], c[2], c[4],
+                                                       c[6])]
+        except (IndexError, AttributeError):
+            return False
+        h = ac.num_obs_history
+        want = [(256, h), (128, 256), (2, 128), (512, h + 2), (256, 512), (128, 256), (None, 128), (512, h + 2),
+                (256, 512), (128, 256), (1, 128)]
+        ok = all(w[0] in (None, s[0]) and w[1] == s[1] for s, w in zip(shapes, want))
+        return ok and h + 2 <= 272 and shapes[6][0] <= 16 and isinstance(a[1], nn.ELU) and ac.num_privileged_obs == 2
+
+    def pack(self):
+        ac = self.ac
+        mods = [ac.adaptation_module[i] for i in (0, 2, 4)] + [ac.actor_body[i] for i in (0, 2, 4, 6)] + \
+               [ac.critic_body[i] for i in (0, 2, 4, 6)]
+        self.packed = [_pack_linear(m) for m in mods]
+        self.na = ac.actor_body[6].out_features
+        self.args = _PolicyArgs(num_actions=self.na)
+        for i, (w, b) in enumerate(self.packed):
+            self.args.layers[i].w, self.args.layers[i].b = w.data_ptr(), b.data_ptr()
+
+    def forward(self, obs_history, privileged_obs, sample=None):
+        """-> (mean, value, latent) or, with sample = (rng_seed, rng_step, env_id_offset),
+        (mean, value, latent, actions, sigma, log_prob): Normal(mean, std) drawn in-kernel."""
+        if self.packed is None:
+            self.pack()
+        h = obs_history.detach()
+        p = privileged_obs.detach()
+        if not h.is_contiguous():
+            h = h.contiguous()
+        if not p.is_contiguous():
+            p = p.contiguous()
+        n = h.shape[0]
+        na = self.na
+        dev = h.device
+        mean = torch.empty(n, na, device=dev)
+        value = torch.empty(n, 1, device=dev)
+        latent = torch.empty(n, 2, device=dev)
+        a = self.args
+        a.obs_history, a.privileged_obs = h.data_ptr(), p.data_ptr()
+        a.action_mean, a.value, a.latent = mean.data_ptr(), value.data_ptr(), latent.data_ptr()
+        a.n_envs, a.hist_dim = n, h.shape[1]
+        out = (mean, value, latent)
+        if sample is not None:
+            actions = torch.empty(n, na, device=dev)
+            sigma = torch.empty(n, na, device=dev)
+            logp = torch.empty(n, device=dev)
+            self.std = self.ac.std.detach().contiguous()
+            a.std, a.actions, a.action_sigma, a.log_prob = (self.std.data_ptr(), actions.data_ptr(),
+                                                            sigma.data_ptr(), logp.data_ptr())
+            a.rng_seed, a.rng_step, a.env_id_offset = sample
+            out = out + (actions, sigma, logp)
+        else:
+            a.actions = None
+        rc = self.lib.go1_policy_forward(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc != 0:
+            raise RuntimeError(self.lib.go1_rollout_last_error().decode())
+        return out
+
+
 class HipRolloutKernels:
     """ctypes binding of libgo1_rollout.so; raises when the library or the GPU is missing."""
 
@@ -102,6 +202,7 @@ class HipRolloutKernels:
         lib.go1_record_transition.argtypes = [C.POINTER(_Transition), C.c_int32, C.c_float, C.c_void_p]
         lib.go1_gae.argtypes = [C.c_void_p] * 7 + [C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_void_p]
         lib.go1_adv_normalize.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_int64, C.c_void_p]
+        lib.go1_policy_forward.argtypes = [C.POINTER(_PolicyArgs), C.c_void_p]
         self.lib = lib
 
     def _chk(self, rc):
@@ -112,29 +213,36 @@ class HipRolloutKernels:
     def _s():
         return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
+    _SRC = (("obs", "observations"), ("privileged_obs", "privileged_observations"),
+            ("obs_history", "observation_histories"), ("actions", "actions"), ("mu", "action_mean"),
+            ("sigma", "action_sigma"), ("actions_log_prob", "actions_log_prob"), ("values", "values"),
+            ("rewards", "rewards"), ("dones", "dones"), ("time_outs", "time_outs"))
+
     def record(self, st, step, tr, gamma):
-        t = _Transition()
-        src = dict(obs=tr["observations"], privileged_obs=tr["privileged_observations"],
-                   obs_history=tr["observation_histories"], actions=tr["actions"], mu=tr["action_mean"],
-                   sigma=tr["action_sigma"], actions_log_prob=tr["actions_log_prob"], values=tr["values"],
-                   rewards=tr["rewards"], dones=tr["dones"], time_outs=tr.get("time_outs"))
+        t = getattr(st, "_tr_struct", None)
+        if t is None:
+            t = st._tr_struct = _Transition()
+            t.num_obs, t.num_priv = st.observations.shape[-1], st.privileged_observations.shape[-1]
+            t.num_obs_history, t.num_actions = st.observation_histories.shape[-1], st.actions.shape[-1]
+            st._tr_dst = [(k, buf) for k, buf in (
+                ("st_obs", st.observations), ("st_privileged_obs", st.privileged_observations),
+                ("st_obs_history", st.observation_histories), ("st_actions", st.actions), ("st_mu", st.mu),
+                ("st_sigma", st.sigma), ("st_actions_log_prob", st.actions_log_prob), ("st_values", st.values),
+                ("st_rewards", st.rewards), ("st_dones", st.dones))]
         keep = []
-        for k, v in src.items():
+        for k, name in self._SRC:
+            v = tr.get(name)
             if v is None:
+                setattr(t, k, None)
                 continue
-            v = v.detach()
             if v.dtype == torch.bool:
                 v = v.view(torch.uint8)
-            v = v.contiguous()
+            if not v.is_contiguous():
+                v = v.contiguous()
             keep.append(v)
             setattr(t, k, v.data_ptr())
-        for k, buf in (("st_obs", st.observations), ("st_privileged_obs", st.privileged_observations),
-                       ("st_obs_history", st.observation_histories), ("st_actions", st.actions),
-                       ("st_mu", st.mu), ("st_sigma", st.sigma), ("st_actions_log_prob", st.actions_log_prob),
-                       ("st_values", st.values), ("st_rewards", st.rewards), ("st_dones", st.dones)):
+        for k, buf in st._tr_dst:
             setattr(t, k, buf[step].data_ptr())
-        t.num_obs, t.num_priv = st.observations.shape[-1], st.privileged_observations.shape[-1]
-        t.num_obs_history, t.num_actions = st.observation_histories.shape[-1], st.actions.shape[-1]
         self._chk(self.lib.go1_record_transition(C.byref(t), st.num_envs, gamma, self._s()))
         return keep
 
@@ -143,6 +251,9 @@ class HipRolloutKernels:
         self._chk(self.lib.go1_gae(st.rewards.data_ptr(), st.dones.data_ptr(), st.values.data_ptr(), lv.data_ptr(),
                                    st.returns.data_ptr(), st.advantages.data_ptr(), st.adv_stats.data_ptr(),
                                    st.num_transitions_per_env, st.num_envs, gamma, lam, self._s()))
+
+    def policy(self, ac):
+        return FusedPolicy(ac, self.lib) if FusedPolicy.supported(ac) else None
 
     def normalize(self, st, count):
         self._chk(self.lib.go1_adv_normalize(st.advantages.data_ptr(), st.adv_stats.data_ptr(), float(count),
@@ -354,6 +465,10 @@ class PPO:
                                                             lr=PPO_Args.adaptation_module_learning_rate)
         self.transition = RolloutStorage.Transition()
         self.learning_rate = PPO_Args.learning_rate
+        self.fused = None  # FusedPolicy once the storage (and its kernels) exist
+        self.sample_seed = 0x5EED
+        self._sample_step = 0
+        self.env_id_offset = 0
         if _world() > 1:  # every rank starts from rank 0's weights
             for p in self.actor_critic.parameters():
                 torch.distributed.broadcast(p.data, 0)
@@ -362,6 +477,10 @@ class PPO:
                      obs_history_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, privileged_obs_shape,
                                       obs_history_shape, action_shape, self.device, kernels=self.kernels)
+        pol = getattr(self.storage.kernels, "policy", None)
+        self.fused = pol(self.actor_critic) if pol is not None else None
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            self.env_id_offset = torch.distributed.get_rank() * num_envs
 
     def test_mode(self):
         self.actor_critic.eval()
@@ -372,8 +491,20 @@ class PPO:
     def act(self, obs, privileged_obs, obs_history):
         ac = self.actor_critic
         t = self.transition
-        t.actions = ac.act(obs_history).detach()
-        t.values = ac.evaluate(obs_history, privileged_obs).detach()
+        if self.fused is not None and not torch.is_grad_enabled():
+            # one kernel: adaptation module + actor + critic + Normal(mean, std) sample + log_prob
+            self._sample_step += 1
+            mean, values, _, actions, sigma, logp = self.fused.forward(
+                obs_history, privileged_obs, sample=(self.sample_seed, self._sample_step, self.env_id_offset))
+            t.actions, t.values, t.actions_log_prob, t.action_mean, t.action_sigma = actions, values, logp, mean, sigma
+            t.observations = obs
+            t.critic_observations = obs
+            t.privileged_observations = privileged_obs
+            t.observation_histories = obs_history
+            return t.actions
+        else:
+            t.actions = ac.act(obs_history).detach()
+            t.values = ac.evaluate(obs_history, privileged_obs).detach()
         t.actions_log_prob = ac.get_actions_log_prob(t.actions).detach()
         t.action_mean = ac.action_mean.detach()
         t.action_sigma = ac.action_std.detach()
@@ -395,7 +526,10 @@ class PPO:
         self.actor_critic.reset(dones)
 
     def compute_returns(self, last_critic_obs, last_critic_privileged_obs):
-        last_values = self.actor_critic.evaluate(last_critic_obs, last_critic_privileged_obs).detach()
+        if self.fused is not None and not torch.is_grad_enabled():
+            last_values = self.fused.forward(last_critic_obs, last_critic_privileged_obs)[1]
+        else:
+            last_values = self.actor_critic.evaluate(last_critic_obs, last_critic_privileged_obs).detach()
         self.storage.compute_returns(last_values, PPO_Args.gamma, PPO_Args.lam)
 
     def _allreduce_grads(self):
@@ -476,6 +610,8 @@ class PPO:
         n_up = A.num_learning_epochs * A.num_mini_batches
         n_ad = n_up * A.num_adaptation_module_substeps
         self.storage.clear()
+        if self.fused is not None:
+            self.fused.pack()  # the rollout kernel reads the updated weights
         return (mean_value_loss / n_up, mean_surrogate_loss / n_up, mean_adapt / n_ad, 0.0, 0.0,
                 mean_adapt_test / n_ad, 0.0, 0.0)
 

@@ -177,3 +177,56 @@ def test_ddp_normalisation_and_gradients_gloo():
     res = sorted(q.get(timeout=5) for _ in range(2))
     for rank, ok_adv, same_w, same_lr in res:
         assert ok_adv and same_w and same_lr, res
+
+
+@pytest.mark.gpu
+def test_fused_policy_kernel_matches_reference_actor_critic():
+    """One MFMA kernel for adaptation module + actor + critic (f32; summation order
+    differs from hipBLASLt / the reference's CPU GEMMs: rtol 2e-5)."""
+    d = _fixture()
+    ac = _ac(d, "cuda:0")
+    k = R.HipRolloutKernels()
+    pol = k.policy(ac)
+    assert pol is not None
+    hist, priv = (torch.from_numpy(d[x]).cuda() for x in ("in/hist", "in/priv"))
+    mean, value, latent = pol.forward(hist, priv)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(latent.cpu().numpy(), d["ac/latent"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(mean.cpu().numpy(), d["ac/mean"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(value.cpu().numpy(), d["ac/value"], rtol=2e-5, atol=2e-5)
+    # ragged batch (not a multiple of the 16-env tile) and a larger one
+    for n in (37, 4096):
+        g = torch.Generator(device="cuda").manual_seed(n)
+        h = torch.randn(n, 261, device="cuda", generator=g)
+        p = torch.randn(n, 2, device="cuda", generator=g)
+        m2, v2, l2 = pol.forward(h, p)
+        with torch.no_grad():
+            lt = ac.adaptation_module(h)
+            mt = ac.actor_body(torch.cat((h, lt), -1))
+            vt = ac.critic_body(torch.cat((h, p), -1))
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(l2.cpu().numpy(), lt.cpu().numpy(), rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(m2.cpu().numpy(), mt.cpu().numpy(), rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(v2.cpu().numpy(), vt.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_fused_policy_sampling_is_normal_with_matching_log_prob():
+    d = _fixture()
+    ac = _ac(d, "cuda:0")
+    pol = R.HipRolloutKernels().policy(ac)
+    n = 8192
+    g = torch.Generator(device="cuda").manual_seed(1)
+    h = torch.randn(n, 261, device="cuda", generator=g)
+    p = torch.randn(n, 2, device="cuda", generator=g)
+    mean, value, latent, act, sigma, logp = pol.forward(h, p, sample=(123, 7, 0))
+    torch.cuda.synchronize()
+    z = ((act - mean) / sigma).cpu().numpy()
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+    np.testing.assert_array_equal(sigma.cpu().numpy(), np.broadcast_to(d["ac/std"][0], sigma.shape))
+    ref = torch.distributions.Normal(mean, sigma).log_prob(act).sum(-1)
+    np.testing.assert_allclose(logp.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-4)
+    # same counter -> same draws; next counter -> different draws
+    act2 = pol.forward(h, p, sample=(123, 7, 0))[3]
+    act3 = pol.forward(h, p, sample=(123, 8, 0))[3]
+    assert torch.equal(act, act2) and not torch.equal(act, act3)

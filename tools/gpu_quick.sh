@@ -6,6 +6,6 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps 500 --warmup 50 --no-cpu-baseline --no-rollout > gpurun_out/bench_quick.log 2>&1 || exit $?
-python -c "import json; d=json.loads(open('gpurun_out/bench_quick.log').read().strip().splitlines()[-1]); print('value', round(d['value']/1e6,2), 'M env-steps/s; ms/step', round(d['ms_per_step'],4), 'kernel ms', round(d['roofline']['kernel_ms'],4))"
+timeout -k 10 300 python bench.py --steps 500 --warmup 50 --no-cpu-baseline $BENCH_EXTRA > gpurun_out/bench_quick.log 2>&1 || exit $?
+python -c "import json; d=json.loads(open('gpurun_out/bench_quick.log').read().strip().splitlines()[-1]); print('value', round(d['value']/1e6,2), 'M env-steps/s; ms/step', round(d['ms_per_step'],4), 'kernel ms', round(d['roofline']['kernel_ms'],4), 'rollout', d.get('rollout'))"
 for x in "$@"; do echo "== $x"; timeout -k 10 120 $x || exit $?; done
