@@ -148,8 +148,8 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
 }
 
 // ------------------------------------------------------------------ policy inference
-// ActorCritic.act / evaluate (actor_critic.py:121-150) for 16 envs per workgroup of 4
-// waves, every layer on v_mfma_f32_16x16x4_f32 with weights as the A operand
+// ActorCritic.act / evaluate (actor_critic.py:121-150) for 16 envs per workgroup of 8
+// waves (two per SIMD, so one wave's MFMAs cover the other's weight loads), every layer on v_mfma_f32_16x16x4_f32 with weights as the A operand
 // (16 output features x 4 k) and activations as B (4 k x 16 envs):
 //   adaptation: hist(261) -> 256 -> 128 -> 2 (latent)
 //   actor:      [hist, latent](263) -> 512 -> 256 -> 128 -> 12 (action mean)
@@ -168,44 +168,54 @@ __device__ __forceinline__ float elu(float x) { return x > 0.0f ? x : expm1f(x);
 // [tile][k/16][lane][4]: one 16-byte load per lane feeds four K-steps of one tile, and
 // the next group's loads are issued before the current group's MFMAs (double buffer).
 template <int NT, int NL>
+__device__ __forceinline__ void policy_group(const f4_t (&w)[NL][NT], const float (*const* src)[16], int g, int q,
+                                             int c, f4_t (&acc)[NL][NT]) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    float bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bv[u] = src[l][16 * g + 4 * u + q][c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) acc[l][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[l][i][u], bv[u], acc[l][i], 0, 0, 0);
+  }
+}
+
+template <int NT, int NL>
+__device__ __forceinline__ void policy_load(const PolicyLayer* L, int G, int g, int tile0, int tstride, int lane,
+                                            f4_t (&w)[NL][NT]) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+      w[l][i] = reinterpret_cast<const f4_t*>(L[l].w)[((size_t)(tile0 + i * tstride) * G + g) * 64 + lane];
+}
+
+// NT output tiles (tile0 + i * tstride) of NL layers at the same depth (the actor and the
+// critic advance together) for the 16 envs: acc = b + W x, ELU (act), store to
+// dst[feature][env].  Weights are packed [tile][k/16][lane][4]: one 16-byte load per lane
+// feeds four K-steps of one tile; loads run two groups ahead of the MFMAs.
+template <int NT, int NL>
 __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const float (*const* src)[16], int tile0,
                                              int tstride, float (*const* dst)[16], bool act, int lane) {
-  // NL layers (the actor and the critic at the same depth) advance together: 2 x NT
-  // independent accumulators keep the MFMA pipe busy while the next weights load
   const int q = lane >> 4, c = lane & 15;
   const int G = S >> 2;  // groups of four K-steps (K padded to a multiple of 16)
   f4_t acc[NL][NT], wa[NL][NT], wb[NL][NT];
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      const int t = tile0 + i * tstride;
-      acc[l][i] = *reinterpret_cast<const f4_t*>(L[l].b + 16 * t + 4 * q);
-      wa[l][i] = reinterpret_cast<const f4_t*>(L[l].w)[((size_t)t * G + 0) * 64 + lane];
-    }
-  for (int g = 0; g < G; ++g) {
+    for (int i = 0; i < NT; ++i)
+      acc[l][i] = *reinterpret_cast<const f4_t*>(L[l].b + 16 * (tile0 + i * tstride) + 4 * q);
+  policy_load<NT, NL>(L, G, 0, tile0, tstride, lane, wa);
+  if (G > 1) policy_load<NT, NL>(L, G, 1, tile0, tstride, lane, wb);
+  for (int g = 0; g < G; g += 2) {
+    policy_group<NT, NL>(wa, src, g, q, c, acc);
+    if (g + 2 < G) policy_load<NT, NL>(L, G, g + 2, tile0, tstride, lane, wa);
     if (g + 1 < G) {
-#pragma unroll
-      for (int l = 0; l < NL; ++l)
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-          wb[l][i] = reinterpret_cast<const f4_t*>(L[l].w)[((size_t)(tile0 + i * tstride) * G + g + 1) * 64 + lane];
+      policy_group<NT, NL>(wb, src, g + 1, q, c, acc);
+      if (g + 3 < G) policy_load<NT, NL>(L, G, g + 3, tile0, tstride, lane, wb);
     }
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      float bv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) bv[u] = src[l][16 * g + 4 * u + q][c];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-          acc[l][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[l][i][u], bv[u], acc[l][i], 0, 0, 0);
-    }
-#pragma unroll
-    for (int l = 0; l < NL; ++l)
-#pragma unroll
-      for (int i = 0; i < NT; ++i) wa[l][i] = wb[l][i];
   }
 #pragma unroll
   for (int l = 0; l < NL; ++l)
@@ -217,14 +227,14 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const 
     }
 }
 
-__global__ __launch_bounds__(256) void policy_kernel(go1_policy_args P) {
+__global__ __launch_bounds__(512) void policy_kernel(go1_policy_args P) {
   __shared__ float xa[PIN][16], xc[PIN][16];  // actor / critic inputs (adaptation uses xa)
   __shared__ float h1[2][512][16];             // layer-1 outputs (actor, critic); layer 3 reuses it
   __shared__ float h2[2][256][16];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int e0 = blockIdx.x * 16;
   const int ne = min(16, P.n_envs - e0);
-  for (int idx = tid; idx < 16 * PIN; idx += 256) {
+  for (int idx = tid; idx < 16 * PIN; idx += 512) {
     const int e = idx / PIN, k = idx - e * PIN;
     float v = 0.0f;
     if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
@@ -237,13 +247,13 @@ __global__ __launch_bounds__(256) void policy_kernel(go1_policy_args P) {
   {
     const float(*s0[1])[16] = {xa};
     float(*d0[1])[16] = {h1[0]};
-    policy_tiles<4, 1>(Ls + 0, PIN / 4, s0, wave, 4, d0, true, lane);  // 256
+    policy_tiles<2, 1>(Ls + 0, PIN / 4, s0, wave, 8, d0, true, lane);  // 256
   }
   __syncthreads();
   {
     const float(*s0[1])[16] = {h1[0]};
     float(*d0[1])[16] = {h2[0]};
-    policy_tiles<2, 1>(Ls + 1, 256 / 4, s0, wave, 4, d0, true, lane);  // 128
+    policy_tiles<1, 1>(Ls + 1, 256 / 4, s0, wave, 8, d0, true, lane);  // 128
   }
   __syncthreads();
   if (wave == 0) {
@@ -271,19 +281,19 @@ __global__ __launch_bounds__(256) void policy_kernel(go1_policy_args P) {
   {
     const float(*s1[2])[16] = {xa, xc};
     float(*d1[2])[16] = {h1[0], h1[1]};
-    policy_tiles<8, 2>(LA1, PIN / 4, s1, wave, 4, d1, true, lane);  // 512
+    policy_tiles<4, 2>(LA1, PIN / 4, s1, wave, 8, d1, true, lane);  // 512
   }
   __syncthreads();
   {
     const float(*s2[2])[16] = {h1[0], h1[1]};
     float(*d2[2])[16] = {h2[0], h2[1]};
-    policy_tiles<4, 2>(LA2, 512 / 4, s2, wave, 4, d2, true, lane);  // 256
+    policy_tiles<2, 2>(LA2, 512 / 4, s2, wave, 8, d2, true, lane);  // 256
   }
   __syncthreads();
   {
     const float(*s3[2])[16] = {h2[0], h2[1]};
     float(*d3[2])[16] = {h1[0], h1[1]};
-    policy_tiles<2, 2>(LA3, 256 / 4, s3, wave, 4, d3, true, lane);  // 128
+    policy_tiles<1, 2>(LA3, 256 / 4, s3, wave, 8, d3, true, lane);  // 128
   }
   __syncthreads();
   if (wave < 2) {
@@ -386,7 +396,7 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
   for (int i = 0; i < GO1_POLICY_LAYERS; ++i)
     if (!args->layers[i].w || !args->layers[i].b) return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer");
   go1_policy_args P = *args;
-  hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(256), 0, (hipStream_t)stream, P);
+  hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(512), 0, (hipStream_t)stream, P);
   RT_TRY(hipGetLastError());
   return GO1_OK_RT;
 }

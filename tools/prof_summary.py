@@ -66,8 +66,9 @@ def main():
             w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
             w.writeheader()
             w.writerows(rows)
-    means, counts, meta = counters(src)
-    out = {"kernel": "go1_step_kernel<false>", "passes_per_counter": counts, "per_dispatch_mean": means,
+    match = sys.argv[4] if len(sys.argv) > 4 else "go1_step_kernel"
+    means, counts, meta = counters(src, match)
+    out = {"kernel": match, "passes_per_counter": counts, "per_dispatch_mean": means,
            "resources": meta}
     if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
         fetch = means["FETCH_SIZE"] * 1024
