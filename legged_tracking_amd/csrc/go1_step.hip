@@ -328,6 +328,17 @@ __device__ __forceinline__ void rigid_si(const float* body, float mscale, SI& I)
   I.c[0] = m; I.c[1] = 0.0f; I.c[2] = 0.0f; I.c[3] = m; I.c[4] = 0.0f; I.c[5] = m;
 }
 
+// the 12 leg bodies' rigid inertias (mass scale 1), 21 floats each, precomputed in LDS
+#define GO1_RIG_OFF (GO1_MODEL_FLOATS + 24)
+#define GO1_PHYS_LDS (GO1_RIG_OFF + 12 * 21)
+__device__ __forceinline__ void rigid_si_lds(const float* lds, int body, SI& I) {
+  const float* r = lds + GO1_RIG_OFF + body * 21;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { I.a[i] = r[i]; I.c[i] = r[15 + i]; }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) I.b[i] = r[6 + i];
+}
+
 // force cross product v x* f
 __device__ __forceinline__ void crf(const float* v, const float* f, float* o) {
   float a[3], b[3], c[3];
@@ -637,11 +648,14 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
 // two per lane, so each wave has four envs and the whole grid fills every SIMD.
 // cf_out: this lane's reported contact forces (thigh, calf, foot of its leg; base).
-__device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const float* tau, float h, const float* g,
-                             float friction, float payload, const Terr& T, int leg, int role, bool cf_out,
-                             float* cf_leg, float* cf_base) {
+// `lds` = the model block (GO1_MODEL_FLOATS) followed by the 24 hard joint limits, staged
+// in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
+// because the physics keeps every VGPR busy, and LDS answers faster than the caches.
+__device__ void phys_substep(const go1_config* __restrict__ cfg, const float* lds, Phys& S, const float* tau, float h,
+                             const float* g, float friction, float payload, const Terr& T, int leg, int role,
+                             bool cf_out, float* cf_leg, float* cf_base) {
 #pragma clang fp contract(fast)
-  const float* model = cfg->model;
+  const float* model = lds;
   MARK(phys_begin);
   const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
   float R[9];
@@ -691,7 +705,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
       // rigid inertia about the link origin, bias force v x* I v, minus gravity
       const float* B = model + 10 * (1 + leg * 3 + j);
       SI I;
-      rigid_si(B, 1.0f, I);
+      rigid_si_lds(lds, leg * 3 + j, I);
       float hm[6];
       si_mul(I, vj, hm);
       crf(vj, hm, pA[j]);
@@ -767,13 +781,13 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
   float pp6[6];
   {
     SI IA;
-    rigid_si(model + 10 * (1 + leg * 3 + 2), 1.0f, IA);
+    rigid_si_lds(lds, leg * 3 + 2, IA);
 #pragma unroll
     for (int j = 2; j >= 0; --j) {
       const int ax = j == 0 ? 0 : 1;
       const int dof = leg * 3 + j;
       float t = tau[j];
-      const float lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1];
+      const float lo = lds[GO1_MODEL_FLOATS + dof * 2], hi = lds[GO1_MODEL_FLOATS + dof * 2 + 1];
       if (S.q[j] > hi) t -= cfg->limit_stiffness * (S.q[j] - hi) + cfg->limit_damping * S.qd[j];
       else if (S.q[j] < lo) t -= cfg->limit_stiffness * (S.q[j] - lo) + cfg->limit_damping * S.qd[j];
 #pragma unroll
@@ -802,7 +816,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, Phys& S, const 
       xform_inertia(ax, cs[j][0], cs[j][1], origin + j * 3, Ia, It);
       xfT(ax, cs[j][0], cs[j][1], origin + j * 3, pa, pt);
       if (j > 0) {
-        rigid_si(model + 10 * (1 + leg * 3 + j - 1), 1.0f, IA);
+        rigid_si_lds(lds, leg * 3 + j - 1, IA);
         si_add(IA, It);
 #pragma unroll
         for (int i = 0; i < 6; ++i) pA[j - 1][i] += pt[i];
@@ -1011,6 +1025,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
   __shared__ float2 s_patch[SEPB][PSZ * PSZ];
   __shared__ int s_patch_meta[SEPB][3];
+  __shared__ float s_phys[GO1_PHYS_LDS];
+  for (int i = lane; i < GO1_MODEL_FLOATS + 24; i += 64)
+    s_phys[i] = i < GO1_MODEL_FLOATS ? c->model[i] : c->hard_limits[i - GO1_MODEL_FLOATS];
+  if (lane < 12) {
+    SI I;
+    rigid_si(c->model + 10 * (1 + lane), 1.0f, I);
+    float* r = s_phys + GO1_RIG_OFF + lane * 21;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { r[i] = I.a[i]; r[15 + i] = I.c[i]; }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r[6 + i] = I.b[i];
+  }
+  __syncthreads();
   if (c->terrain_kind == 1) {
     const int tix = K.ter.env_tile[e];
     T.tile = K.ter.tiles + (size_t)tix * 2 * c->hf_nx * c->hf_ny;
@@ -1135,7 +1162,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
 #ifndef GO1_ABL_NO_PHYS
-        phys_substep(c, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_leg, cf_base);
+        phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_leg, cf_base);
 #else
         (void)last; (void)h;
         P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];

@@ -17,7 +17,7 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(REPO, "legged_tracking_amd", "csrc", "go1_step.hip")
     extra = sys.argv[1:]
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
                     "-DGO1_ISA_MARKS", *extra, "-c", "--save-temps", "-o", os.path.join(OUT, "k.o"), src],
                    cwd=OUT, check=True)
     s = open(os.path.join(OUT, "go1_step-hip-amdgcn-amd-amdhsa-gfx950.s")).read().splitlines()
