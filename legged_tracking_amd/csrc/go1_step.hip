@@ -328,17 +328,6 @@ __device__ __forceinline__ void rigid_si(const float* body, float mscale, SI& I)
   I.c[0] = m; I.c[1] = 0.0f; I.c[2] = 0.0f; I.c[3] = m; I.c[4] = 0.0f; I.c[5] = m;
 }
 
-// the 12 leg bodies' rigid inertias (mass scale 1), 21 floats each, precomputed in LDS
-#define GO1_RIG_OFF (GO1_MODEL_FLOATS + 24)
-#define GO1_PHYS_LDS (GO1_RIG_OFF + 12 * 21)
-__device__ __forceinline__ void rigid_si_lds(const float* lds, int body, SI& I) {
-  const float* r = lds + GO1_RIG_OFF + body * 21;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) { I.a[i] = r[i]; I.c[i] = r[15 + i]; }
-#pragma unroll
-  for (int i = 0; i < 9; ++i) I.b[i] = r[6 + i];
-}
-
 // force cross product v x* f
 __device__ __forceinline__ void crf(const float* v, const float* f, float* o) {
   float a[3], b[3], c[3];
@@ -705,7 +694,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       // rigid inertia about the link origin, bias force v x* I v, minus gravity
       const float* B = model + 10 * (1 + leg * 3 + j);
       SI I;
-      rigid_si_lds(lds, leg * 3 + j, I);
+      rigid_si(B, 1.0f, I);
       float hm[6];
       si_mul(I, vj, hm);
       crf(vj, hm, pA[j]);
@@ -781,7 +770,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
   float pp6[6];
   {
     SI IA;
-    rigid_si_lds(lds, leg * 3 + 2, IA);
+    rigid_si(model + 10 * (1 + leg * 3 + 2), 1.0f, IA);
 #pragma unroll
     for (int j = 2; j >= 0; --j) {
       const int ax = j == 0 ? 0 : 1;
@@ -816,7 +805,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       xform_inertia(ax, cs[j][0], cs[j][1], origin + j * 3, Ia, It);
       xfT(ax, cs[j][0], cs[j][1], origin + j * 3, pa, pt);
       if (j > 0) {
-        rigid_si_lds(lds, leg * 3 + j - 1, IA);
+        rigid_si(model + 10 * (1 + leg * 3 + j - 1), 1.0f, IA);
         si_add(IA, It);
 #pragma unroll
         for (int i = 0; i < 6; ++i) pA[j - 1][i] += pt[i];
@@ -1025,18 +1014,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
   __shared__ float2 s_patch[SEPB][PSZ * PSZ];
   __shared__ int s_patch_meta[SEPB][3];
-  __shared__ float s_phys[GO1_PHYS_LDS];
+  __shared__ float s_phys[GO1_MODEL_FLOATS + 24];
   for (int i = lane; i < GO1_MODEL_FLOATS + 24; i += 64)
     s_phys[i] = i < GO1_MODEL_FLOATS ? c->model[i] : c->hard_limits[i - GO1_MODEL_FLOATS];
-  if (lane < 12) {
-    SI I;
-    rigid_si(c->model + 10 * (1 + lane), 1.0f, I);
-    float* r = s_phys + GO1_RIG_OFF + lane * 21;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) { r[i] = I.a[i]; r[15 + i] = I.c[i]; }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) r[6 + i] = I.b[i];
-  }
   __syncthreads();
   if (c->terrain_kind == 1) {
     const int tix = K.ter.env_tile[e];
