@@ -113,6 +113,34 @@ def cpu_baseline(n_envs, budget_s=12.0, max_steps=400):
                       f"{dt:.1f} s on {threads} threads of {cores} visible ({model})"}
 
 
+def env_sweep(n, dev, steps=100, warmup=10):
+    """Env-only throughput at n envs on this GPU (4k ... 256k envs/GPU sweep)."""
+    import torch
+    from legged_tracking_amd import config as CF, native, terrain as T
+    cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=32, cols=32)
+    c = CF.build_abi_config(cfg, n_envs=n)
+    td = T.build(cfg, n, np.random.RandomState(11))
+    g = native.Go1Native(c, str(dev))
+    g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    rng = np.random.default_rng(5)
+    g.state["friction"].copy_(torch.from_numpy(rng.uniform(0.1, 3.0, (n, 1)).astype(np.float32)))
+    g.reset_envs(torch.ones(n, dtype=torch.bool, device=dev), rng_seed=5, rng_step=0)
+    g.state["episode_length"].copy_(torch.from_numpy(rng.integers(0, 500, (n, 1)).astype(np.int32)))
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    grav, gvec = CF.gravity_state([0.1, -0.2, 0.3])
+    ring = torch.randn((8, n, 12), device=dev)
+    for k in range(warmup):
+        g.step(ring[k % 8], gvec, grav, scales, rng_seed=5, rng_step=1 + k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        g.step(ring[k % 8], gvec, grav, scales, rng_seed=5, rng_step=1 + warmup + k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    g.close()
+    return {"envs_per_gpu": n, "value": n * steps / dt, "ms_per_step": dt / steps * 1e3}
+
+
 def rollout_rate(n, dev, steps, warmup, prof=None):
     """Secondary line (SURVEY 8(d) "report both env-only and rollout (act + step) rates"):
     the Runner's rollout loop -- ActorCritic.act + value (hipBLASLt GEMMs), env.step
@@ -167,6 +195,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--rollout-only", action="store_true", help="profile helper: time only the rollout loop")
+    ap.add_argument("--sweep", default="", help="comma-separated envs/GPU for an extra size sweep (e.g. 16384,65536)")
     args = ap.parse_args()
 
     import torch
@@ -266,6 +295,8 @@ def main():
                          "valu_issue_frac_pmc": valu_frac,
                          "note": "latency/VALU-issue bound, not HBM bound: see DESIGN.md section 5"},
         }
+        if args.sweep:
+            line["sweep"] = [env_sweep(int(x), dev) for x in args.sweep.split(",")]
         if not args.no_rollout:
             line["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24))
         if not args.no_cpu_baseline:
