@@ -227,14 +227,19 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const 
     }
 }
 
-__global__ __launch_bounds__(512) void policy_kernel(go1_policy_args P) {
+#ifndef GO1_POLICY_WAVES
+#define GO1_POLICY_WAVES 16
+#endif
+constexpr int PW = GO1_POLICY_WAVES;  // waves per workgroup (8: two per SIMD, 16: four per SIMD)
+
+__global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   __shared__ float xa[PIN][16], xc[PIN][16];  // actor / critic inputs (adaptation uses xa)
   __shared__ float h1[2][512][16];             // layer-1 outputs (actor, critic); layer 3 reuses it
   __shared__ float h2[2][256][16];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int e0 = blockIdx.x * 16;
   const int ne = min(16, P.n_envs - e0);
-  for (int idx = tid; idx < 16 * PIN; idx += 512) {
+  for (int idx = tid; idx < 16 * PIN; idx += 64 * PW) {
     const int e = idx / PIN, k = idx - e * PIN;
     float v = 0.0f;
     if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
@@ -247,13 +252,13 @@ __global__ __launch_bounds__(512) void policy_kernel(go1_policy_args P) {
   {
     const float(*s0[1])[16] = {xa};
     float(*d0[1])[16] = {h1[0]};
-    policy_tiles<2, 1>(Ls + 0, PIN / 4, s0, wave, 8, d0, true, lane);  // 256
+    policy_tiles<16 / PW, 1>(Ls + 0, PIN / 4, s0, wave, PW, d0, true, lane);  // 256
   }
   __syncthreads();
   {
     const float(*s0[1])[16] = {h1[0]};
     float(*d0[1])[16] = {h2[0]};
-    policy_tiles<1, 1>(Ls + 1, 256 / 4, s0, wave, 8, d0, true, lane);  // 128
+    if (wave < 8) policy_tiles<1, 1>(Ls + 1, 256 / 4, s0, wave, 8, d0, true, lane);  // 128
   }
   __syncthreads();
   if (wave == 0) {
@@ -281,19 +286,27 @@ __global__ __launch_bounds__(512) void policy_kernel(go1_policy_args P) {
   {
     const float(*s1[2])[16] = {xa, xc};
     float(*d1[2])[16] = {h1[0], h1[1]};
-    policy_tiles<4, 2>(LA1, PIN / 4, s1, wave, 8, d1, true, lane);  // 512
+    policy_tiles<32 / PW, 2>(LA1, PIN / 4, s1, wave, PW, d1, true, lane);  // 512
   }
   __syncthreads();
   {
     const float(*s2[2])[16] = {h1[0], h1[1]};
     float(*d2[2])[16] = {h2[0], h2[1]};
-    policy_tiles<2, 2>(LA2, 512 / 4, s2, wave, 8, d2, true, lane);  // 256
+    policy_tiles<16 / PW, 2>(LA2, 512 / 4, s2, wave, PW, d2, true, lane);  // 256
   }
   __syncthreads();
   {
     const float(*s3[2])[16] = {h2[0], h2[1]};
     float(*d3[2])[16] = {h1[0], h1[1]};
-    policy_tiles<1, 2>(LA3, 256 / 4, s3, wave, 8, d3, true, lane);  // 128
+    if (PW == 8) {
+      policy_tiles<1, 2>(LA3, 256 / 4, s3, wave, 8, d3, true, lane);  // 128
+    } else {  // one tile per wave: waves 0-7 the actor's, 8-15 the critic's
+      const int l = wave >> 3;
+      const float(*s1[1])[16] = {l ? h2[1] : h2[0]};
+      float(*d1[1])[16] = {l ? h1[1] : h1[0]};
+      const PolicyLayer L3 = l ? Ls[9] : Ls[5];
+      policy_tiles<1, 1>(&L3, 256 / 4, s1, wave & 7, 8, d1, true, lane);
+    }
   }
   __syncthreads();
   if (wave < 2) {
@@ -396,7 +409,7 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
   for (int i = 0; i < GO1_POLICY_LAYERS; ++i)
     if (!args->layers[i].w || !args->layers[i].b) return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer");
   go1_policy_args P = *args;
-  hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(512), 0, (hipStream_t)stream, P);
+  hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(64 * PW), 0, (hipStream_t)stream, P);
   RT_TRY(hipGetLastError());
   return GO1_OK_RT;
 }
