@@ -407,17 +407,36 @@ __device__ __forceinline__ void rot_congruence(int ax, float c, float s, const f
   }
 }
 
+// Q = E^T M E for a symmetric M stored (xx xy xz yy yz zz) into a full 3x3 Q.  E^T rotates
+// the two indices (p, r) other than the axis f by R = [[c, -s'], [s', c]] (s' = s for x,
+// -s for y), so with c2 = c^2 - s'^2, s2 = 2 c s', h = (Mpp + Mrr) / 2, d = (Mpp - Mrr) / 2:
+//   Qff = Mff, Qfp = c Mfp - s' Mfr, Qfr = s' Mfp + c Mfr,
+//   Qpp = h + d c2 - Mpr s2, Qrr = h - d c2 + Mpr s2, Qpr = d s2 + Mpr c2.
+__device__ __forceinline__ void rot_congruence_sym(int ax, float c, float s, float c2, float s2, const float* m,
+                                                   float* Q) {
+  const int f = ax, pI = ax == 0 ? 1 : 0, rI = 2;
+  const float sp = ax == 0 ? s : -s;
+  auto at = [&](int i, int j) -> float { return S3(m, i, j); };
+  const float mff = at(f, f), mfp = at(f, pI), mfr = at(f, rI), mpp = at(pI, pI), mrr = at(rI, rI), mpr = at(pI, rI);
+  const float h = 0.5f * (mpp + mrr), d = 0.5f * (mpp - mrr);
+  const float qfp = c * mfp - sp * mfr, qfr = sp * mfp + c * mfr;
+  const float qpp = h + d * c2 - mpr * s2, qrr = h - d * c2 + mpr * s2, qpr = d * s2 + mpr * c2;
+  Q[f * 3 + f] = mff;
+  Q[f * 3 + pI] = qfp; Q[pI * 3 + f] = qfp;
+  Q[f * 3 + rI] = qfr; Q[rI * 3 + f] = qfr;
+  Q[pI * 3 + pI] = qpp; Q[rI * 3 + rI] = qrr;
+  Q[pI * 3 + rI] = qpr; Q[rI * 3 + pI] = qpr;
+}
+
 // X^T Ia X for X = [[E, 0], [-E r~, E]]: rotate the blocks by E^T(.)E, then translate by r:
 //   A'' = A' + r~ B'^T - B' r~ - r~ C' r~ ,  B'' = B' + r~ C' ,  C'' = C'.
 __device__ __forceinline__ void xform_inertia(int ax, float cq, float sq, const float* r, const SI& In, SI& Out) {
-  float M[9], A[9], B[9], C[9];
-  M[0] = In.a[0]; M[1] = In.a[1]; M[2] = In.a[2]; M[3] = In.a[1]; M[4] = In.a[3]; M[5] = In.a[4];
-  M[6] = In.a[2]; M[7] = In.a[4]; M[8] = In.a[5];
-  rot_congruence(ax, cq, sq, M, A);
+  float A[9], B[9], C[9];
+  const float sp = ax == 0 ? sq : -sq;
+  const float c2 = cq * cq - sp * sp, s2 = 2.0f * cq * sp;
+  rot_congruence_sym(ax, cq, sq, c2, s2, In.a, A);
   rot_congruence(ax, cq, sq, In.b, B);
-  M[0] = In.c[0]; M[1] = In.c[1]; M[2] = In.c[2]; M[3] = In.c[1]; M[4] = In.c[3]; M[5] = In.c[4];
-  M[6] = In.c[2]; M[7] = In.c[4]; M[8] = In.c[5];
-  rot_congruence(ax, cq, sq, M, C);
+  rot_congruence_sym(ax, cq, sq, c2, s2, In.c, C);
   // translation, with (M r~) row i = (row i of M) x r and r~ B'^T = -(B' r~)^T
   float RC[9], BR[9], RCR[9];
 #pragma unroll
@@ -786,17 +805,19 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       const float invD = frcp(D[j]);
       D[j] = invD;  // the forward pass only needs 1 / D
       const float Ua[3] = {U[j][0], U[j][1], U[j][2]}, Ul[3] = {U[j][3], U[j][4], U[j][5]};
-      SI Ia;
-      Ia.a[0] = IA.a[0] - Ua[0] * Ua[0] * invD; Ia.a[1] = IA.a[1] - Ua[0] * Ua[1] * invD;
-      Ia.a[2] = IA.a[2] - Ua[0] * Ua[2] * invD; Ia.a[3] = IA.a[3] - Ua[1] * Ua[1] * invD;
-      Ia.a[4] = IA.a[4] - Ua[1] * Ua[2] * invD; Ia.a[5] = IA.a[5] - Ua[2] * Ua[2] * invD;
+      const float Va[3] = {Ua[0] * invD, Ua[1] * invD, Ua[2] * invD};  // U / D
+      const float Vl[3] = {Ul[0] * invD, Ul[1] * invD, Ul[2] * invD};
+      SI Ia;  // IA - U U^T / D (fused multiply-subtracts)
+      Ia.a[0] = IA.a[0] - Ua[0] * Va[0]; Ia.a[1] = IA.a[1] - Ua[0] * Va[1];
+      Ia.a[2] = IA.a[2] - Ua[0] * Va[2]; Ia.a[3] = IA.a[3] - Ua[1] * Va[1];
+      Ia.a[4] = IA.a[4] - Ua[1] * Va[2]; Ia.a[5] = IA.a[5] - Ua[2] * Va[2];
 #pragma unroll
       for (int a = 0; a < 3; ++a)
 #pragma unroll
-        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Ua[a] * Ul[b] * invD;
-      Ia.c[0] = IA.c[0] - Ul[0] * Ul[0] * invD; Ia.c[1] = IA.c[1] - Ul[0] * Ul[1] * invD;
-      Ia.c[2] = IA.c[2] - Ul[0] * Ul[2] * invD; Ia.c[3] = IA.c[3] - Ul[1] * Ul[1] * invD;
-      Ia.c[4] = IA.c[4] - Ul[1] * Ul[2] * invD; Ia.c[5] = IA.c[5] - Ul[2] * Ul[2] * invD;
+        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Ua[a] * Vl[b];
+      Ia.c[0] = IA.c[0] - Ul[0] * Vl[0]; Ia.c[1] = IA.c[1] - Ul[0] * Vl[1];
+      Ia.c[2] = IA.c[2] - Ul[0] * Vl[2]; Ia.c[3] = IA.c[3] - Ul[1] * Vl[1];
+      Ia.c[4] = IA.c[4] - Ul[1] * Vl[2]; Ia.c[5] = IA.c[5] - Ul[2] * Vl[2];
       float Iac[6], pa[6], pt[6];
       si_mul(Ia, cj[j], Iac);
 #pragma unroll
