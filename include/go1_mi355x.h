@@ -169,7 +169,8 @@ typedef struct go1_step_args {
   float* rew;                  /* (n_envs) */
   uint8_t* reset;              /* (n_envs) bool */
   uint8_t* time_out;           /* (n_envs) bool */
-  uint8_t* extras_time_outs;   /* (n_envs) bool, rebound only on steps with a reset (:289-291) */
+  uint8_t* extras_time_outs;   /* (n_envs) bool, rebound only on steps with a reset (:289-291);
+                                  current after go1_sync_time_outs (see below) */
   int32_t* any_reset;          /* reserved (the library keeps its own flag words) */
   float* contact_forces;       /* (n_envs, 17, 3) or NULL */
   /* optional debug outputs (NULL = not written) */
@@ -201,6 +202,11 @@ int go1_create(const go1_config* cfg, go1_handle** out);
 int go1_bind(go1_handle* h, const go1_state* state);
 int go1_set_terrain(go1_handle* h, const go1_terrain* terrain);
 int go1_step(go1_handle* h, const go1_step_args* args, void* stream);
+/* extras["time_outs"] (:289-291) is rebound to time_out only on steps with a reset.  The
+ * rebinding for step k is applied by the kernel of step k+1 (no launch of its own); call
+ * this to have extras_time_outs of the last go1_step current now (one tiny launch,
+ * idempotent; the env's extras["time_outs"] read does it). */
+int go1_sync_time_outs(go1_handle* h, void* stream);
 /* Reset envs whose mask[e] != 0: reset_idx semantics (:218-296) incl. DR draws;
  * uniforms NULL -> Philox(rng_seed, rng_step). */
 int go1_reset_envs(go1_handle* h, const uint8_t* mask, const float* uniforms, uint64_t rng_seed,

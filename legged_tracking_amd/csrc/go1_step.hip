@@ -947,7 +947,14 @@ struct KArgs {
   go1_state st;
   go1_terrain ter;
   go1_step_args a;
-  int32_t* any_reset;
+  // extras["time_outs"] rebinding (:289-291) without a launch of its own: flag words
+  // [3] ("some env reset in step k" for k mod 3); this step sets flags[cur], applies the
+  // previous step's rebinding for its own envs in the prologue (prev_time_out != NULL),
+  // and clears flags[nxt] for the next step.
+  int32_t* flags;
+  int cur, prv, nxt;
+  const uint8_t* prev_time_out;
+  uint8_t* prev_extras;
 };
 
 // reset_idx for one env, computed redundantly by the 4 lanes of its quad (:218-296)
@@ -1014,6 +1021,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   MlpFrag F;
   mlp_load(c->actuator, lane, F);
   const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset};
+  // the previous step's extras["time_outs"] rebinding, for this wave's envs (flags of the
+  // previous launch are complete now), and the flag the next launch will set is cleared
+  if (K.prev_time_out && sub16 == 0 && K.flags[K.prv]) K.prev_extras[e] = K.prev_time_out[e];
+  if (blockIdx.x == 0 && lane == 0) K.flags[K.nxt] = 0;
   const size_t d0 = (size_t)e * NDOF + leg * 3;
   const float* lag_in = st.lag + (size_t)e * 84 + leg * 3;
 
@@ -1518,15 +1529,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (A.dbg_reached) A.dbg_reached[e] = reached;
   }
   // one atomic per wave when any env of the wave reset (extras["time_outs"] rebinding, :289-291)
-  if (__ballot(reset && leg == 0) != 0ull && (threadIdx.x & 63) == 0) atomicOr(K.any_reset, 1);
+  if (__ballot(reset && leg == 0) != 0ull && (threadIdx.x & 63) == 0) atomicOr(K.flags + K.cur, 1);
 }
 
-// extras["time_outs"] is rebound to time_out_buf only on steps where reset_idx ran.
-__global__ void go1_finalize_kernel(int n, const int32_t* __restrict__ any_reset, int32_t* __restrict__ next_flag,
-                                    const uint8_t* __restrict__ time_out, uint8_t* __restrict__ extras) {
+// extras["time_outs"] = time_out of the last step, if any env reset in it (go1_sync_time_outs:
+// the rebinding of that step, applied on demand; idempotent).
+__global__ void go1_finalize_kernel(int n, const int32_t* __restrict__ flag, const uint8_t* __restrict__ time_out,
+                                    uint8_t* __restrict__ extras) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) *next_flag = 0;
-  if (e < n && *any_reset) extras[e] = time_out[e];
+  if (e < n && *flag) extras[e] = time_out[e];
 }
 
 // reset of masked envs (env.reset(), :46-55 of trajectory_tracking/__init__.py)
@@ -1590,8 +1601,10 @@ struct go1_handle {
   go1_state st;
   go1_terrain ter;
   bool bound = false, has_terrain = false;
-  int32_t* d_flags = nullptr;  // any_reset double buffer
-  uint64_t parity = 0;
+  int32_t* d_flags = nullptr;  // 3 "some env reset in step k" words (k mod 3)
+  uint64_t count = 0;          // go1_step calls so far
+  const uint8_t* prev_time_out = nullptr;
+  uint8_t* prev_extras = nullptr;
 };
 
 static thread_local std::string g_err;
@@ -1635,7 +1648,7 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   if (!h) return fail(GO1_E_ARG, "go1_create: out of host memory");
   h->cfg = *cfg;
   hipError_t e1 = hipMalloc(&h->d_cfg, sizeof(go1_config));
-  hipError_t e2 = hipMalloc(&h->d_flags, 2 * sizeof(int32_t));
+  hipError_t e2 = hipMalloc(&h->d_flags, 3 * sizeof(int32_t));
   if (e1 != hipSuccess || e2 != hipSuccess) {
     if (h->d_cfg) (void)hipFree(h->d_cfg);
     if (h->d_flags) (void)hipFree(h->d_flags);
@@ -1643,7 +1656,7 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
     return fail(GO1_E_HIP, "go1_create: hipMalloc failed");
   }
   HIP_TRY(hipMemcpy(h->d_cfg, cfg, sizeof(go1_config), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(h->d_flags, 0, 2 * sizeof(int32_t)));
+  HIP_TRY(hipMemset(h->d_flags, 0, 3 * sizeof(int32_t)));
   *out = h;
   return GO1_OK;
 }
@@ -1681,22 +1694,34 @@ int go1_step(go1_handle* h, const go1_step_args* a, void* stream) {
   if (inj && (!a->inj_root || !a->inj_contact)) return fail(GO1_E_ARG, "go1_step: partial injected state");
   hipStream_t s = (hipStream_t)stream;
   const int n = h->cfg.n_envs;
-  int32_t* flag = h->d_flags + (h->parity & 1);
-  int32_t* next = h->d_flags + ((h->parity + 1) & 1);
-  h->parity++;
   KArgs K;
   K.st = h->st;
   K.ter = h->ter;
   K.a = *a;
-  K.any_reset = flag;
+  K.flags = h->d_flags;
+  K.cur = (int)(h->count % 3);
+  K.prv = (int)((h->count + 2) % 3);
+  K.nxt = (int)((h->count + 1) % 3);
+  K.prev_time_out = h->prev_time_out;
+  K.prev_extras = h->prev_extras;
   dim3 grid(n / SEPB), block(TPB);
   if (a->ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_begin, s));
   if (inj) hipLaunchKernelGGL(go1_step_kernel<true>, grid, block, 0, s, h->d_cfg, K);
   else hipLaunchKernelGGL(go1_step_kernel<false>, grid, block, 0, s, h->d_cfg, K);
   HIP_TRY(hipGetLastError());
   if (a->ev_end) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_end, s));
-  hipLaunchKernelGGL(go1_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, flag, next, a->time_out,
-                     a->extras_time_outs);
+h->prev_time_out = a->time_out;
+  h->prev_extras = a->extras_time_outs;
+  h->count++;
+  return GO1_OK;
+}
+
+int go1_sync_time_outs(go1_handle* h, void* stream) {
+  if (!h) return fail(GO1_E_ARG, "go1_sync_time_outs: null handle");
+  if (!h->prev_time_out) return GO1_OK;  // no step yet
+  const int n = h->cfg.n_envs;
+  hipLaunchKernelGGL(go1_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n,
+                     h->d_flags + (h->count + 2) % 3, h->prev_time_out, h->prev_extras);
   HIP_TRY(hipGetLastError());
   return GO1_OK;
 }

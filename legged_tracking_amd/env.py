@@ -291,7 +291,8 @@ class LeggedRobot:
         dict.__setitem__(ex, "train/episode", self._train_ep)
         dict.__setitem__(ex, "eval/episode", self._eval_ep)
         dict.__setitem__(ex, "timeouts", self._timeouts)
-        dict.__setitem__(ex, "time_outs", torch.zeros(self.num_train_envs, dtype=torch.bool, device=self.device))
+        # the rebinding of the last step is applied on read (go1_sync_time_outs)
+        ex.set_lazy("time_outs", lambda: self._sim.sync_time_outs()[: self.num_train_envs])
 
     # ------------------------------------------------------------------ views
     @property
@@ -409,7 +410,6 @@ class LeggedRobot:
         self._rng_step += 1
         self._elog.advance()
         self._slot = (s + 1) % OUT_RING
-        dict.__setitem__(self.extras, "time_outs", self._sim.extras_time_outs)
         # post-physics host bookkeeping (:126, :826-830, :171-182)
         self.common_step_counter += 1
         c = self.common_step_counter

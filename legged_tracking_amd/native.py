@@ -36,6 +36,7 @@ def lib():
     l.go1_set_terrain.argtypes = [C.c_void_p, C.POINTER(abi.Go1Terrain)]
     l.go1_step.argtypes = [C.c_void_p, C.POINTER(abi.Go1StepArgs), C.c_void_p]
     l.go1_reset_envs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
+    l.go1_sync_time_outs.argtypes = [C.c_void_p, C.c_void_p]
     l.go1_actuator_net.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     l.go1_destroy.argtypes = [C.c_void_p]
     if l.go1_abi_version() != 1:
@@ -170,6 +171,12 @@ class Go1Native:
         a.aux = aux.data_ptr() if aux is not None else None
         a.ev_begin, a.ev_end = events if events is not None else (None, None)  # hipEvent_t pair as ints
         _check(self._lib_step(self.h, C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+
+    def sync_time_outs(self):
+        """Make extras_time_outs current for the last step (the rebinding of step k is
+        otherwise applied by the kernel of step k+1)."""
+        _check(lib().go1_sync_time_outs(self.h, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        return self.extras_time_outs
 
     def reset_envs(self, mask, uniforms=None, rng_seed=0, rng_step=0):
         m = mask.to(torch.uint8).contiguous()

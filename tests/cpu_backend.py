@@ -65,6 +65,9 @@ class OracleBackend:
             aux.copy_(torch.from_numpy(o["aux"]))
         return o
 
+    def sync_time_outs(self):
+        return self.extras_time_outs
+
     def reset_envs(self, mask, uniforms=None, rng_seed=0, rng_step=0):
         O.reset_envs(self.cfg, self.state.np, self.ter, mask.numpy().astype(np.uint8), rng_seed=rng_seed,
                      rng_step=rng_step)

@@ -71,6 +71,8 @@ def test_fused_step_replays_reference_fixture(name):
         elog.fill_(float("nan"))
         g.step(_dev(inp["actions"]), inp["gravity_vec"], inp["sim_gravity"], inp["reward_scales"], uniforms=u,
                inj=inj, debug=dbg, episode_log=elog, aux=aux)
+        if t % 2 == 0:
+            g.sync_time_outs()  # odd steps: the next step's kernel applies the rebinding itself
         torch.cuda.synchronize()
         # oracle on the same inputs
         ost = st.copy()
@@ -111,11 +113,13 @@ def test_fused_step_replays_reference_fixture(name):
         np.testing.assert_allclose(obs, d[f"s{t}/obs"], rtol=2e-5, atol=2e-5)
         np.testing.assert_allclose(g.rew.cpu().numpy(), d[f"s{t}/rew"], rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(dbg["torques"].cpu().numpy(), d[f"s{t}/torques"], rtol=2e-5, atol=2e-5)
-        if d[f"s{t}/extras_time_outs"].size:
+        if t % 2 == 0 and d[f"s{t}/extras_time_outs"].size:
             # extras["time_outs"] is rebound only on steps with a reset; the stale
             # buffer from an earlier step is not part of the per-step fixture
             if d[f"s{t}/reset"].any():
                 np.testing.assert_array_equal(g.extras_time_outs.cpu().numpy(), d[f"s{t}/extras_time_outs"])
+        if t % 2 == 0 and t > 0 and d[f"s{t - 1}/reset"].any() and not d[f"s{t}/reset"].any():
+            np.testing.assert_array_equal(g.extras_time_outs.cpu().numpy(), d[f"s{t - 1}/time_out"])
 
 
 def _sim_setup(n, terrain="single_path", seed=0):
