@@ -42,7 +42,7 @@ import torch
 from . import abi, config as CF, layout as L, terrain as T
 
 OUT_RING = 4
-EPISODE_RING = 64
+EPISODE_RING = 64  # steps per half of the episode-log ring (fewer for very large n_envs)
 _LAZY = object()
 
 
@@ -98,11 +98,12 @@ class EpisodeLogRing:
     def __init__(self, env, n, device):
         self.env = env
         self.dev = device
-        self.buf = torch.zeros((2, EPISODE_RING, n, abi.GO1_EPISODE_LOG), device=device)
+        self.R = R = int(min(EPISODE_RING, max(4, (1 << 22) // max(n, 1))))  # <= 16 MB per half
+        self.buf = torch.zeros((2, R, n, abi.GO1_EPISODE_LOG), device=device)
         self.half, self.slot, self.done = 0, 0, 0  # write position; slots of this half already drained
         self.cuda = device.type == "cuda"
         if self.cuda:
-            self.host = torch.zeros((2, EPISODE_RING, n, abi.GO1_EPISODE_LOG), pin_memory=True)
+            self.host = torch.zeros((2, R, n, abi.GO1_EPISODE_LOG), pin_memory=True)
             self.side = torch.cuda.Stream(device)
             self.copied = [None, None]  # event per half: host copy finished
         self.inflight = None  # (half, first slot) copied to host, not yet turned into deque entries
@@ -115,7 +116,7 @@ class EpisodeLogRing:
 
     def advance(self):
         self.slot += 1
-        if self.slot == EPISODE_RING:
+        if self.slot == self.R:
             h, first = self.half, self.done
             self.half, self.slot, self.done = h ^ 1, 0, 0
             if self.cuda:

@@ -84,7 +84,7 @@ def test_episode_log_and_timeouts_follow_reset_order():
     env._sim.step = spy
     # stagger episode ends so that resets land on many steps, past one ring wrap
     env.episode_length_buf = torch.arange(32, dtype=torch.int32) * 3 + 500 - 90
-    for _ in range(E.EPISODE_RING + 30):
+    for _ in range(env._elog.R + 30):
         env.step(torch.zeros(32, 12))
     ep = env.extras["train/episode"]
     want = {k: [] for k in ("episode_length", "reached", "goal_distance")}
