@@ -270,6 +270,10 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) { return v 
 // =====================================================================
 //                  native articulated-body integrator (f32)
 // =====================================================================
+// Everything from here to the step kernel is integrator code (compared with the f64
+// oracle within a tolerance): FMA contraction on, including in the inlined helpers
+// (a pragma inside phys_substep alone does not reach them).
+#pragma clang fp contract(fast)
 // Spatial vectors (angular; linear).  6x6 symmetric articulated inertia stored as
 // [[A, B], [B^T, C]], A and C symmetric (xx xy xz yy yz zz), B row-major 3x3.
 struct SI {
@@ -939,6 +943,8 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
     }
   }
 }
+
+#pragma clang fp contract(off)
 
 // =====================================================================
 //                          the fused step kernel
