@@ -38,6 +38,25 @@
 
 #ifdef GO1_ISA_MARKS  // section markers for static instruction accounting (tools/isa_sections.py)
 #define MARK(x) asm volatile("; MARK " #x)
+#elif defined(GO1_STAMPS)
+// Diagnostic build only (tools/stamps.py): every marker records (source line, s_memtime)
+// into a buffer of its own, read back by go1_debug_stamps.  Never built into the product.
+#define GO1_STAMP_WAVES 4096
+#define GO1_STAMP_SLOTS 160
+__device__ unsigned long long g_go1_stamps[GO1_STAMP_WAVES * GO1_STAMP_SLOTS];
+__shared__ unsigned s_go1_stamp_k;
+__device__ __forceinline__ void go1_stamp(unsigned line) {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned i = s_go1_stamp_k;
+  if (blockIdx.x < GO1_STAMP_WAVES && i < GO1_STAMP_SLOTS)
+    g_go1_stamps[blockIdx.x * GO1_STAMP_SLOTS + i] = ((unsigned long long)line << 48) | (t & 0xffffffffffffull);
+  s_go1_stamp_k = i + 1;
+  __builtin_amdgcn_sched_barrier(0);
+}
+#define MARK(x) go1_stamp(__LINE__)
 #else
 #define MARK(x)
 #endif
@@ -379,22 +398,48 @@ __device__ __forceinline__ void mat3T_vec(const float* E, const float* v, float*
   o[0] = x; o[1] = y; o[2] = z;
 }
 
-// motion transform parent -> child: (w, v) -> (E w, E (v - r x w))
-__device__ __forceinline__ void xm(int ax, float c, float s, const float* r, const float* vin, float* vout) {
-  float rw[3], t[3];
-  cross3(r, vin, rw);
-  t[0] = vin[3] - rw[0]; t[1] = vin[4] - rw[1]; t[2] = vin[5] - rw[2];
+// Joint offsets are sparse in the Go1 model (go1_create checks it): hip (x, y, 0), thigh
+// (0, y, 0), calf (0, 0, z).  `M` = mask of the components of r that may be non-zero
+// (bit i = component i), a constant after inlining and unrolling, so the products with
+// the zero components are never emitted (not even as 0 * x, which IEEE forbids folding).
+__host__ __device__ __forceinline__ constexpr int offset_mask(int j) { return j == 0 ? 3 : (j == 1 ? 2 : 4); }
+// which components of a x b can be non-zero, a and b with masks ma, mb
+__device__ __forceinline__ constexpr int cross_mask(int ma, int mb) {
+  int m = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int p = (i + 1) % 3, q = (i + 2) % 3;
+    if ((((ma >> p) & 1) && ((mb >> q) & 1)) || (((ma >> q) & 1) && ((mb >> p) & 1))) m |= 1 << i;
+  }
+  return m;
+}
+// component i of a x b (a_p b_q - a_q b_p) with only the terms the masks allow
+__device__ __forceinline__ float cross_c(int ma, int mb, int i, const float* a, const float* b) {
+  const int p = (i + 1) % 3, q = (i + 2) % 3;
+  const bool t1 = ((ma >> p) & 1) && ((mb >> q) & 1), t2 = ((ma >> q) & 1) && ((mb >> p) & 1);
+  if (t1 && t2) return a[p] * b[q] - a[q] * b[p];
+  if (t1) return a[p] * b[q];
+  if (t2) return -(a[q] * b[p]);
+  return 0.0f;
+}
+
+// motion transform parent -> child: (w, v) -> (E w, E (v - r x w)), r with mask M
+__device__ __forceinline__ void xm(int ax, float c, float s, int M, const float* r, const float* vin, float* vout) {
+  const int cm = cross_mask(M, 7);
+  float t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = ((cm >> i) & 1) ? vin[3 + i] - cross_c(M, 7, i, r, vin) : vin[3 + i];
   rE(ax, c, s, vin, vout);
   rE(ax, c, s, t, vout + 3);
 }
 
-// force transform child -> parent: (n, f) -> (E^T n + r x E^T f, E^T f)
-__device__ __forceinline__ void xfT(int ax, float c, float s, const float* r, const float* fin, float* fout) {
-  float n[3], f[3], rf[3];
+// force transform child -> parent: (n, f) -> (E^T n + r x E^T f, E^T f), r with mask M
+__device__ __forceinline__ void xfT(int ax, float c, float s, int M, const float* r, const float* fin, float* fout) {
+  const int cm = cross_mask(M, 7);
+  float n[3], f[3];
   rET(ax, c, s, fin, n);
   rET(ax, c, s, fin + 3, f);
-  cross3(r, f, rf);
-  fout[0] = n[0] + rf[0]; fout[1] = n[1] + rf[1]; fout[2] = n[2] + rf[2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) fout[i] = ((cm >> i) & 1) ? n[i] + cross_c(M, 7, i, r, f) : n[i];
   fout[3] = f[0]; fout[4] = f[1]; fout[5] = f[2];
 }
 
@@ -432,9 +477,11 @@ __device__ __forceinline__ void rot_congruence_sym(int ax, float c, float s, flo
   Q[pI * 3 + rI] = qpr; Q[rI * 3 + pI] = qpr;
 }
 
-// X^T Ia X for X = [[E, 0], [-E r~, E]]: rotate the blocks by E^T(.)E, then translate by r:
-//   A'' = A' + r~ B'^T - B' r~ - r~ C' r~ ,  B'' = B' + r~ C' ,  C'' = C'.
-__device__ __forceinline__ void xform_inertia(int ax, float cq, float sq, const float* r, const SI& In, SI& Out) {
+// X^T Ia X for X = [[E, 0], [-E r~, E]]: rotate the blocks by E^T(.)E, then translate by r
+// (mask M):  A'' = A' + r~ B'^T - B' r~ - r~ C' r~ ,  B'' = B' + r~ C' ,  C'' = C'.
+// RC = r~ C' has non-zero rows mc, BR = B' r~ non-zero columns mb, RCR = RC r~ both.
+__device__ __forceinline__ void xform_inertia(int ax, float cq, float sq, int M, const float* r, const SI& In,
+                                              SI& Out) {
   float A[9], B[9], C[9];
   const float sp = ax == 0 ? sq : -sq;
   const float c2 = cq * cq - sp * sp, s2 = 2.0f * cq * sp;
@@ -442,29 +489,37 @@ __device__ __forceinline__ void xform_inertia(int ax, float cq, float sq, const 
   rot_congruence(ax, cq, sq, In.b, B);
   rot_congruence_sym(ax, cq, sq, c2, s2, In.c, C);
   // translation, with (M r~) row i = (row i of M) x r and r~ B'^T = -(B' r~)^T
+  const int mc = cross_mask(M, 7), mb = cross_mask(7, M);
   float RC[9], BR[9], RCR[9];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {  // r~ C': column j = r x C'[:, j]
     const float col[3] = {C[j], C[3 + j], C[6 + j]};
-    float t[3];
-    cross3(r, col, t);
-    RC[j] = t[0]; RC[3 + j] = t[1]; RC[6 + j] = t[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) RC[3 * i + j] = ((mc >> i) & 1) ? cross_c(M, 7, i, r, col) : 0.0f;
   }
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    cross3(B + 3 * i, r, BR + 3 * i);    // B' r~
-    cross3(RC + 3 * i, r, RCR + 3 * i);  // r~ C' r~
-  }
-  // upper triangle of A'' = A' - BR^T - BR - RCR (symmetric)
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      BR[3 * i + j] = ((mb >> j) & 1) ? cross_c(7, M, j, B + 3 * i, r) : 0.0f;              // B' r~
+      RCR[3 * i + j] = ((mc >> i) & (mb >> j) & 1) ? cross_c(7, M, j, RC + 3 * i, r) : 0.0f;  // r~ C' r~
+    }
+  // upper triangle of A'' = A' - BR^T - BR - RCR (symmetric); zero terms are skipped
   const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
   for (int t = 0; t < 6; ++t) {
     const int i = II[t], j = JJ[t];
-    Out.a[t] = A[i * 3 + j] - BR[j * 3 + i] - BR[i * 3 + j] - RCR[i * 3 + j];
+    float v = A[i * 3 + j];
+    if ((mb >> i) & 1) v -= BR[j * 3 + i];
+    if ((mb >> j) & 1) v -= BR[i * 3 + j];
+    if ((mc >> i) & (mb >> j) & 1) v -= RCR[i * 3 + j];
+    Out.a[t] = v;
     Out.c[t] = C[i * 3 + j];
   }
 #pragma unroll
-  for (int i = 0; i < 9; ++i) Out.b[i] = B[i] + RC[i];
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Out.b[3 * i + j] = ((mc >> i) & 1) ? B[3 * i + j] + RC[3 * i + j] : B[3 * i + j];
 }
 
 __device__ __forceinline__ void si_add(SI& A, const SI& B) {
@@ -699,7 +754,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       pm_sincosf(S.q[j], &sn, &cn);
       cs[j][0] = cn; cs[j][1] = sn;
       float vj[6];
-      xm(ax, cn, sn, r, vp, vj);
+      xm(ax, cn, sn, offset_mask(j), r, vp, vj);
       vj[ax] += S.qd[j];
       // c_j = v_j x (S qd): S = unit axis ax
       {
@@ -709,9 +764,11 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
         cross3(vj + 3, sq, cj[j] + 3);
       }
       // world pose of link j: p = pp + Rp r ; Rw rows = E (rows of Rp)
-      float rw[3];
-      mat3_vec(Rp, r, rw);
-      pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)  // pp += Rp r over the components r may have
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if ((offset_mask(j) >> k) & 1) pp[i] += Rp[3 * i + k] * r[k];
 #pragma unroll
       for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
       // rigid inertia about the link origin, bias force v x* I v, minus gravity
@@ -827,8 +884,8 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
 #pragma unroll
       for (int i = 0; i < 6; ++i) pa[i] = pA[j][i] + Iac[i] + U[j][i] * u[j] * invD;
       SI It;
-      xform_inertia(ax, cs[j][0], cs[j][1], origin + j * 3, Ia, It);
-      xfT(ax, cs[j][0], cs[j][1], origin + j * 3, pa, pt);
+      xform_inertia(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
+      xfT(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
       if (j > 0) {
         rigid_si(model + 10 * (1 + leg * 3 + j - 1), 1.0f, IA);
         si_add(IA, It);
@@ -883,7 +940,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
     for (int j = 0; j < 3; ++j) {
       const int ax = j == 0 ? 0 : 1;
       float aj[6];
-      xm(ax, cs[j][0], cs[j][1], origin + j * 3, ap, aj);
+      xm(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, ap, aj);
 #pragma unroll
       for (int i = 0; i < 6; ++i) aj[i] += cj[j][i];
       float Ua = 0.0f;
@@ -1024,6 +1081,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const bool owner = role == 0;  // the lane of a leg that stores its per-leg outputs
   const int e = blockIdx.x * SEPB + el;  // n % 16 == 0 (go1_create): every wave is full
   (void)n;
+#ifdef GO1_STAMPS
+  s_go1_stamp_k = 0;
+#endif
+  MARK(kernel_begin);
   MlpFrag F;
   mlp_load(c->actuator, lane, F);
   const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset};
@@ -1536,6 +1597,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   // one atomic per wave when any env of the wave reset (extras["time_outs"] rebinding, :289-291)
   if (__ballot(reset && leg == 0) != 0ull && (threadIdx.x & 63) == 0) atomicOr(K.flags + K.cur, 1);
+  MARK(kernel_end);
 }
 
 // extras["time_outs"] = time_out of the last step, if any env reset in it (go1_sync_time_outs:
@@ -1627,6 +1689,12 @@ static int fail(int code, const std::string& msg) {
   } while (0)
 
 extern "C" {
+#ifdef GO1_STAMPS
+int go1_debug_stamps(void* host, size_t bytes) {
+  if (bytes > sizeof(g_go1_stamps)) bytes = sizeof(g_go1_stamps);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_go1_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int go1_abi_version(void) { return GO1_ABI_VERSION; }
 
@@ -1650,6 +1718,11 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   if (!cfg->measure_front_half)
     return fail(GO1_E_ARG, "go1_create: only the 261-wide front-half height scan is on this path "
                            "(Cfg.terrain.measure_front_half, scripts/train.py:53)");
+  for (int leg = 0; leg < 4; ++leg)  // joint offsets must have the sparsity the kernel exploits
+    for (int j = 0; j < 3; ++j)
+      for (int k = 0; k < 3; ++k)
+        if (!((offset_mask(j) >> k) & 1) && cfg->model[13 * 10 + leg * 9 + j * 3 + k] != 0.0f)
+          return fail(GO1_E_ARG, "go1_create: joint offsets must be hip (x, y, 0), thigh (0, y, 0), calf (0, 0, z)");
   go1_handle* h = new (std::nothrow) go1_handle();
   if (!h) return fail(GO1_E_ARG, "go1_create: out of host memory");
   h->cfg = *cfg;

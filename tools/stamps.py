@@ -1,0 +1,78 @@
+"""Where one step-kernel launch spends its time, per source section (diagnostic build).
+
+  local:  bash tools/variants.sh build stamps "-DGO1_STAMPS"
+  gpurun: python tools/stamps.py [n_envs]
+
+Runs the bench workload on the stamps build (every MARK() records (line, s_memtime)),
+then prints, per section (the code after a marker, up to the next executed marker), the
+mean cycles per wave summed over all its executions in the launch and its share of the
+wave's lifetime.  Read the SHARES: the stamps' waits forbid overlaps the real kernel has.
+"""
+import ctypes as C
+import collections
+import os
+import re
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["GO1_LIB_OVERRIDE"] = os.path.join(ROOT, "legged_tracking_amd", "_build", "libgo1_var_stamps.so")
+WAVES, SLOTS = 4096, 160
+
+
+def main():
+    import torch
+    from legged_tracking_amd import config as CF, native, terrain as T
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    dev = torch.device("cuda", 0)
+    cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=32, cols=32)
+    c = CF.build_abi_config(cfg, n_envs=n)
+    td = T.build(cfg, n, np.random.RandomState(11))
+    g = native.Go1Native(c, str(dev))
+    g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    rng = np.random.default_rng(100)
+    g.state["friction"].copy_(torch.from_numpy(rng.uniform(0.1, 3.0, (n, 1)).astype(np.float32)))
+    g.reset_envs(torch.ones(n, dtype=torch.bool, device=dev), rng_seed=11, rng_step=0)
+    g.state["episode_length"].copy_(torch.from_numpy(rng.integers(0, 500, (n, 1)).astype(np.int32)))
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    grav, gvec = CF.gravity_state(rng.uniform(-1, 1, 3))
+    ring = torch.randn((8, n, 12), device=dev)
+    for k in range(30):
+        g.step(ring[k % 8], gvec, grav, scales, rng_seed=11, rng_step=1 + k)
+    torch.cuda.synchronize()
+    lib = native.lib()
+    buf = np.zeros(WAVES * SLOTS, np.uint64)
+    assert lib.go1_debug_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
+    g.close()
+
+    src = open(os.path.join(ROOT, "legged_tracking_amd", "csrc", "go1_step.hip")).read().splitlines()
+    name = {i + 1: m.group(1) for i, l in enumerate(src) for m in [re.search(r"MARK\((\w+)\)", l)] if m}
+    nw = min(WAVES, n // 4)
+    b = buf[: nw * SLOTS].reshape(nw, SLOTS)
+    line = (b >> np.uint64(48)).astype(np.int64)
+    t = (b & np.uint64((1 << 48) - 1)).astype(np.int64)
+    tot = collections.Counter()
+    cnt = collections.Counter()
+    life = []
+    for w in range(nw):
+        k = int(np.count_nonzero(line[w]))
+        if k < 2:
+            continue
+        life.append(t[w, k - 1] - t[w, 0])
+        for i in range(k - 1):
+            nm = name.get(int(line[w, i]), str(line[w, i]))
+            tot[nm] += int(t[w, i + 1] - t[w, i])
+            cnt[nm] += 1
+    L = float(np.mean(life))
+    starts = t[:, 0]
+    print(f"waves {len(life)}; mean wave lifetime {L:.0f} cycles (s_memtime); start spread "
+          f"{(starts.max() - starts.min()):.0f} cycles; stamps per wave {int(np.mean(np.count_nonzero(line, 1)))}")
+    print(f"{'section (after marker)':28s} {'cycles/wave':>12s} {'share':>7s} {'execs':>6s}")
+    for nm, v in sorted(tot.items(), key=lambda x: -x[1]):
+        print(f"{nm:28s} {v / len(life):12.0f} {v / len(life) / L:7.1%} {cnt[nm] / len(life):6.1f}")
+
+
+if __name__ == "__main__":
+    main()
