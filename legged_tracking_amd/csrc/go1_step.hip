@@ -110,8 +110,9 @@ struct Rng {
 // moves stay in the VALU (no LDS round trip)
 __device__ __forceinline__ float qsum(float v) {
 #if GO1_DPP
-  v = v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
-  v = v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  // update_dpp(0, ., bound_ctrl) lets the compiler fold the move into the add (v_add_f32_dpp)
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));  // [1,0,3,2]
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));  // [2,3,0,1]
 #else
   v = v + __shfl_xor(v, 1);
   v = v + __shfl_xor(v, 2);
@@ -349,6 +350,31 @@ __device__ __forceinline__ void rigid_si(const float* body, float mscale, SI& I)
   I.b[3] = m * c2; I.b[4] = 0.0f; I.b[5] = -m * c0;
   I.b[6] = -m * c1; I.b[7] = m * c0; I.b[8] = 0.0f;
   I.c[0] = m; I.c[1] = 0.0f; I.c[2] = 0.0f; I.c[3] = m; I.c[4] = 0.0f; I.c[5] = m;
+}
+
+// Rigid-body bias force v x* (I v) of a body (mass m, COM c, inertia Ic about the COM;
+// model layout) from its momentum, without building the 6x6 inertia:
+//   p = m (v + w x c),  L = Ic w + c x p,  v x* (L, p) = (w x L + v x p, w x p).
+__device__ __forceinline__ void rigid_bias(const float* body, float mscale, const float* vel, float* o) {
+  const float m = body[0] * mscale;
+  const float* c = body + 1;
+  const float* w = vel;
+  const float* v = vel + 3;
+  float wc[3], p[3], L[3], cp[3];
+  cross3(w, c, wc);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p[i] = m * (v[i] + wc[i]);
+  const float ixx = body[4] * mscale, ixy = body[5] * mscale, ixz = body[6] * mscale;
+  const float iyy = body[7] * mscale, iyz = body[8] * mscale, izz = body[9] * mscale;
+  cross3(c, p, cp);
+  L[0] = ixx * w[0] + ixy * w[1] + ixz * w[2] + cp[0];
+  L[1] = ixy * w[0] + iyy * w[1] + iyz * w[2] + cp[1];
+  L[2] = ixz * w[0] + iyz * w[1] + izz * w[2] + cp[2];
+  float a[3], b[3];
+  cross3(w, L, a);
+  cross3(v, p, b);
+  o[0] = a[0] + b[0]; o[1] = a[1] + b[1]; o[2] = a[2] + b[2];
+  cross3(w, p, o + 3);
 }
 
 // force cross product v x* f
@@ -773,11 +799,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
       // rigid inertia about the link origin, bias force v x* I v, minus gravity
       const float* B = model + 10 * (1 + leg * 3 + j);
-      SI I;
-      rigid_si(B, 1.0f, I);
-      float hm[6];
-      si_mul(I, vj, hm);
-      crf(vj, hm, pA[j]);
+      rigid_bias(B, 1.0f, vj, pA[j]);
       float gl[3];
       mat3T_vec(Rp, g, gl);
       float fg[3] = {B[0] * gl[0], B[0] * gl[1], B[0] * gl[2]}, cg[3];
@@ -906,9 +928,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
   rigid_si(bb, mscale, I0);
   float p0[6];
   {
-    float hm[6];
-    si_mul(I0, vb, hm);
-    crf(vb, hm, p0);
+    rigid_bias(bb, mscale, vb, p0);
     float gb[3];
     mat3T_vec(R, g, gb);
     const float m = bb[0] * mscale;
