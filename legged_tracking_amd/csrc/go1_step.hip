@@ -81,8 +81,9 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 __device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    uint32_t l0 = 0xD2511F53u * c[0], h0 = __umulhi(0xD2511F53u, c[0]);
-    uint32_t l1 = 0xCD9E8D57u * c[2], h1 = __umulhi(0xCD9E8D57u, c[2]);
+    // one v_mad_u64_u32 per product gives both halves (instead of v_mul_lo + v_mul_hi)
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32), l1 = (uint32_t)p1, h1 = (uint32_t)(p1 >> 32);
     uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
     c[0] = n0; c[1] = l1; c[2] = n2; c[3] = l0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
@@ -823,6 +824,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
   //      corner 2 leg, corner 2 leg + 1]; forces in the body frame of the point's body
   float fth[6] = {0, 0, 0, 0, 0, 0}, fca[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
   float Fth[3] = {0, 0, 0}, Fca[3] = {0, 0, 0}, Fft[3] = {0, 0, 0}, Fb[3] = {0, 0, 0};
+#ifndef GO1_ABL_NO_CONTACT
 #pragma unroll
   for (int sidx = 0; sidx < 2; ++sidx) {
     const int p = 2 * role + sidx;
@@ -859,6 +861,9 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       Fb[i] += on_base ? F[i] : 0.0f;
     }
   }
+#else  // ablation build only: no contacts
+  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
+#endif
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     pA[1][i] -= rsum(fth[i]);
@@ -1130,6 +1135,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     vh[1][j] = st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j];
   }
   const float friction = st.friction[e], payload = st.payload[e];
+  const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
   __shared__ float2 s_patch[SEPB][PSZ * PSZ];
   __shared__ int s_patch_meta[SEPB][3];
@@ -1290,6 +1296,60 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 4; ++i) root[3 + i] = P.quat[i];
   }
+  // ---- every post-physics input in one batch of loads, ahead of this kernel's first
+  // post-physics store: one memory round trip instead of one per section
+  const int ep_in = st.episode_length[e];
+  const int idx_in = st.curr_pose_index[e];
+  const int coll_in = st.collision_count[e];
+  const float restitution = st.restitution[e];
+  float traj_in[6], ldv[3], la[3], sums[GO1_NUM_SUMS];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) traj_in[i] = st.trajectory[(size_t)e * 6 + i];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    ldv[j] = st.last_dof_vel[d0 + j];
+    la[j] = st.last_actions[d0 + j];
+  }
+#pragma unroll
+  for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = st.episode_sums[(size_t)e * GO1_NUM_SUMS + k];
+  // height scan (:1918-1965) samples at the post-physics, pre-reset pose: the gathers are
+  // issued here and consumed by the height observations at the end
+  const bool hplane = c->terrain_kind == 0;
+  const float scan_x = root[0], scan_y = root[1];
+  float camx = 0.0f, camy = 0.0f;
+  if (!hplane) {
+    const float cos_p = pm_cosf(cam_pitch);
+    camx = c->camera_offset_x * cos_p;
+    camy = 0.0f * cos_p;
+  }
+  auto sample = [&](int i, int j, float& h0, float& h1) {
+    if (hplane) { h0 = 1.0f; h1 = 0.0f; return; }
+    float px = c->height_grid_x[i] + scan_x;
+    float py = c->height_grid_y[j] + scan_y;
+    if (c->camera_zero) { px = px + camx; py = py + camy; }
+    px = px - T.ox;
+    py = py - T.oy;
+    // .long() truncation then clip (:1948-1952); the float is bounded first so that a
+    // non-finite pose cannot turn the conversion into undefined behaviour
+    const float fx = fminf(fmaxf(px / c->horizontal_scale, -1.0f), (float)c->hf_nx);
+    const float fy = fminf(fmaxf(py / c->horizontal_scale, -1.0f), (float)c->hf_ny);
+    int ix = (int)fx, iy = (int)fy;
+    ix = ix < 0 ? 0 : (ix > c->hf_nx - 2 ? c->hf_nx - 2 : ix);
+    iy = iy < 0 ? 0 : (iy > c->hf_ny - 2 ? c->hf_ny - 2 : iy);
+    h0 = T.tile[(size_t)ix * c->hf_ny + iy];
+    h1 = T.tile[((size_t)c->hf_nx + ix) * c->hf_ny + iy];
+  };
+  const int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
+  const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
+  // the env's 16 lanes take points sub16 + 16 k (n_pts <= 112 for the front half)
+  constexpr int KPTS = 7;
+  float hv[KPTS][2];
+#pragma unroll
+  for (int k = 0; k < KPTS; ++k) {
+    const int p = min(sub16 + 16 * k, n_pts - 1);
+    sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[k][0], hv[k][1]);
+  }
+
   if (A.contact_forces && owner) {
     float* o = A.contact_forces + (size_t)e * NB * 3;
     if (leg == 0) { o[0] = cf_base[0]; o[1] = cf_base[1]; o[2] = cf_base[2]; }
@@ -1301,7 +1361,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   MARK(post_begin);
   // ================= post_physics_step (:114-169), contraction off =================
-  const int ep = st.episode_length[e] + 1;
+  const int ep = ep_in + 1;
   float blv[3], bav[3], pg[3], rpy[3], rel_lin[3], rel_rot[3];
   {
     const float qb[4] = {root[3], root[4], root[5], root[6]};
@@ -1309,14 +1369,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     quat_rotate_inverse_f(qb, root + 10, bav);
     quat_rotate_inverse_f(qb, A.gravity_vec, pg);
     // _plan_target_pose / _compute_relative_target_pose (:850-932)
-    const float* tr = st.trajectory + (size_t)e * 6;
+    const float* tr = traj_in;
     const float rel_in[3] = {tr[0] - root[0], tr[1] - root[1], tr[2] - root[2]};
     quat_apply_yaw_inverse_f(qb, rel_in, rel_lin);
     quat_to_rpy_f(qb, rpy);
 #pragma unroll
     for (int i = 0; i < 3; ++i) rel_rot[i] = wrap_to_pi_f(tr[3 + i] - rpy[i]);
   }
-  const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
   float cmd[2] = {rel_lin[0], rel_lin[1]};
 
   MARK(post_kin_done);
@@ -1331,7 +1390,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
   const bool switched = rel_norm < c->switch_dist;
-  int idx = st.curr_pose_index[e];
+  int idx = idx_in;
   if (switched) { idx += 1; if (idx > 0) idx = 0; }
   const bool reached = switched && idx == 0;
   // collision count (:848): this lane's thigh + calf, base on lane 0
@@ -1360,8 +1419,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // rewards (:320-355, reward_crawling.py)
   float terms[GO1_NUM_TERMS];
   {
-    const float* ldv = st.last_dof_vel + d0;
-    const float* la = st.last_actions + d0;
     float x[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) x[j] = sq_f(torque[j]);
@@ -1405,9 +1462,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     terms[9] = expf(-ae / c->tracking_sigma_ang);
   }
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
-  float sums[GO1_NUM_SUMS];
-#pragma unroll
-  for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = st.episode_sums[(size_t)e * GO1_NUM_SUMS + k];
 #pragma unroll
   for (int k = 0; k < GO1_NUM_TERMS; ++k) {
     const float r = terms[k] * A.reward_scales[k];
@@ -1424,10 +1478,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   MARK(rewards_done);
   // ---- reset_idx (:218-296); the height scan below still samples at the pre-reset pose
-  const float scan_x = root[0], scan_y = root[1];
   float traj_new[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) traj_new[i] = st.trajectory[(size_t)e * 6 + i];
+  for (int i = 0; i < 6; ++i) traj_new[i] = traj_in[i];
   if (A.episode_log && owner && leg == 0 && !reset) A.episode_log[(size_t)e * GO1_EPISODE_LOG + 13] = 0.0f;
   if (reset && A.episode_log && owner && leg == 0) {
     // reset_idx logging (:256-271): pre-reset sums, episode length, reached, goal distance
@@ -1446,7 +1499,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     cmd[0] = 0.0f;  // commands is a view of local_relative_linear, zeroed by reset_idx (:252, :802)
     cmd[1] = 0.0f;
   }
-  const int coll_count = reset ? 0 : st.collision_count[e] + (int)coll;
+  const int coll_count = reset ? 0 : coll_in + (int)coll;
 
   MARK(reset_done);
   // ---- compute_observations (:357-475)
@@ -1474,45 +1527,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     put(29 + d, aj, 0.0f, false);
   }
   MARK(obs_props_done);
-  // height scan (:1918-1965) fused with the height observations (:395-411)
+  // height observations (:395-411) from the samples gathered after the physics
   {
-    const bool plane = c->terrain_kind == 0;
-    float camx = 0.0f, camy = 0.0f;
-    if (!plane) {
-      const float cos_p = pm_cosf(cam_pitch);
-      camx = c->camera_offset_x * cos_p;
-      camy = 0.0f * cos_p;
-    }
-    auto sample = [&](int i, int j, float& h0, float& h1) {
-      if (plane) { h0 = 1.0f; h1 = 0.0f; return; }
-      float px = c->height_grid_x[i] + scan_x;
-      float py = c->height_grid_y[j] + scan_y;
-      if (c->camera_zero) { px = px + camx; py = py + camy; }
-      px = px - T.ox;
-      py = py - T.oy;
-      // .long() truncation then clip (:1948-1952); the float is bounded first so that a
-      // non-finite pose cannot turn the conversion into undefined behaviour
-      const float fx = fminf(fmaxf(px / c->horizontal_scale, -1.0f), (float)c->hf_nx);
-      const float fy = fminf(fmaxf(py / c->horizontal_scale, -1.0f), (float)c->hf_ny);
-      int ix = (int)fx, iy = (int)fy;
-      ix = ix < 0 ? 0 : (ix > c->hf_nx - 2 ? c->hf_nx - 2 : ix);
-      iy = iy < 0 ? 0 : (iy > c->hf_ny - 2 ? c->hf_ny - 2 : iy);
-      h0 = T.tile[(size_t)ix * c->hf_ny + iy];
-      h1 = T.tile[((size_t)c->hf_nx + ix) * c->hf_ny + iy];
-    };
-    const int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
-    const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
     const float zroot = root[2];  // post-reset (:401)
     const float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
-    // the env's 16 lanes take points sub16 + 16 k (n_pts <= 112 for the front half):
-    // indices first, then all loads in flight together, then the observation arithmetic
-    constexpr int KPTS = 7;
-    float hv[KPTS][2];
-#pragma unroll
-    for (int k = 0; k < KPTS; ++k) {
-      const int p = min(sub16 + 16 * k, n_pts - 1);
-      sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[k][0], hv[k][1]);
-    }
 #pragma unroll
     for (int k = 0; k < KPTS; ++k) {
       const int p = sub16 + 16 * k;
@@ -1547,7 +1565,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (sub16 == 0) {
     float* pv = A.priv + (size_t)e * GO1_NUM_PRIV;
     pv[0] = clampf((friction - c->priv_friction_shift) * c->priv_friction_scale, -clip, clip);
-    pv[1] = clampf((st.restitution[e] - c->priv_rest_shift) * c->priv_rest_scale, -clip, clip);
+    pv[1] = clampf((restitution - c->priv_rest_shift) * c->priv_rest_scale, -clip, clip);
   }
 
   MARK(priv_done);
