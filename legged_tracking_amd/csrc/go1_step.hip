@@ -103,6 +103,15 @@ struct Rng {
   }
 };
 
+// ---------------------------------------------------------------- lane-indexed selects
+// a[i] for a lane-dependent i in 0..3 as two levels of bit-test selects (v_cndmask): an
+// equality chain (i == 0 ? .. : i == 1 ? ..) is turned into a switch with divergent branches
+__device__ __forceinline__ float sel4(int i, float a0, float a1, float a2, float a3) {
+  const bool lo = i & 1, hi = i & 2;
+  return hi ? (lo ? a3 : a2) : (lo ? a1 : a0);
+}
+__device__ __forceinline__ float sel3(int i, const float* a) { return sel4(i, a[0], a[1], a[2], a[2]); }
+
 // ---------------------------------------------------------------- quad helpers
 #ifndef GO1_DPP
 #define GO1_DPP 1
@@ -1134,6 +1143,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     vh[0][j] = st.vel_hist[(size_t)e * 24 + leg * 3 + j];
     vh[1][j] = st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j];
   }
+  // per-joint constants and the lag-ring slots the sub-steps read (1..4 for decimation
+  // <= 4): loaded here so that no sub-step waits on a memory round trip
+  float dflt[3], tlim[3], lag_pre[4][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    dflt[j] = c->default_dof_pos[leg * 3 + j];
+    tlim[j] = c->torque_limits[leg * 3 + j];
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) lag_pre[sl][j] = lag_in[(sl + 1) * 12 + j];
+  }
   const float friction = st.friction[e], payload = st.payload[e];
   const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
@@ -1213,8 +1232,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int d = leg * 3 + j;
-      const float lg = slot < GO1_LAG_SLOTS ? lag_in[slot * 12 + j] : scaled[j];
-      tgt[j] = lg + c->default_dof_pos[d];
+      const float lg = slot <= 4 ? sel4(slot - 1, lag_pre[0][j], lag_pre[1][j], lag_pre[2][j], lag_pre[3][j])
+                                 : (slot < GO1_LAG_SLOTS ? lag_in[slot * 12 + j] : scaled[j]);
+      tgt[j] = lg + dflt[j];
       const float err = q[j] - tgt[j] + offset[j];
       xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
       xin[j][3] = qd[j]; xin[j][4] = vh[0][j]; xin[j][5] = vh[1][j];
@@ -1227,8 +1247,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const float* y = xin[j];
-      const float b0 = lq == 0 ? y[0] : (lq == 1 ? y[1] : (lq == 2 ? y[2] : y[3]));
-      const float b1v = lq == 0 ? y[4] : (lq == 1 ? y[5] : 0.0f);
+      const float b0 = sel4(lq, y[0], y[1], y[2], y[3]);
+      const float b1v = sel4(lq, y[4], y[5], 0.0f, 0.0f);
 #ifdef GO1_ABL_NO_MLP
       const float t = 0.0f * (b0 + b1v);  // ablation build only: no actuator net
 #else
@@ -1249,7 +1269,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       vh[1][j] = vh[0][j];
       vh[0][j] = qd[j];
       const float t = tq[j] * strength[j];
-      const float lim = c->torque_limits[d];
+      const float lim = tlim[j];
       torque[j] = clampf(t, -lim, lim);
       if (A.dbg_torques && owner) A.dbg_torques[((size_t)sub * n + e) * NDOF + d] = torque[j];
     }
@@ -1519,9 +1539,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   if (role < 3) {
     const int j = role, d = leg * 3 + role;
-    const float qj = j == 0 ? q[0] : (j == 1 ? q[1] : q[2]);
-    const float qdj = j == 0 ? qd[0] : (j == 1 ? qd[1] : qd[2]);
-    const float aj = j == 0 ? act[0] : (j == 1 ? act[1] : act[2]);
+    const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act);
     put(5 + d, (qj - c->default_dof_pos[d]) * c->obs_scale_dof_pos, c->noise_dof_pos, true);
     put(17 + d, qdj * c->obs_scale_dof_vel, c->noise_dof_vel, true);
     put(29 + d, aj, 0.0f, false);
@@ -1594,7 +1612,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // leg, role 3 of leg 0 stores the env-level state
   if (role < 3) {
     const int j = role;
-    auto pick = [&](const float* v3) { return j == 0 ? v3[0] : (j == 1 ? v3[1] : v3[2]); };
+    auto pick = [&](const float* v3) { return sel3(j, v3); };
     const size_t dj = d0 + j;
     st.dof_pos[dj] = pick(q);
     st.dof_vel[dj] = pick(qd);

@@ -47,12 +47,12 @@ PM_FN void pm_sincosf(float x, float* s, float* c) {
   /* bounded before the conversion: a NaN / huge argument must not be undefined behaviour */
   int q = ((int)fminf(fmaxf(j, -1.0e6f), 1.0e6f)) & 3;
   float sp = pm_sin_poly(r), cp = pm_cos_poly(r);
-  switch (q) {
-    case 0: *s = sp; *c = cp; break;
-    case 1: *s = cp; *c = -sp; break;
-    case 2: *s = -sp; *c = -cp; break;
-    default: *s = -cp; *c = sp; break;
-  }
+  /* quadrant by bit-test selects (a switch would become divergent branches):
+     q = 0: (sp, cp), 1: (cp, -sp), 2: (-sp, -cp), 3: (-cp, sp) */
+  const bool swap = q & 1, sneg = q & 2, cneg = (q ^ (q >> 1)) & 1;
+  const float a = swap ? cp : sp, b = swap ? sp : cp;
+  *s = sneg ? -a : a;
+  *c = cneg ? -b : b;
 }
 
 PM_FN float pm_sinf(float x) { float s, c; pm_sincosf(x, &s, &c); return s; }

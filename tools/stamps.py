@@ -18,7 +18,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["GO1_LIB_OVERRIDE"] = os.path.join(ROOT, "legged_tracking_amd", "_build", "libgo1_var_stamps.so")
+os.environ["GO1_LIB_OVERRIDE"] = os.path.join(ROOT, "legged_tracking_amd", "_build", "libgo1_var_%s.so" % os.environ.get("GO1_STAMPS_VARIANT", "stamps"))
 WAVES, SLOTS = 4096, 160
 
 
