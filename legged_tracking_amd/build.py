@@ -9,13 +9,15 @@ BUILD = os.path.join(HERE, "_build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off"]
 
-# The step kernel is VALU-issue bound on scalar f32 chains: packed-f32 (v_pk_*) code
-# generation adds register-pair moves that cost more than it saves (measured -3 %).
-NO_PK = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+# The step kernel is VALU-issue bound.  One wave issues a v_pk_fma_f32 (two FMAs) as fast
+# as a v_fma_f32 (tools/probes/pk_rate.hip), so the kernel packs by hand where the data
+# pair up naturally (f2 types); the SLP auto-vectoriser stays off: its packing of scalar
+# code adds register-pair moves that cost more than they save (measured -3 %).
+STEP_FLAGS = ["-fno-slp-vectorize"]
 
 # name -> (source, extra dependencies, extra flags)
 LIBS = {
-    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", os.path.join(INC, "go1_mi355x.h")], NO_PK),
+    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", os.path.join(INC, "go1_mi355x.h")], STEP_FLAGS),
     "libgo1_rollout.so": ("rollout.hip", [os.path.join(INC, "go1_rollout.h")], []),
 }
 OUT = os.path.join(BUILD, "libgo1_mi355x.so")  # the step library (kept for callers of build())

@@ -66,6 +66,9 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #ifndef GO1_CONTACT_ROLL
 #define GO1_CONTACT_ROLL 0
 #endif
+#ifndef GO1_PK_CONTACT
+#define GO1_PK_CONTACT 1
+#endif
 #ifndef GO1_TRUNK_PTS
 #define GO1_TRUNK_PTS 2
 #endif
@@ -661,6 +664,79 @@ struct CP {
   float k, d, kf, mu;
 };
 
+// ---- packed (v_pk_*_f32) contact: one wave issues a v_pk_fma_f32 (two FMAs) as fast as a
+// v_fma_f32 (tools/probes/pk_rate.hip), so the floor and ceiling layers of a point are
+// carried as the two halves of an f2 all the way from the bilinear patch to the force.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
+
+// (floor, ceiling) heights and gradients at world (x, y), bilinear: the LDS patch stores
+// (floor, ceiling) per cell, i.e. already in f2 layout
+__device__ __forceinline__ void height_query_pk(const Terr& T, float x, float y, f2& h, f2& gx, f2& gy) {
+  if (!T.tile) {
+    h = f2{0.0f, 1e9f};
+    gx = f2s(0.0f);
+    gy = f2s(0.0f);
+    return;
+  }
+  const float ihs = frcp(T.hs);
+  const float u = fminf(fmaxf((x - T.ox) * ihs, -4.0f), (float)(T.nx + 4));
+  const float v = fminf(fmaxf((y - T.oy) * ihs, -4.0f), (float)(T.ny + 4));
+  const float fu = floorf(u), fv = floorf(v);
+  const int i = (int)fu, j = (int)fv;
+  const float a = u - fu, b = v - fv;
+  f2 c00, c10, c01, c11;
+  const int li = i - T.pi0, lj = j - T.pj0;
+  if (T.patch && li >= 0 && li < PSZ - 1 && lj >= 0 && lj < PSZ - 1) {
+    const float2* pp = T.patch + li * PSZ + lj;
+    const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZ], q11 = pp[PSZ + 1];
+    c00 = f2{q00.x, q00.y}; c01 = f2{q01.x, q01.y}; c10 = f2{q10.x, q10.y}; c11 = f2{q11.x, q11.y};
+  } else {
+    c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
+    c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
+    c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
+    c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
+  }
+  const float a1 = 1.0f - a, b1 = 1.0f - b;
+  h = (a1 * b1) * c00 + (a * b1) * c10 + (a1 * b) * c01 + (a * b) * c11;
+  gx = (b1 * (c10 - c00) + b * (c11 - c01)) * ihs;
+  gy = (a1 * (c01 - c00) + a * (c11 - c10)) * ihs;
+}
+
+// penalty contact of a sphere (centre p, velocity pv, radius r) with the floor (pushes up)
+// and the ceiling (pushes down), both layers at once; F = floor + ceiling force
+__device__ __forceinline__ void sphere_contact_pk(const Terr& T, const CP& C, const float* p, const float* pv, float r,
+                                                  float* F) {
+  f2 h, gx, gy;
+  height_query_pk(T, p[0], p[1], h, gx, gy);
+  const f2 sg = f2{1.0f, -1.0f};
+  const f2 dv = sg * (h - p[2]) + r;  // floor: h + r - z, ceiling: z + r - h
+  f2 nx = -sg * gx, ny = -sg * gy;
+  f2 inv = nx * nx + ny * ny + 1.0f;
+  inv = f2{frsq(inv.x), frsq(inv.y)};
+  nx = nx * inv;
+  ny = ny * inv;
+  const f2 nz = sg * inv;
+  const f2 depth = dv * inv;
+  const f2 vn = pv[0] * nx + pv[1] * ny + pv[2] * nz;
+  const f2 fn = C.k * depth - C.d * vn;
+  const f2 vtx = pv[0] - vn * nx, vty = pv[1] - vn * ny, vtz = pv[2] - vn * nz;
+  const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
+  const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
+  const f2 vtn = vt2 * ivt;
+  const f2 cf = C.kf * vtn, cm = C.mu * fn;
+  const f2 ft = f2{fminf(cf.x, cm.x), fminf(cf.y, cm.y)};
+  const f2 fti = ft * ivt;
+  // a layer acts only in penetration with a compressive normal force
+  const bool ax = dv.x > 0.0f && fn.x > 0.0f, ay = dv.y > 0.0f && fn.y > 0.0f;
+  const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
+  const f2 sc = f2{(ax && vtn.x > 1e-9f) ? fti.x : 0.0f, (ay && vtn.y > 1e-9f) ? fti.y : 0.0f};
+  const f2 Fx = fa * nx - sc * vtx, Fy = fa * ny - sc * vty, Fz = fa * nz - sc * vtz;
+  F[0] = Fx.x + Fx.y;
+  F[1] = Fy.x + Fy.y;
+  F[2] = Fz.x + Fz.y;
+}
+
 __device__ __forceinline__ void sphere_contact(const Terr& T, const CP& C, const float* p, const float* pv, float r,
                                                float* F) {
   F[0] = F[1] = F[2] = 0.0f;
@@ -854,7 +930,11 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
     const float rr = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
     float pw[3], vw[3], F[3], f6[6] = {0, 0, 0, 0, 0, 0};
     point_kin(Rs, ps, vs, lp, pw, vw);
+#if GO1_PK_CONTACT
+    sphere_contact_pk(T, C, pw, vw, rr, F);
+#else
     sphere_contact(T, C, pw, vw, rr, F);
+#endif
     point_force(Rs, lp, F, f6);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {

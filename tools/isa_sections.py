@@ -11,13 +11,15 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = "/tmp/go1_isa"
+sys.path.insert(0, REPO)
+from legged_tracking_amd.build import STEP_FLAGS as PKFLAGS  # noqa: E402
 
 
 def main():
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(REPO, "legged_tracking_amd", "csrc", "go1_step.hip")
     extra = sys.argv[1:]
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", *PKFLAGS,
                     "-DGO1_ISA_MARKS", *extra, "-c", "--save-temps", "-o", os.path.join(OUT, "k.o"), src],
                    cwd=OUT, check=True)
     s = open(os.path.join(OUT, "go1_step-hip-amdgcn-amd-amdhsa-gfx950.s")).read().splitlines()
