@@ -552,7 +552,7 @@ def f32(x):
 
 # Native physics constants (no reference counterpart: PhysX is closed)
 PHYSICS = dict(contact_stiffness=2.0e4, contact_damping=80.0, friction_damping=60.0,
-               limit_stiffness=150.0, limit_damping=2.0, n_internal=2)
+               limit_stiffness=2000.0, limit_damping=20.0, n_internal=2)
 
 
 def build_abi_config(cfg, n_envs=None, physics=None, actuator=None, hf_shape=(80, 40)):

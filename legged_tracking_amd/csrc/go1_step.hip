@@ -76,6 +76,7 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #define NB 17
 #define EPB 16          // envs per block of the reset kernel (4 lanes per env)
 #define TPB 64          // one wave per block
+#define GO1_DIVERGED 1.0e4f  // |state component| treated as a diverged integrator
 #define SEPB 4          // envs per wave of the step kernel (16 lanes per env: 4 roles x 4 legs)
 #define PI_F 3.14159265358979323846f
 #define TWO_PI_F 6.28318548202514648438f  // (float)(2*pi), torch's f32 scalar
@@ -972,12 +973,17 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       const int ax = j == 0 ? 0 : 1;
       const int dof = leg * 3 + j;
       float t = tau[j];
+      // joint-limit spring-damper, implicit in the joint: the torque at the end of the
+      // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
+      // into the joint inertia D (unconditionally stable for any k, d)
       const float lo = lds[GO1_MODEL_FLOATS + dof * 2], hi = lds[GO1_MODEL_FLOATS + dof * 2 + 1];
-      if (S.q[j] > hi) t -= cfg->limit_stiffness * (S.q[j] - hi) + cfg->limit_damping * S.qd[j];
-      else if (S.q[j] < lo) t -= cfg->limit_stiffness * (S.q[j] - lo) + cfg->limit_damping * S.qd[j];
+      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
+      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
+      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
+      t -= lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f;
 #pragma unroll
       for (int i = 0; i < 6; ++i) U[j][i] = si_get(IA, i, ax);
-      D[j] = si_get(IA, ax, ax);
+      D[j] = si_get(IA, ax, ax) + (lim_on ? h * dl + h * h * kl : 0.0f);
       u[j] = t - pA[j][ax];
       const float invD = frcp(D[j]);
       D[j] = invD;  // the forward pass only needs 1 / D
@@ -1463,19 +1469,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // ================= post_physics_step (:114-169), contraction off =================
   const int ep = ep_in + 1;
   float blv[3], bav[3], pg[3], rpy[3], rel_lin[3], rel_rot[3];
-  {
+  auto post_kin = [&](const float* tr) {
     const float qb[4] = {root[3], root[4], root[5], root[6]};
     quat_rotate_inverse_f(qb, root + 7, blv);
     quat_rotate_inverse_f(qb, root + 10, bav);
     quat_rotate_inverse_f(qb, A.gravity_vec, pg);
     // _plan_target_pose / _compute_relative_target_pose (:850-932)
-    const float* tr = traj_in;
     const float rel_in[3] = {tr[0] - root[0], tr[1] - root[1], tr[2] - root[2]};
     quat_apply_yaw_inverse_f(qb, rel_in, rel_lin);
     quat_to_rpy_f(qb, rpy);
 #pragma unroll
     for (int i = 0; i < 3; ++i) rel_rot[i] = wrap_to_pi_f(tr[3 + i] - rpy[i]);
-  }
+  };
+  post_kin(traj_in);
   float cmd[2] = {rel_lin[0], rel_lin[1]};
 
   MARK(post_kin_done);
@@ -1501,18 +1507,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // check_termination (:198-216)
   const bool time_out = (float)ep > c->max_episode_length;
-  bool reset = time_out;
+  bool reset = time_out, diverged = false;
   if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = true;
   if (!INJ) {
     // native-integrator divergence guard (no reference counterpart: PhysX does not
-    // return non-finite states): an env whose state is not finite is reset
+    // return non-finite states): an env whose state is not finite, or beyond
+    // GO1_DIVERGED in any component, is reset, and nothing of its diverged state reaches
+    // an output (zero reward, post-reset observations, see below)
     bool finite = true;
 #pragma unroll
-    for (int i = 0; i < 13; ++i) finite = finite && isfinite(root[i]);
+    for (int i = 0; i < 13; ++i) finite = finite && fabsf(root[i]) < GO1_DIVERGED;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) finite = finite && isfinite(q[j]) && isfinite(qd[j]);
-    finite = qsum(finite ? 0.0f : 1.0f) == 0.0f;
-    if (!finite) reset = true;
+    for (int j = 0; j < 3; ++j) finite = finite && fabsf(q[j]) < GO1_DIVERGED && fabsf(qd[j]) < GO1_DIVERGED;
+    diverged = qsum(finite ? 0.0f : 1.0f) != 0.0f;
+    if (diverged) reset = true;
   }
 
   MARK(termination_done);
@@ -1561,6 +1569,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float ae = sq_f(ta - bav[2]);
     terms[9] = expf(-ae / c->tracking_sigma_ang);
   }
+  if (diverged)
+#pragma unroll
+    for (int k = 0; k < GO1_NUM_TERMS; ++k) terms[k] = 0.0f;
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
 #pragma unroll
   for (int k = 0; k < GO1_NUM_TERMS; ++k) {
@@ -1589,7 +1600,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int k = 0; k < GO1_NUM_SUMS; ++k) lg[k] = sums[k];
     lg[13] = (float)ep;
     lg[14] = reached ? 1.0f : 0.0f;
-    lg[15] = norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+    lg[15] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
   }
   if (reset) {
     reset_env(c, K.ter, rng, e, leg, root, q, qd, strength, offset, traj_new);
@@ -1598,6 +1609,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = 0.0f;
     cmd[0] = 0.0f;  // commands is a view of local_relative_linear, zeroed by reset_idx (:252, :802)
     cmd[1] = 0.0f;
+    // a diverged env observes (and stores as its pitch) its post-reset pose instead
+    if (diverged) post_kin(traj_new);
   }
   const int coll_count = reset ? 0 : coll_in + (int)coll;
 
@@ -1684,7 +1697,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     if (owner)
 #pragma unroll
-      for (int i = 0; i < 3; ++i) ax[20 + leg * 3 + i] = torque[i];
+      for (int i = 0; i < 3; ++i) ax[20 + leg * 3 + i] = diverged ? 0.0f : torque[i];
   }
 
   MARK(aux_done);

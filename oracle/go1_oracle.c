@@ -573,11 +573,16 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
       double t = tau[dof];
       /* native joint-limit spring-damper at the URDF limits */
-      double lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1];
-      if (S->q[dof] > hi) t -= cfg->limit_stiffness * (S->q[dof] - hi) + cfg->limit_damping * S->qd[dof];
-      else if (S->q[dof] < lo) t -= cfg->limit_stiffness * (S->q[dof] - lo) + cfg->limit_damping * S->qd[dof];
+      /* implicit in the joint: the torque at the end of the sub-step, -k (q + h qd') - d qd'
+         with qd' = qd + h qdd, moves (h d + h^2 k) qdd to the joint inertia D */
+      double lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1], Dimp = 0.0;
+      if (S->q[dof] > hi || S->q[dof] < lo) {
+        double ex = S->q[dof] > hi ? S->q[dof] - hi : S->q[dof] - lo;
+        t -= cfg->limit_stiffness * (ex + h * S->qd[dof]) + cfg->limit_damping * S->qd[dof];
+        Dimp = h * cfg->limit_damping + h * h * cfg->limit_stiffness;
+      }
       for (int i = 0; i < 6; ++i) U[l][j][i] = IA[j].m[i][ax];
-      D[l][j] = IA[j].m[ax][ax];
+      D[l][j] = IA[j].m[ax][ax] + Dimp;
       u[l][j] = t - pA[j][ax];
       M6 Ia;
       double pa[6], Iac[6];
@@ -793,6 +798,22 @@ static void foot_world(const Model* M, const float* root, const float* dp, int l
 }
 
 /* Full step for env e.  Returns nothing; writes outputs. */
+#define GO1_DIVERGED 1.0e4f /* |state component| treated as a diverged integrator (HIP kernel) */
+
+/* base velocities, projected gravity, relative target pose and rpy of a root state
+ * (:119-136, _compute_relative_target_pose :922-932) */
+static void post_kin(const float* root, const float* gravity_vec, const float* tr, float* blv, float* bav, float* pg,
+                     float* rel_lin, float* rpy, float* rel_rot) {
+  float q[4] = {root[3], root[4], root[5], root[6]};
+  quat_rotate_inverse_f(q, root + 7, blv);
+  quat_rotate_inverse_f(q, root + 10, bav);
+  quat_rotate_inverse_f(q, gravity_vec, pg);
+  float rel_in[3] = {tr[0] - root[0], tr[1] - root[1], tr[2] - root[2]};
+  quat_apply_yaw_inverse_f(q, rel_in, rel_lin);
+  quat_to_rpy_f(q, rpy);
+  for (int i = 0; i < 3; ++i) rel_rot[i] = wrap_to_pi_f(tr[3 + i] - rpy[i]);
+}
+
 static void step_env(const go1_config* c, const Model* M, const go1_state* st, const go1_terrain* ter,
                      const go1_step_args* a, int e) {
   const int n = c->n_envs;
@@ -857,11 +878,8 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   /* ---------------- post_physics_step (:114-169) */
   int ep = st->episode_length[e] + 1;
   st->episode_length[e] = ep;
-  float q[4] = {root[3], root[4], root[5], root[6]};
-  float blv[3], bav[3], pg[3];
-  quat_rotate_inverse_f(q, root + 7, blv);
-  quat_rotate_inverse_f(q, root + 10, bav);
-  quat_rotate_inverse_f(q, a->gravity_vec, pg);
+  float blv[3], bav[3], pg[3], rel_lin[3], rpy[3], rel_rot[3];
+  post_kin(root, a->gravity_vec, st->trajectory + (size_t)e * 6, blv, bav, pg, rel_lin, rpy, rel_rot);
 
   /* _get_heights (:1918-1965), camera pitch = previous step's base_rotation */
   float* brot = st->base_rotation + (size_t)e * 3;
@@ -896,15 +914,6 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   }
   if (a->dbg_heights) memcpy(a->dbg_heights + (size_t)e * 2 * GO1_GRID_X * GO1_GRID_Y, heights, sizeof(heights));
 
-  /* _plan_target_pose / _compute_relative_target_pose (:850-932) */
-  float* tr = st->trajectory + (size_t)e * 6;
-  float rel_in[3] = {tr[0] - root[0], tr[1] - root[1], tr[2] - root[2]};
-  float rel_lin[3];
-  quat_apply_yaw_inverse_f(q, rel_in, rel_lin);
-  float rpy[3];
-  quat_to_rpy_f(q, rpy);
-  float rel_rot[3];
-  for (int i = 0; i < 3; ++i) rel_rot[i] = wrap_to_pi_f(tr[3 + i] - rpy[i]);
   for (int i = 0; i < 3; ++i) brot[i] = rpy[i];
   float cmd[2] = {rel_lin[0], rel_lin[1]}; /* command_type "xy" (:801-802) */
 
@@ -936,13 +945,14 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
 
   /* check_termination (:198-216) */
   int time_out = (float)ep > c->max_episode_length;
-  int reset = time_out;
+  int reset = time_out, diverged = 0;
   if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = 1;
   if (!a->inj_dof) { /* native-integrator divergence guard (see the HIP kernel) */
     int finite = 1;
-    for (int i = 0; i < 13; ++i) finite = finite && isfinite(root[i]);
-    for (int d = 0; d < NDOF; ++d) finite = finite && isfinite(dp[d]) && isfinite(dv[d]);
-    if (!finite) reset = 1;
+    for (int i = 0; i < 13; ++i) finite = finite && fabsf(root[i]) < GO1_DIVERGED;
+    for (int d = 0; d < NDOF; ++d) finite = finite && fabsf(dp[d]) < GO1_DIVERGED && fabsf(dv[d]) < GO1_DIVERGED;
+    diverged = !finite;
+    if (diverged) reset = 1;
   }
 
   /* compute_reward (:320-355) with RewardsCrawling terms */
@@ -988,6 +998,8 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     float ae = sq_f(ta - bav[2]);
     terms[9] = expf(-ae / c->tracking_sigma_ang);
   }
+  if (diverged) /* nothing of a diverged state reaches an output */
+    for (int k2 = 0; k2 < GO1_NUM_TERMS; ++k2) terms[k2] = 0.0f;
   if (a->dbg_terms) memcpy(a->dbg_terms + (size_t)e * GO1_NUM_TERMS, terms, sizeof(terms));
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
   float* sums = st->episode_sums + (size_t)e * GO1_NUM_SUMS;
@@ -1011,12 +1023,16 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     for (int k2 = 0; k2 < GO1_NUM_SUMS; ++k2) lg[k2] = sums[k2];
     lg[13] = (float)ep;
     lg[14] = reached ? 1.0f : 0.0f;
-    lg[15] = norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+    lg[15] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
   }
   if (reset) {
     reset_env(c, st, ter, e, a, U);
     cmd[0] = 0.0f;
     cmd[1] = 0.0f;
+    if (diverged) { /* a diverged env observes (and stores as its pitch) its post-reset pose */
+      post_kin(root, a->gravity_vec, st->trajectory + (size_t)e * 6, blv, bav, pg, rel_lin, rpy, rel_rot);
+      for (int i = 0; i < 3; ++i) brot[i] = rpy[i];
+    }
   }
   if (a->dbg_commands) { a->dbg_commands[e * 2] = cmd[0]; a->dbg_commands[e * 2 + 1] = cmd[1]; }
 
@@ -1073,7 +1089,7 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     ax[6] = cmd[0];
     ax[7] = cmd[1];
     for (int l = 0; l < 4; ++l) foot_world(M, root, dp, l, ax + 8 + 3 * l);
-    for (int d = 0; d < NDOF; ++d) ax[20 + d] = torque[d];
+    for (int d = 0; d < NDOF; ++d) ax[20 + d] = diverged ? 0.0f : torque[d];
   }
 
   /* epilogue (:148-153) */

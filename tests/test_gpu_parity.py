@@ -208,6 +208,8 @@ def test_diverged_envs_reset_without_faulting():
     st["root"][17, 2] = np.inf
     st["root"][40, 0:2] = 1e30
     st["dof_pos"][63, 4] = -np.inf
+    st["dof_vel"][50, 7] = 3e4  # finite but beyond GO1_DIVERGED
+    bad = np.append(bad, 50)
     g = native.Go1Native(c, DEV)
     g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
     g.state.load(st.arrays)
@@ -218,10 +220,12 @@ def test_diverged_envs_reset_without_faulting():
         torch.cuda.synchronize()
         if t == 0:
             assert g.reset.cpu().numpy()[bad].all()
+            # nothing of a diverged state reaches an output: zero reward, post-reset obs
+            np.testing.assert_array_equal(g.rew.cpu().numpy()[bad], 0.0)
+        assert np.isfinite(g.obs.cpu().numpy()).all() and np.isfinite(g.rew.cpu().numpy()).all()
+        assert np.isfinite(g.state["base_rotation"].cpu().numpy()).all()
     gs = g.state.numpy()
     assert np.isfinite(gs["root"]).all() and np.isfinite(gs["dof_pos"]).all()
-    good = np.setdiff1d(np.arange(n), bad)
-    assert np.isfinite(g.obs.cpu().numpy()[good]).all()
 
 
 def test_env_api_on_gpu_matches_oracle_backend():

@@ -4,10 +4,11 @@
 #   gpurun: bash tools/variants.sh run NAME [NAME ...]
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 B="$ROOT/legged_tracking_amd/_build"
+BASEFLAGS=${BASEFLAGS--fno-slp-vectorize}
 if [ "$1" = build ]; then
   shift
   while [ $# -gt 1 ]; do
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off -fno-slp-vectorize $2 \
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off $BASEFLAGS $2 \
       -o "$B/libgo1_var_$1.so" "$ROOT/legged_tracking_amd/csrc/go1_step.hip" || exit 1
     echo "built $1: $2"; shift 2
   done
