@@ -25,6 +25,7 @@
 // integrator uses FMA contraction and native sin/cos (f32, compared with the
 // oracle's f64 integrator within a tolerance).
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -76,7 +77,20 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #define NB 17
 #define EPB 16          // envs per block of the reset kernel (4 lanes per env)
 #define TPB 64          // one wave per block
-#define GO1_DIVERGED 1.0e4f  // |state component| treated as a diverged integrator
+// LDS copy of the per-joint config arrays, contiguous in go1_config from default_dof_pos
+// (checked at go1_create): default_dof_pos, dof_pos_limits, torque_limits, hard_limits,
+// height_grid_x, height_grid_y, after the model block
+#define LDS_DDP (GO1_MODEL_FLOATS)
+#define LDS_DPL (LDS_DDP + 12)
+#define LDS_TL (LDS_DPL + 24)
+#define LDS_HL (LDS_TL + 12)
+#define LDS_GX (LDS_HL + 24)
+#define LDS_GY (LDS_GX + GO1_GRID_X)
+#define LDS_FLOATS (LDS_GY + GO1_GRID_Y)
+#define GO1_DIVERGED 1.0e4f
+static_assert(offsetof(go1_config, height_grid_y) - offsetof(go1_config, default_dof_pos) ==
+                  (LDS_GY - LDS_DDP) * sizeof(float),
+              "per-joint config arrays must be contiguous in go1_config");  // |state component| treated as a diverged integrator
 #define SEPB 4          // envs per wave of the step kernel (16 lanes per env: 4 roles x 4 legs)
 #define PI_F 3.14159265358979323846f
 #define TWO_PI_F 6.28318548202514648438f  // (float)(2*pi), torch's f32 scalar
@@ -828,7 +842,7 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
 // two per lane, so each wave has four envs and the whole grid fills every SIMD.
 // cf_out: this lane's reported contact forces (thigh, calf, foot of its leg; base).
-// `lds` = the model block (GO1_MODEL_FLOATS) followed by the 24 hard joint limits, staged
+// `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
 // in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
 __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* lds, Phys& S, const float* tau, float h,
@@ -976,7 +990,7 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
       // joint-limit spring-damper, implicit in the joint: the torque at the end of the
       // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
       // into the joint inertia D (unconditionally stable for any k, d)
-      const float lo = lds[GO1_MODEL_FLOATS + dof * 2], hi = lds[GO1_MODEL_FLOATS + dof * 2 + 1];
+      const float lo = lds[LDS_HL + dof * 2], hi = lds[LDS_HL + dof * 2 + 1];
       const bool lim_on = S.q[j] > hi || S.q[j] < lo;
       const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
       const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
@@ -1244,9 +1258,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
   __shared__ float2 s_patch[SEPB][PSZ * PSZ];
   __shared__ int s_patch_meta[SEPB][3];
-  __shared__ float s_phys[GO1_MODEL_FLOATS + 24];
-  for (int i = lane; i < GO1_MODEL_FLOATS + 24; i += 64)
-    s_phys[i] = i < GO1_MODEL_FLOATS ? c->model[i] : c->hard_limits[i - GO1_MODEL_FLOATS];
+  __shared__ float s_phys[LDS_FLOATS];
+  for (int i = lane; i < LDS_FLOATS; i += 64)
+    s_phys[i] = i < GO1_MODEL_FLOATS ? c->model[i] : c->default_dof_pos[i - GO1_MODEL_FLOATS];
   __syncthreads();
   if (c->terrain_kind == 1) {
     const int tix = K.ter.env_tile[e];
@@ -1430,8 +1444,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   auto sample = [&](int i, int j, float& h0, float& h1) {
     if (hplane) { h0 = 1.0f; h1 = 0.0f; return; }
-    float px = c->height_grid_x[i] + scan_x;
-    float py = c->height_grid_y[j] + scan_y;
+    float px = s_phys[LDS_GX + i] + scan_x;
+    float py = s_phys[LDS_GY + j] + scan_y;
     if (c->camera_zero) { px = px + camx; py = py + camy; }
     px = px - T.ox;
     py = py - T.oy;
@@ -1541,8 +1555,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int d = leg * 3 + j;
-      const float lo = q[j] - c->dof_pos_limits[2 * d];
-      const float hi = q[j] - c->dof_pos_limits[2 * d + 1];
+      const float lo = q[j] - s_phys[LDS_DPL + 2 * d];
+      const float hi = q[j] - s_phys[LDS_DPL + 2 * d + 1];
       const float o = -(lo < 0.0f ? lo : 0.0f);
       x[j] = o + (hi > 0.0f ? hi : 0.0f);
     }
@@ -1633,7 +1647,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (role < 3) {
     const int j = role, d = leg * 3 + role;
     const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act);
-    put(5 + d, (qj - c->default_dof_pos[d]) * c->obs_scale_dof_pos, c->noise_dof_pos, true);
+    put(5 + d, (qj - s_phys[LDS_DDP + d]) * c->obs_scale_dof_pos, c->noise_dof_pos, true);
     put(17 + d, qdj * c->obs_scale_dof_vel, c->noise_dof_vel, true);
     put(29 + d, aj, 0.0f, false);
   }
