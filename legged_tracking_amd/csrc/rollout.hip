@@ -232,12 +232,26 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const 
 #endif
 constexpr int PW = GO1_POLICY_WAVES;  // waves per workgroup (8: two per SIMD, 16: four per SIMD)
 
+#ifdef GO1_POLICY_STAMPS  // diagnostic build only (tools/policy_stamps.py): s_memtime per wave per phase
+#define PSTAMP_SLOTS 12
+__device__ unsigned long long g_pstamps[512 * 16 * PSTAMP_SLOTS];
+#define PSTAMP(k)                                                                                   \
+  do {                                                                                              \
+    unsigned long long t_;                                                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                   \
+    if (blockIdx.x < 512) g_pstamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * PSTAMP_SLOTS + (k)] = t_; \
+  } while (0)
+#else
+#define PSTAMP(k)
+#endif
+
 __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   __shared__ float xa[PIN][16], xc[PIN][16];  // actor / critic inputs (adaptation uses xa)
   __shared__ float h1[2][512][16];             // layer-1 outputs (actor, critic); layer 3 reuses it
   __shared__ float h2[2][256][16];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int e0 = blockIdx.x * 16;
+  PSTAMP(0);
   const int ne = min(16, P.n_envs - e0);
   for (int idx = tid; idx < 16 * PIN; idx += 64 * PW) {
     const int e = idx / PIN, k = idx - e * PIN;
@@ -247,6 +261,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     xc[k][e] = (e < ne && k >= P.hist_dim && k < P.hist_dim + 2) ? P.privileged_obs[(size_t)(e0 + e) * 2 + (k - P.hist_dim)] : v;
   }
   __syncthreads();
+  PSTAMP(1);
   const PolicyLayer* Ls = P.layers;
   // adaptation module (xa rows >= hist_dim are still zero)
   {
@@ -255,12 +270,14 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     policy_tiles<16 / PW, 1>(Ls + 0, PIN / 4, s0, wave, PW, d0, true, lane);  // 256
   }
   __syncthreads();
+  PSTAMP(2);
   {
     const float(*s0[1])[16] = {h1[0]};
     float(*d0[1])[16] = {h2[0]};
     if (wave < 8) policy_tiles<1, 1>(Ls + 1, 256 / 4, s0, wave, 8, d0, true, lane);  // 128
   }
   __syncthreads();
+  PSTAMP(3);
   if (wave == 0) {
     const int q = lane >> 4, c = lane & 15;
     f4_t acc = *reinterpret_cast<const f4_t*>(Ls[2].b + 4 * q);
@@ -281,6 +298,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     }
   }
   __syncthreads();
+  PSTAMP(4);
   // actor and critic, layer by layer; wave w takes tiles w, w + 4, ... of both nets
   const PolicyLayer LA1[2] = {Ls[3], Ls[7]}, LA2[2] = {Ls[4], Ls[8]}, LA3[2] = {Ls[5], Ls[9]};
   {
@@ -289,12 +307,14 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     policy_tiles<32 / PW, 2>(LA1, PIN / 4, s1, wave, PW, d1, true, lane);  // 512
   }
   __syncthreads();
+  PSTAMP(5);
   {
     const float(*s2[2])[16] = {h1[0], h1[1]};
     float(*d2[2])[16] = {h2[0], h2[1]};
     policy_tiles<16 / PW, 2>(LA2, 512 / 4, s2, wave, PW, d2, true, lane);  // 256
   }
   __syncthreads();
+  PSTAMP(6);
   {
     const float(*s3[2])[16] = {h2[0], h2[1]};
     float(*d3[2])[16] = {h1[0], h1[1]};
@@ -309,6 +329,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     }
   }
   __syncthreads();
+  PSTAMP(7);
   if (wave < 2) {
     const int q = lane >> 4, c = lane & 15;
     const PolicyLayer L = Ls[wave == 0 ? 6 : 10];
@@ -367,11 +388,19 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
       }
     }
   }
+  PSTAMP(8);
 }
 
 }  // namespace
 
 extern "C" {
+
+#ifdef GO1_POLICY_STAMPS
+int go1_policy_stamps(void* host, size_t bytes) {
+  if (bytes > sizeof(g_pstamps)) bytes = sizeof(g_pstamps);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pstamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 const char* go1_rollout_last_error(void) { return g_err.c_str(); }
 
