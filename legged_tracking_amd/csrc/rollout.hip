@@ -157,6 +157,12 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
 // ELU between layers.  Activations stay in LDS as [feature][env] (B-fragment reads are
 // conflict-free rows of 16 floats); weights are pre-packed on the host into fragment
 // order (one coalesced 256 B load per MFMA, L2-resident: 2.8 MB for all three nets).
+#ifndef GO1_POLICY_SCHED
+#define GO1_POLICY_SCHED 1
+#endif
+#ifndef GO1_POLICY_PREFETCH
+#define GO1_POLICY_PREFETCH 2
+#endif
 constexpr int PIN = 272;  // 261 / 263 inputs padded to a multiple of 16
 
 typedef go1_policy_layer PolicyLayer;  // w packed [n/16][k/4][64], b [n padded to 16]
@@ -190,6 +196,11 @@ __device__ __forceinline__ void policy_load(const PolicyLayer* L, int G, int g, 
 #pragma unroll
     for (int i = 0; i < NT; ++i)
       w[l][i] = reinterpret_cast<const f4_t*>(L[l].w)[((size_t)(tile0 + i * tstride) * G + g) * 64 + lane];
+#if GO1_POLICY_SCHED
+  // keep the prefetch where it is written: otherwise the scheduler sinks the loads next to
+  // their MFMAs and the waits become vmcnt(1), exposing the L2 latency every group
+  __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
 // NT output tiles (tile0 + i * tstride) of NL layers at the same depth (the actor and the
@@ -207,6 +218,57 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const 
 #pragma unroll
     for (int i = 0; i < NT; ++i)
       acc[l][i] = *reinterpret_cast<const f4_t*>(L[l].b + 16 * (tile0 + i * tstride) + 4 * q);
+#if GO1_POLICY_PREFETCH == 3
+  // weights two groups ahead, B operands (LDS) one group ahead of the MFMAs
+  float ba[NL][4], bb[NL][4];
+  auto read_b = [&](int g, float (&b)[NL][4]) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) b[l][u] = src[l][16 * g + 4 * u + q][c];
+  };
+  auto mfma_group = [&](const f4_t (&w)[NL][NT], const float (&b)[NL][4]) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) acc[l][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[l][i][u], b[l][u], acc[l][i], 0, 0, 0);
+  };
+  policy_load<NT, NL>(L, G, 0, tile0, tstride, lane, wa);
+  if (G > 1) policy_load<NT, NL>(L, G, 1, tile0, tstride, lane, wb);
+  read_b(0, ba);
+  for (int g = 0; g < G; g += 2) {
+    if (g + 1 < G) read_b(g + 1, bb);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_group(wa, ba);
+    if (g + 2 < G) {
+      policy_load<NT, NL>(L, G, g + 2, tile0, tstride, lane, wa);
+      read_b(g + 2, ba);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + 1 < G) {
+      mfma_group(wb, bb);
+      if (g + 3 < G) policy_load<NT, NL>(L, G, g + 3, tile0, tstride, lane, wb);
+    }
+  }
+#elif GO1_POLICY_PREFETCH == 4
+  // four weight buffers: loads run three groups ahead of the MFMAs
+  f4_t wc[NL][NT], wd[NL][NT];
+  policy_load<NT, NL>(L, G, 0, tile0, tstride, lane, wa);
+  if (G > 1) policy_load<NT, NL>(L, G, 1, tile0, tstride, lane, wb);
+  if (G > 2) policy_load<NT, NL>(L, G, 2, tile0, tstride, lane, wc);
+  for (int g = 0; g < G; g += 4) {
+    if (g + 3 < G) policy_load<NT, NL>(L, G, g + 3, tile0, tstride, lane, wd);
+    policy_group<NT, NL>(wa, src, g, q, c, acc);
+    if (g + 4 < G) policy_load<NT, NL>(L, G, g + 4, tile0, tstride, lane, wa);
+    if (g + 1 < G) policy_group<NT, NL>(wb, src, g + 1, q, c, acc);
+    if (g + 5 < G) policy_load<NT, NL>(L, G, g + 5, tile0, tstride, lane, wb);
+    if (g + 2 < G) policy_group<NT, NL>(wc, src, g + 2, q, c, acc);
+    if (g + 6 < G) policy_load<NT, NL>(L, G, g + 6, tile0, tstride, lane, wc);
+    if (g + 3 < G) policy_group<NT, NL>(wd, src, g + 3, q, c, acc);
+  }
+#else
   policy_load<NT, NL>(L, G, 0, tile0, tstride, lane, wa);
   if (G > 1) policy_load<NT, NL>(L, G, 1, tile0, tstride, lane, wb);
   for (int g = 0; g < G; g += 2) {
@@ -217,6 +279,7 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const 
       if (g + 3 < G) policy_load<NT, NL>(L, G, g + 3, tile0, tstride, lane, wb);
     }
   }
+#endif
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
