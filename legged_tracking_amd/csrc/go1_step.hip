@@ -174,6 +174,7 @@ __device__ __forceinline__ float rowsum4(float p) {
 // f32-input MFMA is bit-for-bit a k-ordered fmaf chain, and the oracle uses the
 // same k order (oracle/go1_oracle.c go1o_actuator_eval): torques are bit-identical.
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct MlpFrag {
   float w1[2][2];  // [mo][s] = W1[16 mo + i][4 s + q]  (0 for k >= 6)
@@ -206,27 +207,6 @@ __device__ __forceinline__ void mlp_load(const float* __restrict__ W, int lane, 
   F.b3 = W[1312];
 }
 
-#ifndef GO1_FAST_SOFTSIGN
-#define GO1_FAST_SOFTSIGN 1
-#endif
-// x / (|x| + 1).  The fast form (hardware reciprocal + one FMA residual correction)
-// equals the IEEE quotient for every finite |x| < 2^126 (exhaustive check over all
-// 2^32 inputs on gfx950: tools/probes/softsign_div.hip); for |x| >= 2^24 the IEEE
-// quotient is exactly +-1 (|x| + 1 rounds to |x|), and inf gives NaN, as IEEE.
-__device__ __forceinline__ float softsign(float x) {
-#if GO1_FAST_SOFTSIGN
-  const float ax = fabsf(x);
-  const float d = ax + 1.0f;
-  const float r = __builtin_amdgcn_rcpf(d);
-  const float q0 = x * r;
-  const float q = fmaf(fmaf(-q0, d, x), r, q0);
-  const float big = ax == __builtin_inff() ? __builtin_nanf("") : copysignf(1.0f, x);
-  return ax >= 16777216.0f ? big : q;
-#else
-  return x / (fabsf(x) + 1.0f);
-#endif
-}
-
 // b0 = X[k = q][item], b1v = X[k = 4 + q][item] (0 for q >= 2).  Returns the torque
 // of item (lane & 15) in all four lanes of the item.  Needs all 64 lanes active.
 __device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v) {
@@ -240,7 +220,11 @@ __device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) h1[m][r] = softsign(a1[m][r]);
+    for (int r = 0; r < 4; r += 2) {
+      const f2 h = pm_softsign2(f2{a1[m][r], a1[m][r + 1]});
+      h1[m][r] = h.x;
+      h1[m][r + 1] = h.y;
+    }
   f4 a2[2] = {F.b2[0], F.b2[1]};
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -249,11 +233,20 @@ __device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v
 #pragma unroll
       for (int mo = 0; mo < 2; ++mo)
         a2[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w2[mo][4 * m + r], h1[m][r], a2[mo], 0, 0, 0);
+  float h2[2][4];
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo)
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      const f2 h = pm_softsign2(f2{a2[mo][r], a2[mo][r + 1]});
+      h2[mo][r] = h.x;
+      h2[mo][r + 1] = h.y;
+    }
   float p = 0.0f;
 #pragma unroll
   for (int mo = 0; mo < 2; ++mo)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) p = fmaf(F.w3[mo][r], softsign(a2[mo][r]), p);
+    for (int r = 0; r < 4; ++r) p = fmaf(F.w3[mo][r], h2[mo][r], p);
   return rowsum4(p) + F.b3;
 }
 
@@ -682,7 +675,6 @@ struct CP {
 // ---- packed (v_pk_*_f32) contact: one wave issues a v_pk_fma_f32 (two FMAs) as fast as a
 // v_fma_f32 (tools/probes/pk_rate.hip), so the floor and ceiling layers of a point are
 // carried as the two halves of an f2 all the way from the bilinear patch to the force.
-typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
 
 // (floor, ceiling) heights and gradients at world (x, y), bilinear: the LDS patch stores

@@ -104,4 +104,48 @@ PM_FN float pm_atan2f(float y, float x) {
   return r;
 }
 
+/* ---- softsign x / (|x| + 1) of the actuator net, bit-identical to the IEEE quotient for
+ * every f32 input (exhaustive check of both forms over all 2^32 inputs on gfx950:
+ * tools/probes/softsign_div.hip).  Fast form: hardware reciprocal of d = |x| + 1 and one
+ * FMA residual correction of the quotient, exact for all finite |x| < 2^126.  For
+ * |x| >= 2^30 the IEEE quotient is exactly +-1 (|x| + 1 rounds to |x|), which is also what
+ * the fast form returns for an input clamped to +-2^30, so the input is clamped there
+ * (between 2^24 and 2^25 |x| + 1 can round UP, and the quotient is then not +-1);
+ * fma(q, x - x, q) returns q for finite x and NaN for inf / NaN, as IEEE does. */
+#ifndef GO1_FAST_SOFTSIGN
+#define GO1_FAST_SOFTSIGN 1
+#endif
+typedef float pm_f2 __attribute__((ext_vector_type(2)));
+#define PM_SOFTSIGN_LIM 1073741824.0f /* 2^30 */
+
+PM_FN float pm_softsign(float x) {
+#if GO1_FAST_SOFTSIGN
+  const float xc = fminf(fmaxf(x, -PM_SOFTSIGN_LIM), PM_SOFTSIGN_LIM);
+  const float d = fabsf(xc) + 1.0f;
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float q0 = xc * r;
+  /* residual t = q0 d - x, q = q0 - t r: the same roundings as q0 + (x - q0 d) r, and the
+     sign of a zero quotient survives (-0 -> -0) */
+  const float q = fmaf(-fmaf(q0, d, -xc), r, q0);
+  return fmaf(q, x - x, q);
+#else
+  return x / (fabsf(x) + 1.0f);
+#endif
+}
+
+/* two softsigns in the halves of v_pk_mul / v_pk_fma (same roundings as pm_softsign) */
+PM_FN pm_f2 pm_softsign2(pm_f2 x) {
+#if GO1_FAST_SOFTSIGN
+  const pm_f2 xc = {fminf(fmaxf(x.x, -PM_SOFTSIGN_LIM), PM_SOFTSIGN_LIM),
+                    fminf(fmaxf(x.y, -PM_SOFTSIGN_LIM), PM_SOFTSIGN_LIM)};
+  const pm_f2 d = {fabsf(xc.x) + 1.0f, fabsf(xc.y) + 1.0f};
+  const pm_f2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const pm_f2 q0 = xc * r;
+  const pm_f2 q = __builtin_elementwise_fma(-__builtin_elementwise_fma(q0, d, -xc), r, q0);
+  return __builtin_elementwise_fma(q, x - x, q);
+#else
+  return pm_f2{x.x / (fabsf(x.x) + 1.0f), x.y / (fabsf(x.y) + 1.0f)};
+#endif
+}
+
 #endif

@@ -40,6 +40,11 @@ def test_actuator_net_bit_exact_vs_oracle():
     rng = np.random.default_rng(0)
     x = rng.normal(0, 1, (200003, 6)).astype(np.float32)
     x[:1000] *= 30.0  # saturate the softsign
+    # pre-activations beyond 2^24 (the clamped path), up to overflow, and non-finite inputs
+    x[1000:1100] *= 1e7
+    x[1100:1200] *= 1e30
+    x[1200:1300] *= np.float32(3e38)
+    x[1300, 0], x[1301, 3], x[1302, 5] = np.inf, -np.inf, np.nan
     got = g.actuator(_dev(x)).cpu().numpy()
     want = O.actuator(CF.load_actuator(), x)
     np.testing.assert_array_equal(got, want)
