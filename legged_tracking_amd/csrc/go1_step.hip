@@ -67,6 +67,9 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #ifndef GO1_CONTACT_ROLL
 #define GO1_CONTACT_ROLL 0
 #endif
+#ifndef GO1_PK_POINTS
+#define GO1_PK_POINTS 1
+#endif
 #ifndef GO1_PK_CONTACT
 #define GO1_PK_CONTACT 1
 #endif
@@ -916,7 +919,72 @@ __device__ void phys_substep(const go1_config* __restrict__ cfg, const float* ld
   //      corner 2 leg, corner 2 leg + 1]; forces in the body frame of the point's body
   float fth[6] = {0, 0, 0, 0, 0, 0}, fca[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
   float Fth[3] = {0, 0, 0}, Fca[3] = {0, 0, 0}, Fft[3] = {0, 0, 0}, Fb[3] = {0, 0, 0};
-#ifndef GO1_ABL_NO_CONTACT
+#if !defined(GO1_ABL_NO_CONTACT) && GO1_PK_POINTS
+  {
+    // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
+    // the body-frame force; x = point 2 role, y = point 2 role + 1.  Bodies:
+    // role 0 (thigh, thigh), 1 (thigh, calf), 2 (calf, foot on the calf), 3 (base, base)
+    const bool xt = role <= 1, xc = role == 2, yt = role == 0, yc = role == 1 || role == 2;
+    f2 Rs[9], ps[3], vs[6], lp[3], rr;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rs[i] = f2{xt ? Rl[0][i] : (xc ? Rl[1][i] : R[i]), yt ? Rl[0][i] : (yc ? Rl[1][i] : R[i])};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      ps[i] = f2{xt ? pl[0][i] : (xc ? pl[1][i] : S.pos[i]), yt ? pl[0][i] : (yc ? pl[1][i] : S.pos[i])};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) vs[i] = f2{xt ? vl[0][i] : (xc ? vl[1][i] : vb[i]), yt ? vl[0][i] : (yc ? vl[1][i] : vb[i])};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = 2 * role + h;
+      const bool on_thigh = p < 3, on_base = p >= 6;
+      const int cx = leg * 2 + (p - 6);
+      const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
+      lp[0][h] = on_base ? ((cx & 1) ? th[0] : -th[0]) : (p == 5 ? foot[0] : 0.0f);
+      lp[1][h] = on_base ? ((cx & 2) ? th[1] : -th[1]) : (p == 5 ? foot[1] : 0.0f);
+      lp[2][h] = on_base ? ((cx & 4) ? th[2] : -th[2]) : (p == 5 ? foot[2] : lz);
+      rr[h] = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
+    }
+    // point kinematics: v = R (v_lin + w x lp), p = p_body + R lp
+    const f2 wl[3] = {vs[1] * lp[2] - vs[2] * lp[1], vs[2] * lp[0] - vs[0] * lp[2], vs[0] * lp[1] - vs[1] * lp[0]};
+    const f2 vlin[3] = {vs[3] + wl[0], vs[4] + wl[1], vs[5] + wl[2]};
+    f2 pw[3], vw[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pw[i] = ps[i] + Rs[3 * i] * lp[0] + Rs[3 * i + 1] * lp[1] + Rs[3 * i + 2] * lp[2];
+      vw[i] = Rs[3 * i] * vlin[0] + Rs[3 * i + 1] * vlin[1] + Rs[3 * i + 2] * vlin[2];
+    }
+    float Fa[3], Fb2[3];
+    {
+      const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
+      const float pb[3] = {pw[0].y, pw[1].y, pw[2].y}, vb2[3] = {vw[0].y, vw[1].y, vw[2].y};
+      sphere_contact_pk(T, C, pa, va, rr.x, Fa);
+      sphere_contact_pk(T, C, pb, vb2, rr.y, Fb2);
+    }
+    const f2 F[3] = {f2{Fa[0], Fb2[0]}, f2{Fa[1], Fb2[1]}, f2{Fa[2], Fb2[2]}};
+    // body-frame force f = R^T F and moment lp x f
+    f2 f6[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) f6[3 + j] = Rs[j] * F[0] + Rs[3 + j] * F[1] + Rs[6 + j] * F[2];
+    f6[0] = lp[1] * f6[5] - lp[2] * f6[4];
+    f6[1] = lp[2] * f6[3] - lp[0] * f6[5];
+    f6[2] = lp[0] * f6[4] - lp[1] * f6[3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const float tot = f6[i].x + f6[i].y;
+      fth[i] = role == 0 ? tot : (role == 1 ? f6[i].x : 0.0f);
+      fca[i] = role == 2 ? tot : (role == 1 ? f6[i].y : 0.0f);
+      fbase[i] = role == 3 ? tot : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float tot = F[i].x + F[i].y;
+      Fth[i] = role == 0 ? tot : (role == 1 ? F[i].x : 0.0f);
+      Fca[i] = role == 1 ? F[i].y : (role == 2 ? F[i].x : 0.0f);
+      Fft[i] = role == 2 ? F[i].y : 0.0f;
+      Fb[i] = role == 3 ? tot : 0.0f;
+    }
+  }
+#elif !defined(GO1_ABL_NO_CONTACT)
 #pragma unroll
   for (int sidx = 0; sidx < 2; ++sidx) {
     const int p = 2 * role + sidx;
