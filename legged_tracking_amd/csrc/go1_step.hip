@@ -64,6 +64,12 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #ifndef GO1_MLP_UNROLL_N
 #define GO1_MLP_UNROLL_N 4
 #endif
+#ifndef GO1_GLDS  // LDS-DMA staging of the model block and terrain patches
+#define GO1_GLDS 1
+#endif
+#ifndef GO1_MLP3  // the three MLP groups of a sub-step layer by layer (mlp_group3)
+#define GO1_MLP3 1
+#endif
 #ifndef GO1_CONTACT_ROLL
 #define GO1_CONTACT_ROLL 0
 #endif
@@ -251,6 +257,58 @@ __device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v
 #pragma unroll
     for (int r = 0; r < 4; ++r) p = fmaf(F.w3[mo][r], h2[mo][r], p);
   return rowsum4(p) + F.b3;
+}
+
+// The three groups of a sub-step (joints 0..2) at once, layer by layer: 6 independent
+// accumulator chains per layer keep the matrix pipe busy (one v_mfma_f32_16x16x4_f32 per
+// 32 cycles per SIMD), and the softsign VALU of one group issues under the MFMAs of the
+// next.  Each chain's k order is mlp_group's, so the torques are bit-identical to it.
+__device__ __forceinline__ void mlp_group3(const MlpFrag& F, const float* b0, const float* b1v, float* t) {
+  f4 a1[3][2];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) a1[g][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][0], b0[g], F.b1[mo], 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) a1[g][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][1], b1v[g], a1[g][mo], 0, 0, 0);
+  float h1[3][2][4];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f2 h = pm_softsign2(f2{a1[g][m][r], a1[g][m][r + 1]});
+        h1[g][m][r] = h.x;
+        h1[g][m][r + 1] = h.y;
+      }
+  f4 a2[3][2];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) { a2[g][0] = F.b2[0]; a2[g][1] = F.b2[1]; }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int mo = 0; mo < 2; ++mo)
+          a2[g][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w2[mo][4 * m + r], h1[g][m][r], a2[g][mo], 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    float p = 0.0f;
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo)
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f2 h = pm_softsign2(f2{a2[g][mo][r], a2[g][mo][r + 1]});
+        p = fmaf(F.w3[mo][r], h.x, p);
+        p = fmaf(F.w3[mo][r + 1], h.y, p);
+      }
+    t[g] = rowsum4(p) + F.b3;
+  }
 }
 
 // ---------------------------------------------------------------- torch-order f32 math
@@ -823,6 +881,12 @@ __device__ void foot_world(const float* __restrict__ model, const float* root, c
   out[0] = pp[0] + fw[0]; out[1] = pp[1] + fw[1]; out[2] = pp[2] + fw[2];
 }
 
+// The config block through the constant address space: every uniform field read is a
+// scalar (SMEM) load.  Through a generic pointer the compiler cannot prove that the
+// kernel's stores leave the block unchanged, and emits vector loads, each a full memory
+// round trip at its first use (inside the sub-step loop too).
+typedef const __attribute__((address_space(4))) go1_config CCfg;
+
 struct Phys {
   float pos[3], quat[4], v[3], w[3];  // base (replicated on the 16 lanes of the env)
   float q[3], qd[3];                   // this lane's leg
@@ -840,7 +904,7 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
 // in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
-__device__ void phys_substep(const go1_config* __restrict__ cfg, const float* lds, Phys& S, const float* tau, float h,
+__device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau, float h,
                              const float* g, float friction, float payload, const Terr& T, int leg, int role,
                              bool cf_out, float* cf_leg, float* cf_base) {
 #pragma clang fp contract(fast)
@@ -1215,7 +1279,7 @@ struct KArgs {
 };
 
 // reset_idx for one env, computed redundantly by the 4 lanes of its quad (:218-296)
-__device__ void reset_env(const go1_config* __restrict__ c, const go1_terrain& ter, const Rng& rng, int e, int leg,
+__device__ void reset_env(CCfg* __restrict__ c, const go1_terrain& ter, const Rng& rng, int e, int leg,
                           float* root, float* q, float* qd, float* strength, float* offset, float* traj) {
   float s = rng(0) * c->strength_range + c->strength_lo;
 #pragma unroll
@@ -1263,7 +1327,8 @@ __device__ void reset_env(const go1_config* __restrict__ c, const go1_terrain& t
 
 template <bool INJ>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) void go1_step_kernel(
-    const go1_config* __restrict__ c, KArgs K) {
+    const go1_config* __restrict__ c_gen, KArgs K) {
+  CCfg* __restrict__ c = (CCfg*)c_gen;
   const go1_state& st = K.st;
   const go1_step_args& A = K.a;
   const int n = c->n_envs;
@@ -1280,11 +1345,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
   MARK(kernel_begin);
   MlpFrag F;
-  mlp_load(c->actuator, lane, F);
+  mlp_load(c_gen->actuator, lane, F);  // lane-indexed: generic pointer
   const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset};
   // the previous step's extras["time_outs"] rebinding, for this wave's envs (flags of the
   // previous launch are complete now), and the flag the next launch will set is cleared
-  if (K.prev_time_out && sub16 == 0 && K.flags[K.prv]) K.prev_extras[e] = K.prev_time_out[e];
+  // (loaded with the state, applied after the prologue's single wait: no round trip of its own)
+  const bool rebind = K.prev_time_out != nullptr;
+  int rebind_flag = rebind ? K.flags[K.prv] : 0;
+  const uint8_t rebind_val = rebind ? K.prev_time_out[e] : 0;
   if (blockIdx.x == 0 && lane == 0) K.flags[K.nxt] = 0;
   const size_t d0 = (size_t)e * NDOF + leg * 3;
   const float* lag_in = st.lag + (size_t)e * 84 + leg * 3;
@@ -1305,41 +1373,99 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   // per-joint constants and the lag-ring slots the sub-steps read (1..4 for decimation
   // <= 4): loaded here so that no sub-step waits on a memory round trip
-  float dflt[3], tlim[3], lag_pre[4][3];
+  float dflt[3], tlim[3], lag_pre[GO1_LAG_SLOTS - 1][3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     dflt[j] = c->default_dof_pos[leg * 3 + j];
     tlim[j] = c->torque_limits[leg * 3 + j];
 #pragma unroll
-    for (int sl = 0; sl < 4; ++sl) lag_pre[sl][j] = lag_in[(sl + 1) * 12 + j];
+    for (int sl = 0; sl < GO1_LAG_SLOTS - 1; ++sl) lag_pre[sl][j] = lag_in[(sl + 1) * 12 + j];
   }
   const float friction = st.friction[e], payload = st.payload[e];
   const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
+  Phys P;
+  if (!INJ) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      P.pos[i] = st.root[(size_t)e * 13 + i];
+      P.v[i] = st.root[(size_t)e * 13 + 7 + i];
+      P.w[i] = st.root[(size_t)e * 13 + 10 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
+  }
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
   __shared__ float2 s_patch[SEPB][PSZ * PSZ];
-  __shared__ int s_patch_meta[SEPB][3];
-  __shared__ float s_phys[LDS_FLOATS];
-  for (int i = lane; i < LDS_FLOATS; i += 64)
-    s_phys[i] = i < GO1_MODEL_FLOATS ? c->model[i] : c->default_dof_pos[i - GO1_MODEL_FLOATS];
-  __syncthreads();
+  __shared__ float s_phys[(LDS_FLOATS + 63) / 64 * 64];
+  // Block = one wave, so LDS needs no barrier here (a wave's LDS operations execute in
+  // order).  The model block and the terrain patches are staged with LDS-DMA
+  // (global_load_lds: no VGPR round trip, no __syncthreads fence draining the state loads);
+  // nothing reads them before the first sub-step's physics, so the first actuator-net
+  // evaluation runs while they land (the compiler waits vmcnt before the first ds_read).
+  int tix = 0;  // the env's terrain tile and origin, loaded with the state
   if (c->terrain_kind == 1) {
-    const int tix = K.ter.env_tile[e];
-    T.tile = K.ter.tiles + (size_t)tix * 2 * c->hf_nx * c->hf_ny;
+    tix = K.ter.env_tile[e];
     T.ox = K.ter.env_terrain_origin[(size_t)e * 3];
     T.oy = K.ter.env_terrain_origin[(size_t)e * 3 + 1];
+  }
+#if GO1_GLDS
+  // every ordinary load of the prologue is waited for here, once: a use of an ordinary load
+  // result while LDS-DMA is in flight would make the compiler wait vmcnt(0) for the DMA too.
+  // The model block goes through VGPRs (ds_write after this wait): LDS written by DMA makes
+  // the compiler wait vmcnt(0) before every later ds_read of it, which would serialise the
+  // post-physics gathers behind the height-grid reads.
+  {
+    float mv[(LDS_FLOATS + 63) / 64];
+#pragma unroll
+    for (int k = 0; k < (LDS_FLOATS + 63) / 64; ++k) {
+      const int i = 64 * k + lane;
+      mv[k] = i < GO1_MODEL_FLOATS ? c_gen->model[i] : c_gen->default_dof_pos[min(i, LDS_FLOATS - 1) - GO1_MODEL_FLOATS];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#pragma unroll
+    for (int k = 0; k < (LDS_FLOATS + 63) / 64; ++k) s_phys[64 * k + lane] = mv[k];  // padded to 64
+  }
+#else
+  for (int i = lane; i < LDS_FLOATS; i += 64)
+    s_phys[i] = i < GO1_MODEL_FLOATS ? c_gen->model[i] : c_gen->default_dof_pos[i - GO1_MODEL_FLOATS];
+  __syncthreads();
+#endif
+  if (c->terrain_kind == 1) {
+    T.tile = K.ter.tiles + (size_t)tix * 2 * c->hf_nx * c->hf_ny;
     if (!INJ) {
       // patch centred on the base at the start of the step
-      const float bx = st.root[(size_t)e * 13], by = st.root[(size_t)e * 13 + 1];
+      const float bx = P.pos[0], by = P.pos[1];
       T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(c->hf_nx + 64))) - PSZ / 2;
       T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(c->hf_ny + 64))) - PSZ / 2;
       T.patch = &s_patch[el][0];
+      const int nx = c->hf_nx, ny = c->hf_ny;
+#if GO1_GLDS
+      // 32 LDS-DMA dword loads per wave: load k fills s_patch[k / 8] dwords 64 (k % 8) ..
+      // + 63, i.e. cells 32 (k % 8) + lane / 2, floor (lane even) or ceiling (lane odd).
+      // The env's tile and patch corner come from its lane 4 el (wave-uniform readlane).
+      const int cj = (lane >> 1) & 15, ci_l = lane >> 5;
+      const size_t layer_off = (lane & 1) ? 0 : (size_t)nx;  // floor = layer 1, ceiling = layer 0
+#pragma unroll
+      for (int el2 = 0; el2 < SEPB; ++el2) {
+        const int tix_s = __builtin_amdgcn_readlane(tix, 4 * el2);
+        const int pi_s = __builtin_amdgcn_readlane(T.pi0, 4 * el2);
+        const int pj_s = __builtin_amdgcn_readlane(T.pj0, 4 * el2);
+        const float* tl = K.ter.tiles + (size_t)tix_s * 2 * nx * ny;
+        const int gj = min(max(pj_s + cj, 0), ny - 1);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int gi = min(max(pi_s + 2 * k + ci_l, 0), nx - 1);
+          __builtin_amdgcn_global_load_lds(tl + (layer_off + gi) * ny + gj, (float*)&s_patch[el2][0] + 64 * k, 4, 0, 0);
+        }
+      }
+#else
+      __shared__ int s_patch_meta[SEPB][3];
       if (sub16 == 0) {
         s_patch_meta[el][0] = tix;
         s_patch_meta[el][1] = T.pi0;
         s_patch_meta[el][2] = T.pj0;
       }
       __syncthreads();
-      const int nx = c->hf_nx, ny = c->hf_ny;
       // 2 envs x 256 cells per pass: 8 cells (16 loads) in flight per lane
 #pragma unroll 1
       for (int el0 = 0; el0 < SEPB; el0 += 2) {
@@ -1358,24 +1484,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int k = 0; k < 8; ++k) s_patch[el0 + (k >> 2)][threadIdx.x + 64 * (k & 3)] = v[k];
       }
       __syncthreads();
+#endif
     }
   }
+  asm volatile("" : "+v"(rebind_flag));  // kept in a VGPR: a scalar branch on it would wait early
+  if (rebind && sub16 == 0 && rebind_flag) K.prev_extras[e] = rebind_val;
   float scaled[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     scaled[j] = act[j] * c->action_scale;
     if (j == 0) scaled[j] = scaled[j] * c->hip_scale_reduction;
-  }
-  Phys P;
-  if (!INJ) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      P.pos[i] = st.root[(size_t)e * 13 + i];
-      P.v[i] = st.root[(size_t)e * 13 + 7 + i];
-      P.w[i] = st.root[(size_t)e * 13 + 10 + i];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
   }
 
   // ---------------- decimation loop (:82-88)
@@ -1392,8 +1510,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int d = leg * 3 + j;
-      const float lg = slot <= 4 ? sel4(slot - 1, lag_pre[0][j], lag_pre[1][j], lag_pre[2][j], lag_pre[3][j])
-                                 : (slot < GO1_LAG_SLOTS ? lag_in[slot * 12 + j] : scaled[j]);
+      float lg = scaled[j];  // slot is wave-uniform: scalar-condition selects, no load in the loop
+#pragma unroll
+      for (int sl = GO1_LAG_SLOTS - 2; sl >= 0; --sl) lg = slot == sl + 1 ? lag_pre[sl][j] : lg;
       tgt[j] = lg + dflt[j];
       const float err = q[j] - tgt[j] + offset[j];
       xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
@@ -1404,18 +1523,22 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // its own leg and receives the item's torque in place.
     MARK(mlp_begin);
     float tq[3] = {0.0f, 0.0f, 0.0f};
+    float b0[3], b1v[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const float* y = xin[j];
-      const float b0 = sel4(lq, y[0], y[1], y[2], y[3]);
-      const float b1v = sel4(lq, y[4], y[5], 0.0f, 0.0f);
-#ifdef GO1_ABL_NO_MLP
-      const float t = 0.0f * (b0 + b1v);  // ablation build only: no actuator net
-#else
-      const float t = mlp_group(F, b0, b1v);
-#endif
-      tq[j] = t;
+      b0[j] = sel4(lq, y[0], y[1], y[2], y[3]);
+      b1v[j] = sel4(lq, y[4], y[5], 0.0f, 0.0f);
     }
+#ifdef GO1_ABL_NO_MLP
+#pragma unroll
+    for (int j = 0; j < 3; ++j) tq[j] = 0.0f * (b0[j] + b1v[j]);  // ablation build only: no actuator net
+#elif GO1_MLP3
+    mlp_group3(F, b0, b1v, tq);
+#else
+#pragma unroll
+    for (int j = 0; j < 3; ++j) tq[j] = mlp_group(F, b0[j], b1v[j]);
+#endif
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
     for (int j = 0; j < 3; ++j) tq[j] += -20.0f * xin[j][0] - 0.5f * xin[j][3];  // PD stand-in
@@ -1765,7 +1888,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     if (role == 1) {
       float fp[3];
-      foot_world(c->model, root, q, leg, fp);
+      foot_world(c_gen->model, root, q, leg, fp);
 #pragma unroll
       for (int i = 0; i < 3; ++i) ax[8 + leg * 3 + i] = fp[i];
     }
@@ -1832,9 +1955,10 @@ __global__ void go1_finalize_kernel(int n, const int32_t* __restrict__ flag, con
 }
 
 // reset of masked envs (env.reset(), :46-55 of trajectory_tracking/__init__.py)
-__global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __restrict__ c, go1_state st,
+__global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __restrict__ c_gen, go1_state st,
                                                         go1_terrain ter, const uint8_t* __restrict__ mask,
                                                         const float* __restrict__ U, uint64_t seed, uint64_t step) {
+  CCfg* __restrict__ c = (CCfg*)c_gen;
   const int leg = threadIdx.x & 3;
   const int e = blockIdx.x * EPB + (threadIdx.x >> 2);
   if (e >= c->n_envs || !mask[e]) return;
