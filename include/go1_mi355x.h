@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GO1_ABI_VERSION 1
+#define GO1_ABI_VERSION 2
 
 #define GO1_NUM_DOF 12
 #define GO1_NUM_BODIES 17
@@ -189,6 +189,9 @@ typedef struct go1_step_args {
   /* optional hipEvent_t pair recorded around the fused step kernel alone (NULL = none) */
   void* ev_begin;
   void* ev_end;
+  /* optional second copy of obs (NULL = not written): HistoryWrapper's obs_history for a history
+     length of 1 (history_wrapper.py:18-24 builds it as a copy of obs every step) */
+  float* obs_history;          /* (n_envs, 261) */
 } go1_step_args;
 
 typedef struct go1_handle go1_handle;
@@ -207,6 +210,13 @@ int go1_step(go1_handle* h, const go1_step_args* args, void* stream);
  * this to have extras_time_outs of the last go1_step current now (one tiny launch,
  * idempotent; the env's extras["time_outs"] read does it). */
 int go1_sync_time_outs(go1_handle* h, void* stream);
+/* The pending rebinding of the last step without applying it: out = {flag, pending, extras}
+ * device pointers (int32 flag word, the step's uint8 time_out buffer, extras_time_outs), all 0
+ * before the first step.  A consumer on the same stream that reads extras_time_outs before the
+ * next go1_step uses `*flag ? pending[e] : extras[e]` and may write pending[e] into extras[e]
+ * (go1_sync_time_outs does exactly that in a kernel of its own); the record kernel of the PPO
+ * rollout (go1_rollout.h, go1_transition.time_outs_flag) does it while recording. */
+int go1_time_outs_pending(go1_handle* h, int64_t out[3]);
 /* Reset envs whose mask[e] != 0: reset_idx semantics (:218-296) incl. DR draws;
  * uniforms NULL -> Philox(rng_seed, rng_step). */
 int go1_reset_envs(go1_handle* h, const uint8_t* mask, const float* uniforms, uint64_t rng_seed,

@@ -42,6 +42,14 @@ typedef struct go1_transition {
   float *st_values, *st_rewards;
   uint8_t* st_dones;
   int32_t num_obs, num_priv, num_obs_history, num_actions;
+  /* Deferred extras["time_outs"] rebinding (go1_step rebinds only on steps with a reset,
+   * legged_robot_trajectory_tracking.py:289-291, and defers it, see go1_time_outs_pending):
+   * when time_outs_flag is non-NULL and *time_outs_flag != 0, the time-outs of this transition
+   * are time_outs_pending, and they are also copied into time_outs_dst (the env's
+   * extras["time_outs"] tensor, current afterwards).  NULL = time_outs is used as is. */
+  const int32_t* time_outs_flag;
+  const uint8_t* time_outs_pending;
+  uint8_t* time_outs_dst;
 } go1_transition;
 
 /* Fused policy inference (ActorCritic.act / evaluate, actor_critic.py:121-150) for the

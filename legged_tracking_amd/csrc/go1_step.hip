@@ -1814,10 +1814,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   MARK(reset_done);
   // ---- compute_observations (:357-475)
   float* o = A.obs + (size_t)e * GO1_NUM_OBS;
+  float* oh = A.obs_history ? A.obs_history + (size_t)e * GO1_NUM_OBS : nullptr;  // optional second copy
   const float clip = c->clip_obs;
   auto put = [&](int i, float v, float nv, bool noisy) {
     if (noisy && c->add_noise) v = v + (2.0f * rng(47 + i) - 1.0f) * nv;
-    o[i] = clampf(v, -clip, clip);
+    v = clampf(v, -clip, clip);
+    o[i] = v;
+    if (oh) oh[i] = v;
   };
   // role r < 3 writes joint r of its leg; role 3 of leg 0 writes gravity and commands
   if (role == 3 && leg == 0) {
@@ -1855,7 +1858,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             hh = hh / c->ceiling_height;
             hh = hh - 0.5f;
           }
-          o[41 + layer * n_pts + p] = clampf(hh * c->obs_scale_heights, -clip, clip);
+          const float v = clampf(hh * c->obs_scale_heights, -clip, clip);
+          o[41 + layer * n_pts + p] = v;
+          if (oh) oh[41 + layer * n_pts + p] = v;
         }
       }
     }
@@ -2149,6 +2154,16 @@ int go1_sync_time_outs(go1_handle* h, void* stream) {
   hipLaunchKernelGGL(go1_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n,
                      h->d_flags + (h->count + 2) % 3, h->prev_time_out, h->prev_extras);
   HIP_TRY(hipGetLastError());
+  return GO1_OK;
+}
+
+int go1_time_outs_pending(go1_handle* h, int64_t out[3]) {
+  if (!h || !out) return fail(GO1_E_ARG, "go1_time_outs_pending: null argument");
+  out[0] = out[1] = out[2] = 0;
+  if (!h->prev_time_out) return GO1_OK;  // no step yet: extras_time_outs is current
+  out[0] = (int64_t)(uintptr_t)(h->d_flags + (h->count + 2) % 3);
+  out[1] = (int64_t)(uintptr_t)h->prev_time_out;
+  out[2] = (int64_t)(uintptr_t)h->prev_extras;
   return GO1_OK;
 }
 

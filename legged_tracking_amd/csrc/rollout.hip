@@ -137,10 +137,16 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
       for (int64_t i = tid; i < g.n; i += stride) g.dst[i] = g.src[i];
     }
   }
+  const bool rebind = tr.time_outs_flag && *tr.time_outs_flag != 0;
   for (int64_t e = tid; e < n; e += stride) {
     const float v = tr.values[e];
     float r = tr.rewards[e];
-    if (tr.time_outs) r = r + gamma * (v * (tr.time_outs[e] ? 1.0f : 0.0f));
+    const uint8_t* to = rebind ? tr.time_outs_pending : tr.time_outs;
+    if (to) {
+      const uint8_t t = to[e];
+      if (rebind && tr.time_outs_dst) tr.time_outs_dst[e] = t;
+      r = r + gamma * (v * (t ? 1.0f : 0.0f));
+    }
     tr.st_rewards[e] = r;
     tr.st_values[e] = v;
     tr.st_dones[e] = tr.dones[e] ? 1 : 0;
@@ -290,6 +296,30 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const 
     }
 }
 
+// Partial product of one output tile over K groups [g0, g0 + NG) (16 K values each), no
+// bias: the K-split form of the narrow layers, where a whole layer is one or a few tiles and
+// one wave walking all of K would run a serial MFMA chain behind one L2 round trip per group.
+// All NG weight fragments are loaded up front (one round trip).
+template <int NG>
+__device__ __forceinline__ f4_t tile_partial(const PolicyLayer& L, int Gs, int tile, int g0, const float (*src)[16],
+                                             int lane) {
+  const int q = lane >> 4, c = lane & 15;
+  f4_t w[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) w[i] = reinterpret_cast<const f4_t*>(L.w)[((size_t)tile * Gs + g0 + i) * 64 + lane];
+  f4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < NG; ++i)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[i][u], src[16 * (g0 + i) + 4 * u + q][c], acc, 0, 0, 0);
+  return acc;
+}
+
+#ifndef GO1_POLICY_KSPLIT  // K-split narrow layers (needs 16 waves per workgroup)
+#define GO1_POLICY_KSPLIT 1
+#endif
+
 #ifndef GO1_POLICY_WAVES
 #define GO1_POLICY_WAVES 16
 #endif
@@ -334,6 +364,51 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   }
   __syncthreads();
   PSTAMP(2);
+#if GO1_POLICY_KSPLIT && GO1_POLICY_WAVES == 16
+  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7; the upper half's
+  // partial goes through LDS (h2[1], free until the actor/critic's second layer)
+  {
+    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1][0][0]);
+    const int q = lane >> 4, c = lane & 15, t = wave & 7, half = wave >> 3;
+    f4_t acc = tile_partial<8>(Ls[1], 16, t, 8 * half, h1[0], lane);
+    if (half) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[t][4 * q + r][c] = acc[r];
+    }
+    __syncthreads();
+    if (!half) {
+      const f4_t b = *reinterpret_cast<const f4_t*>(Ls[1].b + 16 * t + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h2[0][16 * t + 4 * q + r][c] = elu((b[r] + acc[r]) + scr[t][4 * q + r][c]);
+    }
+  }
+  __syncthreads();
+  PSTAMP(3);
+  // 128 -> 2 (the latent): one K group per wave (8 waves), partials summed by wave 0
+  {
+    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1][0][0]);
+    const int q = lane >> 4, c = lane & 15;
+    if (wave < 8) {
+      const f4_t acc = tile_partial<1>(Ls[2], 8, 0, wave, h2[0], lane);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = acc[r];
+    }
+    __syncthreads();
+    if (wave == 0 && q == 0) {
+      float l0 = Ls[2].b[0], l1 = Ls[2].b[1];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) { l0 += scr[w][0][c]; l1 += scr[w][1][c]; }
+      // features 0, 1: the latent, also the actor's inputs hist_dim, hist_dim + 1
+      xa[P.hist_dim][c] = l0;
+      xa[P.hist_dim + 1][c] = l1;
+      if (c < ne && P.latent) {
+        P.latent[(size_t)(e0 + c) * 2] = l0;
+        P.latent[(size_t)(e0 + c) * 2 + 1] = l1;
+      }
+    }
+  }
+  __syncthreads();
+#else
   {
     const float(*s0[1])[16] = {h1[0]};
     float(*d0[1])[16] = {h2[0]};
@@ -361,6 +436,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     }
   }
   __syncthreads();
+#endif
   PSTAMP(4);
   // actor and critic, layer by layer; wave w takes tiles w, w + 4, ... of both nets
   const PolicyLayer LA1[2] = {Ls[3], Ls[7]}, LA2[2] = {Ls[4], Ls[8]}, LA3[2] = {Ls[5], Ls[9]};
@@ -393,10 +469,31 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   }
   __syncthreads();
   PSTAMP(7);
+#if GO1_POLICY_KSPLIT && GO1_POLICY_WAVES == 16
+  // 128 -> num_actions (actor, waves 0-7) and 128 -> 1 (critic, waves 8-15): one K group per
+  // wave, partials through LDS (h2, free once the third layer has read it)
+  {
+    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0][0][0]);
+    const int q = lane >> 4, c = lane & 15, net = wave >> 3;
+    const f4_t part = tile_partial<1>(Ls[net ? 10 : 6], 8, 0, wave & 7, h1[net], lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = part[r];
+  }
+  __syncthreads();
+#endif
   if (wave < 2) {
     const int q = lane >> 4, c = lane & 15;
     const PolicyLayer L = Ls[wave == 0 ? 6 : 10];
     f4_t acc = *reinterpret_cast<const f4_t*>(L.b + 4 * q);
+#if GO1_POLICY_KSPLIT && GO1_POLICY_WAVES == 16
+    {
+      float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0][0][0]);
+#pragma unroll
+      for (int w = 0; w < 8; ++w)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] += scr[8 * wave + w][4 * q + r][c];
+    }
+#else
     const f4_t* W = reinterpret_cast<const f4_t*>(L.w);
     for (int g = 0; g < 128 / 16; ++g) {
       const f4_t w = W[g * 64 + lane];
@@ -404,6 +501,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
       for (int u = 0; u < 4; ++u)
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u], h1[wave][16 * g + 4 * u + q][c], acc, 0, 0, 0);
     }
+#endif
     if (wave == 0 && P.actions) {
       // Normal(mean, std).sample() and its log_prob summed over the actions
       // (actor_critic.py:137-145), Box-Muller on Philox4x32-10 uniforms keyed by

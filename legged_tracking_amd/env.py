@@ -77,6 +77,12 @@ class StepExtras(dict):
     def get(self, key, default=None):
         return self[key] if key in self else default
 
+    def deferred_time_outs(self):
+        """extras["time_outs"] with its pending rebinding left to the consumer: returns
+        (tensor, (flag, pending, dst) device pointers or None).  The PPO record kernel resolves
+        it (rollout.py PPO.process_env_step), saving the sync launch a plain read costs."""
+        return self._env._deferred_time_outs()
+
     def items(self):
         return [(k, self[k]) for k in list(self.keys())]
 
@@ -232,6 +238,8 @@ class LeggedRobot:
         dev = self.device
         # output rings
         self._obs = torch.zeros((OUT_RING, n, self.num_obs), device=dev)
+        self._obs_hist = None  # ring of kernel-written obs copies, allocated by _history_tap()
+        self._last_hist = None
         self._priv = torch.zeros((OUT_RING, n, self.num_privileged_obs), device=dev)
         self._rew = torch.zeros((OUT_RING, n), device=dev)
         self._reset = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
@@ -294,6 +302,15 @@ class LeggedRobot:
         dict.__setitem__(ex, "timeouts", self._timeouts)
         # the rebinding of the last step is applied on read (go1_sync_time_outs)
         ex.set_lazy("time_outs", lambda: self._sim.sync_time_outs()[: self.num_train_envs])
+
+    def _deferred_time_outs(self):
+        sim = self._sim
+        p = sim.time_outs_pending() if hasattr(sim, "time_outs_pending") else None
+        if p is None and hasattr(sim, "time_outs_pending"):
+            return sim.extras_time_outs[: self.num_train_envs], None
+        if p is None:  # a backend without the deferred protocol: plain (synchronising) read
+            return self.extras["time_outs"], None
+        return sim.extras_time_outs[: self.num_train_envs], p
 
     # ------------------------------------------------------------------ views
     @property
@@ -388,6 +405,14 @@ class LeggedRobot:
     def get_observations(self):
         return self.obs_buf
 
+    def _history_tap(self):
+        """Have the step kernel also write each step's obs into a ring of its own: the
+        HistoryWrapper's obs_history for a history length of 1 (a fresh copy of obs every
+        step, history_wrapper.py:18-24) without a separate copy launch."""
+        if self._obs_hist is None:
+            self._obs_hist = torch.zeros_like(self._obs)
+        return True
+
     def get_privileged_observations(self):
         return self.privileged_obs_buf
 
@@ -406,8 +431,11 @@ class LeggedRobot:
         s = self._slot
         out = dict(obs=self._obs[s], priv=self._priv[s], rew=self._rew[s], reset=self._reset[s],
                    time_out=self._time_out[s])
+        hist = self._obs_hist[s] if self._obs_hist is not None else None
         self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
-                       rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux)
+                       rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux,
+                       obs_history=hist)
+        self._last_hist = hist
         self._rng_step += 1
         self._elog.advance()
         self._slot = (s + 1) % OUT_RING
@@ -540,6 +568,8 @@ class HistoryWrapper:
         self.obs_history = torch.zeros(self.env.num_envs, self.num_obs_history, dtype=torch.float,
                                        device=self.env.device)
         self.num_privileged_obs = self.env.num_privileged_obs
+        # history length 1: the step kernel writes obs_history (a copy of obs) itself
+        self._tap = self.obs_history_length == 1 and hasattr(self.env, "_history_tap") and self.env._history_tap()
 
     def __getattr__(self, name):
         return getattr(self.env, name)
@@ -553,7 +583,10 @@ class HistoryWrapper:
     def step(self, action):
         obs, rew, done, info = self.env.step(action)
         privileged_obs = info["privileged_obs"]
-        self._push(obs)
+        if self._tap:
+            self.obs_history = self.env._last_hist
+        else:
+            self._push(obs)
         return {"obs": obs, "privileged_obs": privileged_obs, "obs_history": self.obs_history}, rew, done, info
 
     def get_observations(self):

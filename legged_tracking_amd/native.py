@@ -37,9 +37,10 @@ def lib():
     l.go1_step.argtypes = [C.c_void_p, C.POINTER(abi.Go1StepArgs), C.c_void_p]
     l.go1_reset_envs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
     l.go1_sync_time_outs.argtypes = [C.c_void_p, C.c_void_p]
+    l.go1_time_outs_pending.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     l.go1_actuator_net.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     l.go1_destroy.argtypes = [C.c_void_p]
-    if l.go1_abi_version() != 1:
+    if l.go1_abi_version() != 2:
         raise NativeError("ABI version mismatch")
     _lib = l
     return l
@@ -117,7 +118,7 @@ class Go1Native:
         _check(lib().go1_set_terrain(self.h, C.byref(s)))
 
     def step(self, actions, gravity_vec, sim_gravity, reward_scales, rng_seed=0, rng_step=0, uniforms=None,
-             inj=None, debug=None, events=None, episode_log=None, aux=None, out=None):
+             inj=None, debug=None, events=None, episode_log=None, aux=None, out=None, obs_history=None):
         """One fused LeggedRobot.step on the current stream.  `debug` is an optional dict
         of preallocated tensors (torques, heights, terms, commands, reached); `out` may
         replace the default output buffers (obs, priv, rew, reset, time_out).
@@ -170,6 +171,9 @@ class Go1Native:
             assert aux.is_contiguous() and aux.shape == (self.n, abi.GO1_AUX)
         a.aux = aux.data_ptr() if aux is not None else None
         a.ev_begin, a.ev_end = events if events is not None else (None, None)  # hipEvent_t pair as ints
+        if obs_history is not None:
+            assert obs_history.is_contiguous() and obs_history.shape == (self.n, abi.GO1_NUM_OBS)
+        a.obs_history = obs_history.data_ptr() if obs_history is not None else None
         _check(self._lib_step(self.h, C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
 
     def sync_time_outs(self):
@@ -177,6 +181,13 @@ class Go1Native:
         otherwise applied by the kernel of step k+1)."""
         _check(lib().go1_sync_time_outs(self.h, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
         return self.extras_time_outs
+
+    def time_outs_pending(self):
+        """(flag, pending, extras) device pointers of the last step's deferred extras["time_outs"]
+        rebinding (None before the first step); see go1_time_outs_pending."""
+        out = (C.c_int64 * 3)()
+        _check(lib().go1_time_outs_pending(self.h, out))
+        return tuple(int(x) for x in out) if out[0] else None
 
     def reset_envs(self, mask, uniforms=None, rng_seed=0, rng_step=0):
         m = mask.to(torch.uint8).contiguous()

@@ -86,7 +86,8 @@ class _Transition(C.Structure):
                                           "st_obs", "st_privileged_obs", "st_obs_history", "st_actions", "st_mu",
                                           "st_sigma", "st_actions_log_prob", "st_values", "st_rewards",
                                           "st_dones")] + [
-        ("num_obs", C.c_int32), ("num_priv", C.c_int32), ("num_obs_history", C.c_int32), ("num_actions", C.c_int32)]
+        ("num_obs", C.c_int32), ("num_priv", C.c_int32), ("num_obs_history", C.c_int32), ("num_actions", C.c_int32),
+        ("time_outs_flag", C.c_void_p), ("time_outs_pending", C.c_void_p), ("time_outs_dst", C.c_void_p)]
 
 
 class _PolicyLayer(C.Structure):
@@ -243,6 +244,8 @@ class HipRolloutKernels:
             setattr(t, k, v.data_ptr())
         for k, buf in st._tr_dst:
             setattr(t, k, buf[step].data_ptr())
+        d = tr.get("time_outs_deferred")  # (flag, pending, dst) device pointers, or None
+        t.time_outs_flag, t.time_outs_pending, t.time_outs_dst = d if d is not None else (None, None, None)
         self._chk(self.lib.go1_record_transition(C.byref(t), st.num_envs, gamma, self._s()))
         return keep
 
@@ -369,6 +372,7 @@ class RolloutStorage:
             self.action_sigma = None
             self.env_bins = None
             self.time_outs = None
+            self.time_outs_deferred = None
 
         def clear(self):
             self.__init__()
@@ -405,6 +409,7 @@ class RolloutStorage:
         tr = {k: getattr(transition, k) for k in ("observations", "privileged_observations", "observation_histories",
                                                   "actions", "action_mean", "action_sigma", "actions_log_prob",
                                                   "values", "rewards", "dones", "time_outs")}
+        tr["time_outs_deferred"] = getattr(transition, "time_outs_deferred", None)
         self._keep = self.kernels.record(self, self.step, tr, gamma)
         self.step += 1
 
@@ -520,7 +525,14 @@ class PPO:
         t = self.transition
         t.rewards = rewards
         t.dones = dones
-        t.time_outs = infos["time_outs"] if "time_outs" in infos else None
+        t.time_outs_deferred = None
+        deferred = getattr(infos, "deferred_time_outs", None)
+        if deferred is not None and "time_outs" in infos:
+            # the env's pending extras["time_outs"] rebinding is resolved by the record kernel
+            # (no separate sync launch); the tensor it leaves current is the one read here
+            t.time_outs, t.time_outs_deferred = deferred()
+        else:
+            t.time_outs = infos["time_outs"] if "time_outs" in infos else None
         self.storage.add_transitions(t, gamma=PPO_Args.gamma)
         t.clear()
         self.actor_critic.reset(dones)

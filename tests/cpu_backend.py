@@ -49,6 +49,8 @@ class OracleBackend:
         o = O.step(self.cfg, self.state.np, self.ter, actions.numpy(), gravity_vec, sim_gravity, reward_scales,
                    rng_seed=rng_seed, rng_step=rng_step, debug=True)
         out["obs"].copy_(torch.from_numpy(o["obs"]))
+        if kw.get("obs_history") is not None:  # the kernel's optional second copy of obs
+            kw["obs_history"].copy_(out["obs"])
         out["priv"].copy_(torch.from_numpy(o["priv"]))
         out["rew"].copy_(torch.from_numpy(o["rew"]))
         out["reset"].copy_(torch.from_numpy(o["reset"].astype(bool)))

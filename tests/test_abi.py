@@ -47,4 +47,4 @@ def test_argument_errors_are_reported_not_thrown():
 def test_oracle_library_builds_and_loads():
     from oracle import oracle as O
     O.lib()
-    assert O.lib().go1o_abi_version() == 1
+    assert O.lib().go1o_abi_version() == 2

@@ -277,3 +277,47 @@ def test_env_api_on_gpu_matches_oracle_backend():
     to = len(g.extras["timeouts"])
     assert len(ep["episode_length"]) == len(ep["rew_total"]) > 0 and (to == 4000 or to % n == 0)
     assert torch.isfinite(g.env.obs_buf).all()
+
+
+@pytest.mark.gpu
+def test_history_tap_and_deferred_time_outs_in_record():
+    """HistoryWrapper with history length 1 takes obs_history from the step kernel's second
+    copy of obs (equal values, its own buffer); the PPO record kernel resolving the deferred
+    extras["time_outs"] rebinding bootstraps exactly like a synchronised read, and leaves
+    extras["time_outs"] current."""
+    from legged_tracking_amd import env as E, rollout as R
+    n, T = 256, 8
+    cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=4, cols=4)
+    env = E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device=DEV, cfg=cfg, seed=5, rank=0, world_size=1))
+    assert env._tap
+    env.reset()
+    k = R.HipRolloutKernels()
+    mk = lambda: R.RolloutStorage(n, T, [261], [2], [261], [12], device=DEV, kernels=k)  # noqa: E731
+    sa, sb = mk(), mk()
+    gamma = 0.99
+    rebinds = 0
+    for t in range(3 * T):
+        od, rew, done, info = env.step(torch.randn(n, 12, device=DEV))
+        obs, hist = od["obs"], od["obs_history"]
+        assert hist.data_ptr() != obs.data_ptr() and torch.equal(hist, obs)
+        tr = dict(observations=obs, privileged_observations=od["privileged_obs"], observation_histories=hist,
+                  actions=torch.zeros(n, 12, device=DEV), action_mean=torch.zeros(n, 12, device=DEV),
+                  action_sigma=torch.ones(n, 12, device=DEV), actions_log_prob=torch.zeros(n, 1, device=DEV),
+                  values=torch.rand(n, 1, device=DEV) + 1.0, rewards=rew, dones=done)
+        to_a, deferred = info.deferred_time_outs()
+        rebinds += deferred is not None
+        if sa.step == T:
+            sa.clear()
+            sb.clear()
+        keep = k.record(sa, sa.step, dict(tr, time_outs=to_a, time_outs_deferred=deferred), gamma)
+        sa.step += 1
+        after = to_a.clone()
+        to_b = info["time_outs"]  # synchronised read (go1_sync_time_outs)
+        k.record(sb, sb.step, dict(tr, time_outs=to_b, time_outs_deferred=None), gamma)
+        sb.step += 1
+        torch.cuda.synchronize()
+        assert torch.equal(after, to_b)
+        assert torch.equal(sa.rewards[sa.step - 1], sb.rewards[sb.step - 1])
+        del keep
+    assert rebinds > 0
+    assert sb.rewards.abs().sum() > 0
