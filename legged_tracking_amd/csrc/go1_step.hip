@@ -33,6 +33,8 @@
 #include <string>
 
 #include "../../include/go1_mi355x.h"
+#include "go1_model_consts.h"
+static_assert(GO1_MODEL_CONST_FLOATS == GO1_MODEL_FLOATS, "regenerate go1_model_consts.h");
 #include "pmath.h"
 
 #pragma clang fp contract(off)
@@ -908,7 +910,18 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
                              const float* g, float friction, float payload, const Terr& T, int leg, int role,
                              bool cf_out, float* cf_leg, float* cf_base) {
 #pragma clang fp contract(fast)
-  const float* model = lds;
+  // Model constants are compile-time literals (go1_model_consts.h, checked against the
+  // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
+  // Per-leg floats are the FL values times the leg's mirror signs (loop-invariant products).
+  (void)lds;
+  const float* model = GO1_MODEL_F32;
+  const float msx = (leg & 2) ? -1.0f : 1.0f, msy = (leg & 1) ? -1.0f : 1.0f, msxy = msx * msy;
+  float LC[39];
+#pragma unroll
+  for (int i = 0; i < 39; ++i) {
+    const int p = GO1_LEG_SIGN[i];
+    LC[i] = p == 0 ? GO1_LEG_FL[i] : GO1_LEG_FL[i] * (p == 1 ? msx : (p == 2 ? msy : msxy));
+  }
   MARK(phys_begin);
   const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
   float R[9];
@@ -918,7 +931,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   mat3T_vec(R, S.v, vb + 3);
   const float* th = model + 13 * 10 + 4 * 9 + 3 + 1;  // trunk half extents
   // ---- this leg: kinematics, rigid bias forces and gravity (hip -> calf)
-  const float* origin = model + 13 * 10 + leg * 9;
+  const float* origin = LC + 30;
   const float* foot = model + 13 * 10 + 4 * 9;
   const float foot_r = foot[3];
   const float thigh_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3];
@@ -958,7 +971,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
 #pragma unroll
       for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
       // rigid inertia about the link origin, bias force v x* I v, minus gravity
-      const float* B = model + 10 * (1 + leg * 3 + j);
+      const float* B = LC + 10 * j;
       rigid_bias(B, 1.0f, vj, pA[j]);
       float gl[3];
       mat3T_vec(Rp, g, gl);
@@ -1105,7 +1118,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   float pp6[6];
   {
     SI IA;
-    rigid_si(model + 10 * (1 + leg * 3 + 2), 1.0f, IA);
+    rigid_si(LC + 20, 1.0f, IA);
 #pragma unroll
     for (int j = 2; j >= 0; --j) {
       const int ax = j == 0 ? 0 : 1;
@@ -1114,7 +1127,8 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       // joint-limit spring-damper, implicit in the joint: the torque at the end of the
       // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
       // into the joint inertia D (unconditionally stable for any k, d)
-      const float lo = lds[LDS_HL + dof * 2], hi = lds[LDS_HL + dof * 2 + 1];
+      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
+      (void)dof;
       const bool lim_on = S.q[j] > hi || S.q[j] < lo;
       const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
       const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
@@ -1147,7 +1161,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       xform_inertia(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
       xfT(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
       if (j > 0) {
-        rigid_si(model + 10 * (1 + leg * 3 + j - 1), 1.0f, IA);
+        rigid_si(LC + 10 * (j - 1), 1.0f, IA);
         si_add(IA, It);
 #pragma unroll
         for (int i = 0; i < 6; ++i) pA[j - 1][i] += pt[i];
@@ -2075,6 +2089,14 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
       for (int k = 0; k < 3; ++k)
         if (!((offset_mask(j) >> k) & 1) && cfg->model[13 * 10 + leg * 9 + j * 3 + k] != 0.0f)
           return fail(GO1_E_ARG, "go1_create: joint offsets must be hip (x, y, 0), thigh (0, y, 0), calf (0, 0, z)");
+  // the integrator's model constants are compiled in (go1_model_consts.h): the block must match
+  if (memcmp(cfg->model, GO1_MODEL_F32, sizeof(GO1_MODEL_F32)) != 0)
+    return fail(GO1_E_ARG, "go1_create: model block differs from the compiled Go1 model "
+                           "(regenerate csrc/go1_model_consts.h with tools/gen_model_consts.py)");
+  for (int leg = 1; leg < 4; ++leg)  // the integrator reads leg 0's joint limits for every leg
+    for (int k = 0; k < 6; ++k)
+      if (cfg->hard_limits[leg * 6 + k] != cfg->hard_limits[k])
+        return fail(GO1_E_ARG, "go1_create: hard joint limits must be the same for every leg");
   go1_handle* h = new (std::nothrow) go1_handle();
   if (!h) return fail(GO1_E_ARG, "go1_create: out of host memory");
   h->cfg = *cfg;

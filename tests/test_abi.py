@@ -48,3 +48,25 @@ def test_oracle_library_builds_and_loads():
     from oracle import oracle as O
     O.lib()
     assert O.lib().go1o_abi_version() == 2
+
+
+def test_compiled_model_constants_match_model_block():
+    """csrc/go1_model_consts.h (the integrator's compile-time Go1 constants) is generated from
+    model.py; go1_create rejects a model block that differs from it, before touching the GPU."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_model_consts.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    from legged_tracking_amd import config as CF
+    lib = native.lib()
+    h = C.c_void_p()
+    cfg = CF.build_abi_config(CF.readme_config(n_envs=16, terrain="single_path", rows=2, cols=2))
+    cfg.model[11] = cfg.model[11] * 1.5  # FL hip COM x
+    assert lib.go1_create(C.byref(cfg), C.byref(h)) == -1
+    assert b"compiled Go1 model" in lib.go1_last_error()
+    cfg = CF.build_abi_config(CF.readme_config(n_envs=16, terrain="single_path", rows=2, cols=2))
+    cfg.hard_limits[7] = cfg.hard_limits[7] + 0.1
+    assert lib.go1_create(C.byref(cfg), C.byref(h)) == -1
+    assert b"hard joint limits" in lib.go1_last_error()
