@@ -172,6 +172,35 @@ __device__ __forceinline__ float rowsum4(float p) {
 #endif
 }
 
+// N independent row sums stage by stage (all permlane16 swaps, then their adds, then the
+// permlane32 stage): one value at a time, every sum paid a register copy, a hazard nop and
+// the full swap latency, twice
+template <int N>
+__device__ __forceinline__ void rowsum4_n(float* v) {
+#if GO1_DPP
+  float a[N], b[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+    a[i] = __uint_as_float(r[0]);
+    b[i] = __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = a[i] + b[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+    a[i] = __uint_as_float(r[0]);
+    b[i] = __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = a[i] + b[i];
+#else
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = rowsum4(v[i]);
+#endif
+}
+
 // ---------------------------------------------------------------- actuator net
 // eval_actuator_network (:1311-1320) on the matrix cores.  One "group" = 16
 // (env, joint) items; each item is carried by the 4 lanes {i, 16+i, 32+i, 48+i}
@@ -908,7 +937,7 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
 __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau, float h,
                              const float* g, float friction, float payload, const Terr& T, int leg, int role,
-                             bool cf_out, float* cf_leg, float* cf_base) {
+                             bool cf_out, float* cf_raw) {
 #pragma clang fp contract(fast)
   // Model constants are compile-time literals (go1_model_consts.h, checked against the
   // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
@@ -1105,11 +1134,17 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
 #else  // ablation build only: no contacts
   (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
 #endif
+  {
+    float red[18];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    pA[1][i] -= rsum(fth[i]);
-    pA[2][i] -= rsum(fca[i]);
-    fbase[i] = rsum(fbase[i]);
+    for (int i = 0; i < 6; ++i) { red[i] = fth[i]; red[6 + i] = fca[i]; red[12 + i] = fbase[i]; }
+    rowsum4_n<18>(red);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      pA[1][i] -= red[i];
+      pA[2][i] -= red[6 + i];
+      fbase[i] = red[12 + i];
+    }
   }
   MARK(leg_kin_contacts_done);
   // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
@@ -1262,15 +1297,26 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     S.q[j] += h * S.qd[j];
   }
   MARK(integrate_done);
-  if (cf_out) {
+  // this lane's contact forces of the sub-step (the last sub-step's survive the loop); summed
+  // over the roles once, after the loop (cf_sum): no branch and no cross-lane work here
+  (void)cf_out;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      cf_leg[i] = rsum(Fth[i]);
-      cf_leg[3 + i] = rsum(Fca[i]);
-      cf_leg[6 + i] = rsum(Fft[i]);
-      cf_base[i] = qsum(rsum(Fb[i]));
-    }
+  for (int i = 0; i < 3; ++i) {
+    cf_raw[i] = Fth[i];
+    cf_raw[3 + i] = Fca[i];
+    cf_raw[6 + i] = Fft[i];
+    cf_raw[9 + i] = Fb[i];
   }
+}
+
+// reported contact forces from the last sub-step's per-lane values: thigh, calf, foot of
+// the lane's leg (role sums) and the base (role and leg sums)
+__device__ __forceinline__ void cf_sum(float* cf_raw, float* cf_leg, float* cf_base) {
+  rowsum4_n<12>(cf_raw);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) cf_leg[i] = cf_raw[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) cf_base[i] = qsum(cf_raw[9 + i]);
 }
 
 #pragma clang fp contract(off)
@@ -1515,7 +1561,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // (:973), so sub-step s reads the slot s+1 of the incoming ring and the ring
   // leaves the step as [old4, old5, old6, scaled x 4].
   float torque[3], tgt[3];
-  float cf_leg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_base[3] = {0, 0, 0};
+  float cf_raw[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
   const int dec = c->decimation;
   for (int sub = 0; sub < dec; ++sub) {
     // _compute_torques (:957-996): inputs of this lane's three joints ...
@@ -1584,7 +1630,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
 #ifndef GO1_ABL_NO_PHYS
-        phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_leg, cf_base);
+        phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw);
 #else
         (void)last; (void)h;
         P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];
@@ -1594,6 +1640,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }
     }
   }
+  cf_sum(cf_raw, cf_leg, cf_base);
   float root[13];
   if (INJ) {
 #pragma unroll

@@ -120,7 +120,7 @@ typedef float pm_f2 __attribute__((ext_vector_type(2)));
 
 PM_FN float pm_softsign(float x) {
 #if GO1_FAST_SOFTSIGN
-  const float xc = fminf(fmaxf(x, -PM_SOFTSIGN_LIM), PM_SOFTSIGN_LIM);
+  const float xc = __builtin_amdgcn_fmed3f(x, -PM_SOFTSIGN_LIM, PM_SOFTSIGN_LIM);
   const float d = fabsf(xc) + 1.0f;
   const float r = __builtin_amdgcn_rcpf(d);
   const float q0 = xc * r;
@@ -136,8 +136,10 @@ PM_FN float pm_softsign(float x) {
 /* two softsigns in the halves of v_pk_mul / v_pk_fma (same roundings as pm_softsign) */
 PM_FN pm_f2 pm_softsign2(pm_f2 x) {
 #if GO1_FAST_SOFTSIGN
-  const pm_f2 xc = {fminf(fmaxf(x.x, -PM_SOFTSIGN_LIM), PM_SOFTSIGN_LIM),
-                    fminf(fmaxf(x.y, -PM_SOFTSIGN_LIM), PM_SOFTSIGN_LIM)};
+  /* one v_med3_f32 per half: fminf / fmaxf add a canonicalising v_max_f32 each (a NaN x
+     becomes NaN again through the final fma with x - x, whatever the clamp returns) */
+  const pm_f2 xc = {__builtin_amdgcn_fmed3f(x.x, -PM_SOFTSIGN_LIM, PM_SOFTSIGN_LIM),
+                    __builtin_amdgcn_fmed3f(x.y, -PM_SOFTSIGN_LIM, PM_SOFTSIGN_LIM)};
   const pm_f2 d = {fabsf(xc.x) + 1.0f, fabsf(xc.y) + 1.0f};
   const pm_f2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
   const pm_f2 q0 = xc * r;
