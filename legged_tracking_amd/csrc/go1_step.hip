@@ -130,6 +130,18 @@ struct Rng {
     philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     return (float)(c[slot & 3] >> 8) * (1.0f / 16777216.0f);
   }
+  // the four uniforms of slots 4 blk .. 4 blk + 3 (one Philox block), as operator() returns them
+  __device__ void quad(int blk, float* u) const {
+    if (U) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = U[(size_t)e * GO1_U_PER_ENV + 4 * blk + k];
+      return;
+    }
+    uint32_t c[4] = {(uint32_t)gid, (uint32_t)blk, (uint32_t)step, (uint32_t)(step >> 32)};
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = (float)(c[k] >> 8) * (1.0f / 16777216.0f);
+  }
 };
 
 // ---------------------------------------------------------------- lane-indexed selects
@@ -1443,6 +1455,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const float friction = st.friction[e], payload = st.payload[e];
   const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
+  // ---- the post-physics state inputs ride with the prologue loads (one wait for all of
+  // them); they are held across the sub-step loop (AGPRs), so after the physics only the
+  // height-scan gathers make a memory round trip
+  const int ep_in = st.episode_length[e];
+  const int idx_in = st.curr_pose_index[e];
+  const int coll_in = st.collision_count[e];
+  const float restitution = st.restitution[e];
+  float traj_in[6], ldv[3], la[3], sums[GO1_NUM_SUMS];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) traj_in[i] = st.trajectory[(size_t)e * 6 + i];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    ldv[j] = st.last_dof_vel[d0 + j];
+    la[j] = st.last_actions[d0 + j];
+  }
+#pragma unroll
+  for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = st.episode_sums[(size_t)e * GO1_NUM_SUMS + k];
   Phys P;
   if (!INJ) {
 #pragma unroll
@@ -1660,22 +1689,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 4; ++i) root[3 + i] = P.quat[i];
   }
-  // ---- every post-physics input in one batch of loads, ahead of this kernel's first
-  // post-physics store: one memory round trip instead of one per section
-  const int ep_in = st.episode_length[e];
-  const int idx_in = st.curr_pose_index[e];
-  const int coll_in = st.collision_count[e];
-  const float restitution = st.restitution[e];
-  float traj_in[6], ldv[3], la[3], sums[GO1_NUM_SUMS];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) traj_in[i] = st.trajectory[(size_t)e * 6 + i];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    ldv[j] = st.last_dof_vel[d0 + j];
-    la[j] = st.last_actions[d0 + j];
-  }
-#pragma unroll
-  for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = st.episode_sums[(size_t)e * GO1_NUM_SUMS + k];
   // height scan (:1918-1965) samples at the post-physics, pre-reset pose: the gathers are
   // issued here and consumed by the height observations at the end
   const bool hplane = c->terrain_kind == 0;
@@ -1877,26 +1890,41 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float* o = A.obs + (size_t)e * GO1_NUM_OBS;
   float* oh = A.obs_history ? A.obs_history + (size_t)e * GO1_NUM_OBS : nullptr;  // optional second copy
   const float clip = c->clip_obs;
-  auto put = [&](int i, float v, float nv, bool noisy) {
-    if (noisy && c->add_noise) v = v + (2.0f * rng(47 + i) - 1.0f) * nv;
+  // noise uniforms rng(47 + i) (:472-473): every lane draws exactly two Philox blocks, the
+  // same two-block code path in all lanes (the per-value calls of the two store branches
+  // ran five Philox evaluations per wave, one after the other): role r < 3 needs slots
+  // 52 + d (dof pos) and 64 + d (dof vel), role 3 slots 47, 48, 49 (gravity)
+  const int dn = leg * 3 + (role < 3 ? role : 0);
+  float uA[4], uB[4];
+  {
+    const int sa = role < 3 ? 52 + dn : 44, sb = role < 3 ? 64 + dn : 48;
+    if (c->add_noise) {
+      rng.quad(sa >> 2, uA);
+      rng.quad(sb >> 2, uB);
+    }
+  }
+  auto put = [&](int i, float v, float nv, float u, bool noisy) {
+    if (noisy && c->add_noise) v = v + (2.0f * u - 1.0f) * nv;
     v = clampf(v, -clip, clip);
     o[i] = v;
     if (oh) oh[i] = v;
   };
   // role r < 3 writes joint r of its leg; role 3 of leg 0 writes gravity and commands
   if (role == 3 && leg == 0) {
-    put(0, pg[0], c->noise_gravity, true);
-    put(1, pg[1], c->noise_gravity, true);
-    put(2, pg[2], c->noise_gravity, true);
-    put(3, cmd[0] * 1.0f, 0.0f, false);
-    put(4, cmd[1] * 1.0f, 0.0f, false);
+    put(0, pg[0], c->noise_gravity, uA[3], true);
+    put(1, pg[1], c->noise_gravity, uB[0], true);
+    put(2, pg[2], c->noise_gravity, uB[1], true);
+    put(3, cmd[0] * 1.0f, 0.0f, 0.0f, false);
+    put(4, cmd[1] * 1.0f, 0.0f, 0.0f, false);
   }
   if (role < 3) {
-    const int j = role, d = leg * 3 + role;
+    const int j = role, d = dn;
     const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act);
-    put(5 + d, (qj - s_phys[LDS_DDP + d]) * c->obs_scale_dof_pos, c->noise_dof_pos, true);
-    put(17 + d, qdj * c->obs_scale_dof_vel, c->noise_dof_vel, true);
-    put(29 + d, aj, 0.0f, false);
+    const float un = sel4((52 + d) & 3, uA[0], uA[1], uA[2], uA[3]);
+    const float uv = sel4((64 + d) & 3, uB[0], uB[1], uB[2], uB[3]);
+    put(5 + d, (qj - s_phys[LDS_DDP + d]) * c->obs_scale_dof_pos, c->noise_dof_pos, un, true);
+    put(17 + d, qdj * c->obs_scale_dof_vel, c->noise_dof_vel, uv, true);
+    put(29 + d, aj, 0.0f, 0.0f, false);
   }
   MARK(obs_props_done);
   // height observations (:395-411) from the samples gathered after the physics
