@@ -381,7 +381,13 @@ __device__ __forceinline__ void quat_apply_yaw_inverse_f(const float* q, const f
 }
 
 __device__ __forceinline__ float remainder_f(float a, float b) {
-  float m = fmodf(a, b);
+  // fmodf is exact; so are its two cheap cases, which cover every angle this path wraps
+  // (|a| < 2 |b|): a itself for |a| < |b|, and sign(a) (|a| - |b|) for |b| <= |a| < 2 |b|
+  // (Sterbenz; the sign of a zero result is a's, as fmodf gives it).  The library's
+  // iterative fmodf runs only for the rare larger |a|.
+  const float aa = fabsf(a), ab = fabsf(b);
+  float m = aa < ab ? a : copysignf(aa - ab, a);
+  if (!(aa < 2.0f * ab)) m = fmodf(a, b);  // also NaN / inf inputs
   if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
   return m;
 }
