@@ -725,16 +725,21 @@ __device__ __forceinline__ void quat_to_R(const float* q, float* R) {
   R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
 }
 
-// Terrain view of one env.  `patch` is an LDS copy of the PSZ x PSZ cells around
+// Terrain view of one env.  `patch` is an LDS copy of the PSZX x PSZY cells around
 // the env's base at the start of the step, floor and ceiling interleaved, filled
 // once per step by the whole block; the integrator's contact queries hit it and
 // fall back to the HBM tile outside it (identical values: a pure cache).
-#define PSZ 16
+// 20 rows (x) x 16 columns (y): the legs' bounding box spans up to 14 cells in x and 12 in y
+// (p99 under N(0, 1) actions), the patch is placed on its centre, and the rows leave room for
+// the motion during the step
+#define PSZX 20
+#define PSZY 16
+static_assert(PSZY == 16 && PSZX % 2 == 0, "the LDS-DMA patch staging maps 2 rows of 16 cells to a wave");
 struct Terr {
   const float* tile;  // (2, nx, ny) or nullptr
   int nx, ny;
   float ox, oy, hs;
-  const float2* patch;  // LDS, PSZ x PSZ (floor, ceiling) or nullptr
+  const float2* patch;  // LDS, PSZX x PSZY (floor, ceiling) or nullptr
   int pi0, pj0;
 };
 
@@ -760,9 +765,9 @@ __device__ __forceinline__ void height_query2(const Terr& T, float x, float y, f
   const float a = u - fu, b = v - fv;
   float2 c00, c10, c01, c11;
   const int li = i - T.pi0, lj = j - T.pj0;
-  if (T.patch && li >= 0 && li < PSZ - 1 && lj >= 0 && lj < PSZ - 1) {
-    const float2* pp = T.patch + li * PSZ + lj;
-    c00 = pp[0]; c01 = pp[1]; c10 = pp[PSZ]; c11 = pp[PSZ + 1];
+  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
+    const float2* pp = T.patch + li * PSZY + lj;
+    c00 = pp[0]; c01 = pp[1]; c10 = pp[PSZY]; c11 = pp[PSZY + 1];
   } else {
     c00 = make_float2(tile_at(T, 1, i, j), tile_at(T, 0, i, j));
     c10 = make_float2(tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j));
@@ -804,9 +809,9 @@ __device__ __forceinline__ void height_query_pk(const Terr& T, float x, float y,
   const float a = u - fu, b = v - fv;
   f2 c00, c10, c01, c11;
   const int li = i - T.pi0, lj = j - T.pj0;
-  if (T.patch && li >= 0 && li < PSZ - 1 && lj >= 0 && lj < PSZ - 1) {
-    const float2* pp = T.patch + li * PSZ + lj;
-    const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZ], q11 = pp[PSZ + 1];
+  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
+    const float2* pp = T.patch + li * PSZY + lj;
+    const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];
     c00 = f2{q00.x, q00.y}; c01 = f2{q01.x, q01.y}; c10 = f2{q10.x, q10.y}; c11 = f2{q11.x, q11.y};
   } else {
     c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
@@ -928,6 +933,54 @@ __device__ void foot_world(const float* __restrict__ model, const float* root, c
   float fw[3];
   mat3_vec(Rp, foot, fw);
   out[0] = pp[0] + fw[0]; out[1] = pp[1] + fw[1]; out[2] = pp[2] + fw[2];
+}
+
+// Centre (x, y) of the bounding box of the env's hips, knees and feet at the start of the
+// step: the terrain patch is placed on it rather than on the base (16 x 16 cells around the
+// base left ~6 % of the envs with a leg outside it, and one such lane sends its whole wave
+// through the HBM fallback of every contact query).  Hardware sin / cos: only the placement
+// of the patch depends on this, and the patch is a pure cache of the tile.
+__device__ __forceinline__ float quad_min(float v) {
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true)));
+  return fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true)));
+}
+__device__ __forceinline__ float quad_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true)));
+  return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true)));
+}
+__device__ __forceinline__ void legs_bbox_centre(const float* pos, const float* quat, const float* q, int leg,
+                                                 float* cx, float* cy) {
+  const float sx = (leg & 2) ? -1.0f : 1.0f, sy = (leg & 1) ? -1.0f : 1.0f;
+  float Rp[9], pp[3] = {pos[0], pos[1], pos[2]};
+  quat_to_R(quat, Rp);
+  float xmin = 1e30f, xmax = -1e30f, ymin = 1e30f, ymax = -1e30f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float o[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = 30 + 3 * j + k, sp = GO1_LEG_SIGN[i];
+      o[k] = GO1_LEG_FL[i] * (sp == 0 ? 1.0f : (sp == 1 ? sx : (sp == 2 ? sy : sx * sy)));
+    }
+    float rw[3];
+    mat3_vec(Rp, o, rw);
+    pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];  // hip, thigh, calf (knee) origins
+    if (j != 1) {
+      xmin = fminf(xmin, pp[0]); xmax = fmaxf(xmax, pp[0]);
+      ymin = fminf(ymin, pp[1]); ymax = fmaxf(ymax, pp[1]);
+    }
+    float sn, cn;
+    __sincosf(q[j], &sn, &cn);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rE(j == 0 ? 0 : 1, cn, sn, Rp + 3 * a, Rp + 3 * a);
+  }
+  float fw[3];
+  mat3_vec(Rp, GO1_MODEL_F32 + 13 * 10 + 4 * 9, fw);  // foot offset in the calf frame
+  const float fx = pp[0] + fw[0], fy = pp[1] + fw[1];
+  xmin = quad_min(fminf(xmin, fx)); xmax = quad_max(fmaxf(xmax, fx));
+  ymin = quad_min(fminf(ymin, fy)); ymax = quad_max(fmaxf(ymax, fy));
+  *cx = 0.5f * (xmin + xmax);
+  *cy = 0.5f * (ymin + ymax);
 }
 
 // The config block through the constant address space: every uniform field read is a
@@ -1490,7 +1543,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
   }
   Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
-  __shared__ float2 s_patch[SEPB][PSZ * PSZ];
+  __shared__ float2 s_patch[SEPB][PSZX * PSZY];
   __shared__ float s_phys[(LDS_FLOATS + 63) / 64 * 64];
   // Block = one wave, so LDS needs no barrier here (a wave's LDS operations execute in
   // order).  The model block and the terrain patches are staged with LDS-DMA
@@ -1528,15 +1581,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (c->terrain_kind == 1) {
     T.tile = K.ter.tiles + (size_t)tix * 2 * c->hf_nx * c->hf_ny;
     if (!INJ) {
-      // patch centred on the base at the start of the step
-      const float bx = P.pos[0], by = P.pos[1];
-      T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(c->hf_nx + 64))) - PSZ / 2;
-      T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(c->hf_ny + 64))) - PSZ / 2;
+      // patch centred on the legs' bounding box at the start of the step
+      float bx, by;
+      legs_bbox_centre(P.pos, P.quat, q, leg, &bx, &by);
+      T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(c->hf_nx + 64))) - PSZX / 2;
+      T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(c->hf_ny + 64))) - PSZY / 2;
       T.patch = &s_patch[el][0];
       const int nx = c->hf_nx, ny = c->hf_ny;
 #if GO1_GLDS
-      // 32 LDS-DMA dword loads per wave: load k fills s_patch[k / 8] dwords 64 (k % 8) ..
-      // + 63, i.e. cells 32 (k % 8) + lane / 2, floor (lane even) or ceiling (lane odd).
+      // 4 x PSZX / 2 LDS-DMA dword loads per wave: load k of env el2 fills s_patch[el2]
+      // dwords 64 k .. 64 k + 63, i.e. cells 32 k + lane / 2 (rows 2 k, 2 k + 1 of PSZY = 16
+      // columns), floor (lane even) or ceiling (lane odd).
       // The env's tile and patch corner come from its lane 4 el (wave-uniform readlane).
       const int cj = (lane >> 1) & 15, ci_l = lane >> 5;
       const size_t layer_off = (lane & 1) ? 0 : (size_t)nx;  // floor = layer 1, ceiling = layer 0
@@ -1548,7 +1603,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float* tl = K.ter.tiles + (size_t)tix_s * 2 * nx * ny;
         const int gj = min(max(pj_s + cj, 0), ny - 1);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < PSZX / 2; ++k) {
           const int gi = min(max(pi_s + 2 * k + ci_l, 0), nx - 1);
           __builtin_amdgcn_global_load_lds(tl + (layer_off + gi) * ny + gj, (float*)&s_patch[el2][0] + 64 * k, 4, 0, 0);
         }
@@ -1561,23 +1616,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         s_patch_meta[el][2] = T.pj0;
       }
       __syncthreads();
-      // 2 envs x 256 cells per pass: 8 cells (16 loads) in flight per lane
-#pragma unroll 1
-      for (int el0 = 0; el0 < SEPB; el0 += 2) {
-        float2 v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int el = el0 + (k >> 2);
-          const int cell = threadIdx.x + 64 * (k & 3);  // PSZ * PSZ = 256 = 4 x 64
-          const int ci = cell >> 4, cj = cell & 15;
-          const int gi = min(max(s_patch_meta[el][1] + ci, 0), nx - 1);
-          const int gj = min(max(s_patch_meta[el][2] + cj, 0), ny - 1);
-          const float* tl = K.ter.tiles + (size_t)s_patch_meta[el][0] * 2 * nx * ny;
-          v[k] = make_float2(tl[((size_t)nx + gi) * ny + gj], tl[(size_t)gi * ny + gj]);
+      for (int el2 = 0; el2 < SEPB; ++el2)
+        for (int cell = lane; cell < PSZX * PSZY; cell += 64) {
+          const int gi = min(max(s_patch_meta[el2][1] + cell / PSZY, 0), nx - 1);
+          const int gj = min(max(s_patch_meta[el2][2] + cell % PSZY, 0), ny - 1);
+          const float* tl = K.ter.tiles + (size_t)s_patch_meta[el2][0] * 2 * nx * ny;
+          s_patch[el2][cell] = make_float2(tl[((size_t)nx + gi) * ny + gj], tl[(size_t)gi * ny + gj]);
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s_patch[el0 + (k >> 2)][threadIdx.x + 64 * (k & 3)] = v[k];
-      }
       __syncthreads();
 #endif
     }
