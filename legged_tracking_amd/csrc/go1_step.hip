@@ -458,6 +458,30 @@ __device__ __forceinline__ void si_mul(const SI& M, const float* v, float* o) {
   }
 }
 
+// y = M v for a v whose components ax and 3 + ax are zero (c_j of a joint about axis ax)
+__device__ __forceinline__ void si_mul_sparse(const SI& M, const float* v, int ax, float* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    float s = 0.0f, t = 0.0f;
+    bool fs = true, ft = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      s = fs ? S3(M.a, i, j) * v[j] : s + S3(M.a, i, j) * v[j];
+      t = ft ? M.b[j * 3 + i] * v[j] : t + M.b[j * 3 + i] * v[j];
+      fs = false; ft = false;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      s = s + M.b[i * 3 + j] * v[3 + j];
+      t = t + S3(M.c, i, j) * v[3 + j];
+    }
+    o[i] = s;
+    o[3 + i] = t;
+  }
+}
+
 __device__ __forceinline__ float si_get(const SI& M, int i, int j) {
   if (i < 3 && j < 3) return S3(M.a, i, j);
   if (i >= 3 && j >= 3) return S3(M.c, i - 3, j - 3);
@@ -477,10 +501,11 @@ __device__ __forceinline__ void rigid_si(const float* body, float mscale, SI& I)
   I.a[4] = body[8] * mscale - m * c1 * c2;
   I.a[5] = body[9] * mscale + m * (cc - c2 * c2);
   // B = m c~
-  I.b[0] = 0.0f; I.b[1] = -m * c2; I.b[2] = m * c1;
-  I.b[3] = m * c2; I.b[4] = 0.0f; I.b[5] = -m * c0;
-  I.b[6] = -m * c1; I.b[7] = m * c0; I.b[8] = 0.0f;
-  I.c[0] = m; I.c[1] = 0.0f; I.c[2] = 0.0f; I.c[3] = m; I.c[4] = 0.0f; I.c[5] = m;
+  // structural zeros as -0.0: the compiler folds x + (-0.0) = x in si_add, not x + (+0.0)
+  I.b[0] = -0.0f; I.b[1] = -m * c2; I.b[2] = m * c1;
+  I.b[3] = m * c2; I.b[4] = -0.0f; I.b[5] = -m * c0;
+  I.b[6] = -m * c1; I.b[7] = m * c0; I.b[8] = -0.0f;
+  I.c[0] = m; I.c[1] = -0.0f; I.c[2] = -0.0f; I.c[3] = m; I.c[4] = -0.0f; I.c[5] = m;
 }
 
 // Rigid-body bias force v x* (I v) of a body (mass m, COM c, inertia Ic about the COM;
@@ -1055,12 +1080,14 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       float vj[6];
       xm(ax, cn, sn, offset_mask(j), r, vp, vj);
       vj[ax] += S.qd[j];
-      // c_j = v_j x (S qd): S = unit axis ax
+      // c_j = v_j x (S qd), S = unit axis ax: components ax and 3 + ax are exactly zero and
+      // are never read (si_mul_sparse, the forward pass), the others are single products
       {
-        float sq[3] = {0, 0, 0};
-        sq[ax] = S.qd[j];
-        cross3(vj, sq, cj[j]);
-        cross3(vj + 3, sq, cj[j] + 3);
+        const float qdj = S.qd[j];
+        const int p1 = (ax + 1) % 3, p2 = (ax + 2) % 3;  // (w x e_ax)_p1 = w_p2, (.)_p2 = -w_p1
+        cj[j][ax] = 0.0f; cj[j][3 + ax] = 0.0f;
+        cj[j][p1] = vj[p2] * qdj; cj[j][p2] = -(vj[p1] * qdj);
+        cj[j][3 + p1] = vj[3 + p2] * qdj; cj[j][3 + p2] = -(vj[3 + p1] * qdj);
       }
       // world pose of link j: p = pp + Rp r ; Rw rows = E (rows of Rp)
 #pragma unroll
@@ -1260,7 +1287,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       Ia.c[2] = IA.c[2] - Ul[0] * Vl[2]; Ia.c[3] = IA.c[3] - Ul[1] * Vl[1];
       Ia.c[4] = IA.c[4] - Ul[1] * Vl[2]; Ia.c[5] = IA.c[5] - Ul[2] * Vl[2];
       float Iac[6], pa[6], pt[6];
-      si_mul(Ia, cj[j], Iac);
+      si_mul_sparse(Ia, cj[j], ax, Iac);
 #pragma unroll
       for (int i = 0; i < 6; ++i) pa[i] = pA[j][i] + Iac[i] + U[j][i] * u[j] * invD;
       SI It;
@@ -1320,7 +1347,8 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       float aj[6];
       xm(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, ap, aj);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) aj[i] += cj[j][i];
+      for (int i = 0; i < 6; ++i)
+        if (i % 3 != ax) aj[i] += cj[j][i];  // components ax, 3 + ax of c_j are zero
       float Ua = 0.0f;
 #pragma unroll
       for (int i = 0; i < 6; ++i) Ua += U[j][i] * aj[i];
