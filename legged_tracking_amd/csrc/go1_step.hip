@@ -1097,15 +1097,11 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
           if ((offset_mask(j) >> k) & 1) pp[i] += Rp[3 * i + k] * r[k];
 #pragma unroll
       for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
-      // rigid inertia about the link origin, bias force v x* I v, minus gravity
+      // rigid bias force v x* I v about the link origin.  Gravity is not a per-link force here:
+      // a uniform field is a fictitious base acceleration (Featherstone's a_0 = -a_g), so the
+      // recursion runs on accelerations relative to free fall and the base adds g back at the end
       const float* B = LC + 10 * j;
       rigid_bias(B, 1.0f, vj, pA[j]);
-      float gl[3];
-      mat3T_vec(Rp, g, gl);
-      float fg[3] = {B[0] * gl[0], B[0] * gl[1], B[0] * gl[2]}, cg[3];
-      cross3(B + 1, fg, cg);
-      pA[j][0] -= cg[0]; pA[j][1] -= cg[1]; pA[j][2] -= cg[2];
-      pA[j][3] -= fg[0]; pA[j][4] -= fg[1]; pA[j][5] -= fg[2];
       if (j > 0) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) Rl[j - 1][i] = Rp[i];
@@ -1311,16 +1307,9 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   const float mscale = (bb[0] + payload) * frcp(bb[0]);
   SI I0;
   rigid_si(bb, mscale, I0);
-  float p0[6];
-  {
-    rigid_bias(bb, mscale, vb, p0);
-    float gb[3];
-    mat3T_vec(R, g, gb);
-    const float m = bb[0] * mscale;
-    float fg[3] = {m * gb[0], m * gb[1], m * gb[2]}, cg[3];
-    cross3(bb + 1, fg, cg);
-    p0[0] -= cg[0]; p0[1] -= cg[1]; p0[2] -= cg[2]; p0[3] -= fg[0]; p0[4] -= fg[1]; p0[5] -= fg[2];
-  }
+  float p0[6], gb[3];
+  rigid_bias(bb, mscale, vb, p0);
+  mat3T_vec(R, g, gb);  // gravity in the base frame: added to the relative base acceleration below
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     Ip.a[i] = qsum(Ip.a[i]);
@@ -1362,7 +1351,8 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   // ---- semi-implicit Euler (base identical in the quad)
   float wv[3], alb[3], aw[3], al[3];
   cross3(vb, vb + 3, wv);
-  alb[0] = a0[3] + wv[0]; alb[1] = a0[4] + wv[1]; alb[2] = a0[5] + wv[2];
+  // a0 is relative to free fall: the base's linear acceleration is a0_lin + g
+  alb[0] = a0[3] + gb[0] + wv[0]; alb[1] = a0[4] + gb[1] + wv[1]; alb[2] = a0[5] + gb[2] + wv[2];
   mat3_vec(R, a0, aw);
   mat3_vec(R, alb, al);
 #pragma unroll
