@@ -434,6 +434,14 @@ struct SI {
 // Integrator-only fast math (hardware v_rcp_f32 / v_rsq_f32, ~1 ulp): the f32
 // integrator is compared with the f64 oracle within a tolerance, never bitwise.
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// hardware v_sin_f32 / v_cos_f32 on the angle in revolutions reduced to [0, 1) by v_fract_f32:
+// 5 issue slots instead of the portable polynomial's ~25 (integrator only; absolute error
+// ~1e-6, the step is compared with the f64 oracle within a tolerance)
+__device__ __forceinline__ void hw_sincosf(float x, float* s, float* c) {
+  const float r = __builtin_amdgcn_fractf(x * 0.159154943091895336f);
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+}
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
 
 #define S3(m, i, j) m[((i) == 0 ? ((j) == 0 ? 0 : (j) == 1 ? 1 : 2) : (i) == 1 ? ((j) == 0 ? 1 : (j) == 1 ? 3 : 4) : ((j) == 0 ? 2 : (j) == 1 ? 4 : 5))]
@@ -1075,7 +1083,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       const int ax = j == 0 ? 0 : 1;
       const float* r = origin + j * 3;
       float sn, cn;
-      pm_sincosf(S.q[j], &sn, &cn);
+      hw_sincosf(S.q[j], &sn, &cn);
       cs[j][0] = cn; cs[j][1] = sn;
       float vj[6];
       xm(ax, cn, sn, offset_mask(j), r, vp, vj);
@@ -1367,7 +1375,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     const float wn = wn2 * iwn;
     const float thh = 0.5f * h * wn;
     float sth, cth;
-    pm_sincosf(thh, &sth, &cth);
+    hw_sincosf(thh, &sth, &cth);
     const float sc = thh > 1e-12f ? sth * iwn : 0.5f * h;
     const float dq[4] = {S.w[0] * sc, S.w[1] * sc, S.w[2] * sc, cth};
     float* q = S.quat;
