@@ -1595,7 +1595,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int i = 64 * k + lane;
       mv[k] = i < GO1_MODEL_FLOATS ? c_gen->model[i] : c_gen->default_dof_pos[min(i, LDS_FLOATS - 1) - GO1_MODEL_FLOATS];
     }
+    MARK(pro_loads_issued);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    MARK(pro_loads_landed);
 #pragma unroll
     for (int k = 0; k < (LDS_FLOATS + 63) / 64; ++k) s_phys[64 * k + lane] = mv[k];  // padded to 64
   }
@@ -1610,6 +1612,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // patch centred on the legs' bounding box at the start of the step
       float bx, by;
       legs_bbox_centre(P.pos, P.quat, q, leg, &bx, &by);
+      MARK(pro_bbox_done);
       T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(c->hf_nx + 64))) - PSZX / 2;
       T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(c->hf_ny + 64))) - PSZY / 2;
       T.patch = &s_patch[el][0];
@@ -1653,6 +1656,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
     }
   }
+  MARK(pro_dma_issued);
   asm volatile("" : "+v"(rebind_flag));  // kept in a VGPR: a scalar branch on it would wait early
   if (rebind && sub16 == 0 && rebind_flag) K.prev_extras[e] = rebind_val;
   float scaled[3];
