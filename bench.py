@@ -220,6 +220,7 @@ def main():
     n_global = n * world
     cfg = CF.readme_config(n_envs=n_global, terrain="single_path", rows=32, cols=32)
     c = CF.build_abi_config(cfg, n_envs=n)
+    c.env_id_offset = rank * n  # global env ids key the Philox streams, as in TrajectoryTrackingEnv
     d = CF.derived(cfg)
     # terrain: 32 x 32 tunnels replicated on every rank; env (global id) -> tile (id mod 1024)
     td = T.build(cfg, n_global, np.random.RandomState(11))

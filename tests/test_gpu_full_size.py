@@ -1,0 +1,119 @@
+"""The fused step at BASELINE's full size (configs[2]: 4096 Go1, single_path tunnels on a 32 x 32
+sub-terrain grid), through size-independent properties:
+
+  * sharding: one handle of 4096 envs and two handles of 2048 (global env ids 0.. and 2048..,
+    i.e. what ranks 0 and 1 of a 2-GPU run compute) produce bit-identical states and outputs
+    step after step -- the multi-GPU path has no collective, so this is its whole contract;
+  * invariants over 40 steps of N(0, 1) actions: finite outputs, observations within the clip,
+    time-out => reset, reset envs restart their episode, heights within the camera_zero clip;
+  * one-step integrator agreement with the f64 oracle over all 4096 envs (the tolerance of
+    tests/test_gpu_parity.py::test_native_integrator_step_vs_f64_oracle).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from legged_tracking_amd import config as CF, native, terrain as T  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+DEV = "cuda:0"
+N = 4096
+
+
+def _setup(seed=7):
+    cfg = CF.readme_config(n_envs=N, terrain="single_path", rows=32, cols=32)
+    td = T.build(cfg, N, np.random.RandomState(11))
+    rng = np.random.default_rng(seed)
+    dr = {"friction": rng.uniform(0.1, 3.0, (N, 1)), "restitution": rng.uniform(0.0, 0.4, (N, 1)),
+          "payload": rng.uniform(-1.0, 3.0, (N, 1))}
+    ep = rng.integers(0, 500, (N, 1)).astype(np.int32)
+    return cfg, td, dr, ep, rng
+
+
+def _handle(cfg, td, dr, ep, lo, hi):
+    c = CF.build_abi_config(cfg, n_envs=hi - lo)
+    c.env_id_offset = lo
+    g = native.Go1Native(c, DEV)
+    sl = slice(lo, hi)
+    g.set_terrain(td.tiles, td.env_tile[sl], td.env_terrain_origin[sl], td.env_origins[sl])
+    for k, v in dr.items():
+        g.state[k].copy_(torch.from_numpy(v[sl].astype(np.float32)))
+    keep = g.reset_envs(torch.ones(hi - lo, dtype=torch.bool, device=DEV), rng_seed=11, rng_step=0)
+    g.state["episode_length"].copy_(torch.from_numpy(ep[sl]))
+    return c, g, keep
+
+
+def test_full_size_sharded_handles_are_bit_identical_to_one():
+    cfg, td, dr, ep, rng = _setup()
+    c, one, k1 = _handle(cfg, td, dr, ep, 0, N)
+    _, lo, k2 = _handle(cfg, td, dr, ep, 0, N // 2)
+    _, hi, k3 = _handle(cfg, td, dr, ep, N // 2, N)
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    grav, gvec = CF.gravity_state([0.3, -0.2, 0.1])
+    torch.cuda.synchronize()
+    del k1, k2, k3
+    for t in range(12):
+        a = torch.randn(N, 12, device=DEV)
+        one.step(a, gvec, grav, scales, rng_seed=5, rng_step=t)
+        lo.step(a[: N // 2].contiguous(), gvec, grav, scales, rng_seed=5, rng_step=t)
+        hi.step(a[N // 2:].contiguous(), gvec, grav, scales, rng_seed=5, rng_step=t)
+        torch.cuda.synchronize()
+        for name in ("obs", "priv", "rew", "reset", "time_out"):
+            whole = getattr(one, name).cpu().numpy()
+            parts = np.concatenate([getattr(lo, name).cpu().numpy(), getattr(hi, name).cpu().numpy()])
+            np.testing.assert_array_equal(whole, parts, err_msg=f"step {t}: {name}")
+    s1, sl, sh = one.state.numpy(), lo.state.numpy(), hi.state.numpy()
+    for k in s1:
+        np.testing.assert_array_equal(s1[k], np.concatenate([sl[k], sh[k]]), err_msg=k)
+
+
+def test_full_size_invariants_over_40_steps():
+    cfg, td, dr, ep, rng = _setup(seed=8)
+    c, g, keep = _handle(cfg, td, dr, ep, 0, N)
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    grav, gvec = CF.gravity_state([0.0, 0.0, 0.0])
+    clip = float(c.clip_obs)
+    torch.cuda.synchronize()
+    del keep
+    n_reset = 0
+    for t in range(40):
+        ep_before = g.state["episode_length"].cpu().numpy()[:, 0].copy()
+        g.step(torch.randn(N, 12, device=DEV), gvec, grav, scales, rng_seed=6, rng_step=t)
+        torch.cuda.synchronize()
+        obs, rew = g.obs.cpu().numpy(), g.rew.cpu().numpy()
+        reset, tout = g.reset.cpu().numpy().astype(bool), g.time_out.cpu().numpy().astype(bool)
+        ep_after = g.state["episode_length"].cpu().numpy()[:, 0]
+        assert np.isfinite(obs).all() and np.isfinite(rew).all()
+        assert np.abs(obs).max() <= clip
+        assert not (tout & ~reset).any(), "time-out without reset"
+        np.testing.assert_array_equal(tout, ep_before + 1 > 500)
+        assert (ep_after[reset] == 0).all(), "reset envs restart their episode"
+        np.testing.assert_array_equal(ep_after[~reset], ep_before[~reset] + 1)
+        # camera_zero heights: clip(h, -0.3, 0.3) * obs_scale_heights
+        hs = float(c.obs_scale_heights)
+        assert np.abs(obs[:, 41:]).max() <= 0.3 * hs + 1e-7
+        n_reset += int(reset.sum())
+    assert n_reset > 0  # the random episode lengths make some envs time out in 40 steps
+
+
+def test_full_size_one_step_integrator_vs_f64_oracle():
+    cfg, td, dr, ep, rng = _setup(seed=9)
+    c, g, keep = _handle(cfg, td, dr, ep, 0, N)
+    torch.cuda.synchronize()
+    del keep
+    st = O.NpState(N, g.state.numpy())
+    ter = O.NpTerrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    grav, gvec = CF.gravity_state([0.2, -0.1, 0.3])
+    act = rng.normal(0, 1, (N, 12)).astype(np.float32)
+    g.step(torch.from_numpy(act).to(DEV), gvec, grav, scales, rng_seed=3, rng_step=1)
+    torch.cuda.synchronize()
+    out = O.step(c, st, ter, act, gvec, grav, scales, rng_seed=3, rng_step=1, debug=False)
+    gs = g.state.numpy()
+    for k, tol in (("dof_pos", 2e-3), ("dof_vel", 5e-2), ("root", 2e-3)):
+        err = np.abs(gs[k] - st[k]) / np.maximum(1.0, np.abs(st[k]))
+        assert np.percentile(err, 99) < tol, (k, np.percentile(err, 99))
+    assert (g.reset.cpu().numpy() == out["reset"].astype(bool)).mean() > 0.98
