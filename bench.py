@@ -1,25 +1,33 @@
-"""Benchmark of the fused MI355X Go1 step (BASELINE.json metric).
+"""Benchmark of the MI355X Go1 trajectory-tracking env step (BASELINE.json metric).
 
-One "step" = one LeggedRobot.step() (4 sim sub-steps of actuator net + native
-articulated-body integrator, then the full post-physics: height scan, targets,
-rewards, terminations, resets, observations) over 4096 envs per GPU on the
-single_path tunnel (BASELINE configs[2]; configs[1] is the velocity-tracking env,
-which is not on this path).  Inputs are synthetic and already resident in HBM
-when the timed region starts: a ring of N(0,1) action batches (the actor's
-init_noise_std = 1.0, ppo_cse/actor_critic.py:11) generated on the device.
+One "step" = one VecEnv.step of HistoryWrapper(TrajectoryTrackingEnv) -- the call
+scripts/train.py's Runner makes ("wall time of the VecEnv.step loop"):
+the fused HIP LeggedRobot.step (4 sim sub-steps of actuator net + native articulated-
+body integrator, then the whole post-physics: height scan, targets, rewards,
+terminations, resets, observations) plus the env's host bookkeeping (gravity schedule,
+output ring, episode-log ring, HistoryWrapper).  4096 envs per GPU on the single_path
+tunnel (BASELINE configs[2]).  Inputs are synthetic and already resident in HBM when
+the timed region starts: a ring of N(0,1) action batches (the actor's init_noise_std
+= 1.0, ppo_cse/actor_critic.py:11) generated on the device.
 
-Multi-GPU: one process per GPU (torch.distributed.run), envs sharded by global
-env id (rank r owns [r*N, (r+1)*N)), no collective inside the step ->
-"scaling": "weak".  value = sum over ranks of envs x steps / max-over-ranks time.
+Multi-GPU: one process per GPU.  `--gpus N` (N > 1) launches the N ranks itself
+(children started before anything touches the GPU, rendezvous on 127.0.0.1), or runs
+as one rank of an external `torch.distributed.run` (RANK / WORLD_SIZE in the env; the
+world size must equal --gpus).  Envs are sharded by global env id (rank r owns
+[r*N, (r+1)*N)); the step has no collective -> "scaling": "weak";
+value = sum over ranks of envs x steps / max-over-ranks time.
 
-Also reported: roofline of the fused step kernel (HIP events around that kernel
-alone on the launch stream) and the CPU oracle (oracle/, "port") timed on a
-bounded sample on the host cores of rank 0.
+Also reported: the raw fused-kernel loop (Go1Native.step alone), the roofline of the
+fused step kernel (HIP events around that kernel, on its launch stream, over the timed
+region), the PPO rollout rate (act + step + record) and the CPU oracle timed on a
+bounded sample on rank 0's host cores (N = 1 only).
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,7 +40,7 @@ METRIC = "env-steps/sec (whole node) at 4096 Go1/GPU, 1/2/4/8 MI355X; %HBM roofl
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
 
-# Algorithmic HBM bytes per env-step of the fused kernel (DESIGN.md "Roofline accounting"):
+# Algorithmic HBM bytes per env-step of the fused kernel:
 #   reads : actions 48, root 52, dof pos/vel 96, lag 336, err/vel history 192, motor strength/offset 96,
 #           last actions/dof vel 96, friction/restitution/payload 12, episode length/pose index/collisions 12,
 #           trajectory 24, base rotation 12, episode sums 52, terrain index+origins 28,
@@ -41,28 +49,33 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
 #           lag 336, err/vel history 192, last actions/dof vel 96, joint targets 48, strength/offset 96,
 #           trajectory 24, base rotation 12, episode sums 52, counters 12               -> 2,279 B
 BYTES_PER_ENV_STEP = 1936 + 2279
-# Algorithmic FLOPs per env-step: actuator net 12 joints x 4 sub-steps x 2,688 (exact: 1,248 FMA + 64
-# softsign x 3 flops + 32 ...); the integrator and post-physics are not counted here.
+# The VecEnv.step path additionally has the kernel write the HistoryWrapper's obs_history copy
+# (1,044 B), the episode log row (64 B) and the extras aux row (128 B).
+BYTES_PER_ENV_STEP_VECENV = BYTES_PER_ENV_STEP + 1044 + 64 + 128
+# Algorithmic FLOPs per env-step: actuator net 12 joints x 4 sub-steps x 2,688; the
+# integrator and post-physics are not counted here.
 FLOPS_PER_ENV_STEP = 12 * 4 * 2688
-
 
 # PMC-measured HBM bytes per launch of the step kernel (tools/profile.sh + tools/prof_summary.py;
 # FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  Re-collected whenever the kernel changes.
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01", "step_counters.json")
+TRAFFIC_FILES = [os.path.join(REPO, "profiles", r, "step_counters.json") for r in ("r02", "r01")]
 
 
 def pmc_traffic(n_envs):
-    """(HBM bytes per launch, VALU issue fraction, source) from the committed PMC summary."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            d = json.load(f)
-        if int(d["resources"]["Grid_Size"]) != 16 * n_envs:  # 16 lanes per env
-            return None, None, None
-        pw = d.get("per_wave", {})
-        valu = pw["SQ_ACTIVE_INST_VALU"] / pw["SQ_WAVE_CYCLES"] if "SQ_ACTIVE_INST_VALU" in pw else None
-        return d["hbm_bytes_per_launch"]["traffic"], valu, os.path.relpath(TRAFFIC_FILE, REPO)
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
-        return None, None, None
+    """HBM bytes per launch (raw FETCH+WRITE and with FETCH doubled), VALU issue fraction, source."""
+    for path in TRAFFIC_FILES:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if int(d["resources"]["Grid_Size"]) != 16 * n_envs:  # 16 lanes per env
+                continue
+            pw = d.get("per_wave", {})
+            valu = pw["SQ_ACTIVE_INST_VALU"] / pw["SQ_WAVE_CYCLES"] if "SQ_ACTIVE_INST_VALU" in pw else None
+            h = d["hbm_bytes_per_launch"]
+            return h["traffic"], h.get("traffic_upper_fetch_doubled"), valu, os.path.relpath(path, REPO)
+        except (OSError, KeyError, ValueError, ZeroDivisionError):
+            continue
+    return None, None, None, None
 
 
 def hip():
@@ -74,12 +87,44 @@ def hip():
     return h
 
 
+class EventPairs:
+    """hipEvent_t pairs recorded by the library around the fused kernel (on its launch stream)."""
+
+    def __init__(self, n):
+        self.hp = hip()
+        self.ev = []
+        for _ in range(2 * n):
+            e = C.c_void_p()
+            assert self.hp.hipEventCreate(C.byref(e)) == 0
+            self.ev.append(e)
+
+    def pair(self, k):
+        return self.ev[2 * k].value, self.ev[2 * k + 1].value
+
+    def ms(self, k):
+        m = C.c_float()
+        assert self.hp.hipEventElapsedTime(C.byref(m), self.ev[2 * k], self.ev[2 * k + 1]) == 0
+        return m.value
+
+    def close(self):
+        for e in self.ev:
+            self.hp.hipEventDestroy(e)
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: the process's CPU share.  The GPU box sets OMP_NUM_THREADS to
+    its per-GPU share (16) and asks jobs to stay within it; otherwise every core in the affinity mask."""
+    cores = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    return (min(int(share), cores) if share and share.isdigit() and int(share) > 0 else cores), cores
+
+
 def cpu_baseline(n_envs, budget_s=12.0, max_steps=400):
-    """Time the CPU oracle (a C restatement, OpenMP over envs) on the same workload."""
+    """Time the CPU oracle's f32-integrator build (a C restatement, OpenMP over envs) on the same
+    workload (checker code timed as a baseline only; never the measured product)."""
     from legged_tracking_amd import config as CF, terrain as T
     from oracle import oracle as O
-    cores = len(os.sched_getaffinity(0))
-    threads = min(cores, 16)
+    threads, cores = cpu_threads()
     os.environ["OMP_NUM_THREADS"] = str(threads)
     cfg = CF.readme_config(n_envs=n_envs, terrain="single_path", rows=32, cols=32)
     c = CF.build_abi_config(cfg)
@@ -93,11 +138,11 @@ def cpu_baseline(n_envs, budget_s=12.0, max_steps=400):
     grav, gvec = CF.gravity_state(rng.uniform(-1, 1, 3))
     scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
     acts = [rng.normal(0, 1, (n_envs, 12)).astype(np.float32) for _ in range(8)]
-    O.step(c, st, ter, acts[0], gvec, grav, scales, rng_seed=1, rng_step=1, debug=False)  # warm
+    O.step(c, st, ter, acts[0], gvec, grav, scales, rng_seed=1, rng_step=1, debug=False, precision="f32")  # warm
     t0 = time.perf_counter()
     k = 0
     while k < max_steps and time.perf_counter() - t0 < budget_s:
-        O.step(c, st, ter, acts[k % 8], gvec, grav, scales, rng_seed=1, rng_step=2 + k, debug=False)
+        O.step(c, st, ter, acts[k % 8], gvec, grav, scales, rng_seed=1, rng_step=2 + k, debug=False, precision="f32")
         k += 1
     dt = time.perf_counter() - t0
     model = "unknown"
@@ -109,46 +154,67 @@ def cpu_baseline(n_envs, budget_s=12.0, max_steps=400):
     except OSError:
         pass
     return {"value": n_envs * k / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{k} steps x {n_envs} envs of the C oracle (f64 integrator, same single_path workload), "
-                      f"{dt:.1f} s on {threads} threads of {cores} visible ({model})"}
+            "sample": f"{k} steps x {n_envs} envs of the C oracle (f32 integrator, same single_path workload), "
+                      f"{dt:.1f} s on {threads} OpenMP threads (this process's CPU share; {cores} cores in its "
+                      f"affinity mask, {model})"}
 
 
-def env_sweep(n, dev, steps=100, warmup=10):
-    """Env-only throughput at n envs on this GPU (4k ... 256k envs/GPU sweep)."""
-    import torch
-    from legged_tracking_amd import config as CF, native, terrain as T
+def make_env(n, rank, world, dev):
+    from legged_tracking_amd import config as CF, env as E
     cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=32, cols=32)
-    c = CF.build_abi_config(cfg, n_envs=n)
-    td = T.build(cfg, n, np.random.RandomState(11))
-    g = native.Go1Native(c, str(dev))
-    g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
-    rng = np.random.default_rng(5)
-    g.state["friction"].copy_(torch.from_numpy(rng.uniform(0.1, 3.0, (n, 1)).astype(np.float32)))
-    g.reset_envs(torch.ones(n, dtype=torch.bool, device=dev), rng_seed=5, rng_step=0)
-    g.state["episode_length"].copy_(torch.from_numpy(rng.integers(0, 500, (n, 1)).astype(np.int32)))
-    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
-    grav, gvec = CF.gravity_state([0.1, -0.2, 0.3])
-    ring = torch.randn((8, n, 12), device=dev)
+    return E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device=str(dev), cfg=cfg, seed=11, rank=rank,
+                                                    world_size=world))
+
+
+def kernel_loop(env, ring, steps, warmup, every=4):
+    """The fused kernel alone (Go1Native.step, no env host code) on the env's own handle."""
+    import torch
+    base = env.env
+    sim = base._sim
+    grav, gvec = base._sim_gravity, base._gravity_vec
+    scales = base._scale_vector()
+    ev = EventPairs((steps + every - 1) // every)
     for k in range(warmup):
-        g.step(ring[k % 8], gvec, grav, scales, rng_seed=5, rng_step=1 + k)
+        sim.step(ring[k % len(ring)], gvec, grav, scales, rng_seed=7, rng_step=(1 << 40) + k)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
-        g.step(ring[k % 8], gvec, grav, scales, rng_seed=5, rng_step=1 + warmup + k)
+        e = ev.pair(k // every) if k % every == 0 else None
+        sim.step(ring[k % len(ring)], gvec, grav, scales, rng_seed=7, rng_step=(1 << 40) + warmup + k, events=e)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    g.close()
-    return {"envs_per_gpu": n, "value": n * steps / dt, "ms_per_step": dt / steps * 1e3}
+    kt = [ev.ms(i) for i in range((steps + every - 1) // every)]
+    ev.close()
+    return dt, float(np.mean(kt))
 
 
-def rollout_rate(n, dev, steps, warmup, prof=None):
-    """Secondary line (SURVEY 8(d) "report both env-only and rollout (act + step) rates"):
-    the Runner's rollout loop -- ActorCritic.act + value (hipBLASLt GEMMs), env.step
-    through TrajectoryTrackingEnv/HistoryWrapper, transition record kernel -- at n envs."""
+def env_sweep(n, dev, steps=100, warmup=10):
+    """Env-only VecEnv.step throughput at n envs on this GPU (4k ... 256k envs/GPU sweep)."""
     import torch
-    from legged_tracking_amd import config as CF, env as E, rollout as R
-    cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=32, cols=32)
-    env = E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device=str(dev), cfg=cfg, seed=11, rank=0, world_size=1))
+    env = make_env(n, 0, 1, dev)
+    env.reset()
+    ring = torch.randn((8, n, 12), device=dev)
+    for k in range(warmup):
+        env.step(ring[k % 8])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.step(ring[k % 8])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kdt, kms = kernel_loop(env, ring, steps, warmup)
+    env.close()
+    return {"envs_per_gpu": n, "value": n * steps / dt, "ms_per_step": dt / steps * 1e3,
+            "kernel_ms": kms, "kernel_loop_env_steps_per_s": n * steps / kdt}
+
+
+def rollout_rate(n, dev, steps, warmup):
+    """Secondary line (SURVEY 8(d) "report both env-only and rollout (act + step) rates"): the
+    Runner's rollout loop -- fused PPO.act kernel, env.step through TrajectoryTrackingEnv /
+    HistoryWrapper, transition record kernel -- at n envs."""
+    import torch
+    from legged_tracking_amd import rollout as R
+    env = make_env(n, 0, 1, dev)
     ac = R.ActorCritic(env.num_obs, env.num_privileged_obs, env.num_obs_history, env.num_actions).to(dev)
     alg = R.PPO(ac, device=dev)
     T = 24
@@ -170,21 +236,83 @@ def rollout_rate(n, dev, steps, warmup, prof=None):
         for _ in range(warmup):
             one()
         torch.cuda.synchronize()
-        if prof is not None:
-            prof.enable()
         t0 = time.perf_counter()
         for _ in range(steps):
             one()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        if prof is not None:
-            prof.disable()
+    env.close()
     return {"value": n * steps / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
             "what": "PPO.act (fused MFMA adaptation+actor+critic kernel, Normal sample) + TrajectoryTrackingEnv.step "
                     "+ HistoryWrapper + process_env_step record kernel, 1 GPU",
             "fused_policy": alg.fused is not None}
 
 
+# ---------------------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n, argv):
+    """Start n ranks of this script (one per GPU) and wait for them.  Runs before anything in this
+    process touches the GPU (no torch import), so the children are ordinary fresh processes."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            r = p.wait()
+            rc = rc or r
+            if r != 0:  # one rank failed: the others would wait at a barrier forever
+                for q in procs:
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def selftest_rank(args, rank, world):
+    """--selftest: the launcher and the cross-rank reduction on CPU (gloo), no GPU and no env:
+    each rank 'steps' a tiny numpy workload; rank 0 prints the line the real run would."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world
+    x = np.zeros(1024, np.float32)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        x += np.float32(k)
+    elapsed = time.perf_counter() - t0 + 1e-3 * (rank + 1)
+    t = torch.tensor([elapsed, float(rank)], dtype=torch.float64)
+    per = [torch.zeros_like(t) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(per, t)
+    else:
+        per = [t]
+    if rank == 0:
+        el = max(float(p[0]) for p in per)
+        n = args.envs_per_gpu
+        print(json.dumps({"metric": METRIC, "value": n * world * args.steps / el, "n_gpus": world,
+                          "world_size_seen": world, "ranks": [int(p[1]) for p in per], "selftest": True,
+                          "config": {"global_envs": n * world, "parallelism": f"env-shard x{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+# ---------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,117 +326,119 @@ def main():
     ap.add_argument("--event-every", type=int, default=4,
                     help="record the HIP event pair around every k-th step kernel of the timed loop")
     ap.add_argument("--sweep", default="", help="comma-separated envs/GPU for an extra size sweep (e.g. 16384,65536)")
+    ap.add_argument("--selftest", action="store_true", help="CPU-only launcher test (gloo, no GPU work)")
     args = ap.parse_args()
 
-    import torch
-    if args.rollout_only:
-        print(json.dumps(rollout_rate(args.envs_per_gpu, torch.device("cuda", 0), args.steps, args.warmup)))
-        return
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the line would misreport n_gpus")
+    if args.selftest:
+        sys.exit(selftest_rank(args, rank, world))
+
+    import torch
+    dev = torch.device("cuda", local)
+    if args.rollout_only:
+        torch.cuda.set_device(dev)
+        print(json.dumps(rollout_rate(args.envs_per_gpu, dev, args.steps, args.warmup)))
+        return
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != world:
+            raise SystemExit("world size mismatch")
     torch.cuda.set_device(dev)
 
-    from legged_tracking_amd import config as CF, native, terrain as T
     n = args.envs_per_gpu
     n_global = n * world
-    cfg = CF.readme_config(n_envs=n_global, terrain="single_path", rows=32, cols=32)
-    c = CF.build_abi_config(cfg, n_envs=n)
-    c.env_id_offset = rank * n  # global env ids key the Philox streams, as in TrajectoryTrackingEnv
-    d = CF.derived(cfg)
-    # terrain: 32 x 32 tunnels replicated on every rank; env (global id) -> tile (id mod 1024)
-    td = T.build(cfg, n_global, np.random.RandomState(11))
-    sl = slice(rank * n, (rank + 1) * n)
-    g = native.Go1Native(c, str(dev))
-    g.set_terrain(td.tiles, td.env_tile[sl], td.env_terrain_origin[sl], td.env_origins[sl])
-    rng = np.random.default_rng(100 + rank)
-    g.state["friction"].copy_(torch.from_numpy(rng.uniform(0.1, 3.0, (n, 1)).astype(np.float32)))
-    g.state["restitution"].copy_(torch.from_numpy(rng.uniform(0.0, 0.4, (n, 1)).astype(np.float32)))
-    g.state["payload"].copy_(torch.from_numpy(rng.uniform(-1.0, 3.0, (n, 1)).astype(np.float32)))
-    keep = g.reset_envs(torch.ones(n, dtype=torch.bool, device=dev), rng_seed=11, rng_step=rank)
-    g.state["episode_length"].copy_(torch.from_numpy(rng.integers(0, 500, (n, 1)).astype(np.int32)))
-    scales = CF.reward_scale_vector(d["reward_scales"])
-    grav, gvec = CF.gravity_state(rng.uniform(-1, 1, 3))
-    ring = torch.randn((64, n, 12), device=dev)
+    env = make_env(n, rank, world, dev)
+    env.reset()
+    ring = torch.randn((64, n, 12), device=dev, generator=torch.Generator(device=dev).manual_seed(100 + rank))
     torch.cuda.synchronize()
-    del keep
 
-    hp = hip()
-    n_ev = args.steps
-    evs = []
-    for _ in range(2 * n_ev):
-        e = C.c_void_p()
-        assert hp.hipEventCreate(C.byref(e)) == 0
-        evs.append(e)
-
-    seed = 20240101
+    every = max(1, args.event_every)
+    n_ev = (args.steps + every - 1) // every
+    ev = EventPairs(n_ev)
+    base = env.env
     for k in range(args.warmup):
-        g.step(ring[k % 64], gvec, grav, scales, rng_seed=seed, rng_step=k)
+        env.step(ring[k % 64])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    base.kernel_events.extend(ev.pair(k // every) if k % every == 0 else None for k in range(args.steps))
     t0 = time.perf_counter()
-    every = max(1, args.event_every)
     for k in range(args.steps):
-        ev = (evs[2 * k].value, evs[2 * k + 1].value) if k % every == 0 else None
-        g.step(ring[k % 64], gvec, grav, scales, rng_seed=seed, rng_step=args.warmup + k, events=ev)
+        env.step(ring[k % 64])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kt = []
-    for k in range(0, args.steps, every):
-        ms = C.c_float()
-        hp.hipEventElapsedTime(C.byref(ms), evs[2 * k], evs[2 * k + 1])
-        kt.append(ms.value)
-    kernel_ms = float(np.mean(kt))
+    base.kernel_events.clear()
+    kernel_ms = float(np.mean([ev.ms(i) for i in range(n_ev)]))
+    ev.close()
     if not os.environ.get("GO1_BENCH_ALLOW_NONFINITE"):
-        assert torch.isfinite(g.obs).all(), "non-finite observations"
+        assert torch.isfinite(base.obs_buf).all(), "non-finite observations"
+    # the fused kernel alone on the same handle (no env host code)
+    kdt, kms_raw = kernel_loop(env, ring, min(args.steps, 200), min(args.warmup, 10))
+    mine = torch.tensor([elapsed, kernel_ms, kdt, kms_raw], device=dev, dtype=torch.float64)
+    per_rank = [mine]
     if dist:
-        t = torch.tensor([elapsed, kernel_ms], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        per_rank = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+    per_rank = [p.tolist() for p in per_rank]
+    elapsed = max(p[0] for p in per_rank)
+    kernel_ms = max(p[1] for p in per_rank)
+    kdt = max(p[2] for p in per_rank)
 
     if rank == 0:
         value = n_global * args.steps / elapsed
-        achieved_gbs = BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
+        achieved_gbs = BYTES_PER_ENV_STEP_VECENV * n / (kernel_ms * 1e-3) / 1e9
         achieved_tf = FLOPS_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e12
-        traffic, valu_frac, traffic_src = pmc_traffic(n)
+        traffic, traffic_x2, valu_frac, traffic_src = pmc_traffic(n)
+        ksteps = min(args.steps, 200)
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "BASELINE configs[2]: Go1 single_path tunnel (32x32 sub-terrains), 2x10x11 front "
-                                   "height scan, actuator net, e2e rewards, DR; N(0,1) actions",
-                       "envs_per_gpu": n, "global_envs": n_global, "decimation": c.decimation,
-                       "integrator_substeps": c.n_internal, "parallelism": f"env-shard x{world}"},
+            "config": {"workload": "BASELINE configs[2]: VecEnv.step of HistoryWrapper(TrajectoryTrackingEnv), Go1 "
+                                   "single_path tunnel (32x32 sub-terrains), 2x10x11 front height scan, actuator "
+                                   "net, e2e rewards, DR; N(0,1) actions",
+                       "envs_per_gpu": n, "global_envs": n_global, "decimation": base._abi_cfg.decimation,
+                       "integrator_substeps": base._abi_cfg.n_internal, "parallelism": f"env-shard x{world}",
+                       "world_size_seen": world},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * n,
+                         "traffic_fetch_doubled": traffic_x2,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP_VECENV * n,
                          "kernel": "go1_step_kernel<false>", "kernel_ms": kernel_ms,
-                         "bytes_per_env_step": BYTES_PER_ENV_STEP,
-                         "fp32_tflops_actuator_only": achieved_tf, "fp32_frac_actuator_only": achieved_tf / FP32_PEAK_TFLOPS,
+                         "bytes_per_env_step": BYTES_PER_ENV_STEP_VECENV,
+                         "fp32_tflops_actuator_only": achieved_tf,
+                         "fp32_frac_actuator_only": achieved_tf / FP32_PEAK_TFLOPS,
                          "valu_issue_frac_pmc": valu_frac,
                          "note": "latency/VALU-issue bound, not HBM bound: see DESIGN.md section 5"},
+            "kernel_loop": {"value": n_global * ksteps / kdt, "unit": "env-steps/s", "ms_per_step": kdt / ksteps * 1e3,
+                            "kernel_ms": max(p[3] for p in per_rank),
+                            "what": "Go1Native.step alone (the fused kernel launch, no env host code)"},
+            "per_rank": [{"rank": r, "elapsed_s": p[0], "kernel_ms": p[1]} for r, p in enumerate(per_rank)],
         }
         if args.sweep:
             line["sweep"] = [env_sweep(int(x), dev) for x in args.sweep.split(",")]
-        if not args.no_rollout:
+        if not args.no_rollout and world == 1:
             line["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24))
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(n, budget_s=args.cpu_budget)
         print(json.dumps(line), flush=True)
-    for e in evs:
-        hp.hipEventDestroy(e)
+    env.close()
     if dist:
+        dist.barrier()
         dist.destroy_process_group()
 
 

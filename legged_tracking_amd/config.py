@@ -555,8 +555,80 @@ PHYSICS = dict(contact_stiffness=2.0e4, contact_damping=80.0, friction_damping=6
                limit_stiffness=2000.0, limit_damping=20.0, n_internal=2)
 
 
+def _get(cfg, path, default=None):
+    obj = cfg
+    for part in path.split("."):
+        if not hasattr(obj, part):
+            return default
+        obj = getattr(obj, part)
+    return obj
+
+
+# Cfg values the HIP step implements, checked before a handle is built: anything else raises
+# NotImplementedError instead of silently training on different rewards / targets / observations.
+#   path -> (allowed values, reference line the value selects)
+SUPPORTED = {
+    "rewards.only_positive_rewards": ((False,), "legged_robot_trajectory_tracking.py:341-342"),
+    "rewards.only_positive_rewards_ji22_style": ((False,), ":343-344"),
+    "rewards.lin_vel_form": (("exp",), "reward_crawling.py:88-104"),
+    "rewards.reward_container_name": (("RewardsCrawling",), ":1373-1377"),
+    "env.terminate_end_of_trajectory": ((False,), ":211-213, reward_crawling.py:64-66"),
+    "env.use_terminal_body_rotation": ((False,), ":215-216"),
+    "env.rotate_camera": ((False,), ":1934-1936"),
+    "env.timestep_in_obs": ((False,), ":375-377"),
+    "env.observe_heights": ((True,), ":388-423"),
+    "env.command_type": (("xy",), ":801-816"),
+    "env.observe_command": ((True,), ":367-377"),
+    "env.observe_vel": ((False,), ":445-453"),
+    "env.observe_only_ang_vel": ((False,), ":455-457"),
+    "env.observe_only_lin_vel": ((False,), ":459-461"),
+    "env.observe_yaw": ((False,), ":463-468"),
+    "env.observe_contact_states": ((False,), ":470-473"),
+    "env.observe_two_prev_actions": ((False,), ":425-427"),
+    "env.observe_timing_parameter": ((False,), ":429-431"),
+    "env.observe_clock_inputs": ((False,), ":433-435"),
+    "terrain.measure_front_half": ((True,), ":395-399"),
+    "commands.traj_function": (("fixed_target",), "trajectory_function.py:14-93"),
+    "commands.traj_length": ((1,), "trajectory_function.py:14-26"),
+    "commands.sampling_based_planning": ((False,), ":850-921 (OMPL planner)"),
+    "commands.switch_upon_reach": ((True,), ":836-839"),
+    "control.control_type": (("actuator_net",), ":957-996"),
+    "domain_rand.lag_timesteps": ((6,), ":973-974"),
+    "domain_rand.randomize_lag_timesteps": ((True,), ":973-974"),
+    "domain_rand.randomize_com_displacement": ((False,), ":735-742"),
+    "domain_rand.push_robots": ((False,), ":1055-1071"),
+    "domain_rand.randomize_rigids_after_start": ((False,), ":226-228"),
+    "curriculum_thresholds.cl_fix_target": ((False,), ":188-196"),
+}
+
+
+def unsupported(cfg):
+    """[(path, value, allowed, reference line)] for every Cfg value the HIP step does not implement."""
+    bad = []
+    for path, (allowed, ref) in SUPPORTED.items():
+        v = _get(cfg, path, allowed[0])
+        if isinstance(v, (np.bool_, np.integer)):
+            v = v.item()
+        if v not in allowed:
+            bad.append((path, v, allowed, ref))
+    mesh, ttype = _get(cfg, "terrain.mesh_type", "trimesh"), _get(cfg, "terrain.terrain_type", "")
+    if mesh != "plane" and ttype != "single_path":
+        bad.append(("terrain.terrain_type", ttype, ("single_path",), "tunnel_fn.py:99-163"))
+    return bad
+
+
+def check_supported(cfg):
+    bad = unsupported(cfg)
+    if bad:
+        lines = "; ".join(f"Cfg.{p} = {v!r} (implemented: {', '.join(map(repr, a))}; reference {r})"
+                          for p, v, a, r in bad)
+        raise NotImplementedError("not on the accelerated path: " + lines)
+
+
 def build_abi_config(cfg, n_envs=None, physics=None, actuator=None, hf_shape=(80, 40)):
-    """go1_config for the C ABI from a (mutated) Cfg."""
+    """go1_config for the C ABI from a (mutated) Cfg (raises NotImplementedError for any Cfg value
+    the HIP step does not implement, see SUPPORTED)."""
+    check_supported(cfg)
     physics = dict(PHYSICS, **(physics or {}))
     d = derived(cfg)
     c = abi.Go1Config()

@@ -276,6 +276,8 @@ class LeggedRobot:
         self._train_ep, self._eval_ep, self._timeouts = _episode_dicts()
         self._install_extras()
         self._rng_step = 0
+        # measurement hook (bench.py): hipEvent_t pairs to record around the next steps' kernel
+        self.kernel_events = deque()
 
     # ------------------------------------------------------------------ host state
     def _randomize_gravity(self, external_force=None):
@@ -434,7 +436,7 @@ class LeggedRobot:
         hist = self._obs_hist[s] if self._obs_hist is not None else None
         self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
                        rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux,
-                       obs_history=hist)
+                       obs_history=hist, events=self.kernel_events.popleft() if self.kernel_events else None)
         self._last_hist = hist
         self._rng_step += 1
         self._elog.advance()

@@ -31,6 +31,18 @@
 #include "../include/go1_mi355x.h"
 #include "portable_math.h"
 
+/* Working precision of the native integrator restatement: double for the oracle
+ * (libgo1_oracle.so), float for the like-for-like CPU timing baseline
+ * (libgo1_oracle_f32.so, -DGO1O_REAL=float -fsingle-precision-constant; <tgmath.h>
+ * makes sqrt/sin/cos/floor/fmin/fmax follow the argument type).  The post-physics
+ * code is f32 in both builds (explicit sqrtf/expf/... calls). */
+#ifndef GO1O_REAL
+#define GO1O_REAL double
+#endif
+typedef GO1O_REAL real;
+#include <tgmath.h>
+#undef I /* <complex.h> (via <tgmath.h>) defines I; the model uses it as a field name */
+
 #define NDOF 12
 #define NB 17
 #define PI_F 3.14159265358979323846f
@@ -183,17 +195,17 @@ static float sum12_legs(const float* x) {
 /* ====================================================================== */
 /*                      native physics, f64 restatement                    */
 /* ====================================================================== */
-typedef struct { double m[6][6]; } M6;
+typedef struct { real m[6][6]; } M6;
 
 typedef struct {
-  double mass, com[3], I[3][3]; /* inertia about COM */
+  real mass, com[3], I[3][3]; /* inertia about COM */
 } Body;
 
 typedef struct {
   Body base;
   Body leg[4][3];
-  double origin[4][3][3]; /* joint origins in parent frame */
-  double foot[3], foot_r, trunk_half[3], thigh_r, calf_r;
+  real origin[4][3][3]; /* joint origins in parent frame */
+  real foot[3], foot_r, trunk_half[3], thigh_r, calf_r;
 } Model;
 
 static void load_model(const go1_config* c, Model* M) {
@@ -207,7 +219,7 @@ static void load_model(const go1_config* c, Model* M) {
     Body* B = bodies[b];
     B->mass = p[k++];
     for (int i = 0; i < 3; ++i) B->com[i] = p[k++];
-    double xx = p[k++], xy = p[k++], xz = p[k++], yy = p[k++], yz = p[k++], zz = p[k++];
+    real xx = p[k++], xy = p[k++], xz = p[k++], yy = p[k++], yz = p[k++], zz = p[k++];
     B->I[0][0] = xx; B->I[0][1] = xy; B->I[0][2] = xz;
     B->I[1][0] = xy; B->I[1][1] = yy; B->I[1][2] = yz;
     B->I[2][0] = xz; B->I[2][1] = yz; B->I[2][2] = zz;
@@ -222,20 +234,20 @@ static void load_model(const go1_config* c, Model* M) {
   M->calf_r = p[k++];
 }
 
-static void cross3(const double* a, const double* b, double* o) {
-  double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+static void cross3(const real* a, const real* b, real* o) {
+  real x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   o[0] = x; o[1] = y; o[2] = z;
 }
 
 /* rigid spatial inertia about the body frame origin: [[Ic + m(c.c 1 - c c^T), m c~], [m c~^T, m 1]] */
-static void rigid_inertia(const Body* B, double mass_scale, M6* I) {
-  double m = B->mass * mass_scale;
-  const double* c = B->com;
-  double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+static void rigid_inertia(const Body* B, real mass_scale, M6* I) {
+  real m = B->mass * mass_scale;
+  const real* c = B->com;
+  real cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
   memset(I, 0, sizeof(*I));
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) I->m[i][j] = B->I[i][j] * mass_scale + m * ((i == j ? cc : 0.0) - c[i] * c[j]);
-  double cx[3][3] = {{0, -c[2], c[1]}, {c[2], 0, -c[0]}, {-c[1], c[0], 0}};
+  real cx[3][3] = {{0, -c[2], c[1]}, {c[2], 0, -c[0]}, {-c[1], c[0], 0}};
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
       I->m[i][3 + j] = m * cx[i][j];
@@ -244,17 +256,17 @@ static void rigid_inertia(const Body* B, double mass_scale, M6* I) {
   for (int i = 0; i < 3; ++i) I->m[3 + i][3 + i] = m;
 }
 
-static void m6_vec(const M6* A, const double* v, double* o) {
+static void m6_vec(const M6* A, const real* v, real* o) {
   for (int i = 0; i < 6; ++i) {
-    double s = 0;
+    real s = 0;
     for (int j = 0; j < 6; ++j) s += A->m[i][j] * v[j];
     o[i] = s;
   }
 }
 
 /* spatial force cross product v x* f, v = (w, v), f = (n, f) */
-static void crf(const double* v, const double* f, double* o) {
-  double a[3], b[3], c[3];
+static void crf(const real* v, const real* f, real* o) {
+  real a[3], b[3], c[3];
   cross3(v, f, a);
   cross3(v + 3, f + 3, b);
   cross3(v, f + 3, c);
@@ -263,9 +275,9 @@ static void crf(const double* v, const double* f, double* o) {
 
 /* rotation matrix E (parent->child coords) of a revolute joint about unit axis ax by q:
  * E = Rot(ax, q)^T */
-static void joint_E(int ax, double q, double E[3][3]) {
-  double c = cos(q), s = sin(q);
-  memset(E, 0, sizeof(double) * 9);
+static void joint_E(int ax, real q, real E[3][3]) {
+  real c = cos(q), s = sin(q);
+  memset(E, 0, sizeof(real) * 9);
   if (ax == 0) {
     E[0][0] = 1; E[1][1] = c; E[1][2] = s; E[2][1] = -s; E[2][2] = c;
   } else {
@@ -274,8 +286,8 @@ static void joint_E(int ax, double q, double E[3][3]) {
 }
 
 /* motion transform parent -> child: (w, v) -> (E w, E (v - r x w)) */
-static void xform_motion(double E[3][3], const double* r, const double* vin, double* vout) {
-  double rw[3], t[3];
+static void xform_motion(real E[3][3], const real* r, const real* vin, real* vout) {
+  real rw[3], t[3];
   cross3(r, vin, rw);
   for (int i = 0; i < 3; ++i) t[i] = vin[3 + i] - rw[i];
   for (int i = 0; i < 3; ++i) {
@@ -285,8 +297,8 @@ static void xform_motion(double E[3][3], const double* r, const double* vin, dou
 }
 
 /* force transform child -> parent: (n, f) -> (E^T n + r x E^T f, E^T f) */
-static void xform_force_T(double E[3][3], const double* r, const double* fin, double* fout) {
-  double n[3], f[3], rf[3];
+static void xform_force_T(real E[3][3], const real* r, const real* fin, real* fout) {
+  real n[3], f[3], rf[3];
   for (int i = 0; i < 3; ++i) {
     n[i] = E[0][i] * fin[0] + E[1][i] * fin[1] + E[2][i] * fin[2];
     f[i] = E[0][i] * fin[3] + E[1][i] * fin[4] + E[2][i] * fin[5];
@@ -296,59 +308,59 @@ static void xform_force_T(double E[3][3], const double* r, const double* fin, do
 }
 
 /* X^T A X for X = motion transform (E, r) */
-static void xform_inertia_T(double E[3][3], const double* r, const M6* A, M6* out) {
+static void xform_inertia_T(real E[3][3], const real* r, const M6* A, M6* out) {
   /* build X explicitly: X = [[E, 0], [-E r~, E]] */
-  double X[6][6];
+  real X[6][6];
   memset(X, 0, sizeof(X));
-  double rx[3][3] = {{0, -r[2], r[1]}, {r[2], 0, -r[0]}, {-r[1], r[0], 0}};
+  real rx[3][3] = {{0, -r[2], r[1]}, {r[2], 0, -r[0]}, {-r[1], r[0], 0}};
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
       X[i][j] = E[i][j];
       X[3 + i][3 + j] = E[i][j];
-      double s = 0;
+      real s = 0;
       for (int k = 0; k < 3; ++k) s += E[i][k] * rx[k][j];
       X[3 + i][j] = -s;
     }
-  double T[6][6];
+  real T[6][6];
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) {
-      double s = 0;
+      real s = 0;
       for (int k = 0; k < 6; ++k) s += A->m[i][k] * X[k][j];
       T[i][j] = s;
     }
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) {
-      double s = 0;
+      real s = 0;
       for (int k = 0; k < 6; ++k) s += X[k][i] * T[k][j];
       out->m[i][j] = s;
     }
 }
 
 /* solve SPD 6x6 A x = b (Cholesky) */
-static void solve6(const M6* A, const double* b, double* x) {
-  double L[6][6] = {{0}};
+static void solve6(const M6* A, const real* b, real* x) {
+  real L[6][6] = {{0}};
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j <= i; ++j) {
-      double s = A->m[i][j];
+      real s = A->m[i][j];
       for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
-      if (i == j) L[i][i] = sqrt(s > 1e-300 ? s : 1e-300);
+      if (i == j) L[i][i] = sqrt(s > (real)1e-30 ? s : (real)1e-30);
       else L[i][j] = s / L[j][j];
     }
-  double y[6];
+  real y[6];
   for (int i = 0; i < 6; ++i) {
-    double s = b[i];
+    real s = b[i];
     for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
     y[i] = s / L[i][i];
   }
   for (int i = 5; i >= 0; --i) {
-    double s = y[i];
+    real s = y[i];
     for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
     x[i] = s / L[i][i];
   }
 }
 
-static void quat_to_R(const double* q, double R[3][3]) {
-  double x = q[0], y = q[1], z = q[2], w = q[3];
+static void quat_to_R(const real* q, real R[3][3]) {
+  real x = q[0], y = q[1], z = q[2], w = q[3];
   R[0][0] = 1 - 2 * (y * y + z * z); R[0][1] = 2 * (x * y - z * w); R[0][2] = 2 * (x * z + y * w);
   R[1][0] = 2 * (x * y + z * w); R[1][1] = 1 - 2 * (x * x + z * z); R[1][2] = 2 * (y * z - x * w);
   R[2][0] = 2 * (x * z - y * w); R[2][1] = 2 * (y * z + x * w); R[2][2] = 1 - 2 * (x * x + y * y);
@@ -358,48 +370,48 @@ static void quat_to_R(const double* q, double R[3][3]) {
 typedef struct {
   const float* tile; /* (2, nx, ny) or NULL for plane */
   int nx, ny;
-  double ox, oy, hs;
+  real ox, oy, hs;
 } TerrainView;
 
-static double tile_at(const TerrainView* T, int layer, int i, int j) {
+static real tile_at(const TerrainView* T, int layer, int i, int j) {
   if (i < 0) i = 0;
   if (i > T->nx - 1) i = T->nx - 1;
   if (j < 0) j = 0;
   if (j > T->ny - 1) j = T->ny - 1;
-  return (double)T->tile[((size_t)layer * T->nx + i) * T->ny + j];
+  return (real)T->tile[((size_t)layer * T->nx + i) * T->ny + j];
 }
 
 /* height and gradient of layer at world (x, y) */
-static void height_query(const TerrainView* T, int layer, double x, double y, double* h, double* gx, double* gy) {
+static void height_query(const TerrainView* T, int layer, real x, real y, real* h, real* gx, real* gy) {
   if (!T->tile) {
     *h = layer == 1 ? 0.0 : 1e9;
     *gx = *gy = 0.0;
     return;
   }
-  double u = fmin(fmax((x - T->ox) / T->hs, -4.0), T->nx + 4.0), v = fmin(fmax((y - T->oy) / T->hs, -4.0), T->ny + 4.0);
-  double fu = floor(u), fv = floor(v);
+  real u = fmin(fmax((x - T->ox) / T->hs, -4.0), T->nx + 4.0), v = fmin(fmax((y - T->oy) / T->hs, -4.0), T->ny + 4.0);
+  real fu = floor(u), fv = floor(v);
   int i = (int)fu, j = (int)fv;
-  double a = u - fu, b = v - fv;
-  double h00 = tile_at(T, layer, i, j), h10 = tile_at(T, layer, i + 1, j);
-  double h01 = tile_at(T, layer, i, j + 1), h11 = tile_at(T, layer, i + 1, j + 1);
+  real a = u - fu, b = v - fv;
+  real h00 = tile_at(T, layer, i, j), h10 = tile_at(T, layer, i + 1, j);
+  real h01 = tile_at(T, layer, i, j + 1), h11 = tile_at(T, layer, i + 1, j + 1);
   *h = (1 - a) * (1 - b) * h00 + a * (1 - b) * h10 + (1 - a) * b * h01 + a * b * h11;
   *gx = ((1 - b) * (h10 - h00) + b * (h11 - h01)) / T->hs;
   *gy = ((1 - a) * (h01 - h00) + a * (h11 - h10)) / T->hs;
 }
 
 typedef struct {
-  double k, d, kf, mu;
+  real k, d, kf, mu;
 } ContactParams;
 
 /* penalty contact of a sphere (centre p, velocity pv, radius r) against floor and
  * ceiling; returns world force F */
-static void sphere_contact(const TerrainView* T, const ContactParams* C, const double* p, const double* pv, double r,
-                           double* F) {
+static void sphere_contact(const TerrainView* T, const ContactParams* C, const real* p, const real* pv, real r,
+                           real* F) {
   F[0] = F[1] = F[2] = 0.0;
   for (int layer = 1; layer >= 0; --layer) {
-    double h, gx, gy;
+    real h, gx, gy;
     height_query(T, layer, p[0], p[1], &h, &gx, &gy);
-    double n[3], dv;
+    real n[3], dv;
     if (layer == 1) { /* floor, normal up */
       dv = h + r - p[2];
       n[0] = -gx; n[1] = -gy; n[2] = 1.0;
@@ -408,17 +420,17 @@ static void sphere_contact(const TerrainView* T, const ContactParams* C, const d
       n[0] = gx; n[1] = gy; n[2] = -1.0;
     }
     if (dv <= 0.0) continue;
-    double inv = 1.0 / sqrt(n[0] * n[0] + n[1] * n[1] + 1.0);
+    real inv = 1.0 / sqrt(n[0] * n[0] + n[1] * n[1] + 1.0);
     for (int i = 0; i < 3; ++i) n[i] *= inv;
-    double depth = dv * inv;
-    double vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
-    double fn = C->k * depth - C->d * vn;
+    real depth = dv * inv;
+    real vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
+    real fn = C->k * depth - C->d * vn;
     if (fn <= 0.0) continue;
-    double vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
-    double vtn = sqrt(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
-    double ft = C->kf * vtn, fmax = C->mu * fn;
+    real vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
+    real vtn = sqrt(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
+    real ft = C->kf * vtn, fmax = C->mu * fn;
     if (ft > fmax) ft = fmax;
-    double s = vtn > 1e-9 ? ft / vtn : 0.0;
+    real s = vtn > 1e-9 ? ft / vtn : 0.0;
     for (int i = 0; i < 3; ++i) F[i] += fn * n[i] - s * vt[i];
   }
 }
@@ -430,18 +442,18 @@ static void sphere_contact(const TerrainView* T, const ContactParams* C, const d
  * Trunk: the 8 corners of the collision box (radius 0). */
 #define N_THIGH_PTS 3
 #define N_CALF_PTS 2
-static const double THIGH_PTS_Z[N_THIGH_PTS] = {-0.071, -0.142, -0.213};
-static const double CALF_PTS_Z[N_CALF_PTS] = {-0.071, -0.142};
+static const real THIGH_PTS_Z[N_THIGH_PTS] = {-0.071, -0.142, -0.213};
+static const real CALF_PTS_Z[N_CALF_PTS] = {-0.071, -0.142};
 
 typedef struct {
-  double pos[3], quat[4], v[3], w[3];
-  double q[NDOF], qd[NDOF];
+  real pos[3], quat[4], v[3], w[3];
+  real q[NDOF], qd[NDOF];
 } PhysState;
 
 /* world pose/velocity of a point given body pose (Rb, pb) and body spatial velocity
  * (w, v) in body coords at body origin */
-static void point_kin(double Rb[3][3], const double* pb, const double* vb, const double* lp, double* pw, double* vw) {
-  double wl[3], vl[3];
+static void point_kin(real Rb[3][3], const real* pb, const real* vb, const real* lp, real* pw, real* vw) {
+  real wl[3], vl[3];
   cross3(vb, lp, wl);
   for (int i = 0; i < 3; ++i) vl[i] = vb[3 + i] + wl[i];
   for (int i = 0; i < 3; ++i) {
@@ -451,47 +463,47 @@ static void point_kin(double Rb[3][3], const double* pb, const double* vb, const
 }
 
 /* world force F at local point lp -> body-coords spatial force (n, f) at origin */
-static void point_force(double Rb[3][3], const double* lp, const double* F, double* fs) {
-  double f[3];
+static void point_force(real Rb[3][3], const real* lp, const real* F, real* fs) {
+  real f[3];
   for (int i = 0; i < 3; ++i) f[i] = Rb[0][i] * F[0] + Rb[1][i] * F[1] + Rb[2][i] * F[2];
-  double n[3];
+  real n[3];
   cross3(lp, f, n);
   for (int i = 0; i < 3; ++i) { fs[i] += n[i]; fs[3 + i] += f[i]; }
 }
 
 /* One integrator step of length h with torques tau.  Writes net contact forces
  * per reported body (17 x 3, world) into cf (may be NULL). */
-static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, const double* tau, double h,
-                         const double* g, double friction, double payload, const TerrainView* T, double* cf) {
+static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, const real* tau, real h,
+                         const real* g, real friction, real payload, const TerrainView* T, real* cf) {
   ContactParams C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
-  double R[3][3];
+  real R[3][3];
   quat_to_R(S->quat, R);
-  double vb[6]; /* base spatial velocity, body coords */
+  real vb[6]; /* base spatial velocity, body coords */
   for (int i = 0; i < 3; ++i) {
     vb[i] = R[0][i] * S->w[0] + R[1][i] * S->w[1] + R[2][i] * S->w[2];
     vb[3 + i] = R[0][i] * S->v[0] + R[1][i] * S->v[1] + R[2][i] * S->v[2];
   }
-  double gb[3];
+  real gb[3];
   for (int i = 0; i < 3; ++i) gb[i] = R[0][i] * g[0] + R[1][i] * g[1] + R[2][i] * g[2];
-  if (cf) memset(cf, 0, sizeof(double) * NB * 3);
+  if (cf) memset(cf, 0, sizeof(real) * NB * 3);
 
   /* base rigid inertia (payload added to the trunk, inertia scaled by mass ratio) */
-  double mscale = (M->base.mass + payload) / M->base.mass;
+  real mscale = (M->base.mass + payload) / M->base.mass;
   M6 IA0;
   rigid_inertia(&M->base, mscale, &IA0);
-  double pA0[6], hmom[6];
+  real pA0[6], hmom[6];
   m6_vec(&IA0, vb, hmom);
   crf(vb, hmom, pA0);
   {
-    double fext[6] = {0}, fg[3], cg[3];
-    double m = M->base.mass * mscale;
+    real fext[6] = {0}, fg[3], cg[3];
+    real m = M->base.mass * mscale;
     for (int i = 0; i < 3; ++i) fg[i] = m * gb[i];
     cross3(M->base.com, fg, cg);
     for (int i = 0; i < 3; ++i) { fext[i] += cg[i]; fext[3 + i] += fg[i]; }
     for (int cx = 0; cx < 8; ++cx) {
-      double lp[3] = {(cx & 1) ? M->trunk_half[0] : -M->trunk_half[0], (cx & 2) ? M->trunk_half[1] : -M->trunk_half[1],
+      real lp[3] = {(cx & 1) ? M->trunk_half[0] : -M->trunk_half[0], (cx & 2) ? M->trunk_half[1] : -M->trunk_half[1],
                       (cx & 4) ? M->trunk_half[2] : -M->trunk_half[2]};
-      double pw[3], vw[3], F[3];
+      real pw[3], vw[3], F[3];
       point_kin(R, S->pos, vb, lp, pw, vw);
       sphere_contact(T, &C, pw, vw, 0.0, F);
       point_force(R, lp, F, fext);
@@ -501,27 +513,27 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
   }
 
   /* per-leg quantities kept for the forward pass */
-  double E[4][3][3][3], vj[4][3][6], cj[4][3][6], U[4][3][6], D[4][3], u[4][3];
+  real E[4][3][3][3], vj[4][3][6], cj[4][3][6], U[4][3][6], D[4][3], u[4][3];
   for (int l = 0; l < 4; ++l) {
-    double Rp[3][3], pp[3], vp[6];
+    real Rp[3][3], pp[3], vp[6];
     memcpy(Rp, R, sizeof(Rp));
     memcpy(pp, S->pos, sizeof(pp));
     memcpy(vp, vb, sizeof(vp));
     M6 IA[3];
-    double pA[3][6], Rw[3][3][3], pw_[3][3];
+    real pA[3][6], Rw[3][3][3], pw_[3][3];
     for (int j = 0; j < 3; ++j) {
       int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
-      const double* r = M->origin[l][j];
+      const real* r = M->origin[l][j];
       joint_E(ax, S->q[dof], E[l][j]);
       xform_motion(E[l][j], r, vp, vj[l][j]);
       vj[l][j][ax] += S->qd[dof];
       /* c = v x (S qd) */
-      double sq[3] = {0, 0, 0};
+      real sq[3] = {0, 0, 0};
       sq[ax] = S->qd[dof];
       cross3(vj[l][j], sq, cj[l][j]);
       cross3(vj[l][j] + 3, sq, cj[l][j] + 3);
       /* world pose of the link */
-      double rw[3];
+      real rw[3];
       for (int i = 0; i < 3; ++i) rw[i] = Rp[i][0] * r[0] + Rp[i][1] * r[1] + Rp[i][2] * r[2];
       for (int i = 0; i < 3; ++i) {
         pw_[j][i] = pp[i] + rw[i];
@@ -536,10 +548,10 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
     for (int j = 0; j < 3; ++j) {
       const Body* B = &M->leg[l][j];
       rigid_inertia(B, 1.0, &IA[j]);
-      double hm[6];
+      real hm[6];
       m6_vec(&IA[j], vj[l][j], hm);
       crf(vj[l][j], hm, pA[j]);
-      double gl[3], fext[6] = {0}, fg[3], cg[3];
+      real gl[3], fext[6] = {0}, fg[3], cg[3];
       for (int i = 0; i < 3; ++i) gl[i] = Rw[j][0][i] * g[0] + Rw[j][1][i] * g[1] + Rw[j][2][i] * g[2];
       for (int i = 0; i < 3; ++i) fg[i] = B->mass * gl[i];
       cross3(B->com, fg, cg);
@@ -547,7 +559,7 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       int body_idx = 1 + l * 4 + j; /* hip, thigh, calf */
       if (j == 1) {
         for (int p = 0; p < N_THIGH_PTS; ++p) {
-          double lp[3] = {0, 0, THIGH_PTS_Z[p]}, pw[3], vw[3], F[3];
+          real lp[3] = {0, 0, THIGH_PTS_Z[p]}, pw[3], vw[3], F[3];
           point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
           sphere_contact(T, &C, pw, vw, M->thigh_r, F);
           point_force(Rw[j], lp, F, fext);
@@ -555,10 +567,10 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
         }
       } else if (j == 2) {
         for (int p = 0; p < N_CALF_PTS + 1; ++p) {
-          double lp[3], r = p < N_CALF_PTS ? M->calf_r : M->foot_r;
+          real lp[3], r = p < N_CALF_PTS ? M->calf_r : M->foot_r;
           if (p < N_CALF_PTS) { lp[0] = 0; lp[1] = 0; lp[2] = CALF_PTS_Z[p]; }
           else { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
-          double pw[3], vw[3], F[3];
+          real pw[3], vw[3], F[3];
           point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
           sphere_contact(T, &C, pw, vw, r, F);
           point_force(Rw[j], lp, F, fext);
@@ -571,13 +583,13 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
     /* backward pass calf -> hip */
     for (int j = 2; j >= 0; --j) {
       int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
-      double t = tau[dof];
+      real t = tau[dof];
       /* native joint-limit spring-damper at the URDF limits */
       /* implicit in the joint: the torque at the end of the sub-step, -k (q + h qd') - d qd'
          with qd' = qd + h qdd, moves (h d + h^2 k) qdd to the joint inertia D */
-      double lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1], Dimp = 0.0;
+      real lo = cfg->hard_limits[dof * 2], hi = cfg->hard_limits[dof * 2 + 1], Dimp = 0.0;
       if (S->q[dof] > hi || S->q[dof] < lo) {
-        double ex = S->q[dof] > hi ? S->q[dof] - hi : S->q[dof] - lo;
+        real ex = S->q[dof] > hi ? S->q[dof] - hi : S->q[dof] - lo;
         t -= cfg->limit_stiffness * (ex + h * S->qd[dof]) + cfg->limit_damping * S->qd[dof];
         Dimp = h * cfg->limit_damping + h * h * cfg->limit_stiffness;
       }
@@ -585,13 +597,13 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       D[l][j] = IA[j].m[ax][ax] + Dimp;
       u[l][j] = t - pA[j][ax];
       M6 Ia;
-      double pa[6], Iac[6];
+      real pa[6], Iac[6];
       for (int a = 0; a < 6; ++a)
         for (int b = 0; b < 6; ++b) Ia.m[a][b] = IA[j].m[a][b] - U[l][j][a] * U[l][j][b] / D[l][j];
       m6_vec(&Ia, cj[l][j], Iac);
       for (int i = 0; i < 6; ++i) pa[i] = pA[j][i] + Iac[i] + U[l][j][i] * u[l][j] / D[l][j];
       M6 Ip;
-      double pp2[6];
+      real pp2[6];
       xform_inertia_T(E[l][j], M->origin[l][j], &Ia, &Ip);
       xform_force_T(E[l][j], M->origin[l][j], pa, pp2);
       if (j > 0) {
@@ -604,19 +616,19 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
     }
   }
   /* base acceleration */
-  double a0[6], mp[6];
+  real a0[6], mp[6];
   for (int i = 0; i < 6; ++i) mp[i] = -pA0[i];
   solve6(&IA0, mp, a0);
-  double qdd[NDOF];
+  real qdd[NDOF];
   for (int l = 0; l < 4; ++l) {
-    double ap[6];
+    real ap[6];
     memcpy(ap, a0, sizeof(ap));
     for (int j = 0; j < 3; ++j) {
       int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
-      double aj[6];
+      real aj[6];
       xform_motion(E[l][j], M->origin[l][j], ap, aj);
       for (int i = 0; i < 6; ++i) aj[i] += cj[l][j][i];
-      double Ua = 0;
+      real Ua = 0;
       for (int i = 0; i < 6; ++i) Ua += U[l][j][i] * aj[i];
       qdd[dof] = (u[l][j] - Ua) / D[l][j];
       aj[ax] += qdd[dof];
@@ -624,7 +636,7 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
     }
   }
   /* semi-implicit Euler: classical accelerations of the base in world coords */
-  double wv[3], alin_b[3], aw[3], al[3];
+  real wv[3], alin_b[3], aw[3], al[3];
   cross3(vb, vb + 3, wv);
   for (int i = 0; i < 3; ++i) alin_b[i] = a0[3 + i] + wv[i];
   for (int i = 0; i < 3; ++i) {
@@ -638,16 +650,16 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
   }
   {
     /* q <- exp(h w / 2) (x) q, world-frame angular velocity */
-    double th = 0.5 * h * sqrt(S->w[0] * S->w[0] + S->w[1] * S->w[1] + S->w[2] * S->w[2]);
-    double sc = th > 1e-12 ? sin(th) / (th / (0.5 * h)) : 0.5 * h;
-    double dq[4] = {S->w[0] * sc, S->w[1] * sc, S->w[2] * sc, cos(th)};
-    double* q = S->quat;
-    double nq[4];
+    real th = 0.5 * h * sqrt(S->w[0] * S->w[0] + S->w[1] * S->w[1] + S->w[2] * S->w[2]);
+    real sc = th > 1e-12 ? sin(th) / (th / (0.5 * h)) : 0.5 * h;
+    real dq[4] = {S->w[0] * sc, S->w[1] * sc, S->w[2] * sc, cos(th)};
+    real* q = S->quat;
+    real nq[4];
     nq[3] = dq[3] * q[3] - dq[0] * q[0] - dq[1] * q[1] - dq[2] * q[2];
     nq[0] = dq[3] * q[0] + dq[0] * q[3] + dq[1] * q[2] - dq[2] * q[1];
     nq[1] = dq[3] * q[1] - dq[0] * q[2] + dq[1] * q[3] + dq[2] * q[0];
     nq[2] = dq[3] * q[2] + dq[0] * q[1] - dq[1] * q[0] + dq[2] * q[3];
-    double n = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+    real n = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
     for (int i = 0; i < 4; ++i) q[i] = nq[i] / n;
   }
   for (int d = 0; d < NDOF; ++d) {
@@ -664,12 +676,17 @@ void go1o_physics(const go1_config* cfg, double* pos, double* quat, double* v, d
   Model M;
   load_model(cfg, &M);
   PhysState S;
-  memcpy(S.pos, pos, 24); memcpy(S.quat, quat, 32); memcpy(S.v, v, 24); memcpy(S.w, w, 24);
-  memcpy(S.q, q, 96); memcpy(S.qd, qd, 96);
+  real tr[NDOF], gr[3], cfr[NB * 3];
+  for (int i = 0; i < 3; ++i) { S.pos[i] = pos[i]; S.v[i] = v[i]; S.w[i] = w[i]; gr[i] = g[i]; }
+  for (int i = 0; i < 4; ++i) S.quat[i] = quat[i];
+  for (int d = 0; d < NDOF; ++d) { S.q[d] = q[d]; S.qd[d] = qd[d]; tr[d] = tau[d]; }
   TerrainView T = {tile, cfg->hf_nx, cfg->hf_ny, ox, oy, cfg->horizontal_scale};
-  for (int i = 0; i < n_sub; ++i) phys_substep(&M, cfg, &S, tau, h, g, friction, payload, &T, cf_out);
-  memcpy(pos, S.pos, 24); memcpy(quat, S.quat, 32); memcpy(v, S.v, 24); memcpy(w, S.w, 24);
-  memcpy(q, S.q, 96); memcpy(qd, S.qd, 96);
+  for (int i = 0; i < n_sub; ++i) phys_substep(&M, cfg, &S, tr, (real)h, gr, (real)friction, (real)payload, &T, cfr);
+  for (int i = 0; i < 3; ++i) { pos[i] = S.pos[i]; v[i] = S.v[i]; w[i] = S.w[i]; }
+  for (int i = 0; i < 4; ++i) quat[i] = S.quat[i];
+  for (int d = 0; d < NDOF; ++d) { q[d] = S.q[d]; qd[d] = S.qd[d]; }
+  if (cf_out)
+    for (int i = 0; i < NB * 3; ++i) cf_out[i] = cfr[i];
 }
 
 /* ====================================================================== */
@@ -780,13 +797,13 @@ int go1o_reset_envs(const go1_config* c, const go1_state* st, const go1_terrain*
 
 /* World position of leg l's foot body origin (rigid_body_state[:, feet, 0:3]) */
 static void foot_world(const Model* M, const float* root, const float* dp, int l, float* out) {
-  double qd4[4] = {root[3], root[4], root[5], root[6]};
-  double R[3][3], Rp[3][3], pp[3] = {root[0], root[1], root[2]};
+  real qd4[4] = {root[3], root[4], root[5], root[6]};
+  real R[3][3], Rp[3][3], pp[3] = {root[0], root[1], root[2]};
   quat_to_R(qd4, R);
   memcpy(Rp, R, sizeof(Rp));
   for (int j = 0; j < 3; ++j) {
-    double E[3][3], Rw[3][3];
-    const double* r = M->origin[l][j];
+    real E[3][3], Rw[3][3];
+    const real* r = M->origin[l][j];
     for (int i = 0; i < 3; ++i) pp[i] += Rp[i][0] * r[0] + Rp[i][1] * r[1] + Rp[i][2] * r[2];
     joint_E(j == 0 ? 0 : 1, dp[l * 3 + j], E);
     for (int i = 0; i < 3; ++i)
@@ -830,7 +847,7 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   float cf[NB * 3];
   memset(cf, 0, sizeof(cf));
   const float* tile = NULL;
-  double ox = 0, oy = 0;
+  real ox = 0, oy = 0;
   if (c->terrain_kind == 1) {
     tile = ter->tiles + (size_t)ter->env_tile[e] * 2 * c->hf_nx * c->hf_ny;
     ox = ter->env_terrain_origin[(size_t)e * 3];
@@ -852,11 +869,11 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
       const float* id = a->inj_dof + ((size_t)sub * n + e) * NDOF * 2;
       for (int d = 0; d < NDOF; ++d) { dp[d] = id[2 * d]; dv[d] = id[2 * d + 1]; }
     } else {
-      double tau[NDOF], g[3] = {a->sim_gravity[0], a->sim_gravity[1], a->sim_gravity[2]};
-      double cfd[NB * 3];
+      real tau[NDOF], g[3] = {a->sim_gravity[0], a->sim_gravity[1], a->sim_gravity[2]};
+      real cfd[NB * 3];
       for (int d = 0; d < NDOF; ++d) tau[d] = torque[d];
       TerrainView T = {tile, c->hf_nx, c->hf_ny, ox, oy, c->horizontal_scale};
-      double h = (double)c->sim_dt / c->n_internal;
+      real h = (real)c->sim_dt / c->n_internal;
       for (int k = 0; k < c->n_internal; ++k)
         phys_substep(M, c, &S, tau, h, g, st->friction[e], st->payload[e], &T, cfd);
       for (int d = 0; d < NDOF; ++d) { dp[d] = (float)S.q[d]; dv[d] = (float)S.qd[d]; }

@@ -12,7 +12,10 @@ from legged_tracking_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "libgo1_oracle.so")
+# same source with an f32 integrator: bench.py's like-for-like CPU baseline (never the checker)
+LIB_PATH_F32 = os.path.join(HERE, "_build", "libgo1_oracle_f32.so")
 _lib = None
+_libs = {}
 
 
 def build():
@@ -20,12 +23,14 @@ def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
-def lib():
-    global _lib
+def lib(precision="f64"):
+    """The oracle library: "f64" integrator (the checker) or "f32" (CPU timing baseline)."""
+    path = {"f64": LIB_PATH, "f32": LIB_PATH_F32}[precision]
+    _lib = _libs.get(path)
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        if not os.path.exists(path):
             build()
-        _lib = C.CDLL(LIB_PATH)
+        _lib = _libs[path] = C.CDLL(path)
         _lib.go1o_step.argtypes = [C.POINTER(abi.Go1Config), C.POINTER(abi.Go1State), C.POINTER(abi.Go1Terrain),
                                    C.POINTER(abi.Go1StepArgs)]
         _lib.go1o_reset_envs.argtypes = [C.POINTER(abi.Go1Config), C.POINTER(abi.Go1State),
@@ -79,8 +84,9 @@ class NpTerrain:
 
 
 def step(cfg, state, terrain, actions, gravity_vec, sim_gravity, reward_scales, uniforms=None, rng_seed=0,
-         rng_step=0, inj=None, debug=True):
-    """One oracle step; mutates `state`; returns a dict of outputs."""
+         rng_step=0, inj=None, debug=True, precision="f64"):
+    """One oracle step; mutates `state`; returns a dict of outputs.  precision="f32" runs the
+    f32-integrator build (CPU timing baseline only)."""
     n = cfg.n_envs
     out = dict(obs=np.zeros((n, abi.GO1_NUM_OBS), np.float32), priv=np.zeros((n, 2), np.float32),
                rew=np.zeros(n, np.float32), reset=np.zeros(n, np.uint8), time_out=np.zeros(n, np.uint8),
@@ -119,7 +125,7 @@ def step(cfg, state, terrain, actions, gravity_vec, sim_gravity, reward_scales, 
         a.episode_log, a.aux = abi.ptr(out["episode_log"]), abi.ptr(out["aux"])
     st = state.struct()
     ts = terrain.struct()
-    rc = lib().go1o_step(C.byref(cfg), C.byref(st), C.byref(ts), C.byref(a))
+    rc = lib(precision).go1o_step(C.byref(cfg), C.byref(st), C.byref(ts), C.byref(a))
     assert rc == 0
     return out
 
