@@ -31,22 +31,65 @@
 extern "C" {
 #endif
 
-#define GO1_ABI_VERSION 2
+#define GO1_ABI_VERSION 3
 
 #define GO1_NUM_DOF 12
 #define GO1_NUM_BODIES 17
-#define GO1_NUM_TERMS 10
-#define GO1_NUM_SUMS 13
-#define GO1_NUM_OBS 261
+#define GO1_MAX_TERMS 16   /* reward terms with a nonzero scale (Cfg.reward_scales, :1380-1397) */
+#define GO1_MAX_SUMS (GO1_MAX_TERMS + 3) /* + total, total_pos, total_neg (:1400-1405) */
 #define GO1_NUM_PRIV 2
 #define GO1_LAG_SLOTS 7
-#define GO1_U_PER_ENV 308
+#define GO1_MAX_TRAJ 16    /* waypoints per trajectory (Cfg.commands.traj_length) */
+#define GO1_U_NOISE 47     /* parity-mode uniform slots: 0..46 reset / DR draws, then one per obs column
+                              (compute_observations noise, :472-473), then the trajectory draws */
 #define GO1_MODEL_FLOATS 175
 #define GO1_ACTUATOR_FLOATS 1313 /* w1[32][6] b1[32] w2[32][32] b2[32] w3[32] b3[1] */
 #define GO1_GRID_X 21
 #define GO1_GRID_Y 11
-#define GO1_EPISODE_LOG 16 /* 13 episode sums, episode length, reached, goal distance */
 #define GO1_AUX 32         /* base lin vel 3, base ang vel 3, commands 2, foot pos 12, torques 12 */
+/* Episode-log row (go1_step_args.episode_log): n_terms + 3 episode sums, episode length,
+ * reached, goal distance -> width n_terms + 6. */
+
+/* Reward functions of the two reward containers the trajectory env can select
+ * (Cfg.rewards.reward_container_name, :1373-1377): RewardsCrawling
+ * (go1_gym/envs/rewards/reward_crawling.py) and TrajectoryTrackingRewards
+ * (go1_gym/envs/rewards/trajectory_tracking_reward.py).  Functions with the same
+ * name and body in both share an id; go1_config.term_ids lists, in reward_scales
+ * order, the id of each nonzero-scaled term (GO1_T_NONE: the container has no such
+ * function -- the reference warns, skips it and keeps a zero episode sum, :1390-1395). */
+enum go1_term {
+  GO1_T_TORQUES = 0,      /* both containers */
+  GO1_T_DOF_ACC,
+  GO1_T_COLLISION,
+  GO1_T_ACTION_RATE,
+  GO1_T_DOF_POS_LIMITS,
+  GO1_T_ORIENTATION,
+  GO1_T_ANG_VEL_XY,
+  GO1_T_REACHING_Z,
+  GO1_T_REACHING_ROLL,
+  GO1_T_REACHING_PITCH,
+  GO1_T_EXPLORATION_LIN,  /* RewardsCrawling exploration_lin == TrajectoryTrackingRewards reaching_linear_vel */
+  GO1_T_EXPLORATION_YAW,  /* RewardsCrawling exploration_yaw == TrajectoryTrackingRewards reaching_yaw */
+  GO1_T_BASE_HEIGHT,      /* RewardsCrawling only */
+  GO1_T_LARGE_VEL,
+  GO1_T_E2E,
+  GO1_T_DOF_VEL,          /* TrajectoryTrackingRewards only */
+  GO1_T_DOF_POS,
+  GO1_T_TASK_OLD,
+  GO1_T_REACH_GOAL,
+  GO1_T_REACH_GOAL_T,     /* reach_goal_t: reached x episode length */
+  GO1_T_REACH_GOAL_TR,    /* reach_goal_T: reached x (episode length > T_reach) */
+  GO1_T_TASK,
+  GO1_T_EXPLORATION,
+  GO1_T_STALLING,
+  GO1_T_LINEAR_VEL,
+  GO1_T_LIN_VEL_Z,
+  GO1_T_FEET_AIR_TIME,
+  GO1_T_SURVIVE,
+  GO1_T_REACHING_YAW_ABS,
+  GO1_T_COUNT,
+  GO1_T_NONE = 31
+};
 
 enum {
   GO1_OK = 0,
@@ -71,7 +114,28 @@ typedef struct go1_config {
   int32_t rand_interval;       /* ceil(rand_interval_s / dt) (:1873) */
   int32_t hf_nx, hf_ny;        /* tile pixels: 80 x 40 for single_path */
   int32_t env_id_offset;       /* global id of local env 0 (rank * n_envs): keys the Philox streams */
-  int32_t pad1;
+  int32_t n_terms;             /* reward terms with a nonzero scale, <= GO1_MAX_TERMS */
+  int32_t term_ids[GO1_MAX_TERMS]; /* go1_term of reward slot k, in Cfg.reward_scales order */
+  uint32_t term_mask;          /* OR of (1 << id) over term_ids (the terms the kernel evaluates) */
+  int32_t reward_mode;         /* 0 plain sum, 1 only_positive_rewards (:341-342), 2 ji22 style (:343-344) */
+  int32_t lin_vel_form;        /* exploration_lin: 0 exp, 1 l1, 2 l2, 3 prod (reward_crawling.py:88-104) */
+  int32_t terminate_end_of_trajectory; /* (:211-213; e2e bonus reward_crawling.py:64-66) */
+  int32_t use_terminal_body_rotation;  /* (:215-216) */
+  int32_t rotate_camera;       /* camera pitch 0 in the height scan (:1934-1936) */
+  int32_t observe_heights;     /* (:388) */
+  int32_t timestep_in_obs;     /* episode_length / max_episode_length after the actions (:375-377) */
+  int32_t num_obs;             /* obs row width: 41 + timestep_in_obs + 2 x scanned points */
+  int32_t u_per_env;           /* parity-mode uniform row width: GO1_U_NOISE + num_obs + trajectory draws */
+  int32_t traj_kind;           /* 0 fixed_target, 1 random_target, 2 random_goal (trajectory_function.py) */
+  int32_t traj_length;         /* waypoints per env, <= GO1_MAX_TRAJ */
+  int32_t traj_interp;         /* num_interpolation (random_target) */
+  uint32_t indefinite_slots;   /* bit k: reward slot k has no fixed sign (exploration, feet_air_time, the prod
+                                  form of exploration_lin): its pos / neg bucket is the sign of the sum over
+                                  all envs (:332-335), applied by a second launch (go1_step) */
+  float sigma_rew_neg;         /* ji22 style */
+  float small_vel_threshold, large_dist_threshold;
+  float traj_x_range, traj_y_range, traj_z_range, traj_roll_range, traj_pitch_range, traj_yaw_range;
+  float traj_x_mean, traj_y_mean;
   float sim_dt;                /* 0.005 (config.py:355) */
   float dt;                    /* decimation * sim_dt */
   float action_scale;          /* 0.25 */
@@ -132,11 +196,13 @@ typedef struct go1_state {
   float* payload;          /* 1 */
   int32_t* episode_length; /* 1 */
   int32_t* curr_pose_index;/* 1 */
-  float* trajectory;       /* 6: x y z roll pitch yaw (traj_length = 1) */
+  float* trajectory;       /* 6 x traj_length: waypoints (x y z roll pitch yaw) */
   float* base_rotation;    /* 3: rpy from the previous step (:929) */
   int32_t* collision_count;/* 1 */
-  float* episode_sums;     /* 13 (layout.SUM_KEYS) */
+  float* episode_sums;     /* n_terms + 3: reward_scales order, then total, total_pos, total_neg */
   float* joint_pos_target; /* 12 */
+  float* feet_air_time;    /* 4 (feet_air_time reward, trajectory_tracking_reward.py:126-137) */
+  float* last_contacts;    /* 4, 0 / 1 */
 } go1_state;
 
 /* Terrain: unique tiles (n_tiles, 2, hf_nx, hf_ny) f32 [layer 0 ceiling, 1 floor],
@@ -155,16 +221,16 @@ typedef struct go1_step_args {
   const float* actions;        /* (n_envs, 12) */
   float gravity_vec[3];        /* normalized gravity used for projected_gravity (:134, :658) */
   float sim_gravity[3];        /* gravity applied by the integrator (:657-660) */
-  float reward_scales[GO1_NUM_TERMS]; /* already x dt, decayed (:1380-1385, :171-182) */
+  float reward_scales[GO1_MAX_TERMS]; /* slot order (term_ids), already x dt, decayed (:1380-1385, :171-182) */
   uint64_t rng_seed;
   uint64_t rng_step;           /* Philox counter: one value per call */
-  const float* uniforms;       /* parity mode: (n_envs, GO1_U_PER_ENV); NULL -> Philox */
+  const float* uniforms;       /* parity mode: (n_envs, u_per_env); NULL -> Philox */
   /* parity mode: injected post-physics state instead of the native integrator */
   const float* inj_dof;        /* (decimation, n_envs, 12, 2) pos, vel after each sim step */
   const float* inj_root;       /* (n_envs, 13) after the last sim step */
   const float* inj_contact;    /* (n_envs, 17, 3) net contact forces */
   /* outputs */
-  float* obs;                  /* (n_envs, 261) */
+  float* obs;                  /* (n_envs, num_obs) */
   float* priv;                 /* (n_envs, 2) */
   float* rew;                  /* (n_envs) */
   uint8_t* reset;              /* (n_envs) bool */
@@ -176,13 +242,14 @@ typedef struct go1_step_args {
   /* optional debug outputs (NULL = not written) */
   float* dbg_torques;          /* (decimation, n_envs, 12) */
   float* dbg_heights;          /* (n_envs, 2, 21, 11) measured heights before camera_zero */
-  float* dbg_terms;            /* (n_envs, 10) unscaled reward terms */
+  float* dbg_terms;            /* (n_envs, GO1_MAX_TERMS) unscaled reward terms, slot order */
   float* dbg_commands;         /* (n_envs, 2) */
   uint8_t* dbg_reached;        /* (n_envs) */
   /* optional host-facing outputs (NULL = not written) */
-  float* episode_log;          /* (n_envs, GO1_EPISODE_LOG): rows of envs reset this step hold the
-                                  reset_idx logging of extras["train/episode"] (:256-271); every
-                                  other row gets only column 13 (episode length) = 0 */
+  float* episode_log;          /* (n_envs, n_terms + 6): rows of envs reset this step hold the
+                                  reset_idx logging of extras["train/episode"] (:256-271): the n_terms + 3
+                                  episode sums, episode length, reached, goal distance; every other row
+                                  gets only its episode-length column (n_terms + 3) = 0 */
   float* aux;                  /* (n_envs, GO1_AUX): base_lin_vel, base_ang_vel, commands (post-reset),
                                   foot positions (world), torques of the last sim step: the
                                   TrajectoryTrackingEnv.step extras (trajectory_tracking/__init__.py:25-41) */
@@ -191,7 +258,7 @@ typedef struct go1_step_args {
   void* ev_end;
   /* optional second copy of obs (NULL = not written): HistoryWrapper's obs_history for a history
      length of 1 (history_wrapper.py:18-24 builds it as a copy of obs every step) */
-  float* obs_history;          /* (n_envs, 261) */
+  float* obs_history;          /* (n_envs, num_obs) */
 } go1_step_args;
 
 typedef struct go1_handle go1_handle;

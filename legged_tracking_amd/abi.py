@@ -5,20 +5,35 @@ checks sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
+GO1_ABI_VERSION = 3
 GO1_NUM_DOF = 12
 GO1_NUM_BODIES = 17
-GO1_NUM_TERMS = 10
-GO1_NUM_SUMS = 13
-GO1_NUM_OBS = 261
+GO1_MAX_TERMS = 16
+GO1_MAX_SUMS = GO1_MAX_TERMS + 3
 GO1_NUM_PRIV = 2
 GO1_LAG_SLOTS = 7
-GO1_U_PER_ENV = 308
+GO1_MAX_TRAJ = 16
+GO1_U_NOISE = 47
 GO1_MODEL_FLOATS = 175
 GO1_ACTUATOR_FLOATS = 1313
 GO1_GRID_X = 21
 GO1_GRID_Y = 11
-GO1_EPISODE_LOG = 16
 GO1_AUX = 32
+
+# enum go1_term (include/go1_mi355x.h)
+TERM_IDS = {name: i for i, name in enumerate((
+    "torques", "dof_acc", "collision", "action_rate", "dof_pos_limits", "orientation", "ang_vel_xy",
+    "reaching_z", "reaching_roll", "reaching_pitch", "exploration_lin", "exploration_yaw", "base_height",
+    "large_vel", "e2e", "dof_vel", "dof_pos", "task_old", "reach_goal", "reach_goal_t", "reach_goal_T", "task",
+    "exploration", "stalling", "linear_vel", "lin_vel_z", "feet_air_time", "survive", "reaching_yaw_abs"))}
+GO1_T_COUNT = len(TERM_IDS)
+GO1_T_NONE = 31
+
+
+def episode_log_width(n_terms):
+    """go1_step_args.episode_log row: n_terms + 3 sums, episode length, reached, goal distance."""
+    return n_terms + 6
+
 
 F = C.c_float
 I32 = C.c_int32
@@ -29,7 +44,15 @@ class Go1Config(C.Structure):
     _fields_ = [
         ("n_envs", I32), ("terrain_kind", I32), ("camera_zero", I32), ("measure_front_half", I32),
         ("add_noise", I32), ("use_terminal_body_height", I32), ("custom_origins", I32), ("decimation", I32),
-        ("n_internal", I32), ("rand_interval", I32), ("hf_nx", I32), ("hf_ny", I32), ("env_id_offset", I32), ("pad1", I32),
+        ("n_internal", I32), ("rand_interval", I32), ("hf_nx", I32), ("hf_ny", I32), ("env_id_offset", I32),
+        ("n_terms", I32), ("term_ids", I32 * GO1_MAX_TERMS), ("term_mask", C.c_uint32), ("reward_mode", I32),
+        ("lin_vel_form", I32), ("terminate_end_of_trajectory", I32), ("use_terminal_body_rotation", I32),
+        ("rotate_camera", I32), ("observe_heights", I32), ("timestep_in_obs", I32), ("num_obs", I32),
+        ("u_per_env", I32), ("traj_kind", I32), ("traj_length", I32), ("traj_interp", I32),
+        ("indefinite_slots", C.c_uint32),
+        ("sigma_rew_neg", F), ("small_vel_threshold", F), ("large_dist_threshold", F),
+        ("traj_x_range", F), ("traj_y_range", F), ("traj_z_range", F), ("traj_roll_range", F),
+        ("traj_pitch_range", F), ("traj_yaw_range", F), ("traj_x_mean", F), ("traj_y_mean", F),
         ("sim_dt", F), ("dt", F), ("action_scale", F), ("hip_scale_reduction", F), ("clip_actions", F),
         ("clip_obs", F), ("horizontal_scale", F), ("max_episode_length", F), ("terminal_body_height", F),
         ("switch_dist", F), ("base_height_target", F), ("tracking_sigma_lin", F), ("tracking_sigma_ang", F),
@@ -59,7 +82,7 @@ class Go1State(C.Structure):
         "root", "dof_pos", "dof_vel", "last_actions", "last_dof_vel", "lag", "pos_err_hist", "vel_hist",
         "motor_strength", "motor_offset", "friction", "restitution", "payload", "episode_length",
         "curr_pose_index", "trajectory", "base_rotation", "collision_count", "episode_sums",
-        "joint_pos_target")]
+        "joint_pos_target", "feet_air_time", "last_contacts")]
 
 
 class Go1Terrain(C.Structure):
@@ -69,7 +92,7 @@ class Go1Terrain(C.Structure):
 
 class Go1StepArgs(C.Structure):
     _fields_ = [
-        ("actions", P), ("gravity_vec", F * 3), ("sim_gravity", F * 3), ("reward_scales", F * GO1_NUM_TERMS),
+        ("actions", P), ("gravity_vec", F * 3), ("sim_gravity", F * 3), ("reward_scales", F * GO1_MAX_TERMS),
         ("rng_seed", C.c_uint64), ("rng_step", C.c_uint64), ("uniforms", P),
         ("inj_dof", P), ("inj_root", P), ("inj_contact", P),
         ("obs", P), ("priv", P), ("rew", P), ("reset", P), ("time_out", P), ("extras_time_outs", P),
@@ -79,16 +102,25 @@ class Go1StepArgs(C.Structure):
     ]
 
 
-# state field widths and dtypes (must match go1_state order)
+# state field widths and dtypes (must match go1_state order); None = set by the config:
+# trajectory 6 x traj_length, episode_sums n_terms + 3
 STATE_SPEC = (
     ("root", 13, "f32"), ("dof_pos", 12, "f32"), ("dof_vel", 12, "f32"), ("last_actions", 12, "f32"),
     ("last_dof_vel", 12, "f32"), ("lag", 84, "f32"), ("pos_err_hist", 24, "f32"), ("vel_hist", 24, "f32"),
     ("motor_strength", 12, "f32"), ("motor_offset", 12, "f32"), ("friction", 1, "f32"),
     ("restitution", 1, "f32"), ("payload", 1, "f32"), ("episode_length", 1, "i32"),
-    ("curr_pose_index", 1, "i32"), ("trajectory", 6, "f32"), ("base_rotation", 3, "f32"),
-    ("collision_count", 1, "i32"), ("episode_sums", GO1_NUM_SUMS, "f32"), ("joint_pos_target", 12, "f32"),
+    ("curr_pose_index", 1, "i32"), ("trajectory", None, "f32"), ("base_rotation", 3, "f32"),
+    ("collision_count", 1, "i32"), ("episode_sums", None, "f32"), ("joint_pos_target", 12, "f32"),
+    ("feet_air_time", 4, "f32"), ("last_contacts", 4, "f32"),
 )
 assert tuple(n for n, _, _ in STATE_SPEC) == tuple(n for n, _ in Go1State._fields_)
+
+
+def state_spec(cfg):
+    """[(name, width, dtype)] of the state planes for a go1_config (or anything with n_terms and
+    traj_length attributes)."""
+    w = {"trajectory": 6 * int(cfg.traj_length), "episode_sums": int(cfg.n_terms) + 3}
+    return [(n, w.get(n, wd), dt) for n, wd, dt in STATE_SPEC]
 
 
 def ptr(a):

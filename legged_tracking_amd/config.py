@@ -403,65 +403,126 @@ def config_go1(Cnfg):
     _.rand_interval_s = 6
 
 
-def readme_config(n_envs=4096, terrain="single_path", rows=32, cols=32, camera_zero=None, domain_rand=True):
-    """Cfg as scripts/train.py:46-241 builds it for the README command
-    (--terrain single_path --measure_front_half --camera_zero --old_ppo
-    --penalty_scaler 1.0 --strategy e2e --terminal_body_height 0.0), with
-    num_envs / terrain grid overridable (train.py:128-130 hard-codes 1024/32/32)."""
+TRAIN_FLAGS = (
+    # scripts/train.py:296-338: (flag, argparse kwargs) -- the env / reward flags train_go1 reads
+    ("--strategy", dict(default="vel", choices=["e2e", "pms", "vel"])),
+    ("--exploration_steps", dict(type=int, default=2500)),
+    ("--command_type", dict(default="xy", choices=["xy", "6dof", "xy_norm"])),
+    ("--timestep_in_obs", dict(action="store_true")),
+    ("--num_history", dict(type=int, default=1)),
+    ("--measure_front_half", dict(action="store_true")),
+    ("--rotate_camera", dict(action="store_true")),
+    ("--camera_zero", dict(action="store_true")),
+    ("--blind", dict(action="store_true")),
+    ("--terminal_body_height", dict(type=float, default=0.0)),
+    ("--terrain", dict(default="single_path", choices=["single_path", "multi_path", "plane"])),
+    ("--no_domain_rand", dict(action="store_true")),
+    ("--empty_tunnel", dict(action="store_true")),
+    ("--random_target", dict(action="store_true")),
+    ("--terminate_after_reach", dict(action="store_true")),
+    ("--tunnel_width", dict(type=float, default=2.0)),
+    ("--lin_vel_form", dict(default="exp", choices=["l1", "l2", "exp", "prod"])),
+    ("--r_explore_lin", dict(type=float, default=1.0)),
+    ("--r_explore_yaw", dict(type=float, default=0.4)),
+    ("--penalty_scaler", dict(type=float, default=1.0)),
+    ("--only_positive", dict(action="store_true")),
+    ("--r_orientation", dict(type=float, default=0.0)),
+    ("--r_base_height", dict(type=float, default=20.0)),
+    ("--r_ang_vel", dict(type=float, default=0.001)),
+    ("--t_reach", dict(type=int, default=0)),
+    ("--r_task", dict(type=float, default=1.0)),
+    ("--r_collision", dict(type=float, default=5.0)),
+    ("--r_large_vel", dict(type=float, default=0.0)),
+)
+README_ARGV = ("--terrain", "single_path", "--measure_front_half", "--camera_zero", "--penalty_scaler", "1.0",
+               "--strategy", "e2e", "--terminal_body_height", "0.0")
+
+
+def parse_train_flags(argv=()):
+    import argparse
+    p = argparse.ArgumentParser(add_help=False)
+    for flag, kw in TRAIN_FLAGS:
+        p.add_argument(flag, **kw)
+    args, _ = p.parse_known_args(list(argv))
+    return args
+
+
+def train_config(argv=(), n_envs=None, rows=None, cols=None):
+    """Cfg exactly as scripts/train.py:train_go1 (:46-241) builds it for the command-line flags
+    `argv` (same flag names and defaults, train.py:296-338); num_envs / terrain grid overridable
+    (train.py:128-130 hard-codes 1024 / 32 / 32).  Attribute assignments keep the reference's
+    order: the reward_scales dict order (the reward summation order, :1380-1397) follows it."""
+    args = parse_train_flags(argv)
     C = make_cfg()
     config_go1(C)
-    if camera_zero is None:
-        camera_zero = terrain != "plane"  # plane + camera_zero crashes in the reference (:402)
     C.env.observe_heights = True
-    C.env.command_type = "xy"
-    C.env.num_observations = 261
-    C.env.num_scalar_observations = 261
+    command_type = args.command_type
+    C.env.command_type = command_type
+    if command_type in ("xy", "xy_norm"):
+        C.env.num_observations = 261 if args.measure_front_half else 503
+    else:
+        C.env.num_observations = 265 if args.measure_front_half else 507
+    C.env.num_observations += int(args.timestep_in_obs)
+    C.env.num_scalar_observations = C.env.num_observations
     C.env.num_privileged_obs = 2
-    C.env.num_observation_history = 1
+    C.terrain.measured_points_x = np.linspace(-1, 1, 21)
+    C.terrain.measured_points_y = np.linspace(-0.5, 0.5, 11)
+    C.env.num_observation_history = args.num_history
     C.env.look_from_back = True
-    C.env.terminate_end_of_trajectory = False
+    C.env.viewer_look_at_robot = False
+    C.env.terminate_end_of_trajectory = args.terminate_after_reach
     C.env.record_all_envs = False
     C.env.episode_length_s = 20
-    C.env.rotate_camera = False
-    C.env.camera_zero = camera_zero
-    C.env.timestep_in_obs = False
-    C.terrain.measure_front_half = True
+    C.env.rotate_camera = args.rotate_camera
+    C.env.camera_zero = args.camera_zero
+    C.env.timestep_in_obs = args.timestep_in_obs
+    C.terrain.measure_front_half = args.measure_front_half
     C.asset.penalize_contacts_on = ["thigh", "calf", "base"]
     C.asset.terminate_after_contacts_on = []
     C.rewards.small_vel_threshold = 0.1
     C.rewards.lin_reaching_criterion = 0.3
     C.rewards.ang_reaching_criterion = np.pi / 20.0
-    C.rewards.only_positive_rewards = False
+    C.rewards.only_positive_rewards = args.only_positive
     C.rewards.use_terminal_body_height = True
-    C.rewards.terminal_body_height = 0.0
-    C.rewards.lin_vel_form = "exp"
+    C.rewards.terminal_body_height = args.terminal_body_height
+    C.rewards.lin_vel_form = args.lin_vel_form
+    C.rewards.exploration_steps = +np.inf
     C.rewards.tracking_sigma_lin = 0.05
     C.rewards.base_height_target = 0.28
     C.rewards.target_lin_vel = 0.25
-    p = 1.0
+    p = args.penalty_scaler
     C.reward_scales.dof_acc = -2.5e-7 * p
     C.reward_scales.torques = -1e-5 * p
     C.reward_scales.action_rate = -1e-3 * p
     C.reward_scales.dof_pos_limits = -10.0 * p
-    C.reward_scales.collision = -5.0 * p
-    C.reward_scales.base_height = -20.0 * p
-    C.reward_scales.orientation = -0.0 * p
-    C.reward_scales.ang_vel_xy = -0.001 * p
-    C.reward_scales.large_vel = -0.0 * p
+    C.reward_scales.collision = -args.r_collision * p
+    C.reward_scales.base_height = -args.r_base_height * p
+    C.reward_scales.orientation = -args.r_orientation * p
+    C.reward_scales.ang_vel_xy = -args.r_ang_vel * p
+    C.reward_scales.large_vel = -args.r_large_vel * p
     C.reward_scales.reaching_z = 0.0
     C.reward_scales.reaching_roll = 0.0
     C.reward_scales.reaching_pitch = 0.0
-    C.reward_scales.e2e = 1.0
-    C.rewards.T_reach = 0
-    C.rewards.exploration_steps = 2500
-    C.reward_scales.exploration_lin = 1.0
-    C.reward_scales.exploration_yaw = 0.4
-    C.env.num_envs = n_envs
-    C.terrain.num_cols = cols
-    C.terrain.num_rows = rows
-    if terrain == "plane":
+    if args.strategy == "vel":
+        C.reward_scales.e2e = 0
+        C.rewards.T_reach = args.t_reach
+        C.rewards.exploration_steps = 200000
+    if args.strategy == "e2e":
+        C.reward_scales.e2e = args.r_task
+        C.rewards.T_reach = args.t_reach
+        C.rewards.exploration_steps = args.exploration_steps
+    elif args.strategy == "pms":
+        C.reward_scales.reaching_z = 0.0
+        C.reward_scales.reaching_roll = 0.0
+        C.reward_scales.reaching_pitch = 0.0
+    C.reward_scales.exploration_lin = args.r_explore_lin
+    C.reward_scales.exploration_yaw = args.r_explore_yaw
+    C.env.num_envs = 1024
+    C.terrain.num_cols = 32
+    C.terrain.num_rows = 32
+    if args.terrain == "plane":
         C.terrain.mesh_type = 'plane'
-    elif terrain == "single_path":
+    elif args.terrain == "single_path":
         C.terrain.terrain_type = "single_path"
         C.terrain.terrain_length = 4.0
         C.terrain.terrain_width = 2.0
@@ -469,51 +530,118 @@ def readme_config(n_envs=4096, terrain="single_path", rows=32, cols=32, camera_z
         C.terrain.terrain_ratio_y = 0.5
         C.terrain.ceiling_height = 0.8
         C.terrain.start_loc = 0.32
-        C.terrain.p_flat = 0.9
+        C.terrain.p_flat = 0.0 if args.empty_tunnel else 0.9
         C.terrain.p_double = 0.6
         C.env.episode_length_s = 10.0
         C.commands.sampling_based_planning = False
+    elif args.terrain == "multi_path":
+        C.terrain.terrain_type = "multi_path"
+        C.terrain.terrain_length = 3.0
+        C.terrain.terrain_width = args.tunnel_width
+        C.terrain.terrain_ratio_x = 0.9
+        C.terrain.terrain_ratio_y = 0.25
+        C.terrain.ceiling_height = 0.8
+        C.env.episode_length_s = 8.0
+        C.terrain.start_loc = 0.4
+        C.commands.sampling_based_planning = True
+        C.commands.plan_interval = 100
+    if args.random_target:
+        C.commands.traj_function = "random_target"
+        C.commands.traj_length = 10
+        C.commands.num_interpolation = 1
+        C.commands.sampling_based_planning = False
     else:
-        raise ValueError(f"terrain {terrain!r}: only plane and single_path are on this path")
-    C.commands.traj_function = "fixed_target"
-    C.commands.traj_length = 1
-    C.commands.num_interpolation = 1
-    C.commands.switch_dist = 0.3
-    C.commands.base_x = C.terrain.terrain_length * C.terrain.terrain_ratio_x - 1.0
+        C.commands.traj_function = "fixed_target"
+        C.commands.traj_length = 1
+        C.commands.num_interpolation = 1
+        C.commands.switch_dist = 0.3
+        C.commands.base_x = C.terrain.terrain_length * C.terrain.terrain_ratio_x - 1.0
+    if args.blind:
+        C.env.observe_heights = False
+        C.env.measure_front_half = False  # sets Cfg.env, not Cfg.terrain: no effect (train.py:187)
+        if command_type in ("xy", "xy_norm"):
+            C.env.num_observations = 45 + int(args.timestep_in_obs) - 4
+            C.env.num_scalar_observations = 45 + int(args.timestep_in_obs) - 4
+        else:
+            C.env.num_observations = 45 + int(args.timestep_in_obs) + 2 + 4
+            C.env.num_scalar_observations = 45 + int(args.timestep_in_obs) + 2 + 4
+    enable_random = not args.no_domain_rand
     C.domain_rand.lag_timesteps = 6
     C.domain_rand.randomize_lag_timesteps = True
     C.control.control_type = "actuator_net"
     C.domain_rand.randomize_rigids_after_start = False
-    C.domain_rand.randomize_friction = domain_rand
+    C.env.priv_observe_motion = False
+    C.env.priv_observe_gravity_transformed_motion = False
+    C.domain_rand.randomize_friction_indep = False
+    C.env.priv_observe_friction_indep = False
+    C.domain_rand.randomize_friction = enable_random
     C.env.priv_observe_friction = True
     C.domain_rand.friction_range = [0.1, 3.0]
-    C.domain_rand.randomize_restitution = domain_rand
+    C.domain_rand.randomize_restitution = enable_random
     C.env.priv_observe_restitution = True
     C.domain_rand.restitution_range = [0.0, 0.4]
-    C.domain_rand.randomize_base_mass = domain_rand
+    C.domain_rand.randomize_base_mass = enable_random
     C.env.priv_observe_base_mass = False
     C.domain_rand.added_mass_range = [-1.0, 3.0]
-    C.domain_rand.randomize_gravity = domain_rand
+    C.domain_rand.randomize_gravity = enable_random
     C.domain_rand.gravity_range = [-1.0, 1.0]
     C.domain_rand.gravity_rand_interval_s = 8.0
     C.domain_rand.gravity_impulse_duration = 0.99
     C.env.priv_observe_gravity = False
     C.domain_rand.randomize_com_displacement = False
+    C.domain_rand.com_displacement_range = [-0.15, 0.15]
     C.env.priv_observe_com_displacement = False
-    C.domain_rand.randomize_motor_strength = domain_rand
+    C.domain_rand.randomize_ground_friction = enable_random
+    C.env.priv_observe_ground_friction = False
+    C.env.priv_observe_ground_friction_per_foot = False
+    C.domain_rand.ground_friction_range = [0.0, 0.0]
+    C.domain_rand.randomize_motor_strength = enable_random
     C.domain_rand.motor_strength_range = [0.9, 1.1]
-    C.domain_rand.randomize_motor_offset = domain_rand
-    C.domain_rand.motor_offset_range = [-0.02, 0.02]
-    C.domain_rand.push_robots = False
     C.env.priv_observe_motor_strength = False
+    C.domain_rand.randomize_motor_offset = enable_random
+    C.domain_rand.motor_offset_range = [-0.02, 0.02]
     C.env.priv_observe_motor_offset = False
+    C.domain_rand.push_robots = False
+    C.domain_rand.randomize_Kp_factor = False
+    C.env.priv_observe_Kp_factor = False
+    C.domain_rand.randomize_Kd_factor = False
+    C.env.priv_observe_Kd_factor = False
     C.env.priv_observe_body_velocity = False
     C.env.priv_observe_body_height = False
     C.env.priv_observe_desired_contact_states = False
+    C.env.priv_observe_contact_forces = False
+    C.env.priv_observe_foot_displacement = False
+    C.env.priv_observe_gravity_transformed_foot_displacement = False
     C.normalization.friction_range = [0, 1]
     C.normalization.ground_friction_range = [0, 1]
     C.normalization.clip_actions = 10.0
+    if n_envs is not None:
+        C.env.num_envs = n_envs
+    if rows is not None:
+        C.terrain.num_rows = rows
+    if cols is not None:
+        C.terrain.num_cols = cols
     return C
+
+
+def readme_config(n_envs=4096, terrain="single_path", rows=32, cols=32, camera_zero=None, domain_rand=True,
+                  extra_argv=()):
+    """Cfg as scripts/train.py:46-241 builds it for the README command
+    (--terrain single_path --measure_front_half --camera_zero --old_ppo
+    --penalty_scaler 1.0 --strategy e2e --terminal_body_height 0.0), with
+    num_envs / terrain grid overridable (train.py:128-130 hard-codes 1024/32/32).
+    `extra_argv` appends further train.py flags (variants)."""
+    if terrain not in ("plane", "single_path"):
+        raise ValueError(f"terrain {terrain!r}: only plane and single_path are on this path")
+    if camera_zero is None:
+        camera_zero = terrain != "plane"  # plane + camera_zero crashes in the reference (:402)
+    argv = ["--terrain", terrain, "--measure_front_half", "--penalty_scaler", "1.0", "--strategy", "e2e",
+            "--terminal_body_height", "0.0"]
+    if camera_zero:
+        argv.append("--camera_zero")
+    if not domain_rand:
+        argv.append("--no_domain_rand")
+    return train_config(argv + list(extra_argv), n_envs=n_envs, rows=rows, cols=cols)
 
 
 # ------------------------------------------------------------------ derived values
@@ -568,15 +696,18 @@ def _get(cfg, path, default=None):
 # NotImplementedError instead of silently training on different rewards / targets / observations.
 #   path -> (allowed values, reference line the value selects)
 SUPPORTED = {
-    "rewards.only_positive_rewards": ((False,), "legged_robot_trajectory_tracking.py:341-342"),
-    "rewards.only_positive_rewards_ji22_style": ((False,), ":343-344"),
-    "rewards.lin_vel_form": (("exp",), "reward_crawling.py:88-104"),
-    "rewards.reward_container_name": (("RewardsCrawling",), ":1373-1377"),
-    "env.terminate_end_of_trajectory": ((False,), ":211-213, reward_crawling.py:64-66"),
-    "env.use_terminal_body_rotation": ((False,), ":215-216"),
-    "env.rotate_camera": ((False,), ":1934-1936"),
-    "env.timestep_in_obs": ((False,), ":375-377"),
-    "env.observe_heights": ((True,), ":388-423"),
+    "rewards.only_positive_rewards": ((False, True), "legged_robot_trajectory_tracking.py:341-342"),
+    "rewards.only_positive_rewards_ji22_style": ((False, True), ":343-344"),
+    "rewards.lin_vel_form": (("exp", "l1", "l2", "prod"), "reward_crawling.py:88-104"),
+    "rewards.reward_container_name": (("RewardsCrawling", "TrajectoryTrackingRewards"), ":1373-1377"),
+    "env.terminate_end_of_trajectory": ((False, True), ":211-213, reward_crawling.py:64-66"),
+    "env.use_terminal_body_rotation": ((False, True), ":215-216"),
+    "env.rotate_camera": ((False, True), ":1934-1936"),
+    "env.timestep_in_obs": ((False, True), ":375-377"),
+    "env.observe_heights": ((True, False), ":388-423"),
+    # "6dof" fails in the reference itself: commands (n, 6) * commands_scale, while command_xy_only
+    # (config.py:70, True) sizes the noise vector for 2 commands (:1109); "xy_norm" normalises by
+    # the norm over ALL envs' commands (:803-807), a grid-wide reduction this step does not do
     "env.command_type": (("xy",), ":801-816"),
     "env.observe_command": ((True,), ":367-377"),
     "env.observe_vel": ((False,), ":445-453"),
@@ -587,9 +718,9 @@ SUPPORTED = {
     "env.observe_two_prev_actions": ((False,), ":425-427"),
     "env.observe_timing_parameter": ((False,), ":429-431"),
     "env.observe_clock_inputs": ((False,), ":433-435"),
-    "terrain.measure_front_half": ((True,), ":395-399"),
-    "commands.traj_function": (("fixed_target",), "trajectory_function.py:14-93"),
-    "commands.traj_length": ((1,), "trajectory_function.py:14-26"),
+    "terrain.measure_front_half": ((True, False), ":395-399"),
+    "commands.traj_function": (("fixed_target", "random_target", "random_goal"), "trajectory_function.py:14-93"),
+    "commands.traj_length": (tuple(range(1, 17)), "trajectory_function.py:14-93 (<= GO1_MAX_TRAJ)"),
     "commands.sampling_based_planning": ((False,), ":850-921 (OMPL planner)"),
     "commands.switch_upon_reach": ((True,), ":836-839"),
     "control.control_type": (("actuator_net",), ":957-996"),
@@ -600,6 +731,83 @@ SUPPORTED = {
     "domain_rand.randomize_rigids_after_start": ((False,), ":226-228"),
     "curriculum_thresholds.cl_fix_target": ((False,), ":188-196"),
 }
+
+# reward functions of each container (reward_crawling.py:18-123, trajectory_tracking_reward.py:17-171):
+# reward_scales name -> go1_term name (abi.TERM_IDS)
+_RC = ("torques", "dof_acc", "dof_pos_limits", "collision", "action_rate", "base_height", "ang_vel_xy",
+       "orientation", "large_vel", "e2e", "exploration_lin", "exploration_yaw", "reaching_z", "reaching_roll",
+       "reaching_pitch")
+_TT = ("torques", "dof_vel", "dof_acc", "dof_pos", "collision", "action_rate", "dof_pos_limits", "orientation",
+       "task_old", "reach_goal", "reach_goal_t", "reach_goal_T", "task", "exploration", "stalling", "linear_vel",
+       "lin_vel_z", "ang_vel_xy", "feet_air_time", "survive", "reaching_z", "reaching_roll", "reaching_pitch",
+       "reaching_yaw_abs")
+CONTAINERS = {
+    "RewardsCrawling": {k: k for k in _RC},
+    "TrajectoryTrackingRewards": dict({k: k for k in _TT}, reaching_linear_vel="exploration_lin",
+                                      reaching_yaw="exploration_yaw"),
+}
+# TrajectoryTrackingRewards._reward_reaching_local_goal reads env.replan, which exists only with the
+# sampling-based planner (:861); that planner is not on this path
+_NOT_ON_PATH = {"reaching_local_goal": ":861 (needs the OMPL planner's replan flag)"}
+
+
+def reward_slots(cfg, scales=None):
+    """(names, term ids, indefinite-slot mask) of the reward slots in Cfg.reward_scales order
+    (nonzero scales, :1380-1397).  A name the container has no function for gets GO1_T_NONE (the
+    reference prints a warning, skips it and keeps a zero episode sum, :1390-1395)."""
+    scales = derived(cfg)["reward_scales"] if scales is None else scales
+    cname = _get(cfg, "rewards.reward_container_name", "RewardsCrawling")
+    if cname not in CONTAINERS:
+        raise NotImplementedError(f"reward container {cname!r} is not on the accelerated path")
+    cont = CONTAINERS[cname]
+    form = _get(cfg, "rewards.lin_vel_form", "exp")
+    names, ids, indef = [], [], 0
+    for name in scales:
+        if name == "termination":
+            # both containers lack _reward_termination: the reference raises AttributeError (:349-350)
+            raise AttributeError(f"'{cname}' object has no attribute '_reward_termination'")
+        if name in _NOT_ON_PATH and cname == "TrajectoryTrackingRewards":
+            raise NotImplementedError(f"reward term {name!r}: {_NOT_ON_PATH[name]}")
+        term = cont.get(name)
+        if term is None:
+            print(f"Warning: reward _reward_{name} has nonzero coefficient but was not found!")
+            ids.append(abi.GO1_T_NONE)
+        else:
+            if term == "exploration_lin" and form == "prod" and cname != "RewardsCrawling":
+                # TrajectoryTrackingRewards._reward_reaching_linear_vel has no "prod" branch: it returns None
+                raise TypeError("unsupported operand type(s) for *: 'NoneType' and 'float' "
+                                "(trajectory_tracking_reward.py:143-155 has no 'prod' form)")
+            if term in ("exploration", "feet_air_time") or (term == "exploration_lin" and form == "prod"):
+                indef |= 1 << len(names)
+            ids.append(abi.TERM_IDS[term])
+        names.append(name)
+    if len(names) > abi.GO1_MAX_TERMS:
+        raise NotImplementedError(f"{len(names)} nonzero reward scales; the step supports {abi.GO1_MAX_TERMS}")
+    return names, ids, indef
+
+
+def obs_layout(cfg):
+    """Observation row of compute_observations (:357-475) for the supported flags:
+    gravity 3, commands 2, dof pos 12, dof vel 12, actions 12, [timestep 1], [heights 2 x points]."""
+    ts = int(bool(_get(cfg, "env.timestep_in_obs", False)))
+    heights = bool(_get(cfg, "env.observe_heights", True))
+    rows = GO1_GRID_ROWS_FRONT if _get(cfg, "terrain.measure_front_half", True) else 21
+    n_pts = rows * 11
+    width = 41 + ts + (2 * n_pts if heights else 0)
+    return {"timestep": ts, "heights": heights, "n_points": n_pts, "height_offset": 41 + ts, "width": width}
+
+
+GO1_GRID_ROWS_FRONT = 10  # x rows 11..20 of the 21-row grid (:395-399)
+
+
+def traj_draws(cfg):
+    """Uniform draws per reset of the trajectory function (trajectory_function.py:14-93)."""
+    kind = _get(cfg, "commands.traj_function", "fixed_target")
+    if kind == "random_target":
+        return 6 * (int(cfg.commands.traj_length) // int(cfg.commands.num_interpolation) + 1)
+    if kind == "random_goal":
+        return 3
+    return 0
 
 
 def unsupported(cfg):
@@ -641,6 +849,47 @@ def build_abi_config(cfg, n_envs=None, physics=None, actuator=None, hf_shape=(80
         raise AttributeError("'LeggedRobot' object has no attribute 'camera_pitch_angle' "
                              "(plane terrain + camera_zero fails in the reference, :402)")
     c.measure_front_half = int(bool(cfg.terrain.measure_front_half))
+    ol = obs_layout(cfg)
+    if int(cfg.env.num_observations) != ol["width"]:
+        # compute_observations asserts the width (:475)
+        raise AssertionError(f"Observation shape ({n}, {ol['width']}) does not match num_observations "
+                             f"{cfg.env.num_observations}")
+    c.num_obs = ol["width"]
+    c.observe_heights = int(ol["heights"])
+    c.timestep_in_obs = ol["timestep"]
+    c.rotate_camera = int(bool(_get(cfg, "env.rotate_camera", False)))
+    c.terminate_end_of_trajectory = int(bool(_get(cfg, "env.terminate_end_of_trajectory", False)))
+    c.use_terminal_body_rotation = int(bool(_get(cfg, "env.use_terminal_body_rotation", False)))
+    names, ids, indef = reward_slots(cfg, d["reward_scales"])
+    c.n_terms = len(names)
+    for k, t in enumerate(ids):
+        c.term_ids[k] = t
+    for k in range(len(names), abi.GO1_MAX_TERMS):
+        c.term_ids[k] = abi.GO1_T_NONE
+    c.term_mask = sum(1 << t for t in set(ids) if t != abi.GO1_T_NONE)
+    c.indefinite_slots = indef
+    rw = cfg.rewards
+    c.reward_mode = 1 if rw.only_positive_rewards else (2 if _get(cfg, "rewards.only_positive_rewards_ji22_style",
+                                                                   False) else 0)
+    c.sigma_rew_neg = f32(_get(cfg, "rewards.sigma_rew_neg", 5))
+    c.lin_vel_form = ("exp", "l1", "l2", "prod").index(_get(cfg, "rewards.lin_vel_form", "exp"))
+    used = {t for t in ids}
+    need_small = (c.lin_vel_form == 3 and abi.TERM_IDS["exploration_lin"] in used) or \
+        abi.TERM_IDS["exploration"] in used or abi.TERM_IDS["stalling"] in used
+    need_large = abi.TERM_IDS["task"] in used or abi.TERM_IDS["stalling"] in used
+    for attr, need in (("small_vel_threshold", need_small), ("large_dist_threshold", need_large)):
+        if need and not hasattr(rw, attr):
+            raise AttributeError(f"type object 'rewards' has no attribute '{attr}'")
+        setattr(c, attr, f32(getattr(rw, attr, 0.0)))
+    cm = cfg.commands
+    c.traj_kind = ("fixed_target", "random_target", "random_goal").index(cm.traj_function)
+    c.traj_length = int(cm.traj_length)
+    c.traj_interp = int(getattr(cm, "num_interpolation", 1))
+    if c.traj_kind == 1 and c.traj_length % c.traj_interp != 0:
+        raise AssertionError("traj_length % num_interpolation != 0 (trajectory_function.py:73)")
+    for k in ("x_range", "y_range", "z_range", "roll_range", "pitch_range", "yaw_range", "x_mean", "y_mean"):
+        setattr(c, "traj_" + k, f32(getattr(cm, k, 0.0)))
+    c.u_per_env = abi.GO1_U_NOISE + c.num_obs + traj_draws(cfg)
     c.add_noise = int(bool(cfg.noise.add_noise))
     c.use_terminal_body_height = int(bool(cfg.rewards.use_terminal_body_height))
     c.custom_origins = 0 if plane else 1
@@ -741,9 +990,14 @@ def load_actuator():
     return flat.astype(np.float32)
 
 
-def reward_scale_vector(scales: dict):
-    """f32 vector in layout.REWARD_KEYS order."""
-    return np.array([np.float32(scales.get(k, 0.0)) for k in L.REWARD_KEYS], np.float32)
+def reward_scale_vector(scales: dict, names=None):
+    """f32 vector of GO1_MAX_TERMS reward scales in slot order (the order of `names`, default the
+    order of `scales`: Cfg.reward_scales order), zero-padded."""
+    names = list(scales) if names is None else list(names)
+    v = np.zeros(abi.GO1_MAX_TERMS, np.float32)
+    for k, name in enumerate(names):
+        v[k] = np.float32(scales.get(name, 0.0))
+    return v
 
 
 def _fmaf(a, b, c):

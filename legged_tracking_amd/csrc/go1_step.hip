@@ -124,8 +124,9 @@ struct Rng {
   uint64_t seed, step;
   int e;    // local env index (parity-mode uniforms)
   int gid;  // global env id (Philox counter): local index + go1_config.env_id_offset
+  int ustride;  // parity-mode uniform row width (go1_config.u_per_env)
   __device__ float operator()(int slot) const {
-    if (U) return U[(size_t)e * GO1_U_PER_ENV + slot];
+    if (U) return U[(size_t)e * ustride + slot];
     uint32_t c[4] = {(uint32_t)gid, (uint32_t)slot >> 2, (uint32_t)step, (uint32_t)(step >> 32)};
     philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     return (float)(c[slot & 3] >> 8) * (1.0f / 16777216.0f);
@@ -134,7 +135,7 @@ struct Rng {
   __device__ void quad(int blk, float* u) const {
     if (U) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) u[k] = U[(size_t)e * GO1_U_PER_ENV + 4 * blk + k];
+      for (int k = 0; k < 4; ++k) u[k] = U[(size_t)e * ustride + 4 * blk + k];
       return;
     }
     uint32_t c[4] = {(uint32_t)gid, (uint32_t)blk, (uint32_t)step, (uint32_t)(step >> 32)};
@@ -1433,7 +1434,54 @@ struct KArgs {
   int cur, prv, nxt;
   const uint8_t* prev_time_out;
   uint8_t* prev_extras;
+  // global reward bucketing (go1_config.indefinite_slots != 0): per-env scaled slot rewards
+  // (n_envs, GO1_MAX_TERMS) and this step's bank of their f64 sums over envs
+  float* bucket_r;
+  double* bucket_sum;
 };
+
+// Waypoint w of the trajectory a reset draws (trajectory_function.py), torch's f32 op order.
+// Trajectory uniforms follow the obs-noise slots: slot GO1_U_NOISE + num_obs + k.
+__device__ void traj_waypoint(CCfg* __restrict__ c, const Rng& rng, const float* root, int w, float* o) {
+  const int ub = GO1_U_NOISE + c->num_obs;
+  if (c->traj_kind == 1) {
+    // _traj_fn_random_target (:70-93): num_targets = traj_length / num_interp + 1 poses per channel, drawn
+    // x, y, z, yaw, pitch, roll; pose 0 := 0; waypoint (s, j) = pose s + (j + 1) (pose s+1 - pose s) / ni
+    const int ni = c->traj_interp, nt = c->traj_length / ni + 1, sg = w / ni, j = w % ni;
+    const float rng_of[6] = {c->traj_x_range, c->traj_y_range, c->traj_z_range, c->traj_yaw_range,
+                             c->traj_pitch_range, c->traj_roll_range};
+    const int out_of[6] = {0, 1, 2, 5, 4, 3};  // draw channel -> [x y z roll pitch yaw]
+#pragma unroll
+    for (int ch = 0; ch < 6; ++ch) {
+      const float r = rng_of[ch];
+      const float a = sg == 0 ? 0.0f : rng(ub + ch * nt + sg) * 2.0f * r - r;
+      const float b = rng(ub + ch * nt + sg + 1) * 2.0f * r - r;
+      const float delta = (b - a) / (float)ni;
+      o[out_of[ch]] = a + (float)(j + 1) * delta;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[i] = o[i] + root[i];
+  } else if (c->traj_kind == 2) {
+    // _traj_fn_random_goal (:28-41): one pose, broadcast to every waypoint
+    o[0] = (rng(ub) - 0.5f) * c->traj_x_range + c->traj_x_mean;
+    o[0] = o[0] + root[0];
+    o[1] = (rng(ub + 1) - 0.5f) * c->traj_y_range + c->traj_y_mean;
+    o[1] = o[1] + root[1];
+    o[2] = 0.0f + c->traj_base_z;
+    o[3] = 0.0f;
+    o[4] = 0.0f;
+    o[5] = rng(ub + 2) * 2.0f * c->traj_yaw_range - c->traj_yaw_range;
+  } else {
+    // _traj_fn_fixed_target (:14-26): waypoint w at (w + 1) x (base_x, base_y) from the base
+    const float k = (float)(w + 1);
+    o[0] = k * c->traj_base_x + root[0];
+    o[1] = k * c->traj_base_y + root[1];
+    o[2] = c->traj_base_z;
+    o[3] = c->traj_roll;
+    o[4] = c->traj_pitch;
+    o[5] = c->traj_yaw;
+  }
+}
 
 // reset_idx for one env, computed redundantly by the 4 lanes of its quad (:218-296)
 __device__ void reset_env(CCfg* __restrict__ c, const go1_terrain& ter, const Rng& rng, int e, int leg,
@@ -1474,15 +1522,21 @@ __device__ void reset_env(CCfg* __restrict__ c, const go1_terrain& ter, const Rn
   for (int i = 0; i < 4; ++i) root[3 + i] = qv[i] / qn;
 #pragma unroll
   for (int i = 0; i < 6; ++i) root[7 + i] = c->reset_vel_range * rng(28 + i) + c->reset_vel_lo;
-  traj[0] = c->traj_base_x + root[0];
-  traj[1] = c->traj_base_y + root[1];
-  traj[2] = c->traj_base_z;
-  traj[3] = c->traj_roll;
-  traj[4] = c->traj_pitch;
-  traj[5] = c->traj_yaw;
+  traj_waypoint(c, rng, root, 0, traj);
 }
 
-template <bool INJ>
+// every waypoint w = first, first + stride, ... of the env's new trajectory (_resample_trajectory :949-955)
+__device__ void write_trajectory(CCfg* __restrict__ c, const Rng& rng, const float* root, float* __restrict__ dst,
+                                 int first, int stride) {
+  for (int w = first; w < c->traj_length; w += stride) {
+    float wp[6];
+    traj_waypoint(c, rng, root, w, wp);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) dst[w * 6 + i] = wp[i];
+  }
+}
+
+template <bool INJ, int KPTS>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) void go1_step_kernel(
     const go1_config* __restrict__ c_gen, KArgs K) {
   CCfg* __restrict__ c = (CCfg*)c_gen;
@@ -1503,7 +1557,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   MARK(kernel_begin);
   MlpFrag F;
   mlp_load(c_gen->actuator, lane, F);  // lane-indexed: generic pointer
-  const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset};
+  const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset, c->u_per_env};
   // the previous step's extras["time_outs"] rebinding, for this wave's envs (flags of the
   // previous launch are complete now), and the flag the next launch will set is cleared
   // (loaded with the state, applied after the prologue's single wait: no round trip of its own)
@@ -1547,16 +1601,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int idx_in = st.curr_pose_index[e];
   const int coll_in = st.collision_count[e];
   const float restitution = st.restitution[e];
-  float traj_in[6], ldv[3], la[3], sums[GO1_NUM_SUMS];
+  const int TL = c->traj_length, NT = c->n_terms, NS = NT + 3;
+  float traj_in[6], ldv[3], la[3], sums[GO1_MAX_TERMS], tot[3];
+  {
+    // the current waypoint trajectories[e, curr_pose_index[e]] (:850-853); traj_length 1 needs no index
+    const float* trj = st.trajectory + (size_t)e * 6 * TL;
+    if (TL != 1) trj += 6 * min(max(idx_in, 0), TL - 1);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) traj_in[i] = st.trajectory[(size_t)e * 6 + i];
+    for (int i = 0; i < 6; ++i) traj_in[i] = trj[i];
+  }
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     ldv[j] = st.last_dof_vel[d0 + j];
     la[j] = st.last_actions[d0 + j];
   }
 #pragma unroll
-  for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = st.episode_sums[(size_t)e * GO1_NUM_SUMS + k];
+  for (int k = 0; k < GO1_MAX_TERMS; ++k) sums[k] = k < NT ? st.episode_sums[(size_t)e * NS + k] : 0.0f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) tot[k] = st.episode_sums[(size_t)e * NS + NT + k];
   Phys P;
   if (!INJ) {
 #pragma unroll
@@ -1774,9 +1836,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // issued here and consumed by the height observations at the end
   const bool hplane = c->terrain_kind == 0;
   const float scan_x = root[0], scan_y = root[1];
+  // camera_pitch_angle (:1934-1939): the previous step's pitch, or 0 with rotate_camera
+  const float cam_p = c->rotate_camera ? 0.0f : cam_pitch;
   float camx = 0.0f, camy = 0.0f;
   if (!hplane) {
-    const float cos_p = pm_cosf(cam_pitch);
+    const float cos_p = pm_cosf(cam_p);
     camx = c->camera_offset_x * cos_p;
     camy = 0.0f * cos_p;
   }
@@ -1799,13 +1863,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
   const int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
   const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
-  // the env's 16 lanes take points sub16 + 16 k (n_pts <= 112 for the front half)
-  constexpr int KPTS = 7;
+  // the env's 16 lanes take points sub16 + 16 k (KPTS = 7 for the 110 front-half points, 15 for all 231)
   float hv[KPTS][2];
+  const bool scan = c->observe_heights != 0;
 #pragma unroll
   for (int k = 0; k < KPTS; ++k) {
     const int p = min(sub16 + 16 * k, n_pts - 1);
-    sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[k][0], hv[k][1]);
+    hv[k][0] = hv[k][1] = 0.0f;
+    if (scan) sample(x_start + p / GO1_GRID_Y, p % GO1_GRID_Y, hv[k][0], hv[k][1]);
   }
 
   if (A.contact_forces && owner) {
@@ -1848,9 +1913,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
   const bool switched = rel_norm < c->switch_dist;
+  // waypoint switch, capped at the last waypoint (:836-844)
   int idx = idx_in;
-  if (switched) { idx += 1; if (idx > 0) idx = 0; }
-  const bool reached = switched && idx == 0;
+  if (switched) { idx += 1; if (idx > TL - 1) idx = TL - 1; }
+  const bool reached = switched && idx == TL - 1;
   // collision count (:848): this lane's thigh + calf, base on lane 0
   float coll_l = (norm3_f(cf_leg[0], cf_leg[1], cf_leg[2]) > 0.1f ? 1.0f : 0.0f) +
                  (norm3_f(cf_leg[3], cf_leg[4], cf_leg[5]) > 0.1f ? 1.0f : 0.0f);
@@ -1861,6 +1927,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const bool time_out = (float)ep > c->max_episode_length;
   bool reset = time_out, diverged = false;
   if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = true;
+  if (c->terminate_end_of_trajectory && reached && (float)ep > c->t_reach) reset = true;  // (:211-213)
+  if (c->use_terminal_body_rotation && pg[2] > 0.0f) reset = true;                        // (:215-216)
   if (!INJ) {
     // native-integrator divergence guard (no reference counterpart: PhysX does not
     // return non-finite states): an env whose state is not finite, or beyond
@@ -1876,89 +1944,215 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 
   MARK(termination_done);
-  // rewards (:320-355, reward_crawling.py)
-  float terms[GO1_NUM_TERMS];
+  // ---- compute_reward (:320-355): the container's functions (reward_crawling.py,
+  // trajectory_tracking_reward.py) for the terms with a nonzero scale.  Every lane of an env
+  // holds the same term values; the env's lane sub16 == 0 files them in an LDS row by term id,
+  // and the reward is then summed in slot (reward_scales) order.  One wave per block: the
+  // wave's LDS operations complete in order, no barrier.
+  __shared__ float s_terms[SEPB][GO1_T_COUNT];
+  const uint32_t tm = c->term_mask;
+#define HAS(id) ((tm >> (id)) & 1u)
+#define PUT(id, v)                          \
+  do {                                      \
+    const float v_ = (v);                   \
+    if (sub16 == 0) s_terms[el][(id)] = v_; \
+  } while (0)
   {
     float x[3];
+    if (HAS(GO1_T_TORQUES)) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) x[j] = sq_f(torque[j]);
-    terms[0] = qsum((x[0] + x[1]) + x[2]);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) x[j] = sq_f((ldv[j] - qd[j]) / c->dt);
-    terms[1] = qsum((x[0] + x[1]) + x[2]);
-    terms[2] = coll;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) x[j] = sq_f(la[j] - act[j]);
-    terms[3] = qsum((x[0] + x[1]) + x[2]);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int d = leg * 3 + j;
-      const float lo = q[j] - s_phys[LDS_DPL + 2 * d];
-      const float hi = q[j] - s_phys[LDS_DPL + 2 * d + 1];
-      const float o = -(lo < 0.0f ? lo : 0.0f);
-      x[j] = o + (hi > 0.0f ? hi : 0.0f);
+      for (int j = 0; j < 3; ++j) x[j] = sq_f(torque[j]);
+      PUT(GO1_T_TORQUES, qsum((x[0] + x[1]) + x[2]));
     }
-    terms[4] = qsum((x[0] + x[1]) + x[2]);
+    if (HAS(GO1_T_DOF_ACC)) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) x[j] = sq_f((ldv[j] - qd[j]) / c->dt);
+      PUT(GO1_T_DOF_ACC, qsum((x[0] + x[1]) + x[2]));
+    }
+    if (HAS(GO1_T_COLLISION)) PUT(GO1_T_COLLISION, coll);
+    if (HAS(GO1_T_ACTION_RATE)) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) x[j] = sq_f(la[j] - act[j]);
+      PUT(GO1_T_ACTION_RATE, qsum((x[0] + x[1]) + x[2]));
+    }
+    if (HAS(GO1_T_DOF_POS_LIMITS)) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int d = leg * 3 + j;
+        const float lo = q[j] - s_phys[LDS_DPL + 2 * d];
+        const float hi = q[j] - s_phys[LDS_DPL + 2 * d + 1];
+        const float o = -(lo < 0.0f ? lo : 0.0f);
+        x[j] = o + (hi > 0.0f ? hi : 0.0f);
+      }
+      PUT(GO1_T_DOF_POS_LIMITS, qsum((x[0] + x[1]) + x[2]));
+    }
+    if (HAS(GO1_T_DOF_VEL)) {  // trajectory_tracking_reward.py:21-23
+#pragma unroll
+      for (int j = 0; j < 3; ++j) x[j] = sq_f(qd[j]);
+      PUT(GO1_T_DOF_VEL, qsum((x[0] + x[1]) + x[2]));
+    }
+    if (HAS(GO1_T_DOF_POS)) {  // trajectory_tracking_reward.py:31-33
+#pragma unroll
+      for (int j = 0; j < 3; ++j) x[j] = sq_f(q[j] - s_phys[LDS_DDP + leg * 3 + j]);
+      PUT(GO1_T_DOF_POS, qsum((x[0] + x[1]) + x[2]));
+    }
   }
-  terms[5] = sq_f(root[2] - c->base_height_target);
-  terms[6] = sq_f(bav[0]) + sq_f(bav[1]);
+  if (HAS(GO1_T_BASE_HEIGHT)) PUT(GO1_T_BASE_HEIGHT, sq_f(root[2] - c->base_height_target));
+  if (HAS(GO1_T_ANG_VEL_XY)) PUT(GO1_T_ANG_VEL_XY, sq_f(bav[0]) + sq_f(bav[1]));
+  if (HAS(GO1_T_ORIENTATION)) PUT(GO1_T_ORIENTATION, sq_f(pg[0]) + sq_f(pg[1]));
+  const float vxy2 = sq_f(blv[0]) + sq_f(blv[1]);
+  const float vmag = norm2_f(blv[0], blv[1]);
+  if (HAS(GO1_T_LARGE_VEL)) PUT(GO1_T_LARGE_VEL, vxy2 * (vmag > 0.5f ? 1.0f : 0.0f));  // reward_crawling.py:53-56
+  if (HAS(GO1_T_LIN_VEL_Z)) PUT(GO1_T_LIN_VEL_Z, sq_f(blv[2]));
+  if (HAS(GO1_T_REACHING_Z)) PUT(GO1_T_REACHING_Z, sq_f(rel_lin[2]));
+  if (HAS(GO1_T_REACHING_ROLL)) PUT(GO1_T_REACHING_ROLL, sq_f(rel_rot[0]));
+  if (HAS(GO1_T_REACHING_PITCH)) PUT(GO1_T_REACHING_PITCH, sq_f(rel_rot[1]));
+  if (HAS(GO1_T_REACHING_YAW_ABS)) PUT(GO1_T_REACHING_YAW_ABS, sq_f(rel_rot[2]));
+  if (HAS(GO1_T_SURVIVE)) PUT(GO1_T_SURVIVE, 1.0f);
+  if (HAS(GO1_T_REACH_GOAL)) PUT(GO1_T_REACH_GOAL, reached ? 1.0f : 0.0f);
+  if (HAS(GO1_T_REACH_GOAL_T)) PUT(GO1_T_REACH_GOAL_T, (reached ? 1.0f : 0.0f) * (float)ep);
+  if (HAS(GO1_T_REACH_GOAL_TR)) PUT(GO1_T_REACH_GOAL_TR, (reached ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f));
+  if (HAS(GO1_T_LINEAR_VEL)) PUT(GO1_T_LINEAR_VEL, norm3_f(blv[0], blv[1], blv[2]) > 0.7f ? 1.0f : 0.0f);
   {
-    const float mag = norm2_f(rel_lin[0], rel_lin[1]);
-    const float lerr = sq_f(blv[0]) + sq_f(blv[1]);
-    const float r_e2e = expf(-lerr / c->tracking_sigma_lin);
-    terms[7] = r_e2e * (mag < c->switch_dist ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
+    const float mag = rel_norm;
+    if (HAS(GO1_T_E2E)) {  // reward_crawling.py:61-77
+      float r;
+      if (c->terminate_end_of_trajectory) {
+        r = (mag < c->switch_dist ? 1.0f : 0.0f) * c->max_episode_length;
+      } else {
+        const float r_e2e = expf(-vxy2 / c->tracking_sigma_lin);
+        r = r_e2e * (mag < c->switch_dist ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
+      }
+      PUT(GO1_T_E2E, r);
+    }
+    // the target velocity towards the waypoint (reward_crawling.py:83-87, trajectory_tracking_reward.py:79-85)
     float tx = rel_lin[0] / (mag + 1e-6f) * c->target_lin_vel;
     float ty = rel_lin[1] / (mag + 1e-6f) * c->target_lin_vel;
     const float gate = mag > c->lin_reaching_criterion ? 1.0f : 0.0f;
     tx = tx * gate;
     ty = ty * gate;
-    const float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
-    terms[8] = expf(-le / c->tracking_sigma_lin);
+    if (HAS(GO1_T_EXPLORATION_LIN)) {  // reward_crawling.py:79-108
+      float r;
+      const int form = c->lin_vel_form;
+      if (form == 1) {
+        r = fabsf(tx - blv[0]) + fabsf(ty - blv[1]);
+      } else if (form == 3) {
+        const float rx = tx / c->target_lin_vel * blv[0] / (vmag + 1e-6f);
+        const float ry = ty / c->target_lin_vel * blv[1] / (vmag + 1e-6f);
+        r = rx + ry;
+        r = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
+        r = r + expf(-(vmag * vmag) / c->tracking_sigma_lin) * (mag < c->lin_reaching_criterion ? 1.0f : 0.0f);
+      } else {
+        const float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
+        r = form == 2 ? le : expf(-le / c->tracking_sigma_lin);
+      }
+      PUT(GO1_T_EXPLORATION_LIN, r);
+    }
+    if (HAS(GO1_T_TASK)) {  // trajectory_tracking_reward.py:74-89
+      const float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
+      PUT(GO1_T_TASK, expf(-le / c->tracking_sigma_lin) * (mag < c->large_dist_threshold ? 1.0f : 0.0f));
+    }
+    if (HAS(GO1_T_TASK_OLD)) {  // trajectory_tracking_reward.py:51-55
+      float r = 0.5f / (0.5f + mag) / c->t_reach;
+      r = r * ((float)ep > c->t_reach ? 1.0f : 0.0f);
+      PUT(GO1_T_TASK_OLD, r);
+    }
+    if (HAS(GO1_T_EXPLORATION)) {  // trajectory_tracking_reward.py:91-99
+      float r = blv[0] * rel_lin[0] + blv[1] * rel_lin[1];
+      r = r / (mag + 1e-6f);
+      r = r / (vmag + 1e-6f);
+      r = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
+      PUT(GO1_T_EXPLORATION, r);
+    }
+    if (HAS(GO1_T_STALLING)) {  // trajectory_tracking_reward.py:105-108
+      const bool sv = vmag < c->small_vel_threshold, ld = mag > c->large_dist_threshold;
+      PUT(GO1_T_STALLING, -((sv && ld) ? 1.0f : 0.0f));
+    }
+  }
+  if (HAS(GO1_T_EXPLORATION_YAW)) {  // reward_crawling.py:110-120
     float ta = rel_rot[2];
     const float m = fabsf(ta);
     ta = ta / (m + 1e-6f) * c->target_ang_vel;
     ta = ta * (m > c->ang_reaching_criterion ? 1.0f : 0.0f);
-    const float ae = sq_f(ta - bav[2]);
-    terms[9] = expf(-ae / c->tracking_sigma_ang);
+    PUT(GO1_T_EXPLORATION_YAW, expf(-sq_f(ta - bav[2]) / c->tracking_sigma_ang));
   }
-  if (diverged)
-#pragma unroll
-    for (int k = 0; k < GO1_NUM_TERMS; ++k) terms[k] = 0.0f;
+  // feet_air_time (trajectory_tracking_reward.py:126-137) mutates last_contacts / feet_air_time
+  float air_new = 0.0f, lc_new = 0.0f;
+  if (HAS(GO1_T_FEET_AIR_TIME)) {
+    float air = st.feet_air_time[(size_t)e * 4 + leg];
+    const float lc = st.last_contacts[(size_t)e * 4 + leg];
+    const bool contact = cf_leg[8] > 1.0f;  // foot z force
+    const bool filt = contact || lc != 0.0f;
+    lc_new = contact ? 1.0f : 0.0f;
+    const bool first = air > 0.0f && filt;
+    air = air + c->dt;
+    const float r = (air - 0.5f) * (first ? 1.0f : 0.0f);
+    air_new = air * (filt ? 0.0f : 1.0f);
+    PUT(GO1_T_FEET_AIR_TIME, qsum(r));
+  }
+#undef PUT
+#undef HAS
+  // slot order: rew_buf += term * scale; pos / neg bucket by the sign of the sum over envs,
+  // which for a sign-definite term is the sign of its scale (:330-336)
+  const bool global_buckets = c->indefinite_slots != 0;
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
 #pragma unroll
-  for (int k = 0; k < GO1_NUM_TERMS; ++k) {
-    const float r = terms[k] * A.reward_scales[k];
-    rew = rew + r;
-    if (A.reward_scales[k] >= 0.0f) pos = pos + r; else neg = neg + r;
-    sums[k] = sums[k] + r;
+  for (int k = 0; k < GO1_MAX_TERMS; ++k) {
+    if (k < NT) {
+      const int id = c->term_ids[k];
+      float t = id != GO1_T_NONE ? s_terms[el][id] : 0.0f;
+      if (diverged) t = 0.0f;
+      if (A.dbg_terms && owner && leg == 0) A.dbg_terms[(size_t)e * GO1_MAX_TERMS + k] = t;
+      if (id != GO1_T_NONE) {
+        const float r = t * A.reward_scales[k];
+        rew = rew + r;
+        if (A.reward_scales[k] >= 0.0f) pos = pos + r; else neg = neg + r;
+        sums[k] = sums[k] + r;
+        if (global_buckets && sub16 == 0) {
+          K.bucket_r[(size_t)e * GO1_MAX_TERMS + k] = r;
+          atomicAdd(K.bucket_sum + k, (double)r);
+        }
+      }
+    }
   }
-  sums[10] = sums[10] + rew;
-  sums[11] = sums[11] + pos;
-  sums[12] = sums[12] + neg;
-  if (A.dbg_terms && owner && leg == 0)
-#pragma unroll
-    for (int k = 0; k < GO1_NUM_TERMS; ++k) A.dbg_terms[(size_t)e * GO1_NUM_TERMS + k] = terms[k];
+  if (c->reward_mode == 1) rew = rew < 0.0f ? 0.0f : rew;            // only_positive_rewards (:341-342)
+  else if (c->reward_mode == 2) rew = pos * expf(neg / c->sigma_rew_neg);  // ji22 style (:343-344)
+  if (!global_buckets) {
+    tot[0] = tot[0] + rew;
+    tot[1] = tot[1] + pos;
+    tot[2] = tot[2] + neg;
+  } else if (c->reward_mode != 2) {
+    tot[0] = tot[0] + rew;  // the bucket launch adds total_pos / total_neg (and the ji22 reward)
+  }
 
   MARK(rewards_done);
   // ---- reset_idx (:218-296); the height scan below still samples at the pre-reset pose
   float traj_new[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) traj_new[i] = traj_in[i];
-  if (A.episode_log && owner && leg == 0 && !reset) A.episode_log[(size_t)e * GO1_EPISODE_LOG + 13] = 0.0f;
+  const int LOGW = NT + 6;
+  if (A.episode_log && owner && leg == 0 && !reset) A.episode_log[(size_t)e * LOGW + NS] = 0.0f;
   if (reset && A.episode_log && owner && leg == 0) {
     // reset_idx logging (:256-271): pre-reset sums, episode length, reached, goal distance
-    float* lg = A.episode_log + (size_t)e * GO1_EPISODE_LOG;
+    float* lg = A.episode_log + (size_t)e * LOGW;
 #pragma unroll
-    for (int k = 0; k < GO1_NUM_SUMS; ++k) lg[k] = sums[k];
-    lg[13] = (float)ep;
-    lg[14] = reached ? 1.0f : 0.0f;
-    lg[15] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+    for (int k = 0; k < GO1_MAX_TERMS; ++k)
+      if (k < NT) lg[k] = sums[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) lg[NT + k] = tot[k];
+    lg[NS] = (float)ep;
+    lg[NS + 1] = reached ? 1.0f : 0.0f;
+    lg[NS + 2] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
   }
   if (reset) {
     reset_env(c, K.ter, rng, e, leg, root, q, qd, strength, offset, traj_new);
+    write_trajectory(c, rng, root, st.trajectory + (size_t)e * 6 * TL, sub16, 16);
     idx = 0;
 #pragma unroll
-    for (int k = 0; k < GO1_NUM_SUMS; ++k) sums[k] = 0.0f;
+    for (int k = 0; k < GO1_MAX_TERMS; ++k) sums[k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tot[k] = 0.0f;
+    air_new = 0.0f;  // feet_air_time[env_ids] = 0 (:248); last_contacts is kept
     cmd[0] = 0.0f;  // commands is a view of local_relative_linear, zeroed by reset_idx (:252, :802)
     cmd[1] = 0.0f;
     // a diverged env observes (and stores as its pitch) its post-reset pose instead
@@ -1968,8 +2162,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   MARK(reset_done);
   // ---- compute_observations (:357-475)
-  float* o = A.obs + (size_t)e * GO1_NUM_OBS;
-  float* oh = A.obs_history ? A.obs_history + (size_t)e * GO1_NUM_OBS : nullptr;  // optional second copy
+  const int NO = c->num_obs;
+  float* o = A.obs + (size_t)e * NO;
+  float* oh = A.obs_history ? A.obs_history + (size_t)e * NO : nullptr;  // optional second copy
   const float clip = c->clip_obs;
   // noise uniforms rng(47 + i) (:472-473): every lane draws exactly two Philox blocks, the
   // same two-block code path in all lanes (the per-value calls of the two store branches
@@ -1990,7 +2185,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     o[i] = v;
     if (oh) oh[i] = v;
   };
-  // role r < 3 writes joint r of its leg; role 3 of leg 0 writes gravity and commands
+  // role r < 3 writes joint r of its leg; role 3 of leg 0 writes gravity and commands, role 3
+  // of leg 1 the episode progress (timestep_in_obs, :375-377: post-reset episode length)
   if (role == 3 && leg == 0) {
     put(0, pg[0], c->noise_gravity, uA[3], true);
     put(1, pg[1], c->noise_gravity, uB[0], true);
@@ -1998,6 +2194,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     put(3, cmd[0] * 1.0f, 0.0f, 0.0f, false);
     put(4, cmd[1] * 1.0f, 0.0f, 0.0f, false);
   }
+  if (c->timestep_in_obs && role == 3 && leg == 1)
+    put(41, (float)(reset ? 0 : ep) / c->max_episode_length, 0.0f, 0.0f, false);
   if (role < 3) {
     const int j = role, d = dn;
     const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act);
@@ -2009,9 +2207,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   MARK(obs_props_done);
   // height observations (:395-411) from the samples gathered after the physics
-  {
+  if (scan) {
+    const int o_h = 41 + c->timestep_in_obs;
     const float zroot = root[2];  // post-reset (:401)
-    const float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
+    const float cam_z = pm_sinf(cam_p) * c->camera_offset_norm;
 #pragma unroll
     for (int k = 0; k < KPTS; ++k) {
       const int p = sub16 + 16 * k;
@@ -2029,20 +2228,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             hh = hh - 0.5f;
           }
           const float v = clampf(hh * c->obs_scale_heights, -clip, clip);
-          o[41 + layer * n_pts + p] = v;
-          if (oh) oh[41 + layer * n_pts + p] = v;
+          o[o_h + layer * n_pts + p] = v;
+          if (oh) oh[o_h + layer * n_pts + p] = v;
         }
       }
     }
-    MARK(heights_done);
-    if (A.dbg_heights) {
-      float* od = A.dbg_heights + (size_t)e * 2 * GO1_GRID_X * GO1_GRID_Y;
-      for (int p = sub16; p < GO1_GRID_X * GO1_GRID_Y; p += 16) {
-        float h0, h1;
-        sample(p / GO1_GRID_Y, p % GO1_GRID_Y, h0, h1);
-        od[p] = h0;
-        od[GO1_GRID_X * GO1_GRID_Y + p] = h1;
-      }
+  }
+  MARK(heights_done);
+  if (A.dbg_heights) {
+    float* od = A.dbg_heights + (size_t)e * 2 * GO1_GRID_X * GO1_GRID_Y;
+    for (int p = sub16; p < GO1_GRID_X * GO1_GRID_Y; p += 16) {
+      float h0, h1;
+      sample(p / GO1_GRID_Y, p % GO1_GRID_Y, h0, h1);
+      od[p] = h0;
+      od[GO1_GRID_X * GO1_GRID_Y + p] = h1;
     }
   }
   if (sub16 == 0) {
@@ -2098,15 +2297,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     st.vel_hist[(size_t)e * 24 + leg * 3 + j] = pick(vh[0]);
     st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j] = pick(vh[1]);
   }
+  if (role == 3 && (tm >> GO1_T_FEET_AIR_TIME) & 1u) {
+    st.feet_air_time[(size_t)e * 4 + leg] = air_new;
+    st.last_contacts[(size_t)e * 4 + leg] = lc_new;
+  }
   if (role == 3 && leg == 0) {
 #pragma unroll
     for (int i = 0; i < 13; ++i) st.root[(size_t)e * 13 + i] = root[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) st.base_rotation[(size_t)e * 3 + i] = rpy[i];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) st.trajectory[(size_t)e * 6 + i] = traj_new[i];
+    for (int k = 0; k < GO1_MAX_TERMS; ++k)
+      if (k < NT) st.episode_sums[(size_t)e * NS + k] = sums[k];
 #pragma unroll
-    for (int k = 0; k < GO1_NUM_SUMS; ++k) st.episode_sums[(size_t)e * GO1_NUM_SUMS + k] = sums[k];
+    for (int k = 0; k < 3; ++k) st.episode_sums[(size_t)e * NS + NT + k] = tot[k];
     st.episode_length[e] = reset ? 0 : ep;
     st.curr_pose_index[e] = idx;
     st.collision_count[e] = coll_count;
@@ -2137,7 +2341,7 @@ __global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __rest
   const int leg = threadIdx.x & 3;
   const int e = blockIdx.x * EPB + (threadIdx.x >> 2);
   if (e >= c->n_envs || !mask[e]) return;
-  const Rng rng = {U, seed, step, e, e + c->env_id_offset};
+  const Rng rng = {U, seed, step, e, e + c->env_id_offset, c->u_per_env};
   float root[13], q[3], qd[3], strength[3], offset[3], traj[6];
   reset_env(c, ter, rng, e, leg, root, q, qd, strength, offset, traj);
   const size_t d0 = (size_t)e * NDOF + leg * 3;
@@ -2152,16 +2356,51 @@ __global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __rest
 #pragma unroll
     for (int s = 0; s < GO1_LAG_SLOTS; ++s) st.lag[(size_t)e * 84 + s * 12 + leg * 3 + j] = 0.0f;
   }
+  write_trajectory(c, rng, root, st.trajectory + (size_t)e * 6 * c->traj_length, leg, 4);
+  st.feet_air_time[(size_t)e * 4 + leg] = 0.0f;  // (:248)
+  const int ns = c->n_terms + 3;
+  for (int k = leg; k < ns; k += 4) st.episode_sums[(size_t)e * ns + k] = 0.0f;
   if (leg == 0) {
 #pragma unroll
     for (int i = 0; i < 13; ++i) st.root[(size_t)e * 13 + i] = root[i];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) st.trajectory[(size_t)e * 6 + i] = traj[i];
-#pragma unroll
-    for (int k = 0; k < GO1_NUM_SUMS; ++k) st.episode_sums[(size_t)e * GO1_NUM_SUMS + k] = 0.0f;
     st.episode_length[e] = 0;
     st.curr_pose_index[e] = 0;
     st.collision_count[e] = 0;
+  }
+  (void)traj;
+}
+
+// Global pos / neg bucketing (:330-336) when some reward slot has no fixed sign: the step kernel
+// recorded every env's scaled slot rewards and their sums over envs (f64); here each env's
+// rew_buf_pos / rew_buf_neg are rebuilt in slot order with the reference's bucket test on the sum's
+// sign, added to total_pos / total_neg (the state's episode sums, or the episode-log row of an env
+// the step reset), and the ji22-style reward is formed (:343-344).
+__global__ void go1_bucket_kernel(const go1_config* __restrict__ c, go1_state st, const float* __restrict__ r_all,
+                                  const double* __restrict__ bsum, double* __restrict__ bsum_next,
+                                  const uint8_t* __restrict__ reset, float* __restrict__ rew,
+                                  float* __restrict__ episode_log) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nt = c->n_terms, ns = nt + 3;
+  if (blockIdx.x == 0 && threadIdx.x < GO1_MAX_TERMS) bsum_next[threadIdx.x] = 0.0;
+  if (e >= c->n_envs) return;
+  float pos = 0.0f, neg = 0.0f;
+  for (int k = 0; k < nt; ++k) {
+    if (c->term_ids[k] == GO1_T_NONE) continue;
+    const float r = r_all[(size_t)e * GO1_MAX_TERMS + k];
+    const double S = bsum[k];
+    if (S >= 0.0) pos = pos + r;
+    else if (S <= 0.0) neg = neg + r;
+  }
+  float* t = (reset[e] && episode_log) ? episode_log + (size_t)e * (nt + 6) + nt
+                                       : (reset[e] ? nullptr : st.episode_sums + (size_t)e * ns + nt);
+  if (c->reward_mode == 2) {
+    const float rw = pos * expf(neg / c->sigma_rew_neg);
+    rew[e] = rw;
+    if (t) t[0] = t[0] + rw;
+  }
+  if (t) {
+    t[1] = t[1] + pos;
+    t[2] = t[2] + neg;
   }
 }
 
@@ -2192,6 +2431,8 @@ struct go1_handle {
   go1_terrain ter;
   bool bound = false, has_terrain = false;
   int32_t* d_flags = nullptr;  // 3 "some env reset in step k" words (k mod 3)
+  float* d_bucket_r = nullptr;    // global reward bucketing scratch (indefinite_slots != 0)
+  double* d_bucket_sum = nullptr; // 2 banks x GO1_MAX_TERMS
   uint64_t count = 0;          // go1_step calls so far
   const uint8_t* prev_time_out = nullptr;
   uint8_t* prev_extras = nullptr;
@@ -2237,9 +2478,21 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   if (cfg->rand_interval <= 0) return fail(GO1_E_ARG, "go1_create: rand_interval");
   if (cfg->n_envs % EPB != 0)
     return fail(GO1_E_ARG, "go1_create: n_envs must be a multiple of 16 (one wave = 16 envs x 4 legs)");
-  if (!cfg->measure_front_half)
-    return fail(GO1_E_ARG, "go1_create: only the 261-wide front-half height scan is on this path "
-                           "(Cfg.terrain.measure_front_half, scripts/train.py:53)");
+  if (cfg->n_terms < 0 || cfg->n_terms > GO1_MAX_TERMS) return fail(GO1_E_ARG, "go1_create: n_terms");
+  for (int k = 0; k < cfg->n_terms; ++k)
+    if (cfg->term_ids[k] != GO1_T_NONE && (cfg->term_ids[k] < 0 || cfg->term_ids[k] >= GO1_T_COUNT))
+      return fail(GO1_E_ARG, "go1_create: bad term id");
+  if (cfg->traj_length < 1 || cfg->traj_length > GO1_MAX_TRAJ || cfg->traj_kind < 0 || cfg->traj_kind > 2 ||
+      (cfg->traj_kind == 1 && (cfg->traj_interp < 1 || cfg->traj_length % cfg->traj_interp != 0)))
+    return fail(GO1_E_ARG, "go1_create: trajectory shape");
+  {
+    const int n_pts = (cfg->measure_front_half ? GO1_GRID_X - (GO1_GRID_X / 2 + 1) : GO1_GRID_X) * GO1_GRID_Y;
+    const int width = 41 + (cfg->timestep_in_obs ? 1 : 0) + (cfg->observe_heights ? 2 * n_pts : 0);
+    if (cfg->num_obs != width) return fail(GO1_E_ARG, "go1_create: num_obs does not match the observation layout");
+    const int traj_u = cfg->traj_kind == 1 ? 6 * (cfg->traj_length / cfg->traj_interp + 1)
+                                           : (cfg->traj_kind == 2 ? 3 : 0);
+    if (cfg->u_per_env != GO1_U_NOISE + width + traj_u) return fail(GO1_E_ARG, "go1_create: u_per_env");
+  }
   for (int leg = 0; leg < 4; ++leg)  // joint offsets must have the sparsity the kernel exploits
     for (int j = 0; j < 3; ++j)
       for (int k = 0; k < 3; ++k)
@@ -2266,6 +2519,12 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   }
   HIP_TRY(hipMemcpy(h->d_cfg, cfg, sizeof(go1_config), hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(h->d_flags, 0, 3 * sizeof(int32_t)));
+  if (cfg->indefinite_slots) {
+    HIP_TRY(hipMalloc(&h->d_bucket_r, (size_t)cfg->n_envs * GO1_MAX_TERMS * sizeof(float)));
+    HIP_TRY(hipMalloc(&h->d_bucket_sum, 2 * GO1_MAX_TERMS * sizeof(double)));
+    HIP_TRY(hipMemset(h->d_bucket_r, 0, (size_t)cfg->n_envs * GO1_MAX_TERMS * sizeof(float)));
+    HIP_TRY(hipMemset(h->d_bucket_sum, 0, 2 * GO1_MAX_TERMS * sizeof(double)));
+  }
   *out = h;
   return GO1_OK;
 }
@@ -2275,7 +2534,7 @@ int go1_bind(go1_handle* h, const go1_state* s) {
   const void* p[] = {s->root, s->dof_pos, s->dof_vel, s->last_actions, s->last_dof_vel, s->lag, s->pos_err_hist,
                      s->vel_hist, s->motor_strength, s->motor_offset, s->friction, s->restitution, s->payload,
                      s->episode_length, s->curr_pose_index, s->trajectory, s->base_rotation, s->collision_count,
-                     s->episode_sums, s->joint_pos_target};
+                     s->episode_sums, s->joint_pos_target, s->feet_air_time, s->last_contacts};
   for (const void* q : p)
     if (!q) return fail(GO1_E_ARG, "go1_bind: every state plane must be non-null");
   h->st = *s;
@@ -2313,12 +2572,27 @@ int go1_step(go1_handle* h, const go1_step_args* a, void* stream) {
   K.nxt = (int)((h->count + 1) % 3);
   K.prev_time_out = h->prev_time_out;
   K.prev_extras = h->prev_extras;
+  const int bank = (int)(h->count & 1);
+  K.bucket_r = h->d_bucket_r;
+  K.bucket_sum = h->d_bucket_sum ? h->d_bucket_sum + bank * GO1_MAX_TERMS : nullptr;
   dim3 grid(n / SEPB), block(TPB);
+  const bool full = !h->cfg.measure_front_half;  // 231 scanned points: 15 per lane instead of 7
   if (a->ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_begin, s));
-  if (inj) hipLaunchKernelGGL(go1_step_kernel<true>, grid, block, 0, s, h->d_cfg, K);
-  else hipLaunchKernelGGL(go1_step_kernel<false>, grid, block, 0, s, h->d_cfg, K);
+  if (inj) {
+    if (full) hipLaunchKernelGGL((go1_step_kernel<true, 15>), grid, block, 0, s, h->d_cfg, K);
+    else hipLaunchKernelGGL((go1_step_kernel<true, 7>), grid, block, 0, s, h->d_cfg, K);
+  } else {
+    if (full) hipLaunchKernelGGL((go1_step_kernel<false, 15>), grid, block, 0, s, h->d_cfg, K);
+    else hipLaunchKernelGGL((go1_step_kernel<false, 7>), grid, block, 0, s, h->d_cfg, K);
+  }
   HIP_TRY(hipGetLastError());
   if (a->ev_end) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_end, s));
+  if (h->cfg.indefinite_slots) {
+    hipLaunchKernelGGL(go1_bucket_kernel, dim3((n + 255) / 256), dim3(256), 0, s, h->d_cfg, h->st, h->d_bucket_r,
+                       h->d_bucket_sum + bank * GO1_MAX_TERMS, h->d_bucket_sum + (bank ^ 1) * GO1_MAX_TERMS,
+                       a->reset, a->rew, a->episode_log);
+    HIP_TRY(hipGetLastError());
+  }
 h->prev_time_out = a->time_out;
   h->prev_extras = a->extras_time_outs;
   h->count++;
@@ -2370,6 +2644,8 @@ int go1_destroy(go1_handle* h) {
   if (!h) return GO1_OK;
   if (h->d_cfg) (void)hipFree(h->d_cfg);
   if (h->d_flags) (void)hipFree(h->d_flags);
+  if (h->d_bucket_r) (void)hipFree(h->d_bucket_r);
+  if (h->d_bucket_sum) (void)hipFree(h->d_bucket_sum);
   delete h;
   return GO1_OK;
 }

@@ -105,11 +105,12 @@ class EpisodeLogRing:
         self.env = env
         self.dev = device
         self.R = R = int(min(EPISODE_RING, max(4, (1 << 22) // max(n, 1))))  # <= 16 MB per half
-        self.buf = torch.zeros((2, R, n, abi.GO1_EPISODE_LOG), device=device)
+        self.W = W = abi.episode_log_width(len(env.reward_names))
+        self.buf = torch.zeros((2, R, n, W), device=device)
         self.half, self.slot, self.done = 0, 0, 0  # write position; slots of this half already drained
         self.cuda = device.type == "cuda"
         if self.cuda:
-            self.host = torch.zeros((2, R, n, abi.GO1_EPISODE_LOG), pin_memory=True)
+            self.host = torch.zeros((2, R, n, W), pin_memory=True)
             self.side = torch.cuda.Stream(device)
             self.copied = [None, None]  # event per half: host copy finished
         self.inflight = None  # (half, first slot) copied to host, not yet turned into deque entries
@@ -162,7 +163,8 @@ class EpisodeLogRing:
     def _process(self, logs):
         env = self.env
         ntr = env.num_train_envs
-        col = logs[:, :ntr, 13]                              # episode length, 0 = no reset
+        ns = len(env.sum_keys)
+        col = logs[:, :ntr, ns]                              # episode length, 0 = no reset
         steps, envs = np.nonzero(col > 0)                    # by step, then env
         if steps.size == 0:
             return
@@ -170,11 +172,11 @@ class EpisodeLogRing:
         reset_steps = np.unique(steps)
         timeouts = (col[reset_steps] > np.float32(env.max_episode_length)).reshape(-1)[-4000:]
         env._timeouts.extend(timeouts)
-        for i, key in enumerate(L.SUM_KEYS):
+        for i, key in enumerate(env.sum_keys):
             env._train_ep["rew_" + key].extend(rows[:, i])
-        env._train_ep["episode_length"].extend(rows[:, 13])
-        env._train_ep["reached"].extend(rows[:, 14] > 0)
-        env._train_ep["goal_distance"].extend(rows[:, 15])
+        env._train_ep["episode_length"].extend(rows[:, ns])
+        env._train_ep["reached"].extend(rows[:, ns + 1] > 0)
+        env._train_ep["goal_distance"].extend(rows[:, ns + 2])
 
 
 def _episode_dicts():
@@ -214,10 +216,10 @@ class LeggedRobot:
         self.max_episode_length_s = cfg.env.episode_length_s
         self.max_episode_length = d["max_episode_length"]
         self.reward_scales = dict(d["reward_scales"])
-        unknown = set(self.reward_scales) - set(L.REWARD_KEYS)
-        if unknown:
-            raise NotImplementedError(f"reward terms not on the accelerated path: {sorted(unknown)}")
+        # reward slots in Cfg.reward_scales order (the C ABI's term table; unknown terms raise in
+        # build_abi_config, terms the container lacks keep a zero sum as in the reference :1390-1395)
         self.reward_names = list(self.reward_scales)
+        self.sum_keys = tuple(self.reward_names) + ("total", "total_pos", "total_neg")
         self._gravity_interval = d["gravity_rand_interval"]
         self._gravity_duration = d["gravity_rand_duration"]
         n, n_global = self.num_envs, self.num_envs * world_size
@@ -295,7 +297,7 @@ class LeggedRobot:
         return torch.as_tensor(self._gravity_vec, device=self.device).repeat(self.num_envs, 1)
 
     def _scale_vector(self):
-        return CF.reward_scale_vector(self.reward_scales)
+        return CF.reward_scale_vector(self.reward_scales, self.reward_names)
 
     def _install_extras(self):
         ex = self.extras
@@ -402,7 +404,7 @@ class LeggedRobot:
     @property
     def episode_sums(self):
         s = self._sim.state["episode_sums"]
-        return {k: s[:, i] for i, k in enumerate(L.SUM_KEYS)}
+        return {k: s[:, i] for i, k in enumerate(self.sum_keys)}
 
     def get_observations(self):
         return self.obs_buf
@@ -470,7 +472,7 @@ class LeggedRobot:
         st = self._sim.state
         sums = st["episode_sums"][env_ids].cpu().numpy()
         ep = st["episode_length"][env_ids, 0].float().cpu().numpy()
-        for i, key in enumerate(L.SUM_KEYS):
+        for i, key in enumerate(self.sum_keys):
             self._train_ep["rew_" + key].extend(sums[:, i])
         self._train_ep["episode_length"].extend(ep)
         mask = self._reset_mask

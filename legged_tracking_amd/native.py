@@ -40,7 +40,7 @@ def lib():
     l.go1_time_outs_pending.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     l.go1_actuator_net.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     l.go1_destroy.argtypes = [C.c_void_p]
-    if l.go1_abi_version() != 2:
+    if l.go1_abi_version() != abi.GO1_ABI_VERSION:
         raise NativeError("ABI version mismatch")
     _lib = l
     return l
@@ -58,10 +58,10 @@ def _stream():
 class StateTensors:
     """go1_state planes as torch tensors on the device (SoA, row-major (n, width))."""
 
-    def __init__(self, n, device):
+    def __init__(self, n, device, cfg):
         self.n = n
         self.t = {}
-        for name, w, dt in abi.STATE_SPEC:
+        for name, w, dt in abi.state_spec(cfg):
             self.t[name] = torch.zeros((n, w), dtype=torch.float32 if dt == "f32" else torch.int32, device=device)
 
     def struct(self):
@@ -91,10 +91,10 @@ class Go1Native:
         self.h = C.c_void_p()
         with torch.cuda.device(self.device):
             _check(lib().go1_create(C.byref(cfg), C.byref(self.h)))
-            self.state = StateTensors(n, self.device)
+            self.state = StateTensors(n, self.device, cfg)
             _check(lib().go1_bind(self.h, C.byref(self.state.struct())))
             dev = self.device
-            self.obs = torch.zeros((n, abi.GO1_NUM_OBS), device=dev)
+            self.obs = torch.zeros((n, cfg.num_obs), device=dev)
             self.priv = torch.zeros((n, abi.GO1_NUM_PRIV), device=dev)
             self.rew = torch.zeros(n, device=dev)
             self.reset = torch.zeros(n, dtype=torch.bool, device=dev)
@@ -139,11 +139,13 @@ class Go1Native:
             self._consts = key
             a.gravity_vec[:] = [float(x) for x in gravity_vec]
             a.sim_gravity[:] = [float(x) for x in sim_gravity]
-            a.reward_scales[:] = [float(x) for x in reward_scales]
+            rs = np.zeros(abi.GO1_MAX_TERMS, np.float32)
+            rs[:len(reward_scales)] = np.asarray(reward_scales, np.float32)
+            a.reward_scales[:] = [float(x) for x in rs]
         a.rng_seed, a.rng_step = int(rng_seed), int(rng_step)
         a.uniforms = None
         if uniforms is not None:
-            assert uniforms.is_contiguous() and uniforms.shape == (self.n, abi.GO1_U_PER_ENV)
+            assert uniforms.is_contiguous() and uniforms.shape == (self.n, self.cfg.u_per_env)
             a.uniforms = uniforms.data_ptr()
         if inj is not None:
             a.inj_dof, a.inj_root, a.inj_contact = (inj[k].data_ptr() for k in ("dof", "root", "contact"))
@@ -165,14 +167,14 @@ class Go1Native:
                        ("commands", "dbg_commands"), ("reached", "dbg_reached")):
             setattr(a, fld, debug[k].data_ptr() if debug and k in debug else None)
         if episode_log is not None:
-            assert episode_log.is_contiguous() and episode_log.shape == (self.n, abi.GO1_EPISODE_LOG)
+            assert episode_log.is_contiguous() and episode_log.shape == (self.n, abi.episode_log_width(self.cfg.n_terms))
         a.episode_log = episode_log.data_ptr() if episode_log is not None else None
         if aux is not None:
             assert aux.is_contiguous() and aux.shape == (self.n, abi.GO1_AUX)
         a.aux = aux.data_ptr() if aux is not None else None
         a.ev_begin, a.ev_end = events if events is not None else (None, None)  # hipEvent_t pair as ints
         if obs_history is not None:
-            assert obs_history.is_contiguous() and obs_history.shape == (self.n, abi.GO1_NUM_OBS)
+            assert obs_history.is_contiguous() and obs_history.shape == (self.n, self.cfg.num_obs)
         a.obs_history = obs_history.data_ptr() if obs_history is not None else None
         _check(self._lib_step(self.h, C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
 
@@ -216,5 +218,5 @@ class Go1Native:
 def debug_buffers(n, decimation, device):
     return dict(torques=torch.zeros((decimation, n, 12), device=device),
                 heights=torch.zeros((n, 2, 21, 11), device=device),
-                terms=torch.zeros((n, 10), device=device), commands=torch.zeros((n, 2), device=device),
+                terms=torch.zeros((n, abi.GO1_MAX_TERMS), device=device), commands=torch.zeros((n, 2), device=device),
                 reached=torch.zeros(n, dtype=torch.uint8, device=device))

@@ -70,9 +70,9 @@ float go1o_uniform(uint64_t seed, uint64_t step, uint32_t env, uint32_t slot) {
 }
 
 /* parity mode: caller uniforms of local env e; otherwise Philox keyed by the GLOBAL env id */
-static float draw(const go1_step_args* a, const float* U, int env_id_offset, int e, int slot) {
-  if (U) return U[(size_t)e * GO1_U_PER_ENV + slot];
-  return go1o_uniform(a->rng_seed, a->rng_step, (uint32_t)(e + env_id_offset), (uint32_t)slot);
+static float draw(const go1_config* c, const go1_step_args* a, const float* U, int e, int slot) {
+  if (U) return U[(size_t)e * c->u_per_env + slot];
+  return go1o_uniform(a->rng_seed, a->rng_step, (uint32_t)(e + c->env_id_offset), (uint32_t)slot);
 }
 
 /* ------------------------------------------------------------ actuator net */
@@ -726,16 +726,16 @@ static void compute_torques(const go1_config* c, const go1_state* st, int e, con
 static void reset_env(const go1_config* c, const go1_state* st, const go1_terrain* ter, int e, const go1_step_args* a,
                       const float* U) {
   /* _randomize_dof_props (:744-754) */
-  float us = draw(a, U, c->env_id_offset, e, 0);
+  float us = draw(c, a, U, e, 0);
   float s = us * c->strength_range + c->strength_lo;
   for (int d = 0; d < NDOF; ++d) {
     st->motor_strength[(size_t)e * NDOF + d] = s;
-    float uo = draw(a, U, c->env_id_offset, e, 1 + d);
+    float uo = draw(c, a, U, e, 1 + d);
     st->motor_offset[(size_t)e * NDOF + d] = uo * c->offset_range + c->offset_lo;
   }
   /* _reset_dofs (:998-1008) */
   for (int d = 0; d < NDOF; ++d) {
-    float u = draw(a, U, c->env_id_offset, e, 13 + d);
+    float u = draw(c, a, U, e, 13 + d);
     float f = c->reset_dof_range * u + c->reset_dof_lo;
     st->dof_pos[(size_t)e * NDOF + d] = c->default_dof_pos[d] * f;
     st->dof_vel[(size_t)e * NDOF + d] = 0.0f;
@@ -748,13 +748,13 @@ static void reset_env(const go1_config* c, const go1_state* st, const go1_terrai
   r[1] = r[1] + eo[1];
   r[2] = r[2] + eo[2];
   if (c->custom_origins) {
-    float ux = draw(a, U, c->env_id_offset, e, 25), uy = draw(a, U, c->env_id_offset, e, 26);
+    float ux = draw(c, a, U, e, 25), uy = draw(c, a, U, e, 26);
     r[0] = r[0] + (c->x_init_range2 * ux + c->x_init_lo);
     r[1] = r[1] + (c->y_init_range2 * uy + c->y_init_lo);
     r[0] = r[0] + c->x_init_offset;
     r[1] = r[1] + c->y_init_offset;
   }
-  float yaw = c->yaw_range2 * draw(a, U, c->env_id_offset, e, 27) + c->yaw_lo;
+  float yaw = c->yaw_range2 * draw(c, a, U, e, 27) + c->yaw_lo;
   /* quat_from_angle_axis(yaw, z) then quat_unit */
   float th = yaw / 2.0f;
   float sth, cth;
@@ -763,23 +763,64 @@ static void reset_env(const go1_config* c, const go1_state* st, const go1_terrai
   float qn = sqrtf(fmaf(qv[3], qv[3], fmaf(qv[2], qv[2], fmaf(qv[1], qv[1], qv[0] * qv[0]))));
   if (qn < 1e-9f) qn = 1e-9f;
   for (int i = 0; i < 4; ++i) r[3 + i] = qv[i] / qn;
-  for (int i = 0; i < 6; ++i) r[7 + i] = c->reset_vel_range * draw(a, U, c->env_id_offset, e, 28 + i) + c->reset_vel_lo;
-  /* _resample_trajectory + _traj_fn_fixed_target (trajectory_function.py:14-26) */
+  for (int i = 0; i < 6; ++i) r[7 + i] = c->reset_vel_range * draw(c, a, U, e, 28 + i) + c->reset_vel_lo;
+  /* _resample_trajectory (:949-955) */
   st->curr_pose_index[e] = 0;
-  float* tr = st->trajectory + (size_t)e * 6;
-  tr[0] = c->traj_base_x + r[0];
-  tr[1] = c->traj_base_y + r[1];
-  tr[2] = c->traj_base_z;
-  tr[3] = c->traj_roll;
-  tr[4] = c->traj_pitch;
-  tr[5] = c->traj_yaw;
+  float* tr = st->trajectory + (size_t)e * 6 * c->traj_length;
+  const int ub = GO1_U_NOISE + c->num_obs; /* trajectory draws follow the obs-noise slots */
+  if (c->traj_kind == 1) {
+    /* _traj_fn_random_target (trajectory_function.py:70-93): traj_length / num_interp + 1 poses per
+     * channel drawn x, y, z, yaw, pitch, roll (torch.rand * 2 * range - range); pose 0 := 0;
+     * waypoint (s, j) = pose s + (j + 1) * (pose s+1 - pose s) / num_interp; then + base xyz */
+    const int ni = c->traj_interp, nt = c->traj_length / ni + 1;
+    const float rg[6] = {c->traj_x_range, c->traj_y_range, c->traj_z_range, c->traj_yaw_range,
+                         c->traj_pitch_range, c->traj_roll_range};
+    const int col[6] = {0, 1, 2, 5, 4, 3};
+    float pose[6][GO1_MAX_TRAJ + 1];
+    for (int ch = 0; ch < 6; ++ch)
+      for (int t = 0; t < nt; ++t)
+        pose[ch][t] = t == 0 ? 0.0f : draw(c, a, U, e, ub + ch * nt + t) * 2.0f * rg[ch] - rg[ch];
+    for (int sg = 0; sg + 1 < nt; ++sg)
+      for (int j = 0; j < ni; ++j)
+        for (int ch = 0; ch < 6; ++ch) {
+          float delta = (pose[ch][sg + 1] - pose[ch][sg]) / (float)ni;
+          tr[(sg * ni + j) * 6 + col[ch]] = pose[ch][sg] + (float)(j + 1) * delta;
+        }
+    for (int w = 0; w < c->traj_length; ++w)
+      for (int i = 0; i < 3; ++i) tr[w * 6 + i] = tr[w * 6 + i] + r[i];
+  } else if (c->traj_kind == 2) {
+    /* _traj_fn_random_goal (trajectory_function.py:28-41): one pose broadcast to every waypoint */
+    float x = (draw(c, a, U, e, ub) - 0.5f) * c->traj_x_range + c->traj_x_mean;
+    x = x + r[0];
+    float y = (draw(c, a, U, e, ub + 1) - 0.5f) * c->traj_y_range + c->traj_y_mean;
+    y = y + r[1];
+    float yaw = draw(c, a, U, e, ub + 2) * 2.0f * c->traj_yaw_range - c->traj_yaw_range;
+    for (int w = 0; w < c->traj_length; ++w) {
+      float* o = tr + w * 6;
+      o[0] = x; o[1] = y; o[2] = 0.0f + c->traj_base_z; o[3] = 0.0f; o[4] = 0.0f; o[5] = yaw;
+    }
+  } else {
+    /* _traj_fn_fixed_target (trajectory_function.py:14-26): arange(1, T+1) * base_x + base x */
+    for (int w = 0; w < c->traj_length; ++w) {
+      float* o = tr + w * 6;
+      float k = (float)(w + 1);
+      o[0] = k * c->traj_base_x + r[0];
+      o[1] = k * c->traj_base_y + r[1];
+      o[2] = c->traj_base_z;
+      o[3] = c->traj_roll;
+      o[4] = c->traj_pitch;
+      o[5] = c->traj_yaw;
+    }
+  }
   /* buffers (:246-254, :262, :273, :295-296) */
   for (int d = 0; d < NDOF; ++d) {
     st->last_actions[(size_t)e * NDOF + d] = 0.0f;
     st->last_dof_vel[(size_t)e * NDOF + d] = 0.0f;
   }
   st->episode_length[e] = 0;
-  for (int k = 0; k < GO1_NUM_SUMS; ++k) st->episode_sums[(size_t)e * GO1_NUM_SUMS + k] = 0.0f;
+  const int ns = c->n_terms + 3;
+  for (int k = 0; k < ns; ++k) st->episode_sums[(size_t)e * ns + k] = 0.0f;
+  for (int l = 0; l < 4; ++l) st->feet_air_time[(size_t)e * 4 + l] = 0.0f; /* (:248) */
   st->collision_count[e] = 0;
   for (int i = 0; i < 84; ++i) st->lag[(size_t)e * 84 + i] = 0.0f;
 }
@@ -832,7 +873,7 @@ static void post_kin(const float* root, const float* gravity_vec, const float* t
 }
 
 static void step_env(const go1_config* c, const Model* M, const go1_state* st, const go1_terrain* ter,
-                     const go1_step_args* a, int e) {
+                     const go1_step_args* a, int e, float* r_slots) {
   const int n = c->n_envs;
   const float* U = a->uniforms;
   float act[NDOF];
@@ -895,12 +936,17 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   /* ---------------- post_physics_step (:114-169) */
   int ep = st->episode_length[e] + 1;
   st->episode_length[e] = ep;
+  const int TL = c->traj_length, NT = c->n_terms, NS = NT + 3;
+  int idx = st->curr_pose_index[e];
+  /* the current waypoint trajectories[e, curr_pose_index[e]] (:850-853) */
+  const float* traj_cur = st->trajectory + (size_t)e * 6 * TL + 6 * (idx < 0 ? 0 : (idx > TL - 1 ? TL - 1 : idx));
   float blv[3], bav[3], pg[3], rel_lin[3], rpy[3], rel_rot[3];
-  post_kin(root, a->gravity_vec, st->trajectory + (size_t)e * 6, blv, bav, pg, rel_lin, rpy, rel_rot);
+  post_kin(root, a->gravity_vec, traj_cur, blv, bav, pg, rel_lin, rpy, rel_rot);
 
-  /* _get_heights (:1918-1965), camera pitch = previous step's base_rotation */
+  /* _get_heights (:1918-1965), camera pitch = previous step's base_rotation, or 0 with
+   * rotate_camera (:1934-1939) */
   float* brot = st->base_rotation + (size_t)e * 3;
-  float cam_pitch = brot[1];
+  float cam_pitch = c->rotate_camera ? 0.0f : brot[1];
   float heights[2][GO1_GRID_X][GO1_GRID_Y];
   if (c->terrain_kind == 1) {
     const float* eto = ter->env_terrain_origin + (size_t)e * 3;
@@ -936,20 +982,19 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
 
   /* DR every rand_interval (:822-824) */
   if (ep % c->rand_interval == 0) {
-    float us = draw(a, U, c->env_id_offset, e, 34);
+    float us = draw(c, a, U, e, 34);
     float s = us * c->strength_range + c->strength_lo;
     for (int d = 0; d < NDOF; ++d) {
       st->motor_strength[(size_t)e * NDOF + d] = s;
-      st->motor_offset[(size_t)e * NDOF + d] = draw(a, U, c->env_id_offset, e, 35 + d) * c->offset_range + c->offset_lo;
+      st->motor_offset[(size_t)e * NDOF + d] = draw(c, a, U, e, 35 + d) * c->offset_range + c->offset_lo;
     }
   }
-  /* switch / reached (:836-844), traj_length = 1 */
+  /* switch / reached (:836-844): advance on reach, capped at the last waypoint */
   float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
   int switched = rel_norm < c->switch_dist;
-  int idx = st->curr_pose_index[e];
-  if (switched) { idx += 1; if (idx > 0) idx = 0; }
+  if (switched) { idx += 1; if (idx > TL - 1) idx = TL - 1; }
   st->curr_pose_index[e] = idx;
-  int reached = switched && idx == 0;
+  int reached = switched && idx == TL - 1;
   if (a->dbg_reached) a->dbg_reached[e] = (uint8_t)reached;
   /* collision_count (:848): thigh x4, calf x4, base */
   static const int PEN[9] = {2, 6, 10, 14, 3, 7, 11, 15, 0};
@@ -964,6 +1009,8 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
   int time_out = (float)ep > c->max_episode_length;
   int reset = time_out, diverged = 0;
   if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = 1;
+  if (c->terminate_end_of_trajectory && reached && (float)ep > c->t_reach) reset = 1; /* (:211-213) */
+  if (c->use_terminal_body_rotation && pg[2] > 0.0f) reset = 1;                        /* (:215-216) */
   if (!a->inj_dof) { /* native-integrator divergence guard (see the HIP kernel) */
     int finite = 1;
     for (int i = 0; i < 13; ++i) finite = finite && fabsf(root[i]) < GO1_DIVERGED;
@@ -972,89 +1019,174 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     if (diverged) reset = 1;
   }
 
-  /* compute_reward (:320-355) with RewardsCrawling terms */
-  float terms[GO1_NUM_TERMS];
+  /* compute_reward (:320-355): the container's reward functions for the nonzero-scaled terms
+   * (reward_crawling.py, trajectory_tracking_reward.py), by go1_term id */
+  float tv[GO1_T_COUNT];
+  memset(tv, 0, sizeof(tv));
   {
     float x[NDOF];
-    for (int d = 0; d < NDOF; ++d) x[d] = sq_f(torque[d]);
-    terms[0] = sum12_legs(x);
     const float* ldv = st->last_dof_vel + (size_t)e * NDOF;
-    for (int d = 0; d < NDOF; ++d) x[d] = sq_f((ldv[d] - dv[d]) / c->dt);
-    terms[1] = sum12_legs(x);
-    terms[2] = coll;
     const float* la = st->last_actions + (size_t)e * NDOF;
+    for (int d = 0; d < NDOF; ++d) x[d] = sq_f(torque[d]);
+    tv[GO1_T_TORQUES] = sum12_legs(x);
+    for (int d = 0; d < NDOF; ++d) x[d] = sq_f((ldv[d] - dv[d]) / c->dt);
+    tv[GO1_T_DOF_ACC] = sum12_legs(x);
+    tv[GO1_T_COLLISION] = coll;
     for (int d = 0; d < NDOF; ++d) x[d] = sq_f(la[d] - act[d]);
-    terms[3] = sum12_legs(x);
+    tv[GO1_T_ACTION_RATE] = sum12_legs(x);
     for (int d = 0; d < NDOF; ++d) {
       float lo = dp[d] - c->dof_pos_limits[2 * d];
       float hi = dp[d] - c->dof_pos_limits[2 * d + 1];
       float o = -(lo < 0.0f ? lo : 0.0f);
       x[d] = o + (hi > 0.0f ? hi : 0.0f);
     }
-    terms[4] = sum12_legs(x);
-    terms[5] = sq_f(root[2] - c->base_height_target);
-    terms[6] = sq_f(bav[0]) + sq_f(bav[1]);
+    tv[GO1_T_DOF_POS_LIMITS] = sum12_legs(x);
+    for (int d = 0; d < NDOF; ++d) x[d] = sq_f(dv[d]);
+    tv[GO1_T_DOF_VEL] = sum12_legs(x); /* trajectory_tracking_reward.py:21-23 */
+    for (int d = 0; d < NDOF; ++d) x[d] = sq_f(dp[d] - c->default_dof_pos[d]);
+    tv[GO1_T_DOF_POS] = sum12_legs(x); /* :31-33 */
+  }
+  tv[GO1_T_BASE_HEIGHT] = sq_f(root[2] - c->base_height_target);
+  tv[GO1_T_ANG_VEL_XY] = sq_f(bav[0]) + sq_f(bav[1]);
+  tv[GO1_T_ORIENTATION] = sq_f(pg[0]) + sq_f(pg[1]);
+  float vxy2 = sq_f(blv[0]) + sq_f(blv[1]);
+  float vmag = norm2_f(blv[0], blv[1]);
+  tv[GO1_T_LARGE_VEL] = vxy2 * (vmag > 0.5f ? 1.0f : 0.0f); /* reward_crawling.py:53-56 */
+  tv[GO1_T_LIN_VEL_Z] = sq_f(blv[2]);
+  tv[GO1_T_REACHING_Z] = sq_f(rel_lin[2]);
+  tv[GO1_T_REACHING_ROLL] = sq_f(rel_rot[0]);
+  tv[GO1_T_REACHING_PITCH] = sq_f(rel_rot[1]);
+  tv[GO1_T_REACHING_YAW_ABS] = sq_f(rel_rot[2]);
+  tv[GO1_T_SURVIVE] = 1.0f;
+  tv[GO1_T_REACH_GOAL] = reached ? 1.0f : 0.0f;
+  tv[GO1_T_REACH_GOAL_T] = (reached ? 1.0f : 0.0f) * (float)ep;
+  tv[GO1_T_REACH_GOAL_TR] = (reached ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
+  tv[GO1_T_LINEAR_VEL] = norm3_f(blv[0], blv[1], blv[2]) > 0.7f ? 1.0f : 0.0f;
+  {
+    float mag = rel_norm;
     /* e2e (reward_crawling.py:61-77) */
-    float mag = norm2_f(rel_lin[0], rel_lin[1]);
-    float lerr = sq_f(blv[0]) + sq_f(blv[1]);
-    float r_e2e = expf(-lerr / c->tracking_sigma_lin);
-    terms[7] = r_e2e * (mag < c->switch_dist ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
-    /* exploration_lin (:79-94) */
+    if (c->terminate_end_of_trajectory) {
+      tv[GO1_T_E2E] = (mag < c->switch_dist ? 1.0f : 0.0f) * c->max_episode_length;
+    } else {
+      float r_e2e = expf(-vxy2 / c->tracking_sigma_lin);
+      tv[GO1_T_E2E] = r_e2e * (mag < c->switch_dist ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
+    }
+    /* target velocity towards the waypoint (reward_crawling.py:83-87) */
     float tx = rel_lin[0] / (mag + 1e-6f) * c->target_lin_vel;
     float ty = rel_lin[1] / (mag + 1e-6f) * c->target_lin_vel;
     float gate = mag > c->lin_reaching_criterion ? 1.0f : 0.0f;
     tx = tx * gate;
     ty = ty * gate;
     float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
-    terms[8] = expf(-le / c->tracking_sigma_lin);
-    /* exploration_yaw (:110-120) */
+    /* exploration_lin (reward_crawling.py:79-108) / reaching_linear_vel */
+    if (c->lin_vel_form == 1) {
+      tv[GO1_T_EXPLORATION_LIN] = fabsf(tx - blv[0]) + fabsf(ty - blv[1]);
+    } else if (c->lin_vel_form == 2) {
+      tv[GO1_T_EXPLORATION_LIN] = le;
+    } else if (c->lin_vel_form == 3) {
+      float rx = tx / c->target_lin_vel * blv[0] / (vmag + 1e-6f);
+      float ry = ty / c->target_lin_vel * blv[1] / (vmag + 1e-6f);
+      float r = rx + ry;
+      r = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
+      r = r + expf(-(vmag * vmag) / c->tracking_sigma_lin) * (mag < c->lin_reaching_criterion ? 1.0f : 0.0f);
+      tv[GO1_T_EXPLORATION_LIN] = r;
+    } else {
+      tv[GO1_T_EXPLORATION_LIN] = expf(-le / c->tracking_sigma_lin);
+    }
+    /* task (trajectory_tracking_reward.py:74-89), task_old (:51-55) */
+    tv[GO1_T_TASK] = expf(-le / c->tracking_sigma_lin) * (mag < c->large_dist_threshold ? 1.0f : 0.0f);
+    {
+      float r = 0.5f / (0.5f + mag) / c->t_reach;
+      tv[GO1_T_TASK_OLD] = r * ((float)ep > c->t_reach ? 1.0f : 0.0f);
+    }
+    /* exploration (:91-99) */
+    {
+      float r = blv[0] * rel_lin[0] + blv[1] * rel_lin[1];
+      r = r / (mag + 1e-6f);
+      r = r / (vmag + 1e-6f);
+      tv[GO1_T_EXPLORATION] = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
+    }
+    /* stalling (:105-108) */
+    tv[GO1_T_STALLING] = -((vmag < c->small_vel_threshold && mag > c->large_dist_threshold) ? 1.0f : 0.0f);
+  }
+  {
+    /* exploration_yaw (reward_crawling.py:110-120) / reaching_yaw */
     float ta = rel_rot[2];
     float m = fabsf(ta);
     ta = ta / (m + 1e-6f) * c->target_ang_vel;
     ta = ta * (m > c->ang_reaching_criterion ? 1.0f : 0.0f);
     float ae = sq_f(ta - bav[2]);
-    terms[9] = expf(-ae / c->tracking_sigma_ang);
+    tv[GO1_T_EXPLORATION_YAW] = expf(-ae / c->tracking_sigma_ang);
+  }
+  if (c->term_mask & (1u << GO1_T_FEET_AIR_TIME)) {
+    /* feet_air_time (trajectory_tracking_reward.py:126-137): mutates last_contacts / feet_air_time */
+    float* air = st->feet_air_time + (size_t)e * 4;
+    float* lc = st->last_contacts + (size_t)e * 4;
+    float rl[4];
+    for (int l = 0; l < 4; ++l) {
+      int contact = cf[(4 + 4 * l) * 3 + 2] > 1.0f;
+      int filt = contact || lc[l] != 0.0f;
+      lc[l] = contact ? 1.0f : 0.0f;
+      int first = air[l] > 0.0f && filt;
+      air[l] = air[l] + c->dt;
+      rl[l] = (air[l] - 0.5f) * (first ? 1.0f : 0.0f);
+      air[l] = air[l] * (filt ? 0.0f : 1.0f);
+    }
+    tv[GO1_T_FEET_AIR_TIME] = (rl[0] + rl[1]) + (rl[2] + rl[3]); /* the HIP kernel's quad-sum order */
   }
   if (diverged) /* nothing of a diverged state reaches an output */
-    for (int k2 = 0; k2 < GO1_NUM_TERMS; ++k2) terms[k2] = 0.0f;
-  if (a->dbg_terms) memcpy(a->dbg_terms + (size_t)e * GO1_NUM_TERMS, terms, sizeof(terms));
+    memset(tv, 0, sizeof(tv));
+  /* slot order (reward_scales order); pos / neg by the sign of the scale for sign-definite terms,
+   * by the sign of the sum over envs (second pass, go1o_step) when some slot is indefinite */
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
-  float* sums = st->episode_sums + (size_t)e * GO1_NUM_SUMS;
-  for (int k = 0; k < GO1_NUM_TERMS; ++k) {
-    float r = terms[k] * a->reward_scales[k];
+  float* sums = st->episode_sums + (size_t)e * NS;
+  for (int k = 0; k < NT; ++k) {
+    int id = c->term_ids[k];
+    float t = id == GO1_T_NONE ? 0.0f : tv[id];
+    if (a->dbg_terms) a->dbg_terms[(size_t)e * GO1_MAX_TERMS + k] = t;
+    if (id == GO1_T_NONE) continue;
+    float r = t * a->reward_scales[k];
     rew = rew + r;
-    /* sign of torch.sum(rew) == sign of the scale for these sign-definite terms */
     if (a->reward_scales[k] >= 0.0f) pos = pos + r; else neg = neg + r;
     sums[k] = sums[k] + r;
+    if (r_slots) r_slots[(size_t)e * GO1_MAX_TERMS + k] = r;
   }
-  sums[10] = sums[10] + rew;
-  sums[11] = sums[11] + pos;
-  sums[12] = sums[12] + neg;
+  if (c->reward_mode == 1) rew = rew < 0.0f ? 0.0f : rew;                /* (:341-342) */
+  else if (c->reward_mode == 2) rew = pos * expf(neg / c->sigma_rew_neg); /* (:343-344) */
+  if (!c->indefinite_slots) {
+    sums[NT] = sums[NT] + rew;
+    sums[NT + 1] = sums[NT + 1] + pos;
+    sums[NT + 2] = sums[NT + 2] + neg;
+  } else if (c->reward_mode != 2) {
+    sums[NT] = sums[NT] + rew;
+  }
 
   /* reset_idx (:218-296) for this env.  self.commands is a VIEW of
    * local_relative_linear[:, :2] (:802), which reset_idx zeroes in place (:252),
    * so a reset env observes a zero command this step. */
-  if (a->episode_log && !reset) a->episode_log[(size_t)e * GO1_EPISODE_LOG + 13] = 0.0f;
+  const int LOGW = NT + 6;
+  if (a->episode_log && !reset) a->episode_log[(size_t)e * LOGW + NS] = 0.0f;
   if (reset && a->episode_log) { /* reset_idx logging (:256-271) */
-    float* lg = a->episode_log + (size_t)e * GO1_EPISODE_LOG;
-    for (int k2 = 0; k2 < GO1_NUM_SUMS; ++k2) lg[k2] = sums[k2];
-    lg[13] = (float)ep;
-    lg[14] = reached ? 1.0f : 0.0f;
-    lg[15] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+    float* lg = a->episode_log + (size_t)e * LOGW;
+    for (int k2 = 0; k2 < NS; ++k2) lg[k2] = sums[k2];
+    lg[NS] = (float)ep;
+    lg[NS + 1] = reached ? 1.0f : 0.0f;
+    lg[NS + 2] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
   }
   if (reset) {
     reset_env(c, st, ter, e, a, U);
     cmd[0] = 0.0f;
     cmd[1] = 0.0f;
     if (diverged) { /* a diverged env observes (and stores as its pitch) its post-reset pose */
-      post_kin(root, a->gravity_vec, st->trajectory + (size_t)e * 6, blv, bav, pg, rel_lin, rpy, rel_rot);
+      post_kin(root, a->gravity_vec, st->trajectory + (size_t)e * 6 * TL, blv, bav, pg, rel_lin, rpy, rel_rot);
       for (int i = 0; i < 3; ++i) brot[i] = rpy[i];
     }
   }
   if (a->dbg_commands) { a->dbg_commands[e * 2] = cmd[0]; a->dbg_commands[e * 2 + 1] = cmd[1]; }
 
-  /* compute_observations (:357-475) -- post-reset dof/root, pre-reset gravity/cmd/heights */
-  float* o = a->obs + (size_t)e * GO1_NUM_OBS;
+  /* compute_observations (:357-475) -- post-reset dof/root/episode length, pre-reset gravity/cmd/heights */
+  const int NO = c->num_obs;
+  float* o = a->obs + (size_t)e * NO;
   o[0] = pg[0]; o[1] = pg[1]; o[2] = pg[2];
   o[3] = cmd[0] * 1.0f; o[4] = cmd[1] * 1.0f;
   for (int d = 0; d < NDOF; ++d) {
@@ -1062,36 +1194,39 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     o[17 + d] = dv[d] * c->obs_scale_dof_vel;
     o[29 + d] = act[d];
   }
-  int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
   int k = 41;
-  float zroot = root[2];
-  float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
-  for (int layer = 0; layer < 2; ++layer)
-    for (int i = x_start; i < GO1_GRID_X; ++i)
-      for (int j = 0; j < GO1_GRID_Y; ++j) {
-        float h = heights[layer][i][j];
-        if (c->camera_zero) {
-          h = h - zroot;
-          h = h - cam_z;
-          h = h < -0.3f ? -0.3f : (h > 0.3f ? 0.3f : h);
-        } else {
-          h = h < 0.0f ? 0.0f : (h > c->ceiling_height ? c->ceiling_height : h);
-          h = h / c->ceiling_height;
-          h = h - 0.5f;
+  if (c->timestep_in_obs) o[k++] = (float)st->episode_length[e] / c->max_episode_length; /* (:375-377) */
+  if (c->observe_heights) {
+    int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
+    float zroot = root[2];
+    float cam_z = pm_sinf(cam_pitch) * c->camera_offset_norm;
+    for (int layer = 0; layer < 2; ++layer)
+      for (int i = x_start; i < GO1_GRID_X; ++i)
+        for (int j = 0; j < GO1_GRID_Y; ++j) {
+          float h = heights[layer][i][j];
+          if (c->camera_zero) {
+            h = h - zroot;
+            h = h - cam_z;
+            h = h < -0.3f ? -0.3f : (h > 0.3f ? 0.3f : h);
+          } else {
+            h = h < 0.0f ? 0.0f : (h > c->ceiling_height ? c->ceiling_height : h);
+            h = h / c->ceiling_height;
+            h = h - 0.5f;
+          }
+          o[k++] = h * c->obs_scale_heights;
         }
-        o[k++] = h * c->obs_scale_heights;
-      }
+  }
   if (c->add_noise) {
-    for (int i = 0; i < GO1_NUM_OBS; ++i) {
+    for (int i = 0; i < NO; ++i) {
       float nv = 0.0f;
       if (i < 3) nv = c->noise_gravity;
       else if (i >= 5 && i < 17) nv = c->noise_dof_pos;
       else if (i >= 17 && i < 29) nv = c->noise_dof_vel;
-      float u = draw(a, U, c->env_id_offset, e, 47 + i);
+      float u = draw(c, a, U, e, GO1_U_NOISE + i);
       o[i] = o[i] + (2.0f * u - 1.0f) * nv;
     }
   }
-  for (int i = 0; i < GO1_NUM_OBS; ++i) {
+  for (int i = 0; i < NO; ++i) {
     float v = o[i];
     o[i] = v < -c->clip_obs ? -c->clip_obs : (v > c->clip_obs ? c->clip_obs : v);
   }
@@ -1123,13 +1258,45 @@ int go1o_step(const go1_config* c, const go1_state* st, const go1_terrain* ter, 
   Model M;
   load_model(c, &M);
   int any = 0;
+  const int n = c->n_envs;
+  float* r_slots = c->indefinite_slots ? (float*)calloc((size_t)n * GO1_MAX_TERMS, sizeof(float)) : NULL;
 #pragma omp parallel for schedule(static) reduction(| : any)
-  for (int e = 0; e < c->n_envs; ++e) {
-    step_env(c, &M, st, ter, a, e);
+  for (int e = 0; e < n; ++e) {
+    step_env(c, &M, st, ter, a, e, r_slots);
     any |= a->reset[e];
   }
+  if (r_slots) {
+    /* global pos / neg buckets (:330-336): sign of the sum of each slot over all envs */
+    const int NT = c->n_terms, NS = NT + 3;
+    double S[GO1_MAX_TERMS];
+    for (int k = 0; k < NT; ++k) {
+      S[k] = 0.0;
+      for (int e = 0; e < n; ++e) S[k] += r_slots[(size_t)e * GO1_MAX_TERMS + k];
+    }
+    for (int e = 0; e < n; ++e) {
+      float pos = 0.0f, neg = 0.0f;
+      for (int k = 0; k < NT; ++k) {
+        if (c->term_ids[k] == GO1_T_NONE) continue;
+        float r = r_slots[(size_t)e * GO1_MAX_TERMS + k];
+        if (S[k] >= 0.0) pos = pos + r;
+        else if (S[k] <= 0.0) neg = neg + r;
+      }
+      float* t = a->reset[e] ? (a->episode_log ? a->episode_log + (size_t)e * (NT + 6) + NT : NULL)
+                             : st->episode_sums + (size_t)e * NS + NT;
+      if (c->reward_mode == 2) {
+        float rw = pos * expf(neg / c->sigma_rew_neg);
+        a->rew[e] = rw;
+        if (t) t[0] = t[0] + rw;
+      }
+      if (t) {
+        t[1] = t[1] + pos;
+        t[2] = t[2] + neg;
+      }
+    }
+    free(r_slots);
+  }
   if (a->extras_time_outs && any)
-    for (int e = 0; e < c->n_envs; ++e) a->extras_time_outs[e] = a->time_out[e];
+    for (int e = 0; e < n; ++e) a->extras_time_outs[e] = a->time_out[e];
   return 0;
 }
 

@@ -44,13 +44,20 @@ def lib(precision="f64"):
     return _lib
 
 
-class NpState:
-    """Numpy SoA state matching go1_state."""
+class _Readme:
+    """Plane widths of the README configuration (10 reward terms, one waypoint)."""
+    n_terms = 10
+    traj_length = 1
 
-    def __init__(self, n, init=None):
+
+class NpState:
+    """Numpy SoA state matching go1_state (plane widths from `cfg`: a go1_config)."""
+
+    def __init__(self, n, init=None, cfg=None):
         self.n = n
+        self.cfg = cfg if cfg is not None else _Readme
         self.arrays = {}
-        for name, w, dt in abi.STATE_SPEC:
+        for name, w, dt in abi.state_spec(self.cfg):
             a = np.zeros((n, w), np.float32 if dt == "f32" else np.int32)
             if init is not None and name in init:
                 src = np.asarray(init[name])
@@ -64,7 +71,7 @@ class NpState:
         return self.arrays[k]
 
     def copy(self):
-        s = NpState(self.n)
+        s = NpState(self.n, cfg=self.cfg)
         for k, v in self.arrays.items():
             s.arrays[k] = v.copy()
         return s
@@ -88,14 +95,15 @@ def step(cfg, state, terrain, actions, gravity_vec, sim_gravity, reward_scales, 
     """One oracle step; mutates `state`; returns a dict of outputs.  precision="f32" runs the
     f32-integrator build (CPU timing baseline only)."""
     n = cfg.n_envs
-    out = dict(obs=np.zeros((n, abi.GO1_NUM_OBS), np.float32), priv=np.zeros((n, 2), np.float32),
+    out = dict(obs=np.zeros((n, cfg.num_obs), np.float32), priv=np.zeros((n, 2), np.float32),
                rew=np.zeros(n, np.float32), reset=np.zeros(n, np.uint8), time_out=np.zeros(n, np.uint8),
                contact_forces=np.zeros((n, 17, 3), np.float32))
     if debug:
         out.update(torques=np.zeros((cfg.decimation, n, 12), np.float32),
-                   heights=np.zeros((n, 2, 21, 11), np.float32), terms=np.zeros((n, 10), np.float32),
+                   heights=np.zeros((n, 2, 21, 11), np.float32),
+                   terms=np.zeros((n, abi.GO1_MAX_TERMS), np.float32),
                    commands=np.zeros((n, 2), np.float32), reached=np.zeros(n, np.uint8),
-                   episode_log=np.full((n, abi.GO1_EPISODE_LOG), np.nan, np.float32),
+                   episode_log=np.full((n, abi.episode_log_width(cfg.n_terms)), np.nan, np.float32),
                    aux=np.zeros((n, abi.GO1_AUX), np.float32))
     actions = np.ascontiguousarray(actions, np.float32)
     keep = [actions]
@@ -104,11 +112,14 @@ def step(cfg, state, terrain, actions, gravity_vec, sim_gravity, reward_scales, 
     for i in range(3):
         a.gravity_vec[i] = float(gravity_vec[i])
         a.sim_gravity[i] = float(sim_gravity[i])
-    for i in range(abi.GO1_NUM_TERMS):
-        a.reward_scales[i] = float(reward_scales[i])
+    rs = np.zeros(abi.GO1_MAX_TERMS, np.float32)
+    rs[:len(reward_scales)] = np.asarray(reward_scales, np.float32)
+    for i in range(abi.GO1_MAX_TERMS):
+        a.reward_scales[i] = float(rs[i])
     a.rng_seed, a.rng_step = rng_seed, rng_step
     if uniforms is not None:
         u = np.ascontiguousarray(uniforms, np.float32)
+        assert u.shape == (n, cfg.u_per_env), (u.shape, cfg.u_per_env)
         keep.append(u)
         a.uniforms = abi.ptr(u)
     if inj is not None:

@@ -12,8 +12,8 @@ from oracle import oracle as O
 
 
 class _State:
-    def __init__(self, n):
-        self.np = O.NpState(n)
+    def __init__(self, n, cfg):
+        self.np = O.NpState(n, cfg=cfg)
         self.t = {k: torch.from_numpy(v) for k, v in self.np.arrays.items()}
 
     def __getitem__(self, k):
@@ -33,7 +33,7 @@ class OracleBackend:
         self.cfg = cfg
         self.n = n = cfg.n_envs
         self.device = torch.device("cpu")
-        self.state = _State(n)
+        self.state = _State(n, cfg)
         self.contact_forces = torch.zeros((n, 17, 3))
         self.extras_time_outs = torch.zeros(n, dtype=torch.bool)
         self.ter = None
@@ -61,7 +61,7 @@ class OracleBackend:
         if episode_log is not None:
             el = o["episode_log"]
             rs = o["reset"].astype(bool)
-            episode_log[~torch.from_numpy(rs), 13] = 0.0
+            episode_log[~torch.from_numpy(rs), self.cfg.n_terms + 3] = 0.0
             episode_log[torch.from_numpy(rs)] = torch.from_numpy(el[rs])
         if aux is not None:
             aux.copy_(torch.from_numpy(o["aux"]))

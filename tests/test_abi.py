@@ -47,7 +47,8 @@ def test_argument_errors_are_reported_not_thrown():
 def test_oracle_library_builds_and_loads():
     from oracle import oracle as O
     O.lib()
-    assert O.lib().go1o_abi_version() == 2
+    assert O.lib().go1o_abi_version() == abi.GO1_ABI_VERSION
+    assert O.lib("f32").go1o_abi_version() == abi.GO1_ABI_VERSION
 
 
 def test_compiled_model_constants_match_model_block():

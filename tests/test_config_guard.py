@@ -1,0 +1,99 @@
+"""Cfg values the HIP step does not implement raise instead of silently training on other
+rewards / targets / observations (ADVICE high); the implemented train.py
+variants map onto the C ABI's config fields."""
+import numpy as np
+import pytest
+
+from legged_tracking_amd import abi, config as CF
+
+
+def _abi(argv=(), n=32, **over):
+    cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=4, cols=4, extra_argv=argv)
+    for path, v in over.items():
+        obj = cfg
+        parts = path.split(".")
+        for p in parts[:-1]:
+            obj = getattr(obj, p)
+        setattr(obj, parts[-1], v)
+    return CF.build_abi_config(cfg, n_envs=n)
+
+
+@pytest.mark.parametrize("argv, over, exc, text", [
+    (("--command_type", "6dof"), {}, NotImplementedError, "command_type"),
+    (("--command_type", "xy_norm"), {}, NotImplementedError, "command_type"),
+    ((), {"commands.sampling_based_planning": True}, NotImplementedError, "sampling_based_planning"),
+    ((), {"commands.traj_function": "valid_goal"}, NotImplementedError, "traj_function"),
+    ((), {"commands.switch_upon_reach": False}, NotImplementedError, "switch_upon_reach"),
+    ((), {"control.control_type": "P"}, NotImplementedError, "control_type"),
+    ((), {"domain_rand.push_robots": True}, NotImplementedError, "push_robots"),
+    ((), {"env.observe_vel": True}, NotImplementedError, "observe_vel"),
+    ((), {"terrain.terrain_type": "multi_path"}, NotImplementedError, "terrain_type"),
+    ((), {"rewards.reward_container_name": "CoRLRewards"}, NotImplementedError, "reward_container_name"),
+    ((), {"reward_scales.termination": -1.0}, AttributeError, "_reward_termination"),
+    ((), {"env.num_observations": 262}, AssertionError, "num_observations"),
+    ((), {"rewards.reward_container_name": "TrajectoryTrackingRewards", "rewards.lin_vel_form": "prod",
+          "reward_scales.reaching_linear_vel": 1.0}, TypeError, "prod"),
+    ((), {"rewards.reward_container_name": "TrajectoryTrackingRewards", "reward_scales.reaching_local_goal": 1.0},
+     NotImplementedError, "reaching_local_goal"),
+    ((), {"rewards.reward_container_name": "TrajectoryTrackingRewards", "reward_scales.stalling": 1.0},
+     AttributeError, "large_dist_threshold"),
+])
+def test_unimplemented_values_raise(argv, over, exc, text):
+    with pytest.raises(exc, match=text):
+        _abi(argv, **over)
+
+
+def test_more_reward_terms_than_slots_raise():
+    over = {f"reward_scales.{k}": 0.1 for k in ("orientation", "large_vel", "reaching_z", "reaching_roll",
+                                                 "reaching_pitch", "a1", "a2")}
+    with pytest.raises(NotImplementedError, match="nonzero reward scales"):
+        _abi((), **over)
+
+
+def test_readme_config_layout():
+    c = _abi()
+    assert c.n_terms == 10 and c.num_obs == 261 and c.u_per_env == 308 and c.traj_length == 1
+    names = list(CF.derived(CF.readme_config(n_envs=32, rows=4, cols=4))["reward_scales"])
+    assert [abi.TERM_IDS[k] for k in names] == list(c.term_ids[:10])
+    assert c.reward_mode == 0 and c.lin_vel_form == 0 and c.indefinite_slots == 0
+
+
+def test_train_flags_map_onto_the_abi():
+    assert _abi(("--only_positive",)).reward_mode == 1
+    assert _abi((), **{"rewards.only_positive_rewards_ji22_style": True}).reward_mode == 2
+    c = _abi(("--lin_vel_form", "prod"))
+    assert c.lin_vel_form == 3 and c.indefinite_slots == 1 << 8  # exploration_lin is slot 8
+    assert _abi(("--lin_vel_form", "l1")).lin_vel_form == 1
+    c = _abi(("--terminate_after_reach", "--rotate_camera", "--timestep_in_obs"))
+    assert (c.terminate_end_of_trajectory, c.rotate_camera, c.timestep_in_obs, c.num_obs) == (1, 1, 1, 262)
+    c = _abi(("--random_target",))
+    assert (c.traj_kind, c.traj_length, c.u_per_env) == (1, 10, 47 + 261 + 66)
+    c = _abi(("--blind",))
+    assert c.observe_heights == 0 and c.num_obs == 41
+    c = _abi(("--r_orientation", "0.5", "--r_large_vel", "0.2", "--strategy", "vel"))
+    names = list(CF.derived(CF.readme_config(n_envs=32, rows=4, cols=4, extra_argv=(
+        "--r_orientation", "0.5", "--r_large_vel", "0.2", "--strategy", "vel")))["reward_scales"])
+    assert "e2e" not in names and "orientation" in names and c.n_terms == len(names) == 11
+
+
+def test_default_reference_cfg_is_only_positive():
+    """make_cfg() + config_go1 without train.py keeps the reference default only_positive_rewards=True
+    (config.py:259): the HIP step now implements it instead of ignoring it."""
+    C = CF.make_cfg()
+    CF.config_go1(C)
+    assert C.rewards.only_positive_rewards is True
+    assert not [b for b in CF.unsupported(C) if b[0] == "rewards.only_positive_rewards"]
+
+
+def test_trajectory_tracking_container_maps_names():
+    names, ids, indef = CF.reward_slots(CF.readme_config(n_envs=32, rows=4, cols=4), {
+        "torques": 1.0, "base_height": 1.0, "feet_air_time": 1.0, "reaching_linear_vel": 1.0, "exploration": 1.0})
+    assert ids[:2] == [abi.TERM_IDS["torques"], abi.TERM_IDS["base_height"]]  # RewardsCrawling by default
+    cfg = CF.readme_config(n_envs=32, rows=4, cols=4)
+    cfg.rewards.reward_container_name = "TrajectoryTrackingRewards"
+    names, ids, indef = CF.reward_slots(cfg, {"torques": 1.0, "base_height": 1.0, "feet_air_time": 1.0,
+                                              "reaching_linear_vel": 1.0, "exploration": 1.0})
+    assert ids == [abi.TERM_IDS["torques"], abi.GO1_T_NONE, abi.TERM_IDS["feet_air_time"],
+                   abi.TERM_IDS["exploration_lin"], abi.TERM_IDS["exploration"]]
+    assert indef == (1 << 2) | (1 << 4)
+    assert np.array_equal(CF.reward_scale_vector({"a": 2.0, "b": 3.0})[:3], [2.0, 3.0, 0.0])

@@ -22,7 +22,12 @@ from legged_tracking_amd import config as CF, native, terrain as T  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from tests import golden_io as G  # noqa: E402
 
-FIXTURES = ["step_single_path.npz", "step_plane.npz", "step_single_path_events.npz"]
+import os  # noqa: E402
+
+from legged_tracking_amd import abi  # noqa: E402
+
+# the README fixtures and every variant (train.py flags / reward containers, tests/golden/make_golden.py)
+FIXTURES = sorted(f for f in os.listdir(G.GOLDEN) if f.startswith("step_") and f.endswith(".npz"))
 DEV = "cuda:0"
 
 
@@ -65,10 +70,11 @@ def test_fused_step_replays_reference_fixture(name):
     g = native.Go1Native(c, DEV)
     g.set_terrain(ter.tiles, ter.env_tile, ter.eto, ter.eo)
     dbg = native.debug_buffers(n, c.decimation, DEV)
-    elog = torch.full((n, 16), float("nan"), device=DEV)
+    ns = c.n_terms + 3
+    elog = torch.full((n, abi.episode_log_width(c.n_terms)), float("nan"), device=DEV)
     aux = torch.zeros((n, 32), device=DEV)
     for t in range(int(d["meta/n_steps"])):
-        st = G.state_at(d, t, "pre")
+        st = G.state_at(d, t, "pre", c)
         g.state.load(st.arrays)
         inp = G.step_inputs(d, t)
         inj = {k: _dev(v, torch.float32) for k, v in inp["inj"].items()}
@@ -95,11 +101,13 @@ def test_fused_step_replays_reference_fixture(name):
         np.testing.assert_array_equal(obs, oo["obs"])
         np.testing.assert_array_equal(g.priv.cpu().numpy(), oo["priv"])
         np.testing.assert_allclose(g.rew.cpu().numpy(), oo["rew"], rtol=2e-6, atol=1e-9)
+        np.testing.assert_allclose(dbg["terms"].cpu().numpy()[:, :c.n_terms], oo["terms"][:, :c.n_terms], rtol=2e-6,
+                                   atol=1e-9)
         # reset_idx logging rows (NaN elsewhere) and the step extras
         rs = d[f"s{t}/reset"].astype(bool)
         el = elog.cpu().numpy()
-        assert (el[~rs][:, 13] == 0).all()
-        np.testing.assert_array_equal(el[rs][:, 13:15], oo["episode_log"][rs][:, 13:15])
+        assert (el[~rs][:, ns] == 0).all()
+        np.testing.assert_array_equal(el[rs][:, ns:ns + 2], oo["episode_log"][rs][:, ns:ns + 2])
         np.testing.assert_allclose(el[rs], oo["episode_log"][rs], rtol=2e-6, atol=1e-8)
         ax = aux.cpu().numpy()
         np.testing.assert_array_equal(ax[:, :8], oo["aux"][:, :8])
@@ -132,7 +140,7 @@ def _sim_setup(n, terrain="single_path", seed=0):
     c = CF.build_abi_config(cfg)
     td = T.build(cfg, n, np.random.RandomState(11))
     ter = O.NpTerrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
-    st = O.NpState(n)
+    st = O.NpState(n, cfg=c)
     rng = np.random.default_rng(seed)
     st["friction"][:, 0] = rng.uniform(0.1, 3.0, n)
     st["restitution"][:, 0] = rng.uniform(0.0, 0.4, n)
@@ -185,7 +193,7 @@ def test_native_integrator_step_vs_f64_oracle(terrain):
         agree = (g.reset.cpu().numpy() == out["reset"].astype(bool)).mean()
         assert agree > 0.98
         # continue both from the GPU state so the comparison stays one-step
-        st = O.NpState(n, gs)
+        st = O.NpState(n, gs, c)
 
 
 def test_philox_streams_match_oracle():
