@@ -185,6 +185,7 @@ def kernel_loop(env, ring, steps, warmup, every=4):
     dt = time.perf_counter() - t0
     kt = [ev.ms(i) for i in range((steps + every - 1) // every)]
     ev.close()
+    kernel_loop.last = kt
     return dt, float(np.mean(kt))
 
 
@@ -327,6 +328,7 @@ def main():
                     help="record the HIP event pair around every k-th step kernel of the timed loop")
     ap.add_argument("--sweep", default="", help="comma-separated envs/GPU for an extra size sweep (e.g. 16384,65536)")
     ap.add_argument("--selftest", action="store_true", help="CPU-only launcher test (gloo, no GPU work)")
+    ap.add_argument("--kernel-only", action="store_true", help="A/B helper: time only the fused kernel")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -341,6 +343,16 @@ def main():
 
     import torch
     dev = torch.device("cuda", local)
+    if args.kernel_only:  # A/B helper: the fused kernel alone, HIP-event statistics
+        torch.cuda.set_device(dev)
+        env = make_env(args.envs_per_gpu, 0, 1, dev)
+        env.reset()
+        ring = torch.randn((64, args.envs_per_gpu, 12), device=dev)
+        kdt, kms = kernel_loop(env, ring, args.steps, args.warmup, every=1)
+        kt = np.array(kernel_loop.last)
+        print(json.dumps({"kernel_ms_mean": kms, "kernel_ms_median": float(np.median(kt)),
+                          "kernel_ms_p10": float(np.percentile(kt, 10)), "loop_ms_per_step": kdt / args.steps * 1e3}))
+        return
     if args.rollout_only:
         torch.cuda.set_device(dev)
         print(json.dumps(rollout_rate(args.envs_per_gpu, dev, args.steps, args.warmup)))

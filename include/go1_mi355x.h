@@ -132,6 +132,7 @@ typedef struct go1_config {
   uint32_t indefinite_slots;   /* bit k: reward slot k has no fixed sign (exploration, feet_air_time, the prod
                                   form of exploration_lin): its pos / neg bucket is the sign of the sum over
                                   all envs (:332-335), applied by a second launch (go1_step) */
+  uint32_t live_slots;         /* bit k: slot k < n_terms has a reward function (term_ids[k] != GO1_T_NONE) */
   float sigma_rew_neg;         /* ji22 style */
   float small_vel_threshold, large_dist_threshold;
   float traj_x_range, traj_y_range, traj_z_range, traj_roll_range, traj_pitch_range, traj_yaw_range;

@@ -49,7 +49,7 @@ class Go1Config(C.Structure):
         ("lin_vel_form", I32), ("terminate_end_of_trajectory", I32), ("use_terminal_body_rotation", I32),
         ("rotate_camera", I32), ("observe_heights", I32), ("timestep_in_obs", I32), ("num_obs", I32),
         ("u_per_env", I32), ("traj_kind", I32), ("traj_length", I32), ("traj_interp", I32),
-        ("indefinite_slots", C.c_uint32),
+        ("indefinite_slots", C.c_uint32), ("live_slots", C.c_uint32),
         ("sigma_rew_neg", F), ("small_vel_threshold", F), ("large_dist_threshold", F),
         ("traj_x_range", F), ("traj_y_range", F), ("traj_z_range", F), ("traj_roll_range", F),
         ("traj_pitch_range", F), ("traj_yaw_range", F), ("traj_x_mean", F), ("traj_y_mean", F),

@@ -868,6 +868,7 @@ def build_abi_config(cfg, n_envs=None, physics=None, actuator=None, hf_shape=(80
         c.term_ids[k] = abi.GO1_T_NONE
     c.term_mask = sum(1 << t for t in set(ids) if t != abi.GO1_T_NONE)
     c.indefinite_slots = indef
+    c.live_slots = sum(1 << k for k, t in enumerate(ids) if t != abi.GO1_T_NONE)
     rw = cfg.rewards
     c.reward_mode = 1 if rw.only_positive_rewards else (2 if _get(cfg, "rewards.only_positive_rewards_ji22_style",
                                                                    False) else 0)

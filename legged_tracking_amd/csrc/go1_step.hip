@@ -1602,7 +1602,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int coll_in = st.collision_count[e];
   const float restitution = st.restitution[e];
   const int TL = c->traj_length, NT = c->n_terms, NS = NT + 3;
-  float traj_in[6], ldv[3], la[3], sums[GO1_MAX_TERMS], tot[3];
+  float traj_in[6], ldv[3], la[3];
   {
     // the current waypoint trajectories[e, curr_pose_index[e]] (:850-853); traj_length 1 needs no index
     const float* trj = st.trajectory + (size_t)e * 6 * TL;
@@ -1615,10 +1615,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     ldv[j] = st.last_dof_vel[d0 + j];
     la[j] = st.last_actions[d0 + j];
   }
-#pragma unroll
-  for (int k = 0; k < GO1_MAX_TERMS; ++k) sums[k] = k < NT ? st.episode_sums[(size_t)e * NS + k] : 0.0f;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) tot[k] = st.episode_sums[(size_t)e * NS + NT + k];
+  // reward slot k (Cfg.reward_scales order) belongs to the env's lane sub16 == k: its term id,
+  // scale and episode sum; lanes 0..2 also carry total, total_pos, total_neg
+  const int my_id = sub16 < NT ? c_gen->term_ids[sub16] : GO1_T_NONE;
+  const float my_scale = A.reward_scales[sub16];
+  float my_sum = sub16 < NT ? st.episode_sums[(size_t)e * NS + sub16] : 0.0f;
+  float my_tot = sub16 < 3 ? st.episode_sums[(size_t)e * NS + NT + sub16] : 0.0f;
   Phys P;
   if (!INJ) {
 #pragma unroll
@@ -1951,134 +1953,115 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // wave's LDS operations complete in order, no barrier.
   __shared__ float s_terms[SEPB][GO1_T_COUNT];
   const uint32_t tm = c->term_mask;
-#define HAS(id) ((tm >> (id)) & 1u)
 #define PUT(id, v)                          \
   do {                                      \
     const float v_ = (v);                   \
     if (sub16 == 0) s_terms[el][(id)] = v_; \
   } while (0)
-  {
-    float x[3];
-    if (HAS(GO1_T_TORQUES)) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) x[j] = sq_f(torque[j]);
-      PUT(GO1_T_TORQUES, qsum((x[0] + x[1]) + x[2]));
-    }
-    if (HAS(GO1_T_DOF_ACC)) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) x[j] = sq_f((ldv[j] - qd[j]) / c->dt);
-      PUT(GO1_T_DOF_ACC, qsum((x[0] + x[1]) + x[2]));
-    }
-    if (HAS(GO1_T_COLLISION)) PUT(GO1_T_COLLISION, coll);
-    if (HAS(GO1_T_ACTION_RATE)) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) x[j] = sq_f(la[j] - act[j]);
-      PUT(GO1_T_ACTION_RATE, qsum((x[0] + x[1]) + x[2]));
-    }
-    if (HAS(GO1_T_DOF_POS_LIMITS)) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int d = leg * 3 + j;
-        const float lo = q[j] - s_phys[LDS_DPL + 2 * d];
-        const float hi = q[j] - s_phys[LDS_DPL + 2 * d + 1];
-        const float o = -(lo < 0.0f ? lo : 0.0f);
-        x[j] = o + (hi > 0.0f ? hi : 0.0f);
-      }
-      PUT(GO1_T_DOF_POS_LIMITS, qsum((x[0] + x[1]) + x[2]));
-    }
-    if (HAS(GO1_T_DOF_VEL)) {  // trajectory_tracking_reward.py:21-23
-#pragma unroll
-      for (int j = 0; j < 3; ++j) x[j] = sq_f(qd[j]);
-      PUT(GO1_T_DOF_VEL, qsum((x[0] + x[1]) + x[2]));
-    }
-    if (HAS(GO1_T_DOF_POS)) {  // trajectory_tracking_reward.py:31-33
-#pragma unroll
-      for (int j = 0; j < 3; ++j) x[j] = sq_f(q[j] - s_phys[LDS_DDP + leg * 3 + j]);
-      PUT(GO1_T_DOF_POS, qsum((x[0] + x[1]) + x[2]));
-    }
-  }
-  if (HAS(GO1_T_BASE_HEIGHT)) PUT(GO1_T_BASE_HEIGHT, sq_f(root[2] - c->base_height_target));
-  if (HAS(GO1_T_ANG_VEL_XY)) PUT(GO1_T_ANG_VEL_XY, sq_f(bav[0]) + sq_f(bav[1]));
-  if (HAS(GO1_T_ORIENTATION)) PUT(GO1_T_ORIENTATION, sq_f(pg[0]) + sq_f(pg[1]));
   const float vxy2 = sq_f(blv[0]) + sq_f(blv[1]);
   const float vmag = norm2_f(blv[0], blv[1]);
-  if (HAS(GO1_T_LARGE_VEL)) PUT(GO1_T_LARGE_VEL, vxy2 * (vmag > 0.5f ? 1.0f : 0.0f));  // reward_crawling.py:53-56
-  if (HAS(GO1_T_LIN_VEL_Z)) PUT(GO1_T_LIN_VEL_Z, sq_f(blv[2]));
-  if (HAS(GO1_T_REACHING_Z)) PUT(GO1_T_REACHING_Z, sq_f(rel_lin[2]));
-  if (HAS(GO1_T_REACHING_ROLL)) PUT(GO1_T_REACHING_ROLL, sq_f(rel_rot[0]));
-  if (HAS(GO1_T_REACHING_PITCH)) PUT(GO1_T_REACHING_PITCH, sq_f(rel_rot[1]));
-  if (HAS(GO1_T_REACHING_YAW_ABS)) PUT(GO1_T_REACHING_YAW_ABS, sq_f(rel_rot[2]));
-  if (HAS(GO1_T_SURVIVE)) PUT(GO1_T_SURVIVE, 1.0f);
-  if (HAS(GO1_T_REACH_GOAL)) PUT(GO1_T_REACH_GOAL, reached ? 1.0f : 0.0f);
-  if (HAS(GO1_T_REACH_GOAL_T)) PUT(GO1_T_REACH_GOAL_T, (reached ? 1.0f : 0.0f) * (float)ep);
-  if (HAS(GO1_T_REACH_GOAL_TR)) PUT(GO1_T_REACH_GOAL_TR, (reached ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f));
-  if (HAS(GO1_T_LINEAR_VEL)) PUT(GO1_T_LINEAR_VEL, norm3_f(blv[0], blv[1], blv[2]) > 0.7f ? 1.0f : 0.0f);
+  const float mag = rel_norm;
+  // the target velocity towards the waypoint (reward_crawling.py:83-87, trajectory_tracking_reward.py:79-85)
+  float tx = rel_lin[0] / (mag + 1e-6f) * c->target_lin_vel;
+  float ty = rel_lin[1] / (mag + 1e-6f) * c->target_lin_vel;
   {
-    const float mag = rel_norm;
-    if (HAS(GO1_T_E2E)) {  // reward_crawling.py:61-77
-      float r;
-      if (c->terminate_end_of_trajectory) {
-        r = (mag < c->switch_dist ? 1.0f : 0.0f) * c->max_episode_length;
-      } else {
-        const float r_e2e = expf(-vxy2 / c->tracking_sigma_lin);
-        r = r_e2e * (mag < c->switch_dist ? 1.0f : 0.0f) * ((float)ep > c->t_reach ? 1.0f : 0.0f);
-      }
-      PUT(GO1_T_E2E, r);
-    }
-    // the target velocity towards the waypoint (reward_crawling.py:83-87, trajectory_tracking_reward.py:79-85)
-    float tx = rel_lin[0] / (mag + 1e-6f) * c->target_lin_vel;
-    float ty = rel_lin[1] / (mag + 1e-6f) * c->target_lin_vel;
     const float gate = mag > c->lin_reaching_criterion ? 1.0f : 0.0f;
     tx = tx * gate;
     ty = ty * gate;
-    if (HAS(GO1_T_EXPLORATION_LIN)) {  // reward_crawling.py:79-108
-      float r;
-      const int form = c->lin_vel_form;
-      if (form == 1) {
-        r = fabsf(tx - blv[0]) + fabsf(ty - blv[1]);
-      } else if (form == 3) {
-        const float rx = tx / c->target_lin_vel * blv[0] / (vmag + 1e-6f);
-        const float ry = ty / c->target_lin_vel * blv[1] / (vmag + 1e-6f);
-        r = rx + ry;
-        r = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
-        r = r + expf(-(vmag * vmag) / c->tracking_sigma_lin) * (mag < c->lin_reaching_criterion ? 1.0f : 0.0f);
-      } else {
-        const float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
-        r = form == 2 ? le : expf(-le / c->tracking_sigma_lin);
-      }
-      PUT(GO1_T_EXPLORATION_LIN, r);
-    }
-    if (HAS(GO1_T_TASK)) {  // trajectory_tracking_reward.py:74-89
-      const float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
-      PUT(GO1_T_TASK, expf(-le / c->tracking_sigma_lin) * (mag < c->large_dist_threshold ? 1.0f : 0.0f));
-    }
-    if (HAS(GO1_T_TASK_OLD)) {  // trajectory_tracking_reward.py:51-55
-      float r = 0.5f / (0.5f + mag) / c->t_reach;
-      r = r * ((float)ep > c->t_reach ? 1.0f : 0.0f);
-      PUT(GO1_T_TASK_OLD, r);
-    }
-    if (HAS(GO1_T_EXPLORATION)) {  // trajectory_tracking_reward.py:91-99
-      float r = blv[0] * rel_lin[0] + blv[1] * rel_lin[1];
-      r = r / (mag + 1e-6f);
-      r = r / (vmag + 1e-6f);
-      r = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
-      PUT(GO1_T_EXPLORATION, r);
-    }
-    if (HAS(GO1_T_STALLING)) {  // trajectory_tracking_reward.py:105-108
-      const bool sv = vmag < c->small_vel_threshold, ld = mag > c->large_dist_threshold;
-      PUT(GO1_T_STALLING, -((sv && ld) ? 1.0f : 0.0f));
-    }
   }
-  if (HAS(GO1_T_EXPLORATION_YAW)) {  // reward_crawling.py:110-120
+  const float le = sq_f(tx - blv[0]) + sq_f(ty - blv[1]);
+  {
+    float x[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = sq_f(torque[j]);
+    PUT(GO1_T_TORQUES, qsum((x[0] + x[1]) + x[2]));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = sq_f((ldv[j] - qd[j]) / c->dt);
+    PUT(GO1_T_DOF_ACC, qsum((x[0] + x[1]) + x[2]));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = sq_f(la[j] - act[j]);
+    PUT(GO1_T_ACTION_RATE, qsum((x[0] + x[1]) + x[2]));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int d = leg * 3 + j;
+      const float lo = q[j] - s_phys[LDS_DPL + 2 * d];
+      const float hi = q[j] - s_phys[LDS_DPL + 2 * d + 1];
+      const float o = -(lo < 0.0f ? lo : 0.0f);
+      x[j] = o + (hi > 0.0f ? hi : 0.0f);
+    }
+    PUT(GO1_T_DOF_POS_LIMITS, qsum((x[0] + x[1]) + x[2]));
+  }
+  PUT(GO1_T_COLLISION, coll);
+  PUT(GO1_T_BASE_HEIGHT, sq_f(root[2] - c->base_height_target));
+  PUT(GO1_T_ANG_VEL_XY, sq_f(bav[0]) + sq_f(bav[1]));
+  PUT(GO1_T_ORIENTATION, sq_f(pg[0]) + sq_f(pg[1]));
+  PUT(GO1_T_LARGE_VEL, vxy2 * (vmag > 0.5f ? 1.0f : 0.0f));  // reward_crawling.py:53-56
+  PUT(GO1_T_LIN_VEL_Z, sq_f(blv[2]));
+  PUT(GO1_T_REACHING_Z, sq_f(rel_lin[2]));
+  PUT(GO1_T_REACHING_ROLL, sq_f(rel_rot[0]));
+  PUT(GO1_T_REACHING_PITCH, sq_f(rel_rot[1]));
+  PUT(GO1_T_REACHING_YAW_ABS, sq_f(rel_rot[2]));
+  PUT(GO1_T_SURVIVE, 1.0f);
+  {
+    const float rch = reached ? 1.0f : 0.0f, after = (float)ep > c->t_reach ? 1.0f : 0.0f;
+    PUT(GO1_T_REACH_GOAL, rch);
+    PUT(GO1_T_REACH_GOAL_T, rch * (float)ep);
+    PUT(GO1_T_REACH_GOAL_TR, rch * after);
+    PUT(GO1_T_LINEAR_VEL, norm3_f(blv[0], blv[1], blv[2]) > 0.7f ? 1.0f : 0.0f);
+    PUT(GO1_T_STALLING, -((vmag < c->small_vel_threshold && mag > c->large_dist_threshold) ? 1.0f : 0.0f));
+    // e2e (reward_crawling.py:61-77)
+    const float r_e2e = expf(-vxy2 / c->tracking_sigma_lin) * (mag < c->switch_dist ? 1.0f : 0.0f) * after;
+    const float r_end = (mag < c->switch_dist ? 1.0f : 0.0f) * c->max_episode_length;
+    PUT(GO1_T_E2E, c->terminate_end_of_trajectory ? r_end : r_e2e);
+  }
+  {  // exploration_lin (reward_crawling.py:79-108) / reaching_linear_vel
+    const int form = c->lin_vel_form;
+    float r = expf(-le / c->tracking_sigma_lin);
+    r = form == 1 ? fabsf(tx - blv[0]) + fabsf(ty - blv[1]) : r;
+    r = form == 2 ? le : r;
+    if (form == 3) {
+      const float rx = tx / c->target_lin_vel * blv[0] / (vmag + 1e-6f);
+      const float ry = ty / c->target_lin_vel * blv[1] / (vmag + 1e-6f);
+      r = rx + ry;
+      r = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
+      r = r + expf(-(vmag * vmag) / c->tracking_sigma_lin) * (mag < c->lin_reaching_criterion ? 1.0f : 0.0f);
+    }
+    PUT(GO1_T_EXPLORATION_LIN, r);
+  }
+  {  // exploration_yaw (reward_crawling.py:110-120) / reaching_yaw
     float ta = rel_rot[2];
     const float m = fabsf(ta);
     ta = ta / (m + 1e-6f) * c->target_ang_vel;
     ta = ta * (m > c->ang_reaching_criterion ? 1.0f : 0.0f);
     PUT(GO1_T_EXPLORATION_YAW, expf(-sq_f(ta - bav[2]) / c->tracking_sigma_ang));
   }
+  // the rest of TrajectoryTrackingRewards, only when one of them is scaled
+  constexpr uint32_t TT_HEAVY = (1u << GO1_T_DOF_VEL) | (1u << GO1_T_DOF_POS) | (1u << GO1_T_TASK) |
+                                (1u << GO1_T_TASK_OLD) | (1u << GO1_T_EXPLORATION);
+  if (tm & TT_HEAVY) {
+    float x[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = sq_f(qd[j]);
+    PUT(GO1_T_DOF_VEL, qsum((x[0] + x[1]) + x[2]));  // trajectory_tracking_reward.py:21-23
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = sq_f(q[j] - s_phys[LDS_DDP + leg * 3 + j]);
+    PUT(GO1_T_DOF_POS, qsum((x[0] + x[1]) + x[2]));  // :31-33
+    // task (:74-89)
+    PUT(GO1_T_TASK, expf(-le / c->tracking_sigma_lin) * (mag < c->large_dist_threshold ? 1.0f : 0.0f));
+    {  // task_old (:51-55)
+      float r = 0.5f / (0.5f + mag) / c->t_reach;
+      PUT(GO1_T_TASK_OLD, r * ((float)ep > c->t_reach ? 1.0f : 0.0f));
+    }
+    {  // exploration (:91-99)
+      float r = blv[0] * rel_lin[0] + blv[1] * rel_lin[1];
+      r = r / (mag + 1e-6f);
+      r = r / (vmag + 1e-6f);
+      PUT(GO1_T_EXPLORATION, r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f));
+    }
+  }
   // feet_air_time (trajectory_tracking_reward.py:126-137) mutates last_contacts / feet_air_time
   float air_new = 0.0f, lc_new = 0.0f;
-  if (HAS(GO1_T_FEET_AIR_TIME)) {
+  if ((tm >> GO1_T_FEET_AIR_TIME) & 1u) {
     float air = st.feet_air_time[(size_t)e * 4 + leg];
     const float lc = st.last_contacts[(size_t)e * 4 + leg];
     const bool contact = cf_leg[8] > 1.0f;  // foot z force
@@ -2091,38 +2074,51 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     PUT(GO1_T_FEET_AIR_TIME, qsum(r));
   }
 #undef PUT
-#undef HAS
-  // slot order: rew_buf += term * scale; pos / neg bucket by the sign of the sum over envs,
-  // which for a sign-definite term is the sign of its scale (:330-336)
+  // slot order: rew_buf += term * scale (:326-340).  Lane k forms slot k's scaled reward and
+  // updates its episode sum; every lane then adds the slots up in order from LDS.  pos / neg bucket
+  // by the sign of the sum over envs, which for a sign-definite term is the sign of its scale.
+  __shared__ float s_r[SEPB][GO1_MAX_TERMS];
   const bool global_buckets = c->indefinite_slots != 0;
+  const bool live = (c->live_slots >> sub16) & 1u;
+  {
+    float t = live ? s_terms[el][my_id] : 0.0f;
+    if (diverged) t = 0.0f;
+    if (A.dbg_terms && sub16 < NT) A.dbg_terms[(size_t)e * GO1_MAX_TERMS + sub16] = t;
+    const float r = t * my_scale;
+    s_r[el][sub16] = r;
+    if (live) my_sum = my_sum + r;
+    if (global_buckets && live) {
+      K.bucket_r[(size_t)e * GO1_MAX_TERMS + sub16] = r;
+      atomicAdd(K.bucket_sum + sub16, (double)r);
+    }
+  }
+  // sign of each slot's scale, as a slot bitmask (every env of the wave has the same scales):
+  // slot k of env 0 is lane 16 (k >> 2) + (k & 3)
+  const uint64_t nonneg = __ballot(my_scale >= 0.0f);
+  const uint32_t posm = (uint32_t)((nonneg & 0xFull) | ((nonneg >> 12) & 0xF0ull) | ((nonneg >> 24) & 0xF00ull) |
+                                   ((nonneg >> 36) & 0xF000ull));
+  const uint32_t livem = c->live_slots;
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
+  {
+    float rr[GO1_MAX_TERMS];
 #pragma unroll
-  for (int k = 0; k < GO1_MAX_TERMS; ++k) {
-    if (k < NT) {
-      const int id = c->term_ids[k];
-      float t = id != GO1_T_NONE ? s_terms[el][id] : 0.0f;
-      if (diverged) t = 0.0f;
-      if (A.dbg_terms && owner && leg == 0) A.dbg_terms[(size_t)e * GO1_MAX_TERMS + k] = t;
-      if (id != GO1_T_NONE) {
-        const float r = t * A.reward_scales[k];
-        rew = rew + r;
-        if (A.reward_scales[k] >= 0.0f) pos = pos + r; else neg = neg + r;
-        sums[k] = sums[k] + r;
-        if (global_buckets && sub16 == 0) {
-          K.bucket_r[(size_t)e * GO1_MAX_TERMS + k] = r;
-          atomicAdd(K.bucket_sum + k, (double)r);
-        }
+    for (int k = 0; k < GO1_MAX_TERMS; ++k) rr[k] = s_r[el][k];
+#pragma unroll
+    for (int k = 0; k < GO1_MAX_TERMS; ++k) {
+      if ((livem >> k) & 1u) {
+        rew = rew + rr[k];
+        if ((posm >> k) & 1u) pos = pos + rr[k]; else neg = neg + rr[k];
       }
     }
   }
   if (c->reward_mode == 1) rew = rew < 0.0f ? 0.0f : rew;            // only_positive_rewards (:341-342)
   else if (c->reward_mode == 2) rew = pos * expf(neg / c->sigma_rew_neg);  // ji22 style (:343-344)
+  // episode sums total / total_pos / total_neg (:346-348); with global buckets the bucket launch
+  // adds total_pos / total_neg (and the ji22 reward)
+  if (sub16 == 0 && !(global_buckets && c->reward_mode == 2)) my_tot = my_tot + rew;
   if (!global_buckets) {
-    tot[0] = tot[0] + rew;
-    tot[1] = tot[1] + pos;
-    tot[2] = tot[2] + neg;
-  } else if (c->reward_mode != 2) {
-    tot[0] = tot[0] + rew;  // the bucket launch adds total_pos / total_neg (and the ji22 reward)
+    if (sub16 == 1) my_tot = my_tot + pos;
+    if (sub16 == 2) my_tot = my_tot + neg;
   }
 
   MARK(rewards_done);
@@ -2132,26 +2128,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int i = 0; i < 6; ++i) traj_new[i] = traj_in[i];
   const int LOGW = NT + 6;
   if (A.episode_log && owner && leg == 0 && !reset) A.episode_log[(size_t)e * LOGW + NS] = 0.0f;
-  if (reset && A.episode_log && owner && leg == 0) {
+  if (reset && A.episode_log) {
     // reset_idx logging (:256-271): pre-reset sums, episode length, reached, goal distance
     float* lg = A.episode_log + (size_t)e * LOGW;
-#pragma unroll
-    for (int k = 0; k < GO1_MAX_TERMS; ++k)
-      if (k < NT) lg[k] = sums[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) lg[NT + k] = tot[k];
-    lg[NS] = (float)ep;
-    lg[NS + 1] = reached ? 1.0f : 0.0f;
-    lg[NS + 2] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+    if (sub16 < NT) lg[sub16] = my_sum;
+    if (sub16 < 3) lg[NT + sub16] = my_tot;
+    if (sub16 == 0) {
+      lg[NS] = (float)ep;
+      lg[NS + 1] = reached ? 1.0f : 0.0f;
+      lg[NS + 2] = diverged ? 0.0f : norm3_f(rel_lin[0], rel_lin[1], rel_lin[2]);
+    }
   }
   if (reset) {
     reset_env(c, K.ter, rng, e, leg, root, q, qd, strength, offset, traj_new);
     write_trajectory(c, rng, root, st.trajectory + (size_t)e * 6 * TL, sub16, 16);
     idx = 0;
-#pragma unroll
-    for (int k = 0; k < GO1_MAX_TERMS; ++k) sums[k] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) tot[k] = 0.0f;
+    my_sum = 0.0f;
+    my_tot = 0.0f;
     air_new = 0.0f;  // feet_air_time[env_ids] = 0 (:248); last_contacts is kept
     cmd[0] = 0.0f;  // commands is a view of local_relative_linear, zeroed by reset_idx (:252, :802)
     cmd[1] = 0.0f;
@@ -2306,11 +2299,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int i = 0; i < 13; ++i) st.root[(size_t)e * 13 + i] = root[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) st.base_rotation[(size_t)e * 3 + i] = rpy[i];
-#pragma unroll
-    for (int k = 0; k < GO1_MAX_TERMS; ++k)
-      if (k < NT) st.episode_sums[(size_t)e * NS + k] = sums[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) st.episode_sums[(size_t)e * NS + NT + k] = tot[k];
     st.episode_length[e] = reset ? 0 : ep;
     st.curr_pose_index[e] = idx;
     st.collision_count[e] = coll_count;
@@ -2320,6 +2308,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (A.dbg_commands) { A.dbg_commands[e * 2] = cmd[0]; A.dbg_commands[e * 2 + 1] = cmd[1]; }
     if (A.dbg_reached) A.dbg_reached[e] = reached;
   }
+  if (sub16 < NT) st.episode_sums[(size_t)e * NS + sub16] = my_sum;
+  if (sub16 < 3) st.episode_sums[(size_t)e * NS + NT + sub16] = my_tot;
   // one atomic per wave when any env of the wave reset (extras["time_outs"] rebinding, :289-291)
   if (__ballot(reset && leg == 0) != 0ull && (threadIdx.x & 63) == 0) atomicOr(K.flags + K.cur, 1);
   MARK(kernel_end);
