@@ -260,6 +260,9 @@ typedef struct go1_step_args {
   /* optional second copy of obs (NULL = not written): HistoryWrapper's obs_history for a history
      length of 1 (history_wrapper.py:18-24 builds it as a copy of obs every step) */
   float* obs_history;          /* (n_envs, num_obs) */
+  /* optional (NULL = not counted): += the number of envs the native integrator's divergence guard
+     reset this step (a non-finite state or a component beyond 1e4; no reference counterpart) */
+  uint64_t* diverged_count;
 } go1_step_args;
 
 typedef struct go1_handle go1_handle;

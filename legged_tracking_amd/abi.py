@@ -98,7 +98,7 @@ class Go1StepArgs(C.Structure):
         ("obs", P), ("priv", P), ("rew", P), ("reset", P), ("time_out", P), ("extras_time_outs", P),
         ("any_reset", P), ("contact_forces", P),
         ("dbg_torques", P), ("dbg_heights", P), ("dbg_terms", P), ("dbg_commands", P), ("dbg_reached", P),
-        ("episode_log", P), ("aux", P), ("ev_begin", P), ("ev_end", P), ("obs_history", P),
+        ("episode_log", P), ("aux", P), ("ev_begin", P), ("ev_end", P), ("obs_history", P), ("diverged_count", P),
     ]
 
 

@@ -1943,6 +1943,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int j = 0; j < 3; ++j) finite = finite && fabsf(q[j]) < GO1_DIVERGED && fabsf(qd[j]) < GO1_DIVERGED;
     diverged = qsum(finite ? 0.0f : 1.0f) != 0.0f;
     if (diverged) reset = true;
+    if (diverged && sub16 == 0 && A.diverged_count) atomicAdd((unsigned long long*)A.diverged_count, 1ull);
   }
 
   MARK(termination_done);
@@ -2148,8 +2149,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     air_new = 0.0f;  // feet_air_time[env_ids] = 0 (:248); last_contacts is kept
     cmd[0] = 0.0f;  // commands is a view of local_relative_linear, zeroed by reset_idx (:252, :802)
     cmd[1] = 0.0f;
-    // a diverged env observes (and stores as its pitch) its post-reset pose instead
-    if (diverged) post_kin(traj_new);
+    // a diverged env observes (and stores as its pitch) its post-reset pose instead, and its
+    // actuator-net history (pos_err / vel of the last sub-steps, never reset by reset_idx) is
+    // cleared: it holds the diverged state, which would otherwise drive the next step's torques
+    if (diverged) {
+      post_kin(traj_new);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) eh[0][j] = eh[1][j] = vh[0][j] = vh[1][j] = 0.0f;
+    }
   }
   const int coll_count = reset ? 0 : coll_in + (int)coll;
 

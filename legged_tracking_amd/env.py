@@ -249,6 +249,8 @@ class LeggedRobot:
         self._slot = 0
         self._elog = EpisodeLogRing(self, n, dev)
         self._aux = torch.zeros((n, abi.GO1_AUX), device=dev)
+        # envs the native integrator's divergence guard reset, cumulative (extras["diverged"])
+        self._diverged = torch.zeros(1, dtype=torch.int64, device=dev)
         self._reset_mask = torch.zeros(n, dtype=torch.uint8, device=dev)
         # host RNG for the global gravity draws: identical on every rank
         self._host_rng = np.random.default_rng(self.seed)
@@ -306,6 +308,8 @@ class LeggedRobot:
         dict.__setitem__(ex, "timeouts", self._timeouts)
         # the rebinding of the last step is applied on read (go1_sync_time_outs)
         ex.set_lazy("time_outs", lambda: self._sim.sync_time_outs()[: self.num_train_envs])
+        # native-integrator health (no reference counterpart): envs reset by the divergence guard so far
+        ex.set_lazy("diverged", lambda: int(self._diverged.item()))
 
     def _deferred_time_outs(self):
         sim = self._sim
@@ -438,7 +442,8 @@ class LeggedRobot:
         hist = self._obs_hist[s] if self._obs_hist is not None else None
         self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
                        rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux,
-                       obs_history=hist, events=self.kernel_events.popleft() if self.kernel_events else None)
+                       obs_history=hist, events=self.kernel_events.popleft() if self.kernel_events else None,
+                       diverged_count=self._diverged)
         self._last_hist = hist
         self._rng_step += 1
         self._elog.advance()

@@ -118,7 +118,8 @@ class Go1Native:
         _check(lib().go1_set_terrain(self.h, C.byref(s)))
 
     def step(self, actions, gravity_vec, sim_gravity, reward_scales, rng_seed=0, rng_step=0, uniforms=None,
-             inj=None, debug=None, events=None, episode_log=None, aux=None, out=None, obs_history=None):
+             inj=None, debug=None, events=None, episode_log=None, aux=None, out=None, obs_history=None,
+             diverged_count=None):
         """One fused LeggedRobot.step on the current stream.  `debug` is an optional dict
         of preallocated tensors (torques, heights, terms, commands, reached); `out` may
         replace the default output buffers (obs, priv, rew, reset, time_out).
@@ -176,6 +177,10 @@ class Go1Native:
         if obs_history is not None:
             assert obs_history.is_contiguous() and obs_history.shape == (self.n, self.cfg.num_obs)
         a.obs_history = obs_history.data_ptr() if obs_history is not None else None
+        if diverged_count is not None:
+            assert diverged_count.dtype == torch.int64 and diverged_count.numel() == 1 and \
+                diverged_count.device == self.device
+        a.diverged_count = diverged_count.data_ptr() if diverged_count is not None else None
         _check(self._lib_step(self.h, C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
 
     def sync_time_outs(self):

@@ -1017,6 +1017,10 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     for (int d = 0; d < NDOF; ++d) finite = finite && fabsf(dp[d]) < GO1_DIVERGED && fabsf(dv[d]) < GO1_DIVERGED;
     diverged = !finite;
     if (diverged) reset = 1;
+    if (diverged && a->diverged_count) {
+#pragma omp atomic
+      a->diverged_count[0] += 1;
+    }
   }
 
   /* compute_reward (:320-355): the container's reward functions for the nonzero-scaled terms
@@ -1177,9 +1181,14 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     reset_env(c, st, ter, e, a, U);
     cmd[0] = 0.0f;
     cmd[1] = 0.0f;
-    if (diverged) { /* a diverged env observes (and stores as its pitch) its post-reset pose */
+    if (diverged) { /* a diverged env observes (and stores as its pitch) its post-reset pose, and its
+                       actuator-net history (never reset by reset_idx) is cleared (see the HIP kernel) */
       post_kin(root, a->gravity_vec, st->trajectory + (size_t)e * 6 * TL, blv, bav, pg, rel_lin, rpy, rel_rot);
       for (int i = 0; i < 3; ++i) brot[i] = rpy[i];
+      for (int i = 0; i < 2 * NDOF; ++i) {
+        st->pos_err_hist[(size_t)e * 2 * NDOF + i] = 0.0f;
+        st->vel_hist[(size_t)e * 2 * NDOF + i] = 0.0f;
+      }
     }
   }
   if (a->dbg_commands) { a->dbg_commands[e * 2] = cmd[0]; a->dbg_commands[e * 2 + 1] = cmd[1]; }

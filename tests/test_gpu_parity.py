@@ -166,6 +166,27 @@ def test_reset_kernel_matches_oracle():
         np.testing.assert_array_equal(gs[k], st[k], err_msg=k)
 
 
+# One-step error of the f32 HIP integrator against the f64 oracle, relative to max(1, |x|), over
+# EVERY env.  Measured on the MI355X (tools/integrator_stats.py, 4096 envs x 6 steps, single_path
+# and plane): max 2e-4 (dof_pos), 4.6e-3 (dof_vel), 1.3e-3 (root), resets identical.  The only
+# larger errors belong to envs whose contact SET differs between the two (a point within f32
+# rounding of the surface: penalty contact switches on in one and not in the other, a
+# discontinuity in the force): 1 env in 49,152 (0.93 in dof_vel).  Those envs are named by that
+# test, counted (at most 1 per 1,000) and excluded from the max-error bound.
+INTEGRATOR_MAX_ERR = {"dof_pos": 2e-3, "dof_vel": 2e-2, "root": 5e-3}
+
+
+def check_integrator_step(gs, st, cf_gpu, cf_oracle, reset_gpu, reset_oracle):
+    flip = ((np.linalg.norm(cf_gpu, axis=2) > 0) != (np.linalg.norm(cf_oracle, axis=2) > 0)).any(axis=1)
+    n = flip.size
+    assert flip.sum() <= 1 + n // 1000, f"{flip.sum()} envs with a different contact set"
+    for k, tol in INTEGRATOR_MAX_ERR.items():
+        err = (np.abs(gs[k] - st[k]) / np.maximum(1.0, np.abs(st[k]))).max(axis=1)
+        assert err[~flip].max() < tol, (k, err[~flip].max(), int(np.argmax(np.where(flip, 0, err))))
+    np.testing.assert_array_equal(reset_gpu[~flip], reset_oracle[~flip])
+    return int(flip.sum())
+
+
 @pytest.mark.parametrize("terrain", ["single_path", "plane"])
 def test_native_integrator_step_vs_f64_oracle(terrain):
     n = 256
@@ -184,14 +205,9 @@ def test_native_integrator_step_vs_f64_oracle(terrain):
         torch.cuda.synchronize()
         out = O.step(c, st, ter, act, gvec, grav, scales, rng_seed=3, rng_step=100 + t, debug=False)
         gs = g.state.numpy()
-        for k, tol in (("dof_pos", 2e-3), ("dof_vel", 5e-2), ("root", 2e-3)):
-            err = np.abs(gs[k] - st[k])
-            # velocities scale with the contact stiffness: compare relative to magnitude
-            scale = np.maximum(1.0, np.abs(st[k]))
-            assert np.percentile(err / scale, 99) < tol, (k, np.percentile(err / scale, 99))
+        check_integrator_step(gs, st, g.contact_forces.cpu().numpy(), out["contact_forces"],
+                              g.reset.cpu().numpy().astype(bool), out["reset"].astype(bool))
         assert np.isfinite(g.obs.cpu().numpy()).all()
-        agree = (g.reset.cpu().numpy() == out["reset"].astype(bool)).mean()
-        assert agree > 0.98
         # continue both from the GPU state so the comparison stays one-step
         st = O.NpState(n, gs, c)
 
@@ -228,8 +244,9 @@ def test_diverged_envs_reset_without_faulting():
     g.state.load(st.arrays)
     grav, gvec = CF.gravity_state([0.0, 0.0, 0.0])
     scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    count = torch.zeros(1, dtype=torch.int64, device=DEV)
     for t in range(2):
-        g.step(_dev(np.zeros((n, 12), np.float32)), gvec, grav, scales, rng_seed=1, rng_step=t)
+        g.step(_dev(np.zeros((n, 12), np.float32)), gvec, grav, scales, rng_seed=1, rng_step=t, diverged_count=count)
         torch.cuda.synchronize()
         if t == 0:
             assert g.reset.cpu().numpy()[bad].all()
@@ -239,6 +256,7 @@ def test_diverged_envs_reset_without_faulting():
         assert np.isfinite(g.state["base_rotation"].cpu().numpy()).all()
     gs = g.state.numpy()
     assert np.isfinite(gs["root"]).all() and np.isfinite(gs["dof_pos"]).all()
+    assert int(count.item()) == len(bad)  # counted once each (extras["diverged"]), then healthy
 
 
 def test_env_api_on_gpu_matches_oracle_backend():
@@ -269,9 +287,19 @@ def test_env_api_on_gpu_matches_oracle_backend():
         og, rg, dg, ig = g.step(torch.from_numpy(a).to(DEV))
         oc, rc, dc, ic = c.step(torch.from_numpy(a))
         torch.cuda.synchronize()
+        cfg_ = g.env._sim.contact_forces.cpu().numpy()
+        cfc = c.env._sim.contact_forces.numpy()
+        flip = ((np.linalg.norm(cfg_, axis=2) > 0) != (np.linalg.norm(cfc, axis=2) > 0)).any(axis=1)
+        assert flip.sum() <= 1 + n // 1000
+        # proprioceptive columns: integrator tolerance (INTEGRATOR_MAX_ERR) on every env with the same
+        # contact set; the same Philox noise on both sides
         err = np.abs(og["obs"].cpu().numpy()[:, :41] - oc["obs"].numpy()[:, :41])
-        assert np.percentile(err, 99) < 5e-2, np.percentile(err, 99)
-        assert (dg.cpu().numpy() == dc.numpy()).mean() > 0.98
+        assert err[~flip].max() < 2e-2, err[~flip].max()
+        # height columns (camera_zero: sample - base z, x 0.1): within the pose error, except a scan
+        # point within the pose error of a cell boundary, which may sample the neighbouring cell
+        dh = np.abs(og["obs"].cpu().numpy()[:, 41:] - oc["obs"].numpy()[:, 41:]) > 1e-3
+        assert dh[~flip].mean() < 1e-2, dh[~flip].mean()
+        np.testing.assert_array_equal(dg.cpu().numpy()[~flip], dc.numpy()[~flip])
         for k in ("joint_pos", "body_linear_vel", "foot_positions", "torques", "contact_states"):
             assert ig[k].shape == ic[k].shape, k
         # continue both from the GPU state so each comparison is one step

@@ -1,0 +1,119 @@
+"""Physical invariants of the native articulated-body integrator (VERDICT r01 missing #3).
+
+PhysX itself is absent, so besides the builder's own f64 oracle these are the independent
+evidence that the dynamics are physics.  The momenta and energy are computed by
+tests/physics_ref.py (numpy forward kinematics of the URDF model, sharing no code with the HIP
+kernel or the C oracle), on trajectories produced by the HIP kernel (`-m gpu`) and by the f64
+oracle (CPU).
+
+Scenarios (plane terrain, 64 envs, random orientation / velocities / joint angles):
+  * zero gravity, no contact, zero joint torque, 100 env steps (800 sub-steps of 2.5 ms): linear
+    and angular momentum conserved, and energy conserved for the envs whose joints stay off
+    their limits (the limit spring-damper dissipates).  Semi-implicit Euler conserves them to
+    first order in the sub-step (the f64 oracle's drift halves with it).
+    Measured: HIP |dp| 2.3e-4 kg m/s, |dL| 4.0e-5 kg m^2/s, |dE|/E 4.8e-5; f64 oracle 3.4e-5,
+    4.0e-5, 6.7e-6.  Bounds: |dp|, |dL| < 2e-3, |dE| / E < 5e-4.
+  * free fall (gravity on, no contact), one env step: the change of total momentum is M g dt (the
+    COM falls with g).  Measured 2.1e-4 relative (HIP and oracle).  Bound 1e-3.
+  * static stance (gravity, actuator net holding the default pose, zero actions), 150 env steps:
+    the base settles (measured height 0.263 m, |v| 5e-4 m/s) and the reported contact forces carry
+    the weight (measured sum F_z / M g = 1.000).  Bounds: height in (0.20, 0.40) m, |v| < 5e-2,
+    |sum F_z / M g - 1| < 2 %.
+"""
+import numpy as np
+import pytest
+
+from tests import physics_drive as D
+
+STEPS = 100
+G0 = (0.0, 0.0, 0.0)
+GZ = (0.0, 0.0, -9.81)
+
+
+def _roll(backend, *a, **k):
+    return D.hip_roll(*a, **k) if backend == "hip" else D.oracle_roll(*a, **k)
+
+
+def _args(backend, c, td, ter, st, scales):
+    return (c, td, st, scales) if backend == "hip" else (c, ter, st, scales)
+
+
+def _free_flight(backend):
+    c, td, ter, st, scales = D.setup(seed=1, qd_sigma=0.05, w_sigma=0.1)
+    i0 = D.all_invariants(st, G0)
+    last = None
+    for s, cf, reset in _roll(backend, *_args(backend, c, td, ter, st, scales), STEPS, G0):
+        assert not reset.any()
+        assert (np.abs(cf) == 0).all(), "no contact in free flight"
+        last = s
+    i1 = D.all_invariants(last, G0)
+    dp = np.array([np.linalg.norm(b["momentum"] - a["momentum"]) for a, b in zip(i0, i1)])
+    dl = np.array([np.linalg.norm(b["ang_momentum"] - a["ang_momentum"]) for a, b in zip(i0, i1)])
+    de = np.array([abs(b["energy"] - a["energy"]) / a["energy"] for a, b in zip(i0, i1)])
+    # energy only for envs whose joints stayed off their limits (the limit damper dissipates)
+    lim = np.array([c.hard_limits[i] for i in range(24)]).reshape(12, 2)
+    q = last["dof_pos"]
+    free = ~(((q < lim[:, 0] + 0.05) | (q > lim[:, 1] - 0.05)).any(axis=1))
+    print(f"\n{backend}: max |dp| {dp.max():.2e}  max |dL| {dl.max():.2e}  max |dE|/E {de[free].max():.2e} "
+          f"({free.sum()} envs off limits)")
+    assert dp.max() < 2e-3, dp.max()
+    assert dl.max() < 2e-3, dl.max()
+    assert free.sum() >= st.n // 2
+    assert de[free].max() < 5e-4, de[free].max()
+
+
+def _free_fall(backend):
+    c, td, ter, st, scales = D.setup(seed=2)
+    i0 = D.all_invariants(st, GZ)
+    s, cf, reset = next(_roll(backend, *_args(backend, c, td, ter, st, scales), 1, GZ))
+    i1 = D.all_invariants(s, GZ)
+    acc = np.array([(b["momentum"] - a["momentum"]) / (a["mass"] * D.STEP_DT) for a, b in zip(i0, i1)])
+    err = np.abs(acc - np.array(GZ)).max(axis=1) / 9.81
+    print(f"\n{backend}: free fall COM acceleration max rel err {err.max():.2e}")
+    assert err.max() < 1e-3, err.max()
+
+
+def _stance(backend):
+    c, td, ter, st, scales = D.setup(seed=3, strength=1.0, stance=True)
+    mass = D.all_invariants(st, GZ)[0]["mass"]
+    hist = []
+    for t, (s, cf, reset) in enumerate(_roll(backend, *_args(backend, c, td, ter, st, scales), 150, GZ)):
+        assert not reset.any()
+        if t >= 130:
+            hist.append((s["root"].copy(), cf.sum(axis=1)[:, 2]))
+    z = np.array([h[0][:, 2] for h in hist])
+    v = np.array([np.linalg.norm(h[0][:, 7:10], axis=1) for h in hist])
+    fz = np.array([h[1] for h in hist]).mean(axis=0)
+    w = mass * 9.81
+    print(f"\n{backend}: stance height {z.mean():.3f} (min {z.min():.3f}) max |v| {v.max():.2e} "
+          f"sum Fz / Mg {fz.mean() / w:.3f} [{fz.min() / w:.3f}, {fz.max() / w:.3f}]")
+    assert 0.20 < z.min() and z.max() < 0.40
+    assert v.max() < 5e-2
+    assert np.abs(fz / w - 1.0).max() < 0.02
+
+
+@pytest.mark.gpu
+def test_hip_free_flight_conserves_momentum_and_energy():
+    _free_flight("hip")
+
+
+@pytest.mark.gpu
+def test_hip_free_fall_com_accelerates_with_g():
+    _free_fall("hip")
+
+
+@pytest.mark.gpu
+def test_hip_static_stance_carries_the_weight():
+    _stance("hip")
+
+
+def test_oracle_free_flight_conserves_momentum_and_energy():
+    _free_flight("oracle")
+
+
+def test_oracle_free_fall_com_accelerates_with_g():
+    _free_fall("oracle")
+
+
+def test_oracle_static_stance_carries_the_weight():
+    _stance("oracle")
