@@ -17,7 +17,8 @@ STEP_FLAGS = ["-fno-slp-vectorize"]
 
 # name -> (source, extra dependencies, extra flags)
 LIBS = {
-    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", os.path.join(INC, "go1_mi355x.h")], STEP_FLAGS),
+    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", "go1_model_consts.h", os.path.join(INC, "go1_mi355x.h")],
+                         STEP_FLAGS),
     "libgo1_rollout.so": ("rollout.hip", [os.path.join(INC, "go1_rollout.h")], []),
 }
 OUT = os.path.join(BUILD, "libgo1_mi355x.so")  # the step library (kept for callers of build())

@@ -5,20 +5,19 @@
 //   4 x [actuator-net torques (:957-996, :1311-1320) -> native articulated-body
 //        integrator (replaces gym.simulate / fetch_results / refresh, :82-88)]
 //   -> post-physics: kinematics (:130-136), height scan (:1918-1970), target and
-//      command logic (:774-932), terminations (:198-216), RewardsCrawling terms
+//      command logic (:774-932), terminations (:198-216), reward terms of both containers
 //      (:320-355), reset_idx (:218-296), observations (:357-475), epilogue (:148-153).
 //
-// Decomposition: one env = one quad of lanes, lane l = leg l (FL, FR, RL, RR).
-// A 64-lane wave carries 16 envs; a block is one wave (4096 envs -> 256 blocks,
-// one per CU).  Each lane runs its leg's three actuator-net evaluations, its
-// leg's forward kinematics, contacts and ABA backward pass; the leg's
-// articulated inertia and bias force are summed over the quad with DPP-level
-// shuffles (__shfl_xor 1, 2), every lane of the quad solves the 6x6 base system
-// redundantly (bit-identical), then runs its leg's forward pass.
-// State is SoA row-major (n_envs, width) in HBM: a wave reads 16 contiguous env
-// rows per field (coalesced); nothing is staged through LDS because no datum is
-// shared between envs except the config/weights (scalar loads, SGPR-resident).
-//
+// Decomposition: 16 lanes per env = 4 legs x 4 roles, lane = 16 role + 4 env + leg; a 64-lane
+// wave carries 4 envs and a block is one wave (4096 envs -> 1024 waves, one per SIMD).  The four
+// roles of a leg run that leg's kinematics and articulated-body passes redundantly (the 3-link
+// chain is sequential) and split the parallel work: the leg's contact points, the actuator-net
+// MFMA columns (a role is one row of the 16 x 4 B operand), the height-scan gathers and the
+// stores.  Leg sums use DPP quad_perm, role sums v_permlane16/32_swap; both are butterflies, so
+// every lane of an env holds bit-identical base quantities and solves the base 6 x 6 system.
+// State is SoA row-major (n_envs, width) in HBM.  LDS holds the Go1 model block and per-joint
+// config (ds_write after the prologue loads), the env's 20 x 16 (floor, ceiling) terrain patch
+// (LDS-DMA, global_load_lds, at step start) and the per-env reward-term table.  See DESIGN.md 5.
 // Numerics: the post-physics section is compiled with FP contraction OFF and
 // uses the deterministic transcendentals of pmath.h, so it is bit-identical to
 // the CPU oracle (oracle/go1_oracle.c) given the same physical state; the

@@ -635,7 +635,7 @@ class Runner:
     module and actor body, the formats scripts/eval.py and the deploy stack read)."""
 
     def __init__(self, env, device="cpu", runner_args=RunnerArgs, ac_args=AC_Args, log_wandb=False, kernels=None,
-                 save_dir="last_run/checkpoints"):
+                 save_dir=None):
         self.device = device
         self.env = env
         self.runner_args = runner_args
@@ -707,19 +707,36 @@ class Runner:
             self.tot_time += time.time() - start
             self.current_learning_iteration = it
             if it % self.runner_args.save_interval == 0:
-                self.save(self.save_dir)
-        self.save(self.save_dir)
+                self.save(self.checkpoint_dir())
+        self.save(self.checkpoint_dir())
 
-    def save(self, save_path):
-        """ac_weights.pt + adaptation_module_latest.jit + body_latest.jit (__init__.py:274-319)."""
+    def checkpoint_dir(self):
+        """Where the reference's Runner writes checkpoints (ppo_cse/__init__.py:276-279):
+        wandb.run.dir/checkpoints with wandb logging, last_run/checkpoints otherwise."""
+        if self.save_dir is not None:
+            return self.save_dir
+        if self.log_wandb:
+            import wandb
+            return os.path.join(wandb.run.dir, "checkpoints")
+        return "last_run/checkpoints"
+
+    def save(self, save_path=None):
+        """ac_weights.pt + adaptation_module_latest.jit + body_latest.jit (__init__.py:274-319), uploaded
+        with wandb.save when logging to wandb (:294-297)."""
         if _world() > 1 and torch.distributed.get_rank() != 0:
             return
+        save_path = save_path or self.checkpoint_dir()
         os.makedirs(save_path, exist_ok=True)
         ac = self.alg.actor_critic
-        torch.save(ac.state_dict(), os.path.join(save_path, "ac_weights.pt"))
-        torch.jit.script(copy.deepcopy(ac.adaptation_module).to("cpu")).save(
-            os.path.join(save_path, "adaptation_module_latest.jit"))
-        torch.jit.script(copy.deepcopy(ac.actor_body).to("cpu")).save(os.path.join(save_path, "body_latest.jit"))
+        paths = [os.path.join(save_path, "ac_weights.pt"), os.path.join(save_path, "adaptation_module_latest.jit"),
+                 os.path.join(save_path, "body_latest.jit")]
+        torch.save(ac.state_dict(), paths[0])
+        torch.jit.script(copy.deepcopy(ac.adaptation_module).to("cpu")).save(paths[1])
+        torch.jit.script(copy.deepcopy(ac.actor_body).to("cpu")).save(paths[2])
+        if self.log_wandb:
+            import wandb
+            for path in paths:
+                wandb.save(path)
 
     def get_inference_policy(self, device=None):
         self.alg.actor_critic.eval()

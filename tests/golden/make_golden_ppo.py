@@ -6,7 +6,9 @@ records, on seeded synthetic inputs:
   * ActorCritic (actor_critic.py:21-156): state dict, adaptation latent, action mean,
     value, log-prob and entropy for given actions;
   * PPO.process_env_step time-out bootstrap (ppo.py:79-92);
-  * RolloutStorage.compute_returns GAE + normalisation (rollout_storage.py:76-90).
+  * RolloutStorage.compute_returns GAE + normalisation (rollout_storage.py:76-90);
+  * one PPO.update (ppo.py:98-206): minibatch permutation, losses, adaptive learning rate,
+    updated weights.
 Writes tests/golden/ppo_rollout.npz.
 """
 import os
@@ -82,6 +84,38 @@ def main():
     out["gae/raw_advantages"] = (st.returns - st.values).numpy()[..., 0]
     out["gae/gamma"] = np.float64(PPO_Args.gamma)
     out["gae/lam"] = np.float64(PPO_Args.lam)
+
+    # one PPO.update (ppo.py:98-206) on this storage: the minibatch permutation it draws, its
+    # returned losses, the adaptive learning rate after the KL steps and the updated weights
+    for k in ("observations", "privileged_observations", "observation_histories", "actions", "values", "returns",
+              "actions_log_prob", "advantages", "mu", "sigma", "rewards", "dones"):
+        out["upd/storage/" + k] = getattr(st, k).numpy().copy()
+    for k, v in ac.state_dict().items():
+        out["upd/sd_before/" + k] = v.numpy().copy()
+    out["upd/lr_before"] = np.float64(alg.learning_rate)
+    perms = []
+    real_randperm = torch.randperm
+
+    def randperm(*a, **k):
+        r = real_randperm(*a, **k)
+        perms.append(r.numpy().copy())
+        return r
+
+    torch.manual_seed(17)
+    torch.randperm = randperm
+    try:
+        losses = alg.update()
+    finally:
+        torch.randperm = real_randperm
+    assert len(perms) == 1
+    out["upd/perm"] = perms[0]
+    out["upd/losses"] = np.array(losses, np.float64)
+    out["upd/lr_after"] = np.float64(alg.learning_rate)
+    for k, v in ac.state_dict().items():
+        out["upd/sd_after/" + k] = v.numpy().copy()
+    for k in ("num_learning_epochs", "num_mini_batches", "clip_param", "learning_rate", "max_grad_norm",
+              "value_loss_coef", "entropy_coef", "desired_kl", "num_adaptation_module_substeps"):
+        out["upd/args/" + k] = np.float64(getattr(PPO_Args, k))
     path = os.path.join(HERE, "ppo_rollout.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, len(out))

@@ -1,5 +1,5 @@
 """The fused step at BASELINE's full size (configs[2]: 4096 Go1, single_path tunnels on a 32 x 32
-sub-terrain grid), through size-independent properties:
+sub-terrain grid; and the 4096-env plane of configs[1]'s terrain), through size-independent properties:
 
   * sharding: one handle of 4096 envs and two handles of 2048 (global env ids 0.. and 2048..,
     i.e. what ranks 0 and 1 of a 2-GPU run compute) produce bit-identical states and outputs
@@ -23,13 +23,13 @@ DEV = "cuda:0"
 N = 4096
 
 
-def _setup(seed=7):
-    cfg = CF.readme_config(n_envs=N, terrain="single_path", rows=32, cols=32)
+def _setup(seed=7, terrain="single_path"):
+    cfg = CF.readme_config(n_envs=N, terrain=terrain, rows=32, cols=32)
     td = T.build(cfg, N, np.random.RandomState(11))
     rng = np.random.default_rng(seed)
     dr = {"friction": rng.uniform(0.1, 3.0, (N, 1)), "restitution": rng.uniform(0.0, 0.4, (N, 1)),
           "payload": rng.uniform(-1.0, 3.0, (N, 1))}
-    ep = rng.integers(0, 500, (N, 1)).astype(np.int32)
+    ep = rng.integers(0, 500 if terrain != "plane" else 1000, (N, 1)).astype(np.int32)
     return cfg, td, dr, ep, rng
 
 
@@ -70,8 +70,9 @@ def test_full_size_sharded_handles_are_bit_identical_to_one():
         np.testing.assert_array_equal(s1[k], np.concatenate([sl[k], sh[k]]), err_msg=k)
 
 
-def test_full_size_invariants_over_40_steps():
-    cfg, td, dr, ep, rng = _setup(seed=8)
+@pytest.mark.parametrize("terrain", ["single_path", "plane"])
+def test_full_size_invariants_over_40_steps(terrain):
+    cfg, td, dr, ep, rng = _setup(seed=8, terrain=terrain)
     c, g, keep = _handle(cfg, td, dr, ep, 0, N)
     scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
     grav, gvec = CF.gravity_state([0.0, 0.0, 0.0])
@@ -90,23 +91,30 @@ def test_full_size_invariants_over_40_steps():
         assert np.isfinite(obs).all() and np.isfinite(rew).all()
         assert np.abs(obs).max() <= clip
         assert not (tout & ~reset).any(), "time-out without reset"
-        np.testing.assert_array_equal(tout, ep_before + 1 > 500)
+        np.testing.assert_array_equal(tout, ep_before + 1 > float(c.max_episode_length))  # 500 tunnel, 1000 plane
         assert (ep_after[reset] == 0).all(), "reset envs restart their episode"
         np.testing.assert_array_equal(ep_after[~reset], ep_before[~reset] + 1)
-        # camera_zero heights: clip(h, -0.3, 0.3) * obs_scale_heights
         hs = float(c.obs_scale_heights)
-        assert np.abs(obs[:, 41:]).max() <= 0.3 * hs + 1e-7
+        if terrain == "plane":
+            # dummy plane heights (:1928-1932): ceiling 1, floor 0 -> clip(h, 0, ceiling) / ceiling - 0.5
+            top = np.float32(np.float32(min(1.0, float(c.ceiling_height))) / np.float32(c.ceiling_height) - 0.5)
+            assert (obs[:, 41:151] == np.float32(top * np.float32(hs))).all()
+            assert (obs[:, 151:] == np.float32(np.float32(-0.5) * np.float32(hs))).all()
+        else:
+            # camera_zero heights: clip(h, -0.3, 0.3) * obs_scale_heights
+            assert np.abs(obs[:, 41:]).max() <= 0.3 * hs + 1e-7
         n_reset += int(reset.sum())
     assert n_reset > 0  # the random episode lengths make some envs time out in 40 steps
     assert int(diverged.item()) == 0, "the native integrator's divergence guard fired"
 
 
-def test_full_size_one_step_integrator_vs_f64_oracle():
-    cfg, td, dr, ep, rng = _setup(seed=9)
+@pytest.mark.parametrize("terrain", ["single_path", "plane"])
+def test_full_size_one_step_integrator_vs_f64_oracle(terrain):
+    cfg, td, dr, ep, rng = _setup(seed=9, terrain=terrain)
     c, g, keep = _handle(cfg, td, dr, ep, 0, N)
     torch.cuda.synchronize()
     del keep
-    st = O.NpState(N, g.state.numpy())
+    st = O.NpState(N, g.state.numpy(), c)
     ter = O.NpTerrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
     scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
     grav, gvec = CF.gravity_state([0.2, -0.1, 0.3])

@@ -230,3 +230,100 @@ def test_fused_policy_sampling_is_normal_with_matching_log_prob():
     act2 = pol.forward(h, p, sample=(123, 7, 0))[3]
     act3 = pol.forward(h, p, sample=(123, 8, 0))[3]
     assert torch.equal(act, act2) and not torch.equal(act, act3)
+
+
+def _ppo_update_from_fixture(d, device, kernels):
+    """One rollout.PPO.update on the storage the reference's PPO.update saw (ppo.py:98-206), with
+    the reference's minibatch permutation."""
+    ac = R.ActorCritic(261, 2, 261, 12)
+    ac.load_state_dict({k[len("upd/sd_before/"):]: torch.from_numpy(d[k]) for k in d.files
+                        if k.startswith("upd/sd_before/")})
+    for k in ("num_learning_epochs", "num_mini_batches", "clip_param", "learning_rate", "max_grad_norm",
+              "value_loss_coef", "entropy_coef", "desired_kl", "num_adaptation_module_substeps"):
+        assert float(getattr(R.PPO_Args, k)) == float(d["upd/args/" + k]), k
+    alg = R.PPO(ac, device=device, kernels=kernels)
+    T, n = d["gae/rewards_in"].shape
+    alg.init_storage(n, T, [261], [2], [261], [12])
+    st = alg.storage
+    for k in ("observations", "privileged_observations", "observation_histories", "actions", "values", "returns",
+              "actions_log_prob", "advantages", "mu", "sigma", "rewards"):
+        getattr(st, k).copy_(torch.from_numpy(d["upd/storage/" + k]))
+    st.step = T
+    perm = torch.from_numpy(d["upd/perm"])
+    real = torch.randperm
+    torch.randperm = lambda *a, **k: perm.to(k.get("device") or "cpu")
+    try:
+        losses = alg.update()
+    finally:
+        torch.randperm = real
+    return alg, losses
+
+
+def _check_update(d, alg, losses, rtol_loss, atol_w, atol_max=None):
+    """Losses, the adaptive learning rate and every updated weight.  `atol_w` bounds 99.99 % of the
+    weights; `atol_max` (default atol_w) every weight."""
+    want = d["upd/losses"]
+    np.testing.assert_allclose(np.array(losses, np.float64), want, rtol=rtol_loss, atol=1e-7)
+    assert alg.learning_rate == float(d["upd/lr_after"])  # adaptive-KL schedule: same decisions
+    sd = alg.actor_critic.state_dict()
+    diffs = []
+    for k in d.files:
+        if k.startswith("upd/sd_after/"):
+            got = sd[k[len("upd/sd_after/"):]].detach().cpu().numpy()
+            before = d["upd/sd_before/" + k[len("upd/sd_after/"):]]
+            diff = np.abs(got - d[k]).ravel()
+            assert diff.max() <= (atol_max or atol_w), (k, diff.max())
+            diffs.append(diff)
+            assert not np.array_equal(d[k], before) or k.endswith("std")  # the update moved the weights
+    diffs = np.concatenate(diffs)
+    assert np.percentile(diffs, 99.99) <= atol_w, np.percentile(diffs, 99.99)
+    return float(diffs.max())
+
+
+def test_ppo_update_matches_reference_on_cpu():
+    """CPU: the same torch ops in the same order as ppo.py -> losses within 1e-5, weights within 1e-6
+    after 20 Adam steps (5 epochs x 4 minibatches) with the adaptive-KL learning rate."""
+    d = _fixture()
+    alg, losses = _ppo_update_from_fixture(d, "cpu", TorchRolloutKernels())
+    _check_update(d, alg, losses, rtol_loss=1e-5, atol_w=1e-6)
+
+
+@pytest.mark.gpu
+def test_ppo_update_matches_reference_on_gpu():
+    """MI355X: the update's GEMMs run on hipBLASLt with another reduction order than the CPU's.  Adam
+    normalises each gradient component, so a component whose gradient is near zero can step by up
+    to the learning rate in either direction on either side: the weights may differ by at most the
+    schedule's total step, sum_t lr_t < 1e-3 / (1 - 1 / 1.5) = 3e-3 (the adaptive KL rule divides lr
+    by 1.5 per minibatch here); 99.99 % of the 700k weights agree within 1e-4, the losses within
+    1e-3 relative, and the KL schedule takes the same decisions."""
+    d = _fixture()
+    alg, losses = _ppo_update_from_fixture(d, "cuda:0", R.HipRolloutKernels())
+    w = _check_update(d, alg, losses, rtol_loss=1e-3, atol_w=1e-4, atol_max=3e-3)
+    print(f"\nPPO.update on the GPU vs the reference (CPU): max |dw| {w:.2e}")
+
+
+@pytest.mark.gpu
+def test_runner_learn_on_gpu_through_hip_env_and_rollout_kernels(tmp_path):
+    """Runner.learn(2) end to end on the MI355X: HIP env step, fused policy / record / GAE kernels,
+    PPO.update on the GPU, checkpoints in the reference's three formats."""
+    from legged_tracking_amd import config as CF, env as E
+    n = 256
+    R.RunnerArgs.num_steps_per_env = 8
+    R.PPO_Args.num_learning_epochs, R.PPO_Args.num_mini_batches = 2, 2
+    try:
+        cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=4, cols=4)
+        env = E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device="cuda:0", cfg=cfg, seed=4, rank=0, world_size=1))
+        assert env.env._sim.__class__.__name__ == "Go1Native"
+        runner = R.Runner(env, device="cuda:0", save_dir=str(tmp_path / "checkpoints"))
+        assert runner.alg.fused is not None  # the fused MFMA policy kernel drives the rollout
+        before = {k: v.clone() for k, v in runner.alg.actor_critic.state_dict().items()}
+        runner.learn(2, init_at_random_ep_len=True)
+        torch.cuda.synchronize()
+    finally:
+        R.RunnerArgs.num_steps_per_env, R.PPO_Args.num_learning_epochs, R.PPO_Args.num_mini_batches = 24, 5, 4
+    after = runner.alg.actor_critic.state_dict()
+    assert any(not torch.equal(before[k], after[k]) for k in before)
+    assert all(torch.isfinite(v).all() for v in after.values())
+    sd = torch.load(tmp_path / "checkpoints" / "ac_weights.pt", weights_only=True, map_location="cpu")
+    assert set(sd) == set(after)
+    assert env.extras["diverged"] == 0
