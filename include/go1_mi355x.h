@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GO1_ABI_VERSION 3
+#define GO1_ABI_VERSION 4
 
 #define GO1_NUM_DOF 12
 #define GO1_NUM_BODIES 17
@@ -263,6 +263,14 @@ typedef struct go1_step_args {
   /* optional (NULL = not counted): += the number of envs the native integrator's divergence guard
      reset this step (a non-finite state or a component beyond 1e4; no reference counterpart) */
   uint64_t* diverged_count;
+  /* optional compact episode log (NULL = episode_log is the per-env (n_envs, n_terms + 6) layout):
+     every env reset this step appends one row of n_terms + 8 floats -- the n_terms + 6 values above,
+     then episode_log_tag and the env index -- at row atomicAdd(episode_log_count, ...) of episode_log
+     (rows at or beyond episode_log_cap are dropped; size it n_envs x steps for none).  Rows of one
+     step are in no particular order: order them by (tag, env) for the reference's logging order. */
+  int32_t* episode_log_count;
+  int32_t episode_log_cap;
+  int32_t episode_log_tag;
 } go1_step_args;
 
 typedef struct go1_handle go1_handle;

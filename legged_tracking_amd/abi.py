@@ -5,7 +5,7 @@ checks sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
-GO1_ABI_VERSION = 3
+GO1_ABI_VERSION = 4
 GO1_NUM_DOF = 12
 GO1_NUM_BODIES = 17
 GO1_MAX_TERMS = 16
@@ -99,6 +99,7 @@ class Go1StepArgs(C.Structure):
         ("any_reset", P), ("contact_forces", P),
         ("dbg_torques", P), ("dbg_heights", P), ("dbg_terms", P), ("dbg_commands", P), ("dbg_reached", P),
         ("episode_log", P), ("aux", P), ("ev_begin", P), ("ev_end", P), ("obs_history", P), ("diverged_count", P),
+        ("episode_log_count", P), ("episode_log_cap", I32), ("episode_log_tag", I32),
     ]
 
 

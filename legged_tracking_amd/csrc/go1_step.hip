@@ -2127,10 +2127,28 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
   for (int i = 0; i < 6; ++i) traj_new[i] = traj_in[i];
   const int LOGW = NT + 6;
-  if (A.episode_log && owner && leg == 0 && !reset) A.episode_log[(size_t)e * LOGW + NS] = 0.0f;
-  if (reset && A.episode_log) {
+  const bool compact = A.episode_log_count != nullptr;
+  if (A.episode_log && !compact && owner && leg == 0 && !reset) A.episode_log[(size_t)e * LOGW + NS] = 0.0f;
+  // compact log: the wave's reset envs append their rows (LOGW + 2 wide: + step tag, env id)
+  // at one atomic per wave; the host orders the rows by (tag, env) as the reference logs them
+  int log_row = -1;
+  if (compact) {
+    const uint64_t rmask = __ballot(reset && owner && leg == 0);  // lane 4 el: env el's role 0, leg 0
+    if (rmask != 0ull) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(A.episode_log_count, __popcll(rmask));
+      base = __shfl(base, 0);
+      log_row = base + __popcll(rmask & ((1ull << (4 * el)) - 1ull));
+      if (log_row >= A.episode_log_cap) log_row = -1;  // the host sized the buffer for the worst case
+    }
+  }
+  if (reset && A.episode_log && (!compact || log_row >= 0)) {
     // reset_idx logging (:256-271): pre-reset sums, episode length, reached, goal distance
-    float* lg = A.episode_log + (size_t)e * LOGW;
+    float* lg = compact ? A.episode_log + (size_t)log_row * (LOGW + 2) : A.episode_log + (size_t)e * LOGW;
+    if (compact && sub16 == 0) {
+      lg[LOGW] = (float)A.episode_log_tag;
+      lg[LOGW + 1] = (float)e;
+    }
     if (sub16 < NT) lg[sub16] = my_sum;
     if (sub16 < 3) lg[NT + sub16] = my_tot;
     if (sub16 == 0) {
@@ -2573,6 +2591,9 @@ int go1_step(go1_handle* h, const go1_step_args* a, void* stream) {
   K.bucket_sum = h->d_bucket_sum ? h->d_bucket_sum + bank * GO1_MAX_TERMS : nullptr;
   dim3 grid(n / SEPB), block(TPB);
   const bool full = !h->cfg.measure_front_half;  // 231 scanned points: 15 per lane instead of 7
+  if (a->episode_log_count && (!a->episode_log || a->episode_log_cap < 0 || h->cfg.indefinite_slots))
+    return fail(GO1_E_ARG, "go1_step: a compact episode log needs episode_log, a capacity >= 0 and no indefinite "
+                           "reward slots (their bucket pass rewrites rows by env)");
   if (a->ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_begin, s));
   if (inj) {
     if (full) hipLaunchKernelGGL((go1_step_kernel<true, 15>), grid, block, 0, s, h->d_cfg, K);

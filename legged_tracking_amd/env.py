@@ -94,32 +94,47 @@ class EpisodeLogRing:
     """Device ring of the kernel's per-step episode log (go1_step_args.episode_log) and its
     asynchronous trip to the host.
 
-    Two halves of EPISODE_RING steps.  When a half fills, a side stream copies it to
-    pinned host memory while the next half is written; the copy is turned into deque
-    entries on the host one half later (long finished, no wait), so the rollout never
-    blocks on logging.  Reading extras["train/episode"] / ["timeouts"] drains everything
-    synchronously.  Deques keep their last 4000 entries (deque(maxlen=4000), as the
-    reference), so only the newest 4000 values per key are materialised."""
+    Two halves of R steps.  When a half fills, a side stream copies it to pinned host
+    memory while the next half is written; the copy is turned into deque entries on the
+    host one half later (long finished, no wait), so the rollout never blocks on logging.
+    Reading extras["train/episode"] / ["timeouts"] drains everything synchronously.
+    Deques keep their last 4000 entries (deque(maxlen=4000), as the reference), so only
+    the newest 4000 values per key are materialised.
 
-    def __init__(self, env, n, device):
+    On the HIP backend the log is compact (go1_step_args.episode_log_count): only envs
+    reset in a step append a row (+ step tag, env index), so a half's host trip and its
+    processing scale with the resets, not with n_envs x R.  The async copy takes a prefix of
+    `prefix` rows; a half with more rows fetches the rest when it is processed."""
+
+    def __init__(self, env, n, device, compact=False):
         self.env = env
         self.dev = device
+        self.n = n
         self.R = R = int(min(EPISODE_RING, max(4, (1 << 22) // max(n, 1))))  # <= 16 MB per half
         self.W = W = abi.episode_log_width(len(env.reward_names))
-        self.buf = torch.zeros((2, R, n, W), device=device)
-        self.half, self.slot, self.done = 0, 0, 0  # write position; slots of this half already drained
         self.cuda = device.type == "cuda"
+        self.compact = compact and self.cuda
+        if self.compact:
+            self.cap = R * n  # every env reset on every step of the half still fits
+            self.prefix = min(self.cap, max(4 * n, 1024))
+            self.buf = torch.zeros((2, self.cap, W + 2), device=device)
+            self.count = torch.zeros((2, 1), dtype=torch.int32, device=device)
+        else:
+            self.buf = torch.zeros((2, R, n, W), device=device)
+        self.half, self.slot, self.done = 0, 0, 0  # write position; slots (compact: rows) already drained
         if self.cuda:
-            self.host = torch.zeros((2, R, n, W), pin_memory=True)
+            hshape = (2, self.prefix, W + 2) if self.compact else (2, R, n, W)
+            self.host = torch.zeros(hshape, pin_memory=True)
+            self.host_count = torch.zeros((2, 1), dtype=torch.int32, pin_memory=True)
             self.side = torch.cuda.Stream(device)
             self.copied = [None, None]  # event per half: host copy finished
-        self.inflight = None  # (half, first slot) copied to host, not yet turned into deque entries
+        self.inflight = None  # (half, first slot / row) copied to host, not yet turned into deque entries
 
     def next_slot(self):
-        """Buffer the kernel writes this step's log into."""
+        """Buffer the kernel writes this step's log into (compact: the half's row buffer)."""
         if self.slot == 0 and self.cuda and self.copied[self.half] is not None:
             torch.cuda.current_stream(self.dev).wait_event(self.copied[self.half])  # half free again
-        return self.buf[self.half, self.slot]
+        return self.buf[self.half] if self.compact else self.buf[self.half, self.slot]
 
     def advance(self):
         self.slot += 1
@@ -132,7 +147,11 @@ class EpisodeLogRing:
                 ev.record(torch.cuda.current_stream(self.dev))
                 self.side.wait_event(ev)
                 with torch.cuda.stream(self.side):
-                    self.host[h].copy_(self.buf[h], non_blocking=True)
+                    if self.compact:
+                        self.host_count[h].copy_(self.count[h], non_blocking=True)
+                        self.host[h].copy_(self.buf[h, :self.prefix], non_blocking=True)
+                    else:
+                        self.host[h].copy_(self.buf[h], non_blocking=True)
                     done = torch.cuda.Event()
                     done.record(self.side)
                 self.copied[h] = done
@@ -140,25 +159,84 @@ class EpisodeLogRing:
             else:
                 self._process(self.buf[h, first:].numpy())
 
+    def _half_rows(self, h, first, cnt, host):
+        """Rows [first, cnt) of compact half h (host prefix + a synchronous fetch beyond it)."""
+        p = min(cnt, self.prefix) if host else first
+        parts = [self.host[h, first:p].numpy()] if host and p > first else []
+        if cnt > max(p, first):
+            parts.append(self.buf[h, max(p, first):cnt].cpu().numpy())
+        return np.concatenate(parts) if parts else np.zeros((0, self.W + 2), np.float32)
+
     def _drain_inflight(self):
         if self.inflight is not None:
             h, first = self.inflight
             self.inflight = None
             self.copied[h].synchronize()
-            self._process(self.host[h, first:].numpy())
+            if self.compact:
+                rows = self._half_rows(h, first, int(self.host_count[h, 0]), host=True)
+                with torch.cuda.stream(self.side):  # after the copy (same stream): the half starts empty
+                    self.count[h].zero_()
+                done = torch.cuda.Event()
+                done.record(self.side)
+                self.copied[h] = done
+                self._process_rows(rows)
+            else:
+                self._process(self.host[h, first:].numpy())
 
     def drain(self):
         """Everything logged so far, synchronously (extras read)."""
         if self.cuda:
             self._drain_inflight()
-        if self.slot > self.done:
+        if self.compact:
+            cnt = int(self.count[self.half, 0].item())
+            if cnt > self.done:
+                self._process_rows(self._half_rows(self.half, self.done, cnt, host=False))
+                self.done = cnt
+        elif self.slot > self.done:
             self._process(self.buf[self.half, self.done:self.slot].cpu().numpy())
             self.done = self.slot
 
     def reset(self):
         if self.cuda:
             self._drain_inflight()
-        self.done = self.slot
+        self.drain()
+
+    def _process_rows(self, rows):
+        """Compact rows (m, W + 2) -> the dense (steps, envs, W) processing of _process, without
+        building the dense array: order by (step tag, env) as the reference logs them (:256-271)."""
+        env = self.env
+        ntr = env.num_train_envs
+        ns = len(env.sum_keys)
+        W = self.W
+        if rows.shape[0] == 0:
+            return
+        tag, eid = rows[:, W].astype(np.int64), rows[:, W + 1].astype(np.int64)
+        keep = (eid < ntr) & (rows[:, ns] > 0)
+        rows, tag, eid = rows[keep], tag[keep], eid[keep]
+        if rows.shape[0] == 0:
+            return
+        order = np.lexsort((eid, tag))
+        rows, tag, eid = rows[order], tag[order], eid[order]
+        # timeouts: for each step with a reset, time_out of every train env (False unless reset
+        # with episode length > max_episode_length), newest 4000 values
+        steps = np.unique(tag)
+        need = min(len(steps), 4000 // max(ntr, 1) + 1)
+        tail = steps[len(steps) - need:]
+        to = np.zeros((need, ntr), bool)
+        sel = tag >= tail[0]
+        pos = np.searchsorted(tail, tag[sel])
+        to[pos, eid[sel]] = rows[sel, ns] > np.float32(env.max_episode_length)
+        env._timeouts.extend(to.reshape(-1)[-4000:])
+        self._extend(rows[-4000:])
+
+    def _extend(self, rows):
+        env = self.env
+        ns = len(env.sum_keys)
+        for i, key in enumerate(env.sum_keys):
+            env._train_ep["rew_" + key].extend(rows[:, i])
+        env._train_ep["episode_length"].extend(rows[:, ns])
+        env._train_ep["reached"].extend(rows[:, ns + 1] > 0)
+        env._train_ep["goal_distance"].extend(rows[:, ns + 2])
 
     def _process(self, logs):
         env = self.env
@@ -172,11 +250,7 @@ class EpisodeLogRing:
         reset_steps = np.unique(steps)
         timeouts = (col[reset_steps] > np.float32(env.max_episode_length)).reshape(-1)[-4000:]
         env._timeouts.extend(timeouts)
-        for i, key in enumerate(env.sum_keys):
-            env._train_ep["rew_" + key].extend(rows[:, i])
-        env._train_ep["episode_length"].extend(rows[:, ns])
-        env._train_ep["reached"].extend(rows[:, ns + 1] > 0)
-        env._train_ep["goal_distance"].extend(rows[:, ns + 2])
+        self._extend(rows)
 
 
 def _episode_dicts():
@@ -247,7 +321,11 @@ class LeggedRobot:
         self._reset = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
         self._time_out = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
         self._slot = 0
-        self._elog = EpisodeLogRing(self, n, dev)
+        # the compact episode log needs the HIP backend's prepared-args path, and rows that the
+        # global pos/neg bucket pass (indefinite reward slots) does not rewrite by env index
+        self._fast = hasattr(self._sim, "prepare")
+        self._elog = EpisodeLogRing(self, n, dev, compact=self._fast and not self._abi_cfg.indefinite_slots)
+        self._prepared = {}
         self._aux = torch.zeros((n, abi.GO1_AUX), device=dev)
         # envs the native integrator's divergence guard reset, cumulative (extras["diverged"])
         self._diverged = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -300,6 +378,16 @@ class LeggedRobot:
 
     def _scale_vector(self):
         return CF.reward_scale_vector(self.reward_scales, self.reward_names)
+
+    def _step_consts(self):
+        """(key, gravity_vec, sim_gravity, reward_scales) of the next step; the key changes
+        only when one of them does (gravity schedule, exploration decay)."""
+        key = (self._gravity_vec.tobytes(), self._sim_gravity.tobytes(),
+               tuple(self.reward_scales[k] for k in self.reward_names))
+        c = getattr(self, "_consts_cache", None)
+        if c is None or c[0] != key:
+            c = self._consts_cache = (key, self._gravity_vec, self._sim_gravity, self._scale_vector())
+        return c
 
     def _install_extras(self):
         ex = self.extras
@@ -437,13 +525,25 @@ class LeggedRobot:
         if a.shape != (self.num_envs, self.num_actions):
             raise ValueError(f"actions must be ({self.num_envs}, {self.num_actions}), got {tuple(a.shape)}")
         s = self._slot
-        out = dict(obs=self._obs[s], priv=self._priv[s], rew=self._rew[s], reset=self._reset[s],
-                   time_out=self._time_out[s])
-        hist = self._obs_hist[s] if self._obs_hist is not None else None
-        self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
-                       rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux,
-                       obs_history=hist, events=self.kernel_events.popleft() if self.kernel_events else None,
-                       diverged_count=self._diverged)
+        events = self.kernel_events.popleft() if self.kernel_events else None
+        if self._fast:
+            el = self._elog
+            log = el.next_slot()
+            key = (s, el.half if el.compact else el.slot + el.R * el.half, self._obs_hist is not None)
+            p = self._prepared.get(key)
+            if p is None:
+                p = self._prepared[key] = self._prepare_slot(s, log)
+            args, out, hist = p
+            ck, gvec, sgrav, scales = self._step_consts()
+            self._sim.step_prepared(args, a, gvec, sgrav, scales, ck, self.seed, self._rng_step, events=events,
+                                    log_tag=el.slot)
+        else:
+            out = dict(obs=self._obs[s], priv=self._priv[s], rew=self._rew[s], reset=self._reset[s],
+                       time_out=self._time_out[s])
+            hist = self._obs_hist[s] if self._obs_hist is not None else None
+            self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
+                           rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux,
+                           obs_history=hist, events=events, diverged_count=self._diverged)
         self._last_hist = hist
         self._rng_step += 1
         self._elog.advance()
@@ -457,6 +557,16 @@ class LeggedRobot:
             self._randomize_gravity(np.zeros(3, np.float32))
         self.update_curriculum()
         return out["obs"], out["priv"], out["rew"], out["reset"], self.extras
+
+    def _prepare_slot(self, s, log):
+        """Validated go1_step_args for output-ring slot s and this episode-log buffer."""
+        out = dict(obs=self._obs[s], priv=self._priv[s], rew=self._rew[s], reset=self._reset[s],
+                   time_out=self._time_out[s])
+        hist = self._obs_hist[s] if self._obs_hist is not None else None
+        el = self._elog
+        args = self._sim.prepare(out, aux=self._aux, obs_history=hist, diverged_count=self._diverged,
+                                 episode_log=log, log_count=el.count[el.half] if el.compact else None)
+        return args, out, hist
 
     def update_curriculum(self):
         """update_curriculum (:171-182): exploration scales decay after exploration_steps."""

@@ -105,6 +105,7 @@ class Go1Native:
         self._args = None
         self._consts = None
         self._lib_step = lib().go1_step
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
 
     def set_terrain(self, tiles, env_tile, env_terrain_origin, env_origins):
         d = self.device
@@ -182,6 +183,69 @@ class Go1Native:
                 diverged_count.device == self.device
         a.diverged_count = diverged_count.data_ptr() if diverged_count is not None else None
         _check(self._lib_step(self.h, C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+
+    # ------------------------------------------------------------------ per-step fast path
+    def prepare(self, out, aux=None, obs_history=None, diverged_count=None, episode_log=None, log_count=None):
+        """A validated go1_step_args for step_prepared: the env builds one per (output-ring slot,
+        episode-log half) once, so the per-step host work is a handful of field writes and the
+        ctypes call (the loop is otherwise host-bound at ~60 us per step).  `episode_log` with
+        `log_count` selects the compact log (go1_step_args.episode_log_count)."""
+        a = abi.Go1StepArgs()
+        a.contact_forces = self.contact_forces.data_ptr()
+        a.extras_time_outs = self.extras_time_outs.data_ptr()
+        for k in ("obs", "priv", "rew", "reset", "time_out"):
+            v, ref = out[k], getattr(self, k)
+            if v.device != self.device or not v.is_contiguous() or v.shape != ref.shape or v.dtype != ref.dtype:
+                raise NativeError(f"output buffer {k!r} does not match the expected shape / dtype / device")
+            setattr(a, k, v.data_ptr())
+        if aux is not None:
+            if not aux.is_contiguous() or aux.shape != (self.n, abi.GO1_AUX) or aux.device != self.device:
+                raise NativeError("aux must be a contiguous (n_envs, GO1_AUX) float32 tensor on the env's device")
+            a.aux = aux.data_ptr()
+        if obs_history is not None:
+            if not obs_history.is_contiguous() or obs_history.shape != (self.n, self.cfg.num_obs):
+                raise NativeError("obs_history must be a contiguous (n_envs, num_obs) tensor")
+            a.obs_history = obs_history.data_ptr()
+        if diverged_count is not None:
+            if diverged_count.dtype != torch.int64 or diverged_count.numel() != 1 or \
+                    diverged_count.device != self.device:
+                raise NativeError("diverged_count must be one int64 on the env's device")
+            a.diverged_count = diverged_count.data_ptr()
+        if episode_log is not None:
+            w = abi.episode_log_width(self.cfg.n_terms)
+            if log_count is None:
+                if episode_log.shape != (self.n, w) or not episode_log.is_contiguous():
+                    raise NativeError("episode_log must be a contiguous (n_envs, n_terms + 6) tensor")
+            else:
+                if episode_log.dim() != 2 or episode_log.shape[1] != w + 2 or not episode_log.is_contiguous() or \
+                        log_count.dtype != torch.int32 or log_count.device != self.device:
+                    raise NativeError("a compact episode log is a contiguous (cap, n_terms + 8) tensor + an int32 count")
+                a.episode_log_count = log_count.data_ptr()
+                a.episode_log_cap = int(episode_log.shape[0])
+            a.episode_log = episode_log.data_ptr()
+        a._consts = None
+        return a
+
+    def step_prepared(self, a, actions, gravity_vec, sim_gravity, reward_scales, consts_key, rng_seed, rng_step,
+                      events=None, log_tag=0):
+        """go1_step with a prepare()d argument block.  `consts_key` identifies (gravity_vec,
+        sim_gravity, reward_scales): they are re-copied into the block only when it changes."""
+        if actions.dtype != torch.float32 or actions.shape != (self.n, 12) or not actions.is_contiguous() or \
+                actions.device != self.device:
+            raise NativeError("actions must be a contiguous (n_envs, 12) float32 tensor on the env's device")
+        a.actions = actions.data_ptr()
+        if a._consts != consts_key:
+            a._consts = consts_key
+            a.gravity_vec[:] = [float(x) for x in gravity_vec]
+            a.sim_gravity[:] = [float(x) for x in sim_gravity]
+            rs = np.zeros(abi.GO1_MAX_TERMS, np.float32)
+            rs[:len(reward_scales)] = np.asarray(reward_scales, np.float32)
+            a.reward_scales[:] = [float(x) for x in rs]
+        a.rng_seed, a.rng_step, a.episode_log_tag = rng_seed, rng_step, log_tag
+        a.ev_begin, a.ev_end = events if events is not None else (None, None)
+        rc = self._lib_step(self.h, C.byref(a), torch._C._cuda_getCurrentRawStream(self._dev_index))
+        if rc:
+            _check(rc)
 
     def sync_time_outs(self):
         """Make extras_time_outs current for the last step (the rebinding of step k is

@@ -187,3 +187,42 @@ def test_sharded_envs_reproduce_single_rank_gloo():
         p.join(180)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+def test_compact_episode_log_rows_match_dense_processing():
+    """The HIP backend's compact episode log (rows of reset envs only, appended in no particular
+    order within a step, go1_step_args.episode_log_count) yields exactly the deques the dense
+    per-env log does (reset_idx logging order :256-271: by step, then env; timeouts of every
+    train env on each step with a reset; newest 4000 entries)."""
+    from types import SimpleNamespace
+    rng = np.random.default_rng(3)
+    names = ["a", "b", "c"]
+
+    def fake(ntr):
+        tr, ev, to = E._episode_dicts()
+        return SimpleNamespace(reward_names=names, num_train_envs=ntr, sum_keys=tuple(names) + ("t", "p", "n"),
+                               max_episode_length=500, _timeouts=to, _train_ep=tr)
+
+    for n, R, p_reset in ((48, 16, 0.05), (4096, 8, 0.01), (300, 64, 0.3)):
+        ntr = n - 5
+        dense_env, comp_env = fake(ntr), fake(ntr)
+        W = E.abi.episode_log_width(len(names))
+        logs = rng.normal(size=(R, n, W)).astype(np.float32)
+        rs = rng.random((R, n)) < p_reset
+        ns = len(names) + 3
+        logs[:, :, ns] = np.where(rs, rng.integers(1, 1000, (R, n)), 0).astype(np.float32)
+        rows = []
+        for t in range(R):
+            ids = np.nonzero(rs[t])[0]
+            rng.shuffle(ids)  # atomics: no order within a step
+            for e in ids:
+                rows.append(np.concatenate([logs[t, e], [t, e]]).astype(np.float32))
+        rows = np.array(rows, np.float32).reshape(-1, W + 2)
+        dense = E.EpisodeLogRing(dense_env, n, torch.device("cpu"))
+        comp = E.EpisodeLogRing(comp_env, n, torch.device("cpu"))
+        dense._process(logs)
+        comp._process_rows(rows)
+        assert list(dense_env._timeouts) == list(comp_env._timeouts)
+        assert dense_env._train_ep.keys() == comp_env._train_ep.keys()
+        for k in dense_env._train_ep:
+            np.testing.assert_array_equal(np.array(dense_env._train_ep[k]), np.array(comp_env._train_ep[k]))

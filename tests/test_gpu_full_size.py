@@ -126,3 +126,37 @@ def test_full_size_one_step_integrator_vs_f64_oracle(terrain):
     from tests.test_gpu_parity import check_integrator_step
     check_integrator_step(gs, st, g.contact_forces.cpu().numpy(), out["contact_forces"],
                           g.reset.cpu().numpy().astype(bool), out["reset"].astype(bool))
+
+
+def test_env_fast_path_and_compact_log_match_generic_path():
+    """TrajectoryTrackingEnv.step on the prepared-args path with the compact episode log (the
+    bench / rollout path) against the generic go1_step call with the dense per-env log: identical
+    observations, rewards and resets step after step, and identical extras["train/episode"] /
+    ["timeouts"] deques across two episode-log ring wraps (4096 envs, resets staggered)."""
+    from legged_tracking_amd import env as E
+    envs = []
+    for fast in (True, False):
+        cfg = CF.readme_config(n_envs=N, terrain="single_path", rows=32, cols=32)
+        env = E.TrajectoryTrackingEnv(sim_device=DEV, cfg=cfg, seed=5)
+        if not fast:  # the generic path: per-call validation, dense (n_envs, W) log
+            env._fast = False
+            env._elog = E.EpisodeLogRing(env, N, env.device, compact=False)
+        env.reset()
+        env.episode_length_buf = torch.arange(N, dtype=torch.int32, device=DEV) % 300 + 200
+        envs.append(env)
+    assert envs[0]._elog.compact and not envs[1]._elog.compact
+    ring = torch.randn((16, N, 12), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    steps = 2 * envs[0]._elog.R + 17
+    for k in range(steps):
+        outs = [e.step(ring[k % 16]) for e in envs]
+        if k % 8 == 0 or k == steps - 1:
+            for a, b in zip(outs[0][:3], outs[1][:3]):
+                assert torch.equal(a, b), k
+    ea, eb = (e.extras["train/episode"] for e in envs)
+    assert len(ea["episode_length"]) > 100
+    assert ea.keys() == eb.keys()
+    for k in ea:
+        np.testing.assert_array_equal(np.array(ea[k]), np.array(eb[k]), err_msg=k)
+    assert list(envs[0].extras["timeouts"]) == list(envs[1].extras["timeouts"])
+    for e in envs:
+        e.close()
