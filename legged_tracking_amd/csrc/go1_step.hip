@@ -1554,6 +1554,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   s_go1_stamp_k = 0;
 #endif
   MARK(kernel_begin);
+#ifdef GO1_ABL_EMPTY  // ablation build only: launch and wave dispatch alone
+  if (c->n_envs > 0) return;
+#endif
   MlpFrag F;
   mlp_load(c_gen->actuator, lane, F);  // lane-indexed: generic pointer
   const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset, c->u_per_env};
@@ -1866,7 +1869,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
   // the env's 16 lanes take points sub16 + 16 k (KPTS = 7 for the 110 front-half points, 15 for all 231)
   float hv[KPTS][2];
+#ifdef GO1_ABL_NO_SCAN  // ablation build only: no height-scan gathers
+  const bool scan = false;
+#else
   const bool scan = c->observe_heights != 0;
+#endif
 #pragma unroll
   for (int k = 0; k < KPTS; ++k) {
     const int p = min(sub16 + 16 * k, n_pts - 1);
@@ -2291,7 +2298,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   MARK(aux_done);
   // ---------------- write back (epilogue :148-153): role r < 3 stores joint r of its
   // leg, role 3 of leg 0 stores the env-level state
+#ifdef GO1_ABL_NO_STORE  // ablation build only: no state write-back
+  if (false) {
+#else
   if (role < 3) {
+#endif
     const int j = role;
     auto pick = [&](const float* v3) { return sel3(j, v3); };
     const size_t dj = d0 + j;

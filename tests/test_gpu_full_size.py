@@ -160,3 +160,51 @@ def test_env_fast_path_and_compact_log_match_generic_path():
     assert list(envs[0].extras["timeouts"]) == list(envs[1].extras["timeouts"])
     for e in envs:
         e.close()
+
+
+def test_full_size_height_scan_bit_exact_from_post_physics_pose():
+    """The height scan (_get_heights :1918-1965: grid + base xy (+ camera offset), / horizontal_scale,
+    .long() truncation, clip to [0, shape - 2], gather of both layers) against a numpy restatement
+    at the GPU's own post-physics base pose, every step, every env that did not reset (a reset env's
+    state holds its post-reset pose): bit-exact.  The front-half points come from the LDS scan
+    window staged at step start, the back half (debug output only) from the HBM tile, so both paths
+    of the kernel's sampling are compared.  The previous pitch is zeroed before each step, so the
+    camera offset is camera_offset_x * cos(0) = camera_offset_x exactly."""
+    cfg, td, dr, ep, rng = _setup(seed=12)
+    c, g, keep = _handle(cfg, td, dr, ep, 0, N)
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    grav, gvec = CF.gravity_state([0.0, 0.0, 0.0])
+    dbg = native.debug_buffers(N, c.decimation, DEV)
+    torch.cuda.synchronize()
+    del keep
+    gx = np.array([c.height_grid_x[i] for i in range(21)], np.float32)
+    gy = np.array([c.height_grid_y[i] for i in range(11)], np.float32)
+    hs, nx, ny = np.float32(c.horizontal_scale), int(c.hf_nx), int(c.hf_ny)
+    camx = np.float32(c.camera_offset_x) if c.camera_zero else np.float32(0.0)
+    org = td.env_terrain_origin.astype(np.float32)
+    tiles = td.tiles.astype(np.float32)
+    checked = 0
+    for t in range(6):
+        g.state["base_rotation"][:, 1] = 0.0
+        g.step(torch.randn(N, 12, device=DEV), gvec, grav, scales, rng_seed=8, rng_step=t, debug=dbg)
+        torch.cuda.synchronize()
+        keepenv = ~g.reset.cpu().numpy().astype(bool)
+        root = g.state["root"].cpu().numpy()
+        px = (gx[None, :] + root[:, 0:1]).astype(np.float32)
+        py = (gy[None, :] + root[:, 1:2]).astype(np.float32)
+        if c.camera_zero:
+            px = (px + camx).astype(np.float32)
+            py = (py + np.float32(0.0)).astype(np.float32)
+        px = (px - org[:, 0:1]).astype(np.float32)
+        py = (py - org[:, 1:2]).astype(np.float32)
+        fx = np.minimum(np.maximum(px / hs, np.float32(-1.0)), np.float32(nx)).astype(np.float32)
+        fy = np.minimum(np.maximum(py / hs, np.float32(-1.0)), np.float32(ny)).astype(np.float32)
+        ix = np.clip(np.trunc(fx).astype(np.int64), 0, nx - 2)
+        iy = np.clip(np.trunc(fy).astype(np.int64), 0, ny - 2)
+        tix = td.env_tile.astype(np.int64)
+        want = tiles[tix[:, None, None, None], np.arange(2)[None, :, None, None], ix[:, None, :, None],
+                     iy[:, None, None, :]]
+        got = dbg["heights"].cpu().numpy()
+        np.testing.assert_array_equal(got[keepenv], want[keepenv], err_msg=f"step {t}")
+        checked += int(keepenv.sum())
+    assert checked > 5 * N
