@@ -284,6 +284,13 @@ int go1_create(const go1_config* cfg, go1_handle** out);
 int go1_bind(go1_handle* h, const go1_state* state);
 int go1_set_terrain(go1_handle* h, const go1_terrain* terrain);
 int go1_step(go1_handle* h, const go1_step_args* args, void* stream);
+/* Kernel variant.  go1_create selects a step kernel specialised for the README configuration
+ * (scripts/train.py's README command: the integer flags of legged_tracking_amd/csrc/go1_spec.h
+ * folded at compile time) when the config matches it, the generic kernel otherwise; both compute
+ * identical results.  enable = 0 forces the generic kernel; enable = 1 fails (GO1_E_ARG) for a
+ * config that does not match.  go1_is_specialized returns 1 when the specialised kernel runs. */
+int go1_specialize(go1_handle* h, int enable);
+int go1_is_specialized(go1_handle* h);
 /* extras["time_outs"] (:289-291) is rebound to time_out only on steps with a reset.  The
  * rebinding for step k is applied by the kernel of step k+1 (no launch of its own); call
  * this to have extras_time_outs of the last go1_step current now (one tiny launch,

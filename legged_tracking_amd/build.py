@@ -17,7 +17,7 @@ STEP_FLAGS = ["-fno-slp-vectorize"]
 
 # name -> (source, extra dependencies, extra flags)
 LIBS = {
-    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", "go1_model_consts.h", os.path.join(INC, "go1_mi355x.h")],
+    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", "go1_model_consts.h", "go1_spec.h", os.path.join(INC, "go1_mi355x.h")],
                          STEP_FLAGS),
     "libgo1_rollout.so": ("rollout.hip", [os.path.join(INC, "go1_rollout.h")], []),
 }

@@ -33,6 +33,7 @@
 
 #include "../../include/go1_mi355x.h"
 #include "go1_model_consts.h"
+#include "go1_spec.h"
 static_assert(GO1_MODEL_CONST_FLOATS == GO1_MODEL_FLOATS, "regenerate go1_model_consts.h");
 #include "pmath.h"
 
@@ -1535,7 +1536,10 @@ __device__ void write_trajectory(CCfg* __restrict__ c, const Rng& rng, const flo
   }
 }
 
-template <bool INJ, int KPTS>
+// CI(field): an integer config field, a compile-time constant in the specialised instantiation
+// (go1_spec.h, the README configuration; go1_create selects it when every field matches)
+#define CI(f) (SPEC ? (decltype(c->f))(GO1_SPEC_##f) : c->f)
+template <bool INJ, int KPTS, bool SPEC>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) void go1_step_kernel(
     const go1_config* __restrict__ c_gen, KArgs K) {
   CCfg* __restrict__ c = (CCfg*)c_gen;
@@ -1559,7 +1563,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
   MlpFrag F;
   mlp_load(c_gen->actuator, lane, F);  // lane-indexed: generic pointer
-  const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset, c->u_per_env};
+  const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset, CI(u_per_env)};
   // the previous step's extras["time_outs"] rebinding, for this wave's envs (flags of the
   // previous launch are complete now), and the flag the next launch will set is cleared
   // (loaded with the state, applied after the prologue's single wait: no round trip of its own)
@@ -1574,7 +1578,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float act[3], q[3], qd[3], eh[2][3], vh[2][3], strength[3], offset[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    act[j] = clampf(A.actions[d0 + j], -c->clip_actions, c->clip_actions);
+    act[j] = clampf(A.actions[d0 + j], -CI(clip_actions), CI(clip_actions));
     q[j] = st.dof_pos[d0 + j];
     qd[j] = st.dof_vel[d0 + j];
     strength[j] = st.motor_strength[d0 + j];
@@ -1603,7 +1607,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int idx_in = st.curr_pose_index[e];
   const int coll_in = st.collision_count[e];
   const float restitution = st.restitution[e];
-  const int TL = c->traj_length, NT = c->n_terms, NS = NT + 3;
+  const int TL = CI(traj_length), NT = CI(n_terms), NS = NT + 3;
   float traj_in[6], ldv[3], la[3];
   {
     // the current waypoint trajectories[e, curr_pose_index[e]] (:850-853); traj_length 1 needs no index
@@ -1634,7 +1638,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
   }
-  Terr T = {nullptr, c->hf_nx, c->hf_ny, 0.0f, 0.0f, c->horizontal_scale, nullptr, 0, 0};
+  Terr T = {nullptr, CI(hf_nx), CI(hf_ny), 0.0f, 0.0f, CI(horizontal_scale), nullptr, 0, 0};
   __shared__ float2 s_patch[SEPB][PSZX * PSZY];
   __shared__ float s_phys[(LDS_FLOATS + 63) / 64 * 64];
   // Block = one wave, so LDS needs no barrier here (a wave's LDS operations execute in
@@ -1643,7 +1647,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // nothing reads them before the first sub-step's physics, so the first actuator-net
   // evaluation runs while they land (the compiler waits vmcnt before the first ds_read).
   int tix = 0;  // the env's terrain tile and origin, loaded with the state
-  if (c->terrain_kind == 1) {
+  if (CI(terrain_kind) == 1) {
     tix = K.ter.env_tile[e];
     T.ox = K.ter.env_terrain_origin[(size_t)e * 3];
     T.oy = K.ter.env_terrain_origin[(size_t)e * 3 + 1];
@@ -1672,17 +1676,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     s_phys[i] = i < GO1_MODEL_FLOATS ? c_gen->model[i] : c_gen->default_dof_pos[i - GO1_MODEL_FLOATS];
   __syncthreads();
 #endif
-  if (c->terrain_kind == 1) {
-    T.tile = K.ter.tiles + (size_t)tix * 2 * c->hf_nx * c->hf_ny;
+  if (CI(terrain_kind) == 1) {
+    T.tile = K.ter.tiles + (size_t)tix * 2 * CI(hf_nx) * CI(hf_ny);
     if (!INJ) {
       // patch centred on the legs' bounding box at the start of the step
       float bx, by;
       legs_bbox_centre(P.pos, P.quat, q, leg, &bx, &by);
       MARK(pro_bbox_done);
-      T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(c->hf_nx + 64))) - PSZX / 2;
-      T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(c->hf_ny + 64))) - PSZY / 2;
+      T.pi0 = (int)floorf(fminf(fmaxf((bx - T.ox) / T.hs, -64.0f), (float)(CI(hf_nx) + 64))) - PSZX / 2;
+      T.pj0 = (int)floorf(fminf(fmaxf((by - T.oy) / T.hs, -64.0f), (float)(CI(hf_ny) + 64))) - PSZY / 2;
       T.patch = &s_patch[el][0];
-      const int nx = c->hf_nx, ny = c->hf_ny;
+      const int nx = CI(hf_nx), ny = CI(hf_ny);
 #if GO1_GLDS
       // 4 x PSZX / 2 LDS-DMA dword loads per wave: load k of env el2 fills s_patch[el2]
       // dwords 64 k .. 64 k + 63, i.e. cells 32 k + lane / 2 (rows 2 k, 2 k + 1 of PSZY = 16
@@ -1728,8 +1732,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float scaled[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    scaled[j] = act[j] * c->action_scale;
-    if (j == 0) scaled[j] = scaled[j] * c->hip_scale_reduction;
+    scaled[j] = act[j] * CI(action_scale);
+    if (j == 0) scaled[j] = scaled[j] * CI(hip_scale_reduction);
   }
 
   // ---------------- decimation loop (:82-88)
@@ -1838,41 +1842,41 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   // height scan (:1918-1965) samples at the post-physics, pre-reset pose: the gathers are
   // issued here and consumed by the height observations at the end
-  const bool hplane = c->terrain_kind == 0;
+  const bool hplane = CI(terrain_kind) == 0;
   const float scan_x = root[0], scan_y = root[1];
   // camera_pitch_angle (:1934-1939): the previous step's pitch, or 0 with rotate_camera
-  const float cam_p = c->rotate_camera ? 0.0f : cam_pitch;
+  const float cam_p = CI(rotate_camera) ? 0.0f : cam_pitch;
   float camx = 0.0f, camy = 0.0f;
   if (!hplane) {
     const float cos_p = pm_cosf(cam_p);
-    camx = c->camera_offset_x * cos_p;
+    camx = CI(camera_offset_x) * cos_p;
     camy = 0.0f * cos_p;
   }
   auto sample = [&](int i, int j, float& h0, float& h1) {
     if (hplane) { h0 = 1.0f; h1 = 0.0f; return; }
     float px = s_phys[LDS_GX + i] + scan_x;
     float py = s_phys[LDS_GY + j] + scan_y;
-    if (c->camera_zero) { px = px + camx; py = py + camy; }
+    if (CI(camera_zero)) { px = px + camx; py = py + camy; }
     px = px - T.ox;
     py = py - T.oy;
     // .long() truncation then clip (:1948-1952); the float is bounded first so that a
     // non-finite pose cannot turn the conversion into undefined behaviour
-    const float fx = fminf(fmaxf(px / c->horizontal_scale, -1.0f), (float)c->hf_nx);
-    const float fy = fminf(fmaxf(py / c->horizontal_scale, -1.0f), (float)c->hf_ny);
+    const float fx = fminf(fmaxf(px / CI(horizontal_scale), -1.0f), (float)CI(hf_nx));
+    const float fy = fminf(fmaxf(py / CI(horizontal_scale), -1.0f), (float)CI(hf_ny));
     int ix = (int)fx, iy = (int)fy;
-    ix = ix < 0 ? 0 : (ix > c->hf_nx - 2 ? c->hf_nx - 2 : ix);
-    iy = iy < 0 ? 0 : (iy > c->hf_ny - 2 ? c->hf_ny - 2 : iy);
-    h0 = T.tile[(size_t)ix * c->hf_ny + iy];
-    h1 = T.tile[((size_t)c->hf_nx + ix) * c->hf_ny + iy];
+    ix = ix < 0 ? 0 : (ix > CI(hf_nx) - 2 ? CI(hf_nx) - 2 : ix);
+    iy = iy < 0 ? 0 : (iy > CI(hf_ny) - 2 ? CI(hf_ny) - 2 : iy);
+    h0 = T.tile[(size_t)ix * CI(hf_ny) + iy];
+    h1 = T.tile[((size_t)CI(hf_nx) + ix) * CI(hf_ny) + iy];
   };
-  const int x_start = c->measure_front_half ? GO1_GRID_X / 2 + 1 : 0;
+  const int x_start = CI(measure_front_half) ? GO1_GRID_X / 2 + 1 : 0;
   const int n_pts = (GO1_GRID_X - x_start) * GO1_GRID_Y;
   // the env's 16 lanes take points sub16 + 16 k (KPTS = 7 for the 110 front-half points, 15 for all 231)
   float hv[KPTS][2];
 #ifdef GO1_ABL_NO_SCAN  // ablation build only: no height-scan gathers
   const bool scan = false;
 #else
-  const bool scan = c->observe_heights != 0;
+  const bool scan = CI(observe_heights) != 0;
 #endif
 #pragma unroll
   for (int k = 0; k < KPTS; ++k) {
@@ -1911,16 +1915,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   MARK(post_kin_done);
   // DR every rand_interval (:822-824)
-  if (ep % c->rand_interval == 0) {
-    const float sv = rng(34) * c->strength_range + c->strength_lo;
+  if (ep % CI(rand_interval) == 0) {
+    const float sv = rng(34) * CI(strength_range) + CI(strength_lo);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       strength[j] = sv;
-      offset[j] = rng(35 + leg * 3 + j) * c->offset_range + c->offset_lo;
+      offset[j] = rng(35 + leg * 3 + j) * CI(offset_range) + CI(offset_lo);
     }
   }
   const float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
-  const bool switched = rel_norm < c->switch_dist;
+  const bool switched = rel_norm < CI(switch_dist);
   // waypoint switch, capped at the last waypoint (:836-844)
   int idx = idx_in;
   if (switched) { idx += 1; if (idx > TL - 1) idx = TL - 1; }
@@ -1932,11 +1936,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const float coll = qsum(coll_l);
 
   // check_termination (:198-216)
-  const bool time_out = (float)ep > c->max_episode_length;
+  const bool time_out = (float)ep > CI(max_episode_length);
   bool reset = time_out, diverged = false;
-  if (c->use_terminal_body_height && root[2] < c->terminal_body_height) reset = true;
-  if (c->terminate_end_of_trajectory && reached && (float)ep > c->t_reach) reset = true;  // (:211-213)
-  if (c->use_terminal_body_rotation && pg[2] > 0.0f) reset = true;                        // (:215-216)
+  if (CI(use_terminal_body_height) && root[2] < CI(terminal_body_height)) reset = true;
+  if (CI(terminate_end_of_trajectory) && reached && (float)ep > CI(t_reach)) reset = true;  // (:211-213)
+  if (CI(use_terminal_body_rotation) && pg[2] > 0.0f) reset = true;                        // (:215-216)
   if (!INJ) {
     // native-integrator divergence guard (no reference counterpart: PhysX does not
     // return non-finite states): an env whose state is not finite, or beyond
@@ -1959,7 +1963,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // and the reward is then summed in slot (reward_scales) order.  One wave per block: the
   // wave's LDS operations complete in order, no barrier.
   __shared__ float s_terms[SEPB][GO1_T_COUNT];
-  const uint32_t tm = c->term_mask;
+  const uint32_t tm = CI(term_mask);
 #define PUT(id, v)                          \
   do {                                      \
     const float v_ = (v);                   \
@@ -1969,10 +1973,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const float vmag = norm2_f(blv[0], blv[1]);
   const float mag = rel_norm;
   // the target velocity towards the waypoint (reward_crawling.py:83-87, trajectory_tracking_reward.py:79-85)
-  float tx = rel_lin[0] / (mag + 1e-6f) * c->target_lin_vel;
-  float ty = rel_lin[1] / (mag + 1e-6f) * c->target_lin_vel;
+  float tx = rel_lin[0] / (mag + 1e-6f) * CI(target_lin_vel);
+  float ty = rel_lin[1] / (mag + 1e-6f) * CI(target_lin_vel);
   {
-    const float gate = mag > c->lin_reaching_criterion ? 1.0f : 0.0f;
+    const float gate = mag > CI(lin_reaching_criterion) ? 1.0f : 0.0f;
     tx = tx * gate;
     ty = ty * gate;
   }
@@ -1983,7 +1987,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int j = 0; j < 3; ++j) x[j] = sq_f(torque[j]);
     PUT(GO1_T_TORQUES, qsum((x[0] + x[1]) + x[2]));
 #pragma unroll
-    for (int j = 0; j < 3; ++j) x[j] = sq_f((ldv[j] - qd[j]) / c->dt);
+    for (int j = 0; j < 3; ++j) x[j] = sq_f((ldv[j] - qd[j]) / CI(dt));
     PUT(GO1_T_DOF_ACC, qsum((x[0] + x[1]) + x[2]));
 #pragma unroll
     for (int j = 0; j < 3; ++j) x[j] = sq_f(la[j] - act[j]);
@@ -1999,7 +2003,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     PUT(GO1_T_DOF_POS_LIMITS, qsum((x[0] + x[1]) + x[2]));
   }
   PUT(GO1_T_COLLISION, coll);
-  PUT(GO1_T_BASE_HEIGHT, sq_f(root[2] - c->base_height_target));
+  PUT(GO1_T_BASE_HEIGHT, sq_f(root[2] - CI(base_height_target)));
   PUT(GO1_T_ANG_VEL_XY, sq_f(bav[0]) + sq_f(bav[1]));
   PUT(GO1_T_ORIENTATION, sq_f(pg[0]) + sq_f(pg[1]));
   PUT(GO1_T_LARGE_VEL, vxy2 * (vmag > 0.5f ? 1.0f : 0.0f));  // reward_crawling.py:53-56
@@ -2010,37 +2014,37 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   PUT(GO1_T_REACHING_YAW_ABS, sq_f(rel_rot[2]));
   PUT(GO1_T_SURVIVE, 1.0f);
   {
-    const float rch = reached ? 1.0f : 0.0f, after = (float)ep > c->t_reach ? 1.0f : 0.0f;
+    const float rch = reached ? 1.0f : 0.0f, after = (float)ep > CI(t_reach) ? 1.0f : 0.0f;
     PUT(GO1_T_REACH_GOAL, rch);
     PUT(GO1_T_REACH_GOAL_T, rch * (float)ep);
     PUT(GO1_T_REACH_GOAL_TR, rch * after);
     PUT(GO1_T_LINEAR_VEL, norm3_f(blv[0], blv[1], blv[2]) > 0.7f ? 1.0f : 0.0f);
-    PUT(GO1_T_STALLING, -((vmag < c->small_vel_threshold && mag > c->large_dist_threshold) ? 1.0f : 0.0f));
+    PUT(GO1_T_STALLING, -((vmag < CI(small_vel_threshold) && mag > CI(large_dist_threshold)) ? 1.0f : 0.0f));
     // e2e (reward_crawling.py:61-77)
-    const float r_e2e = expf(-vxy2 / c->tracking_sigma_lin) * (mag < c->switch_dist ? 1.0f : 0.0f) * after;
-    const float r_end = (mag < c->switch_dist ? 1.0f : 0.0f) * c->max_episode_length;
-    PUT(GO1_T_E2E, c->terminate_end_of_trajectory ? r_end : r_e2e);
+    const float r_e2e = expf(-vxy2 / CI(tracking_sigma_lin)) * (mag < CI(switch_dist) ? 1.0f : 0.0f) * after;
+    const float r_end = (mag < CI(switch_dist) ? 1.0f : 0.0f) * CI(max_episode_length);
+    PUT(GO1_T_E2E, CI(terminate_end_of_trajectory) ? r_end : r_e2e);
   }
   {  // exploration_lin (reward_crawling.py:79-108) / reaching_linear_vel
-    const int form = c->lin_vel_form;
-    float r = expf(-le / c->tracking_sigma_lin);
+    const int form = CI(lin_vel_form);
+    float r = expf(-le / CI(tracking_sigma_lin));
     r = form == 1 ? fabsf(tx - blv[0]) + fabsf(ty - blv[1]) : r;
     r = form == 2 ? le : r;
     if (form == 3) {
-      const float rx = tx / c->target_lin_vel * blv[0] / (vmag + 1e-6f);
-      const float ry = ty / c->target_lin_vel * blv[1] / (vmag + 1e-6f);
+      const float rx = tx / CI(target_lin_vel) * blv[0] / (vmag + 1e-6f);
+      const float ry = ty / CI(target_lin_vel) * blv[1] / (vmag + 1e-6f);
       r = rx + ry;
-      r = r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f);
-      r = r + expf(-(vmag * vmag) / c->tracking_sigma_lin) * (mag < c->lin_reaching_criterion ? 1.0f : 0.0f);
+      r = r * (vmag > CI(small_vel_threshold) ? 1.0f : 0.0f);
+      r = r + expf(-(vmag * vmag) / CI(tracking_sigma_lin)) * (mag < CI(lin_reaching_criterion) ? 1.0f : 0.0f);
     }
     PUT(GO1_T_EXPLORATION_LIN, r);
   }
   {  // exploration_yaw (reward_crawling.py:110-120) / reaching_yaw
     float ta = rel_rot[2];
     const float m = fabsf(ta);
-    ta = ta / (m + 1e-6f) * c->target_ang_vel;
-    ta = ta * (m > c->ang_reaching_criterion ? 1.0f : 0.0f);
-    PUT(GO1_T_EXPLORATION_YAW, expf(-sq_f(ta - bav[2]) / c->tracking_sigma_ang));
+    ta = ta / (m + 1e-6f) * CI(target_ang_vel);
+    ta = ta * (m > CI(ang_reaching_criterion) ? 1.0f : 0.0f);
+    PUT(GO1_T_EXPLORATION_YAW, expf(-sq_f(ta - bav[2]) / CI(tracking_sigma_ang)));
   }
   // the rest of TrajectoryTrackingRewards, only when one of them is scaled
   constexpr uint32_t TT_HEAVY = (1u << GO1_T_DOF_VEL) | (1u << GO1_T_DOF_POS) | (1u << GO1_T_TASK) |
@@ -2054,16 +2058,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int j = 0; j < 3; ++j) x[j] = sq_f(q[j] - s_phys[LDS_DDP + leg * 3 + j]);
     PUT(GO1_T_DOF_POS, qsum((x[0] + x[1]) + x[2]));  // :31-33
     // task (:74-89)
-    PUT(GO1_T_TASK, expf(-le / c->tracking_sigma_lin) * (mag < c->large_dist_threshold ? 1.0f : 0.0f));
+    PUT(GO1_T_TASK, expf(-le / CI(tracking_sigma_lin)) * (mag < CI(large_dist_threshold) ? 1.0f : 0.0f));
     {  // task_old (:51-55)
-      float r = 0.5f / (0.5f + mag) / c->t_reach;
-      PUT(GO1_T_TASK_OLD, r * ((float)ep > c->t_reach ? 1.0f : 0.0f));
+      float r = 0.5f / (0.5f + mag) / CI(t_reach);
+      PUT(GO1_T_TASK_OLD, r * ((float)ep > CI(t_reach) ? 1.0f : 0.0f));
     }
     {  // exploration (:91-99)
       float r = blv[0] * rel_lin[0] + blv[1] * rel_lin[1];
       r = r / (mag + 1e-6f);
       r = r / (vmag + 1e-6f);
-      PUT(GO1_T_EXPLORATION, r * (vmag > c->small_vel_threshold ? 1.0f : 0.0f));
+      PUT(GO1_T_EXPLORATION, r * (vmag > CI(small_vel_threshold) ? 1.0f : 0.0f));
     }
   }
   // feet_air_time (trajectory_tracking_reward.py:126-137) mutates last_contacts / feet_air_time
@@ -2075,7 +2079,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const bool filt = contact || lc != 0.0f;
     lc_new = contact ? 1.0f : 0.0f;
     const bool first = air > 0.0f && filt;
-    air = air + c->dt;
+    air = air + CI(dt);
     const float r = (air - 0.5f) * (first ? 1.0f : 0.0f);
     air_new = air * (filt ? 0.0f : 1.0f);
     PUT(GO1_T_FEET_AIR_TIME, qsum(r));
@@ -2085,8 +2089,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // updates its episode sum; every lane then adds the slots up in order from LDS.  pos / neg bucket
   // by the sign of the sum over envs, which for a sign-definite term is the sign of its scale.
   __shared__ float s_r[SEPB][GO1_MAX_TERMS];
-  const bool global_buckets = c->indefinite_slots != 0;
-  const bool live = (c->live_slots >> sub16) & 1u;
+  const bool global_buckets = CI(indefinite_slots) != 0;
+  const bool live = (CI(live_slots) >> sub16) & 1u;
   {
     float t = live ? s_terms[el][my_id] : 0.0f;
     if (diverged) t = 0.0f;
@@ -2104,7 +2108,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const uint64_t nonneg = __ballot(my_scale >= 0.0f);
   const uint32_t posm = (uint32_t)((nonneg & 0xFull) | ((nonneg >> 12) & 0xF0ull) | ((nonneg >> 24) & 0xF00ull) |
                                    ((nonneg >> 36) & 0xF000ull));
-  const uint32_t livem = c->live_slots;
+  const uint32_t livem = CI(live_slots);
   float rew = 0.0f, pos = 0.0f, neg = 0.0f;
   {
     float rr[GO1_MAX_TERMS];
@@ -2118,11 +2122,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
   }
-  if (c->reward_mode == 1) rew = rew < 0.0f ? 0.0f : rew;            // only_positive_rewards (:341-342)
-  else if (c->reward_mode == 2) rew = pos * expf(neg / c->sigma_rew_neg);  // ji22 style (:343-344)
+  if (CI(reward_mode) == 1) rew = rew < 0.0f ? 0.0f : rew;            // only_positive_rewards (:341-342)
+  else if (CI(reward_mode) == 2) rew = pos * expf(neg / CI(sigma_rew_neg));  // ji22 style (:343-344)
   // episode sums total / total_pos / total_neg (:346-348); with global buckets the bucket launch
   // adds total_pos / total_neg (and the ji22 reward)
-  if (sub16 == 0 && !(global_buckets && c->reward_mode == 2)) my_tot = my_tot + rew;
+  if (sub16 == 0 && !(global_buckets && CI(reward_mode) == 2)) my_tot = my_tot + rew;
   if (!global_buckets) {
     if (sub16 == 1) my_tot = my_tot + pos;
     if (sub16 == 2) my_tot = my_tot + neg;
@@ -2186,10 +2190,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   MARK(reset_done);
   // ---- compute_observations (:357-475)
-  const int NO = c->num_obs;
+  const int NO = CI(num_obs);
   float* o = A.obs + (size_t)e * NO;
   float* oh = A.obs_history ? A.obs_history + (size_t)e * NO : nullptr;  // optional second copy
-  const float clip = c->clip_obs;
+  const float clip = CI(clip_obs);
   // noise uniforms rng(47 + i) (:472-473): every lane draws exactly two Philox blocks, the
   // same two-block code path in all lanes (the per-value calls of the two store branches
   // ran five Philox evaluations per wave, one after the other): role r < 3 needs slots
@@ -2198,13 +2202,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float uA[4], uB[4];
   {
     const int sa = role < 3 ? 52 + dn : 44, sb = role < 3 ? 64 + dn : 48;
-    if (c->add_noise) {
+    if (CI(add_noise)) {
       rng.quad(sa >> 2, uA);
       rng.quad(sb >> 2, uB);
     }
   }
   auto put = [&](int i, float v, float nv, float u, bool noisy) {
-    if (noisy && c->add_noise) v = v + (2.0f * u - 1.0f) * nv;
+    if (noisy && CI(add_noise)) v = v + (2.0f * u - 1.0f) * nv;
     v = clampf(v, -clip, clip);
     o[i] = v;
     if (oh) oh[i] = v;
@@ -2212,29 +2216,29 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // role r < 3 writes joint r of its leg; role 3 of leg 0 writes gravity and commands, role 3
   // of leg 1 the episode progress (timestep_in_obs, :375-377: post-reset episode length)
   if (role == 3 && leg == 0) {
-    put(0, pg[0], c->noise_gravity, uA[3], true);
-    put(1, pg[1], c->noise_gravity, uB[0], true);
-    put(2, pg[2], c->noise_gravity, uB[1], true);
+    put(0, pg[0], CI(noise_gravity), uA[3], true);
+    put(1, pg[1], CI(noise_gravity), uB[0], true);
+    put(2, pg[2], CI(noise_gravity), uB[1], true);
     put(3, cmd[0] * 1.0f, 0.0f, 0.0f, false);
     put(4, cmd[1] * 1.0f, 0.0f, 0.0f, false);
   }
-  if (c->timestep_in_obs && role == 3 && leg == 1)
-    put(41, (float)(reset ? 0 : ep) / c->max_episode_length, 0.0f, 0.0f, false);
+  if (CI(timestep_in_obs) && role == 3 && leg == 1)
+    put(41, (float)(reset ? 0 : ep) / CI(max_episode_length), 0.0f, 0.0f, false);
   if (role < 3) {
     const int j = role, d = dn;
     const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act);
     const float un = sel4((52 + d) & 3, uA[0], uA[1], uA[2], uA[3]);
     const float uv = sel4((64 + d) & 3, uB[0], uB[1], uB[2], uB[3]);
-    put(5 + d, (qj - s_phys[LDS_DDP + d]) * c->obs_scale_dof_pos, c->noise_dof_pos, un, true);
-    put(17 + d, qdj * c->obs_scale_dof_vel, c->noise_dof_vel, uv, true);
+    put(5 + d, (qj - s_phys[LDS_DDP + d]) * CI(obs_scale_dof_pos), CI(noise_dof_pos), un, true);
+    put(17 + d, qdj * CI(obs_scale_dof_vel), CI(noise_dof_vel), uv, true);
     put(29 + d, aj, 0.0f, 0.0f, false);
   }
   MARK(obs_props_done);
   // height observations (:395-411) from the samples gathered after the physics
   if (scan) {
-    const int o_h = 41 + c->timestep_in_obs;
+    const int o_h = 41 + CI(timestep_in_obs);
     const float zroot = root[2];  // post-reset (:401)
-    const float cam_z = pm_sinf(cam_p) * c->camera_offset_norm;
+    const float cam_z = pm_sinf(cam_p) * CI(camera_offset_norm);
 #pragma unroll
     for (int k = 0; k < KPTS; ++k) {
       const int p = sub16 + 16 * k;
@@ -2242,16 +2246,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int layer = 0; layer < 2; ++layer) {
           float hh = hv[k][layer];
-          if (c->camera_zero) {
+          if (CI(camera_zero)) {
             hh = hh - zroot;
             hh = hh - cam_z;
             hh = clampf(hh, -0.3f, 0.3f);
           } else {
-            hh = clampf(hh, 0.0f, c->ceiling_height);
-            hh = hh / c->ceiling_height;
+            hh = clampf(hh, 0.0f, CI(ceiling_height));
+            hh = hh / CI(ceiling_height);
             hh = hh - 0.5f;
           }
-          const float v = clampf(hh * c->obs_scale_heights, -clip, clip);
+          const float v = clampf(hh * CI(obs_scale_heights), -clip, clip);
           o[o_h + layer * n_pts + p] = v;
           if (oh) oh[o_h + layer * n_pts + p] = v;
         }
@@ -2270,8 +2274,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   if (sub16 == 0) {
     float* pv = A.priv + (size_t)e * GO1_NUM_PRIV;
-    pv[0] = clampf((friction - c->priv_friction_shift) * c->priv_friction_scale, -clip, clip);
-    pv[1] = clampf((restitution - c->priv_rest_shift) * c->priv_rest_scale, -clip, clip);
+    pv[0] = clampf((friction - CI(priv_friction_shift)) * CI(priv_friction_scale), -clip, clip);
+    pv[1] = clampf((restitution - CI(priv_rest_shift)) * CI(priv_rest_scale), -clip, clip);
   }
 
   MARK(priv_done);
@@ -2459,11 +2463,23 @@ struct go1_handle {
   float* d_bucket_r = nullptr;    // global reward bucketing scratch (indefinite_slots != 0)
   double* d_bucket_sum = nullptr; // 2 banks x GO1_MAX_TERMS
   uint64_t count = 0;          // go1_step calls so far
+  bool spec = false;           // every GO1_SPEC_FIELDS value matches: the specialised kernel runs
   const uint8_t* prev_time_out = nullptr;
   uint8_t* prev_extras = nullptr;
 };
 
 static thread_local std::string g_err;
+
+// the specialised kernel's values must match bit for bit (-0.0 and 0.0 are different constants)
+template <class T>
+static bool spec_eq(T a, T b) { return memcmp(&a, &b, sizeof(T)) == 0; }
+static bool spec_match(const go1_config& c) {
+  bool m = true;
+#define GO1_SPEC_CHECK(f, v) m = m && spec_eq(c.f, (decltype(c.f))(v));
+  GO1_SPEC_FIELDS(GO1_SPEC_CHECK)
+#undef GO1_SPEC_CHECK
+  return m;
+}
 
 static int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -2534,6 +2550,7 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   go1_handle* h = new (std::nothrow) go1_handle();
   if (!h) return fail(GO1_E_ARG, "go1_create: out of host memory");
   h->cfg = *cfg;
+  h->spec = spec_match(*cfg);
   hipError_t e1 = hipMalloc(&h->d_cfg, sizeof(go1_config));
   hipError_t e2 = hipMalloc(&h->d_flags, 3 * sizeof(int32_t));
   if (e1 != hipSuccess || e2 != hipSuccess) {
@@ -2607,11 +2624,13 @@ int go1_step(go1_handle* h, const go1_step_args* a, void* stream) {
                            "reward slots (their bucket pass rewrites rows by env)");
   if (a->ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_begin, s));
   if (inj) {
-    if (full) hipLaunchKernelGGL((go1_step_kernel<true, 15>), grid, block, 0, s, h->d_cfg, K);
-    else hipLaunchKernelGGL((go1_step_kernel<true, 7>), grid, block, 0, s, h->d_cfg, K);
+    if (full) hipLaunchKernelGGL((go1_step_kernel<true, 15, false>), grid, block, 0, s, h->d_cfg, K);
+    else hipLaunchKernelGGL((go1_step_kernel<true, 7, false>), grid, block, 0, s, h->d_cfg, K);
+  } else if (h->spec) {  // the README configuration (go1_spec.h): measure_front_half, 7 points per lane
+    hipLaunchKernelGGL((go1_step_kernel<false, 7, true>), grid, block, 0, s, h->d_cfg, K);
   } else {
-    if (full) hipLaunchKernelGGL((go1_step_kernel<false, 15>), grid, block, 0, s, h->d_cfg, K);
-    else hipLaunchKernelGGL((go1_step_kernel<false, 7>), grid, block, 0, s, h->d_cfg, K);
+    if (full) hipLaunchKernelGGL((go1_step_kernel<false, 15, false>), grid, block, 0, s, h->d_cfg, K);
+    else hipLaunchKernelGGL((go1_step_kernel<false, 7, false>), grid, block, 0, s, h->d_cfg, K);
   }
   HIP_TRY(hipGetLastError());
   if (a->ev_end) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_end, s));
@@ -2626,6 +2645,15 @@ h->prev_time_out = a->time_out;
   h->count++;
   return GO1_OK;
 }
+
+int go1_specialize(go1_handle* h, int enable) {
+  if (!h) return fail(GO1_E_ARG, "go1_specialize: null handle");
+  if (enable && !spec_match(h->cfg)) return fail(GO1_E_ARG, "go1_specialize: the config differs from the specialised one (go1_spec.h)");
+  h->spec = enable != 0;
+  return GO1_OK;
+}
+
+int go1_is_specialized(go1_handle* h) { return h && h->spec ? 1 : 0; }
 
 int go1_sync_time_outs(go1_handle* h, void* stream) {
   if (!h) return fail(GO1_E_ARG, "go1_sync_time_outs: null handle");

@@ -40,6 +40,8 @@ def lib():
     l.go1_time_outs_pending.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     l.go1_actuator_net.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     l.go1_destroy.argtypes = [C.c_void_p]
+    l.go1_specialize.argtypes = [C.c_void_p, C.c_int]
+    l.go1_is_specialized.argtypes = [C.c_void_p]
     if l.go1_abi_version() != abi.GO1_ABI_VERSION:
         raise NativeError("ABI version mismatch")
     _lib = l
@@ -246,6 +248,15 @@ class Go1Native:
         rc = self._lib_step(self.h, C.byref(a), torch._C._cuda_getCurrentRawStream(self._dev_index))
         if rc:
             _check(rc)
+
+    def specialize(self, enable):
+        """Force the generic step kernel (False) or the README-config specialisation (True; raises
+        if this config differs from it).  go1_create picks the specialisation when it applies."""
+        _check(lib().go1_specialize(self.h, int(bool(enable))))
+
+    @property
+    def specialized(self):
+        return bool(lib().go1_is_specialized(self.h))
 
     def sync_time_outs(self):
         """Make extras_time_outs current for the last step (the rebinding of step k is

@@ -208,3 +208,47 @@ def test_full_size_height_scan_bit_exact_from_post_physics_pose():
         np.testing.assert_array_equal(got[keepenv], want[keepenv], err_msg=f"step {t}")
         checked += int(keepenv.sum())
     assert checked > 5 * N
+
+
+def test_specialised_kernel_is_bit_identical_to_generic():
+    """go1_create runs the README-configuration specialisation of the step kernel (integer flags
+    of go1_spec.h folded at compile time) for this config; forced onto the generic instantiation,
+    a second handle must produce bit-identical outputs and state, step after step, with debug
+    outputs, aux, the compact episode log and resets included."""
+    cfg, td, dr, ep, rng = _setup(seed=13)
+    c, ga, k1 = _handle(cfg, td, dr, ep, 0, N)
+    _, gb, k2 = _handle(cfg, td, dr, ep, 0, N)
+    assert ga.specialized and gb.specialized
+    gb.specialize(False)
+    assert not gb.specialized
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    grav, gvec = CF.gravity_state([0.1, -0.3, 0.2])
+    W = 10 + 8  # n_terms + 8: compact rows
+    bufs = []
+    for g in (ga, gb):
+        bufs.append(dict(dbg=native.debug_buffers(N, c.decimation, DEV), aux=torch.zeros((N, 32), device=DEV),
+                         log=torch.zeros((N * 16, W), device=DEV), cnt=torch.zeros(1, dtype=torch.int32, device=DEV),
+                         div=torch.zeros(1, dtype=torch.int64, device=DEV)))
+    torch.cuda.synchronize()
+    del k1, k2
+    for t in range(16):
+        a = torch.randn(N, 12, device=DEV)
+        for g, b in zip((ga, gb), bufs):
+            args = g.prepare(dict(obs=g.obs, priv=g.priv, rew=g.rew, reset=g.reset, time_out=g.time_out),
+                             aux=b["aux"], diverged_count=b["div"], episode_log=b["log"], log_count=b["cnt"])
+            g.step_prepared(args, a, gvec, grav, scales, ("k", t), 5, t, log_tag=t)
+            g.step(a, gvec, grav, scales, rng_seed=6, rng_step=1000 + t, debug=b["dbg"])
+        torch.cuda.synchronize()
+        for name in ("obs", "priv", "rew", "reset", "time_out", "contact_forces"):
+            np.testing.assert_array_equal(getattr(ga, name).cpu().numpy(), getattr(gb, name).cpu().numpy(),
+                                          err_msg=f"step {t}: {name}")
+        for k in ("aux", "div", "cnt"):
+            np.testing.assert_array_equal(bufs[0][k].cpu().numpy(), bufs[1][k].cpu().numpy(), err_msg=f"{t}: {k}")
+        for k, v in bufs[0]["dbg"].items():
+            np.testing.assert_array_equal(v.cpu().numpy(), bufs[1]["dbg"][k].cpu().numpy(), err_msg=f"{t}: {k}")
+    rows = [b["log"][: int(b["cnt"].item())].cpu().numpy() for b in bufs]
+    order = [np.lexsort((r[:, -1], r[:, -2])) for r in rows]
+    np.testing.assert_array_equal(rows[0][order[0]], rows[1][order[1]])
+    sa, sb = ga.state.numpy(), gb.state.numpy()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
