@@ -1483,36 +1483,41 @@ __device__ void traj_waypoint(CCfg* __restrict__ c, const Rng& rng, const float*
   }
 }
 
-// reset_idx for one env, computed redundantly by the 4 lanes of its quad (:218-296)
-__device__ void reset_env(CCfg* __restrict__ c, const go1_terrain& ter, const Rng& rng, int e, int leg,
-                          float* root, float* q, float* qd, float* strength, float* offset, float* traj) {
-  float s = rng(0) * c->strength_range + c->strength_lo;
+// reset_idx for one env, computed redundantly by the lanes of the env (:218-296).  `u(slot)` is
+// the reset's uniform of slots 0 .. GO1_RESET_SLOTS - 1 (the step kernel draws their Philox
+// blocks once per env, one block per lane, and passes them through LDS); `rng` serves the
+// trajectory draws beyond them.  `eo` = env_origins[e] (loaded ahead by the caller).
+#define GO1_RESET_SLOTS 36
+template <class U>
+__device__ void reset_env(CCfg* __restrict__ c, const U& u, const Rng& rng, const float* eo, int leg,
+                          const float* ddp, float* root, float* q, float* qd, float* strength, float* offset,
+                          float* traj) {
+  float s = u(0) * c->strength_range + c->strength_lo;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int d = leg * 3 + j;
     strength[j] = s;
-    offset[j] = rng(1 + d) * c->offset_range + c->offset_lo;
+    offset[j] = u(1 + d) * c->offset_range + c->offset_lo;
   }
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int d = leg * 3 + j;
-    float f = c->reset_dof_range * rng(13 + d) + c->reset_dof_lo;
-    q[j] = c->default_dof_pos[d] * f;
+    float f = c->reset_dof_range * u(13 + d) + c->reset_dof_lo;
+    q[j] = ddp[d] * f;
     qd[j] = 0.0f;
   }
 #pragma unroll
   for (int i = 0; i < 13; ++i) root[i] = c->base_init_state[i];
-  const float* eo = ter.env_origins + (size_t)e * 3;
   root[0] = root[0] + eo[0];
   root[1] = root[1] + eo[1];
   root[2] = root[2] + eo[2];
   if (c->custom_origins) {
-    root[0] = root[0] + (c->x_init_range2 * rng(25) + c->x_init_lo);
-    root[1] = root[1] + (c->y_init_range2 * rng(26) + c->y_init_lo);
+    root[0] = root[0] + (c->x_init_range2 * u(25) + c->x_init_lo);
+    root[1] = root[1] + (c->y_init_range2 * u(26) + c->y_init_lo);
     root[0] = root[0] + c->x_init_offset;
     root[1] = root[1] + c->y_init_offset;
   }
-  float yaw = c->yaw_range2 * rng(27) + c->yaw_lo;
+  float yaw = c->yaw_range2 * u(27) + c->yaw_lo;
   float thh = yaw / 2.0f, sth, cth;
   pm_sincosf(thh, &sth, &cth);
   float qv[4] = {0.0f * sth, 0.0f * sth, 1.0f * sth, cth};
@@ -1521,9 +1526,10 @@ __device__ void reset_env(CCfg* __restrict__ c, const go1_terrain& ter, const Rn
 #pragma unroll
   for (int i = 0; i < 4; ++i) root[3 + i] = qv[i] / qn;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) root[7 + i] = c->reset_vel_range * rng(28 + i) + c->reset_vel_lo;
+  for (int i = 0; i < 6; ++i) root[7 + i] = c->reset_vel_range * u(28 + i) + c->reset_vel_lo;
   traj_waypoint(c, rng, root, 0, traj);
 }
+static_assert(28 + 6 <= GO1_RESET_SLOTS, "reset_env's uniform slots");
 
 // every waypoint w = first, first + stride, ... of the env's new trajectory (_resample_trajectory :949-955)
 __device__ void write_trajectory(CCfg* __restrict__ c, const Rng& rng, const float* root, float* __restrict__ dst,
@@ -1599,6 +1605,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int sl = 0; sl < GO1_LAG_SLOTS - 1; ++sl) lag_pre[sl][j] = lag_in[(sl + 1) * 12 + j];
   }
   const float friction = st.friction[e], payload = st.payload[e];
+  // the env origin a reset needs, with the prologue loads (no memory round trip in the reset path)
+  const float eo_pre[3] = {K.ter.env_origins[(size_t)e * 3], K.ter.env_origins[(size_t)e * 3 + 1],
+                           K.ter.env_origins[(size_t)e * 3 + 2]};
   const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
   // ---- the post-physics state inputs ride with the prologue loads (one wait for all of
   // them); they are held across the sub-step loop (AGPRs), so after the physics only the
@@ -2169,8 +2178,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   }
   if (reset) {
-    reset_env(c, K.ter, rng, e, leg, root, q, qd, strength, offset, traj_new);
+#ifndef GO1_ABL_NO_RESET  // ablation build only: resets keep the state
+    {
+      // the reset's uniforms (slots 0 .. 35 = Philox blocks 0 .. 8): lane sub16 < 9 of the env
+      // draws block sub16 (one evaluation per lane instead of one per draw), the env's lanes read
+      // them back from LDS (one wave per block: its LDS operations complete in order)
+      __shared__ float s_ru[SEPB][GO1_RESET_SLOTS];
+      if (sub16 < GO1_RESET_SLOTS / 4) {
+        float uq[4];
+        rng.quad(sub16, uq);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s_ru[el][4 * sub16 + k] = uq[k];
+      }
+      const float* ru = s_ru[el];
+      auto u = [ru](int slot) { return ru[slot]; };
+      reset_env(c, u, rng, eo_pre, leg, s_phys + LDS_DDP, root, q, qd, strength, offset, traj_new);
+    }
     write_trajectory(c, rng, root, st.trajectory + (size_t)e * 6 * TL, sub16, 16);
+#endif
     idx = 0;
     my_sum = 0.0f;
     my_tot = 0.0f;
@@ -2372,7 +2397,9 @@ __global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __rest
   if (e >= c->n_envs || !mask[e]) return;
   const Rng rng = {U, seed, step, e, e + c->env_id_offset, c->u_per_env};
   float root[13], q[3], qd[3], strength[3], offset[3], traj[6];
-  reset_env(c, ter, rng, e, leg, root, q, qd, strength, offset, traj);
+  const float eo[3] = {ter.env_origins[(size_t)e * 3], ter.env_origins[(size_t)e * 3 + 1],
+                       ter.env_origins[(size_t)e * 3 + 2]};
+  reset_env(c, rng, rng, eo, leg, c_gen->default_dof_pos, root, q, qd, strength, offset, traj);
   const size_t d0 = (size_t)e * NDOF + leg * 3;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
