@@ -842,7 +842,11 @@ __device__ __forceinline__ void height_query_pk(const Terr& T, float x, float y,
   const int i = (int)fu, j = (int)fv;
   const float a = u - fu, b = v - fv;
   f2 c00, c10, c01, c11;
+#ifdef GO1_ABL_NO_FALLBACK  // ablation build only: every query from the (clamped) LDS patch
+  const int li = min(max(i - T.pi0, 0), PSZX - 2), lj = min(max(j - T.pj0, 0), PSZY - 2);
+#else
   const int li = i - T.pi0, lj = j - T.pj0;
+#endif
   if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
     const float2* pp = T.patch + li * PSZY + lj;
     const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];

@@ -66,6 +66,9 @@ def main():
             tot[nm] += int(t[w, i + 1] - t[w, i])
             cnt[nm] += 1
     L = float(np.mean(life))
+    lf = np.array(life, np.float64)
+    print(f"wave lifetime cycles: p50 {np.percentile(lf, 50):.0f}  p90 {np.percentile(lf, 90):.0f}  "
+          f"p99 {np.percentile(lf, 99):.0f}  max {lf.max():.0f}  min {lf.min():.0f}")
     starts = t[:, 0]
     print(f"waves {len(life)}; mean wave lifetime {L:.0f} cycles (s_memtime); start spread "
           f"{(starts.max() - starts.min()):.0f} cycles; stamps per wave {int(np.mean(np.count_nonzero(line, 1)))}")
