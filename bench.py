@@ -50,8 +50,10 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
 #           trajectory 24, base rotation 12, episode sums 52, counters 12               -> 2,279 B
 BYTES_PER_ENV_STEP = 1936 + 2279
 # The VecEnv.step path additionally has the kernel write the HistoryWrapper's obs_history copy
-# (1,044 B), the episode log row (64 B) and the extras aux row (128 B).
-BYTES_PER_ENV_STEP_VECENV = BYTES_PER_ENV_STEP + 1044 + 64 + 128
+# (1,044 B) and the extras aux row (128 B); the compact episode log writes a 72-B row per reset env
+# only (~8 per step at 4096 envs: < 0.2 B per env-step, not counted).
+BYTES_PER_ENV_STEP_VECENV = BYTES_PER_ENV_STEP + 1044 + 128
+PREWARM_S = 0.25
 # Algorithmic FLOPs per env-step: actuator net 12 joints x 4 sub-steps x 2,688; the
 # integrator and post-physics are not counted here.
 FLOPS_PER_ENV_STEP = 12 * 4 * 2688
@@ -377,6 +379,17 @@ def main():
     n_ev = (args.steps + every - 1) // every
     ev = EventPairs(n_ev)
     base = env.env
+    # clock pre-warm: the GPU ramps its clocks over the first ~10-20 ms of sustained load (a 500-step
+    # loop right after 50 warmup steps measured 68.5 us/step, after 200 warmup steps 57.7), so the
+    # env is stepped for PREWARM_S seconds (untimed, reported as "prewarm_steps") before the W
+    # warmup steps the caller asked for
+    prewarm = 0
+    t_pw = time.perf_counter()
+    while time.perf_counter() - t_pw < PREWARM_S:
+        for _ in range(16):
+            env.step(ring[prewarm % 64])
+            prewarm += 1
+        torch.cuda.synchronize()
     for k in range(args.warmup):
         env.step(ring[k % 64])
     torch.cuda.synchronize()
@@ -417,7 +430,8 @@ def main():
         ksteps = min(args.steps, 200)
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "warmup": args.warmup, "prewarm_steps": prewarm, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "BASELINE configs[2]: VecEnv.step of HistoryWrapper(TrajectoryTrackingEnv), Go1 "
                                    "single_path tunnel (32x32 sub-terrains), 2x10x11 front height scan, actuator "
