@@ -55,11 +55,15 @@ typedef struct go1_transition {
 /* Fused policy inference (ActorCritic.act / evaluate, actor_critic.py:121-150) for the
  * default AC_Args architecture: adaptation 261 -> 256 -> 128 -> 2, actor
  * [hist, latent] -> 512 -> 256 -> 128 -> num_actions, critic [hist, priv] -> 512 -> 256
- * -> 128 -> 1, ELU.  Weights packed by legged_tracking_amd/rollout.py (fragment order,
+ * -> 128 -> 1, ELU, to f32 accuracy on f16 matrix cores (3xF16 split products, see rollout.hip).
+ * Weights split and packed by legged_tracking_amd/rollout.py (fragment order,
  * layers: a1 a2 a3 p1 p2 p3 p4 c1 c2 c3 c4). */
 #define GO1_POLICY_LAYERS 11
 typedef struct go1_policy_layer {
-  const float* w; /* [n/16][k/4][64], n and k padded to 16 / 4 */
+  /* [n/16][k/16][64 lanes][8] f16 (n, k padded to 16): each weight w split into hi = f16(w) and
+     lo = f16(w - hi); record (t, g, lane = 16 q + m) = hi, then lo, of W[16 t + m][16 g + 4 q + r],
+     r = 0..3 (16 bytes: the lane's A fragments of v_mfma_f32_16x16x16_f16 for both halves) */
+  const void* w;
   const float* b; /* [n padded to 16] */
 } go1_policy_layer;
 typedef struct go1_policy_args {

@@ -154,44 +154,69 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
 }
 
 // ------------------------------------------------------------------ policy inference
-// ActorCritic.act / evaluate (actor_critic.py:121-150) for 16 envs per workgroup of 8
-// waves (two per SIMD, so one wave's MFMAs cover the other's weight loads), every layer on v_mfma_f32_16x16x4_f32 with weights as the A operand
-// (16 output features x 4 k) and activations as B (4 k x 16 envs):
+// ActorCritic.act / evaluate (actor_critic.py:121-150) for 16 envs per workgroup of 16 waves:
 //   adaptation: hist(261) -> 256 -> 128 -> 2 (latent)
 //   actor:      [hist, latent](263) -> 512 -> 256 -> 128 -> 12 (action mean)
 //   critic:     [hist, priv](263)   -> 512 -> 256 -> 128 -> 1  (value)
-// ELU between layers.  Activations stay in LDS as [feature][env] (B-fragment reads are
-// conflict-free rows of 16 floats); weights are pre-packed on the host into fragment
-// order (one coalesced 256 B load per MFMA, L2-resident: 2.8 MB for all three nets).
+// ELU between layers.  f32 accuracy from f16 matrix cores ("3xF16"): every f32 weight and
+// activation x is split into hi = f16(x) and lo = f16(x - hi) (22 significant bits together),
+// and each 16-deep K group of a dot product is three v_mfma_f32_16x16x16_f16,
+//   acc += Whi Xhi + Whi Xlo + Wlo Xhi
+// with products exact in f32 and f32 accumulation; the dropped Wlo Xlo term is ~2^-22 of the
+// product, below the f32 rounding of the sums.  Three f16 MFMAs (8 cycles each on gfx950) replace
+// four v_mfma_f32_16x16x4_f32 (32 cycles each) per 16 K values.  Weights are split and packed on
+// the host into fragment order: one 16-byte load per lane per (tile, K group) = 4 hi + 4 lo
+// halves, L2-resident (2.8 MB for all three nets).  Activations live in LDS already split, as
+// [k/4][env][4] halves (hi plane, then lo plane): a B fragment (k = 16 g + 4 q + r, env c) is one
+// 8-byte read per plane, and a layer's output tile (rows 4 q + r of env c) is one 8-byte write.
 #ifndef GO1_POLICY_SCHED
 #define GO1_POLICY_SCHED 1
 #endif
-#ifndef GO1_POLICY_PREFETCH
-#define GO1_POLICY_PREFETCH 2
-#endif
 constexpr int PIN = 272;  // 261 / 263 inputs padded to a multiple of 16
+constexpr int PW = 16;    // waves per workgroup (four per SIMD)
 
-typedef go1_policy_layer PolicyLayer;  // w packed [n/16][k/4][64], b [n padded to 16]
+typedef go1_policy_layer PolicyLayer;  // w packed [n/16][k/16][64 lanes][4 hi + 4 lo halves], b [n padded to 16]
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+
+// split activation planes in LDS: element (k, env c) at [k / 4][c][k % 4] of hi, and of lo
+struct ActV {
+  h4_t* hi;
+  h4_t* lo;
+};
+template <int K>
+struct Act {
+  h4_t hi[K / 4][16];
+  h4_t lo[K / 4][16];
+  __device__ ActV v() { return ActV{&hi[0][0], &lo[0][0]}; }
+};
 
 __device__ __forceinline__ float elu(float x) { return x > 0.0f ? x : expm1f(x); }
 
-// NT output tiles (tile indices tile0 + i * tstride) of one layer for the 16 envs:
-// acc = b + W x, then ELU (act) and store to dst[feature][env].  Weights are packed
-// [tile][k/16][lane][4]: one 16-byte load per lane feeds four K-steps of one tile, and
-// the next group's loads are issued before the current group's MFMAs (double buffer).
-template <int NT, int NL>
-__device__ __forceinline__ void policy_group(const f4_t (&w)[NL][NT], const float (*const* src)[16], int g, int q,
-                                             int c, f4_t (&acc)[NL][NT]) {
+// four consecutive features 4 kq .. 4 kq + 3 of env c, split into the two planes
+__device__ __forceinline__ void act_store4(ActV d, int kq, int c, f4_t v) {
+  h4_t h, l;
 #pragma unroll
-  for (int l = 0; l < NL; ++l) {
-    float bv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) bv[u] = src[l][16 * g + 4 * u + q][c];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int i = 0; i < NT; ++i) acc[l][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[l][i][u], bv[u], acc[l][i], 0, 0, 0);
+  for (int r = 0; r < 4; ++r) {
+    h[r] = (_Float16)v[r];
+    l[r] = (_Float16)(v[r] - (float)h[r]);
   }
+  d.hi[kq * 16 + c] = h;
+  d.lo[kq * 16 + c] = l;
+}
+__device__ __forceinline__ void act_store1(ActV d, int k, int c, float v) {
+  const _Float16 h = (_Float16)v;
+  reinterpret_cast<_Float16*>(d.hi)[((k >> 2) * 16 + c) * 4 + (k & 3)] = h;
+  reinterpret_cast<_Float16*>(d.lo)[((k >> 2) * 16 + c) * 4 + (k & 3)] = (_Float16)(v - (float)h);
+}
+
+// acc += W x over one 16-deep K group: w = (4 hi, 4 lo) halves of the lane's A fragment
+__device__ __forceinline__ f4_t mfma3(f4_t w, h4_t xh, h4_t xl, f4_t acc) {
+  typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+  const h8_t wv = __builtin_bit_cast(h8_t, w);
+  const h4_t wh = {wv[0], wv[1], wv[2], wv[3]}, wl = {wv[4], wv[5], wv[6], wv[7]};
+  acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wl, xh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wh, xl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(wh, xh, acc, 0, 0, 0);
 }
 
 template <int NT, int NL>
@@ -209,100 +234,57 @@ __device__ __forceinline__ void policy_load(const PolicyLayer* L, int G, int g, 
 #endif
 }
 
-// NT output tiles (tile0 + i * tstride) of NL layers at the same depth (the actor and the
-// critic advance together) for the 16 envs: acc = b + W x, ELU (act), store to
-// dst[feature][env].  Weights are packed [tile][k/16][lane][4]: one 16-byte load per lane
-// feeds four K-steps of one tile; loads run two groups ahead of the MFMAs.
 template <int NT, int NL>
-__device__ __forceinline__ void policy_tiles(const PolicyLayer* L, int S, const float (*const* src)[16], int tile0,
-                                             int tstride, float (*const* dst)[16], bool act, int lane) {
+__device__ __forceinline__ void policy_group(const f4_t (&w)[NL][NT], const ActV* src, int g, int q, int c,
+                                             f4_t (&acc)[NL][NT]) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const h4_t xh = src[l].hi[(4 * g + q) * 16 + c], xl = src[l].lo[(4 * g + q) * 16 + c];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[l][i] = mfma3(w[l][i], xh, xl, acc[l][i]);
+  }
+}
+
+// NT output tiles (tile0 + i * tstride) of NL layers at the same depth (the actor and the critic
+// advance together) for the 16 envs: acc = b + W x, ELU (act), store split to dst.  The G K groups
+// are unrolled and the weight fragments run D groups ahead of the MFMAs: with three 8-cycle f16
+// MFMAs per fragment the layers are bound by the L2 -> CU weight stream, which needs ~12
+// 16-byte loads in flight per lane (64 B/clk/CU x the L2 latency, 16 waves).
+template <int NT, int NL, int G, int D>
+__device__ __forceinline__ void policy_tiles(const PolicyLayer* L, const ActV* src, int tile0, int tstride,
+                                             const ActV* dst, bool act, int lane) {
   const int q = lane >> 4, c = lane & 15;
-  const int G = S >> 2;  // groups of four K-steps (K padded to a multiple of 16)
-  f4_t acc[NL][NT], wa[NL][NT], wb[NL][NT];
+  f4_t acc[NL][NT], w[D][NL][NT];
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
     for (int i = 0; i < NT; ++i)
       acc[l][i] = *reinterpret_cast<const f4_t*>(L[l].b + 16 * (tile0 + i * tstride) + 4 * q);
-#if GO1_POLICY_PREFETCH == 3
-  // weights two groups ahead, B operands (LDS) one group ahead of the MFMAs
-  float ba[NL][4], bb[NL][4];
-  auto read_b = [&](int g, float (&b)[NL][4]) {
 #pragma unroll
-    for (int l = 0; l < NL; ++l)
+  for (int g = 0; g < D && g < G; ++g) policy_load<NT, NL>(L, G, g, tile0, tstride, lane, w[g]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) b[l][u] = src[l][16 * g + 4 * u + q][c];
-  };
-  auto mfma_group = [&](const f4_t (&w)[NL][NT], const float (&b)[NL][4]) {
-#pragma unroll
-    for (int l = 0; l < NL; ++l)
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < NT; ++i) acc[l][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[l][i][u], b[l][u], acc[l][i], 0, 0, 0);
-  };
-  policy_load<NT, NL>(L, G, 0, tile0, tstride, lane, wa);
-  if (G > 1) policy_load<NT, NL>(L, G, 1, tile0, tstride, lane, wb);
-  read_b(0, ba);
-  for (int g = 0; g < G; g += 2) {
-    if (g + 1 < G) read_b(g + 1, bb);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_group(wa, ba);
-    if (g + 2 < G) {
-      policy_load<NT, NL>(L, G, g + 2, tile0, tstride, lane, wa);
-      read_b(g + 2, ba);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (g + 1 < G) {
-      mfma_group(wb, bb);
-      if (g + 3 < G) policy_load<NT, NL>(L, G, g + 3, tile0, tstride, lane, wb);
-    }
+  for (int g = 0; g < G; ++g) {
+    policy_group<NT, NL>(w[g % D], src, g, q, c, acc);
+    if (g + D < G) policy_load<NT, NL>(L, G, g + D, tile0, tstride, lane, w[g % D]);
   }
-#elif GO1_POLICY_PREFETCH == 4
-  // four weight buffers: loads run three groups ahead of the MFMAs
-  f4_t wc[NL][NT], wd[NL][NT];
-  policy_load<NT, NL>(L, G, 0, tile0, tstride, lane, wa);
-  if (G > 1) policy_load<NT, NL>(L, G, 1, tile0, tstride, lane, wb);
-  if (G > 2) policy_load<NT, NL>(L, G, 2, tile0, tstride, lane, wc);
-  for (int g = 0; g < G; g += 4) {
-    if (g + 3 < G) policy_load<NT, NL>(L, G, g + 3, tile0, tstride, lane, wd);
-    policy_group<NT, NL>(wa, src, g, q, c, acc);
-    if (g + 4 < G) policy_load<NT, NL>(L, G, g + 4, tile0, tstride, lane, wa);
-    if (g + 1 < G) policy_group<NT, NL>(wb, src, g + 1, q, c, acc);
-    if (g + 5 < G) policy_load<NT, NL>(L, G, g + 5, tile0, tstride, lane, wb);
-    if (g + 2 < G) policy_group<NT, NL>(wc, src, g + 2, q, c, acc);
-    if (g + 6 < G) policy_load<NT, NL>(L, G, g + 6, tile0, tstride, lane, wc);
-    if (g + 3 < G) policy_group<NT, NL>(wd, src, g + 3, q, c, acc);
-  }
-#else
-  policy_load<NT, NL>(L, G, 0, tile0, tstride, lane, wa);
-  if (G > 1) policy_load<NT, NL>(L, G, 1, tile0, tstride, lane, wb);
-  for (int g = 0; g < G; g += 2) {
-    policy_group<NT, NL>(wa, src, g, q, c, acc);
-    if (g + 2 < G) policy_load<NT, NL>(L, G, g + 2, tile0, tstride, lane, wa);
-    if (g + 1 < G) {
-      policy_group<NT, NL>(wb, src, g + 1, q, c, acc);
-      if (g + 3 < G) policy_load<NT, NL>(L, G, g + 3, tile0, tstride, lane, wb);
-    }
-  }
-#endif
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
-      const int t = tile0 + i * tstride;
+      f4_t v = acc[l][i];
+      if (act) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dst[l][16 * t + 4 * q + r][c] = act ? elu(acc[l][i][r]) : acc[l][i][r];
+        for (int r = 0; r < 4; ++r) v[r] = elu(v[r]);
+      }
+      act_store4(dst[l], 4 * (tile0 + i * tstride) + q, c, v);
     }
 }
 
-// Partial product of one output tile over K groups [g0, g0 + NG) (16 K values each), no
-// bias: the K-split form of the narrow layers, where a whole layer is one or a few tiles and
-// one wave walking all of K would run a serial MFMA chain behind one L2 round trip per group.
-// All NG weight fragments are loaded up front (one round trip).
+// Partial product of one output tile over K groups [g0, g0 + NG), no bias: the K-split form of
+// the narrow layers (one wave walking all of K would run a serial MFMA chain behind one L2
+// round trip per group).  All NG weight fragments are loaded up front (one round trip).
 template <int NG>
-__device__ __forceinline__ f4_t tile_partial(const PolicyLayer& L, int Gs, int tile, int g0, const float (*src)[16],
-                                             int lane) {
+__device__ __forceinline__ f4_t tile_partial(const PolicyLayer& L, int Gs, int tile, int g0, ActV src, int lane) {
   const int q = lane >> 4, c = lane & 15;
   f4_t w[NG];
 #pragma unroll
@@ -310,20 +292,9 @@ __device__ __forceinline__ f4_t tile_partial(const PolicyLayer& L, int Gs, int t
   f4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int i = 0; i < NG; ++i)
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[i][u], src[16 * (g0 + i) + 4 * u + q][c], acc, 0, 0, 0);
+    acc = mfma3(w[i], src.hi[(4 * (g0 + i) + q) * 16 + c], src.lo[(4 * (g0 + i) + q) * 16 + c], acc);
   return acc;
 }
-
-#ifndef GO1_POLICY_KSPLIT  // K-split narrow layers (needs 16 waves per workgroup)
-#define GO1_POLICY_KSPLIT 1
-#endif
-
-#ifndef GO1_POLICY_WAVES
-#define GO1_POLICY_WAVES 16
-#endif
-constexpr int PW = GO1_POLICY_WAVES;  // waves per workgroup (8: two per SIMD, 16: four per SIMD)
 
 #ifdef GO1_POLICY_STAMPS  // diagnostic build only (tools/policy_stamps.py): s_memtime per wave per phase
 #define PSTAMP_SLOTS 12
@@ -339,38 +310,37 @@ __device__ unsigned long long g_pstamps[512 * 16 * PSTAMP_SLOTS];
 #endif
 
 __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
-  __shared__ float xa[PIN][16], xc[PIN][16];  // actor / critic inputs (adaptation uses xa)
-  __shared__ float h1[2][512][16];             // layer-1 outputs (actor, critic); layer 3 reuses it
-  __shared__ float h2[2][256][16];
+  __shared__ Act<PIN> xa, xc;  // actor / critic inputs (the adaptation module reads xa)
+  __shared__ Act<512> h1[2];   // layer-1 outputs (actor, critic); layer 3 reuses them
+  __shared__ Act<256> h2[2];   // layer-2 outputs; also the f32 scratch of the K-split partials
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int e0 = blockIdx.x * 16;
   PSTAMP(0);
   const int ne = min(16, P.n_envs - e0);
+  const ActV va = xa.v(), vc = xc.v();
   for (int idx = tid; idx < 16 * PIN; idx += 64 * PW) {
     const int e = idx / PIN, k = idx - e * PIN;
     float v = 0.0f;
     if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
-    xa[k][e] = v;
-    xc[k][e] = (e < ne && k >= P.hist_dim && k < P.hist_dim + 2) ? P.privileged_obs[(size_t)(e0 + e) * 2 + (k - P.hist_dim)] : v;
+    act_store1(va, k, e, v);
+    act_store1(vc, k, e,
+               (e < ne && k >= P.hist_dim && k < P.hist_dim + 2) ? P.privileged_obs[(size_t)(e0 + e) * 2 + (k - P.hist_dim)]
+                                                                 : v);
   }
   __syncthreads();
   PSTAMP(1);
   const PolicyLayer* Ls = P.layers;
+  const ActV vh1[2] = {h1[0].v(), h1[1].v()}, vh2[2] = {h2[0].v(), h2[1].v()};
   // adaptation module (xa rows >= hist_dim are still zero)
-  {
-    const float(*s0[1])[16] = {xa};
-    float(*d0[1])[16] = {h1[0]};
-    policy_tiles<16 / PW, 1>(Ls + 0, PIN / 4, s0, wave, PW, d0, true, lane);  // 256
-  }
+  policy_tiles<1, 1, PIN / 16, 8>(Ls + 0, &va, wave, PW, &vh1[0], true, lane);  // 256
   __syncthreads();
   PSTAMP(2);
-#if GO1_POLICY_KSPLIT && GO1_POLICY_WAVES == 16
-  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7; the upper half's
-  // partial goes through LDS (h2[1], free until the actor/critic's second layer)
+  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7; the upper half's partial
+  // goes through LDS (h2[1], free until the actor/critic's second layer)
   {
-    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1][0][0]);
+    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1]);
     const int q = lane >> 4, c = lane & 15, t = wave & 7, half = wave >> 3;
-    f4_t acc = tile_partial<8>(Ls[1], 16, t, 8 * half, h1[0], lane);
+    f4_t acc = tile_partial<8>(Ls[1], 16, t, 8 * half, vh1[0], lane);
     if (half) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) scr[t][4 * q + r][c] = acc[r];
@@ -378,18 +348,20 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     __syncthreads();
     if (!half) {
       const f4_t b = *reinterpret_cast<const f4_t*>(Ls[1].b + 16 * t + 4 * q);
+      f4_t v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h2[0][16 * t + 4 * q + r][c] = elu((b[r] + acc[r]) + scr[t][4 * q + r][c]);
+      for (int r = 0; r < 4; ++r) v[r] = elu((b[r] + acc[r]) + scr[t][4 * q + r][c]);
+      act_store4(vh2[0], 4 * t + q, c, v);
     }
   }
   __syncthreads();
   PSTAMP(3);
   // 128 -> 2 (the latent): one K group per wave (8 waves), partials summed by wave 0
   {
-    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1][0][0]);
+    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1]);
     const int q = lane >> 4, c = lane & 15;
     if (wave < 8) {
-      const f4_t acc = tile_partial<1>(Ls[2], 8, 0, wave, h2[0], lane);
+      const f4_t acc = tile_partial<1>(Ls[2], 8, 0, wave, vh2[0], lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = acc[r];
     }
@@ -399,8 +371,8 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
 #pragma unroll
       for (int w = 0; w < 8; ++w) { l0 += scr[w][0][c]; l1 += scr[w][1][c]; }
       // features 0, 1: the latent, also the actor's inputs hist_dim, hist_dim + 1
-      xa[P.hist_dim][c] = l0;
-      xa[P.hist_dim + 1][c] = l1;
+      act_store1(va, P.hist_dim, c, l0);
+      act_store1(va, P.hist_dim + 1, c, l1);
       if (c < ne && P.latent) {
         P.latent[(size_t)(e0 + c) * 2] = l0;
         P.latent[(size_t)(e0 + c) * 2 + 1] = l1;
@@ -408,100 +380,48 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     }
   }
   __syncthreads();
-#else
-  {
-    const float(*s0[1])[16] = {h1[0]};
-    float(*d0[1])[16] = {h2[0]};
-    if (wave < 8) policy_tiles<1, 1>(Ls + 1, 256 / 4, s0, wave, 8, d0, true, lane);  // 128
-  }
-  __syncthreads();
-  PSTAMP(3);
-  if (wave == 0) {
-    const int q = lane >> 4, c = lane & 15;
-    f4_t acc = *reinterpret_cast<const f4_t*>(Ls[2].b + 4 * q);
-    const f4_t* W = reinterpret_cast<const f4_t*>(Ls[2].w);
-    for (int g = 0; g < 128 / 16; ++g) {
-      const f4_t w = W[g * 64 + lane];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u], h2[0][16 * g + 4 * u + q][c], acc, 0, 0, 0);
-    }
-    if (q == 0) {  // features 0, 1: the latent, also the actor's inputs hist_dim, hist_dim + 1
-      xa[P.hist_dim][c] = acc[0];
-      xa[P.hist_dim + 1][c] = acc[1];
-      if (c < ne && P.latent) {
-        P.latent[(size_t)(e0 + c) * 2] = acc[0];
-        P.latent[(size_t)(e0 + c) * 2 + 1] = acc[1];
-      }
-    }
-  }
-  __syncthreads();
-#endif
   PSTAMP(4);
-  // actor and critic, layer by layer; wave w takes tiles w, w + 4, ... of both nets
-  const PolicyLayer LA1[2] = {Ls[3], Ls[7]}, LA2[2] = {Ls[4], Ls[8]}, LA3[2] = {Ls[5], Ls[9]};
+  // actor and critic, layer by layer; wave w takes tiles w, w + 16, ... of both nets
+  const PolicyLayer LA1[2] = {Ls[3], Ls[7]}, LA2[2] = {Ls[4], Ls[8]};
   {
-    const float(*s1[2])[16] = {xa, xc};
-    float(*d1[2])[16] = {h1[0], h1[1]};
-    policy_tiles<32 / PW, 2>(LA1, PIN / 4, s1, wave, PW, d1, true, lane);  // 512
+    const ActV s1[2] = {va, vc};
+    policy_tiles<2, 2, PIN / 16, 3>(LA1, s1, wave, PW, vh1, true, lane);  // 512
   }
   __syncthreads();
   PSTAMP(5);
-  {
-    const float(*s2[2])[16] = {h1[0], h1[1]};
-    float(*d2[2])[16] = {h2[0], h2[1]};
-    policy_tiles<16 / PW, 2>(LA2, 512 / 4, s2, wave, PW, d2, true, lane);  // 256
-  }
+  policy_tiles<1, 2, 512 / 16, 6>(LA2, vh1, wave, PW, vh2, true, lane);  // 256
   __syncthreads();
   PSTAMP(6);
-  {
-    const float(*s3[2])[16] = {h2[0], h2[1]};
-    float(*d3[2])[16] = {h1[0], h1[1]};
-    if (PW == 8) {
-      policy_tiles<1, 2>(LA3, 256 / 4, s3, wave, 8, d3, true, lane);  // 128
-    } else {  // one tile per wave: waves 0-7 the actor's, 8-15 the critic's
-      const int l = wave >> 3;
-      const float(*s1[1])[16] = {l ? h2[1] : h2[0]};
-      float(*d1[1])[16] = {l ? h1[1] : h1[0]};
-      const PolicyLayer L3 = l ? Ls[9] : Ls[5];
-      policy_tiles<1, 1>(&L3, 256 / 4, s1, wave & 7, 8, d1, true, lane);
-    }
+  {  // 256 -> 128, one tile per wave: waves 0-7 the actor's, 8-15 the critic's
+    const bool critic = wave >= 8;
+    const PolicyLayer L3 = critic ? Ls[9] : Ls[5];
+    const ActV src = critic ? h2[1].v() : h2[0].v(), dst = critic ? h1[1].v() : h1[0].v();
+    policy_tiles<1, 1, 256 / 16, 8>(&L3, &src, wave & 7, 8, &dst, true, lane);
   }
   __syncthreads();
   PSTAMP(7);
-#if GO1_POLICY_KSPLIT && GO1_POLICY_WAVES == 16
   // 128 -> num_actions (actor, waves 0-7) and 128 -> 1 (critic, waves 8-15): one K group per
   // wave, partials through LDS (h2, free once the third layer has read it)
   {
-    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0][0][0]);
-    const int q = lane >> 4, c = lane & 15, net = wave >> 3;
-    const f4_t part = tile_partial<1>(Ls[net ? 10 : 6], 8, 0, wave & 7, h1[net], lane);
+    float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0]);
+    const int q = lane >> 4, c = lane & 15;
+    const bool critic = wave >= 8;
+    const f4_t part = tile_partial<1>(Ls[critic ? 10 : 6], 8, 0, wave & 7, critic ? h1[1].v() : h1[0].v(), lane);
 #pragma unroll
     for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = part[r];
   }
   __syncthreads();
-#endif
   if (wave < 2) {
     const int q = lane >> 4, c = lane & 15;
     const PolicyLayer L = Ls[wave == 0 ? 6 : 10];
     f4_t acc = *reinterpret_cast<const f4_t*>(L.b + 4 * q);
-#if GO1_POLICY_KSPLIT && GO1_POLICY_WAVES == 16
     {
-      float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0][0][0]);
+      float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0]);
 #pragma unroll
       for (int w = 0; w < 8; ++w)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] += scr[8 * wave + w][4 * q + r][c];
     }
-#else
-    const f4_t* W = reinterpret_cast<const f4_t*>(L.w);
-    for (int g = 0; g < 128 / 16; ++g) {
-      const f4_t w = W[g * 64 + lane];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u], h1[wave][16 * g + 4 * u + q][c], acc, 0, 0, 0);
-    }
-#endif
     if (wave == 0 && P.actions) {
       // Normal(mean, std).sample() and its log_prob summed over the actions
       // (actor_critic.py:137-145), Box-Muller on Philox4x32-10 uniforms keyed by

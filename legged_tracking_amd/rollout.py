@@ -103,19 +103,25 @@ class _PolicyArgs(C.Structure):
 
 
 def _pack_linear(lin):
-    """nn.Linear -> (weights in MFMA A-fragment order, bias padded to 16).
+    """nn.Linear -> (weights split and packed for csrc/rollout.hip's 3xF16 MFMA, bias padded to 16).
 
-    Packed [n/16][k/16][lane = 16 q + m][u] = W[16 t + m][16 g + 4 u + q]: lane (m, q)
-    of output tile t reads one float4 per group g of four K-steps (k = 16 g + 4 u + q)."""
-    W, b = lin.weight.detach(), lin.bias.detach()
+    Every weight w is split into hi = f16(w) and lo = f16(w - hi).  Packed as 16-byte records
+    [n/16][k/16][lane = 16 q + m][hi r = 0..3, lo r = 0..3] of W[16 t + m][16 g + 4 q + r]: lane
+    (m, q) of output tile t reads one record per 16-deep K group g -- its A fragments of
+    v_mfma_f32_16x16x16_f16 (rows m, k = 4 q .. 4 q + 3) for both halves of the split."""
+    W, b = lin.weight.detach().float(), lin.bias.detach().float()
     n, k = W.shape
     npad, kpad = -(-n // 16) * 16, -(-k // 16) * 16
     Wp = torch.zeros(npad, kpad, device=W.device, dtype=torch.float32)
     Wp[:n, :k] = W
     bp = torch.zeros(npad, device=W.device, dtype=torch.float32)
     bp[:n] = b
-    # [t, m, g, u, q] -> [t, g, q, m, u]
-    return Wp.view(npad // 16, 16, kpad // 16, 4, 4).permute(0, 2, 4, 1, 3).contiguous(), bp
+    hi = Wp.to(torch.float16)
+    lo = (Wp - hi.float()).to(torch.float16)
+    # [t, m, g, q, r] -> [t, g, q, m, r], then hi and lo side by side in the last dimension
+    def frag(x):
+        return x.view(npad // 16, 16, kpad // 16, 4, 4).permute(0, 2, 3, 1, 4)
+    return torch.cat([frag(hi), frag(lo)], dim=-1).contiguous(), bp
 
 
 class FusedPolicy:
