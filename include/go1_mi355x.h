@@ -14,6 +14,8 @@
  *                         (+ gym.set_*_tensor_indexed :1011-1013, :1050-1052)
  *   go1_set_terrain() <- Terrain env_height_samples / env_terrain_origin
  *                         (_get_env_origins :1808-1847)
+ *   go1_tunnel_tiles() <- Terrain(cfg) tile generation (go1_gym/utils/tunnel.py:51-217,
+ *                         tunnel_fn.py:99-163), seeded numpy stream reproduced on the device
  *
  * All device pointers are owned by the caller (PyTorch tensors); the library
  * never allocates or frees them.  Every call is asynchronous on the caller's
@@ -283,6 +285,27 @@ const char* go1_last_error(void);
 int go1_create(const go1_config* cfg, go1_handle** out);
 int go1_bind(go1_handle* h, const go1_state* state);
 int go1_set_terrain(go1_handle* h, const go1_terrain* terrain);
+
+/* Tunnel terrain generator on the device (no handle needed): the single_path tiles of a
+ * num_rows x num_cols grid, bit-identical to the reference's Terrain(cfg) built after
+ * np.random.seed(seed) (go1_gym/utils/tunnel.py:51-126, 189-217 with
+ * TerrainFunctions.single_path, go1_gym/utils/tunnel_fn.py:99-163 and vec_plane_from_points :3-21).
+ * Replaces the host numpy loop the reference runs once at env creation.
+ *   extents: device int32 (n_sub, 4) = start_x, end_x, start_y, end_y of each sub-terrain's tunnel
+ *            inside its tile (add_terrain_to_map :193-196), n_sub = num_rows * num_cols, row-major;
+ *   records: device scratch, n_sub * GO1_TUNNEL_REC doubles (the drawn wedge parameters);
+ *   tiles:   device output (n_sub, 2, tile_x, tile_y) f32, layer 0 ceiling, 1 floor (go1_terrain.tiles). */
+#define GO1_TUNNEL_REC 40
+typedef struct go1_tunnel_params {
+  int32_t num_rows, num_cols;   /* Cfg.terrain.num_rows / num_cols */
+  int32_t tile_x, tile_y;       /* int(terrain_length / hs), int(terrain_width / hs) */
+  int32_t sub_x, sub_y;         /* SubTerrain shape: int(tile_y * terrain_ratio_y), int(tile_x * terrain_ratio_x) */
+  uint32_t seed;                /* np.random.RandomState(seed) / np.random.seed(seed), 0 <= seed < 2^32 */
+  int32_t pad;
+  double horizontal_scale, vertical_scale, ceiling_height, p_flat, p_double;
+} go1_tunnel_params;
+int go1_tunnel_tiles(const go1_tunnel_params* p, const int32_t* extents, double* records, float* tiles,
+                     void* stream);
 int go1_step(go1_handle* h, const go1_step_args* args, void* stream);
 /* Kernel variant.  go1_create selects a step kernel specialised for the README configuration
  * (scripts/train.py's README command: the integer flags of legged_tracking_amd/csrc/go1_spec.h

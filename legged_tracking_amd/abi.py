@@ -90,6 +90,16 @@ class Go1Terrain(C.Structure):
                 ("n_tiles", I32), ("pad", I32)]
 
 
+GO1_TUNNEL_REC = 40
+
+
+class Go1TunnelParams(C.Structure):
+    _fields_ = [("num_rows", I32), ("num_cols", I32), ("tile_x", I32), ("tile_y", I32), ("sub_x", I32),
+                ("sub_y", I32), ("seed", C.c_uint32), ("pad", I32), ("horizontal_scale", C.c_double),
+                ("vertical_scale", C.c_double), ("ceiling_height", C.c_double), ("p_flat", C.c_double),
+                ("p_double", C.c_double)]
+
+
 class Go1StepArgs(C.Structure):
     _fields_ = [
         ("actions", P), ("gravity_vec", F * 3), ("sim_gravity", F * 3), ("reward_scales", F * GO1_MAX_TERMS),

@@ -15,19 +15,19 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp
 # code adds register-pair moves that cost more than they save (measured -3 %).
 STEP_FLAGS = ["-fno-slp-vectorize"]
 
-# name -> (source, extra dependencies, extra flags)
+# name -> (sources, extra dependencies, extra flags)
 LIBS = {
-    "libgo1_mi355x.so": ("go1_step.hip", ["pmath.h", "go1_model_consts.h", "go1_spec.h", os.path.join(INC, "go1_mi355x.h")],
-                         STEP_FLAGS),
-    "libgo1_rollout.so": ("rollout.hip", [os.path.join(INC, "go1_rollout.h")], []),
+    "libgo1_mi355x.so": (["go1_step.hip", "go1_terrain.hip"],
+                         ["pmath.h", "go1_model_consts.h", "go1_spec.h", os.path.join(INC, "go1_mi355x.h")], STEP_FLAGS),
+    "libgo1_rollout.so": (["rollout.hip"], [os.path.join(INC, "go1_rollout.h")], []),
 }
 OUT = os.path.join(BUILD, "libgo1_mi355x.so")  # the step library (kept for callers of build())
 
 
 def _paths(name):
-    src, deps, _ = LIBS[name]
-    src = os.path.join(HERE, "csrc", src)
-    return src, [src] + [d if os.path.isabs(d) else os.path.join(HERE, "csrc", d) for d in deps]
+    srcs, deps, _ = LIBS[name]
+    srcs = [os.path.join(HERE, "csrc", s) for s in srcs]
+    return srcs, srcs + [d if os.path.isabs(d) else os.path.join(HERE, "csrc", d) for d in deps]
 
 
 def needs_build(name):
@@ -42,8 +42,8 @@ def build(force=False, verbose=False, names=None):
     for name in names or LIBS:
         if not force and not needs_build(name):
             continue
-        src, _ = _paths(name)
-        cmd = [HIPCC, *FLAGS, *LIBS[name][2], "-o", os.path.join(BUILD, name), src]
+        srcs, _ = _paths(name)
+        cmd = [HIPCC, *FLAGS, *LIBS[name][2], "-o", os.path.join(BUILD, name), *srcs]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -2516,6 +2516,8 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+// the library's other translation units (go1_terrain.hip) report through the same message
+int go1_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
 
 #define HIP_TRY(x)                                                                      \
   do {                                                                                  \

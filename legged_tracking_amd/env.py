@@ -301,14 +301,18 @@ class LeggedRobot:
         self._abi_cfg.env_id_offset = rank * n
         # terrain: the global grid is built identically on every rank (same seed), each
         # rank binds the slice of global env ids it owns (_get_env_origins :1808-1847)
-        td = T.build(cfg, n_global, np.random.RandomState(self.seed))
-        sl = slice(rank * n, (rank + 1) * n)
-        self.terrain = td
+        # the tunnel tiles come from the GPU generator (go1_tunnel_tiles) with the native backend,
+        # bit-identical to the host restatement T.make_single_path that injected test backends use
+        tiles_fn = None
         if backend is None:  # the HIP library (no CPU fallback); tests inject a factory
             from . import native
             backend = lambda c: native.Go1Native(c, sim_device)  # noqa: E731
+            tiles_fn = lambda t, lay: native.tunnel_tiles(t, lay, self.seed, self._sim.device)  # noqa: E731
         self._sim = backend(self._abi_cfg)
         self.device = self._sim.device
+        td = T.build(cfg, n_global, np.random.RandomState(self.seed), tiles_fn=tiles_fn)
+        sl = slice(rank * n, (rank + 1) * n)
+        self.terrain = td
         self._sim.set_terrain(td.tiles, td.env_tile[sl], td.env_terrain_origin[sl], td.env_origins[sl])
         self.env_origins = torch.as_tensor(td.env_origins[sl], device=self.device)
         dev = self.device

@@ -42,6 +42,7 @@ def lib():
     l.go1_destroy.argtypes = [C.c_void_p]
     l.go1_specialize.argtypes = [C.c_void_p, C.c_int]
     l.go1_is_specialized.argtypes = [C.c_void_p]
+    l.go1_tunnel_tiles.argtypes = [C.POINTER(abi.Go1TunnelParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     if l.go1_abi_version() != abi.GO1_ABI_VERSION:
         raise NativeError("ABI version mismatch")
     _lib = l
@@ -55,6 +56,28 @@ def _check(rc):
 
 def _stream():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def tunnel_tiles(cfg_terrain, layout, seed, device):
+    """single_path tiles generated on the GPU (go1_tunnel_tiles): the tiles the reference's
+    Terrain(cfg) builds after np.random.seed(seed), as a (rows, cols, 2, tile_x, tile_y) f32
+    tensor on `device` (tunnel.py:51-217, tunnel_fn.py:99-163)."""
+    t = cfg_terrain
+    rows, cols = int(t.num_rows), int(t.num_cols)
+    if not 0 <= int(seed) < 2 ** 32:
+        raise ValueError("seed must be in [0, 2**32) (numpy RandomState)")
+    p = abi.Go1TunnelParams(num_rows=rows, num_cols=cols, tile_x=layout.tile_x, tile_y=layout.tile_y,
+                            sub_x=layout.sub_shape[0], sub_y=layout.sub_shape[1], seed=int(seed),
+                            horizontal_scale=float(t.horizontal_scale), vertical_scale=float(t.vertical_scale),
+                            ceiling_height=float(t.ceiling_height), p_flat=float(t.p_flat),
+                            p_double=float(t.p_double))
+    ext = torch.as_tensor(np.ascontiguousarray(layout.extents, np.int32)).to(device)
+    rec = torch.empty((rows * cols, abi.GO1_TUNNEL_REC), dtype=torch.float64, device=device)
+    tiles = torch.empty((rows, cols, 2, layout.tile_x, layout.tile_y), dtype=torch.float32, device=device)
+    with torch.cuda.device(device):
+        _check(lib().go1_tunnel_tiles(C.byref(p), ext.data_ptr(), rec.data_ptr(), tiles.data_ptr(), _stream()))
+    torch.cuda.current_stream(device).synchronize()  # ext / rec are freed on return
+    return tiles
 
 
 class StateTensors:
@@ -111,7 +134,11 @@ class Go1Native:
 
     def set_terrain(self, tiles, env_tile, env_terrain_origin, env_origins):
         d = self.device
-        t = [torch.as_tensor(np.ascontiguousarray(tiles, np.float32)).to(d),
+        if isinstance(tiles, torch.Tensor):  # device-generated tiles (tunnel_tiles)
+            tiles = tiles.to(d, torch.float32).contiguous()
+        else:
+            tiles = torch.as_tensor(np.ascontiguousarray(tiles, np.float32)).to(d)
+        t = [tiles,
              torch.as_tensor(np.ascontiguousarray(env_tile, np.int32)).to(d),
              torch.as_tensor(np.ascontiguousarray(env_terrain_origin, np.float32)).to(d),
              torch.as_tensor(np.ascontiguousarray(env_origins, np.float32)).to(d)]

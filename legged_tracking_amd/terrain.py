@@ -84,44 +84,73 @@ def single_path_layer(shape, hs, vs, p_flat, p_double, top, rng=np.random):
     return (h / vs).astype(int)
 
 
-def make_single_path(cfg_terrain, rng=np.random):
-    """Tiles for a num_rows x num_cols tunnel grid (tunnel.py:51-126, 189-217)."""
+@dataclass
+class TunnelLayout:
+    """The RNG-free part of the tunnel grid (tunnel.py:59-77, 189-217)."""
+    tile_x: int                 # length_per_env_pixels
+    tile_y: int                 # width_per_env_pixels
+    sub_shape: tuple            # SubTerrain height_field_raw shape (pixel_x, pixel_y)
+    extents: np.ndarray         # (rows * cols, 4) int32: start_x, end_x, start_y, end_y inside the tile
+    env_origins: np.ndarray     # (rows, cols, 3)
+    all_origins: np.ndarray     # (rows, cols, 3)
+
+
+def tunnel_layout(cfg_terrain):
     t = cfg_terrain
-    hs, vs = t.horizontal_scale, t.vertical_scale
+    hs = t.horizontal_scale
     W = int(t.terrain_width / hs)
     Lp = int(t.terrain_length / hs)
     rows, cols = t.num_rows, t.num_cols
+    ext = np.zeros((rows * cols, 4), np.int32)
+    env_origins = np.zeros((rows, cols, 3))
+    all_origins = np.zeros((rows, cols, 3))
+    for k in range(rows * cols):
+        i, j = np.unravel_index(k, (rows, cols))
+        # add_terrain_to_map (:193-196), relative to the tile
+        ext[k] = (int(round((i + 0.5 - t.terrain_ratio_x / 2.) * Lp, 4)) - i * Lp,
+                  int(round((i + 0.5 + t.terrain_ratio_x / 2.) * Lp, 4)) - i * Lp,
+                  int((j + 0.5 - t.terrain_ratio_y / 2.) * W) - j * W,
+                  int((j + 0.5 + t.terrain_ratio_y / 2.) * W) - j * W)
+        env_origins[i, j] = [(i + 0.5 - t.start_loc) * t.terrain_length, (j + 0.5) * t.terrain_width, 0.0]
+        all_origins[i, j] = [i * t.terrain_length, j * t.terrain_width, 0.0]
+    return TunnelLayout(Lp, W, (int(W * t.terrain_ratio_y), int(Lp * t.terrain_ratio_x)), ext, env_origins, all_origins)
+
+
+def make_single_path(cfg_terrain, rng=np.random):
+    """Tiles for a num_rows x num_cols tunnel grid (tunnel.py:51-126, 189-217), host numpy.
+
+    The product env generates the same tiles on the GPU (go1_tunnel_tiles, native.tunnel_tiles);
+    this host restatement is the checker the device generator is compared with bit for bit."""
+    t = cfg_terrain
+    hs, vs = t.horizontal_scale, t.vertical_scale
+    lay = tunnel_layout(t)
+    Lp, W = lay.tile_x, lay.tile_y
+    rows, cols = t.num_rows, t.num_cols
     unit = int(1. / vs)
     tiles = np.empty((rows, cols, 2, Lp, W), np.float64)
-    sub_shape = (int(W * t.terrain_ratio_y), int(Lp * t.terrain_ratio_x))
-    terrain_origins = np.zeros((rows, cols, 3))
-    all_origins = np.zeros((rows, cols, 3))
-    env_origins = np.zeros((rows, cols, 3))
     for k in range(rows * cols):
         i, j = np.unravel_index(k, (rows, cols))
         rng.uniform(0.0, 1.0)  # difficulty: drawn, unused by single_path (tunnel.py:90)
-        top = single_path_layer(sub_shape, hs, vs, t.p_flat, t.p_double, True, rng)
-        bottom = single_path_layer(sub_shape, hs, vs, t.p_flat, t.p_double, False, rng)
+        top = single_path_layer(lay.sub_shape, hs, vs, t.p_flat, t.p_double, True, rng)
+        bottom = single_path_layer(lay.sub_shape, hs, vs, t.p_flat, t.p_double, False, rng)
         top = t.ceiling_height / vs - top
         top = np.clip(top, a_max=None, a_min=0.05 / vs)
-        sx = int(round((i + 0.5 - t.terrain_ratio_x / 2.) * Lp, 4)) - i * Lp
-        ex = int(round((i + 0.5 + t.terrain_ratio_x / 2.) * Lp, 4)) - i * Lp
-        sy = int((j + 0.5 - t.terrain_ratio_y / 2.) * W) - j * W
-        ey = int((j + 0.5 + t.terrain_ratio_y / 2.) * W) - j * W
+        sx, ex, sy, ey = (int(v) for v in lay.extents[k])
         tile = np.empty((2, Lp, W), np.float64)
         tile[0] = unit * t.ceiling_height
         tile[1] = 0.5 * unit
         tile[0, sx:ex, sy:ey] = top.T
         tile[1, sx:ex, sy:ey] = bottom.T
         tiles[i, j] = tile
-        terrain_origins[i, j] = [(i * Lp + sx) * hs, (j * W + sy) * hs, 0]
-        env_origins[i, j] = [(i + 0.5 - t.start_loc) * t.terrain_length, (j + 0.5) * t.terrain_width, 0.0]
-        all_origins[i, j] = [i * t.terrain_length, j * t.terrain_width, 0.0]
-    return (tiles * vs).astype(np.float32), env_origins, all_origins
+    return (tiles * vs).astype(np.float32), lay.env_origins, lay.all_origins
 
 
-def build(cfg, n_envs, rng=np.random):
-    """TerrainData for the envs (legged_robot_trajectory_tracking.py:1808-1858)."""
+def build(cfg, n_envs, rng=np.random, tiles_fn=None):
+    """TerrainData for the envs (legged_robot_trajectory_tracking.py:1808-1858).
+
+    tiles_fn(cfg.terrain, layout) -> tiles replaces the host tile generation (the env passes the
+    device generator, native.tunnel_tiles, seeded like `rng`); env origins and tile indices are
+    RNG-free and always built here."""
     t = cfg.terrain
     if t.mesh_type == "plane":
         # grid of robots (:1849-1858)
@@ -136,7 +165,11 @@ def build(cfg, n_envs, rng=np.random):
     if t.terrain_type != "single_path":
         raise ValueError(f"terrain_type {t.terrain_type!r}: only single_path is on this path "
                          "(multi_path is not implemented in the reference either, README.md:9)")
-    tiles, env_origins, all_origins = make_single_path(t, rng)
+    if tiles_fn is None:
+        tiles, env_origins, all_origins = make_single_path(t, rng)
+    else:
+        lay = tunnel_layout(t)
+        tiles, env_origins, all_origins = tiles_fn(t, lay), lay.env_origins, lay.all_origins
     rows, cols = t.num_rows, t.num_cols
     S = rows * cols
     assert n_envs % S == 0, (n_envs, rows, cols)

@@ -1,6 +1,6 @@
 """Static instruction counts between MARK() section markers of the step kernel.
 
-  python tools/isa_sections.py   (compiles go1_step.hip with -DGO1_ISA_MARKS into /tmp)
+  python tools/isa_sections.py   (compiles go1_step.hip with -DGO1_ISA_MARKS into /tmp; counts the specialised product kernel)
 
 Straight-line sections inside the sub-step loop run decimation x n_internal
 times per step, so static counts x trip counts ~ the dynamic SQ_INSTS_VALU."""
@@ -23,7 +23,7 @@ def main():
                     "-DGO1_ISA_MARKS", *extra, "-c", "--save-temps", "-o", os.path.join(OUT, "k.o"), src],
                    cwd=OUT, check=True)
     s = open(os.path.join(OUT, "go1_step-hip-amdgcn-amd-amdhsa-gfx950.s")).read().splitlines()
-    start = next(i for i, l in enumerate(s) if l.startswith("_Z15go1_step_kernelILb0ELi7EE"))
+    start = next(i for i, l in enumerate(s) if l.startswith("_Z15go1_step_kernelILb0ELi7ELb1EE"))
     end = next(i for i in range(start, len(s)) if s[i].startswith(".Lfunc_end"))
     cur, counts = "prologue", {}
     for l in s[start:end]:
