@@ -542,6 +542,31 @@ __device__ __forceinline__ void rigid_bias(const float* body, float mscale, cons
   cross3(w, p, o + 3);
 }
 
+// rigid_bias on a velocity given as (angular, linear) pairs, the result as pairs: the two
+// products with w, w x L and w x p, run as one packed cross product of w with the (L, p) pairs
+__device__ __forceinline__ void rigid_bias2(const float* body, const f2* vel, f2* o) {
+  const float m = body[0];
+  const float* c = body + 1;
+  const float w[3] = {vel[0].x, vel[1].x, vel[2].x}, v[3] = {vel[0].y, vel[1].y, vel[2].y};
+  float wc[3], p[3], L[3], cp[3], b[3];
+  cross3(w, c, wc);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p[i] = m * (v[i] + wc[i]);
+  const float ixx = body[4], ixy = body[5], ixz = body[6], iyy = body[7], iyz = body[8], izz = body[9];
+  cross3(c, p, cp);
+  L[0] = ixx * w[0] + ixy * w[1] + ixz * w[2] + cp[0];
+  L[1] = ixy * w[0] + iyy * w[1] + iyz * w[2] + cp[1];
+  L[2] = ixz * w[0] + iyz * w[1] + izz * w[2] + cp[2];
+  const f2 X[3] = {f2{L[0], p[0]}, f2{L[1], p[1]}, f2{L[2], p[2]}};
+  cross3(v, p, b);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+    const f2 wx = w[i1] * X[i2] - w[i2] * X[i1];
+    o[i] = f2{wx.x + b[i], wx.y};
+  }
+}
+
 // force cross product v x* f
 __device__ __forceinline__ void crf(const float* v, const float* f, float* o) {
   float a[3], b[3], c[3];
@@ -729,6 +754,197 @@ __device__ __forceinline__ void solve6(const SI& M, const float* b, float* x) {
 #pragma unroll
     for (int j = 0; j <= i; ++j) {
       float s = si_get(M, i, j);
+#pragma unroll
+      for (int k = 0; k < j; ++k) s -= LI(i, k) * LI(j, k);
+      if (i == j) LI(i, i) = frsq(fmaxf(s, 1e-30f));  // holds 1 / L_ii
+      else LI(i, j) = s * LI(j, j);
+    }
+  float y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= LI(i, k) * y[k];
+    y[i] = s * LI(i, i);
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s -= LI(k, i) * x[k];
+    x[i] = s * LI(i, i);
+  }
+#undef LI
+}
+
+// ---- packed articulated-body algebra.  One wave alone issues a v_pk_fma_f32 (two FMAs) as
+// fast as a v_fma_f32 (tools/probes/pk_rate.hip), and a spatial quantity pairs up by itself:
+// a spatial vector is three (angular_i, linear_i) pairs, and a spatial inertia keeps its two
+// symmetric 3 x 3 blocks as six (A_t, C_t) pairs -- every rotation, rank-1 update and sum of the
+// articulated-body passes treats the two halves alike.  B (general 3 x 3) stays scalar.
+#ifndef GO1_PACKED_ABA
+#define GO1_PACKED_ABA 1
+#endif
+struct SIP {
+  f2 ac[6];
+  float b[9];
+};
+__host__ __device__ __forceinline__ constexpr int s3i(int i, int j) {
+  return i == 0 ? j : (i == 1 ? (j == 0 ? 1 : j + 2) : (j == 0 ? 2 : (j == 1 ? 4 : 5)));
+}
+
+__device__ __forceinline__ void rigid_sip(const float* body, float mscale, SIP& I) {
+  SI s;
+  rigid_si(body, mscale, s);
+#pragma unroll
+  for (int t = 0; t < 6; ++t) I.ac[t] = f2{s.a[t], s.c[t]};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) I.b[i] = s.b[i];
+}
+
+__device__ __forceinline__ void sip_add(SIP& A, const SIP& B) {
+#pragma unroll
+  for (int t = 0; t < 6; ++t) A.ac[t] += B.ac[t];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) A.b[i] += B.b[i];
+}
+
+// column ax of the 6 x 6 matrix as pairs: (A(i, ax), B^T(i, ax) = B(ax, i))
+__device__ __forceinline__ f2 sip_col(const SIP& M, int ax, int i) { return f2{M.ac[s3i(i, ax)].x, M.b[ax * 3 + i]}; }
+
+// y = M v for a v whose pair ax is zero (c_j of a joint about axis ax); v, y as pairs
+__device__ __forceinline__ void sip_mul_sparse(const SIP& M, const f2* v, int ax, f2* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    f2 st = f2{0.0f, 0.0f};
+    bool first = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      st = first ? M.ac[s3i(i, j)] * v[j] : st + M.ac[s3i(i, j)] * v[j];
+      first = false;
+    }
+    float s = st.x, t = st.y;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      s = s + M.b[i * 3 + j] * v[j].y;
+      t = t + M.b[j * 3 + i] * v[j].x;
+    }
+    o[i] = f2{s, t};
+  }
+}
+
+// E v (rE) and E^T v (rET) on pairs: both halves rotate by the same joint rotation
+__device__ __forceinline__ void rE2(int ax, float c, float s, const f2* v, f2* o) {
+  if (ax == 0) {
+    const f2 y = c * v[1] + s * v[2], z = c * v[2] - s * v[1];
+    o[0] = v[0]; o[1] = y; o[2] = z;
+  } else {
+    const f2 x = c * v[0] - s * v[2], z = s * v[0] + c * v[2];
+    o[0] = x; o[1] = v[1]; o[2] = z;
+  }
+}
+__device__ __forceinline__ void rET2(int ax, float c, float s, const f2* v, f2* o) {
+  if (ax == 0) {
+    const f2 y = c * v[1] - s * v[2], z = s * v[1] + c * v[2];
+    o[0] = v[0]; o[1] = y; o[2] = z;
+  } else {
+    const f2 x = c * v[0] + s * v[2], z = c * v[2] - s * v[0];
+    o[0] = x; o[1] = v[1]; o[2] = z;
+  }
+}
+
+// motion transform parent -> child on pairs: (w, v) -> (E w, E (v - r x w)), r with mask M
+__device__ __forceinline__ void xm2(int ax, float c, float s, int M, const float* r, const f2* vin, f2* vout) {
+  const int cm = cross_mask(M, 7);
+  const float w[3] = {vin[0].x, vin[1].x, vin[2].x};
+  f2 t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = f2{w[i], ((cm >> i) & 1) ? vin[i].y - cross_c(M, 7, i, r, w) : vin[i].y};
+  rE2(ax, c, s, t, vout);
+}
+
+// force transform child -> parent on pairs: (n, f) -> (E^T n + r x E^T f, E^T f), r with mask M
+__device__ __forceinline__ void xfT2(int ax, float c, float s, int M, const float* r, const f2* fin, f2* fout) {
+  const int cm = cross_mask(M, 7);
+  f2 nf[3];
+  rET2(ax, c, s, fin, nf);
+  const float f[3] = {nf[0].y, nf[1].y, nf[2].y};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) fout[i] = f2{((cm >> i) & 1) ? nf[i].x + cross_c(M, 7, i, r, f) : nf[i].x, f[i]};
+}
+
+// X^T Ia X (xform_inertia) with the A and C blocks rotated together as pairs
+__device__ __forceinline__ void xform_inertia2(int ax, float cq, float sq, int M, const float* r, const SIP& In,
+                                               SIP& Out) {
+  const float sp = ax == 0 ? sq : -sq;
+  const float c2 = cq * cq - sp * sp, s2 = 2.0f * cq * sp;
+  // rot_congruence_sym on (A, C) pairs
+  const int f = ax, pI = ax == 0 ? 1 : 0, rI = 2;
+  const f2 mff = In.ac[s3i(f, f)], mfp = In.ac[s3i(f, pI)], mfr = In.ac[s3i(f, rI)];
+  const f2 mpp = In.ac[s3i(pI, pI)], mrr = In.ac[s3i(rI, rI)], mpr = In.ac[s3i(pI, rI)];
+  const f2 h = 0.5f * (mpp + mrr), d = 0.5f * (mpp - mrr);
+  const f2 qfp = cq * mfp - sp * mfr, qfr = sp * mfp + cq * mfr;
+  const f2 qpp = h + d * c2 - mpr * s2, qrr = h - d * c2 + mpr * s2, qpr = d * s2 + mpr * c2;
+  f2 Q[9];
+  Q[f * 3 + f] = mff;
+  Q[f * 3 + pI] = qfp; Q[pI * 3 + f] = qfp;
+  Q[f * 3 + rI] = qfr; Q[rI * 3 + f] = qfr;
+  Q[pI * 3 + pI] = qpp; Q[rI * 3 + rI] = qrr;
+  Q[pI * 3 + rI] = qpr; Q[rI * 3 + pI] = qpr;
+  float B[9], C[9];
+  rot_congruence(ax, cq, sq, In.b, B);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) C[i] = Q[i].y;
+  // translation by r (xform_inertia): A'' = A' - BR^T - BR - RCR, B'' = B' + RC, C'' = C'
+  const int mc = cross_mask(M, 7), mb = cross_mask(7, M);
+  float RC[9], BR[9], RCR[9];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float col[3] = {C[j], C[3 + j], C[6 + j]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) RC[3 * i + j] = ((mc >> i) & 1) ? cross_c(M, 7, i, r, col) : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      BR[3 * i + j] = ((mb >> j) & 1) ? cross_c(7, M, j, B + 3 * i, r) : 0.0f;
+      RCR[3 * i + j] = ((mc >> i) & (mb >> j) & 1) ? cross_c(7, M, j, RC + 3 * i, r) : 0.0f;
+    }
+  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int i = II[t], j = JJ[t];
+    float v = Q[i * 3 + j].x;
+    if ((mb >> i) & 1) v -= BR[j * 3 + i];
+    if ((mb >> j) & 1) v -= BR[i * 3 + j];
+    if ((mc >> i) & (mb >> j) & 1) v -= RCR[i * 3 + j];
+    Out.ac[t] = f2{v, C[i * 3 + j]};
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Out.b[3 * i + j] = ((mc >> i) & 1) ? B[3 * i + j] + RC[3 * i + j] : B[3 * i + j];
+}
+
+__device__ __forceinline__ float sip_get(const SIP& M, int i, int j) {
+  if (i < 3 && j < 3) return M.ac[s3i(i, j)].x;
+  if (i >= 3 && j >= 3) return M.ac[s3i(i - 3, j - 3)].y;
+  if (i < 3) return M.b[i * 3 + (j - 3)];
+  return M.b[j * 3 + (i - 3)];
+}
+
+// 6x6 SPD solve (Cholesky) of the packed inertia, identical instruction stream in every lane
+__device__ __forceinline__ void solve6p(const SIP& M, const float* b, float* x) {
+  float L[21];
+#define LI(i, j) L[(i) * ((i) + 1) / 2 + (j)]
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      float s = sip_get(M, i, j);
 #pragma unroll
       for (int k = 0; k < j; ++k) s -= LI(i, k) * LI(j, k);
       if (i == j) LI(i, i) = frsq(fmaxf(s, 1e-30f));  // holds 1 / L_ii
@@ -1074,8 +1290,59 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   const float foot_r = foot[3];
   const float thigh_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3];
   const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
-  float cs[3][2], cj[3][6], pA[3][6];
+  float cs[3][2];
   float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
+#if GO1_PACKED_ABA
+  f2 cjp[3][3], pAp[3][3];  // c_j and the articulated bias force as (angular, linear) pairs
+  {
+    float Rp[9], pp[3];
+    f2 vp[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rp[i] = R[i];
+    pp[0] = S.pos[0]; pp[1] = S.pos[1]; pp[2] = S.pos[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vp[i] = f2{vb[i], vb[3 + i]};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int ax = j == 0 ? 0 : 1;
+      const float* r = origin + j * 3;
+      float sn, cn;
+      hw_sincosf(S.q[j], &sn, &cn);
+      cs[j][0] = cn; cs[j][1] = sn;
+      f2 vj[3];
+      xm2(ax, cn, sn, offset_mask(j), r, vp, vj);
+      vj[ax].x += S.qd[j];
+      // c_j = v_j x (S qd), S = unit axis ax: pair ax is exactly zero and never read
+      {
+        const float qdj = S.qd[j];
+        const int p1 = (ax + 1) % 3, p2 = (ax + 2) % 3;  // (w x e_ax)_p1 = w_p2, (.)_p2 = -w_p1
+        cjp[j][ax] = f2{0.0f, 0.0f};
+        cjp[j][p1] = vj[p2] * qdj;
+        cjp[j][p2] = -(vj[p1] * qdj);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)  // pp += Rp r over the components r may have
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if ((offset_mask(j) >> k) & 1) pp[i] += Rp[3 * i + k] * r[k];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
+      // rigid bias force v x* I v about the link origin (gravity: a base acceleration, below)
+      rigid_bias2(LC + 10 * j, vj, pAp[j]);
+      if (j > 0) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Rl[j - 1][i] = Rp[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pl[j - 1][i] = pp[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { vl[j - 1][i] = vj[i].x; vl[j - 1][3 + i] = vj[i].y; }
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) vp[i] = vj[i];
+    }
+  }
+#else
+  float cj[3][6], pA[3][6];
   {
     float Rp[9], pp[3], vp[6];
 #pragma unroll
@@ -1127,6 +1394,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       for (int i = 0; i < 6; ++i) vp[i] = vj[i];
     }
   }
+#endif
   MARK(leg_kin_done);
   // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
   //      corner 2 leg, corner 2 leg + 1]; forces in the body frame of the point's body
@@ -1246,14 +1514,126 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
 #pragma unroll
     for (int i = 0; i < 6; ++i) { red[i] = fth[i]; red[6 + i] = fca[i]; red[12 + i] = fbase[i]; }
     rowsum4_n<18>(red);
+#if GO1_PACKED_ABA
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pAp[1][i] -= f2{red[i], red[3 + i]};
+      pAp[2][i] -= f2{red[6 + i], red[9 + i]};
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) fbase[i] = red[12 + i];
+#else
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       pA[1][i] -= red[i];
       pA[2][i] -= red[6 + i];
       fbase[i] = red[12 + i];
     }
+#endif
   }
   MARK(leg_kin_contacts_done);
+#if GO1_PACKED_ABA
+  // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
+  f2 Up[3][3];  // U = column ax of the articulated inertia, (angular, linear) pairs
+  float D[3], u[3];
+  SIP Ip;
+  f2 pp6[3];
+  {
+    SIP IA;
+    rigid_sip(LC + 20, 1.0f, IA);
+#pragma unroll
+    for (int j = 2; j >= 0; --j) {
+      const int ax = j == 0 ? 0 : 1;
+      float t = tau[j];
+      // joint-limit spring-damper, implicit in the joint (see the scalar form below)
+      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
+      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
+      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
+      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
+      t -= lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) Up[j][i] = sip_col(IA, ax, i);
+      D[j] = IA.ac[s3i(ax, ax)].x + (lim_on ? h * dl + h * h * kl : 0.0f);
+      u[j] = t - pAp[j][ax].x;
+      const float invD = frcp(D[j]);
+      D[j] = invD;  // the forward pass only needs 1 / D
+      f2 V[3];  // U / D
+#pragma unroll
+      for (int i = 0; i < 3; ++i) V[i] = Up[j][i] * invD;
+      SIP Ia;  // IA - U U^T / D: the A and C blocks as pairs, B scalar
+      const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Ia.ac[k] = IA.ac[k] - Up[j][II[k]] * V[JJ[k]];
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Up[j][a].x * V[b].y;
+      f2 Iac[3], pa[3], pt[3];
+      sip_mul_sparse(Ia, cjp[j], ax, Iac);
+      const float ud = u[j] * invD;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pa[i] = pAp[j][i] + Iac[i] + Up[j][i] * ud;
+      SIP It;
+      xform_inertia2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
+      xfT2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
+      if (j > 0) {
+        rigid_sip(LC + 10 * (j - 1), 1.0f, IA);
+        sip_add(IA, It);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
+      } else {
+        Ip = It;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pp6[i] = pt[i];
+      }
+    }
+  }
+  MARK(backward_done);
+  // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
+  const float* bb = model;
+  const float mscale = (bb[0] + payload) * frcp(bb[0]);
+  SIP I0;
+  rigid_sip(bb, mscale, I0);
+  float p0[6], gb[3];
+  rigid_bias(bb, mscale, vb, p0);
+  mat3T_vec(R, g, gb);  // gravity in the base frame: added to the relative base acceleration below
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Ip.ac[k] = f2{qsum(Ip.ac[k].x), qsum(Ip.ac[k].y)};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) pp6[i] = f2{qsum(pp6[i].x - fbase[i]), qsum(pp6[i].y - fbase[3 + i])};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Ip.b[i] = qsum(Ip.b[i]);
+  sip_add(I0, Ip);
+  float rhs[6], a0[6];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    rhs[i] = -(p0[i] + pp6[i].x);
+    rhs[3 + i] = -(p0[3 + i] + pp6[i].y);
+  }
+  solve6p(I0, rhs, a0);
+  MARK(base_solve_done);
+  // ---- forward pass
+  float qdd[3];
+  {
+    f2 ap[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ap[i] = f2{a0[i], a0[3 + i]};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int ax = j == 0 ? 0 : 1;
+      f2 aj[3];
+      xm2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, ap, aj);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i != ax) aj[i] += cjp[j][i];  // pair ax of c_j is zero
+      const f2 ua = Up[j][0] * aj[0] + Up[j][1] * aj[1] + Up[j][2] * aj[2];
+      qdd[j] = (u[j] - (ua.x + ua.y)) * D[j];
+      aj[ax].x += qdd[j];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ap[i] = aj[i];
+    }
+  }
+#else
   // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
   float U[3][6], D[3], u[3];
   SI Ip;
@@ -1360,6 +1740,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       for (int i = 0; i < 6; ++i) ap[i] = aj[i];
     }
   }
+#endif
   MARK(forward_done);
   // ---- semi-implicit Euler (base identical in the quad)
   float wv[3], alb[3], aw[3], al[3];

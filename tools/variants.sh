@@ -9,7 +9,7 @@ if [ "$1" = build ]; then
   shift
   while [ $# -gt 1 ]; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off $BASEFLAGS $2 \
-      -o "$B/libgo1_var_$1.so" "$ROOT/legged_tracking_amd/csrc/go1_step.hip" || exit 1
+      -o "$B/libgo1_var_$1.so" "$ROOT/legged_tracking_amd/csrc/go1_step.hip" "$ROOT/legged_tracking_amd/csrc/go1_terrain.hip" || exit 1
     echo "built $1: $2"; shift 2
   done
   exit 0
