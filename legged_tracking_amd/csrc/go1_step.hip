@@ -544,15 +544,16 @@ __device__ __forceinline__ void rigid_bias(const float* body, float mscale, cons
 
 // rigid_bias on a velocity given as (angular, linear) pairs, the result as pairs: the two
 // products with w, w x L and w x p, run as one packed cross product of w with the (L, p) pairs
-__device__ __forceinline__ void rigid_bias2(const float* body, const f2* vel, f2* o) {
-  const float m = body[0];
+__device__ __forceinline__ void rigid_bias2(const float* body, const f2* vel, f2* o, float mscale = 1.0f) {
+  const float m = body[0] * mscale;
   const float* c = body + 1;
   const float w[3] = {vel[0].x, vel[1].x, vel[2].x}, v[3] = {vel[0].y, vel[1].y, vel[2].y};
   float wc[3], p[3], L[3], cp[3], b[3];
   cross3(w, c, wc);
 #pragma unroll
   for (int i = 0; i < 3; ++i) p[i] = m * (v[i] + wc[i]);
-  const float ixx = body[4], ixy = body[5], ixz = body[6], iyy = body[7], iyz = body[8], izz = body[9];
+  const float ixx = body[4] * mscale, ixy = body[5] * mscale, ixz = body[6] * mscale;
+  const float iyy = body[7] * mscale, iyz = body[8] * mscale, izz = body[9] * mscale;
   cross3(c, p, cp);
   L[0] = ixx * w[0] + ixy * w[1] + ixz * w[2] + cp[0];
   L[1] = ixy * w[0] + iyy * w[1] + iyz * w[2] + cp[1];
@@ -782,9 +783,6 @@ __device__ __forceinline__ void solve6(const SI& M, const float* b, float* x) {
 // a spatial vector is three (angular_i, linear_i) pairs, and a spatial inertia keeps its two
 // symmetric 3 x 3 blocks as six (A_t, C_t) pairs -- every rotation, rank-1 update and sum of the
 // articulated-body passes treats the two halves alike.  B (general 3 x 3) stays scalar.
-#ifndef GO1_PACKED_ABA
-#define GO1_PACKED_ABA 1
-#endif
 struct SIP {
   f2 ac[6];
   float b[9];
@@ -1244,7 +1242,8 @@ __device__ __forceinline__ void legs_bbox_centre(const float* pos, const float* 
 typedef const __attribute__((address_space(4))) go1_config CCfg;
 
 struct Phys {
-  float pos[3], quat[4], v[3], w[3];  // base (replicated on the 16 lanes of the env)
+  float pos[3], quat[4];  // base (replicated on the 16 lanes of the env)
+  f2 wv[3];               // base angular and linear velocity (world) as (w_i, v_i) pairs
   float q[3], qd[3];                   // this lane's leg
 };
 
@@ -1280,9 +1279,10 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
   float R[9];
   quat_to_R(S.quat, R);
-  float vb[6];
-  mat3T_vec(R, S.w, vb);
-  mat3T_vec(R, S.v, vb + 3);
+  f2 vbp[3];  // base-frame (angular, linear) velocity pairs: R^T on both halves at once
+#pragma unroll
+  for (int i = 0; i < 3; ++i) vbp[i] = R[i] * S.wv[0] + R[3 + i] * S.wv[1] + R[6 + i] * S.wv[2];
+  const float vb[6] = {vbp[0].x, vbp[1].x, vbp[2].x, vbp[0].y, vbp[1].y, vbp[2].y};
   const float* th = model + 13 * 10 + 4 * 9 + 3 + 1;  // trunk half extents
   // ---- this leg: kinematics, rigid bias forces and gravity (hip -> calf)
   const float* origin = LC + 30;
@@ -1292,16 +1292,16 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
   float cs[3][2];
   float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
-#if GO1_PACKED_ABA
   f2 cjp[3][3], pAp[3][3];  // c_j and the articulated bias force as (angular, linear) pairs
   {
-    float Rp[9], pp[3];
+    // link frame: rows 0 and 1 of the rotation as pairs over the column (row0_k, row1_k)
+    f2 R01[3], pp01 = f2{S.pos[0], S.pos[1]};
+    float R2[3], pp2 = S.pos[2];
     f2 vp[3];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) Rp[i] = R[i];
-    pp[0] = S.pos[0]; pp[1] = S.pos[1]; pp[2] = S.pos[2];
+    for (int k = 0; k < 3; ++k) { R01[k] = f2{R[k], R[3 + k]}; R2[k] = R[6 + k]; }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) vp[i] = f2{vb[i], vb[3 + i]};
+    for (int i = 0; i < 3; ++i) vp[i] = vbp[i];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int ax = j == 0 ? 0 : 1;
@@ -1321,19 +1321,16 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
         cjp[j][p2] = -(vj[p1] * qdj);
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i)  // pp += Rp r over the components r may have
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if ((offset_mask(j) >> k) & 1) pp[i] += Rp[3 * i + k] * r[k];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
+      for (int k = 0; k < 3; ++k)  // pp += Rp r over the components r may have
+        if ((offset_mask(j) >> k) & 1) { pp01 += R01[k] * r[k]; pp2 += R2[k] * r[k]; }
+      rE2(ax, cn, sn, R01, R01);
+      rE(ax, cn, sn, R2, R2);
       // rigid bias force v x* I v about the link origin (gravity: a base acceleration, below)
       rigid_bias2(LC + 10 * j, vj, pAp[j]);
       if (j > 0) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i) Rl[j - 1][i] = Rp[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) pl[j - 1][i] = pp[i];
+        for (int k = 0; k < 3; ++k) { Rl[j - 1][k] = R01[k].x; Rl[j - 1][3 + k] = R01[k].y; Rl[j - 1][6 + k] = R2[k]; }
+        pl[j - 1][0] = pp01.x; pl[j - 1][1] = pp01.y; pl[j - 1][2] = pp2;
 #pragma unroll
         for (int i = 0; i < 3; ++i) { vl[j - 1][i] = vj[i].x; vl[j - 1][3 + i] = vj[i].y; }
       }
@@ -1341,60 +1338,6 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       for (int i = 0; i < 3; ++i) vp[i] = vj[i];
     }
   }
-#else
-  float cj[3][6], pA[3][6];
-  {
-    float Rp[9], pp[3], vp[6];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) Rp[i] = R[i];
-    pp[0] = S.pos[0]; pp[1] = S.pos[1]; pp[2] = S.pos[2];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) vp[i] = vb[i];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int ax = j == 0 ? 0 : 1;
-      const float* r = origin + j * 3;
-      float sn, cn;
-      hw_sincosf(S.q[j], &sn, &cn);
-      cs[j][0] = cn; cs[j][1] = sn;
-      float vj[6];
-      xm(ax, cn, sn, offset_mask(j), r, vp, vj);
-      vj[ax] += S.qd[j];
-      // c_j = v_j x (S qd), S = unit axis ax: components ax and 3 + ax are exactly zero and
-      // are never read (si_mul_sparse, the forward pass), the others are single products
-      {
-        const float qdj = S.qd[j];
-        const int p1 = (ax + 1) % 3, p2 = (ax + 2) % 3;  // (w x e_ax)_p1 = w_p2, (.)_p2 = -w_p1
-        cj[j][ax] = 0.0f; cj[j][3 + ax] = 0.0f;
-        cj[j][p1] = vj[p2] * qdj; cj[j][p2] = -(vj[p1] * qdj);
-        cj[j][3 + p1] = vj[3 + p2] * qdj; cj[j][3 + p2] = -(vj[3 + p1] * qdj);
-      }
-      // world pose of link j: p = pp + Rp r ; Rw rows = E (rows of Rp)
-#pragma unroll
-      for (int i = 0; i < 3; ++i)  // pp += Rp r over the components r may have
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if ((offset_mask(j) >> k) & 1) pp[i] += Rp[3 * i + k] * r[k];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
-      // rigid bias force v x* I v about the link origin.  Gravity is not a per-link force here:
-      // a uniform field is a fictitious base acceleration (Featherstone's a_0 = -a_g), so the
-      // recursion runs on accelerations relative to free fall and the base adds g back at the end
-      const float* B = LC + 10 * j;
-      rigid_bias(B, 1.0f, vj, pA[j]);
-      if (j > 0) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Rl[j - 1][i] = Rp[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) pl[j - 1][i] = pp[i];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) vl[j - 1][i] = vj[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) vp[i] = vj[i];
-    }
-  }
-#endif
   MARK(leg_kin_done);
   // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
   //      corner 2 leg, corner 2 leg + 1]; forces in the body frame of the point's body
@@ -1514,7 +1457,6 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
 #pragma unroll
     for (int i = 0; i < 6; ++i) { red[i] = fth[i]; red[6 + i] = fca[i]; red[12 + i] = fbase[i]; }
     rowsum4_n<18>(red);
-#if GO1_PACKED_ABA
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       pAp[1][i] -= f2{red[i], red[3 + i]};
@@ -1522,17 +1464,8 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i) fbase[i] = red[12 + i];
-#else
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      pA[1][i] -= red[i];
-      pA[2][i] -= red[6 + i];
-      fbase[i] = red[12 + i];
-    }
-#endif
   }
   MARK(leg_kin_contacts_done);
-#if GO1_PACKED_ABA
   // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
   f2 Up[3][3];  // U = column ax of the articulated inertia, (angular, linear) pairs
   float D[3], u[3];
@@ -1594,8 +1527,9 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   const float mscale = (bb[0] + payload) * frcp(bb[0]);
   SIP I0;
   rigid_sip(bb, mscale, I0);
-  float p0[6], gb[3];
-  rigid_bias(bb, mscale, vb, p0);
+  f2 p0[3];
+  float gb[3];
+  rigid_bias2(bb, vbp, p0, mscale);
   mat3T_vec(R, g, gb);  // gravity in the base frame: added to the relative base acceleration below
 #pragma unroll
   for (int k = 0; k < 6; ++k) Ip.ac[k] = f2{qsum(Ip.ac[k].x), qsum(Ip.ac[k].y)};
@@ -1607,8 +1541,8 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   float rhs[6], a0[6];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    rhs[i] = -(p0[i] + pp6[i].x);
-    rhs[3 + i] = -(p0[3 + i] + pp6[i].y);
+    rhs[i] = -(p0[i].x + pp6[i].x);
+    rhs[3 + i] = -(p0[i].y + pp6[i].y);
   }
   solve6p(I0, rhs, a0);
   MARK(base_solve_done);
@@ -1633,137 +1567,30 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       for (int i = 0; i < 3; ++i) ap[i] = aj[i];
     }
   }
-#else
-  // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
-  float U[3][6], D[3], u[3];
-  SI Ip;
-  float pp6[6];
-  {
-    SI IA;
-    rigid_si(LC + 20, 1.0f, IA);
-#pragma unroll
-    for (int j = 2; j >= 0; --j) {
-      const int ax = j == 0 ? 0 : 1;
-      const int dof = leg * 3 + j;
-      float t = tau[j];
-      // joint-limit spring-damper, implicit in the joint: the torque at the end of the
-      // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
-      // into the joint inertia D (unconditionally stable for any k, d)
-      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
-      (void)dof;
-      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
-      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
-      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
-      t -= lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) U[j][i] = si_get(IA, i, ax);
-      D[j] = si_get(IA, ax, ax) + (lim_on ? h * dl + h * h * kl : 0.0f);
-      u[j] = t - pA[j][ax];
-      const float invD = frcp(D[j]);
-      D[j] = invD;  // the forward pass only needs 1 / D
-      const float Ua[3] = {U[j][0], U[j][1], U[j][2]}, Ul[3] = {U[j][3], U[j][4], U[j][5]};
-      const float Va[3] = {Ua[0] * invD, Ua[1] * invD, Ua[2] * invD};  // U / D
-      const float Vl[3] = {Ul[0] * invD, Ul[1] * invD, Ul[2] * invD};
-      SI Ia;  // IA - U U^T / D (fused multiply-subtracts)
-      Ia.a[0] = IA.a[0] - Ua[0] * Va[0]; Ia.a[1] = IA.a[1] - Ua[0] * Va[1];
-      Ia.a[2] = IA.a[2] - Ua[0] * Va[2]; Ia.a[3] = IA.a[3] - Ua[1] * Va[1];
-      Ia.a[4] = IA.a[4] - Ua[1] * Va[2]; Ia.a[5] = IA.a[5] - Ua[2] * Va[2];
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Ua[a] * Vl[b];
-      Ia.c[0] = IA.c[0] - Ul[0] * Vl[0]; Ia.c[1] = IA.c[1] - Ul[0] * Vl[1];
-      Ia.c[2] = IA.c[2] - Ul[0] * Vl[2]; Ia.c[3] = IA.c[3] - Ul[1] * Vl[1];
-      Ia.c[4] = IA.c[4] - Ul[1] * Vl[2]; Ia.c[5] = IA.c[5] - Ul[2] * Vl[2];
-      float Iac[6], pa[6], pt[6];
-      si_mul_sparse(Ia, cj[j], ax, Iac);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) pa[i] = pA[j][i] + Iac[i] + U[j][i] * u[j] * invD;
-      SI It;
-      xform_inertia(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
-      xfT(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
-      if (j > 0) {
-        rigid_si(LC + 10 * (j - 1), 1.0f, IA);
-        si_add(IA, It);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) pA[j - 1][i] += pt[i];
-      } else {
-        Ip = It;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) pp6[i] = pt[i];
-      }
-    }
-  }
-  MARK(backward_done);
-  // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
-  const float* bb = model;
-  const float mscale = (bb[0] + payload) * frcp(bb[0]);
-  SI I0;
-  rigid_si(bb, mscale, I0);
-  float p0[6], gb[3];
-  rigid_bias(bb, mscale, vb, p0);
-  mat3T_vec(R, g, gb);  // gravity in the base frame: added to the relative base acceleration below
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    Ip.a[i] = qsum(Ip.a[i]);
-    Ip.c[i] = qsum(Ip.c[i]);
-    pp6[i] = qsum(pp6[i] - fbase[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Ip.b[i] = qsum(Ip.b[i]);
-  si_add(I0, Ip);
-  float rhs[6], a0[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) rhs[i] = -(p0[i] + pp6[i]);
-  solve6(I0, rhs, a0);
-  MARK(base_solve_done);
-  // ---- forward pass
-  float qdd[3];
-  {
-    float ap[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) ap[i] = a0[i];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int ax = j == 0 ? 0 : 1;
-      float aj[6];
-      xm(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, ap, aj);
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-        if (i % 3 != ax) aj[i] += cj[j][i];  // components ax, 3 + ax of c_j are zero
-      float Ua = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) Ua += U[j][i] * aj[i];
-      qdd[j] = (u[j] - Ua) * D[j];
-      aj[ax] += qdd[j];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) ap[i] = aj[i];
-    }
-  }
-#endif
   MARK(forward_done);
   // ---- semi-implicit Euler (base identical in the quad)
-  float wv[3], alb[3], aw[3], al[3];
-  cross3(vb, vb + 3, wv);
-  // a0 is relative to free fall: the base's linear acceleration is a0_lin + g
-  alb[0] = a0[3] + gb[0] + wv[0]; alb[1] = a0[4] + gb[1] + wv[1]; alb[2] = a0[5] + gb[2] + wv[2];
-  mat3_vec(R, a0, aw);
-  mat3_vec(R, alb, al);
+  float wxv[3];
+  cross3(vb, vb + 3, wxv);
+  // a0 is relative to free fall: the base's linear acceleration is a0_lin + g; (angular, linear)
+  // body-frame accelerations as pairs, rotated to the world and integrated together
+  f2 ab[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ab[i] = f2{a0[i], a0[3 + i] + gb[i] + wxv[i]};
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    S.w[i] += h * aw[i];
-    S.v[i] += h * al[i];
-    S.pos[i] += h * S.v[i];
+    S.wv[i] += h * (R[3 * i] * ab[0] + R[3 * i + 1] * ab[1] + R[3 * i + 2] * ab[2]);
+    S.pos[i] += h * S.wv[i].y;
   }
   {
-    const float wn2 = S.w[0] * S.w[0] + S.w[1] * S.w[1] + S.w[2] * S.w[2];
+    const float w[3] = {S.wv[0].x, S.wv[1].x, S.wv[2].x};
+    const float wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
     const float iwn = frsq(fmaxf(wn2, 1e-30f));
     const float wn = wn2 * iwn;
     const float thh = 0.5f * h * wn;
     float sth, cth;
     hw_sincosf(thh, &sth, &cth);
     const float sc = thh > 1e-12f ? sth * iwn : 0.5f * h;
-    const float dq[4] = {S.w[0] * sc, S.w[1] * sc, S.w[2] * sc, cth};
+    const float dq[4] = {w[0] * sc, w[1] * sc, w[2] * sc, cth};
     float* q = S.quat;
     float nq[4];
     nq[3] = dq[3] * q[3] - dq[0] * q[0] - dq[1] * q[1] - dq[2] * q[2];
@@ -2026,8 +1853,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       P.pos[i] = st.root[(size_t)e * 13 + i];
-      P.v[i] = st.root[(size_t)e * 13 + 7 + i];
-      P.w[i] = st.root[(size_t)e * 13 + 10 + i];
+      P.wv[i] = f2{st.root[(size_t)e * 13 + 10 + i], st.root[(size_t)e * 13 + 7 + i]};
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
@@ -2229,7 +2055,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   } else {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      root[i] = P.pos[i]; root[7 + i] = P.v[i]; root[10 + i] = P.w[i];
+      root[i] = P.pos[i]; root[7 + i] = P.wv[i].y; root[10 + i] = P.wv[i].x;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) root[3 + i] = P.quat[i];
