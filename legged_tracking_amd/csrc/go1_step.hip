@@ -1040,13 +1040,19 @@ struct CP {
 // carried as the two halves of an f2 all the way from the bilinear patch to the force.
 __device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
 
-// (floor, ceiling) heights and gradients at world (x, y), bilinear: the LDS patch stores
-// (floor, ceiling) per cell, i.e. already in f2 layout
-__device__ __forceinline__ void height_query_pk(const Terr& T, float x, float y, f2& h, f2& gx, f2& gy) {
+// (floor, ceiling) heights and gradients at world (x, y), bilinear, in two halves, so that the
+// corner reads are issued early and land while independent work runs (the articulated-inertia
+// chain of the sub-step): hq_fetch reads the four (floor, ceiling) corners -- the LDS patch stores
+// (floor, ceiling) per cell, i.e. already in f2 layout; the HBM tile outside it -- and hq_finish
+// interpolates.
+struct HQ {
+  f2 c00, c10, c01, c11;
+  float a, b;
+};
+__device__ __forceinline__ void hq_fetch(const Terr& T, float x, float y, HQ& q) {
   if (!T.tile) {
-    h = f2{0.0f, 1e9f};
-    gx = f2s(0.0f);
-    gy = f2s(0.0f);
+    q.c00 = q.c10 = q.c01 = q.c11 = f2{0.0f, 1e9f};
+    q.a = q.b = 0.0f;
     return;
   }
   const float ihs = frcp(T.hs);
@@ -1054,8 +1060,8 @@ __device__ __forceinline__ void height_query_pk(const Terr& T, float x, float y,
   const float v = fminf(fmaxf((y - T.oy) * ihs, -4.0f), (float)(T.ny + 4));
   const float fu = floorf(u), fv = floorf(v);
   const int i = (int)fu, j = (int)fv;
-  const float a = u - fu, b = v - fv;
-  f2 c00, c10, c01, c11;
+  q.a = u - fu;
+  q.b = v - fv;
 #ifdef GO1_ABL_NO_FALLBACK  // ablation build only: every query from the (clamped) LDS patch
   const int li = min(max(i - T.pi0, 0), PSZX - 2), lj = min(max(j - T.pj0, 0), PSZY - 2);
 #else
@@ -1064,25 +1070,28 @@ __device__ __forceinline__ void height_query_pk(const Terr& T, float x, float y,
   if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
     const float2* pp = T.patch + li * PSZY + lj;
     const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];
-    c00 = f2{q00.x, q00.y}; c01 = f2{q01.x, q01.y}; c10 = f2{q10.x, q10.y}; c11 = f2{q11.x, q11.y};
+    q.c00 = f2{q00.x, q00.y}; q.c01 = f2{q01.x, q01.y}; q.c10 = f2{q10.x, q10.y}; q.c11 = f2{q11.x, q11.y};
   } else {
-    c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
-    c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
-    c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
-    c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
+    q.c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
+    q.c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
+    q.c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
+    q.c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
   }
-  const float a1 = 1.0f - a, b1 = 1.0f - b;
-  h = (a1 * b1) * c00 + (a * b1) * c10 + (a1 * b) * c01 + (a * b) * c11;
-  gx = (b1 * (c10 - c00) + b * (c11 - c01)) * ihs;
-  gy = (a1 * (c01 - c00) + a * (c11 - c10)) * ihs;
+}
+__device__ __forceinline__ void hq_finish(const Terr& T, const HQ& q, f2& h, f2& gx, f2& gy) {
+  const float ihs = frcp(T.hs);
+  const float a = q.a, b = q.b, a1 = 1.0f - a, b1 = 1.0f - b;
+  h = (a1 * b1) * q.c00 + (a * b1) * q.c10 + (a1 * b) * q.c01 + (a * b) * q.c11;
+  gx = (b1 * (q.c10 - q.c00) + b * (q.c11 - q.c01)) * ihs;
+  gy = (a1 * (q.c01 - q.c00) + a * (q.c11 - q.c10)) * ihs;
 }
 
 // penalty contact of a sphere (centre p, velocity pv, radius r) with the floor (pushes up)
 // and the ceiling (pushes down), both layers at once; F = floor + ceiling force
-__device__ __forceinline__ void sphere_contact_pk(const Terr& T, const CP& C, const float* p, const float* pv, float r,
-                                                  float* F) {
+__device__ __forceinline__ void sphere_contact_pk(const Terr& T, const HQ& q, const CP& C, const float* p,
+                                                  const float* pv, float r, float* F) {
   f2 h, gx, gy;
-  height_query_pk(T, p[0], p[1], h, gx, gy);
+  hq_finish(T, q, h, gx, gy);
   const f2 sg = f2{1.0f, -1.0f};
   const f2 dv = sg * (h - p[2]) + r;  // floor: h + r - z, ceiling: z + r - h
   f2 nx = -sg * gx, ny = -sg * gy;
@@ -1339,17 +1348,20 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     }
   }
   MARK(leg_kin_done);
-  // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
-  //      corner 2 leg, corner 2 leg + 1]; forces in the body frame of the point's body
+  // ---- contacts, stage 1: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1,
+  //      foot, corner 2 leg, corner 2 leg + 1] -- world position / velocity, terrain corner reads
+  //      issued (they land during the articulated-inertia chain below)
   float fth[6] = {0, 0, 0, 0, 0, 0}, fca[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
   float Fth[3] = {0, 0, 0}, Fca[3] = {0, 0, 0}, Fft[3] = {0, 0, 0}, Fb[3] = {0, 0, 0};
-#if !defined(GO1_ABL_NO_CONTACT) && GO1_PK_POINTS
+#ifndef GO1_ABL_NO_CONTACT
+  // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
+  // the body-frame force; x = point 2 role, y = point 2 role + 1.  Bodies:
+  // role 0 (thigh, thigh), 1 (thigh, calf), 2 (calf, foot on the calf), 3 (base, base)
+  f2 Rs[9], lp[3], rr, pw[3], vw[3];
+  HQ qa, qb;
   {
-    // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
-    // the body-frame force; x = point 2 role, y = point 2 role + 1.  Bodies:
-    // role 0 (thigh, thigh), 1 (thigh, calf), 2 (calf, foot on the calf), 3 (base, base)
     const bool xt = role <= 1, xc = role == 2, yt = role == 0, yc = role == 1 || role == 2;
-    f2 Rs[9], ps[3], vs[6], lp[3], rr;
+    f2 ps[3], vs[6];
 #pragma unroll
     for (int i = 0; i < 9; ++i) Rs[i] = f2{xt ? Rl[0][i] : (xc ? Rl[1][i] : R[i]), yt ? Rl[0][i] : (yc ? Rl[1][i] : R[i])};
 #pragma unroll
@@ -1371,18 +1383,75 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     // point kinematics: v = R (v_lin + w x lp), p = p_body + R lp
     const f2 wl[3] = {vs[1] * lp[2] - vs[2] * lp[1], vs[2] * lp[0] - vs[0] * lp[2], vs[0] * lp[1] - vs[1] * lp[0]};
     const f2 vlin[3] = {vs[3] + wl[0], vs[4] + wl[1], vs[5] + wl[2]};
-    f2 pw[3], vw[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       pw[i] = ps[i] + Rs[3 * i] * lp[0] + Rs[3 * i + 1] * lp[1] + Rs[3 * i + 2] * lp[2];
       vw[i] = Rs[3 * i] * vlin[0] + Rs[3 * i + 1] * vlin[1] + Rs[3 * i + 2] * vlin[2];
     }
+    hq_fetch(T, pw[0].x, pw[1].x, qa);
+    hq_fetch(T, pw[0].y, pw[1].y, qb);
+  }
+#else  // ablation build only: no contacts
+  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
+#endif
+  MARK(leg_kin_contacts_done);
+  // ---- articulated inertias calf -> hip (they depend on q alone, not on the contact or bias
+  //      forces); the hip's goes to the base.  Kept per joint: U = column ax (pairs), 1 / D, the
+  //      joint torque with the limit spring, and Ia c_j for the bias pass.
+  f2 Up[3][3], Iac[3][3];
+  float D[3], teff[3], u[3];
+  SIP Ip;
+  {
+    SIP IA;
+    rigid_sip(LC + 20, 1.0f, IA);
+#pragma unroll
+    for (int j = 2; j >= 0; --j) {
+      const int ax = j == 0 ? 0 : 1;
+      float t = tau[j];
+      // joint-limit spring-damper, implicit in the joint: the torque at the end of the
+      // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
+      // into the joint inertia D (unconditionally stable for any k, d)
+      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
+      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
+      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
+      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
+      teff[j] = t - (lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) Up[j][i] = sip_col(IA, ax, i);
+      const float invD = frcp(IA.ac[s3i(ax, ax)].x + (lim_on ? h * dl + h * h * kl : 0.0f));
+      D[j] = invD;  // the passes only need 1 / D
+      f2 V[3];  // U / D
+#pragma unroll
+      for (int i = 0; i < 3; ++i) V[i] = Up[j][i] * invD;
+      SIP Ia;  // IA - U U^T / D: the A and C blocks as pairs, B scalar
+      const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Ia.ac[k] = IA.ac[k] - Up[j][II[k]] * V[JJ[k]];
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Up[j][a].x * V[b].y;
+      sip_mul_sparse(Ia, cjp[j], ax, Iac[j]);
+      SIP It;
+      xform_inertia2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
+      if (j > 0) {
+        rigid_sip(LC + 10 * (j - 1), 1.0f, IA);
+        sip_add(IA, It);
+      } else {
+        Ip = It;
+      }
+    }
+  }
+  // ---- contacts, stage 2: forces from the landed corners; forces in the body frame of the
+  //      point's body
+#ifndef GO1_ABL_NO_CONTACT
+  {
     float Fa[3], Fb2[3];
     {
       const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
       const float pb[3] = {pw[0].y, pw[1].y, pw[2].y}, vb2[3] = {vw[0].y, vw[1].y, vw[2].y};
-      sphere_contact_pk(T, C, pa, va, rr.x, Fa);
-      sphere_contact_pk(T, C, pb, vb2, rr.y, Fb2);
+      sphere_contact_pk(T, qa, C, pa, va, rr.x, Fa);
+      sphere_contact_pk(T, qb, C, pb, vb2, rr.y, Fb2);
     }
     const f2 F[3] = {f2{Fa[0], Fb2[0]}, f2{Fa[1], Fb2[1]}, f2{Fa[2], Fb2[2]}};
     // body-frame force f = R^T F and moment lp x f
@@ -1408,49 +1477,6 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       Fb[i] = role == 3 ? tot : 0.0f;
     }
   }
-#elif !defined(GO1_ABL_NO_CONTACT)
-#pragma unroll
-  for (int sidx = 0; sidx < 2; ++sidx) {
-    const int p = 2 * role + sidx;
-    const bool on_thigh = p < 3, on_calf = p >= 3 && p < 6, on_base = p >= 6;
-    float Rs[9], ps[3], vs[6];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) Rs[i] = on_thigh ? Rl[0][i] : (on_calf ? Rl[1][i] : R[i]);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) ps[i] = on_thigh ? pl[0][i] : (on_calf ? pl[1][i] : S.pos[i]);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) vs[i] = on_thigh ? vl[0][i] : (on_calf ? vl[1][i] : vb[i]);
-    const int cx = leg * 2 + (p - 6);
-    const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
-    float lp[3];
-    lp[0] = on_base ? ((cx & 1) ? th[0] : -th[0]) : (p == 5 ? foot[0] : 0.0f);
-    lp[1] = on_base ? ((cx & 2) ? th[1] : -th[1]) : (p == 5 ? foot[1] : 0.0f);
-    lp[2] = on_base ? ((cx & 4) ? th[2] : -th[2]) : (p == 5 ? foot[2] : lz);
-    const float rr = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
-    float pw[3], vw[3], F[3], f6[6] = {0, 0, 0, 0, 0, 0};
-    point_kin(Rs, ps, vs, lp, pw, vw);
-#if GO1_PK_CONTACT
-    sphere_contact_pk(T, C, pw, vw, rr, F);
-#else
-    sphere_contact(T, C, pw, vw, rr, F);
-#endif
-    point_force(Rs, lp, F, f6);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      fth[i] += on_thigh ? f6[i] : 0.0f;
-      fca[i] += on_calf ? f6[i] : 0.0f;
-      fbase[i] += on_base ? f6[i] : 0.0f;
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      Fth[i] += on_thigh ? F[i] : 0.0f;
-      Fca[i] += (p == 3 || p == 4) ? F[i] : 0.0f;
-      Fft[i] += p == 5 ? F[i] : 0.0f;
-      Fb[i] += on_base ? F[i] : 0.0f;
-    }
-  }
-#else  // ablation build only: no contacts
-  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
 #endif
   {
     float red[18];
@@ -1465,60 +1491,23 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
 #pragma unroll
     for (int i = 0; i < 6; ++i) fbase[i] = red[12 + i];
   }
-  MARK(leg_kin_contacts_done);
-  // ---- backward pass calf -> hip; the hip's articulated inertia goes to the base
-  f2 Up[3][3];  // U = column ax of the articulated inertia, (angular, linear) pairs
-  float D[3], u[3];
-  SIP Ip;
+  // ---- bias forces calf -> hip (the contact forces are in pA now)
   f2 pp6[3];
-  {
-    SIP IA;
-    rigid_sip(LC + 20, 1.0f, IA);
 #pragma unroll
-    for (int j = 2; j >= 0; --j) {
-      const int ax = j == 0 ? 0 : 1;
-      float t = tau[j];
-      // joint-limit spring-damper, implicit in the joint (see the scalar form below)
-      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
-      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
-      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
-      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
-      t -= lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f;
+  for (int j = 2; j >= 0; --j) {
+    const int ax = j == 0 ? 0 : 1;
+    u[j] = teff[j] - pAp[j][ax].x;
+    const float ud = u[j] * D[j];
+    f2 pa[3], pt[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) Up[j][i] = sip_col(IA, ax, i);
-      D[j] = IA.ac[s3i(ax, ax)].x + (lim_on ? h * dl + h * h * kl : 0.0f);
-      u[j] = t - pAp[j][ax].x;
-      const float invD = frcp(D[j]);
-      D[j] = invD;  // the forward pass only needs 1 / D
-      f2 V[3];  // U / D
+    for (int i = 0; i < 3; ++i) pa[i] = pAp[j][i] + Iac[j][i] + Up[j][i] * ud;
+    xfT2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
+    if (j > 0) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) V[i] = Up[j][i] * invD;
-      SIP Ia;  // IA - U U^T / D: the A and C blocks as pairs, B scalar
-      const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+      for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
+    } else {
 #pragma unroll
-      for (int k = 0; k < 6; ++k) Ia.ac[k] = IA.ac[k] - Up[j][II[k]] * V[JJ[k]];
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Up[j][a].x * V[b].y;
-      f2 Iac[3], pa[3], pt[3];
-      sip_mul_sparse(Ia, cjp[j], ax, Iac);
-      const float ud = u[j] * invD;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) pa[i] = pAp[j][i] + Iac[i] + Up[j][i] * ud;
-      SIP It;
-      xform_inertia2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
-      xfT2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
-      if (j > 0) {
-        rigid_sip(LC + 10 * (j - 1), 1.0f, IA);
-        sip_add(IA, It);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
-      } else {
-        Ip = It;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) pp6[i] = pt[i];
-      }
+      for (int i = 0; i < 3; ++i) pp6[i] = pt[i];
     }
   }
   MARK(backward_done);
@@ -2554,11 +2543,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     st.motor_offset[dj] = pick(offset);
     st.joint_pos_target[dj] = pick(tgt);
     const float sj = pick(scaled);
+    // the surviving old slots come from the prologue's registers (lag_pre = slots 1..6): a
+    // reload of lag_in here put an L2 round trip on the critical path of every wave's end
+    float lagj[GO1_LAG_SLOTS - 1];
+#pragma unroll
+    for (int sl = 0; sl < GO1_LAG_SLOTS - 1; ++sl) lagj[sl] = pick(lag_pre[sl]);
 #pragma unroll
     for (int s2 = 0; s2 < GO1_LAG_SLOTS; ++s2) {
-      const int src = s2 + dec;  // slot after `dec` pushes
-      const float v = reset ? 0.0f : (src < GO1_LAG_SLOTS ? lag_in[src * 12 + j] : sj);
-      st.lag[(size_t)e * 84 + s2 * 12 + leg * 3 + j] = v;
+      const int src = s2 + dec;  // slot after `dec` pushes (dec >= 1: slot 0 never survives)
+      float v = sj;
+#pragma unroll
+      for (int sl = 0; sl < GO1_LAG_SLOTS - 1; ++sl) v = src == sl + 1 ? lagj[sl] : v;
+      st.lag[(size_t)e * 84 + s2 * 12 + leg * 3 + j] = reset ? 0.0f : v;
     }
     st.pos_err_hist[(size_t)e * 24 + leg * 3 + j] = pick(eh[0]);
     st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j] = pick(eh[1]);
