@@ -719,6 +719,8 @@ SUPPORTED = {
     "env.observe_timing_parameter": ((False,), ":429-431"),
     "env.observe_clock_inputs": ((False,), ":433-435"),
     "terrain.measure_front_half": ((True, False), ":395-399"),
+    # with OMPL installed the reference redraws a sub-terrain until a planner finds a path through it
+    "terrain.valid_tunnel_only": ((False,), "go1_gym/utils/tunnel.py:101-118 (OMPL validity check)"),
     "commands.traj_function": (("fixed_target", "random_target", "random_goal"), "trajectory_function.py:14-93"),
     "commands.traj_length": (tuple(range(1, 17)), "trajectory_function.py:14-93 (<= GO1_MAX_TRAJ)"),
     "commands.sampling_based_planning": ((False,), ":850-921 (OMPL planner)"),

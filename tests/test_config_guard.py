@@ -28,6 +28,7 @@ def _abi(argv=(), n=32, **over):
     ((), {"domain_rand.push_robots": True}, NotImplementedError, "push_robots"),
     ((), {"env.observe_vel": True}, NotImplementedError, "observe_vel"),
     ((), {"terrain.terrain_type": "multi_path"}, NotImplementedError, "terrain_type"),
+    ((), {"terrain.valid_tunnel_only": True}, NotImplementedError, "valid_tunnel_only"),
     ((), {"rewards.reward_container_name": "CoRLRewards"}, NotImplementedError, "reward_container_name"),
     ((), {"reward_scales.termination": -1.0}, AttributeError, "_reward_termination"),
     ((), {"env.num_observations": 262}, AssertionError, "num_observations"),
