@@ -666,7 +666,7 @@ if __name__ == "__main__":
     if a.which == "all":
         # one fresh process per fixture: the reference mutates its module-level Cfg
         import subprocess
-        for w in ("single_path", "plane", "events", *VARIANTS):
+        for w in ("single_path", "plane", "events", "full_grid", *VARIANTS):
             subprocess.run([sys.executable, __file__, "--steps", str(a.steps), "--which", w], check=True)
     elif a.which == "single_path":
         # gravity zeroing at counter 396 and resampling at 400 fall inside the window
@@ -677,6 +677,9 @@ if __name__ == "__main__":
     elif a.which == "plane":
         # plane (no camera_zero: the reference raises with it, :402); exploration decay after 2500
         run("plane", 64, 4, a.steps, 12, os.path.join(HERE, "step_plane.npz"), counter_start=2497)
+    elif a.which == "full_grid":
+        # the README grid at full size: 32 x 32 sub-terrains, one env on each (1024 envs), 2 steps
+        run("single_path", 1024, 32, 2, 17, os.path.join(HERE, "step_full_grid.npz"), counter_start=120)
     elif a.which in VARIANTS:
         kw = dict(VARIANTS[a.which])
         terrain = kw.pop("terrain", "single_path")

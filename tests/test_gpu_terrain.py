@@ -63,3 +63,14 @@ def test_env_builds_its_tiles_on_the_gpu():
     np.testing.assert_array_equal(env.terrain.tiles.cpu().numpy(), host.tiles)
     np.testing.assert_array_equal(env.terrain.env_tile, host.env_tile)
     np.testing.assert_array_equal(env.terrain.env_origins, host.env_origins)
+
+
+def test_device_tiles_match_reference_full_grid():
+    """Against the reference's own tiles directly: the README grid (32 x 32 sub-terrains) the reference
+    built after np.random.seed(17) (tests/golden/step_full_grid.npz, one env per sub-terrain)."""
+    from tests import golden_io as G
+    d = G.load("step_full_grid.npz")
+    cfg = CF.readme_config(n_envs=1024, terrain="single_path", rows=32, cols=32)
+    dev = _device_tiles(cfg, 17).reshape(1024, 2, 80, 40)
+    env_tile = np.arange(1024) % 1024
+    np.testing.assert_array_equal(dev[env_tile], d["static/env_height_samples"])

@@ -36,3 +36,14 @@ def test_plane_grid_origins():
     td = T.build(cfg, 10)
     assert td.kind == "plane"
     np.testing.assert_array_equal(td.env_origins[:4, :2], [[0, 0], [0, 3], [0, 6], [3, 0]])
+
+
+def test_full_readme_grid_tiles_bit_exact():
+    """The README grid at full size (32 x 32 sub-terrains, fixture step_full_grid.npz: the
+    reference's Terrain built after np.random.seed(17), one env per sub-terrain)."""
+    d = G.load("step_full_grid.npz")
+    cfg = CF.readme_config(n_envs=1024, terrain="single_path", rows=32, cols=32)
+    td = T.build(cfg, 1024, np.random.RandomState(17))
+    np.testing.assert_array_equal(td.tiles[td.env_tile], d["static/env_height_samples"])
+    np.testing.assert_array_equal(td.env_terrain_origin, d["static/env_terrain_origin"])
+    np.testing.assert_array_equal(td.env_origins, d["static/env_origins"])
