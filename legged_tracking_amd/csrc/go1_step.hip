@@ -353,6 +353,17 @@ __device__ __forceinline__ void mlp_group3(const MlpFrag& F, const float* b0, co
       }
     t[g] = rowsum4(p) + F.b3;
   }
+#ifdef GO1_MLP_SGB
+  // the matrix pipe takes one v_mfma_f32_16x16x4_f32 per 32 cycles and the wave may issue ~6 VALU
+  // instructions in that gap: layer 1 first, then each layer-2 MFMA followed by softsign work
+#pragma unroll
+  for (int i = 0; i < 12; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+  for (int i = 0; i < 48; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, GO1_MLP_SGB, 0);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------- torch-order f32 math

@@ -113,37 +113,55 @@ __global__ __launch_bounds__(64) void tunnel_draw_kernel(go1_tunnel_params p, do
   const double cx = 1.0 * step + start;
   const int n_sub = p.num_rows * p.num_cols;
   for (int k = 0; k < n_sub; ++k) {
-    double r[GO1_TUNNEL_REC];
-    for (int t = 0; t < GO1_TUNNEL_REC; ++t) r[t] = 0.0;
-    r[0] = uniform(s, lane, 0.0, 1.0);  // difficulty (tunnel.py:90), unused by single_path
+    double* R = rec + (size_t)k * GO1_TUNNEL_REC;
+    const double diff = uniform(s, lane, 0.0, 1.0);  // difficulty (tunnel.py:90), unused by single_path
+    if (lane == 0) R[0] = diff;
+#pragma unroll
     for (int layer = 0; layer < 2; ++layer) {
       const bool top = layer == 0;
-      double* L = r + 1 + REC_LAYER * layer;
       const double p1 = uniform(s, lane, 0.0, 1.0), p2 = uniform(s, lane, 0.0, 1.0);
       const int num_y = p2 < p.p_double ? 2 : 1;
-      L[0] = p1; L[1] = p2; L[2] = (double)num_y;
-      // tunnel_fn.py:111-124: offsets y then x, each a (num_y, 1) draw
+      // tunnel_fn.py:111-124: offsets y then x, each a (num_y, 1) draw (register arrays, static
+      // indices: the draws are uniform branches on num_y)
       const double oy = top ? 0.6 : 0.4, ox = top ? 0.3 : 0.2;
-      for (int i = 0; i < num_y; ++i) L[3 + i] = uniform(s, lane, -oy, oy);
-      for (int i = 0; i < num_y; ++i) L[5 + i] = uniform(s, lane, -ox, ox);
+      double offy[2] = {0.0, 0.0}, offx[2] = {0.0, 0.0}, mx[2] = {0.0, 0.0}, mz[2] = {0.0, 0.0};
+      double pw[2] = {0.0, 0.0}, pl[2] = {0.0, 0.0};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        if (i < num_y) offy[i] = uniform(s, lane, -oy, oy);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        if (i < num_y) offx[i] = uniform(s, lane, -ox, ox);
       double hmax, hmin;
       if (p1 < p.p_flat) { hmax = top ? 0.4 : 0.15; hmin = top ? 0.7 : 0.3; }
       else { hmax = 0.0; hmin = 0.0; }
       const double lw_lo = top ? 0.2 : 0.1, lw_hi = top ? 0.4 : 0.3;
       // mean_x (after meshgrid) += offset_x; mean_z = uniform(mean_x) * (hmax - hmin) + hmin
       // (uniform(low=mean_x, high=1.0): range = 1.0 - mean_x, element-wise)
-      for (int i = 0; i < num_y; ++i) {
-        const double mx = cx + L[5 + i];
-        L[7 + i] = mx;
-        const double u = mx + (1.0 - mx) * mt_next_double(s, lane);
-        L[9 + i] = u * (hmax - hmin) + hmin;
-      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        if (i < num_y) {
+          mx[i] = cx + offx[i];
+          const double u = mx[i] + (1.0 - mx[i]) * mt_next_double(s, lane);
+          mz[i] = u * (hmax - hmin) + hmin;
+        }
       // pw, pl = uniform(lw_low, lw_high, size=(2, num_y)): row 0 then row 1
-      for (int i = 0; i < num_y; ++i) L[11 + i] = uniform(s, lane, lw_lo, lw_hi);
-      for (int i = 0; i < num_y; ++i) L[13 + i] = uniform(s, lane, lw_lo, lw_hi);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        if (i < num_y) pw[i] = uniform(s, lane, lw_lo, lw_hi);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        if (i < num_y) pl[i] = uniform(s, lane, lw_lo, lw_hi);
+      if (lane == 0) {
+        double* L = R + 1 + REC_LAYER * layer;
+        L[0] = p1; L[1] = p2; L[2] = (double)num_y;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          L[3 + i] = offy[i]; L[5 + i] = offx[i]; L[7 + i] = mx[i]; L[9 + i] = mz[i];
+          L[11 + i] = pw[i]; L[13 + i] = pl[i];
+        }
+      }
     }
-    if (lane == 0)
-      for (int t = 0; t < GO1_TUNNEL_REC; ++t) rec[(size_t)k * GO1_TUNNEL_REC + t] = r[t];
   }
 }
 
