@@ -353,7 +353,10 @@ __device__ __forceinline__ void mlp_group3(const MlpFrag& F, const float* b0, co
       }
     t[g] = rowsum4(p) + F.b3;
   }
-#ifdef GO1_MLP_SGB
+#ifndef GO1_MLP_SGB  // VALU instructions after each layer-2 MFMA (0: the compiler's own order)
+#define GO1_MLP_SGB 3
+#endif
+#if GO1_MLP_SGB
   // the matrix pipe takes one v_mfma_f32_16x16x4_f32 per 32 cycles and the wave may issue ~6 VALU
   // instructions in that gap: layer 1 first, then each layer-2 MFMA followed by softsign work
 #pragma unroll

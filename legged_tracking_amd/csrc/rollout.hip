@@ -250,9 +250,18 @@ __device__ __forceinline__ void policy_group(const f4_t (&w)[NL][NT], const ActV
 // are unrolled and the weight fragments run D groups ahead of the MFMAs: with three 8-cycle f16
 // MFMAs per fragment the layers are bound by the L2 -> CU weight stream, which needs ~12
 // 16-byte loads in flight per lane (64 B/clk/CU x the L2 latency, 16 waves).
+// the first D weight groups of a policy_tiles phase, issued early: they depend on nothing the
+// workgroup computes, so the adaptation module's can be in flight while the inputs are staged
 template <int NT, int NL, int G, int D>
+__device__ __forceinline__ void policy_prefetch(const PolicyLayer* L, int tile0, int tstride, int lane,
+                                                f4_t (&w)[D][NL][NT]) {
+#pragma unroll
+  for (int g = 0; g < D && g < G; ++g) policy_load<NT, NL>(L, G, g, tile0, tstride, lane, w[g]);
+}
+
+template <int NT, int NL, int G, int D, bool PREFETCHED = false>
 __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, const ActV* src, int tile0, int tstride,
-                                             const ActV* dst, bool act, int lane) {
+                                             const ActV* dst, bool act, int lane, f4_t (*pre)[NL][NT] = nullptr) {
   const int q = lane >> 4, c = lane & 15;
   f4_t acc[NL][NT], w[D][NL][NT];
 #pragma unroll
@@ -260,8 +269,16 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, const ActV* s
 #pragma unroll
     for (int i = 0; i < NT; ++i)
       acc[l][i] = *reinterpret_cast<const f4_t*>(L[l].b + 16 * (tile0 + i * tstride) + 4 * q);
+  if constexpr (PREFETCHED) {
 #pragma unroll
-  for (int g = 0; g < D && g < G; ++g) policy_load<NT, NL>(L, G, g, tile0, tstride, lane, w[g]);
+    for (int g = 0; g < D; ++g)
+#pragma unroll
+      for (int l = 0; l < NL; ++l)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) w[g][l][i] = pre[g][l][i];
+  } else {
+    policy_prefetch<NT, NL, G, D>(L, tile0, tstride, lane, w);
+  }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     policy_group<NT, NL>(w[g % D], src, g, q, c, acc);
@@ -318,6 +335,11 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   PSTAMP(0);
   const int ne = min(16, P.n_envs - e0);
   const ActV va = xa.v(), vc = xc.v();
+#ifndef GO1_POLICY_NO_EARLY
+  // the adaptation module's first weight groups are in flight while the inputs are staged
+  f4_t w_ad[8][1][1];
+  policy_prefetch<1, 1, PIN / 16, 8>(P.layers + 0, wave, PW, lane, w_ad);
+#endif
   for (int idx = tid; idx < 16 * PIN; idx += 64 * PW) {
     const int e = idx / PIN, k = idx - e * PIN;
     float v = 0.0f;
@@ -332,7 +354,11 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   const PolicyLayer* Ls = P.layers;
   const ActV vh1[2] = {h1[0].v(), h1[1].v()}, vh2[2] = {h2[0].v(), h2[1].v()};
   // adaptation module (xa rows >= hist_dim are still zero)
+#ifndef GO1_POLICY_NO_EARLY
+  policy_tiles<1, 1, PIN / 16, 8, true>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, w_ad);  // 256
+#else
   policy_tiles<1, 1, PIN / 16, 8>(Ls + 0, &va, wave, PW, &vh1[0], true, lane);  // 256
+#endif
   __syncthreads();
   PSTAMP(2);
   // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7; the upper half's partial
