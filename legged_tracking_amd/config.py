@@ -678,9 +678,12 @@ def f32(x):
     return float(np.float32(x))
 
 
-# Native physics constants (no reference counterpart: PhysX is closed)
+# Native physics constants (no reference counterpart: PhysX is closed).  One 5 ms
+# integrator step per sim step (as PhysX's substeps = 1, legged_robot_trajectory_tracking_config.py:
+# 355-356): the contacts are linearly implicit (added masses in the articulated inertias), which keeps
+# the penalty contact stable at that step (tools/implicit_contact_study.py)
 PHYSICS = dict(contact_stiffness=2.0e4, contact_damping=80.0, friction_damping=60.0,
-               limit_stiffness=2000.0, limit_damping=20.0, n_internal=2)
+               limit_stiffness=2000.0, limit_damping=20.0, n_internal=1)
 
 
 def _get(cfg, path, default=None):

@@ -439,7 +439,7 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) { return v 
 // Everything from here to the step kernel is integrator code (compared with the f64
 // oracle within a tolerance): FMA contraction on, including in the inlined helpers
 // (a pragma inside phys_substep alone does not reach them).
-#pragma clang fp contract(fast)
+#pragma clang fp contract(on)
 // Spatial vectors (angular; linear).  6x6 symmetric articulated inertia stored as
 // [[A, B], [B^T, C]], A and C symmetric (xx xy xz yy yz zz), B row-major 3x3.
 struct SI {
@@ -1134,6 +1134,53 @@ __device__ __forceinline__ void sphere_contact_pk(const Terr& T, const HQ& q, co
   F[2] = Fz.x + Fz.y;
 }
 
+// The same contact, linearly implicit in the point velocity (the integrator's scheme: one 5 ms step
+// per sim step, like PhysX's substeps = 1).  For an active layer the force at the end of the step,
+// k (depth - h vn') - d vn' (normal) and -c_t vt' (regularised friction, c_t = min(kf, mu fn / |vt|)
+// from the current state), with v' = v + h a_p, splits into an explicit force F and an added mass
+//   Mp = h (h k + d) n n^T + h c_t (I - n n^T)
+// on the point (world frame, summed over floor and ceiling; xx xy xz yy yz zz), which the caller
+// puts into the link's articulated inertia, so the ABA accelerations include the contact response.
+// oracle/go1_oracle.c sphere_contact_im is the f64 restatement.
+__device__ __forceinline__ void sphere_contact_im(const Terr& T, const HQ& q, const CP& C, const float* p,
+                                                  const float* pv, float r, float h, float* F, float* Mp) {
+  f2 hh, gx, gy;
+  hq_finish(T, q, hh, gx, gy);
+  const f2 sg = f2{1.0f, -1.0f};
+  const f2 dv = sg * (hh - p[2]) + r;  // floor: h + r - z, ceiling: z + r - h
+  f2 nx = -sg * gx, ny = -sg * gy;
+  f2 inv = nx * nx + ny * ny + 1.0f;
+  inv = f2{frsq(inv.x), frsq(inv.y)};
+  nx = nx * inv;
+  ny = ny * inv;
+  const f2 nz = sg * inv;
+  const f2 depth = dv * inv;
+  const f2 vn = pv[0] * nx + pv[1] * ny + pv[2] * nz;
+  const f2 fn0 = C.k * depth - C.d * vn;          // activation: compressive at the current state
+  const f2 fn = fn0 - (h * C.k) * vn;              // k depth - (h k + d) vn
+  const f2 vtx = pv[0] - vn * nx, vty = pv[1] - vn * ny, vtz = pv[2] - vn * nz;
+  const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
+  const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
+  const f2 vtn = vt2 * ivt;
+  const f2 cm = C.mu * fn0;
+  // c_t = min(kf, mu fn0 / |vt|); kf in the viscous limit |vt| -> 0
+  const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
+                   (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
+  const bool ax = dv.x > 0.0f && fn0.x > 0.0f, ay = dv.y > 0.0f && fn0.y > 0.0f;
+  const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
+  const f2 sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
+  const f2 Fx = fa * nx - sc * vtx, Fy = fa * ny - sc * vty, Fz = fa * nz - sc * vtz;
+  F[0] = Fx.x + Fx.y;
+  F[1] = Fy.x + Fy.y;
+  F[2] = Fz.x + Fz.y;
+  const float cn = h * (h * C.k + C.d);
+  const f2 cd = h * sc, cnd = f2{ax ? cn : 0.0f, ay ? cn : 0.0f} - cd;  // (cn - cd) on active layers
+  const f2 a = cnd * nx, b = cnd * ny, c = cnd * nz;
+  const f2 mxx = a * nx + cd, mxy = a * ny, mxz = a * nz, myy = b * ny + cd, myz = b * nz, mzz = c * nz + cd;
+  Mp[0] = mxx.x + mxx.y; Mp[1] = mxy.x + mxy.y; Mp[2] = mxz.x + mxz.y;
+  Mp[3] = myy.x + myy.y; Mp[4] = myz.x + myz.y; Mp[5] = mzz.x + mzz.y;
+}
+
 __device__ __forceinline__ void sphere_contact(const Terr& T, const CP& C, const float* p, const float* pv, float r,
                                                float* F) {
   F[0] = F[1] = F[2] = 0.0f;
@@ -1285,7 +1332,7 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau, float h,
                              const float* g, float friction, float payload, const Terr& T, int leg, int role,
                              bool cf_out, float* cf_raw) {
-#pragma clang fp contract(fast)
+#pragma clang fp contract(on)
   // Model constants are compile-time literals (go1_model_consts.h, checked against the
   // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
   // Per-leg floats are the FL values times the leg's mirror signs (loop-invariant products).
@@ -1362,116 +1409,72 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     }
   }
   MARK(leg_kin_done);
-  // ---- contacts, stage 1: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1,
-  //      foot, corner 2 leg, corner 2 leg + 1] -- world position / velocity, terrain corner reads
-  //      issued (they land during the articulated-inertia chain below)
+  // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
+  //      corner 2 leg, corner 2 leg + 1] -- world position / velocity, terrain corners, the explicit
+  //      force (body frame of the point's body) and the added mass of the implicit contact
   float fth[6] = {0, 0, 0, 0, 0, 0}, fca[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
   float Fth[3] = {0, 0, 0}, Fca[3] = {0, 0, 0}, Fft[3] = {0, 0, 0}, Fb[3] = {0, 0, 0};
+  // the contact inertias of this lane's points as one packed SIP per half (x, y = the two points):
+  // [[S M S^T, S M], [M S^T, M]] with M = Rs^T Mp Rs in the body frame, S = lp~
+  SIP cin[2];
 #ifndef GO1_ABL_NO_CONTACT
-  // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
-  // the body-frame force; x = point 2 role, y = point 2 role + 1.  Bodies:
-  // role 0 (thigh, thigh), 1 (thigh, calf), 2 (calf, foot on the calf), 3 (base, base)
-  f2 Rs[9], lp[3], rr, pw[3], vw[3];
-  HQ qa, qb;
   {
-    const bool xt = role <= 1, xc = role == 2, yt = role == 0, yc = role == 1 || role == 2;
-    f2 ps[3], vs[6];
+    // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
+    // the body-frame force; x = point 2 role, y = point 2 role + 1.  Bodies:
+    // role 0 (thigh, thigh), 1 (thigh, calf), 2 (calf, foot on the calf), 3 (base, base)
+    f2 Rs[9], lp[3], rr, pw[3], vw[3];
+    HQ qa, qb;
+    {
+      const bool xt = role <= 1, xc = role == 2, yt = role == 0, yc = role == 1 || role == 2;
+      f2 ps[3], vs[6];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) Rs[i] = f2{xt ? Rl[0][i] : (xc ? Rl[1][i] : R[i]), yt ? Rl[0][i] : (yc ? Rl[1][i] : R[i])};
+      for (int i = 0; i < 9; ++i) Rs[i] = f2{xt ? Rl[0][i] : (xc ? Rl[1][i] : R[i]), yt ? Rl[0][i] : (yc ? Rl[1][i] : R[i])};
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-      ps[i] = f2{xt ? pl[0][i] : (xc ? pl[1][i] : S.pos[i]), yt ? pl[0][i] : (yc ? pl[1][i] : S.pos[i])};
+      for (int i = 0; i < 3; ++i)
+        ps[i] = f2{xt ? pl[0][i] : (xc ? pl[1][i] : S.pos[i]), yt ? pl[0][i] : (yc ? pl[1][i] : S.pos[i])};
 #pragma unroll
-    for (int i = 0; i < 6; ++i) vs[i] = f2{xt ? vl[0][i] : (xc ? vl[1][i] : vb[i]), yt ? vl[0][i] : (yc ? vl[1][i] : vb[i])};
+      for (int i = 0; i < 6; ++i) vs[i] = f2{xt ? vl[0][i] : (xc ? vl[1][i] : vb[i]), yt ? vl[0][i] : (yc ? vl[1][i] : vb[i])};
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int p = 2 * role + h;
-      const bool on_thigh = p < 3, on_base = p >= 6;
-      const int cx = leg * 2 + (p - 6);
-      const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
-      lp[0][h] = on_base ? ((cx & 1) ? th[0] : -th[0]) : (p == 5 ? foot[0] : 0.0f);
-      lp[1][h] = on_base ? ((cx & 2) ? th[1] : -th[1]) : (p == 5 ? foot[1] : 0.0f);
-      lp[2][h] = on_base ? ((cx & 4) ? th[2] : -th[2]) : (p == 5 ? foot[2] : lz);
-      rr[h] = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
-    }
-    // point kinematics: v = R (v_lin + w x lp), p = p_body + R lp
-    const f2 wl[3] = {vs[1] * lp[2] - vs[2] * lp[1], vs[2] * lp[0] - vs[0] * lp[2], vs[0] * lp[1] - vs[1] * lp[0]};
-    const f2 vlin[3] = {vs[3] + wl[0], vs[4] + wl[1], vs[5] + wl[2]};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      pw[i] = ps[i] + Rs[3 * i] * lp[0] + Rs[3 * i + 1] * lp[1] + Rs[3 * i + 2] * lp[2];
-      vw[i] = Rs[3 * i] * vlin[0] + Rs[3 * i + 1] * vlin[1] + Rs[3 * i + 2] * vlin[2];
-    }
-    hq_fetch(T, pw[0].x, pw[1].x, qa);
-    hq_fetch(T, pw[0].y, pw[1].y, qb);
-  }
-#else  // ablation build only: no contacts
-  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
-#endif
-  MARK(leg_kin_contacts_done);
-  // ---- articulated inertias calf -> hip (they depend on q alone, not on the contact or bias
-  //      forces); the hip's goes to the base.  Kept per joint: U = column ax (pairs), 1 / D, the
-  //      joint torque with the limit spring, and Ia c_j for the bias pass.
-  f2 Up[3][3], Iac[3][3];
-  float D[3], teff[3], u[3];
-  SIP Ip;
-  {
-    SIP IA;
-    rigid_sip(LC + 20, 1.0f, IA);
-#pragma unroll
-    for (int j = 2; j >= 0; --j) {
-      const int ax = j == 0 ? 0 : 1;
-      float t = tau[j];
-      // joint-limit spring-damper, implicit in the joint: the torque at the end of the
-      // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
-      // into the joint inertia D (unconditionally stable for any k, d)
-      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
-      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
-      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
-      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
-      teff[j] = t - (lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) Up[j][i] = sip_col(IA, ax, i);
-      const float invD = frcp(IA.ac[s3i(ax, ax)].x + (lim_on ? h * dl + h * h * kl : 0.0f));
-      D[j] = invD;  // the passes only need 1 / D
-      f2 V[3];  // U / D
-#pragma unroll
-      for (int i = 0; i < 3; ++i) V[i] = Up[j][i] * invD;
-      SIP Ia;  // IA - U U^T / D: the A and C blocks as pairs, B scalar
-      const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
-#pragma unroll
-      for (int k = 0; k < 6; ++k) Ia.ac[k] = IA.ac[k] - Up[j][II[k]] * V[JJ[k]];
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Up[j][a].x * V[b].y;
-      sip_mul_sparse(Ia, cjp[j], ax, Iac[j]);
-      SIP It;
-      xform_inertia2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
-      if (j > 0) {
-        rigid_sip(LC + 10 * (j - 1), 1.0f, IA);
-        sip_add(IA, It);
-      } else {
-        Ip = It;
+      for (int hh = 0; hh < 2; ++hh) {
+        const int p = 2 * role + hh;
+        const bool on_thigh = p < 3, on_base = p >= 6;
+        const int cx = leg * 2 + (p - 6);
+        const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
+        lp[0][hh] = on_base ? ((cx & 1) ? th[0] : -th[0]) : (p == 5 ? foot[0] : 0.0f);
+        lp[1][hh] = on_base ? ((cx & 2) ? th[1] : -th[1]) : (p == 5 ? foot[1] : 0.0f);
+        lp[2][hh] = on_base ? ((cx & 4) ? th[2] : -th[2]) : (p == 5 ? foot[2] : lz);
+        rr[hh] = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
       }
+      // point kinematics: v = R (v_lin + w x lp), p = p_body + R lp
+      const f2 wl[3] = {vs[1] * lp[2] - vs[2] * lp[1], vs[2] * lp[0] - vs[0] * lp[2], vs[0] * lp[1] - vs[1] * lp[0]};
+      const f2 vlin[3] = {vs[3] + wl[0], vs[4] + wl[1], vs[5] + wl[2]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pw[i] = ps[i] + Rs[3 * i] * lp[0] + Rs[3 * i + 1] * lp[1] + Rs[3 * i + 2] * lp[2];
+        vw[i] = Rs[3 * i] * vlin[0] + Rs[3 * i + 1] * vlin[1] + Rs[3 * i + 2] * vlin[2];
+      }
+      hq_fetch(T, pw[0].x, pw[1].x, qa);
+      hq_fetch(T, pw[0].y, pw[1].y, qb);
     }
-  }
-  // ---- contacts, stage 2: forces from the landed corners; forces in the body frame of the
-  //      point's body
-#ifndef GO1_ABL_NO_CONTACT
-  {
-    float Fa[3], Fb2[3];
+    float Fa[3], Fb2[3], Ma[6], Mb[6];
     {
       const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
       const float pb[3] = {pw[0].y, pw[1].y, pw[2].y}, vb2[3] = {vw[0].y, vw[1].y, vw[2].y};
-      sphere_contact_pk(T, qa, C, pa, va, rr.x, Fa);
-      sphere_contact_pk(T, qb, C, pb, vb2, rr.y, Fb2);
+      sphere_contact_im(T, qa, C, pa, va, rr.x, h, Fa, Ma);
+      sphere_contact_im(T, qb, C, pb, vb2, rr.y, h, Fb2, Mb);
     }
     const f2 F[3] = {f2{Fa[0], Fb2[0]}, f2{Fa[1], Fb2[1]}, f2{Fa[2], Fb2[2]}};
-    // body-frame force f = R^T F and moment lp x f
+    // the ABA below solves for accelerations relative to free fall (gravity as a base
+    // acceleration), so the added mass would respond to a - g: the force it sees is F - Mp g
+    f2 Fd[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      Fd[i] = F[i] - (f2{Ma[s3i(i, 0)], Mb[s3i(i, 0)]} * g[0] + f2{Ma[s3i(i, 1)], Mb[s3i(i, 1)]} * g[1] +
+                      f2{Ma[s3i(i, 2)], Mb[s3i(i, 2)]} * g[2]);
+    // body-frame force f = R^T Fd and moment lp x f
     f2 f6[6];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) f6[3 + j] = Rs[j] * F[0] + Rs[3 + j] * F[1] + Rs[6 + j] * F[2];
+    for (int j = 0; j < 3; ++j) f6[3 + j] = Rs[j] * Fd[0] + Rs[3 + j] * Fd[1] + Rs[6 + j] * Fd[2];
     f6[0] = lp[1] * f6[5] - lp[2] * f6[4];
     f6[1] = lp[2] * f6[3] - lp[0] * f6[5];
     f6[2] = lp[0] * f6[4] - lp[1] * f6[3];
@@ -1490,13 +1493,70 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       Fft[i] = role == 2 ? F[i].y : 0.0f;
       Fb[i] = role == 3 ? tot : 0.0f;
     }
+    // added masses into the body frame, M = Rs^T Mp Rs (both points as halves), then about the
+    // body origin: A = S M S^T, B = S M, C = M, S = lp~ (S v = lp x v)
+    const f2 Mw[6] = {f2{Ma[0], Mb[0]}, f2{Ma[1], Mb[1]}, f2{Ma[2], Mb[2]},
+                      f2{Ma[3], Mb[3]}, f2{Ma[4], Mb[4]}, f2{Ma[5], Mb[5]}};
+    f2 MR[9];  // Mp Rs (3 x 3, row-major)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        MR[3 * i + j] = Mw[s3i(i, 0)] * Rs[j] + Mw[s3i(i, 1)] * Rs[3 + j] + Mw[s3i(i, 2)] * Rs[6 + j];
+    f2 M[9];  // Rs^T (Mp Rs), symmetric
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = i; j < 3; ++j) {
+        M[3 * i + j] = Rs[i] * MR[j] + Rs[3 + i] * MR[3 + j] + Rs[6 + i] * MR[6 + j];
+        M[3 * j + i] = M[3 * i + j];
+      }
+    f2 SM[9];  // lp~ M: row i = lp x (column of M) components
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      SM[j] = lp[1] * M[6 + j] - lp[2] * M[3 + j];
+      SM[3 + j] = lp[2] * M[j] - lp[0] * M[6 + j];
+      SM[6 + j] = lp[0] * M[3 + j] - lp[1] * M[j];
+    }
+    // (S M) S^T: element (i, j) = (S M)_i . S_j row, S_j row = (lp x e)_j -> -(row i of SM) x lp
+    const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int i = II[k], j = JJ[k];
+      const f2* r = SM + 3 * i;
+      // (S M S^T)_ij = sum_l (SM)_il S_jl, S_j = (0, -lz, ly), (lz, 0, -lx), (-ly, lx, 0)
+      const f2 a = j == 0 ? r[2] * lp[1] - r[1] * lp[2] : (j == 1 ? r[0] * lp[2] - r[2] * lp[0] : r[1] * lp[0] - r[0] * lp[1]);
+      cin[0].ac[k][0] = a.x; cin[1].ac[k][0] = a.y;
+      cin[0].ac[k][1] = M[3 * i + j].x; cin[1].ac[k][1] = M[3 * i + j].y;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { cin[0].b[i] = SM[i].x; cin[1].b[i] = SM[i].y; }
+  }
+#else  // ablation build only: no contacts
+  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) cin[k].ac[t] = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cin[k].b[i] = 0.0f;
   }
 #endif
+  // the lane's contributions per body (thigh, calf, base), then summed over the leg's roles
+  SIP ci_th, ci_ca, ci_bs;
   {
-    float red[18];
+    float red[18 + 63];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { red[i] = fth[i]; red[6 + i] = fca[i]; red[12 + i] = fbase[i]; }
-    rowsum4_n<18>(red);
+#pragma unroll
+    for (int k = 0; k < 21; ++k) {
+      const float x = k < 12 ? cin[0].ac[k >> 1][k & 1] : cin[0].b[k - 12];
+      const float y = k < 12 ? cin[1].ac[k >> 1][k & 1] : cin[1].b[k - 12];
+      red[18 + k] = role == 0 ? x + y : (role == 1 ? x : 0.0f);        // thigh
+      red[39 + k] = role == 2 ? x + y : (role == 1 ? y : 0.0f);        // calf
+      red[60 + k] = role == 3 ? x + y : 0.0f;                          // base (this leg's corners)
+    }
+    rowsum4_n<18 + 63>(red);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       pAp[1][i] -= f2{red[i], red[3 + i]};
@@ -1504,24 +1564,75 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i) fbase[i] = red[12 + i];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      ci_th.ac[k] = f2{red[18 + 2 * k], red[18 + 2 * k + 1]};
+      ci_ca.ac[k] = f2{red[39 + 2 * k], red[39 + 2 * k + 1]};
+      ci_bs.ac[k] = f2{red[60 + 2 * k], red[60 + 2 * k + 1]};
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { ci_th.b[i] = red[30 + i]; ci_ca.b[i] = red[51 + i]; ci_bs.b[i] = red[72 + i]; }
   }
-  // ---- bias forces calf -> hip (the contact forces are in pA now)
+  MARK(leg_kin_contacts_done);
+  // ---- backward pass calf -> hip (articulated inertias with the contact added masses, bias
+  //      forces with the explicit contact forces); the hip's inertia goes to the base
+  f2 Up[3][3];  // U = column ax of the articulated inertia, (angular, linear) pairs
+  float D[3], u[3];
+  SIP Ip;
   f2 pp6[3];
+  {
+    SIP IA;
+    rigid_sip(LC + 20, 1.0f, IA);
+    sip_add(IA, ci_ca);
 #pragma unroll
-  for (int j = 2; j >= 0; --j) {
-    const int ax = j == 0 ? 0 : 1;
-    u[j] = teff[j] - pAp[j][ax].x;
-    const float ud = u[j] * D[j];
-    f2 pa[3], pt[3];
+    for (int j = 2; j >= 0; --j) {
+      const int ax = j == 0 ? 0 : 1;
+      float t = tau[j];
+      // joint-limit spring-damper, implicit in the joint: the torque at the end of the
+      // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
+      // into the joint inertia D (unconditionally stable for any k, d)
+      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
+      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
+      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
+      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
+      t -= lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) pa[i] = pAp[j][i] + Iac[j][i] + Up[j][i] * ud;
-    xfT2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
-    if (j > 0) {
+      for (int i = 0; i < 3; ++i) Up[j][i] = sip_col(IA, ax, i);
+      D[j] = IA.ac[s3i(ax, ax)].x + (lim_on ? h * dl + h * h * kl : 0.0f);
+      u[j] = t - pAp[j][ax].x;
+      const float invD = frcp(D[j]);
+      D[j] = invD;  // the forward pass only needs 1 / D
+      f2 V[3];  // U / D
 #pragma unroll
-      for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
-    } else {
+      for (int i = 0; i < 3; ++i) V[i] = Up[j][i] * invD;
+      SIP Ia;  // IA - U U^T / D: the A and C blocks as pairs, B scalar
+      const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
-      for (int i = 0; i < 3; ++i) pp6[i] = pt[i];
+      for (int k = 0; k < 6; ++k) Ia.ac[k] = IA.ac[k] - Up[j][II[k]] * V[JJ[k]];
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Up[j][a].x * V[b].y;
+      f2 Iac[3], pa[3], pt[3];
+      sip_mul_sparse(Ia, cjp[j], ax, Iac);
+      const float ud = u[j] * invD;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pa[i] = pAp[j][i] + Iac[i] + Up[j][i] * ud;
+      SIP It;
+      xform_inertia2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
+      xfT2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
+      if (j > 0) {
+        rigid_sip(LC + 10 * (j - 1), 1.0f, IA);
+        sip_add(IA, It);
+        if (j == 2) sip_add(IA, ci_th);  // the thigh's contact added masses
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
+      } else {
+        Ip = It;
+        sip_add(Ip, ci_bs);  // this leg's trunk corners: summed over the legs with the hips below
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pp6[i] = pt[i];
+      }
     }
   }
   MARK(backward_done);

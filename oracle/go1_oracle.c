@@ -403,6 +403,85 @@ typedef struct {
   real k, d, kf, mu;
 } ContactParams;
 
+/* The integrator's contact scheme (go1_step.hip sphere_contact_im): contact forces linearly
+ * implicit in the point velocity, so the integrator stays stable at one 5 ms step per sim step
+ * (go1o_set_implicit_contact(0) restores the explicit penalty forces of round 1 for
+ * tools/implicit_contact_study.py).  For an active layer with depth d0 and normal velocity vn, the normal force at the
+ * end of the step, k (d0 - h vn') - d vn' with vn' = vn + h n.a_p, splits into an explicit part
+ * k d0 - (h k + d) vn and an added mass h (h k + d) n n^T on the point; the regularised friction
+ * -c_t vt' (c_t = min(kf, mu fn / |vt|) from the current state) adds h c_t (I - n n^T).  The added
+ * masses enter the links' articulated inertias (point_inertia), so the ABA solves for the
+ * accelerations that already include the contact response. */
+static int g_implicit_contact = 1;
+void go1o_set_implicit_contact(int on) { g_implicit_contact = on; }
+
+/* penalty contact of a sphere (centre p, velocity pv, radius r) against floor and
+ * ceiling; returns world force F (and, implicit option, adds the point's added mass to Mp) */
+static void sphere_contact_im(const TerrainView* T, const ContactParams* C, const real* p, const real* pv, real r,
+                              real* F, real h, real Mp[3][3]) {
+  F[0] = F[1] = F[2] = 0.0;
+  for (int layer = 1; layer >= 0; --layer) {
+    real hh, gx, gy;
+    height_query(T, layer, p[0], p[1], &hh, &gx, &gy);
+    real n[3], dv;
+    if (layer == 1) {
+      dv = hh + r - p[2];
+      n[0] = -gx; n[1] = -gy; n[2] = 1.0;
+    } else {
+      dv = p[2] + r - hh;
+      n[0] = gx; n[1] = gy; n[2] = -1.0;
+    }
+    if (dv <= 0.0) continue;
+    real inv = 1.0 / sqrt(n[0] * n[0] + n[1] * n[1] + 1.0);
+    for (int i = 0; i < 3; ++i) n[i] *= inv;
+    real depth = dv * inv;
+    real vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
+    real fn0 = C->k * depth - C->d * vn;
+    if (fn0 <= 0.0) continue;
+    real fn = C->k * depth - (h * C->k + C->d) * vn;
+    real vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
+    real vtn = sqrt(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
+    real ct = C->kf;
+    if (vtn > 1e-9 && C->mu * fn0 < ct * vtn) ct = C->mu * fn0 / vtn;
+    real cn = h * (h * C->k + C->d), cd = h * ct;
+    for (int i = 0; i < 3; ++i) {
+      F[i] += fn * n[i] - ct * vt[i];
+      for (int j = 0; j < 3; ++j) Mp[i][j] += (cn - cd) * n[i] * n[j] + (i == j ? cd : 0.0);
+    }
+  }
+}
+
+/* the added mass Mp (world, at local point lp of a link with rotation Rb) as a spatial inertia
+ * about the link origin: [[lp~ M lp~^T, lp~ M], [M lp~^T, M]], M = Rb^T Mp Rb */
+static void point_inertia(real Rb[3][3], const real* lp, real Mp[3][3], M6* I) {
+  real M[3][3], S[3][3], SM[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      real a = 0;
+      for (int k = 0; k < 3; ++k)
+        for (int l = 0; l < 3; ++l) a += Rb[k][i] * Mp[k][l] * Rb[l][j];
+      M[i][j] = a;
+    }
+  S[0][0] = 0; S[0][1] = -lp[2]; S[0][2] = lp[1];
+  S[1][0] = lp[2]; S[1][1] = 0; S[1][2] = -lp[0];
+  S[2][0] = -lp[1]; S[2][1] = lp[0]; S[2][2] = 0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      real a = 0;
+      for (int k = 0; k < 3; ++k) a += S[i][k] * M[k][j];
+      SM[i][j] = a;
+    }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      real a = 0;
+      for (int k = 0; k < 3; ++k) a += SM[i][k] * S[j][k];  /* (S M) S^T */
+      I->m[i][j] += a;
+      I->m[i][3 + j] += SM[i][j];
+      I->m[3 + j][i] += SM[i][j];
+      I->m[3 + i][3 + j] += M[i][j];
+    }
+}
+
 /* penalty contact of a sphere (centre p, velocity pv, radius r) against floor and
  * ceiling; returns world force F */
 static void sphere_contact(const TerrainView* T, const ContactParams* C, const real* p, const real* pv, real r,
@@ -505,7 +584,13 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
                       (cx & 4) ? M->trunk_half[2] : -M->trunk_half[2]};
       real pw[3], vw[3], F[3];
       point_kin(R, S->pos, vb, lp, pw, vw);
-      sphere_contact(T, &C, pw, vw, 0.0, F);
+      if (g_implicit_contact) {
+        real Mp[3][3] = {{0}};
+        sphere_contact_im(T, &C, pw, vw, 0.0, F, h, Mp);
+        point_inertia(R, lp, Mp, &IA0);
+      } else {
+        sphere_contact(T, &C, pw, vw, 0.0, F);
+      }
       point_force(R, lp, F, fext);
       if (cf) for (int i = 0; i < 3; ++i) cf[i] += F[i];
     }
@@ -561,7 +646,13 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
         for (int p = 0; p < N_THIGH_PTS; ++p) {
           real lp[3] = {0, 0, THIGH_PTS_Z[p]}, pw[3], vw[3], F[3];
           point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
-          sphere_contact(T, &C, pw, vw, M->thigh_r, F);
+          if (g_implicit_contact) {
+            real Mp[3][3] = {{0}};
+            sphere_contact_im(T, &C, pw, vw, M->thigh_r, F, h, Mp);
+            point_inertia(Rw[j], lp, Mp, &IA[j]);
+          } else {
+            sphere_contact(T, &C, pw, vw, M->thigh_r, F);
+          }
           point_force(Rw[j], lp, F, fext);
           if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
         }
@@ -572,7 +663,13 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
           else { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
           real pw[3], vw[3], F[3];
           point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
-          sphere_contact(T, &C, pw, vw, r, F);
+          if (g_implicit_contact) {
+            real Mp[3][3] = {{0}};
+            sphere_contact_im(T, &C, pw, vw, r, F, h, Mp);
+            point_inertia(Rw[j], lp, Mp, &IA[j]);
+          } else {
+            sphere_contact(T, &C, pw, vw, r, F);
+          }
           point_force(Rw[j], lp, F, fext);
           int bi = p < N_CALF_PTS ? body_idx : body_idx + 1; /* foot body reported separately */
           if (cf) for (int i = 0; i < 3; ++i) cf[bi * 3 + i] += F[i];
@@ -1310,3 +1407,13 @@ int go1o_step(const go1_config* c, const go1_state* st, const go1_terrain* ter, 
 }
 
 int go1o_abi_version(void) { return GO1_ABI_VERSION; }
+
+/* test export (tests/test_oracle_contact.py): the spatial inertia of an added point mass */
+void go1o_point_inertia(const double* Rb9, const double* lp9, const double* Mp9, double* out36) {
+  real Rb[3][3], Mp[3][3], lp[3] = {(real)lp9[0], (real)lp9[1], (real)lp9[2]};
+  M6 I;
+  memset(&I, 0, sizeof(I));
+  for (int i = 0; i < 9; ++i) { Rb[i / 3][i % 3] = (real)Rb9[i]; Mp[i / 3][i % 3] = (real)Mp9[i]; }
+  point_inertia(Rb, lp, Mp, &I);
+  for (int i = 0; i < 36; ++i) out36[i] = I.m[i / 6][i % 6];
+}
