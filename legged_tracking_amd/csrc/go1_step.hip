@@ -214,6 +214,39 @@ __device__ __forceinline__ void rowsum4_n(float* v) {
 #endif
 }
 
+// N values that two bodies split between the row pairs (body L on rows 0-1, body H on rows 2-3):
+// the permlane16 stage sums each pair, then one permlane32 swap hands every lane both results --
+// its two outputs are the low-half value (rows 0-1) and the high-half value (rows 2-3) on every
+// lane.  Three VALU per value where two full row sums cost eight.
+template <int N>
+__device__ __forceinline__ void pairsum_rows_n(const float* v, float* lo, float* hi) {
+#if GO1_DPP
+  float a[N], b[N], s[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+    a[i] = __uint_as_float(r[0]);
+    b[i] = __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) s[i] = a[i] + b[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[i]), __float_as_uint(s[i]), false, false);
+    lo[i] = __uint_as_float(r[0]);
+    hi[i] = __uint_as_float(r[1]);
+  }
+#else
+  const bool low = (threadIdx.x & 63) < 32;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float t = v[i] + __shfl_xor(v[i], 16), o = __shfl_xor(t, 32);
+    lo[i] = low ? t : o;
+    hi[i] = low ? o : t;
+  }
+#endif
+}
+
 // ---------------------------------------------------------------- actuator net
 // eval_actuator_network (:1311-1320) on the matrix cores.  One "group" = 16
 // (env, joint) items; each item is carried by the 4 lanes {i, 16+i, 32+i, 48+i}
@@ -1412,31 +1445,37 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
   //      corner 2 leg, corner 2 leg + 1] -- world position / velocity, terrain corners, the explicit
   //      force (body frame of the point's body) and the added mass of the implicit contact
-  float fth[6] = {0, 0, 0, 0, 0, 0}, fca[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
-  float Fth[3] = {0, 0, 0}, Fca[3] = {0, 0, 0}, Fft[3] = {0, 0, 0}, Fb[3] = {0, 0, 0};
+  // per lane: the leg's (thigh | calf) share in the row pair of its body and the trunk corner's share
+  float fleg[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
+  f2 Fpt[3] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};  // world forces of the lane's two points
+  const bool even = (role & 1) == 0;
   // the contact inertias of this lane's points as one packed SIP per half (x, y = the two points):
   // [[S M S^T, S M], [M S^T, M]] with M = Rs^T Mp Rs in the body frame, S = lp~
   SIP cin[2];
 #ifndef GO1_ABL_NO_CONTACT
   {
     // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
-    // the body-frame force; x = point 2 role, y = point 2 role + 1.  Bodies:
-    // role 0 (thigh, thigh), 1 (thigh, calf), 2 (calf, foot on the calf), 3 (base, base)
+    // the body-frame force.  Points p: thigh 0-2, calf 3-4, foot 5 (on the calf), trunk corners
+    // 6-7 (2 leg, 2 leg + 1).  Rows (roles): 0 (thigh0, thigh1), 1 (thigh2, corner 6),
+    // 2 (calf0, calf1), 3 (foot, corner 7) -- x halves and the even rows' y halves belong to the
+    // thigh on rows 0-1 and to the calf on rows 2-3 (one pair reduction, pairsum_rows_n), the odd
+    // rows' y halves to the trunk
     f2 Rs[9], lp[3], rr, pw[3], vw[3];
     HQ qa, qb;
     {
-      const bool xt = role <= 1, xc = role == 2, yt = role == 0, yc = role == 1 || role == 2;
+      const bool lo_rows = role <= 1;  // x: thigh on rows 0-1, calf on rows 2-3; y: thigh, base, calf, base
       f2 ps[3], vs[6];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) Rs[i] = f2{xt ? Rl[0][i] : (xc ? Rl[1][i] : R[i]), yt ? Rl[0][i] : (yc ? Rl[1][i] : R[i])};
+      for (int i = 0; i < 9; ++i)
+        Rs[i] = f2{lo_rows ? Rl[0][i] : Rl[1][i], even ? (lo_rows ? Rl[0][i] : Rl[1][i]) : R[i]};
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-        ps[i] = f2{xt ? pl[0][i] : (xc ? pl[1][i] : S.pos[i]), yt ? pl[0][i] : (yc ? pl[1][i] : S.pos[i])};
+      for (int i = 0; i < 3; ++i) ps[i] = f2{lo_rows ? pl[0][i] : pl[1][i], even ? (lo_rows ? pl[0][i] : pl[1][i]) : S.pos[i]};
 #pragma unroll
-      for (int i = 0; i < 6; ++i) vs[i] = f2{xt ? vl[0][i] : (xc ? vl[1][i] : vb[i]), yt ? vl[0][i] : (yc ? vl[1][i] : vb[i])};
+      for (int i = 0; i < 6; ++i) vs[i] = f2{lo_rows ? vl[0][i] : vl[1][i], even ? (lo_rows ? vl[0][i] : vl[1][i]) : vb[i]};
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
-        const int p = 2 * role + hh;
+        const int p = hh == 0 ? (role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5)))
+                              : (role == 0 ? 1 : (role == 1 ? 6 : (role == 2 ? 4 : 7)));
         const bool on_thigh = p < 3, on_base = p >= 6;
         const int cx = leg * 2 + (p - 6);
         const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
@@ -1480,19 +1519,11 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     f6[2] = lp[0] * f6[4] - lp[1] * f6[3];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      const float tot = f6[i].x + f6[i].y;
-      fth[i] = role == 0 ? tot : (role == 1 ? f6[i].x : 0.0f);
-      fca[i] = role == 2 ? tot : (role == 1 ? f6[i].y : 0.0f);
-      fbase[i] = role == 3 ? tot : 0.0f;
+      fleg[i] = f6[i].x + (even ? f6[i].y : 0.0f);
+      fbase[i] = even ? 0.0f : f6[i].y;
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float tot = F[i].x + F[i].y;
-      Fth[i] = role == 0 ? tot : (role == 1 ? F[i].x : 0.0f);
-      Fca[i] = role == 1 ? F[i].y : (role == 2 ? F[i].x : 0.0f);
-      Fft[i] = role == 2 ? F[i].y : 0.0f;
-      Fb[i] = role == 3 ? tot : 0.0f;
-    }
+    for (int i = 0; i < 3; ++i) Fpt[i] = F[i];
     // added masses into the body frame, M = Rs^T Mp Rs (both points as halves), then about the
     // body origin: A = S M S^T, B = S M, C = M, S = lp~ (S v = lp x v)
     const f2 Mw[6] = {f2{Ma[0], Mb[0]}, f2{Ma[1], Mb[1]}, f2{Ma[2], Mb[2]},
@@ -1545,33 +1576,33 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   // the lane's contributions per body (thigh, calf, base), then summed over the leg's roles
   SIP ci_th, ci_ca, ci_bs;
   {
-    float red[18 + 63];
+    float lg[6 + 21], bs[6 + 21], th6[6 + 21], ca6[6 + 21];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) { red[i] = fth[i]; red[6 + i] = fca[i]; red[12 + i] = fbase[i]; }
+    for (int i = 0; i < 6; ++i) { lg[i] = fleg[i]; bs[i] = fbase[i]; }
 #pragma unroll
     for (int k = 0; k < 21; ++k) {
       const float x = k < 12 ? cin[0].ac[k >> 1][k & 1] : cin[0].b[k - 12];
       const float y = k < 12 ? cin[1].ac[k >> 1][k & 1] : cin[1].b[k - 12];
-      red[18 + k] = role == 0 ? x + y : (role == 1 ? x : 0.0f);        // thigh
-      red[39 + k] = role == 2 ? x + y : (role == 1 ? y : 0.0f);        // calf
-      red[60 + k] = role == 3 ? x + y : 0.0f;                          // base (this leg's corners)
+      lg[6 + k] = x + (even ? y : 0.0f);  // thigh on rows 0-1, calf on rows 2-3
+      bs[6 + k] = even ? 0.0f : y;        // this leg's trunk corners
     }
-    rowsum4_n<18 + 63>(red);
+    pairsum_rows_n<6 + 21>(lg, th6, ca6);
+    rowsum4_n<6 + 21>(bs);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      pAp[1][i] -= f2{red[i], red[3 + i]};
-      pAp[2][i] -= f2{red[6 + i], red[9 + i]};
+      pAp[1][i] -= f2{th6[i], th6[3 + i]};
+      pAp[2][i] -= f2{ca6[i], ca6[3 + i]};
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) fbase[i] = red[12 + i];
+    for (int i = 0; i < 6; ++i) fbase[i] = bs[i];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      ci_th.ac[k] = f2{red[18 + 2 * k], red[18 + 2 * k + 1]};
-      ci_ca.ac[k] = f2{red[39 + 2 * k], red[39 + 2 * k + 1]};
-      ci_bs.ac[k] = f2{red[60 + 2 * k], red[60 + 2 * k + 1]};
+      ci_th.ac[k] = f2{th6[6 + 2 * k], th6[6 + 2 * k + 1]};
+      ci_ca.ac[k] = f2{ca6[6 + 2 * k], ca6[6 + 2 * k + 1]};
+      ci_bs.ac[k] = f2{bs[6 + 2 * k], bs[6 + 2 * k + 1]};
     }
 #pragma unroll
-    for (int i = 0; i < 9; ++i) { ci_th.b[i] = red[30 + i]; ci_ca.b[i] = red[51 + i]; ci_bs.b[i] = red[72 + i]; }
+    for (int i = 0; i < 9; ++i) { ci_th.b[i] = th6[18 + i]; ci_ca.b[i] = ca6[18 + i]; ci_bs.b[i] = bs[18 + i]; }
   }
   MARK(leg_kin_contacts_done);
   // ---- backward pass calf -> hip (articulated inertias with the contact added masses, bias
@@ -1726,21 +1757,30 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
   (void)cf_out;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    cf_raw[i] = Fth[i];
-    cf_raw[3 + i] = Fca[i];
-    cf_raw[6 + i] = Fft[i];
-    cf_raw[9 + i] = Fb[i];
+    cf_raw[i] = Fpt[i].x;
+    cf_raw[3 + i] = Fpt[i].y;
   }
 }
 
 // reported contact forces from the last sub-step's per-lane values: thigh, calf, foot of
 // the lane's leg (role sums) and the base (role and leg sums)
-__device__ __forceinline__ void cf_sum(float* cf_raw, float* cf_leg, float* cf_base) {
-  rowsum4_n<12>(cf_raw);
+__device__ __forceinline__ void cf_sum(const float* cf_raw, int role, float* cf_leg, float* cf_base) {
+  // cf_raw: world forces of the lane's two points (x, y); rows 0 (thigh, thigh), 1 (thigh, corner),
+  // 2 (calf, calf), 3 (foot, corner)
+  float v[12];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) cf_leg[i] = cf_raw[i];
+  for (int i = 0; i < 3; ++i) {
+    const float x = cf_raw[i], y = cf_raw[3 + i];
+    v[i] = role == 0 ? x + y : (role == 1 ? x : 0.0f);  // thigh
+    v[3 + i] = role == 2 ? x + y : 0.0f;                 // calf
+    v[6 + i] = role == 3 ? x : 0.0f;                     // foot
+    v[9 + i] = (role & 1) ? y : 0.0f;                    // trunk corners
+  }
+  rowsum4_n<12>(v);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) cf_base[i] = qsum(cf_raw[9 + i]);
+  for (int i = 0; i < 9; ++i) cf_leg[i] = v[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) cf_base[i] = qsum(v[9 + i]);
 }
 
 #pragma clang fp contract(off)
@@ -2075,7 +2115,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // (:973), so sub-step s reads the slot s+1 of the incoming ring and the ring
   // leaves the step as [old4, old5, old6, scaled x 4].
   float torque[3], tgt[3];
-  float cf_raw[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
+  float cf_raw[6] = {0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
   const int dec = c->decimation;
   for (int sub = 0; sub < dec; ++sub) {
     // _compute_torques (:957-996): inputs of this lane's three joints ...
@@ -2154,7 +2194,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }
     }
   }
-  cf_sum(cf_raw, cf_leg, cf_base);
+  cf_sum(cf_raw, role, cf_leg, cf_base);
   float root[13];
   if (INJ) {
 #pragma unroll
