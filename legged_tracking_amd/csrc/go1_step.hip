@@ -69,6 +69,9 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #ifndef GO1_GLDS  // LDS-DMA staging of the model block and terrain patches
 #define GO1_GLDS 1
 #endif
+#ifndef GO1_MLP_IN_SUB  // the actuator net inside the first integrator step of a sub-step (phys_substep);
+#define GO1_MLP_IN_SUB 0  // measured 47.8 against 47.7 us ahead of it: off
+#endif
 #ifndef GO1_MLP3  // the three MLP groups of a sub-step layer by layer (mlp_group3)
 #define GO1_MLP3 1
 #endif
@@ -1362,9 +1365,13 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
 // in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
-__device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau, float h,
-                             const float* g, float friction, float payload, const Terr& T, int leg, int role,
-                             bool cf_out, float* cf_raw) {
+// WITH_TQ: the sub-step also runs the actuator net (tq_fn, which writes tau): it is called right
+// after the terrain reads are issued -- the torques are first needed by the bias pass -- so its
+// MFMA chain shares one scheduling region with the contact work (GO1_MLP_IN_SUB).
+template <bool WITH_TQ, class TqFn>
+__device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
+                                             float h, const float* g, float friction, float payload, const Terr& T,
+                                             int leg, int role, bool cf_out, float* cf_raw, TqFn&& tq_fn) {
 #pragma clang fp contract(on)
   // Model constants are compile-time literals (go1_model_consts.h, checked against the
   // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
@@ -1495,6 +1502,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
       hq_fetch(T, pw[0].x, pw[1].x, qa);
       hq_fetch(T, pw[0].y, pw[1].y, qb);
     }
+    if constexpr (WITH_TQ) tq_fn();
     float Fa[3], Fb2[3], Ma[6], Mb[6];
     {
       const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
@@ -1564,6 +1572,7 @@ __device__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, 
     for (int i = 0; i < 9; ++i) { cin[0].b[i] = SM[i].x; cin[1].b[i] = SM[i].y; }
   }
 #else  // ablation build only: no contacts
+  if constexpr (WITH_TQ) tq_fn();
   (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -2118,58 +2127,61 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float cf_raw[6] = {0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
   const int dec = c->decimation;
   for (int sub = 0; sub < dec; ++sub) {
-    // _compute_torques (:957-996): inputs of this lane's three joints ...
-    const int slot = sub + 1;
-    float xin[3][6];
+    // _compute_torques (:957-996) as one closure: the actuator net runs inside the first
+    // integrator step of the sub-step (GO1_MLP_IN_SUB) or ahead of it
+    auto actuator = [&]() {
+      // inputs of this lane's three joints ...
+      const int slot = sub + 1;
+      float xin[3][6];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int d = leg * 3 + j;
-      float lg = scaled[j];  // slot is wave-uniform: scalar-condition selects, no load in the loop
+      for (int j = 0; j < 3; ++j) {
+        float lg = scaled[j];  // slot is wave-uniform: scalar-condition selects, no load in the loop
 #pragma unroll
-      for (int sl = GO1_LAG_SLOTS - 2; sl >= 0; --sl) lg = slot == sl + 1 ? lag_pre[sl][j] : lg;
-      tgt[j] = lg + dflt[j];
-      const float err = q[j] - tgt[j] + offset[j];
-      xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
-      xin[j][3] = qd[j]; xin[j][4] = vh[0][j]; xin[j][5] = vh[1][j];
-    }
-    // ... -> 3 MFMA groups per wave: group j holds joint j of the 16 (env, leg) items
-    // of the wave in column 4 env + leg; row (= role) q supplies inputs q and 4 + q of
-    // its own leg and receives the item's torque in place.
-    MARK(mlp_begin);
-    float tq[3] = {0.0f, 0.0f, 0.0f};
-    float b0[3], b1v[3];
+        for (int sl = GO1_LAG_SLOTS - 2; sl >= 0; --sl) lg = slot == sl + 1 ? lag_pre[sl][j] : lg;
+        tgt[j] = lg + dflt[j];
+        const float err = q[j] - tgt[j] + offset[j];
+        xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
+        xin[j][3] = qd[j]; xin[j][4] = vh[0][j]; xin[j][5] = vh[1][j];
+      }
+      // ... -> 3 MFMA groups per wave: group j holds joint j of the 16 (env, leg) items
+      // of the wave in column 4 env + leg; row (= role) q supplies inputs q and 4 + q of
+      // its own leg and receives the item's torque in place.
+      MARK(mlp_begin);
+      float tq[3] = {0.0f, 0.0f, 0.0f};
+      float b0[3], b1v[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const float* y = xin[j];
-      b0[j] = sel4(lq, y[0], y[1], y[2], y[3]);
-      b1v[j] = sel4(lq, y[4], y[5], 0.0f, 0.0f);
-    }
+      for (int j = 0; j < 3; ++j) {
+        const float* y = xin[j];
+        b0[j] = sel4(lq, y[0], y[1], y[2], y[3]);
+        b1v[j] = sel4(lq, y[4], y[5], 0.0f, 0.0f);
+      }
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
-    for (int j = 0; j < 3; ++j) tq[j] = 0.0f * (b0[j] + b1v[j]);  // ablation build only: no actuator net
+      for (int j = 0; j < 3; ++j) tq[j] = 0.0f * (b0[j] + b1v[j]);  // ablation build only: no actuator net
 #elif GO1_MLP3
-    mlp_group3(F, b0, b1v, tq);
+      mlp_group3(F, b0, b1v, tq);
 #else
 #pragma unroll
-    for (int j = 0; j < 3; ++j) tq[j] = mlp_group(F, b0[j], b1v[j]);
+      for (int j = 0; j < 3; ++j) tq[j] = mlp_group(F, b0[j], b1v[j]);
 #endif
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
-    for (int j = 0; j < 3; ++j) tq[j] += -20.0f * xin[j][0] - 0.5f * xin[j][3];  // PD stand-in
+      for (int j = 0; j < 3; ++j) tq[j] += -20.0f * xin[j][0] - 0.5f * xin[j][3];  // PD stand-in
 #endif
-    MARK(mlp_done);
+      MARK(mlp_done);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int d = leg * 3 + j;
-      eh[1][j] = eh[0][j];
-      eh[0][j] = xin[j][0];
-      vh[1][j] = vh[0][j];
-      vh[0][j] = qd[j];
-      const float t = tq[j] * strength[j];
-      const float lim = tlim[j];
-      torque[j] = clampf(t, -lim, lim);
-      if (A.dbg_torques && owner) A.dbg_torques[((size_t)sub * n + e) * NDOF + d] = torque[j];
-    }
+      for (int j = 0; j < 3; ++j) {
+        eh[1][j] = eh[0][j];
+        eh[0][j] = xin[j][0];
+        vh[1][j] = vh[0][j];
+        vh[0][j] = qd[j];
+        const float t = tq[j] * strength[j];
+        const float lim = tlim[j];
+        torque[j] = clampf(t, -lim, lim);
+      }
+    };
+    const bool in_sub = GO1_MLP_IN_SUB && !INJ;
+    if (!in_sub) actuator();
     if (INJ) {
       const float* id = A.inj_dof + ((size_t)sub * n + e) * NDOF * 2;
 #pragma unroll
@@ -2181,17 +2193,27 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const float h = c->sim_dt / (float)c->n_internal;
 #pragma unroll
       for (int j = 0; j < 3; ++j) { P.q[j] = q[j]; P.qd[j] = qd[j]; }
-      for (int k = 0; k < c->n_internal; ++k) {
-        const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
 #ifndef GO1_ABL_NO_PHYS
-        phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw);
-#else
-        (void)last; (void)h;
-        P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];
-#endif
+      // the first integrator step of the sub-step peeled (it may carry the actuator net)
+      const bool last0 = (sub == dec - 1) && (c->n_internal == 1);
+      if (in_sub)
+        phys_substep<true>(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last0, cf_raw, actuator);
+      else
+        phys_substep<false>(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last0, cf_raw, actuator);
+      for (int k = 1; k < c->n_internal; ++k) {
+        const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
+        phys_substep<false>(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw, actuator);
       }
+#else
+      if (in_sub) actuator();
+      P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];
+#endif
 #pragma unroll
       for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }
+    }
+    if (A.dbg_torques && owner) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) A.dbg_torques[((size_t)sub * n + e) * NDOF + leg * 3 + j] = torque[j];
     }
   }
   cf_sum(cf_raw, role, cf_leg, cf_base);
