@@ -95,9 +95,11 @@ class EpisodeLogRing:
     asynchronous trip to the host.
 
     Two halves of R steps.  When a half fills, a side stream copies it to pinned host
-    memory while the next half is written; the copy is turned into deque entries on the
-    host one half later (long finished, no wait), so the rollout never blocks on logging.
-    Reading extras["train/episode"] / ["timeouts"] drains everything synchronously.
+    memory while the next half is written; one half later (long finished, no wait) the
+    copy's rows are set aside on the host (compact log), and they become deque entries only
+    when extras["train/episode"] / ["timeouts"] is read -- building ~14 deques of 4000
+    numpy scalars costs milliseconds, which the rollout loop used to pay every R steps.
+    Reading those extras drains everything synchronously.
     Deques keep their last 4000 entries (deque(maxlen=4000), as the reference), so only
     the newest 4000 values per key are materialised.
 
@@ -128,7 +130,19 @@ class EpisodeLogRing:
             self.host_count = torch.zeros((2, 1), dtype=torch.int32, pin_memory=True)
             self.side = torch.cuda.Stream(device)
             self.copied = [None, None]  # event per half: host copy finished
+            # the first device->pinned copy on the side stream costs ~6 ms of one-time setup
+            # (measured by tools/rollout_jitter.py at the first hand-off): pay it here, not in
+            # the rollout loop
+            with torch.cuda.stream(self.side):
+                for h in range(2):
+                    if self.compact:
+                        self.host_count[h].copy_(self.count[h], non_blocking=True)
+                        self.host[h].copy_(self.buf[h, :self.prefix], non_blocking=True)
+                    else:
+                        self.host[h].copy_(self.buf[h], non_blocking=True)
+            self.side.synchronize()
         self.inflight = None  # (half, first slot / row) copied to host, not yet turned into deque entries
+        self.pending, self.pending_rows = [], 0  # compact rows on the host, oldest first, not yet in the deques
 
     def next_slot(self):
         """Buffer the kernel writes this step's log into (compact: the half's row buffer)."""
@@ -179,14 +193,36 @@ class EpisodeLogRing:
                 done = torch.cuda.Event()
                 done.record(self.side)
                 self.copied[h] = done
-                self._process_rows(rows)
+                self._defer(rows)
             else:
                 self._process(self.host[h, first:].numpy())
+
+    PENDING_MAX = 1 << 17  # rows set aside before they are turned into deque entries anyway
+
+    def _defer(self, rows):
+        if rows.shape[0]:
+            self.pending.append(rows)
+            self.pending_rows += rows.shape[0]
+            if self.pending_rows > self.PENDING_MAX:
+                self._flush_pending()
+
+    def _flush_pending(self):
+        """Rows set aside, oldest chunk first.  A row's tag is its step's slot in its half, so
+        chunk i's tags are shifted by i R to make them increase across chunks; a step's rows
+        never straddle two chunks, so one pass equals processing the chunks one by one."""
+        if self.pending:
+            for i, r in enumerate(self.pending):
+                if i:
+                    r[:, self.W] += np.float32(i * self.R)
+            rows = np.concatenate(self.pending) if len(self.pending) > 1 else self.pending[0]
+            self.pending, self.pending_rows = [], 0
+            self._process_rows(rows)
 
     def drain(self):
         """Everything logged so far, synchronously (extras read)."""
         if self.cuda:
             self._drain_inflight()
+        self._flush_pending()
         if self.compact:
             cnt = int(self.count[self.half, 0].item())
             if cnt > self.done:
