@@ -167,13 +167,16 @@ def test_reset_kernel_matches_oracle():
 
 
 # One-step error of the f32 HIP integrator against the f64 oracle, relative to max(1, |x|), over
-# EVERY env.  Measured on the MI355X (tools/integrator_stats.py, 4096 envs x 6 steps, single_path
-# and plane): max 2e-4 (dof_pos), 4.6e-3 (dof_vel), 1.3e-3 (root), resets identical.  The only
-# larger errors belong to envs whose contact SET differs between the two (a point within f32
-# rounding of the surface: penalty contact switches on in one and not in the other, a
-# discontinuity in the force): 1 env in 49,152 (0.93 in dof_vel).  Those envs are named by that
-# test, counted (at most 1 per 1,000) and excluded from the max-error bound.
-INTEGRATOR_MAX_ERR = {"dof_pos": 2e-3, "dof_vel": 2e-2, "root": 5e-3}
+# EVERY env.  Measured on the MI355X (tools/integrator_stats.py, 4096 envs x 6 steps, single_path),
+# one 5 ms step per sim step with implicit contacts: the first step after the reset drop (hard
+# landings, the added contact masses at their largest against 0.1-0.3 kg links) max 4.5e-4
+# (dof_pos), 1.7e-2 (dof_vel), 5.4e-3 (root), p99.9 1.6e-4 / 7.0e-3 / 2.2e-3; the later steps max
+# 4e-5 / 1.3e-3 / 1.0e-3; resets identical, no contact-set flips.  (The explicit two-sub-step
+# integrator of rounds 1-2: max 2e-4 / 4.6e-3 / 1.3e-3.)  Envs whose contact SET differs between
+# the two (a point within f32 rounding of the surface: penalty contact switches on in one and not
+# in the other, a discontinuity in the force) are named by that test, counted (at most 1 per
+# 1,000) and excluded from the max-error bound.  Bounds: about twice the measured maxima.
+INTEGRATOR_MAX_ERR = {"dof_pos": 2e-3, "dof_vel": 4e-2, "root": 1e-2}
 
 
 def check_integrator_step(gs, st, cf_gpu, cf_oracle, reset_gpu, reset_oracle):

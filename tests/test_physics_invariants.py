@@ -7,18 +7,18 @@ kernel or the C oracle), on trajectories produced by the HIP kernel (`-m gpu`) a
 oracle (CPU).
 
 Scenarios (plane terrain, 64 envs, random orientation / velocities / joint angles):
-  * zero gravity, no contact, zero joint torque, 100 env steps (800 sub-steps of 2.5 ms): linear
-    and angular momentum conserved, and energy conserved for the envs whose joints stay off
+  * zero gravity, no contact, zero joint torque, 100 env steps (400 integrator steps of 5 ms):
+    linear and angular momentum conserved, and energy conserved for the envs whose joints stay off
     their limits (the limit spring-damper dissipates).  Semi-implicit Euler conserves them to
-    first order in the sub-step (the f64 oracle's drift halves with it).
-    Measured: HIP |dp| 2.3e-4 kg m/s, |dL| 4.0e-5 kg m^2/s, |dE|/E 4.8e-5; f64 oracle 3.4e-5,
-    4.0e-5, 6.7e-6.  Bounds: |dp|, |dL| < 2e-3, |dE| / E < 5e-4.
+    first order in the step.  Measured (one 5 ms step per sim step, implicit
+    contacts): HIP |dp| 9.4e-5 kg m/s, |dL| 8.0e-5 kg m^2/s, |dE|/E 1.4e-5; f64 oracle 6.9e-5,
+    8.0e-5, 1.3e-5.  Bounds: |dp|, |dL| < 2e-3, |dE| / E < 5e-4.
   * free fall (gravity on, no contact), one env step: the change of total momentum is M g dt (the
-    COM falls with g).  Measured 2.1e-4 relative (HIP and oracle).  Bound 1e-3.
+    COM falls with g).  Measured 4.2e-4 relative (HIP and oracle).  Bound 1e-3.
   * static stance (gravity, actuator net holding the default pose, zero actions), 150 env steps:
     the base settles (measured height 0.263 m, |v| 5e-4 m/s) and the reported contact forces carry
-    the weight (measured sum F_z / M g = 1.000).  Bounds: height in (0.20, 0.40) m, |v| < 5e-2,
-    |sum F_z / M g - 1| < 2 %.
+    the weight (measured sum F_z / M g = 1.000), HIP and oracle alike.  Bounds: height in
+    (0.20, 0.40) m, |v| < 5e-2, |sum F_z / M g - 1| < 2 %.
 """
 import numpy as np
 import pytest
