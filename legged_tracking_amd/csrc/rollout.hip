@@ -498,6 +498,233 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   PSTAMP(8);
 }
 
+// ---------------------------------------------------------------- per-net workgroups
+// policy_kernel streams all 2.8 MB of split weights through every CU (each workgroup serves 16 envs
+// with all three nets), the L2 -> CU floor of that decomposition.  Here a workgroup runs ONE net for
+// 32 envs as two 16-env B tiles that share every weight fragment: the first ceil(n / 32)
+// workgroups run the adaptation module + actor (1.6 MB), the others the critic (1.2 MB), so a CU
+// streams at most 1.6 MB for twice the envs.  K order, tile split and partial-sum order are those
+// of policy_kernel, so the outputs are identical.
+#ifndef GO1_POLICY_SPLIT
+#define GO1_POLICY_SPLIT 1
+#endif
+constexpr int SE = 32;  // envs per workgroup of policy_kernel_split
+
+template <int NT, int NL, int ET>
+__device__ __forceinline__ void policy_group_e(const f4_t (&w)[NL][NT], const ActV (*src)[NL], int g, int q, int c,
+                                               f4_t (&acc)[ET][NL][NT]) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int et = 0; et < ET; ++et) {
+      const h4_t xh = src[et][l].hi[(4 * g + q) * 16 + c], xl = src[et][l].lo[(4 * g + q) * 16 + c];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) acc[et][l][i] = mfma3(w[l][i], xh, xl, acc[et][l][i]);
+    }
+}
+
+template <int NT, int NL, int ET, int G, int D>
+__device__ __forceinline__ void policy_tiles_e(const PolicyLayer* L, const ActV (*src)[NL], int tile0, int tstride,
+                                               const ActV (*dst)[NL], bool act, int lane) {
+  const int q = lane >> 4, c = lane & 15;
+  f4_t acc[ET][NL][NT], w[D][NL][NT];
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      const f4_t b = *reinterpret_cast<const f4_t*>(L[l].b + 16 * (tile0 + i * tstride) + 4 * q);
+#pragma unroll
+      for (int et = 0; et < ET; ++et) acc[et][l][i] = b;
+    }
+  policy_prefetch<NT, NL, G, D>(L, tile0, tstride, lane, w);
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    policy_group_e<NT, NL, ET>(w[g % D], src, g, q, c, acc);
+    if (g + D < G) policy_load<NT, NL>(L, G, g + D, tile0, tstride, lane, w[g % D]);
+  }
+#pragma unroll
+  for (int et = 0; et < ET; ++et)
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        f4_t v = acc[et][l][i];
+        if (act) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = elu(v[r]);
+        }
+        act_store4(dst[et][l], 4 * (tile0 + i * tstride) + q, c, v);
+      }
+}
+
+// tile_partial for ET env tiles sharing the weight fragments
+template <int NG, int ET>
+__device__ __forceinline__ void tile_partial_e(const PolicyLayer& L, int Gs, int tile, int g0, const ActV* src, int lane,
+                                               f4_t (&acc)[ET]) {
+  const int q = lane >> 4, c = lane & 15;
+  f4_t w[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) w[i] = reinterpret_cast<const f4_t*>(L.w)[((size_t)tile * Gs + g0 + i) * 64 + lane];
+#pragma unroll
+  for (int et = 0; et < ET; ++et) acc[et] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < NG; ++i)
+#pragma unroll
+    for (int et = 0; et < ET; ++et)
+      acc[et] = mfma3(w[i], src[et].hi[(4 * (g0 + i) + q) * 16 + c], src[et].lo[(4 * (g0 + i) + q) * 16 + c], acc[et]);
+}
+
+__global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P) {
+  __shared__ Act<PIN> xin[2];           // [env tile] inputs (actor: history + latent; critic: history + priv)
+  __shared__ Act<512> h1[2];            // layer-1 outputs; layer 3 reuses them
+  __shared__ Act<256> h2[2];            // layer-2 outputs
+  __shared__ float scr[2][8][16][16];   // [env tile] K-split partials
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int q = lane >> 4, c = lane & 15;
+  const int nblk = (P.n_envs + SE - 1) / SE;
+  const bool critic = (int)blockIdx.x >= nblk;
+  const int e0 = (critic ? (int)blockIdx.x - nblk : (int)blockIdx.x) * SE;
+  const int ne = min(SE, P.n_envs - e0);
+  const ActV vx[2][1] = {{xin[0].v()}, {xin[1].v()}}, v1[2][1] = {{h1[0].v()}, {h1[1].v()}},
+             v2[2][1] = {{h2[0].v()}, {h2[1].v()}};
+  for (int idx = tid; idx < SE * PIN; idx += 64 * PW) {
+    const int e = idx / PIN, k = idx - e * PIN;
+    float v = 0.0f;
+    if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
+    if (critic && e < ne && k >= P.hist_dim && k < P.hist_dim + 2)
+      v = P.privileged_obs[(size_t)(e0 + e) * 2 + (k - P.hist_dim)];
+    act_store1(e < 16 ? vx[0][0] : vx[1][0], k, e & 15, v);  // no runtime index into vx (private memory)
+  }
+  __syncthreads();
+  const PolicyLayer* Ls = P.layers;
+  if (!critic) {
+    // adaptation module 261 -> 256 (xin rows >= hist_dim are still zero)
+    policy_tiles_e<1, 1, 2, PIN / 16, 8>(Ls + 0, vx, wave, PW, v1, true, lane);
+    __syncthreads();
+    {  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7
+      const int t = wave & 7, half = wave >> 3;
+      const ActV src[2] = {v1[0][0], v1[1][0]};
+      f4_t acc[2];
+      tile_partial_e<8, 2>(Ls[1], 16, t, 8 * half, src, lane, acc);
+      if (half) {
+#pragma unroll
+        for (int et = 0; et < 2; ++et)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) scr[et][t][4 * q + r][c] = acc[et][r];
+      }
+      __syncthreads();
+      if (!half) {
+        const f4_t b = *reinterpret_cast<const f4_t*>(Ls[1].b + 16 * t + 4 * q);
+#pragma unroll
+        for (int et = 0; et < 2; ++et) {
+          f4_t v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = elu((b[r] + acc[et][r]) + scr[et][t][4 * q + r][c]);
+          act_store4(v2[et][0], 4 * t + q, c, v);
+        }
+      }
+    }
+    __syncthreads();
+    {  // 128 -> 2 (the latent): one K group per wave (8 waves), partials summed by waves 0 / 1
+      if (wave < 8) {
+        const ActV src[2] = {v2[0][0], v2[1][0]};
+        f4_t acc[2];
+        tile_partial_e<1, 2>(Ls[2], 8, 0, wave, src, lane, acc);
+#pragma unroll
+        for (int et = 0; et < 2; ++et)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) scr[et][wave][4 * q + r][c] = acc[et][r];
+      }
+      __syncthreads();
+      if (wave < 2 && q == 0) {
+        const int et = wave, e = 16 * et + c;
+        float l0 = Ls[2].b[0], l1 = Ls[2].b[1];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) { l0 += scr[et][w][0][c]; l1 += scr[et][w][1][c]; }
+        const ActV d = et ? vx[1][0] : vx[0][0];
+        act_store1(d, P.hist_dim, c, l0);
+        act_store1(d, P.hist_dim + 1, c, l1);
+        if (e < ne && P.latent) {
+          P.latent[(size_t)(e0 + e) * 2] = l0;
+          P.latent[(size_t)(e0 + e) * 2 + 1] = l1;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // actor (Ls 3-6) or critic (Ls 7-10), layer by layer
+  const PolicyLayer* LN = Ls + (critic ? 7 : 3);
+  policy_tiles_e<2, 1, 2, PIN / 16, 6>(LN + 0, vx, wave, PW, v1, true, lane);  // 512
+  __syncthreads();
+  policy_tiles_e<1, 1, 2, 512 / 16, 12>(LN + 1, v1, wave, PW, v2, true, lane);  // 256
+  __syncthreads();
+  if (wave < 8) policy_tiles_e<1, 1, 2, 256 / 16, 8>(LN + 2, v2, wave, 8, v1, true, lane);  // 128 -> h1
+  __syncthreads();
+  if (wave < 8) {  // 128 -> num_actions / 1: one K group per wave, partials through LDS
+    const ActV src[2] = {v1[0][0], v1[1][0]};
+    f4_t part[2];
+    tile_partial_e<1, 2>(LN[3], 8, 0, wave, src, lane, part);
+#pragma unroll
+    for (int et = 0; et < 2; ++et)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[et][wave][4 * q + r][c] = part[et][r];
+  }
+  __syncthreads();
+  if (wave < 2) {
+    const int et = wave, e = 16 * et + c;
+    f4_t acc = *reinterpret_cast<const f4_t*>(LN[3].b + 4 * q);
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += scr[et][w][4 * q + r][c];
+    if (!critic) {
+      if (P.actions) {
+        float lp = 0.0f;
+        f4_t a4, s4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * q + r;
+          const bool real = f < P.num_actions;
+          const float sd = real ? P.std[f] : 1.0f;
+          uint32_t ctr[4] = {(uint32_t)(e0 + e + P.env_id_offset), (uint32_t)f, (uint32_t)P.rng_step,
+                             (uint32_t)(P.rng_step >> 32)};
+          philox4x32(ctr, (uint32_t)P.rng_seed, (uint32_t)(P.rng_seed >> 32));
+          const float u1 = ((float)(ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+          const float u2 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);
+          const float z = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+          a4[r] = acc[r] + sd * z;
+          s4[r] = sd;
+          if (real) lp += -0.5f * z * z - logf(sd) - 0.91893853320467274f;  // log sqrt(2 pi)
+        }
+        auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(lp), __float_as_uint(lp), false, false);
+        lp = __uint_as_float(x[0]) + __uint_as_float(x[1]);
+        auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(lp), __float_as_uint(lp), false, false);
+        lp = __uint_as_float(y[0]) + __uint_as_float(y[1]);
+        if (e < ne) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int f = 4 * q + r;
+            if (f < P.num_actions) {
+              P.actions[(size_t)(e0 + e) * P.num_actions + f] = a4[r];
+              P.action_sigma[(size_t)(e0 + e) * P.num_actions + f] = s4[r];
+            }
+          }
+          if (q == 0) P.log_prob[e0 + e] = lp;
+        }
+      }
+      if (e < ne) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * q + r;
+          if (f < P.num_actions) P.action_mean[(size_t)(e0 + e) * P.num_actions + f] = acc[r];
+        }
+      }
+    } else if (e < ne && q == 0) {
+      P.value[e0 + e] = acc[0];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -545,7 +772,10 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
   for (int i = 0; i < GO1_POLICY_LAYERS; ++i)
     if (!args->layers[i].w || !args->layers[i].b) return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer");
   go1_policy_args P = *args;
-  hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(64 * PW), 0, (hipStream_t)stream, P);
+  if (GO1_POLICY_SPLIT)
+    hipLaunchKernelGGL(policy_kernel_split, dim3(2 * ((P.n_envs + SE - 1) / SE)), dim3(64 * PW), 0, (hipStream_t)stream, P);
+  else
+    hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(64 * PW), 0, (hipStream_t)stream, P);
   RT_TRY(hipGetLastError());
   return GO1_OK_RT;
 }
