@@ -69,6 +69,9 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #ifndef GO1_GLDS  // LDS-DMA staging of the model block and terrain patches
 #define GO1_GLDS 1
 #endif
+#ifndef GO1_BASE_SCHUR  // the base's 6 x 6 solve by 3 x 3 blocks (solve6s) instead of Cholesky (solve6p):
+#define GO1_BASE_SCHUR 0  // GPU suite green, 48.4 against 48.0 us (event-timed A/B), off
+#endif
 #ifndef GO1_MLP_IN_SUB  // the actuator net inside the first integrator step of a sub-step (phys_substep);
 #define GO1_MLP_IN_SUB 0  // measured 47.8 against 47.7 us ahead of it: off
 #endif
@@ -1016,6 +1019,44 @@ __device__ __forceinline__ void solve6p(const SIP& M, const float* b, float* x) 
 #undef LI
 }
 
+// The same solve by 3 x 3 blocks, M = [[A, B], [B^T, C]] (angular, linear): C^-1 and the Schur
+// complement S = A - B C^-1 B^T inverted by adjugates.  Both blocks are SPD (C ~ the mass, S the
+// rotational inertia about the moving COM), and the dependency depth is about half of the
+// Cholesky chain's (GO1_BASE_SCHUR).
+__device__ __forceinline__ void sym3_inv(float a00, float a01, float a02, float a11, float a12, float a22, float* k) {
+  k[0] = a11 * a22 - a12 * a12; k[1] = a02 * a12 - a01 * a22; k[2] = a01 * a12 - a02 * a11;
+  k[3] = a00 * a22 - a02 * a02; k[4] = a01 * a02 - a00 * a12; k[5] = a00 * a11 - a01 * a01;
+  const float id = frcp(a00 * k[0] + a01 * k[1] + a02 * k[2]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) k[i] *= id;
+}
+__device__ __forceinline__ void solve6s(const SIP& M, const float* b, float* x) {
+  float Ci[6], Si[6], X[9], S[6];
+  sym3_inv(M.ac[0].y, M.ac[1].y, M.ac[2].y, M.ac[3].y, M.ac[4].y, M.ac[5].y, Ci);
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      X[3 * a + j] = M.b[3 * a] * Ci[s3i(0, j)] + M.b[3 * a + 1] * Ci[s3i(1, j)] + M.b[3 * a + 2] * Ci[s3i(2, j)];
+  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int a = II[k], c = JJ[k];
+    S[k] = M.ac[k].x - (X[3 * a] * M.b[3 * c] + X[3 * a + 1] * M.b[3 * c + 1] + X[3 * a + 2] * M.b[3 * c + 2]);
+  }
+  sym3_inv(S[0], S[1], S[2], S[3], S[4], S[5], Si);
+  float bw[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) bw[a] = b[a] - (X[3 * a] * b[3] + X[3 * a + 1] * b[4] + X[3 * a + 2] * b[5]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) x[a] = Si[s3i(a, 0)] * bw[0] + Si[s3i(a, 1)] * bw[1] + Si[s3i(a, 2)] * bw[2];
+  float bv[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) bv[j] = b[3 + j] - (M.b[j] * x[0] + M.b[3 + j] * x[1] + M.b[6 + j] * x[2]);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) x[3 + j] = Ci[s3i(j, 0)] * bv[0] + Ci[s3i(j, 1)] * bv[1] + Ci[s3i(j, 2)] * bv[2];
+}
+
 __device__ __forceinline__ void quat_to_R(const float* q, float* R) {
   float x = q[0], y = q[1], z = q[2], w = q[3];
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
@@ -1698,7 +1739,11 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     rhs[i] = -(p0[i].x + pp6[i].x);
     rhs[3 + i] = -(p0[i].y + pp6[i].y);
   }
+#if GO1_BASE_SCHUR
+  solve6s(I0, rhs, a0);
+#else
   solve6p(I0, rhs, a0);
+#endif
   MARK(base_solve_done);
   // ---- forward pass
   float qdd[3];
