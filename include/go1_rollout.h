@@ -85,6 +85,10 @@ typedef struct go1_policy_args {
 
 const char* go1_rollout_last_error(void);
 int go1_policy_forward(const go1_policy_args* args, void* stream);
+/* Which policy kernel go1_policy_forward launches: 1 = per-net workgroups of 32 envs (default),
+ * 0 = one workgroup of 16 envs running all three nets.  Identical outputs (tests/test_rollout.py);
+ * returns the previous setting. */
+int go1_policy_set_split(int split);
 int go1_record_transition(const go1_transition* tr, int32_t n_envs, float gamma, void* stream);
 /* rewards/values/returns/advantages: (T, n) f32; dones (T, n) u8; last_values (n);
  * stats: 2 f64 (sum, sum of squares of the raw advantages), overwritten. */

@@ -763,6 +763,13 @@ int go1_gae(const float* rewards, const uint8_t* dones, const float* values, con
   return GO1_OK_RT;
 }
 
+static int g_policy_split = GO1_POLICY_SPLIT;
+int go1_policy_set_split(int split) {
+  const int prev = g_policy_split;
+  g_policy_split = split ? 1 : 0;
+  return prev;
+}
+
 int go1_policy_forward(const go1_policy_args* args, void* stream) {
   if (!args || args->n_envs <= 0 || !args->obs_history || !args->privileged_obs || !args->action_mean ||
       !args->value)
@@ -772,7 +779,7 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
   for (int i = 0; i < GO1_POLICY_LAYERS; ++i)
     if (!args->layers[i].w || !args->layers[i].b) return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer");
   go1_policy_args P = *args;
-  if (GO1_POLICY_SPLIT)
+  if (g_policy_split)
     hipLaunchKernelGGL(policy_kernel_split, dim3(2 * ((P.n_envs + SE - 1) / SE)), dim3(64 * PW), 0, (hipStream_t)stream, P);
   else
     hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(64 * PW), 0, (hipStream_t)stream, P);

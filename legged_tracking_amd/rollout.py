@@ -210,6 +210,7 @@ class HipRolloutKernels:
         lib.go1_gae.argtypes = [C.c_void_p] * 7 + [C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_void_p]
         lib.go1_adv_normalize.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_int64, C.c_void_p]
         lib.go1_policy_forward.argtypes = [C.POINTER(_PolicyArgs), C.c_void_p]
+        lib.go1_policy_set_split.argtypes = [C.c_int]
         self.lib = lib
 
     def _chk(self, rc):

@@ -211,6 +211,31 @@ def test_fused_policy_kernel_matches_reference_actor_critic():
 
 
 @pytest.mark.gpu
+def test_split_policy_kernel_is_bit_identical_to_single_workgroup_kernel():
+    """policy_kernel_split (a workgroup per net for 32 envs, weight fragments shared by two env
+    tiles; the default) against policy_kernel (16 envs, all three nets per workgroup): same K
+    order, tile split and partial-sum order, so every output is bit-identical, sampling included,
+    on a ragged batch (the last split workgroup holds 16 + 9 envs)."""
+    d = _fixture()
+    ac = _ac(d, "cuda:0")
+    k = R.HipRolloutKernels()
+    pol = k.policy(ac)
+    n = 4096 + 25
+    g = torch.Generator(device="cuda").manual_seed(11)
+    h = torch.randn(n, 261, device="cuda", generator=g)
+    p = torch.randn(n, 2, device="cuda", generator=g)
+    outs = []
+    try:
+        for split in (1, 0):
+            k.lib.go1_policy_set_split(split)
+            outs.append([t.cpu().numpy() for t in pol.forward(h, p, sample=(123, 7, 0))])
+    finally:
+        k.lib.go1_policy_set_split(1)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
 def test_fused_policy_sampling_is_normal_with_matching_log_prob():
     d = _fixture()
     ac = _ac(d, "cuda:0")
