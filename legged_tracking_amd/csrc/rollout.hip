@@ -509,6 +509,14 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
 #define GO1_POLICY_SPLIT 1
 #endif
 constexpr int SE = 32;  // envs per workgroup of policy_kernel_split
+// weight groups in flight per wave, the 512-wide first layers and the 256-wide second: (4, 8), (6, 12),
+// (8, 12), (8, 16) all within 1 % of each other on the rollout loop (2 runs each), so not the limit
+#ifndef GO1_SPLIT_D1
+#define GO1_SPLIT_D1 6
+#endif
+#ifndef GO1_SPLIT_D2
+#define GO1_SPLIT_D2 12
+#endif
 
 template <int NT, int NL, int ET>
 __device__ __forceinline__ void policy_group_e(const f4_t (&w)[NL][NT], const ActV (*src)[NL], int g, int q, int c,
@@ -654,9 +662,9 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
   }
   // actor (Ls 3-6) or critic (Ls 7-10), layer by layer
   const PolicyLayer* LN = Ls + (critic ? 7 : 3);
-  policy_tiles_e<2, 1, 2, PIN / 16, 6>(LN + 0, vx, wave, PW, v1, true, lane);  // 512
+  policy_tiles_e<2, 1, 2, PIN / 16, GO1_SPLIT_D1>(LN + 0, vx, wave, PW, v1, true, lane);  // 512
   __syncthreads();
-  policy_tiles_e<1, 1, 2, 512 / 16, 12>(LN + 1, v1, wave, PW, v2, true, lane);  // 256
+  policy_tiles_e<1, 1, 2, 512 / 16, GO1_SPLIT_D2>(LN + 1, v1, wave, PW, v2, true, lane);  // 256
   __syncthreads();
   if (wave < 8) policy_tiles_e<1, 1, 2, 256 / 16, 8>(LN + 2, v2, wave, 8, v1, true, lane);  // 128 -> h1
   __syncthreads();
