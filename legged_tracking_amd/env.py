@@ -232,11 +232,6 @@ class EpisodeLogRing:
             self._process(self.buf[self.half, self.done:self.slot].cpu().numpy())
             self.done = self.slot
 
-    def reset(self):
-        if self.cuda:
-            self._drain_inflight()
-        self.drain()
-
     def _process_rows(self, rows):
         """Compact rows (m, W + 2) -> the dense (steps, envs, W) processing of _process, without
         building the dense array: order by (step tag, env) as the reference logs them (:256-271)."""
@@ -707,11 +702,14 @@ class TrajectoryTrackingEnv(LeggedRobot):
         return obs, rew, reset, extras
 
     def reset(self):
+        # reset_idx logs every finished episode into the current dicts (it drains the episode log
+        # first); the reference then swaps in empty extras (trajectory_tracking/__init__.py:46-55),
+        # so nothing logged before this reset reaches the new dicts
         self.reset_idx(torch.arange(self.num_envs, device=self.device))
         self.episode_length_buf = torch.randint(int(self.max_episode_length), (self.num_envs,), device=self.device,
                                                 generator=self._gen, dtype=torch.int32)
+        self._elog.drain()  # into the old dicts (empty: reset_idx drained), never into the new ones
         self._train_ep, self._eval_ep, self._timeouts = _episode_dicts()
-        self._elog.reset()
         self._install_extras()
         obs, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
         return obs

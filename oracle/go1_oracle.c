@@ -996,6 +996,11 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     for (int i = 0; i < 3; ++i) {
       S.pos[i] = root[i]; S.v[i] = root[7 + i]; S.w[i] = root[10 + i];
     }
+    /* the integrator works relative to the env's terrain origin: world x, y reach ~100 m, where an f32
+     * ulp is 7.6e-6 m, and the contact forces on a terrain step depend on x with ~1e3 s^-1 gain
+     * (k * height gradient); root - origin is exact in f32 (Sterbenz) and keeps ~1e-7 m resolution */
+    S.pos[0] = (real)root[0] - ox;
+    S.pos[1] = (real)root[1] - oy;
     for (int i = 0; i < 4; ++i) S.quat[i] = root[3 + i];
     for (int d = 0; d < NDOF; ++d) { S.q[d] = dp[d]; S.qd[d] = dv[d]; }
   }
@@ -1010,7 +1015,7 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
       real tau[NDOF], g[3] = {a->sim_gravity[0], a->sim_gravity[1], a->sim_gravity[2]};
       real cfd[NB * 3];
       for (int d = 0; d < NDOF; ++d) tau[d] = torque[d];
-      TerrainView T = {tile, c->hf_nx, c->hf_ny, ox, oy, c->horizontal_scale};
+      TerrainView T = {tile, c->hf_nx, c->hf_ny, 0, 0, c->horizontal_scale};
       real h = (real)c->sim_dt / c->n_internal;
       for (int k = 0; k < c->n_internal; ++k)
         phys_substep(M, c, &S, tau, h, g, st->friction[e], st->payload[e], &T, cfd);
@@ -1025,6 +1030,8 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     for (int i = 0; i < 3; ++i) {
       root[i] = (float)S.pos[i]; root[7 + i] = (float)S.v[i]; root[10 + i] = (float)S.w[i];
     }
+    root[0] = (float)(S.pos[0] + ox);
+    root[1] = (float)(S.pos[1] + oy);
     for (int i = 0; i < 4; ++i) root[3 + i] = (float)S.quat[i];
   }
   if (a->contact_forces)

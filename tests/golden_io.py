@@ -13,6 +13,23 @@ STATE_KEYS = ("root", "dof_pos", "dof_vel", "last_actions", "last_dof_vel", "lag
               "feet_air_time", "last_contacts")
 
 
+def spec_match(c):
+    """True when go1_config `c` equals the specialised step kernel's compile-time configuration
+    (legged_tracking_amd/csrc/go1_spec.h, bit for bit) -- the host-side twin of spec_match() in
+    go1_step.hip, so the parity tests know which fixtures replay through go1_step_kernel<SPEC>."""
+    import re
+    import struct
+    hdr = open(os.path.join(os.path.dirname(GOLDEN), "..", "legged_tracking_amd", "csrc", "go1_spec.h")).read()
+    for field, val in re.findall(r"^  X\((\w+), ([^)]+)\)", hdr, re.M):
+        got = getattr(c, field)
+        if val.endswith("f"):  # exact hex float literal
+            if struct.pack("<f", float(got)) != struct.pack("<f", float.fromhex(val[:-1])):
+                return False
+        elif int(got) != int(val.rstrip("u")):
+            return False
+    return True
+
+
 def load(name):
     return np.load(os.path.join(GOLDEN, name))
 

@@ -226,3 +226,27 @@ def test_compact_episode_log_rows_match_dense_processing():
         assert dense_env._train_ep.keys() == comp_env._train_ep.keys()
         for k in dense_env._train_ep:
             np.testing.assert_array_equal(np.array(dense_env._train_ep[k]), np.array(comp_env._train_ep[k]))
+
+
+def test_reset_starts_with_empty_episode_extras():
+    """TrajectoryTrackingEnv.reset swaps in empty extras after reset_idx (trajectory_tracking/
+    __init__.py:46-55): episodes that ended before the reset -- in the device log, deferred on the
+    host, or logged by reset_idx itself -- never reach the new train/episode and timeouts."""
+    n = 64
+    env = make_env(n=n)
+    env.reset()
+    env.episode_length_buf = torch.full((n,), 499, dtype=torch.int32)  # every env times out within 3 steps
+    rng = np.random.default_rng(0)
+    for _ in range(4):
+        env.step(torch.from_numpy(rng.normal(0, 1, (n, 12)).astype(np.float32)))
+    assert len(env.extras["train/episode"]["episode_length"]) >= n  # the time-outs were logged
+    env.episode_length_buf = torch.full((n,), 499, dtype=torch.int32)
+    env.step(torch.zeros(n, 12))  # logged in the device ring, not read yet
+    env.reset()
+    ep = env.extras["train/episode"]
+    assert all(len(v) == 0 for k, v in ep.items() if k.startswith("rew_") or k == "episode_length"), \
+        {k: len(v) for k, v in ep.items()}
+    assert len(env.extras["timeouts"]) == 0
+    # the reset's own step(zeros) starts a fresh episode everywhere: still nothing to log
+    env.step(torch.zeros(n, 12))
+    assert len(env.extras["train/episode"]["episode_length"]) == 0

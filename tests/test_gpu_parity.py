@@ -59,8 +59,15 @@ def test_actuator_net_bit_exact_vs_oracle():
     assert abs(z - (-0.0041)) < 1e-4 and abs(h - (-1.872)) < 1e-3
 
 
-@pytest.mark.parametrize("name", FIXTURES)
-def test_fused_step_replays_reference_fixture(name):
+# the README-configuration fixtures replay through both step kernels: the specialised
+# instantiation go1_create picks for the bench workload (go1_step_kernel<INJ, 7, SPEC = true>) and
+# the generic one (fields read at run time); every other fixture through the generic kernel
+CASES = [(f, k) for f in FIXTURES for k in ("generic", "specialised")
+         if k == "generic" or G.spec_match(G.fixture_config(G.load(f))[1])]
+
+
+@pytest.mark.parametrize("name,kernel", CASES)
+def test_fused_step_replays_reference_fixture(name, kernel):
     """Injected post-physics state (parity mode): the fused kernel reproduces the
     reference step (torques, heights, masks, rewards, obs, state) and the oracle."""
     d = G.load(name)
@@ -68,6 +75,8 @@ def test_fused_step_replays_reference_fixture(name):
     n = c.n_envs
     ter = G.terrain_of(d)
     g = native.Go1Native(c, DEV)
+    g.specialize(kernel == "specialised")
+    assert g.specialized == (kernel == "specialised")
     g.set_terrain(ter.tiles, ter.env_tile, ter.eto, ter.eo)
     dbg = native.debug_buffers(n, c.decimation, DEV)
     ns = c.n_terms + 3
@@ -167,16 +176,18 @@ def test_reset_kernel_matches_oracle():
 
 
 # One-step error of the f32 HIP integrator against the f64 oracle, relative to max(1, |x|), over
-# EVERY env.  Measured on the MI355X (tools/integrator_stats.py, 4096 envs x 6 steps, single_path),
-# one 5 ms step per sim step with implicit contacts: the first step after the reset drop (hard
-# landings, the added contact masses at their largest against 0.1-0.3 kg links) max 4.5e-4
-# (dof_pos), 1.7e-2 (dof_vel), 5.4e-3 (root), p99.9 1.6e-4 / 7.0e-3 / 2.2e-3; the later steps max
-# 4e-5 / 1.3e-3 / 1.0e-3; resets identical, no contact-set flips.  (The explicit two-sub-step
-# integrator of rounds 1-2: max 2e-4 / 4.6e-3 / 1.3e-3.)  Envs whose contact SET differs between
-# the two (a point within f32 rounding of the surface: penalty contact switches on in one and not
-# in the other, a discontinuity in the force) are named by that test, counted (at most 1 per
-# 1,000) and excluded from the max-error bound.  Bounds: about twice the measured maxima.
-INTEGRATOR_MAX_ERR = {"dof_pos": 2e-3, "dof_vel": 4e-2, "root": 1e-2}
+# EVERY env.  The integrator runs relative to the env's terrain origin (go1_step.hip, round 3):
+# world x, y reach ~100 m, where an f32 ulp is 7.6e-6 m, and on a terrain step the contact forces
+# depend on x with a gain of ~1e3 s^-1, so world-frame contact points had put up to 1.7e-2
+# (dof_vel) / 5.4e-3 (root) into the first step after a reset drop (round-2 bounds 4e-2 / 1e-2).
+# Measured on the MI355X after the change (tools/integrator_stats.py, 4096 envs x 6 steps, single_path
+# and plane, gpurun_out -> profiles/r03/integrator_stats*.json): max 7.8e-6 (dof_pos), 1.13e-3
+# (dof_vel), 8.4e-5 (root); resets identical, no contact-set flips.  Envs whose contact SET differs
+# between the two (a point within f32 rounding of the surface: penalty contact switches on in one
+# and not in the other, a discontinuity in the force) are named by that test, counted (at most 1
+# per 1,000) and excluded from the max-error bound.  Bounds: ~4x the measured maxima, and 4x / 10x
+# below the round-1 bounds (dof_vel 2e-2, root 5e-3).
+INTEGRATOR_MAX_ERR = {"dof_pos": 5e-5, "dof_vel": 5e-3, "root": 5e-4}
 
 
 def check_integrator_step(gs, st, cf_gpu, cf_oracle, reset_gpu, reset_oracle):
@@ -297,7 +308,7 @@ def test_env_api_on_gpu_matches_oracle_backend():
         # proprioceptive columns: integrator tolerance (INTEGRATOR_MAX_ERR) on every env with the same
         # contact set; the same Philox noise on both sides
         err = np.abs(og["obs"].cpu().numpy()[:, :41] - oc["obs"].numpy()[:, :41])
-        assert err[~flip].max() < 2e-2, err[~flip].max()
+        assert err[~flip].max() < 5e-3, err[~flip].max()
         # height columns (camera_zero: sample - base z, x 0.1): within the pose error, except a scan
         # point within the pose error of a cell boundary, which may sample the neighbouring cell
         dh = np.abs(og["obs"].cpu().numpy()[:, 41:] - oc["obs"].numpy()[:, 41:]) > 1e-3

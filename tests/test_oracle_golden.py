@@ -65,3 +65,13 @@ def test_oracle_replays_reference_steps(name):
         G.check_episode_log_and_extras(d, t, out["episode_log"], out["aux"])
         n_resets += int(d[f"s{t}/reset"].sum())
     assert n_resets > 0, "fixture should exercise reset_idx"
+
+
+def test_readme_fixtures_match_the_specialised_kernel():
+    """The README-configuration fixtures (including the full 32x32 grid) must keep matching the
+    specialised step kernel's compile-time configuration (csrc/go1_spec.h), so the shipped
+    instantiation go1_step_kernel<., 7, SPEC> stays pinned by a reference fixture replay on the GPU
+    (tests/test_gpu_parity.py::test_fused_step_replays_reference_fixture[*-specialised])."""
+    for name in ("step_full_grid.npz", "step_single_path.npz", "step_single_path_events.npz"):
+        assert G.spec_match(G.fixture_config(G.load(name))[1]), name
+    assert not G.spec_match(G.fixture_config(G.load("step_plane.npz"))[1])
