@@ -10,7 +10,8 @@
  *                          :1311-1320, gym.set_dof_actuation_force_tensor /
  *                          simulate / fetch_results / refresh_dof_state_tensor
  *                          :82-88, post_physics_step :114-169)
- *   go1_reset_envs()  <- LeggedRobot.reset_idx                 :218-296
+ *   go1_reset_idx()   <- LeggedRobot.reset_idx(env_ids)        :218-296
+ *   go1_reset_envs()     (the same, env ids as a mask)
  *                         (+ gym.set_*_tensor_indexed :1011-1013, :1050-1052)
  *   go1_set_terrain() <- Terrain env_height_samples / env_terrain_origin
  *                         (_get_env_origins :1808-1847)
@@ -33,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GO1_ABI_VERSION 4
+#define GO1_ABI_VERSION 5
 
 #define GO1_NUM_DOF 12
 #define GO1_NUM_BODIES 17
@@ -277,13 +278,30 @@ typedef struct go1_step_args {
 
 typedef struct go1_handle go1_handle;
 
+/* Shape and strides (in elements) of one state plane as the caller's tensor has them
+ * (PyTorch: t.shape, t.stride(), dtype), in go1_state field order.  go1_bind checks every plane
+ * against the layout the kernels index -- (n_envs, width) row-major, dense, f32 / int32 as
+ * go1_state notes -- and rejects a view that differs (GO1_E_ARG naming the plane): a
+ * non-contiguous slice or transpose never reaches a kernel. */
+#define GO1_STATE_PLANES 22
+#define GO1_DTYPE_F32 0
+#define GO1_DTYPE_I32 1
+typedef struct go1_plane {
+  int64_t rows, cols;             /* shape (n_envs, width) */
+  int64_t row_stride, col_stride; /* elements; dense row-major = (cols, 1) */
+  int32_t dtype;                  /* GO1_DTYPE_* */
+  int32_t pad;
+} go1_plane;
+
 int go1_abi_version(void);
 /* sizeof(go1_config), sizeof(go1_state), sizeof(go1_terrain), sizeof(go1_step_args):
  * lets a foreign binding (ctypes / cgo / JNI) verify its struct mirrors. */
 void go1_abi_sizes(int64_t out[4]);
 const char* go1_last_error(void);
 int go1_create(const go1_config* cfg, go1_handle** out);
-int go1_bind(go1_handle* h, const go1_state* state);
+/* Binds the caller's state planes (never copied, allocated or freed).  planes: GO1_STATE_PLANES
+ * descriptors, go1_state order, required. */
+int go1_bind(go1_handle* h, const go1_state* state, const go1_plane* planes);
 int go1_set_terrain(go1_handle* h, const go1_terrain* terrain);
 
 /* Tunnel terrain generator on the device (no handle needed): the single_path tiles of a
@@ -326,8 +344,12 @@ int go1_sync_time_outs(go1_handle* h, void* stream);
  * (go1_sync_time_outs does exactly that in a kernel of its own); the record kernel of the PPO
  * rollout (go1_rollout.h, go1_transition.time_outs_flag) does it while recording. */
 int go1_time_outs_pending(go1_handle* h, int64_t out[3]);
-/* Reset envs whose mask[e] != 0: reset_idx semantics (:218-296) incl. DR draws;
- * uniforms NULL -> Philox(rng_seed, rng_step). */
+/* reset_idx(env_ids) (:218-296) incl. the DR draws, for the n_ids device int32 env ids (local
+ * indices 0 .. n_envs - 1; ids outside that range are skipped, duplicates reset the env once with
+ * the same draws); uniforms NULL -> Philox(rng_seed, rng_step) keyed by global env id. */
+int go1_reset_idx(go1_handle* h, const int32_t* ids, int32_t n_ids, const float* uniforms, uint64_t rng_seed,
+                  uint64_t rng_step, void* stream);
+/* The same for the envs whose mask[e] != 0 (one uint8 per env). */
 int go1_reset_envs(go1_handle* h, const uint8_t* mask, const float* uniforms, uint64_t rng_seed,
                    uint64_t rng_step, void* stream);
 /* Actuator-net torques for (n_rows, 6) inputs -> (n_rows) (eval_actuator_network :1311-1320). */

@@ -5,7 +5,7 @@ checks sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
-GO1_ABI_VERSION = 4
+GO1_ABI_VERSION = 5
 GO1_NUM_DOF = 12
 GO1_NUM_BODIES = 17
 GO1_MAX_TERMS = 16
@@ -83,6 +83,29 @@ class Go1State(C.Structure):
         "motor_strength", "motor_offset", "friction", "restitution", "payload", "episode_length",
         "curr_pose_index", "trajectory", "base_rotation", "collision_count", "episode_sums",
         "joint_pos_target", "feet_air_time", "last_contacts")]
+
+
+GO1_STATE_PLANES = 22
+GO1_DTYPE_F32, GO1_DTYPE_I32 = 0, 1
+
+
+class Go1Plane(C.Structure):
+    """go1_plane: shape and strides (elements) of one state plane, checked by go1_bind."""
+    _fields_ = [("rows", C.c_int64), ("cols", C.c_int64), ("row_stride", C.c_int64), ("col_stride", C.c_int64),
+                ("dtype", I32), ("pad", I32)]
+
+
+def plane_descs(tensors):
+    """go1_plane[GO1_STATE_PLANES] for a {name: tensor} state, in go1_state order (torch shapes /
+    strides as they are: go1_bind, not this helper, decides what it accepts)."""
+    arr = (Go1Plane * GO1_STATE_PLANES)()
+    for i, (name, _) in enumerate(Go1State._fields_):
+        t = tensors[name]
+        shape = tuple(t.shape) + (1,) * (2 - t.dim())
+        stride = tuple(t.stride()) + (1,) * (2 - t.dim())
+        arr[i] = Go1Plane(rows=shape[0], cols=shape[1], row_stride=stride[0], col_stride=stride[1],
+                          dtype=GO1_DTYPE_I32 if str(t.dtype) == "torch.int32" else GO1_DTYPE_F32)
+    return arr
 
 
 class Go1Terrain(C.Structure):

@@ -63,33 +63,6 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #else
 #define MARK(x)
 #endif
-#ifndef GO1_MLP_UNROLL_N
-#define GO1_MLP_UNROLL_N 4
-#endif
-#ifndef GO1_GLDS  // LDS-DMA staging of the model block and terrain patches
-#define GO1_GLDS 1
-#endif
-#ifndef GO1_BASE_SCHUR  // the base's 6 x 6 solve by 3 x 3 blocks (solve6s) instead of Cholesky (solve6p):
-#define GO1_BASE_SCHUR 0  // GPU suite green, 48.4 against 48.0 us (event-timed A/B), off
-#endif
-#ifndef GO1_MLP_IN_SUB  // the actuator net inside the first integrator step of a sub-step (phys_substep);
-#define GO1_MLP_IN_SUB 0  // measured 47.8 against 47.7 us ahead of it: off
-#endif
-#ifndef GO1_MLP3  // the three MLP groups of a sub-step layer by layer (mlp_group3)
-#define GO1_MLP3 1
-#endif
-#ifndef GO1_CONTACT_ROLL
-#define GO1_CONTACT_ROLL 0
-#endif
-#ifndef GO1_PK_POINTS
-#define GO1_PK_POINTS 1
-#endif
-#ifndef GO1_PK_CONTACT
-#define GO1_PK_CONTACT 1
-#endif
-#ifndef GO1_TRUNK_PTS
-#define GO1_TRUNK_PTS 2
-#endif
 #define NDOF 12
 #define NB 17
 #define EPB 16          // envs per block of the reset kernel (4 lanes per env)
@@ -161,34 +134,21 @@ __device__ __forceinline__ float sel4(int i, float a0, float a1, float a2, float
 __device__ __forceinline__ float sel3(int i, const float* a) { return sel4(i, a[0], a[1], a[2], a[2]); }
 
 // ---------------------------------------------------------------- quad helpers
-#ifndef GO1_DPP
-#define GO1_DPP 1
-#endif
 // sum over the quad (lanes xor 1, 2) in the order (l0 + l1) + (l2 + l3); DPP quad_perm
 // moves stay in the VALU (no LDS round trip)
 __device__ __forceinline__ float qsum(float v) {
-#if GO1_DPP
   // update_dpp(0, ., bound_ctrl) lets the compiler fold the move into the add (v_add_f32_dpp)
   v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));  // [1,0,3,2]
   v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));  // [2,3,0,1]
-#else
-  v = v + __shfl_xor(v, 1);
-  v = v + __shfl_xor(v, 2);
-#endif
   return v;
 }
 
 // sum over the four 16-lane rows, (r0 + r1) + (r2 + r3): gfx950 v_permlane16/32_swap
 __device__ __forceinline__ float rowsum4(float p) {
-#if GO1_DPP
   auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(p), __float_as_uint(p), false, false);
   p = __uint_as_float(a[0]) + __uint_as_float(a[1]);
   auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-#else
-  p = p + __shfl_xor(p, 16);
-  return p + __shfl_xor(p, 32);
-#endif
 }
 
 // N independent row sums stage by stage (all permlane16 swaps, then their adds, then the
@@ -196,7 +156,6 @@ __device__ __forceinline__ float rowsum4(float p) {
 // the full swap latency, twice
 template <int N>
 __device__ __forceinline__ void rowsum4_n(float* v) {
-#if GO1_DPP
   float a[N], b[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -214,10 +173,6 @@ __device__ __forceinline__ void rowsum4_n(float* v) {
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] = a[i] + b[i];
-#else
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = rowsum4(v[i]);
-#endif
 }
 
 // N values that two bodies split between the row pairs (body L on rows 0-1, body H on rows 2-3):
@@ -226,7 +181,6 @@ __device__ __forceinline__ void rowsum4_n(float* v) {
 // lane.  Three VALU per value where two full row sums cost eight.
 template <int N>
 __device__ __forceinline__ void pairsum_rows_n(const float* v, float* lo, float* hi) {
-#if GO1_DPP
   float a[N], b[N], s[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -242,15 +196,6 @@ __device__ __forceinline__ void pairsum_rows_n(const float* v, float* lo, float*
     lo[i] = __uint_as_float(r[0]);
     hi[i] = __uint_as_float(r[1]);
   }
-#else
-  const bool low = (threadIdx.x & 63) < 32;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const float t = v[i] + __shfl_xor(v[i], 16), o = __shfl_xor(t, 32);
-    lo[i] = low ? t : o;
-    hi[i] = low ? o : t;
-  }
-#endif
 }
 
 // ---------------------------------------------------------------- actuator net
@@ -392,10 +337,6 @@ __device__ __forceinline__ void mlp_group3(const MlpFrag& F, const float* b0, co
       }
     t[g] = rowsum4(p) + F.b3;
   }
-#ifndef GO1_MLP_SGB  // VALU instructions after each layer-2 MFMA (0: the compiler's own order)
-#define GO1_MLP_SGB 3
-#endif
-#if GO1_MLP_SGB
   // the matrix pipe takes one v_mfma_f32_16x16x4_f32 per 32 cycles and the wave may issue ~6 VALU
   // instructions in that gap: layer 1 first, then each layer-2 MFMA followed by softsign work
 #pragma unroll
@@ -403,9 +344,8 @@ __device__ __forceinline__ void mlp_group3(const MlpFrag& F, const float* b0, co
 #pragma unroll
   for (int i = 0; i < 48; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, GO1_MLP_SGB, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
   }
-#endif
 }
 
 // ---------------------------------------------------------------- torch-order f32 math
@@ -1019,44 +959,6 @@ __device__ __forceinline__ void solve6p(const SIP& M, const float* b, float* x) 
 #undef LI
 }
 
-// The same solve by 3 x 3 blocks, M = [[A, B], [B^T, C]] (angular, linear): C^-1 and the Schur
-// complement S = A - B C^-1 B^T inverted by adjugates.  Both blocks are SPD (C ~ the mass, S the
-// rotational inertia about the moving COM), and the dependency depth is about half of the
-// Cholesky chain's (GO1_BASE_SCHUR).
-__device__ __forceinline__ void sym3_inv(float a00, float a01, float a02, float a11, float a12, float a22, float* k) {
-  k[0] = a11 * a22 - a12 * a12; k[1] = a02 * a12 - a01 * a22; k[2] = a01 * a12 - a02 * a11;
-  k[3] = a00 * a22 - a02 * a02; k[4] = a01 * a02 - a00 * a12; k[5] = a00 * a11 - a01 * a01;
-  const float id = frcp(a00 * k[0] + a01 * k[1] + a02 * k[2]);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) k[i] *= id;
-}
-__device__ __forceinline__ void solve6s(const SIP& M, const float* b, float* x) {
-  float Ci[6], Si[6], X[9], S[6];
-  sym3_inv(M.ac[0].y, M.ac[1].y, M.ac[2].y, M.ac[3].y, M.ac[4].y, M.ac[5].y, Ci);
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      X[3 * a + j] = M.b[3 * a] * Ci[s3i(0, j)] + M.b[3 * a + 1] * Ci[s3i(1, j)] + M.b[3 * a + 2] * Ci[s3i(2, j)];
-  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const int a = II[k], c = JJ[k];
-    S[k] = M.ac[k].x - (X[3 * a] * M.b[3 * c] + X[3 * a + 1] * M.b[3 * c + 1] + X[3 * a + 2] * M.b[3 * c + 2]);
-  }
-  sym3_inv(S[0], S[1], S[2], S[3], S[4], S[5], Si);
-  float bw[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) bw[a] = b[a] - (X[3 * a] * b[3] + X[3 * a + 1] * b[4] + X[3 * a + 2] * b[5]);
-#pragma unroll
-  for (int a = 0; a < 3; ++a) x[a] = Si[s3i(a, 0)] * bw[0] + Si[s3i(a, 1)] * bw[1] + Si[s3i(a, 2)] * bw[2];
-  float bv[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) bv[j] = b[3 + j] - (M.b[j] * x[0] + M.b[3 + j] * x[1] + M.b[6 + j] * x[2]);
-#pragma unroll
-  for (int j = 0; j < 3; ++j) x[3 + j] = Ci[s3i(j, 0)] * bv[0] + Ci[s3i(j, 1)] * bv[1] + Ci[s3i(j, 2)] * bv[2];
-}
-
 __device__ __forceinline__ void quat_to_R(const float* q, float* R) {
   float x = q[0], y = q[1], z = q[2], w = q[3];
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
@@ -1406,13 +1308,9 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
 // in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
-// WITH_TQ: the sub-step also runs the actuator net (tq_fn, which writes tau): it is called right
-// after the terrain reads are issued -- the torques are first needed by the bias pass -- so its
-// MFMA chain shares one scheduling region with the contact work (GO1_MLP_IN_SUB).
-template <bool WITH_TQ, class TqFn>
 __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
                                              float h, const float* g, float friction, float payload, const Terr& T,
-                                             int leg, int role, bool cf_out, float* cf_raw, TqFn&& tq_fn) {
+                                             int leg, int role, bool cf_out, float* cf_raw) {
 #pragma clang fp contract(on)
   // Model constants are compile-time literals (go1_model_consts.h, checked against the
   // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
@@ -1543,7 +1441,6 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       hq_fetch(T, pw[0].x, pw[1].x, qa);
       hq_fetch(T, pw[0].y, pw[1].y, qb);
     }
-    if constexpr (WITH_TQ) tq_fn();
     float Fa[3], Fb2[3], Ma[6], Mb[6];
     {
       const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
@@ -1613,7 +1510,6 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     for (int i = 0; i < 9; ++i) { cin[0].b[i] = SM[i].x; cin[1].b[i] = SM[i].y; }
   }
 #else  // ablation build only: no contacts
-  if constexpr (WITH_TQ) tq_fn();
   (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -1739,11 +1635,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     rhs[i] = -(p0[i].x + pp6[i].x);
     rhs[3 + i] = -(p0[i].y + pp6[i].y);
   }
-#if GO1_BASE_SCHUR
-  solve6s(I0, rhs, a0);
-#else
   solve6p(I0, rhs, a0);
-#endif
   MARK(base_solve_done);
   // ---- forward pass
   float qdd[3];
@@ -2081,7 +1973,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     org_x = K.ter.env_terrain_origin[(size_t)e * 3];
     org_y = K.ter.env_terrain_origin[(size_t)e * 3 + 1];
   }
-#if GO1_GLDS
   // every ordinary load of the prologue is waited for here, once: a use of an ordinary load
   // result while LDS-DMA is in flight would make the compiler wait vmcnt(0) for the DMA too.
   // The model block goes through VGPRs (ds_write after this wait): LDS written by DMA makes
@@ -2100,11 +1991,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int k = 0; k < (LDS_FLOATS + 63) / 64; ++k) s_phys[64 * k + lane] = mv[k];  // padded to 64
   }
-#else
-  for (int i = lane; i < LDS_FLOATS; i += 64)
-    s_phys[i] = i < GO1_MODEL_FLOATS ? c_gen->model[i] : c_gen->default_dof_pos[i - GO1_MODEL_FLOATS];
-  __syncthreads();
-#endif
   if (CI(terrain_kind) == 1) {
     T.tile = K.ter.tiles + (size_t)tix * 2 * CI(hf_nx) * CI(hf_ny);
     if (!INJ) {
@@ -2124,7 +2010,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       T.pj0 = (int)floorf(fminf(fmaxf(by / T.hs, -64.0f), (float)(CI(hf_ny) + 64))) - PSZY / 2;
       T.patch = &s_patch[el][0];
       const int nx = CI(hf_nx), ny = CI(hf_ny);
-#if GO1_GLDS
       // 4 x PSZX / 2 LDS-DMA dword loads per wave: load k of env el2 fills s_patch[el2]
       // dwords 64 k .. 64 k + 63, i.e. cells 32 k + lane / 2 (rows 2 k, 2 k + 1 of PSZY = 16
       // columns), floor (lane even) or ceiling (lane odd).
@@ -2144,23 +2029,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           __builtin_amdgcn_global_load_lds(tl + (layer_off + gi) * ny + gj, (float*)&s_patch[el2][0] + 64 * k, 4, 0, 0);
         }
       }
-#else
-      __shared__ int s_patch_meta[SEPB][3];
-      if (sub16 == 0) {
-        s_patch_meta[el][0] = tix;
-        s_patch_meta[el][1] = T.pi0;
-        s_patch_meta[el][2] = T.pj0;
-      }
-      __syncthreads();
-      for (int el2 = 0; el2 < SEPB; ++el2)
-        for (int cell = lane; cell < PSZX * PSZY; cell += 64) {
-          const int gi = min(max(s_patch_meta[el2][1] + cell / PSZY, 0), nx - 1);
-          const int gj = min(max(s_patch_meta[el2][2] + cell % PSZY, 0), ny - 1);
-          const float* tl = K.ter.tiles + (size_t)s_patch_meta[el2][0] * 2 * nx * ny;
-          s_patch[el2][cell] = make_float2(tl[((size_t)nx + gi) * ny + gj], tl[(size_t)gi * ny + gj]);
-        }
-      __syncthreads();
-#endif
     }
   }
   MARK(pro_dma_issued);
@@ -2181,9 +2049,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float cf_raw[6] = {0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
   const int dec = c->decimation;
   for (int sub = 0; sub < dec; ++sub) {
-    // _compute_torques (:957-996) as one closure: the actuator net runs inside the first
-    // integrator step of the sub-step (GO1_MLP_IN_SUB) or ahead of it
-    auto actuator = [&]() {
+    // _compute_torques (:957-996)
+    {
       // inputs of this lane's three joints ...
       const int slot = sub + 1;
       float xin[3][6];
@@ -2212,11 +2079,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
       for (int j = 0; j < 3; ++j) tq[j] = 0.0f * (b0[j] + b1v[j]);  // ablation build only: no actuator net
-#elif GO1_MLP3
-      mlp_group3(F, b0, b1v, tq);
 #else
-#pragma unroll
-      for (int j = 0; j < 3; ++j) tq[j] = mlp_group(F, b0[j], b1v[j]);
+      mlp_group3(F, b0, b1v, tq);
 #endif
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
@@ -2233,9 +2097,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float lim = tlim[j];
         torque[j] = clampf(t, -lim, lim);
       }
-    };
-    const bool in_sub = GO1_MLP_IN_SUB && !INJ;
-    if (!in_sub) actuator();
+    }
     if (INJ) {
       const float* id = A.inj_dof + ((size_t)sub * n + e) * NDOF * 2;
 #pragma unroll
@@ -2248,18 +2110,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int j = 0; j < 3; ++j) { P.q[j] = q[j]; P.qd[j] = qd[j]; }
 #ifndef GO1_ABL_NO_PHYS
-      // the first integrator step of the sub-step peeled (it may carry the actuator net)
-      const bool last0 = (sub == dec - 1) && (c->n_internal == 1);
-      if (in_sub)
-        phys_substep<true>(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last0, cf_raw, actuator);
-      else
-        phys_substep<false>(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last0, cf_raw, actuator);
-      for (int k = 1; k < c->n_internal; ++k) {
+      for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
-        phys_substep<false>(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw, actuator);
+        phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw);
       }
 #else
-      if (in_sub) actuator();
       P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];
 #endif
 #pragma unroll
@@ -2602,7 +2457,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (lane == 0) base = atomicAdd(A.episode_log_count, __popcll(rmask));
       base = __shfl(base, 0);
       log_row = base + __popcll(rmask & ((1ull << (4 * el)) - 1ull));
-      if (log_row >= A.episode_log_cap) log_row = -1;  // the host sized the buffer for the worst case
+      if (log_row >= A.episode_log_cap) log_row = -1;  // dropped; the count keeps it (the host reports overflow)
     }
   }
   if (reset && A.episode_log && (!compact || log_row >= 0)) {
@@ -2837,14 +2692,24 @@ __global__ void go1_finalize_kernel(int n, const int32_t* __restrict__ flag, con
   if (e < n && *flag) extras[e] = time_out[e];
 }
 
-// reset of masked envs (env.reset(), :46-55 of trajectory_tracking/__init__.py)
+// reset_idx (:218-296) of masked envs, or of a list of env ids (ids != nullptr: slot k of the
+// list -> env ids[k]; out-of-range ids skipped)
 __global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __restrict__ c_gen, go1_state st,
                                                         go1_terrain ter, const uint8_t* __restrict__ mask,
+                                                        const int32_t* __restrict__ ids, int n_ids,
                                                         const float* __restrict__ U, uint64_t seed, uint64_t step) {
   CCfg* __restrict__ c = (CCfg*)c_gen;
   const int leg = threadIdx.x & 3;
-  const int e = blockIdx.x * EPB + (threadIdx.x >> 2);
-  if (e >= c->n_envs || !mask[e]) return;
+  const int slot = blockIdx.x * EPB + (threadIdx.x >> 2);
+  int e;
+  if (ids) {
+    if (slot >= n_ids) return;
+    e = ids[slot];
+    if (e < 0 || e >= c->n_envs) return;
+  } else {
+    e = slot;
+    if (e >= c->n_envs || !mask[e]) return;
+  }
   const Rng rng = {U, seed, step, e, e + c->env_id_offset, c->u_per_env};
   float root[13], q[3], qd[3], strength[3], offset[3], traj[6];
   const float eo[3] = {ter.env_origins[(size_t)e * 3], ter.env_origins[(size_t)e * 3 + 1],
@@ -3050,14 +2915,33 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   return GO1_OK;
 }
 
-int go1_bind(go1_handle* h, const go1_state* s) {
-  if (!h || !s) return fail(GO1_E_ARG, "go1_bind: null argument");
+int go1_bind(go1_handle* h, const go1_state* s, const go1_plane* planes) {
+  if (!h || !s || !planes) return fail(GO1_E_ARG, "go1_bind: null argument (state and plane descriptors required)");
   const void* p[] = {s->root, s->dof_pos, s->dof_vel, s->last_actions, s->last_dof_vel, s->lag, s->pos_err_hist,
                      s->vel_hist, s->motor_strength, s->motor_offset, s->friction, s->restitution, s->payload,
                      s->episode_length, s->curr_pose_index, s->trajectory, s->base_rotation, s->collision_count,
                      s->episode_sums, s->joint_pos_target, s->feet_air_time, s->last_contacts};
-  for (const void* q : p)
-    if (!q) return fail(GO1_E_ARG, "go1_bind: every state plane must be non-null");
+  static_assert(sizeof(p) / sizeof(p[0]) == GO1_STATE_PLANES, "go1_state planes");
+  static const char* names[GO1_STATE_PLANES] = {
+      "root", "dof_pos", "dof_vel", "last_actions", "last_dof_vel", "lag", "pos_err_hist", "vel_hist",
+      "motor_strength", "motor_offset", "friction", "restitution", "payload", "episode_length",
+      "curr_pose_index", "trajectory", "base_rotation", "collision_count", "episode_sums", "joint_pos_target",
+      "feet_air_time", "last_contacts"};
+  const int64_t width[GO1_STATE_PLANES] = {13, 12, 12, 12, 12, 84, 24, 24, 12, 12, 1, 1, 1, 1, 1,
+                                           6 * (int64_t)h->cfg.traj_length, 3, 1, h->cfg.n_terms + 3, 12, 4, 4};
+  for (int i = 0; i < GO1_STATE_PLANES; ++i) {
+    const go1_plane& d = planes[i];
+    const int dt = (i == 13 || i == 14 || i == 17) ? GO1_DTYPE_I32 : GO1_DTYPE_F32;
+    if (!p[i]) return fail(GO1_E_ARG, std::string("go1_bind: state plane ") + names[i] + " is null");
+    if (d.rows != h->cfg.n_envs || d.cols != width[i] || d.dtype != dt)
+      return fail(GO1_E_ARG, std::string("go1_bind: state plane ") + names[i] + " must be (" +
+                                 std::to_string(h->cfg.n_envs) + ", " + std::to_string(width[i]) + ") " +
+                                 (dt == GO1_DTYPE_I32 ? "int32" : "float32"));
+    if (d.col_stride != 1 || (d.rows > 1 && d.row_stride != d.cols))
+      return fail(GO1_E_ARG, std::string("go1_bind: state plane ") + names[i] +
+                                 " is not dense row-major (strides " + std::to_string(d.row_stride) + ", " +
+                                 std::to_string(d.col_stride) + "): pass a contiguous tensor");
+  }
   h->st = *s;
   h->bound = true;
   return GO1_OK;
@@ -3161,7 +3045,18 @@ int go1_reset_envs(go1_handle* h, const uint8_t* mask, const float* uniforms, ui
   if (!h->bound || !h->has_terrain) return fail(GO1_E_STATE, "go1_reset_envs: bind state and terrain first");
   const int n = h->cfg.n_envs;
   hipLaunchKernelGGL(go1_reset_kernel, dim3((n + EPB - 1) / EPB), dim3(TPB), 0, (hipStream_t)stream, h->d_cfg,
-                     h->st, h->ter, mask, uniforms, rng_seed, rng_step);
+                     h->st, h->ter, mask, nullptr, 0, uniforms, rng_seed, rng_step);
+  HIP_TRY(hipGetLastError());
+  return GO1_OK;
+}
+
+int go1_reset_idx(go1_handle* h, const int32_t* ids, int32_t n_ids, const float* uniforms, uint64_t rng_seed,
+                  uint64_t rng_step, void* stream) {
+  if (!h || (!ids && n_ids > 0) || n_ids < 0) return fail(GO1_E_ARG, "go1_reset_idx: bad argument");
+  if (!h->bound || !h->has_terrain) return fail(GO1_E_STATE, "go1_reset_idx: bind state and terrain first");
+  if (n_ids == 0) return GO1_OK;  // reset_idx returns early on an empty list (:220-221)
+  hipLaunchKernelGGL(go1_reset_kernel, dim3((n_ids + EPB - 1) / EPB), dim3(TPB), 0, (hipStream_t)stream, h->d_cfg,
+                     h->st, h->ter, nullptr, ids, n_ids, uniforms, rng_seed, rng_step);
   HIP_TRY(hipGetLastError());
   return GO1_OK;
 }

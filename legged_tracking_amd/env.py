@@ -112,12 +112,20 @@ class EpisodeLogRing:
         self.env = env
         self.dev = device
         self.n = n
-        self.R = R = int(min(EPISODE_RING, max(4, (1 << 22) // max(n, 1))))  # <= 16 MB per half
+        # steps per half: R x n_envs <= 4 M (dense layout: R x n x W floats per half, e.g. 64 x 4096 x 16 x 4 B
+        # = 16 MB at the README size; at 256 k envs R = 16)
+        self.R = R = int(min(EPISODE_RING, max(4, (1 << 22) // max(n, 1))))
         self.W = W = abi.episode_log_width(len(env.reward_names))
         self.cuda = device.type == "cuda"
         self.compact = compact and self.cuda
+        self.dropped = 0  # compact rows the device had no room for (counted, never silently lost)
         if self.compact:
-            self.cap = R * n  # every env reset on every step of the half still fits
+            # Rows of one half: the resets of R steps.  Every env resetting on every step would need
+            # R x n rows (300 MB of (W + 2)-float rows per half at 256 k envs); the cap allows a quarter
+            # of the envs resetting on EVERY step of the half (timeouts alone are n / 500 per step) and
+            # at least 256 k rows.  The kernel counts every row it appends, kept or not (its atomic runs
+            # before the cap test), so an overflow shows up as count > cap on the host.
+            self.cap = min(R * n, max(4 * n, 1 << 18))
             self.prefix = min(self.cap, max(4 * n, 1024))
             self.buf = torch.zeros((2, self.cap, W + 2), device=device)
             self.count = torch.zeros((2, 1), dtype=torch.int32, device=device)
@@ -175,6 +183,12 @@ class EpisodeLogRing:
 
     def _half_rows(self, h, first, cnt, host):
         """Rows [first, cnt) of compact half h (host prefix + a synchronous fetch beyond it)."""
+        if cnt > self.cap:
+            import warnings
+            self.dropped += cnt - max(self.cap, first)
+            warnings.warn(f"episode log: {cnt - self.cap} rows beyond the ring's capacity {self.cap} were dropped "
+                          "(extras['episode_log_dropped'])")
+            cnt = self.cap
         p = min(cnt, self.prefix) if host else first
         parts = [self.host[h, first:p].numpy()] if host and p > first else []
         if cnt > max(p, first):
@@ -364,25 +378,25 @@ class LeggedRobot:
         self._aux = torch.zeros((n, abi.GO1_AUX), device=dev)
         # envs the native integrator's divergence guard reset, cumulative (extras["diverged"])
         self._diverged = torch.zeros(1, dtype=torch.int64, device=dev)
-        self._reset_mask = torch.zeros(n, dtype=torch.uint8, device=dev)
         # host RNG for the global gravity draws: identical on every rank
         self._host_rng = np.random.default_rng(self.seed)
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(self.seed * 1000003 + rank)
-        self._gen = gen
-        # _init_custom_buffers__ / _randomize_rigid_body_props (:1329-1350, :710-733)
+        self._n_global = n_global
+        self._reset_draws = 0
+        # _init_custom_buffers__ / _randomize_rigid_body_props (:1329-1350, :710-733): per-env draws
+        # keyed by GLOBAL env id (every rank draws the global vector and keeps its slice), so an
+        # N-rank run starts from exactly the state one rank with N x the envs does
         st = self._sim.state
         if dr.randomize_friction:
             lo, hi = dr.friction_range
-            st["friction"].copy_(torch.rand((n, 1), generator=gen, device=dev) * (hi - lo) + lo)
+            st["friction"].copy_(self._global_uniform(1, lo, hi))
         else:
             st["friction"].fill_(1.0)
         if dr.randomize_restitution:
             lo, hi = dr.restitution_range
-            st["restitution"].copy_(torch.rand((n, 1), generator=gen, device=dev) * (hi - lo) + lo)
+            st["restitution"].copy_(self._global_uniform(2, lo, hi))
         if dr.randomize_base_mass:
             lo, hi = dr.added_mass_range
-            st["payload"].copy_(torch.rand((n, 1), generator=gen, device=dev) * (hi - lo) + lo)
+            st["payload"].copy_(self._global_uniform(3, lo, hi))
         st["motor_strength"].fill_(1.0)
         # gravity (:1574 then :1221): sim gravity drawn, projection vector reset to -z
         self.common_step_counter = 0
@@ -397,6 +411,16 @@ class LeggedRobot:
         self.kernel_events = deque()
 
     # ------------------------------------------------------------------ host state
+    def _global_rng(self, tag):
+        """numpy Philox stream of (seed, tag): the same on every rank, indexed by global env id."""
+        return np.random.Generator(np.random.Philox(key=[self.seed, tag]))
+
+    def _global_uniform(self, tag, lo, hi):
+        """(n, 1) f32 U(lo, hi) for this rank's envs, element i = global env rank * n + i."""
+        u = self._global_rng(tag).random(self._n_global).astype(np.float32)
+        u = u[self.rank * self.num_envs:(self.rank + 1) * self.num_envs, None]
+        return torch.from_numpy(u * np.float32(hi - lo) + np.float32(lo)).to(self.device)
+
     def _randomize_gravity(self, external_force=None):
         """_randomize_gravity (:645-660): one global draw shared by every env (and rank)."""
         if external_force is not None:
@@ -433,6 +457,9 @@ class LeggedRobot:
         ex.set_lazy("time_outs", lambda: self._sim.sync_time_outs()[: self.num_train_envs])
         # native-integrator health (no reference counterpart): envs reset by the divergence guard so far
         ex.set_lazy("diverged", lambda: int(self._diverged.item()))
+        # compact episode-log rows that overflowed the device ring (0 unless a quarter of the envs reset
+        # on every step of a half)
+        ex.set_lazy("episode_log_dropped", lambda: (self._elog.drain(), self._elog.dropped)[1])
 
     def _deferred_time_outs(self):
         sim = self._sim
@@ -618,6 +645,9 @@ class LeggedRobot:
         env_ids = torch.as_tensor(env_ids, device=self.device).long().flatten()
         if env_ids.numel() == 0:
             return
+        if int(env_ids.min()) < -self.num_envs or int(env_ids.max()) >= self.num_envs:
+            raise IndexError(f"env id out of range for {self.num_envs} envs")  # as the reference's indexing
+        env_ids = torch.remainder(env_ids, self.num_envs)
         self._flush_episode_log()
         st = self._sim.state
         sums = st["episode_sums"][env_ids].cpu().numpy()
@@ -625,10 +655,7 @@ class LeggedRobot:
         for i, key in enumerate(self.sum_keys):
             self._train_ep["rew_" + key].extend(sums[:, i])
         self._train_ep["episode_length"].extend(ep)
-        mask = self._reset_mask
-        mask.zero_()
-        mask[env_ids] = 1
-        self._sim.reset_envs(mask, rng_seed=self.seed, rng_step=(1 << 62) + self._rng_step)
+        self._sim.reset_idx(env_ids, rng_seed=self.seed, rng_step=(1 << 62) + self._rng_step)
         self._rng_step += 1
         tb = self.time_out_buf[: self.num_train_envs]
         self._timeouts.extend(tb.cpu().numpy())
@@ -706,8 +733,11 @@ class TrajectoryTrackingEnv(LeggedRobot):
         # first); the reference then swaps in empty extras (trajectory_tracking/__init__.py:46-55),
         # so nothing logged before this reset reaches the new dicts
         self.reset_idx(torch.arange(self.num_envs, device=self.device))
-        self.episode_length_buf = torch.randint(int(self.max_episode_length), (self.num_envs,), device=self.device,
-                                                generator=self._gen, dtype=torch.int32)
+        # torch.randint(max_episode_length, (num_envs,)) (:49), keyed by global env id like the DR draws
+        self._reset_draws += 1
+        el = self._global_rng(1000 + self._reset_draws).integers(0, int(self.max_episode_length), self._n_global)
+        el = el[self.rank * self.num_envs:(self.rank + 1) * self.num_envs].astype(np.int32)
+        self.episode_length_buf = torch.from_numpy(el).to(self.device)
         self._elog.drain()  # into the old dicts (empty: reset_idx drained), never into the new ones
         self._train_ep, self._eval_ep, self._timeouts = _episode_dicts()
         self._install_extras()

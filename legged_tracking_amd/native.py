@@ -32,10 +32,11 @@ def lib():
     l.go1_abi_version.restype = C.c_int
     l.go1_last_error.restype = C.c_char_p
     l.go1_create.argtypes = [C.POINTER(abi.Go1Config), C.POINTER(C.c_void_p)]
-    l.go1_bind.argtypes = [C.c_void_p, C.POINTER(abi.Go1State)]
+    l.go1_bind.argtypes = [C.c_void_p, C.POINTER(abi.Go1State), C.POINTER(abi.Go1Plane)]
     l.go1_set_terrain.argtypes = [C.c_void_p, C.POINTER(abi.Go1Terrain)]
     l.go1_step.argtypes = [C.c_void_p, C.POINTER(abi.Go1StepArgs), C.c_void_p]
     l.go1_reset_envs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
+    l.go1_reset_idx.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]
     l.go1_sync_time_outs.argtypes = [C.c_void_p, C.c_void_p]
     l.go1_time_outs_pending.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     l.go1_actuator_net.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
@@ -71,7 +72,14 @@ def tunnel_tiles(cfg_terrain, layout, seed, device):
                             horizontal_scale=float(t.horizontal_scale), vertical_scale=float(t.vertical_scale),
                             ceiling_height=float(t.ceiling_height), p_flat=float(t.p_flat),
                             p_double=float(t.p_double))
-    ext = torch.as_tensor(np.ascontiguousarray(layout.extents, np.int32)).to(device)
+    ex = np.ascontiguousarray(layout.extents, np.int32)
+    span = np.stack([ex[:, 1] - ex[:, 0], ex[:, 3] - ex[:, 2]], 1)
+    bad = np.nonzero((span != np.array([layout.sub_shape[1], layout.sub_shape[0]])).any(1))[0]
+    if bad.size:  # the reference's tile[0, sx:ex, sy:ey] = top.T raises on this mismatch (tunnel.py:193-196)
+        k = int(bad[0])
+        raise ValueError(f"sub-terrain {k}: tunnel extent {tuple(span[k])} does not match the sub-terrain shape "
+                         f"{(layout.sub_shape[1], layout.sub_shape[0])} (could not broadcast)")
+    ext = torch.as_tensor(ex).to(device)
     rec = torch.empty((rows * cols, abi.GO1_TUNNEL_REC), dtype=torch.float64, device=device)
     tiles = torch.empty((rows, cols, 2, layout.tile_x, layout.tile_y), dtype=torch.float32, device=device)
     with torch.cuda.device(device):
@@ -117,7 +125,7 @@ class Go1Native:
         with torch.cuda.device(self.device):
             _check(lib().go1_create(C.byref(cfg), C.byref(self.h)))
             self.state = StateTensors(n, self.device, cfg)
-            _check(lib().go1_bind(self.h, C.byref(self.state.struct())))
+            self.bind(self.state)
             dev = self.device
             self.obs = torch.zeros((n, cfg.num_obs), device=dev)
             self.priv = torch.zeros((n, abi.GO1_NUM_PRIV), device=dev)
@@ -131,6 +139,13 @@ class Go1Native:
         self._consts = None
         self._lib_step = lib().go1_step
         self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+
+    def bind(self, state):
+        """go1_bind the planes of `state` (StateTensors or {name: tensor}); the library checks their
+        shapes, dtypes and strides and raises NativeError for anything but dense (n_envs, width)."""
+        t = state.t if hasattr(state, "t") else state
+        s = abi.Go1State(**{k: t[k].data_ptr() for k, _ in abi.Go1State._fields_})
+        _check(lib().go1_bind(self.h, C.byref(s), abi.plane_descs(t)))
 
     def set_terrain(self, tiles, env_tile, env_terrain_origin, env_origins):
         d = self.device
@@ -297,6 +312,14 @@ class Go1Native:
         out = (C.c_int64 * 3)()
         _check(lib().go1_time_outs_pending(self.h, out))
         return tuple(int(x) for x in out) if out[0] else None
+
+    def reset_idx(self, env_ids, uniforms=None, rng_seed=0, rng_step=0):
+        """go1_reset_idx for local env ids (any integer tensor; converted to int32 on the device)."""
+        ids = torch.as_tensor(env_ids, device=self.device).to(torch.int32).flatten().contiguous()
+        _check(lib().go1_reset_idx(self.h, ids.data_ptr(), int(ids.numel()),
+                                   None if uniforms is None else uniforms.data_ptr(), int(rng_seed), int(rng_step),
+                                   _stream()))
+        return ids  # keep alive until the stream passes it
 
     def reset_envs(self, mask, uniforms=None, rng_seed=0, rng_step=0):
         m = mask.to(torch.uint8).contiguous()

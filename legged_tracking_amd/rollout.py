@@ -598,7 +598,9 @@ class PPO:
     def update(self):
         A = PPO_Args
         ac = self.actor_critic
-        mean_value_loss = mean_surrogate_loss = mean_adapt = mean_adapt_test = 0.0
+        # the loss means accumulate on the device (ppo.py:186-187, 200-201 call .item() per mini-batch:
+        # a host sync each); one copy at the end.  The adaptive-LR rule's KL stays a host read.
+        acc = torch.zeros(4, dtype=torch.float32, device=self.device)  # value, surrogate, adapt, adapt_test
         gen = self.storage.mini_batch_generator(A.num_mini_batches, A.num_learning_epochs)
         for (obs_b, critic_obs_b, priv_b, hist_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b,
              old_sigma_b, masks_b, bins_b) in gen:
@@ -638,29 +640,29 @@ class PPO:
             self._allreduce_grads()
             nn.utils.clip_grad_norm_(ac.parameters(), A.max_grad_norm)
             self.optimizer.step()
-            mean_value_loss += value_loss.item()
-            mean_surrogate_loss += surrogate_loss.item()
+            acc[0] += value_loss.detach()
+            acc[1] += surrogate_loss.detach()
             num_train = int(priv_b.shape[0] // 5 * 4)
             for _ in range(A.num_adaptation_module_substeps):
                 pred = ac.adaptation_module(hist_b)
                 with torch.no_grad():
                     target = priv_b
-                sel = torch.linspace(0, pred.shape[1] - 1, steps=pred.shape[1], dtype=torch.long)
-                if A.selective_adaptation_module_loss:
-                    sel = 0
+                # every column (ppo.py:193: linspace(0, w - 1, w) as an index), or column 0
+                sel = 0 if A.selective_adaptation_module_loss else slice(None)
                 adapt_loss = F.mse_loss(pred[:num_train, sel], target[:num_train, sel])
                 adapt_test = F.mse_loss(pred[num_train:, sel], target[num_train:, sel])
                 self.adaptation_module_optimizer.zero_grad()
                 adapt_loss.backward()
                 self._allreduce_grads()
                 self.adaptation_module_optimizer.step()
-                mean_adapt += adapt_loss.item()
-                mean_adapt_test += adapt_test.item()
+                acc[2] += adapt_loss.detach()
+                acc[3] += adapt_test.detach()
         n_up = A.num_learning_epochs * A.num_mini_batches
         n_ad = n_up * A.num_adaptation_module_substeps
         self.storage.clear()
         if self.fused is not None:
             self.fused.pack()  # the rollout kernel reads the updated weights
+        mean_value_loss, mean_surrogate_loss, mean_adapt, mean_adapt_test = (float(x) for x in acc.cpu())
         return (mean_value_loss / n_up, mean_surrogate_loss / n_up, mean_adapt / n_ad, 0.0, 0.0,
                 mean_adapt_test / n_ad, 0.0, 0.0)
 

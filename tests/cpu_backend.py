@@ -70,6 +70,11 @@ class OracleBackend:
     def sync_time_outs(self):
         return self.extras_time_outs
 
+    def reset_idx(self, env_ids, uniforms=None, rng_seed=0, rng_step=0):
+        mask = torch.zeros(self.n, dtype=torch.uint8)
+        mask[torch.as_tensor(env_ids).long().cpu()] = 1
+        return self.reset_envs(mask, uniforms, rng_seed, rng_step)
+
     def reset_envs(self, mask, uniforms=None, rng_seed=0, rng_step=0):
         O.reset_envs(self.cfg, self.state.np, self.ter, mask.numpy().astype(np.uint8), rng_seed=rng_seed,
                      rng_step=rng_step)

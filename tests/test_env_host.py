@@ -141,23 +141,25 @@ def _shard_worker(rank, world, port, q):
         env = make_env(n=n_local, seed=5, cls=E.LeggedRobot)  # rank / world from torch.distributed
         assert (env.rank, env.world_size) == (rank, world) and env._abi_cfg.env_id_offset == rank * n_local
         g = np.random.default_rng(7)
-        fr, pl = g.uniform(0.1, 3.0, (n, 1)), g.uniform(-1, 3, (n, 1))
         el = g.integers(400, 500, n)
         acts = [g.normal(0, 1, (n, 12)).astype(np.float32) for _ in range(6)]
         sl = slice(rank * n_local, (rank + 1) * n_local)
 
-        def prep(e, s):
+        def prep(e, s):  # the construction-time DR draws (friction, restitution, payload) are the env's own
             e.reset_idx(torch.arange(e.num_envs))
-            e.state["friction"].copy_(torch.from_numpy(fr[s]))
-            e.state["payload"].copy_(torch.from_numpy(pl[s]))
-            e.state["restitution"].copy_(torch.from_numpy(pl[s] * 0.1))
-            e.episode_length_buf = torch.from_numpy(el[s].astype(np.int32))
+            e.episode_length_buf = torch.from_numpy(el[s].astype(np.int32))  # resets within the 6 steps
 
         prep(env, sl)
         outs = []
         for a in acts:
             obs, priv, rew, reset, _ = env.step(torch.from_numpy(a[sl]))
             outs.append(torch.cat([obs, priv, rew[:, None], reset[:, None].float()], 1))
+        dr = torch.cat([env.state[k] for k in ("friction", "restitution", "payload")], 1)
+        outs.append(torch.cat([dr, torch.zeros(n_local, local_w := outs[0].shape[1] - 3)], 1))
+        # TrajectoryTrackingEnv.reset's random episode lengths (:49), keyed by global env id too
+        te = make_env(n=n_local, seed=5)
+        te.reset()
+        outs.append(torch.cat([te.episode_length_buf[:, None].float(), torch.zeros(n_local, local_w + 2)], 1))
         local = torch.stack(outs)
         gathered = [torch.zeros_like(local) for _ in range(world)]
         dist.all_gather(gathered, local)
@@ -168,7 +170,14 @@ def _shard_worker(rank, world, port, q):
             for a in acts:
                 obs, priv, rew, reset, _ = full.step(torch.from_numpy(a))
                 ref.append(torch.cat([obs, priv, rew[:, None], reset[:, None].float()], 1))
+            w = ref[0].shape[1]
+            dr = torch.cat([full.state[k] for k in ("friction", "restitution", "payload")], 1)
+            ref.append(torch.cat([dr, torch.zeros(n, w - 3)], 1))
+            te = make_env(n=n, seed=5, rank=0, world=1)
+            te.reset()
+            ref.append(torch.cat([te.episode_length_buf[:, None].float(), torch.zeros(n, w - 1)], 1))
             ref = torch.stack(ref)
+            assert ref[-3, :, :3].std(0).min() > 0 and ref[-1, :, 0].std() > 0  # real draws, not constants
             got = torch.cat(gathered, 1)
             q.put(bool(torch.equal(got, ref)) and bool(ref[..., -1].any()))
     finally:

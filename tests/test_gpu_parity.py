@@ -371,3 +371,48 @@ def test_history_tap_and_deferred_time_outs_in_record():
         del keep
     assert rebinds > 0
     assert sb.rewards.abs().sum() > 0
+
+
+def test_bind_rejects_non_dense_or_mistyped_planes():
+    """go1_bind checks every plane's shape, dtype and strides (go1_plane): a strided view, a
+    transposed plane or a wrong dtype is rejected at the boundary, naming the plane."""
+    n = 64
+    cfg, c, td, ter, st, rng = _sim_setup(n)
+    g = native.Go1Native(c, DEV)
+    planes = dict(g.state.t)
+    bad = dict(planes, root=torch.zeros((n, 26), device=DEV)[:, ::2])  # (n, 13) view, row stride 26
+    with pytest.raises(native.NativeError, match="root.*dense"):
+        g.bind(bad)
+    bad = dict(planes, lag=torch.zeros((84, n), device=DEV).t())  # transposed (n, 84)
+    with pytest.raises(native.NativeError, match="lag"):
+        g.bind(bad)
+    bad = dict(planes, episode_length=torch.zeros((n, 1), device=DEV))  # float32 where int32 is required
+    with pytest.raises(native.NativeError, match="episode_length.*int32"):
+        g.bind(bad)
+    bad = dict(planes, dof_vel=torch.zeros((n + 16, 12), device=DEV))
+    with pytest.raises(native.NativeError, match="dof_vel"):
+        g.bind(bad)
+    g.bind(planes)  # the dense planes bind again
+
+
+def test_reset_idx_ids_match_mask_form():
+    """go1_reset_idx(ids) resets exactly the envs go1_reset_envs(mask) does, with the same draws;
+    duplicate ids reset once, out-of-range ids are skipped."""
+    n = 128
+    cfg, c, td, ter, st, rng = _sim_setup(n)
+    ga, gb = native.Go1Native(c, DEV), native.Go1Native(c, DEV)
+    for g in (ga, gb):
+        g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+        g.state.load(st.arrays)
+    ids = np.array([5, 77, 3, 77, 127, 0, 64], np.int64)
+    mask = np.zeros(n, bool)
+    mask[ids] = True
+    keep_a = ga.reset_idx(torch.from_numpy(np.append(ids, [n, -1, 10 * n])).to(DEV), rng_seed=4, rng_step=9)
+    keep_b = gb.reset_envs(torch.from_numpy(mask).to(DEV), rng_seed=4, rng_step=9)
+    torch.cuda.synchronize()
+    del keep_a, keep_b
+    sa, sb = ga.state.numpy(), gb.state.numpy()
+    for k in G.STATE_KEYS:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    assert not np.array_equal(sa["root"][mask], st["root"][mask])  # the listed envs did reset
+    np.testing.assert_array_equal(sa["root"][~mask], st["root"][~mask])

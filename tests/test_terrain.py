@@ -47,3 +47,19 @@ def test_full_readme_grid_tiles_bit_exact():
     np.testing.assert_array_equal(td.tiles[td.env_tile], d["static/env_height_samples"])
     np.testing.assert_array_equal(td.env_terrain_origin, d["static/env_terrain_origin"])
     np.testing.assert_array_equal(td.env_origins, d["static/env_origins"])
+
+
+def test_device_generator_rejects_extents_that_do_not_fit_the_sub_terrain():
+    """native.tunnel_tiles checks every tunnel extent against the SubTerrain shape before any device
+    work: the reference's tile[0, sx:ex, sy:ey] = top.T (tunnel.py:193-196) raises on a mismatch,
+    where the device rasteriser would extrapolate silently."""
+    import pytest
+    from legged_tracking_amd import native
+    cfg = CF.readme_config(n_envs=64, terrain="single_path", rows=4, cols=4)
+    lay = T.tunnel_layout(cfg.terrain)
+    span = np.stack([lay.extents[:, 1] - lay.extents[:, 0], lay.extents[:, 3] - lay.extents[:, 2]], 1)
+    assert (span == np.array([lay.sub_shape[1], lay.sub_shape[0]])).all()  # the README grid fits
+    lay.extents = lay.extents.copy()
+    lay.extents[5, 1] += 1
+    with pytest.raises(ValueError, match="sub-terrain 5"):
+        native.tunnel_tiles(cfg.terrain, lay, 11, "cpu")
