@@ -40,31 +40,33 @@ METRIC = "env-steps/sec (whole node) at 4096 Go1/GPU, 1/2/4/8 MI355X; %HBM roofl
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
 
-# Algorithmic HBM bytes per env-step of the fused kernel:
-#   reads : actions 48, root 52, dof pos/vel 96, lag 336, err/vel history 192, motor strength/offset 96,
-#           last actions/dof vel 96, friction/restitution/payload 12, episode length/pose index/collisions 12,
-#           trajectory 24, base rotation 12, episode sums 52, terrain index+origins 28,
-#           110 height samples x 2 layers x 4 B = 880                                  -> 1,936 B
-#   writes: obs 1044, priv 8, rew 4, reset/time-out/extras 3, contact forces 204, root 52, dof pos/vel 96,
-#           lag 336, err/vel history 192, last actions/dof vel 96, joint targets 48, strength/offset 96,
-#           trajectory 24, base rotation 12, episode sums 52, counters 12               -> 2,279 B
-BYTES_PER_ENV_STEP = 1936 + 2279
-# The VecEnv.step path additionally has the kernel write the HistoryWrapper's obs_history copy
-# (1,044 B) and the extras aux row (128 B); the compact episode log writes a 72-B row per reset env
-# only (~8 per step at 4096 envs: < 0.2 B per env-step, not counted).
-BYTES_PER_ENV_STEP_VECENV = BYTES_PER_ENV_STEP + 1044 + 128
+# Algorithmic HBM bytes per env-step, SURVEY.md 8(d) (the roofline's unit of work, fixed by the survey):
+#   reads 1,764 B = actions 48 + q 76 + qd 72 + actuator history 192 + 4 consumed lag slots 192 +
+#   last_actions 48 + last_dof_vel 48 + DR params 108 + episode/target state 48 + 13 episode sums 52 +
+#   220 height gathers 880; writes 1,758 B = q, qd 148 + history 192 + lag 192 + last_* 96 + obs 1,044 +
+#   priv 8 + rew/reset/timeout 6 + episode state 20 + sums 52.
+SURVEY_BYTES_PER_ENV_STEP = 3522
+# What the measured VecEnv.step path actually has to move per env-step, reported
+# beside it as bytes_written_by_path: the 8(d) items in this build's layout (lag ring 7 slots, the
+# 12-joint pose as root 13 + dof 24) plus the extras the VecEnv path asks the kernel for (contact
+# forces 204, aux row 128, joint targets 48, the HistoryWrapper's obs_history copy 1,044) -- DESIGN.md
+# section 5 lists the items.
+PATH_BYTES_PER_ENV_STEP = 4215 + 1044 + 128
 PREWARM_S = 0.25
-# Algorithmic FLOPs per env-step: actuator net 12 joints x 4 sub-steps x 2,688; the
-# integrator and post-physics are not counted here.
-FLOPS_PER_ENV_STEP = 12 * 4 * 2688
+# Algorithmic FLOPs per env-step, SURVEY.md 8(d): actuator MLP 132,144 (exact) + ABA / contact /
+# integration ~40,000 (estimate) + post-physics ~6,000 -> ~1.8e5.  The measured count (PMC VALU / MFMA
+# FLOP counters of the step kernel, profiles/r03/step_counters.json) is reported beside it.
+SURVEY_FLOPS_PER_ENV_STEP = 1.8e5
 
 # PMC-measured HBM bytes per launch of the step kernel (tools/profile.sh + tools/prof_summary.py;
 # FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  Re-collected whenever the kernel changes.
-TRAFFIC_FILES = [os.path.join(REPO, "profiles", r, "step_counters.json") for r in ("r02", "r01")]
+TRAFFIC_FILES = [os.path.join(REPO, "profiles", r, "step_counters.json") for r in ("r03", "r02", "r01")]
 
 
-def pmc_traffic(n_envs):
-    """HBM bytes per launch (raw FETCH+WRITE and with FETCH doubled), VALU issue fraction, source."""
+def pmc_counters(n_envs):
+    """From the newest committed PMC summary of the step kernel at this env count: HBM bytes per
+    launch (raw FETCH + WRITE, and with FETCH doubled), written bytes, counted FP32 FLOPs per launch
+    (None if that pass is absent), VALU issue fraction, source file."""
     for path in TRAFFIC_FILES:
         try:
             with open(path) as f:
@@ -74,10 +76,12 @@ def pmc_traffic(n_envs):
             pw = d.get("per_wave", {})
             valu = pw["SQ_ACTIVE_INST_VALU"] / pw["SQ_WAVE_CYCLES"] if "SQ_ACTIVE_INST_VALU" in pw else None
             h = d["hbm_bytes_per_launch"]
-            return h["traffic"], h.get("traffic_upper_fetch_doubled"), valu, os.path.relpath(path, REPO)
+            return dict(traffic=h["traffic"], traffic_x2=h.get("traffic_upper_fetch_doubled"),
+                        written=h.get("write"), flops=d.get("flops_per_launch"), valu=valu,
+                        src=os.path.relpath(path, REPO))
         except (OSError, KeyError, ValueError, ZeroDivisionError):
             continue
-    return None, None, None, None
+    return dict(traffic=None, traffic_x2=None, written=None, flops=None, valu=None, src=None)
 
 
 def hip():
@@ -251,6 +255,48 @@ def rollout_rate(n, dev, steps, warmup):
             "fused_policy": alg.fused is not None}
 
 
+def learn_rate(n, dev, iters=4, warmup=1):
+    """The whole training loop, as the reference's wandb train/fps measures it (ppo_cse/__init__.py:184:
+    (it + 1) x num_envs x num_steps_per_env / elapsed): Runner iterations of rollout (24 x [PPO.act +
+    VecEnv.step + record]), compute_returns (GAE) and PPO.update (5 epochs x 4 mini-batches, Adam, the
+    adaptation-module step), each phase bracketed by a device sync to split the time.  Checkpoint
+    writes (every 400 iterations in the reference) are outside the timed iterations."""
+    import torch
+    from legged_tracking_amd import rollout as R
+    env = make_env(n, 0, 1, dev)
+    runner = R.Runner(env, device=dev, save_dir=None)
+    alg, T = runner.alg, runner.num_steps_per_env
+    od = env.get_observations()
+    obs, priv, hist = od["obs"], od["privileged_obs"], od["obs_history"]
+    runner.alg.actor_critic.train()
+    split = {"rollout": 0.0, "gae": 0.0, "update": 0.0}
+    for it in range(warmup + iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.inference_mode():
+            obs, priv, hist, _ = runner.rollout(obs, priv, hist)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            alg.compute_returns(hist, priv)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+        alg.update()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        if it >= warmup:
+            split["rollout"] += t1 - t0
+            split["gae"] += t2 - t1
+            split["update"] += t3 - t2
+    env.close()
+    it_s = sum(split.values()) / iters
+    return {"value": n * T / it_s, "unit": "env-steps/s", "ms_per_iteration": it_s * 1e3, "iterations": iters,
+            "split_ms_per_iteration": {k: v / iters * 1e3 for k, v in split.items()},
+            "what": f"Runner iteration at {n} envs: {T} rollout steps + GAE + PPO.update "
+                    "(5 epochs x 4 mini-batches), env-steps/s as ppo_cse/__init__.py:184 computes train/fps; "
+                    "BASELINE.md derives ~8,960 (A100) and ~27,300 (A40) whole-loop env-steps/s from the "
+                    "reference's wandb runs (other configs)"}
+
+
 # ---------------------------------------------------------------------------- launcher
 def _free_port():
     s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
@@ -325,6 +371,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rollout", action="store_true")
+    ap.add_argument("--no-learn", action="store_true", help="skip the whole-training-loop leg")
+    ap.add_argument("--learn-only", action="store_true", help="profile helper: time only Runner iterations")
     ap.add_argument("--rollout-only", action="store_true", help="profile helper: time only the rollout loop")
     ap.add_argument("--event-every", type=int, default=4,
                     help="record the HIP event pair around every k-th step kernel of the timed loop")
@@ -358,6 +406,10 @@ def main():
     if args.rollout_only:
         torch.cuda.set_device(dev)
         print(json.dumps(rollout_rate(args.envs_per_gpu, dev, args.steps, args.warmup)))
+        return
+    if args.learn_only:
+        torch.cuda.set_device(dev)
+        print(json.dumps(learn_rate(args.envs_per_gpu, dev)))
         return
     dist = None
     if world > 1:
@@ -424,9 +476,21 @@ def main():
 
     if rank == 0:
         value = n_global * args.steps / elapsed
-        achieved_gbs = BYTES_PER_ENV_STEP_VECENV * n / (kernel_ms * 1e-3) / 1e9
-        achieved_tf = FLOPS_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e12
-        traffic, traffic_x2, valu_frac, traffic_src = pmc_traffic(n)
+        ks = kernel_ms * 1e-3
+        alg = SURVEY_BYTES_PER_ENV_STEP * n
+        achieved_gbs = alg / ks / 1e9
+        pmc = pmc_counters(n)
+        traffic = pmc["traffic"]
+        ratio = lambda t, b: None if t is None else t / b  # noqa: E731
+        fp32 = {"bound_note": "SURVEY 8(d): FP32 compute binds first (~50 flop/B)",
+                "survey_flops_per_env_step": SURVEY_FLOPS_PER_ENV_STEP,
+                "achieved_tflops_survey_flops": SURVEY_FLOPS_PER_ENV_STEP * n / ks / 1e12,
+                "frac_survey_flops": SURVEY_FLOPS_PER_ENV_STEP * n / ks / 1e12 / FP32_PEAK_TFLOPS,
+                "peak_tflops": FP32_PEAK_TFLOPS}
+        if pmc["flops"]:
+            fp32.update(counted_flops_per_launch=pmc["flops"], counted_flops_per_env_step=pmc["flops"] / n,
+                        achieved_tflops_counted=pmc["flops"] / ks / 1e12,
+                        frac_counted=pmc["flops"] / ks / 1e12 / FP32_PEAK_TFLOPS)
         ksteps = min(args.steps, 200)
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -441,14 +505,21 @@ def main():
                        "world_size_seen": world},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_fetch_doubled": traffic_x2,
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP_VECENV * n,
-                         "kernel": "go1_step_kernel<false>", "kernel_ms": kernel_ms,
-                         "bytes_per_env_step": BYTES_PER_ENV_STEP_VECENV,
-                         "fp32_tflops_actuator_only": achieved_tf,
-                         "fp32_frac_actuator_only": achieved_tf / FP32_PEAK_TFLOPS,
-                         "valu_issue_frac_pmc": valu_frac,
+                         "traffic_fetch_doubled": pmc["traffic_x2"],
+                         "traffic_over_algorithmic": ratio(traffic, alg),
+                         "traffic_over_algorithmic_fetch_doubled": ratio(pmc["traffic_x2"], alg),
+                         "write_traffic_over_algorithmic_writes": ratio(pmc["written"], 1758 * n),
+                         "traffic_source": pmc["src"],
+                         "algorithmic_bytes_per_launch": alg, "bytes_per_env_step": SURVEY_BYTES_PER_ENV_STEP,
+                         "bytes_source": "SURVEY.md 8(d): 3,522 B per env-step",
+                         "bytes_written_by_path": {"bytes_per_env_step": PATH_BYTES_PER_ENV_STEP,
+                                                   "achieved_gbs": PATH_BYTES_PER_ENV_STEP * n / ks / 1e9},
+                         "kernel": "go1_step_kernel<false, 7, true> (README-config specialisation)",
+                         "kernel_ms": kernel_ms,
+                         "kernel_ms_method": "hipExtLaunchKernelGGL start/stop events on the kernel's dispatch, "
+                                             "every k-th step of the timed loop, on the launch stream",
+                         "fp32": fp32,
+                         "valu_issue_frac_pmc": pmc["valu"],
                          "note": "latency/VALU-issue bound, not HBM bound: see DESIGN.md section 5"},
             "kernel_loop": {"value": n_global * ksteps / kdt, "unit": "env-steps/s", "ms_per_step": kdt / ksteps * 1e3,
                             "kernel_ms": max(p[3] for p in per_rank),
@@ -459,6 +530,8 @@ def main():
             line["sweep"] = [env_sweep(int(x), dev) for x in args.sweep.split(",")]
         if not args.no_rollout and world == 1:
             line["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24))
+        if not args.no_learn and world == 1:
+            line["learn"] = learn_rate(n, dev)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(n, budget_s=args.cpu_budget)
         print(json.dumps(line), flush=True)

@@ -24,6 +24,7 @@
 // integrator uses FMA contraction and native sin/cos (f32, compared with the
 // oracle's f64 integrator within a tolerance).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
@@ -2985,19 +2986,25 @@ int go1_step(go1_handle* h, const go1_step_args* a, void* stream) {
   if (a->episode_log_count && (!a->episode_log || a->episode_log_cap < 0 || h->cfg.indefinite_slots))
     return fail(GO1_E_ARG, "go1_step: a compact episode log needs episode_log, a capacity >= 0 and no indefinite "
                            "reward slots (their bucket pass rewrites rows by env)");
-  if (a->ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_begin, s));
+  // The optional event pair is attached to the kernel's own dispatch (hipExtLaunchKernelGGL: the
+  // events take the dispatch packet's start / end timestamps, as a profiler's kernel trace does),
+  // so ev_end - ev_begin is the kernel's duration without the queue work of separate event records.
+  hipEvent_t e0 = (hipEvent_t)a->ev_begin, e1 = (hipEvent_t)a->ev_end;
+  auto go = [&](auto kern) {
+    if (e0 || e1) hipExtLaunchKernelGGL(kern, grid, block, 0, s, e0, e1, 0, h->d_cfg, K);
+    else hipLaunchKernelGGL(kern, grid, block, 0, s, h->d_cfg, K);
+  };
   if (inj) {  // parity mode: the README configuration replays through the specialised kernel too
-    if (full) hipLaunchKernelGGL((go1_step_kernel<true, 15, false>), grid, block, 0, s, h->d_cfg, K);
-    else if (h->spec) hipLaunchKernelGGL((go1_step_kernel<true, 7, true>), grid, block, 0, s, h->d_cfg, K);
-    else hipLaunchKernelGGL((go1_step_kernel<true, 7, false>), grid, block, 0, s, h->d_cfg, K);
+    if (full) go(go1_step_kernel<true, 15, false>);
+    else if (h->spec) go(go1_step_kernel<true, 7, true>);
+    else go(go1_step_kernel<true, 7, false>);
   } else if (h->spec) {  // the README configuration (go1_spec.h): measure_front_half, 7 points per lane
-    hipLaunchKernelGGL((go1_step_kernel<false, 7, true>), grid, block, 0, s, h->d_cfg, K);
+    go(go1_step_kernel<false, 7, true>);
   } else {
-    if (full) hipLaunchKernelGGL((go1_step_kernel<false, 15, false>), grid, block, 0, s, h->d_cfg, K);
-    else hipLaunchKernelGGL((go1_step_kernel<false, 7, false>), grid, block, 0, s, h->d_cfg, K);
+    if (full) go(go1_step_kernel<false, 15, false>);
+    else go(go1_step_kernel<false, 7, false>);
   }
   HIP_TRY(hipGetLastError());
-  if (a->ev_end) HIP_TRY(hipEventRecord((hipEvent_t)a->ev_end, s));
   if (h->cfg.indefinite_slots) {
     hipLaunchKernelGGL(go1_bucket_kernel, dim3((n + 255) / 256), dim3(256), 0, s, h->d_cfg, h->st, h->d_bucket_r,
                        h->d_bucket_sum + bank * GO1_MAX_TERMS, h->d_bucket_sum + (bank ^ 1) * GO1_MAX_TERMS,

@@ -46,6 +46,31 @@ def main():
     print(f"{'section (code after marker)':32s} {'VALU':>6s} {'MFMA':>5s} {'VMEM':>5s} {'LDS':>5s} {'SALU':>5s}")
     for k, (v, mf, vm, ld, sa) in counts.items():
         print(f"{k:32s} {v:6d} {mf:5d} {vm:5d} {ld:5d} {sa:5d}")
+    # f32 arithmetic by class, scalar vs packed (the SQ_INSTS_VALU_{FMA,ADD,MUL}_F32 counters count a
+    # v_pk_* instruction once, tools/probes/flop_count.hip): the packed share of each class, for the
+    # FP32-roofline FLOP count (profiles/r03/step_counters.json "flops_per_launch")
+    cls = {"fma": (r"^v_(fma|fmac|fmaak|fmamk|mad|mac)_f32", r"^v_pk_fma_f32"),
+           "add": (r"^v_(add|sub|subrev)_f32", r"^v_pk_add_f32"),
+           "mul": (r"^v_mul_f32", r"^v_pk_mul_f32")}
+    tally = {c: [0, 0] for c in cls}
+    loop = {"mlp_done", "leg_kin_contacts_done", "integrate_done", "leg_kin_done", "backward_done", "base_solve_done",
+            "forward_done", "phys_begin"}
+    cur = "prologue"
+    for l in s[start:end]:
+        m = re.search(r"; MARK (\w+)", l)
+        if m:
+            cur = m.group(1)
+            continue
+        t = l.strip()
+        w = 4 if cur in loop else 1  # decimation 4 x n_internal 1
+        for c, (sc, pk) in cls.items():
+            if re.match(pk, t):
+                tally[c][1] += w
+            elif re.match(sc, t):
+                tally[c][0] += w
+    out = {c: {"scalar": a, "packed": b, "packed_share": b / max(a + b, 1)} for c, (a, b) in tally.items()}
+    import json
+    print(json.dumps({"weighted_static_f32_mix": out}))
 
 
 if __name__ == "__main__":

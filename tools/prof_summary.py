@@ -75,6 +75,28 @@ def main():
         write = means["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = {"fetch": fetch, "write": write, "traffic": fetch + write,
                                        "traffic_upper_fetch_doubled": 2 * fetch + write}
+    # FP32 FLOPs per launch from the VALU / MFMA FLOP counters.  SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32
+    # count instructions per wave, a packed v_pk_* instruction once (tools/probes/flop_count.hip,
+    # profiles/r03/flop_probe.json); SQ_INSTS_VALU_MFMA_MOPS_F32 x 512 = MFMA FLOPs.  The packed share
+    # of each class comes from the kernel's trip-count-weighted static ISA (tools/isa_sections.py ->
+    # <dst>/<tag>_isa_mix.json); without it the count is the lower bound (packed counted once).
+    if all(k in means for k in ("SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+                                "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_MFMA_MOPS_F32")):
+        pk = {"fma": 0.0, "add": 0.0, "mul": 0.0}
+        mix_path = os.path.join(dst, f"{tag}_isa_mix.json")
+        if os.path.exists(mix_path):
+            mix = json.load(open(mix_path))["weighted_static_f32_mix"]
+            pk = {k: mix[k]["packed_share"] for k in pk}
+        lanes = 64
+
+        def flops(p):
+            return lanes * (2 * means["SQ_INSTS_VALU_FMA_F32"] * (1 + p["fma"]) +
+                            means["SQ_INSTS_VALU_ADD_F32"] * (1 + p["add"]) +
+                            means["SQ_INSTS_VALU_MUL_F32"] * (1 + p["mul"]) +
+                            means["SQ_INSTS_VALU_TRANS_F32"]) + 512 * means["SQ_INSTS_VALU_MFMA_MOPS_F32"]
+        out["flops_per_launch"] = flops(pk)
+        out["flops_per_launch_lower_bound"] = flops({"fma": 0.0, "add": 0.0, "mul": 0.0})
+        out["flops_packed_share"] = pk
     if "SQ_WAVES" in means and means["SQ_WAVES"]:
         w = means["SQ_WAVES"]
         out["per_wave"] = {k: means[k] / w for k in means if k.startswith("SQ_") and k != "SQ_WAVES"}
