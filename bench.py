@@ -46,12 +46,17 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA
 #   220 height gathers 880; writes 1,758 B = q, qd 148 + history 192 + lag 192 + last_* 96 + obs 1,044 +
 #   priv 8 + rew/reset/timeout 6 + episode state 20 + sums 52.
 SURVEY_BYTES_PER_ENV_STEP = 3522
-# What the measured VecEnv.step path actually has to move per env-step, reported
-# beside it as bytes_written_by_path: the 8(d) items in this build's layout (lag ring 7 slots, the
-# 12-joint pose as root 13 + dof 24) plus the extras the VecEnv path asks the kernel for (contact
-# forces 204, aux row 128, joint targets 48, the HistoryWrapper's obs_history copy 1,044) -- DESIGN.md
-# section 5 lists the items.
-PATH_BYTES_PER_ENV_STEP = 4215 + 1044 + 128
+# What the measured VecEnv.step path actually moves per env-step (its own item list),
+# reported beside it as bytes_written_by_path:
+#   reads 1,696 B = actions 48, root 52, dof pos/vel 96, stored lag 96 (2 steps of scaled actions),
+#     err/vel history 192, motor strength/offset 96, last actions/dof vel 96, friction/restitution/payload
+#     12, episode length/pose index/collisions 12, trajectory 24, base rotation 12, episode sums 52,
+#     terrain index + origins 28, 110 height samples x 2 layers x 4 B = 880
+#   writes 2,047 B = obs 1,044, priv 8, rew 4, reset/time-out/extras 3, contact forces 204, aux 128,
+#     root 52, dof pos/vel 96, stored lag 96, err/vel history 192, last actions/dof vel 96, joint
+#     targets 48, base rotation 12, episode sums 52, counters 12 (motor strength/offset and the
+#     trajectory are written only on reset / DR steps: < 1 B per env-step)
+PATH_BYTES_PER_ENV_STEP = 1696 + 2047
 PREWARM_S = 0.25
 # Algorithmic FLOPs per env-step, SURVEY.md 8(d): actuator MLP 132,144 (exact) + ABA / contact /
 # integration ~40,000 (estimate) + post-physics ~6,000 -> ~1.8e5.  The measured count (PMC VALU / MFMA

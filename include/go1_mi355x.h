@@ -41,7 +41,13 @@ extern "C" {
 #define GO1_MAX_TERMS 16   /* reward terms with a nonzero scale (Cfg.reward_scales, :1380-1397) */
 #define GO1_MAX_SUMS (GO1_MAX_TERMS + 3) /* + total, total_pos, total_neg (:1400-1405) */
 #define GO1_NUM_PRIV 2
-#define GO1_LAG_SLOTS 7
+#define GO1_LAG_SLOTS 7    /* the reference's lag ring: lag_timesteps + 1 slots, pushed once per sim step */
+/* Stored lag: the scaled actions of the last GO1_LAG_STEPS(decimation) env steps.  Every env step pushes
+ * its scaled action `decimation` times into the reference's 7-slot ring (:973-974), so the ring is
+ * always those few actions, each repeated (slot 6 - j holds entry K - 1 - floor(j / decimation),
+ * K = GO1_LAG_STEPS); storing them instead of the ring moves 2 x 48 B per env-step at decimation 4
+ * instead of re-writing 7 x 48 B. */
+#define GO1_LAG_STEPS(dec) ((GO1_LAG_SLOTS + (dec) - 1) / (dec))
 #define GO1_MAX_TRAJ 16    /* waypoints per trajectory (Cfg.commands.traj_length) */
 #define GO1_U_NOISE 47     /* parity-mode uniform slots: 0..46 reset / DR draws, then one per obs column
                               (compute_observations noise, :472-473), then the trajectory draws */
@@ -190,7 +196,8 @@ typedef struct go1_state {
   float* dof_vel;          /* 12 */
   float* last_actions;     /* 12 */
   float* last_dof_vel;     /* 12 */
-  float* lag;              /* 84: 7 slots x 12, slot 0 oldest (:973-974) */
+  float* lag;              /* 12 x GO1_LAG_STEPS(decimation): scaled actions of the last steps, oldest
+                              first (the reference's 7-slot ring :973-974, stored compactly) */
   float* pos_err_hist;     /* 24: joint_pos_err_last, _last_last (:985-986) */
   float* vel_hist;         /* 24: joint_vel_last, _last_last */
   float* motor_strength;   /* 12 */

@@ -12,6 +12,11 @@ GO1_MAX_TERMS = 16
 GO1_MAX_SUMS = GO1_MAX_TERMS + 3
 GO1_NUM_PRIV = 2
 GO1_LAG_SLOTS = 7
+
+
+def lag_steps(decimation):
+    """GO1_LAG_STEPS: env steps the stored lag keeps (go1_state.lag = 12 x this many floats)."""
+    return (GO1_LAG_SLOTS + int(decimation) - 1) // int(decimation)
 GO1_MAX_TRAJ = 16
 GO1_U_NOISE = 47
 GO1_MODEL_FLOATS = 175
@@ -137,10 +142,10 @@ class Go1StepArgs(C.Structure):
 
 
 # state field widths and dtypes (must match go1_state order); None = set by the config:
-# trajectory 6 x traj_length, episode_sums n_terms + 3
+# lag 12 x GO1_LAG_STEPS(decimation), trajectory 6 x traj_length, episode_sums n_terms + 3
 STATE_SPEC = (
     ("root", 13, "f32"), ("dof_pos", 12, "f32"), ("dof_vel", 12, "f32"), ("last_actions", 12, "f32"),
-    ("last_dof_vel", 12, "f32"), ("lag", 84, "f32"), ("pos_err_hist", 24, "f32"), ("vel_hist", 24, "f32"),
+    ("last_dof_vel", 12, "f32"), ("lag", None, "f32"), ("pos_err_hist", 24, "f32"), ("vel_hist", 24, "f32"),
     ("motor_strength", 12, "f32"), ("motor_offset", 12, "f32"), ("friction", 1, "f32"),
     ("restitution", 1, "f32"), ("payload", 1, "f32"), ("episode_length", 1, "i32"),
     ("curr_pose_index", 1, "i32"), ("trajectory", None, "f32"), ("base_rotation", 3, "f32"),
@@ -151,9 +156,10 @@ assert tuple(n for n, _, _ in STATE_SPEC) == tuple(n for n, _ in Go1State._field
 
 
 def state_spec(cfg):
-    """[(name, width, dtype)] of the state planes for a go1_config (or anything with n_terms and
-    traj_length attributes)."""
-    w = {"trajectory": 6 * int(cfg.traj_length), "episode_sums": int(cfg.n_terms) + 3}
+    """[(name, width, dtype)] of the state planes for a go1_config (or anything with n_terms,
+    traj_length and decimation attributes)."""
+    w = {"trajectory": 6 * int(cfg.traj_length), "episode_sums": int(cfg.n_terms) + 3,
+         "lag": 12 * lag_steps(cfg.decimation)}
     return [(n, w.get(n, wd), dt) for n, wd, dt in STATE_SPEC]
 
 

@@ -1891,7 +1891,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const uint8_t rebind_val = rebind ? K.prev_time_out[e] : 0;
   if (blockIdx.x == 0 && lane == 0) K.flags[K.nxt] = 0;
   const size_t d0 = (size_t)e * NDOF + leg * 3;
-  const float* lag_in = st.lag + (size_t)e * 84 + leg * 3;
+  // stored lag (go1_state.lag): the scaled actions of the last K = GO1_LAG_STEPS(decimation) steps,
+  // oldest first; the README configuration (decimation 4) keeps K = 2 in the specialised kernel
+  const int dec = c->decimation;
+  constexpr int KMAX = SPEC ? 2 : GO1_LAG_SLOTS;
+  const int KL = SPEC ? 2 : GO1_LAG_STEPS(dec);
+  const float* lag_in = st.lag + (size_t)e * 12 * KL + leg * 3;
 
   // ---------------- load
   float act[3], q[3], qd[3], eh[2][3], vh[2][3], strength[3], offset[3];
@@ -1907,15 +1912,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     vh[0][j] = st.vel_hist[(size_t)e * 24 + leg * 3 + j];
     vh[1][j] = st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j];
   }
-  // per-joint constants and the lag-ring slots the sub-steps read (1..4 for decimation
-  // <= 4): loaded here so that no sub-step waits on a memory round trip
-  float dflt[3], tlim[3], lag_pre[GO1_LAG_SLOTS - 1][3];
+  // per-joint constants and the stored lag entries the sub-steps read: loaded here so that no
+  // sub-step waits on a memory round trip
+  float dflt[3], tlim[3], lag_pre[KMAX][3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     dflt[j] = c->default_dof_pos[leg * 3 + j];
     tlim[j] = c->torque_limits[leg * 3 + j];
 #pragma unroll
-    for (int sl = 0; sl < GO1_LAG_SLOTS - 1; ++sl) lag_pre[sl][j] = lag_in[(sl + 1) * 12 + j];
+    for (int k = 0; k < KMAX; ++k) lag_pre[k][j] = k < KL ? lag_in[k * 12 + j] : 0.0f;
   }
   const float friction = st.friction[e], payload = st.payload[e];
   // the env origin a reset needs, with the prologue loads (no memory round trip in the reset path)
@@ -2048,18 +2053,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // leaves the step as [old4, old5, old6, scaled x 4].
   float torque[3], tgt[3];
   float cf_raw[6] = {0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
-  const int dec = c->decimation;
   for (int sub = 0; sub < dec; ++sub) {
     // _compute_torques (:957-996)
     {
       // inputs of this lane's three joints ...
-      const int slot = sub + 1;
+      // the ring's oldest slot after this sub-step's push (:973-974) is old slot sub + 1, i.e. the
+      // scaled action of `back` steps ago (stored entry KL - back), or this step's for back = 0
+      const int m = 6 - sub;
+      const int back = m <= 0 ? 0 : (m + dec - 1) / dec;  // wave-uniform: scalar selects below
       float xin[3][6];
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        float lg = scaled[j];  // slot is wave-uniform: scalar-condition selects, no load in the loop
+        float lg = scaled[j];
 #pragma unroll
-        for (int sl = GO1_LAG_SLOTS - 2; sl >= 0; --sl) lg = slot == sl + 1 ? lag_pre[sl][j] : lg;
+        for (int k = 0; k < KMAX; ++k) lg = back == KL - k ? lag_pre[k][j] : lg;
         tgt[j] = lg + dflt[j];
         const float err = q[j] - tgt[j] + offset[j];
         xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
@@ -2223,7 +2230,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   MARK(post_kin_done);
   // DR every rand_interval (:822-824)
-  if (ep % CI(rand_interval) == 0) {
+  const bool dr_step = ep % CI(rand_interval) == 0;
+  if (dr_step) {
     const float sv = rng(34) * CI(strength_range) + CI(strength_lo);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -2638,23 +2646,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     st.dof_vel[dj] = pick(qd);
     st.last_actions[dj] = pick(act);
     st.last_dof_vel[dj] = pick(qd);
-    st.motor_strength[dj] = pick(strength);
-    st.motor_offset[dj] = pick(offset);
-    st.joint_pos_target[dj] = pick(tgt);
-    const float sj = pick(scaled);
-    // the surviving old slots come from the prologue's registers (lag_pre = slots 1..6): a
-    // reload of lag_in here put an L2 round trip on the critical path of every wave's end
-    float lagj[GO1_LAG_SLOTS - 1];
-#pragma unroll
-    for (int sl = 0; sl < GO1_LAG_SLOTS - 1; ++sl) lagj[sl] = pick(lag_pre[sl]);
-#pragma unroll
-    for (int s2 = 0; s2 < GO1_LAG_SLOTS; ++s2) {
-      const int src = s2 + dec;  // slot after `dec` pushes (dec >= 1: slot 0 never survives)
-      float v = sj;
-#pragma unroll
-      for (int sl = 0; sl < GO1_LAG_SLOTS - 1; ++sl) v = src == sl + 1 ? lagj[sl] : v;
-      st.lag[(size_t)e * 84 + s2 * 12 + leg * 3 + j] = reset ? 0.0f : v;
+    if (reset || dr_step) {  // changed only by a reset or the DR re-randomisation (:822-824)
+      st.motor_strength[dj] = pick(strength);
+      st.motor_offset[dj] = pick(offset);
     }
+    st.joint_pos_target[dj] = pick(tgt);
+    // stored lag shifts by one step: entries 1 .. KL - 1 (from the prologue's registers: a reload
+    // would put an L2 round trip at every wave's end), then this step's scaled action
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < KL) st.lag[(size_t)e * 12 * KL + k * 12 + leg * 3 + j] =
+          reset ? 0.0f : (k == KL - 1 ? pick(scaled) : pick(lag_pre[k + 1 < KMAX ? k + 1 : k]));
     st.pos_err_hist[(size_t)e * 24 + leg * 3 + j] = pick(eh[0]);
     st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j] = pick(eh[1]);
     st.vel_hist[(size_t)e * 24 + leg * 3 + j] = pick(vh[0]);
@@ -2726,7 +2728,8 @@ __global__ __launch_bounds__(TPB) void go1_reset_kernel(const go1_config* __rest
     st.last_actions[d0 + j] = 0.0f;
     st.last_dof_vel[d0 + j] = 0.0f;
 #pragma unroll
-    for (int s = 0; s < GO1_LAG_SLOTS; ++s) st.lag[(size_t)e * 84 + s * 12 + leg * 3 + j] = 0.0f;
+    for (int k = 0; k < GO1_LAG_STEPS(c->decimation); ++k)
+      st.lag[(size_t)e * 12 * GO1_LAG_STEPS(c->decimation) + k * 12 + leg * 3 + j] = 0.0f;
   }
   write_trajectory(c, rng, root, st.trajectory + (size_t)e * 6 * c->traj_length, leg, 4);
   st.feet_air_time[(size_t)e * 4 + leg] = 0.0f;  // (:248)
@@ -2821,7 +2824,9 @@ static bool spec_match(const go1_config& c) {
 #define GO1_SPEC_CHECK(f, v) m = m && spec_eq(c.f, (decltype(c.f))(v));
   GO1_SPEC_FIELDS(GO1_SPEC_CHECK)
 #undef GO1_SPEC_CHECK
-  return m;
+  // the specialised kernel keeps GO1_LAG_STEPS(4) = 2 stored lag entries in registers (the sub-step
+  // loop itself stays run-time)
+  return m && c.decimation == 4;
 }
 
 static int fail(int code, const std::string& msg) {
@@ -2928,7 +2933,8 @@ int go1_bind(go1_handle* h, const go1_state* s, const go1_plane* planes) {
       "motor_strength", "motor_offset", "friction", "restitution", "payload", "episode_length",
       "curr_pose_index", "trajectory", "base_rotation", "collision_count", "episode_sums", "joint_pos_target",
       "feet_air_time", "last_contacts"};
-  const int64_t width[GO1_STATE_PLANES] = {13, 12, 12, 12, 12, 84, 24, 24, 12, 12, 1, 1, 1, 1, 1,
+  const int64_t width[GO1_STATE_PLANES] = {13, 12, 12, 12, 12, 12 * GO1_LAG_STEPS(h->cfg.decimation), 24, 24, 12,
+                                           12, 1, 1, 1, 1, 1,
                                            6 * (int64_t)h->cfg.traj_length, 3, 1, h->cfg.n_terms + 3, 12, 4, 4};
   for (int i = 0; i < GO1_STATE_PLANES; ++i) {
     const go1_plane& d = planes[i];

@@ -62,7 +62,7 @@ STATE_FIELDS = (
     ("dof_vel", 12, "f32"),
     ("last_actions", 12, "f32"),
     ("last_dof_vel", 12, "f32"),
-    ("lag", 84, "f32"),             # 7 slots x 12, slot 0 oldest
+    ("lag", 24, "f32"),             # scaled actions of the last 2 steps (decimation 4), oldest first
     ("pos_err_hist", 24, "f32"),    # joint_pos_err_last, joint_pos_err_last_last
     ("vel_hist", 24, "f32"),        # joint_vel_last, joint_vel_last_last
     ("motor_strength", 12, "f32"),
@@ -78,3 +78,31 @@ STATE_FIELDS = (
     ("episode_sums", N_SUMS, "f32"),
     ("joint_pos_target", 12, "f32"),
 )
+
+
+# ---- the reference's lag ring (lag_buffer: LAG_SLOTS tensors, pushed once per sim step, :973-974)
+# and the stored form (go1_state.lag: the scaled actions of the last K = ceil(LAG_SLOTS / decimation)
+# env steps, oldest first).  A step pushes its scaled action `decimation` times, so ring slot 6 - j
+# (j pushes back) holds stored entry K - 1 - floor(j / decimation).
+def lag_ring_to_stored(ring, decimation):
+    """(n, LAG_SLOTS * 12) ring, slot 0 oldest -> (n, K * 12); raises if the ring is not of that form."""
+    import numpy as np
+    ring = np.asarray(ring).reshape(len(ring), LAG_SLOTS, 12)
+    K = (LAG_SLOTS + decimation - 1) // decimation
+    out = np.empty((ring.shape[0], K, 12), ring.dtype)
+    for k in range(K):
+        out[:, k] = ring[:, LAG_SLOTS - 1 - (K - 1 - k) * decimation]
+    if not np.array_equal(lag_stored_to_ring(out.reshape(len(ring), -1), decimation).reshape(ring.shape), ring):
+        raise ValueError("lag ring is not a sequence of per-step pushes of `decimation` copies")
+    return out.reshape(len(ring), K * 12)
+
+
+def lag_stored_to_ring(stored, decimation):
+    """(n, K * 12) stored lag -> (n, LAG_SLOTS * 12) ring, slot 0 oldest."""
+    import numpy as np
+    K = (LAG_SLOTS + decimation - 1) // decimation
+    stored = np.asarray(stored).reshape(len(stored), K, 12)
+    ring = np.empty((stored.shape[0], LAG_SLOTS, 12), stored.dtype)
+    for s in range(LAG_SLOTS):
+        ring[:, s] = stored[:, K - 1 - (LAG_SLOTS - 1 - s) // decimation]
+    return ring.reshape(len(stored), LAG_SLOTS * 12)

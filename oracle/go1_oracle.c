@@ -789,8 +789,10 @@ void go1o_physics(const go1_config* cfg, double* pos, double* quat, double* v, d
 /* ====================================================================== */
 /*                              the step                                   */
 /* ====================================================================== */
-static void compute_torques(const go1_config* c, const go1_state* st, int e, const float* act, float* torque) {
-  float* lag = st->lag + (size_t)e * 84;
+/* `lag` is the reference's 7-slot ring (lag_buffer, slot 0 oldest), expanded from the stored form by
+ * step_env (lag_expand) and stored back after the physics (lag_store) */
+static void compute_torques(const go1_config* c, const go1_state* st, int e, const float* act, float* torque,
+                            float* lag) {
   float* eh = st->pos_err_hist + (size_t)e * 24;
   float* vh = st->vel_hist + (size_t)e * 24;
   const float* dp = st->dof_pos + (size_t)e * NDOF;
@@ -919,7 +921,22 @@ static void reset_env(const go1_config* c, const go1_state* st, const go1_terrai
   for (int k = 0; k < ns; ++k) st->episode_sums[(size_t)e * ns + k] = 0.0f;
   for (int l = 0; l < 4; ++l) st->feet_air_time[(size_t)e * 4 + l] = 0.0f; /* (:248) */
   st->collision_count[e] = 0;
-  for (int i = 0; i < 84; ++i) st->lag[(size_t)e * 84 + i] = 0.0f;
+  const int K = GO1_LAG_STEPS(c->decimation);
+  for (int i = 0; i < 12 * K; ++i) st->lag[(size_t)e * 12 * K + i] = 0.0f;
+}
+
+/* go1_state.lag (the scaled actions of the last K = GO1_LAG_STEPS(decimation) steps, oldest first) <->
+ * the reference's ring of GO1_LAG_SLOTS per-sim-step pushes (:973-974): slot 6 - j is entry
+ * K - 1 - floor(j / decimation) */
+static void lag_expand(const go1_config* c, const float* stored, float* ring) {
+  const int K = GO1_LAG_STEPS(c->decimation);
+  for (int s = 0; s < GO1_LAG_SLOTS; ++s)
+    memcpy(ring + s * NDOF, stored + (K - 1 - (GO1_LAG_SLOTS - 1 - s) / c->decimation) * NDOF, NDOF * sizeof(float));
+}
+static void lag_store(const go1_config* c, const float* ring, float* stored) {
+  const int K = GO1_LAG_STEPS(c->decimation);
+  for (int k = 0; k < K; ++k)
+    memcpy(stored + k * NDOF, ring + (GO1_LAG_SLOTS - 1 - (K - 1 - k) * c->decimation) * NDOF, NDOF * sizeof(float));
 }
 
 int go1o_reset_envs(const go1_config* c, const go1_state* st, const go1_terrain* ter, const uint8_t* mask,
@@ -991,6 +1008,9 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     ox = ter->env_terrain_origin[(size_t)e * 3];
     oy = ter->env_terrain_origin[(size_t)e * 3 + 1];
   }
+  float ring[GO1_LAG_SLOTS * NDOF];
+  float* lag_st = st->lag + (size_t)e * 12 * GO1_LAG_STEPS(c->decimation);
+  lag_expand(c, lag_st, ring);
   PhysState S;
   if (!a->inj_dof) {
     for (int i = 0; i < 3; ++i) {
@@ -1005,7 +1025,7 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
     for (int d = 0; d < NDOF; ++d) { S.q[d] = dp[d]; S.qd[d] = dv[d]; }
   }
   for (int sub = 0; sub < c->decimation; ++sub) {
-    compute_torques(c, st, e, act, torque);
+    compute_torques(c, st, e, act, torque, ring);
     if (a->dbg_torques)
       for (int d = 0; d < NDOF; ++d) a->dbg_torques[((size_t)sub * n + e) * NDOF + d] = torque[d];
     if (a->inj_dof) {
@@ -1023,6 +1043,7 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
       for (int i = 0; i < NB * 3; ++i) cf[i] = (float)cfd[i];
     }
   }
+  lag_store(c, ring, lag_st);
   if (a->inj_dof) {
     for (int i = 0; i < 13; ++i) root[i] = a->inj_root[(size_t)e * 13 + i];
     for (int i = 0; i < NB * 3; ++i) cf[i] = a->inj_contact[(size_t)e * NB * 3 + i];

@@ -45,9 +45,10 @@ def lib(precision="f64"):
 
 
 class _Readme:
-    """Plane widths of the README configuration (10 reward terms, one waypoint)."""
+    """Plane widths of the README configuration (10 reward terms, one waypoint, decimation 4)."""
     n_terms = 10
     traj_length = 1
+    decimation = 4
 
 
 class NpState:

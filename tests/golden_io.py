@@ -27,7 +27,7 @@ def spec_match(c):
                 return False
         elif int(got) != int(val.rstrip("u")):
             return False
-    return True
+    return int(c.decimation) == 4  # go1_step.hip spec_match: two stored lag entries
 
 
 def load(name):
@@ -71,11 +71,23 @@ def sum_keys(d):
 
 
 def state_at(d, t, which="pre", cfg=None):
+    """The fixture's state before / after step t as an oracle NpState (the reference's 7-slot lag ring
+    converted to the stored form, layout.lag_ring_to_stored, which checks the ring's structure)."""
+    from legged_tracking_amd import layout as L
     n = d["s0/obs"].shape[0]
     init = {k: d[f"s{t}/{which}/{k}"] for k in STATE_KEYS if f"s{t}/{which}/{k}" in d.files}
     if cfg is None:
         cfg = fixture_config(d)[1]
+    if "lag" in init:
+        init["lag"] = L.lag_ring_to_stored(np.asarray(init["lag"]).reshape(n, -1), int(cfg.decimation))
     return O.NpState(n, init, cfg)
+
+
+def state_as_reference(st, key, cfg):
+    """State plane `key` of an NpState / numpy dict in the reference's layout (lag as the 7-slot ring)."""
+    from legged_tracking_amd import layout as L
+    v = st[key]
+    return L.lag_stored_to_ring(v, int(cfg.decimation)) if key == "lag" else v
 
 
 def terrain_of(d):

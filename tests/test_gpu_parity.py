@@ -338,7 +338,8 @@ def test_history_tap_and_deferred_time_outs_in_record():
     from legged_tracking_amd import env as E, rollout as R
     n, T = 256, 8
     cfg = CF.readme_config(n_envs=n, terrain="single_path", rows=4, cols=4)
-    env = E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device=DEV, cfg=cfg, seed=5, rank=0, world_size=1))
+    env = E.HistoryWrapper(E.TrajectoryTrackingEnv(sim_device=DEV, cfg=cfg, seed=5, rank=0, world_size=1),
+                           copy_history=True)
     assert env._tap
     env.reset()
     k = R.HipRolloutKernels()

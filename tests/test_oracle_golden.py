@@ -60,7 +60,8 @@ def test_oracle_replays_reference_steps(name):
         for k in G.STATE_KEYS:
             if k in ("episode_length", "curr_pose_index", "collision_count") or f"s{t}/post/{k}" not in d.files:
                 continue
-            np.testing.assert_allclose(st[k].reshape(d[f"s{t}/post/{k}"].shape), d[f"s{t}/post/{k}"], rtol=1e-4,
+            np.testing.assert_allclose(G.state_as_reference(st, k, c).reshape(d[f"s{t}/post/{k}"].shape),
+                                       d[f"s{t}/post/{k}"], rtol=1e-4,
                                        atol=2e-5, err_msg=f"step {t} state {k}")
         G.check_episode_log_and_extras(d, t, out["episode_log"], out["aux"])
         n_resets += int(d[f"s{t}/reset"].sum())
@@ -75,3 +76,28 @@ def test_readme_fixtures_match_the_specialised_kernel():
     for name in ("step_full_grid.npz", "step_single_path.npz", "step_single_path_events.npz"):
         assert G.spec_match(G.fixture_config(G.load(name))[1]), name
     assert not G.spec_match(G.fixture_config(G.load("step_plane.npz"))[1])
+
+
+def test_lag_ring_and_stored_form_round_trip():
+    """The reference's lag ring after any step is `decimation` pushes per step (:973-974), so the
+    stored form (scaled actions of the last GO1_LAG_STEPS steps) loses nothing; every fixture's ring
+    has that structure (lag_ring_to_stored raises otherwise)."""
+    from legged_tracking_amd import layout as L
+    rng = np.random.default_rng(0)
+    for dec in (1, 2, 3, 4, 5, 7, 8):
+        K = -(-7 // dec)
+        s = rng.normal(size=(5, K * 12)).astype(np.float32)
+        ring = L.lag_stored_to_ring(s, dec)
+        np.testing.assert_array_equal(L.lag_ring_to_stored(ring, dec), s)
+    bad = L.lag_stored_to_ring(rng.normal(size=(2, 24)).astype(np.float32), 4)
+    bad[0, 0] += 1.0
+    with pytest.raises(ValueError):
+        L.lag_ring_to_stored(bad, 4)
+    for name in FIXTURES:
+        d = G.load(name)
+        c = G.fixture_config(d)[1]
+        for t in range(int(d["meta/n_steps"])):
+            for which in ("pre", "post"):
+                if f"s{t}/{which}/lag" in d.files:
+                    ring = d[f"s{t}/{which}/lag"].reshape(c.n_envs, -1)
+                    np.testing.assert_array_equal(L.lag_stored_to_ring(L.lag_ring_to_stored(ring, 4), 4), ring)
