@@ -1,0 +1,557 @@
+"""numpy restatement of the velocity-tracking env step around the physics (BASELINE configs[1]).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker of the HIP velocity step -- never by
+the product path.  Every function cites the reference lines it restates; bare :N means
+go1_gym/envs/base/legged_robot_velocity_tracking.py, corl:N go1_gym/envs/rewards/corl_rewards.py,
+cur:N go1_gym/envs/base/curriculum.py.
+
+Arithmetic is f32 in the reference's operation order (numpy float32 ops are single IEEE operations,
+as torch's CPU kernels are), with these fixed conventions shared with the HIP kernel
+(go1_velocity.hip): 2- / 3- / 4-vector norms sqrt(fma(...)) as torch's CPU norm computes them,
+12-element sums ((x0 + x1) + x2 per leg, then (l0 + l1) + (l2 + l3)), 4-element sums
+(s0 + s1) + (s2 + s3) where torch's own order is unspecified.  The curriculum (Curriculum.sample /
+RewardThresholdCurriculum.update) is f64 like its numpy original.  Draws come in as uniforms: f32 in
+the VU_* layout, f64 (the curricula's RandomState) in the VD_* layout (legged_tracking_amd/
+vel_layout.py).
+
+State dict planes (reference layout): root (n,13), dof_pos, dof_vel, last_actions, last_last_actions,
+last_dof_vel (n,12), lag (n,84 ring, slot 0 oldest), pos_err_hist / vel_hist (n,24: last, last_last),
+motor_strength / motor_offset (n,12), friction / restitution / payload (n,1), episode_length (n,1 i32),
+joint_pos_target / last_joint_pos_target / last_last_joint_pos_target (n,12), commands (n,15),
+gait_indices (n,1), last_contacts (n,4), command_sums (n, T+5), episode_sums (n, T+1), command_bins /
+command_categories (n,1 i32), curriculum_weights (4, n_bins) f64.
+"""
+import math
+
+import numpy as np
+
+from legged_tracking_amd import layout as L, vel_layout as VL, velocity_config as V
+from oracle import oracle as O
+
+F = np.float32
+FEET = (4, 8, 12, 16)
+PENALISED = (2, 6, 10, 14, 3, 7, 11, 15)  # penalize_contacts_on ["thigh", "calf"] (go1_config.py:42)
+
+
+def f(x):
+    return np.asarray(x, np.float32)
+
+
+def fmaf(a, b, c):
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(np.float32)
+
+
+def norm2(x, y):
+    return np.sqrt(fmaf(y, y, f(x) * f(x)))
+
+
+def norm3(x, y, z):
+    return np.sqrt(fmaf(z, z, fmaf(y, y, f(x) * f(x))))
+
+
+def norm4(a, b, c, d):
+    return np.sqrt(fmaf(d, d, fmaf(c, c, fmaf(b, b, f(a) * f(a)))))
+
+
+def sum12(x):
+    x = f(x).reshape(-1, 4, 3)
+    leg = (x[:, :, 0] + x[:, :, 1]) + x[:, :, 2]
+    return (leg[:, 0] + leg[:, 1]) + (leg[:, 2] + leg[:, 3])
+
+
+def sum4(x):
+    x = f(x)
+    return (x[:, 0] + x[:, 1]) + (x[:, 2] + x[:, 3])
+
+
+def remainder(a, b):
+    """torch.remainder for floats: fmod, moved into the divisor's sign."""
+    a = f(a)
+    m = np.fmod(a, F(b))
+    adj = (m != 0) & ((F(b) < 0) != (m < 0))
+    return np.where(adj, m + F(b), m).astype(np.float32)
+
+
+def quat_rotate_inverse(q, v):
+    """isaacgym.torch_utils.quat_rotate_inverse (the C oracle's quat_rotate_inverse_f)."""
+    q, v = f(q), f(v)
+    qw = q[:, 3]
+    s = F(2.0) * (qw * qw) - F(1.0)
+    a = v * s[:, None]
+    c = np.stack([q[:, 1] * v[:, 2] - q[:, 2] * v[:, 1], q[:, 2] * v[:, 0] - q[:, 0] * v[:, 2],
+                  q[:, 0] * v[:, 1] - q[:, 1] * v[:, 0]], 1)
+    b = c * qw[:, None] * F(2.0)
+    d = q[:, 0] * v[:, 0] + q[:, 1] * v[:, 1] + q[:, 2] * v[:, 2]
+    e = q[:, :3] * d[:, None] * F(2.0)
+    return (a - b + e).astype(np.float32)
+
+
+def cross(a, b):
+    return np.stack([a[:, 1] * b[:, 2] - a[:, 2] * b[:, 1], a[:, 2] * b[:, 0] - a[:, 0] * b[:, 2],
+                     a[:, 0] * b[:, 1] - a[:, 1] * b[:, 0]], 1).astype(np.float32)
+
+
+def quat_apply(a, b):
+    """isaacgym.torch_utils.quat_apply: b + w t + xyz x t, t = 2 xyz x b."""
+    xyz = a[:, :3]
+    t = cross(xyz, b) * F(2)
+    return (b + a[:, 3:4] * t + cross(xyz, t)).astype(np.float32)
+
+
+def normalize4(q):
+    n = np.maximum(norm4(q[:, 0], q[:, 1], q[:, 2], q[:, 3]), F(1e-9))
+    return (q / n[:, None]).astype(np.float32)
+
+
+def quat_apply_yaw(q, v):
+    """math_utils.quat_apply_yaw (go1_gym/utils/math_utils.py:12-16)."""
+    qy = f(q).copy()
+    qy[:, :2] = 0
+    return quat_apply(normalize4(qy), f(v))
+
+
+def quat_from_angle_axis(angle, axis):
+    """torch_utils.quat_from_angle_axis for a unit coordinate axis: theta = angle / 2,
+    xyz = axis * sin(theta), w = cos(theta), then quat_unit."""
+    th = f(angle) / F(2)
+    s, c = np.sin(th).astype(np.float32), np.cos(th).astype(np.float32)
+    q = np.zeros((len(th), 4), np.float32)
+    for i in range(3):
+        q[:, i] = F(axis[i]) * s
+    q[:, 3] = c
+    return normalize4(q)
+
+
+def quat_mul(a, b):
+    """isaacgym.torch_utils.quat_mul (the factored product, tests/golden/refstubs)."""
+    x1, y1, z1, w1 = a[:, 0], a[:, 1], a[:, 2], a[:, 3]
+    x2, y2, z2, w2 = b[:, 0], b[:, 1], b[:, 2], b[:, 3]
+    ww = (z1 + x1) * (x2 + y2)
+    yy = (w1 - y1) * (w2 + z2)
+    zz = (w1 + y1) * (w2 - z2)
+    xx = ww + yy + zz
+    qq = F(0.5) * (xx + (z1 - x1) * (x2 - y2))
+    w = qq - ww + (z1 - y1) * (y2 - z2)
+    x = qq - xx + (x1 + w1) * (x2 + w2)
+    y = qq - yy + (w1 - x1) * (y2 + z2)
+    z = qq - zz + (z1 + y1) * (w2 - x2)
+    return np.stack([x, y, z, w], 1).astype(np.float32)
+
+
+def erf32(x):
+    return np.vectorize(math.erf, otypes=[np.float64])(f(x)).astype(np.float32)
+
+
+class Params:
+    """The constants the step reads, computed from a velocity Cfg the way the reference does."""
+
+    def __init__(self, cfg):
+        d = V.vel_derived(cfg)
+        self.cfg = cfg
+        self.dt = d["dt"]
+        self.max_ep = d["max_episode_length"]
+        self.resample_interval = d["resample_interval"]
+        self.rand_interval = d["rand_interval"]
+        self.cur_ep_len = d["curriculum_ep_len"]
+        self.scales = d["reward_scales"]
+        self.names = [k for k in self.scales if k != "termination"]
+        self.sum_keys = list(self.scales) + ["lin_vel_raw", "ang_vel_raw", "lin_vel_residual", "ang_vel_residual",
+                                             "ep_timesteps"]
+        self.ep_keys = list(self.scales) + ["total"]
+        self.grid, self.bin_sizes, self.w0 = V.curriculum_grid(cfg)
+        self.thresholds = {k: getattr(cfg.curriculum_thresholds, k) for k in V.TASK_KEYS}
+        self.cmd_scale = V.commands_scale(cfg)
+        r = cfg.rewards
+        self.tracking_sigma, self.tracking_sigma_yaw = F(r.tracking_sigma), F(r.tracking_sigma_yaw)
+        self.gait_force_sigma, self.gait_vel_sigma = F(r.gait_force_sigma), F(r.gait_vel_sigma)
+        self.kappa = F(r.kappa_gait_probs)
+        self.base_height_target = F(r.base_height_target)
+        self.sigma_rew_neg = F(r.sigma_rew_neg)
+        self.terminal_body_height = F(r.terminal_body_height)
+        lvl = cfg.noise.noise_level
+        ns, os_ = cfg.noise_scales, cfg.obs_scales
+        nv = np.zeros(VL.NUM_OBS, np.float32)
+        nv[0:3] = F(F(1.0) * F(ns.gravity)) * F(lvl)
+        nv[18:30] = F(F(F(1.0) * F(ns.dof_pos)) * F(lvl)) * F(os_.dof_pos)
+        nv[30:42] = F(F(F(1.0) * F(ns.dof_vel)) * F(lvl)) * F(os_.dof_vel)
+        self.noise_vec = nv
+        self.add_noise = bool(cfg.noise.add_noise)
+        self.obs_dof_pos, self.obs_dof_vel = F(os_.dof_pos), F(os_.dof_vel)
+        self.clip_obs, self.clip_actions = F(cfg.normalization.clip_observations), F(cfg.normalization.clip_actions)
+        fs, fsh = V.get_scale_shift(cfg.normalization.friction_range)
+        rs, rsh = V.get_scale_shift(cfg.normalization.restitution_range)
+        self.priv = (F(fsh), F(fs), F(rsh), F(rs))
+        dr = cfg.domain_rand
+        self.strength = (dr.motor_strength_range[1] - dr.motor_strength_range[0], dr.motor_strength_range[0])
+        self.offset = (dr.motor_offset_range[1] - dr.motor_offset_range[0], dr.motor_offset_range[0])
+        t = cfg.terrain
+        self.yaw = (t.yaw_init_range - (-t.yaw_init_range), -t.yaw_init_range)
+        self.base_init = f(list(cfg.init_state.pos) + list(cfg.init_state.rot) + list(cfg.init_state.lin_vel) +
+                           list(cfg.init_state.ang_vel))
+        self.default = f([cfg.init_state.default_joint_angles[n] for n in L.DOF_NAMES])
+        from legged_tracking_amd import config as CF
+        self.soft = CF.soft_dof_limits(cfg.rewards.soft_dof_pos_limit)
+        self.action_scale, self.hip_red = F(cfg.control.action_scale), F(cfg.control.hip_scale_reduction)
+        self.decimation = cfg.control.decimation
+        self.actuator = CF.load_actuator()
+
+
+# ---------------------------------------------------------------- curriculum (f64, numpy semantics)
+def curriculum_update(P, w, bins, success):
+    """RewardThresholdCurriculum.update (cur:135-154) for the envs of one category, in env order."""
+    w = w.copy()
+    sb = bins[success]
+    w[sb] = np.clip(w[sb] + 0.2, 0, 1)
+    rng = np.asarray(V.LOCAL_RANGE, np.float64)
+    for b in sb:  # get_local_bins (cur:123-133), one neighbourhood after the other
+        adj = np.logical_and(P.grid >= P.grid[:, b:b + 1] - rng[:, None],
+                             P.grid <= P.grid[:, b:b + 1] + rng[:, None]).all(axis=0)
+        idx = np.nonzero(adj)[0]
+        w[idx] = np.clip(w[idx] + 0.2, 0, 1)
+    return w
+
+
+def curriculum_sample(P, w, u_choice, u_cells):
+    """Curriculum.sample (cur:67-89) given the RandomState's uniforms: choice by inverse cdf,
+    then a uniform draw inside the chosen cell."""
+    p = w / w.sum()
+    cdf = p.cumsum()
+    cdf /= cdf[-1]
+    idx = np.searchsorted(cdf, u_choice, side="right")
+    cent = P.grid.T[idx]
+    low, high = cent + P.bin_sizes / 2, cent - P.bin_sizes / 2
+    return low + (high - low) * u_cells, idx
+
+
+def resample_commands(P, S, env_ids, u_cat, ud, vd_base):
+    """_resample_commands (:728-842) for env_ids: curriculum update per old category, new category
+    from u_cat, command sample, gaitwise edits, binary phases, small-command zeroing, sums reset."""
+    if len(env_ids) == 0:
+        return
+    ep_len = P.cur_ep_len
+    cats = S["command_categories"][:, 0]
+    for i in range(VL.N_CATEGORIES):
+        ids = env_ids[cats[env_ids] == i]
+        if len(ids) == 0:
+            continue
+        success = np.ones(len(ids), bool)
+        for k in V.TASK_KEYS:
+            if k in P.scales:
+                j = P.sum_keys.index(k)
+                tr = (S["command_sums"][ids, j] / F(ep_len)).astype(np.float32)
+                success &= tr > F(P.thresholds[k] * P.scales[k])
+        S["curriculum_weights"][i] = curriculum_update(P, S["curriculum_weights"][i],
+                                                       S["command_bins"][ids, 0].astype(np.int64), success)
+    p = 1.0 / VL.N_CATEGORIES
+    cat_new = np.full(len(env_ids), -1)
+    for i in range(VL.N_CATEGORIES):
+        cat_new[(F(p * i) <= u_cat) & (u_cat < F(p * (i + 1)))] = i
+    cmd = S["commands"]
+    for i in range(VL.N_CATEGORIES):
+        sel = cat_new == i
+        ids = env_ids[sel]
+        if len(ids) == 0:
+            continue
+        new, bins = curriculum_sample(P, S["curriculum_weights"][i], ud[ids, vd_base], ud[ids, vd_base + 1:vd_base + 16])
+        S["command_bins"][ids, 0] = bins
+        S["command_categories"][ids, 0] = i
+        cmd[ids] = new[:, :VL.NUM_COMMANDS].astype(np.float32)
+    for i in range(VL.N_CATEGORIES):  # gaitwise_curricula (:782-799)
+        ids = env_ids[cat_new == i]
+        if V.CATEGORIES[i] == "pronk":
+            for c in (5, 6, 7):
+                cmd[ids, c] = remainder(cmd[ids, c] / F(2) - F(0.25), 1)
+        elif V.CATEGORIES[i] == "trot":
+            cmd[ids, 5] = cmd[ids, 5] / F(2) + F(0.25)
+            cmd[ids, 6] = 0
+            cmd[ids, 7] = 0
+        elif V.CATEGORIES[i] == "pace":
+            cmd[ids, 5] = 0
+            cmd[ids, 6] = cmd[ids, 6] / F(2) + F(0.25)
+            cmd[ids, 7] = 0
+        elif V.CATEGORIES[i] == "bound":
+            cmd[ids, 5] = 0
+            cmd[ids, 6] = 0
+            cmd[ids, 7] = cmd[ids, 7] / F(2) + F(0.25)
+    for c in (5, 6, 7):  # binary_phases (:832-835): round half to even, / 2, % 1
+        cmd[env_ids, c] = remainder(np.round(F(2) * cmd[env_ids, c]) / F(2.0), 1)
+    keep = (norm2(cmd[env_ids, 0], cmd[env_ids, 1]) > F(0.2)).astype(np.float32)
+    cmd[env_ids, 0] = cmd[env_ids, 0] * keep
+    cmd[env_ids, 1] = cmd[env_ids, 1] * keep
+    S["command_sums"][env_ids] = 0
+
+
+# ---------------------------------------------------------------- gait clock (:844-923)
+def normal_cdf(P, x):
+    """torch.distributions.Normal(0, kappa).cdf: 0.5 (1 + erf((x - 0) * (1 / kappa) / sqrt(2)))."""
+    return (F(0.5) * (F(1) + erf32((f(x) - F(0)) * (F(1) / P.kappa) / F(math.sqrt(2))))).astype(np.float32)
+
+
+def step_contact_targets(P, S):
+    cmd = S["commands"]
+    freq, phases, offsets, bounds, durations = cmd[:, 4], cmd[:, 5], cmd[:, 6], cmd[:, 7], cmd[:, 8]
+    g = remainder(S["gait_indices"][:, 0] + F(P.dt) * freq, 1.0)
+    S["gait_indices"][:, 0] = g
+    fi = [g + phases + offsets + bounds, g + offsets, g + bounds, g + phases]
+    fi = [f(x) for x in fi]
+    foot_indices = remainder(np.stack(fi, 1), 1.0)
+    for idx in fi:
+        r = remainder(idx, 1)
+        stance, swing = r < durations, r > durations
+        idx[stance] = r[stance] * (F(0.5) / durations[stance])
+        idx[swing] = F(0.5) + (r[swing] - durations[swing]) * (F(0.5) / (F(1) - durations[swing]))
+    clock = np.stack([np.sin(F(2 * np.pi) * x) for x in fi], 1).astype(np.float32)
+    desired = np.zeros((len(g), 4), np.float32)
+    for i in range(4):
+        r = remainder(fi[i], 1.0)
+        desired[:, i] = normal_cdf(P, r) * (F(1) - normal_cdf(P, r - F(0.5))) + \
+            normal_cdf(P, r - F(1)) * (F(1) - normal_cdf(P, r - F(0.5) - F(1)))
+    return foot_indices, clock, desired
+
+
+# ---------------------------------------------------------------- rewards (corl:15-202)
+def reward_terms(P, S, q):
+    """q: dict of post-physics quantities.  Returns {name: unscaled term (n,)} (CoRLRewards)."""
+    cmd = S["commands"]
+    blv, bav, pg = q["blv"], q["bav"], q["pg"]
+    out = {}
+    for name in P.names:
+        if name == "tracking_lin_vel":
+            e = F(0)
+            d0, d1 = cmd[:, 0] - blv[:, 0], cmd[:, 1] - blv[:, 1]
+            e = d0 * d0 + d1 * d1
+            v = np.exp(-e / P.tracking_sigma)
+        elif name == "tracking_ang_vel":
+            d = cmd[:, 2] - bav[:, 2]
+            v = np.exp(-(d * d) / P.tracking_sigma_yaw)
+        elif name == "lin_vel_z":
+            v = blv[:, 2] * blv[:, 2]
+        elif name == "ang_vel_xy":
+            v = bav[:, 0] * bav[:, 0] + bav[:, 1] * bav[:, 1]
+        elif name == "orientation":
+            v = pg[:, 0] * pg[:, 0] + pg[:, 1] * pg[:, 1]
+        elif name == "torques":
+            v = sum12(q["torques"] * q["torques"])
+        elif name == "dof_vel":
+            v = sum12(S["dof_vel"] * S["dof_vel"])
+        elif name == "dof_acc":
+            a = (S["last_dof_vel"] - S["dof_vel"]) / F(P.dt)
+            v = sum12(a * a)
+        elif name == "action_rate":
+            a = S["last_actions"] - q["actions"]
+            v = sum12(a * a)
+        elif name == "collision":
+            cf = q["contact"]
+            hit = [(norm3(cf[:, b, 0], cf[:, b, 1], cf[:, b, 2]) > F(0.1)).astype(np.float32) for b in PENALISED]
+            v = ((hit[0] + hit[1]) + (hit[2] + hit[3])) + ((hit[4] + hit[5]) + (hit[6] + hit[7]))
+        elif name == "dof_pos_limits":
+            lo = np.minimum(S["dof_pos"] - P.soft[:, 0], F(0))
+            hi = np.maximum(S["dof_pos"] - P.soft[:, 1], F(0))
+            v = sum12(-lo + hi)
+        elif name == "jump":
+            d = S["root"][:, 2] - (cmd[:, 3] + P.base_height_target)
+            v = -(d * d)
+        elif name == "tracking_contacts_shaped_force":
+            cf = q["contact"]
+            t = [-(F(1) - q["desired"][:, i]) * (F(1) - np.exp(F(-1) * (ff * ff) / P.gait_force_sigma))
+                 for i, ff in enumerate(norm3(cf[:, b, 0], cf[:, b, 1], cf[:, b, 2]) for b in FEET)]
+            v = (((t[0] + t[1]) + t[2]) + t[3]) / F(4)
+        elif name == "tracking_contacts_shaped_vel":
+            fv = q["foot_vel"]
+            t = [-(q["desired"][:, i] * (F(1) - np.exp(F(-1) * (vv * vv) / P.gait_vel_sigma)))
+                 for i, vv in enumerate(norm3(fv[:, i, 0], fv[:, i, 1], fv[:, i, 2]) for i in range(4))]
+            v = (((t[0] + t[1]) + t[2]) + t[3]) / F(4)
+        elif name == "dof_pos":
+            d = S["dof_pos"] - P.default
+            v = sum12(d * d)
+        elif name == "action_smoothness_1":
+            d = S["joint_pos_target"] - S["last_joint_pos_target"]
+            v = sum12((d * d) * (S["last_actions"] != 0))
+        elif name == "action_smoothness_2":
+            d = S["joint_pos_target"] - F(2) * S["last_joint_pos_target"] + S["last_last_joint_pos_target"]
+            v = sum12((d * d) * (S["last_actions"] != 0) * (S["last_last_actions"] != 0))
+        elif name == "feet_slip":
+            cf = q["contact"]
+            contact = np.stack([cf[:, b, 2] > F(1) for b in FEET], 1)
+            filt = contact | (S["last_contacts"] > 0)
+            S["last_contacts"][:] = contact.astype(np.float32)  # the reward function updates it (corl:110)
+            fv = q["foot_vel"]
+            sp = norm2(fv[:, :, 0], fv[:, :, 1])
+            v = sum4(filt * (sp * sp))
+        elif name == "feet_clearance_cmd_linear":
+            ph = F(1) - np.abs(F(1.0) - np.clip(q["foot_indices"] * F(2.0) - F(1.0), F(0), F(1)) * F(2.0))
+            tgt = cmd[:, 9:10] * ph + F(0.02)
+            d = tgt - q["foot_pos"][:, :, 2]
+            v = sum4((d * d) * (F(1) - q["desired"]))
+        elif name == "orientation_control":
+            rp = cmd[:, 10:12]
+            qr = quat_from_angle_axis(-rp[:, 1], (1, 0, 0))
+            qp = quat_from_angle_axis(-rp[:, 0], (0, 1, 0))
+            dq = quat_mul(qr, qp)
+            gv = np.broadcast_to(q["gravity_vec_after"], (len(rp), 3)).astype(np.float32)
+            dpg = quat_rotate_inverse(dq, gv)
+            d0, d1 = pg[:, 0] - dpg[:, 0], pg[:, 1] - dpg[:, 1]
+            v = d0 * d0 + d1 * d1
+        elif name == "raibert_heuristic":
+            base = S["root"][:, 0:3]
+            qc = S["root"][:, 3:7].copy()
+            qc[:, :3] = -qc[:, :3]  # quat_conjugate
+            fb = np.stack([quat_apply_yaw(qc, q["foot_pos"][:, i, :] - base) for i in range(4)], 1)
+            w = cmd[:, 12:13]
+            ys = np.concatenate([w / F(2), -w / F(2), w / F(2), -w / F(2)], 1)
+            ln = cmd[:, 13:14]
+            xs = np.concatenate([ln / F(2), ln / F(2), -ln / F(2), -ln / F(2)], 1)
+            ph = np.abs(F(1.0) - (q["foot_indices"] * F(2.0))) * F(1.0) - F(0.5)
+            freq = cmd[:, 4:5]
+            y_vel = cmd[:, 2:3] * ln / F(2)
+            yo = ph * y_vel * (F(0.5) / freq)
+            yo[:, 2:4] *= F(-1)
+            xo = ph * cmd[:, 0:1] * (F(0.5) / freq)
+            ex = np.abs((xs + xo) - fb[:, :, 0])
+            ey = np.abs((ys + yo) - fb[:, :, 1])
+            v = sum4(ex * ex + ey * ey)
+        else:
+            raise NotImplementedError(name)
+        out[name] = f(v)
+    return out
+
+
+# ---------------------------------------------------------------- the step
+def compute_torques(P, S, act, dof_pos, dof_vel):
+    """_compute_torques (:925-964) for one sim step: lag push, actuator net on the histories."""
+    scaled = (act * P.action_scale).astype(np.float32)
+    scaled[:, [0, 3, 6, 9]] *= P.hip_red
+    lag = S["lag"].reshape(-1, 7, 12)
+    lag[:, :-1] = lag[:, 1:].copy()
+    lag[:, -1] = scaled
+    jpt = (lag[:, 0] + P.default).astype(np.float32)
+    err = (dof_pos - jpt + S["motor_offset"]).astype(np.float32)
+    eh = S["pos_err_hist"].reshape(-1, 2, 12)
+    vh = S["vel_hist"].reshape(-1, 2, 12)
+    x = np.stack([err, eh[:, 0], eh[:, 1], dof_vel, vh[:, 0], vh[:, 1]], -1).reshape(-1, 6)
+    t = O.actuator(P.actuator, x).reshape(-1, 12)
+    eh[:, 1], eh[:, 0] = eh[:, 0].copy(), err
+    vh[:, 1], vh[:, 0] = vh[:, 0].copy(), dof_vel
+    t = (t * S["motor_strength"]).astype(np.float32)
+    S["joint_pos_target"][:] = jpt
+    return np.clip(t, F(-33.5), F(33.5)).astype(np.float32)
+
+
+def reset_envs(P, S, ids, u, env_origins):
+    """reset_idx (:168-257) after _resample_commands: DR, dofs, root, buffers (draws from u)."""
+    sr, sl = P.strength
+    S["motor_strength"][ids] = (u[ids, VL.VU_RESET_STRENGTH:VL.VU_RESET_STRENGTH + 1] * F(sr) + F(sl))
+    orng, olo = P.offset
+    S["motor_offset"][ids] = u[ids, VL.VU_RESET_STRENGTH + 1:VL.VU_RESET_STRENGTH + 13] * F(orng) + F(olo)
+    S["dof_pos"][ids] = P.default * ((F(1.5) - F(0.5)) * u[ids, VL.VU_RESET_DOF:VL.VU_RESET_DOF + 12] + F(0.5))
+    S["dof_vel"][ids] = 0
+    r = np.broadcast_to(P.base_init, (len(ids), 13)).copy()
+    r[:, :3] = r[:, :3] + env_origins[ids]
+    yr, ylo = P.yaw
+    yaw = F(yr) * u[ids, VL.VU_RESET_YAW] + F(ylo)
+    r[:, 3:7] = quat_from_angle_axis(yaw, (0, 0, 1))
+    r[:, 7:13] = F(0.5 - (-0.5)) * u[ids, VL.VU_RESET_VEL:VL.VU_RESET_VEL + 6] + F(-0.5)
+    S["root"][ids] = r
+    for k in ("last_actions", "last_last_actions", "last_dof_vel"):
+        S[k][ids] = 0
+    S["episode_length"][ids] = 0
+    S["gait_indices"][ids] = 0
+    S["lag"][ids] = 0
+
+
+def step(P, S, actions, inj, u, ud, gravity_vec, gravity_vec_after, env_origins):
+    """One VelocityTrackingEasyEnv.step (:60-106, velocity_tracking/__init__.py:22-44) with injected
+    physics (inj: dof (dec, n, 12, 2), root (n, 13), contact (n, 17, 3), feet (n, 4, 6) pos + vel).
+    Mutates S; returns the outputs."""
+    n = len(actions)
+    act = np.clip(f(actions), -P.clip_actions, P.clip_actions)
+    torques = None
+    for sub in range(P.decimation):
+        torques = compute_torques(P, S, act, S["dof_pos"].copy(), S["dof_vel"].copy())
+        S["dof_pos"][:] = inj["dof"][sub][..., 0]
+        S["dof_vel"][:] = inj["dof"][sub][..., 1]
+    S["root"][:] = inj["root"]
+    # post_physics_step (:108-154)
+    S["episode_length"][:, 0] += 1
+    ep = S["episode_length"][:, 0]
+    quat = S["root"][:, 3:7]
+    q = {"blv": quat_rotate_inverse(quat, S["root"][:, 7:10]), "bav": quat_rotate_inverse(quat, S["root"][:, 10:13]),
+         "pg": quat_rotate_inverse(quat, np.broadcast_to(f(gravity_vec), (n, 3))),
+         "foot_pos": f(inj["feet"][:, :, 0:3]), "foot_vel": f(inj["feet"][:, :, 3:6]), "contact": f(inj["contact"]),
+         "torques": torques, "actions": act, "gravity_vec_after": f(gravity_vec_after)}
+    ids_a = np.nonzero(ep % P.resample_interval == 0)[0]
+    resample_commands(P, S, ids_a, u[ids_a, VL.VU_CAT_A], ud, VL.VD_CHOICE_A)
+    q["foot_indices"], clock, q["desired"] = step_contact_targets(P, S)
+    dr = np.nonzero(ep % P.rand_interval == 0)[0]  # _randomize_dof_props (:715-717)
+    sr, sl = P.strength
+    S["motor_strength"][dr] = u[dr, VL.VU_DR_STRENGTH:VL.VU_DR_STRENGTH + 1] * F(sr) + F(sl)
+    orng, olo = P.offset
+    S["motor_offset"][dr] = u[dr, VL.VU_DR_STRENGTH + 1:VL.VU_DR_STRENGTH + 13] * F(orng) + F(olo)
+    # check_termination (:156-166)
+    cf = q["contact"]
+    reset = norm3(cf[:, 0, 0], cf[:, 0, 1], cf[:, 0, 2]) > F(1)
+    time_out = ep.astype(np.float32) > F(P.max_ep)
+    reset |= time_out
+    reset |= S["root"][:, 2] < P.terminal_body_height
+    # compute_reward (:281-318)
+    terms = reward_terms(P, S, q)
+    rew = np.zeros(n, np.float32)
+    pos = np.zeros(n, np.float32)
+    neg = np.zeros(n, np.float32)
+    for name in P.names:
+        r = (terms[name] * F(P.scales[name])).astype(np.float32)
+        rew = rew + r
+        s = np.float64(r.astype(np.float64).sum())
+        if s >= 0:
+            pos = pos + r
+        elif s <= 0:
+            neg = neg + r
+        j = P.ep_keys.index(name)
+        S["episode_sums"][:, j] += r
+        k = P.sum_keys.index(name)
+        if name in ("tracking_contacts_shaped_force", "tracking_contacts_shaped_vel"):
+            S["command_sums"][:, k] += F(P.scales[name]) + r
+        else:
+            S["command_sums"][:, k] += r
+    cfg = P.cfg
+    if cfg.rewards.only_positive_rewards:
+        rew = np.maximum(rew, F(0))
+    elif cfg.rewards.only_positive_rewards_ji22_style:
+        rew = (pos * np.exp(neg / P.sigma_rew_neg)).astype(np.float32)
+    S["episode_sums"][:, -1] += rew
+    cs = S["command_sums"]
+    T = len(P.scales)
+    cs[:, T] += q["blv"][:, 0]
+    cs[:, T + 1] += q["bav"][:, 2]
+    d = q["blv"][:, 0] - S["commands"][:, 0]
+    cs[:, T + 2] += d * d
+    d = q["bav"][:, 2] - S["commands"][:, 2]
+    cs[:, T + 3] += d * d
+    cs[:, T + 4] += F(1)
+    # reset_idx (:168-257)
+    ids_b = np.nonzero(reset)[0]
+    episode_log = None
+    if len(ids_b):
+        resample_commands(P, S, ids_b, u[ids_b, VL.VU_CAT_B], ud, VL.VD_CHOICE_B)
+        reset_envs(P, S, ids_b, u, env_origins)
+        episode_log = {("rew_" + k): f(S["episode_sums"][ids_b, j]).copy() for j, k in enumerate(P.ep_keys)}
+        S["episode_sums"][ids_b] = 0
+    # compute_observations (:320-509)
+    cmd = S["commands"]
+    obs = np.concatenate([q["pg"], cmd * P.cmd_scale, (S["dof_pos"] - P.default) * P.obs_dof_pos,
+                          S["dof_vel"] * P.obs_dof_vel, act, S["last_actions"], clock], 1).astype(np.float32)
+    if P.add_noise:
+        obs = obs + (F(2) * u[:, VL.VU_NOISE:VL.VU_NOISE + VL.NUM_OBS] - F(1)) * P.noise_vec
+    obs = np.clip(obs, -P.clip_obs, P.clip_obs).astype(np.float32)
+    fsh, fs, rsh, rs = P.priv
+    priv = np.concatenate([(S["friction"] - fsh) * fs, (S["restitution"] - rsh) * rs], 1).astype(np.float32)
+    priv = np.clip(priv, -P.clip_obs, P.clip_obs)
+    # epilogue (:144-149)
+    S["last_last_actions"][:] = S["last_actions"]
+    S["last_actions"][:] = act
+    S["last_last_joint_pos_target"][:] = S["last_joint_pos_target"]
+    S["last_joint_pos_target"][:] = S["joint_pos_target"]
+    S["last_dof_vel"][:] = S["dof_vel"]
+    return dict(obs=obs, priv=priv, rew=rew, reset=reset, time_out=time_out, terms=terms, clock=clock,
+                desired=q["desired"], foot_indices=q["foot_indices"], torques=torques, episode_log=episode_log,
+                resample_a=ids_a, resample_b=ids_b)

@@ -100,3 +100,31 @@ def get_axis_params(value, axis_idx, x_value=0.0, dtype=np.float64, n_dims=3):
     params = np.where(zs == 1.0, value, zs)
     params[0] = x_value
     return list(params.astype(dtype))
+
+
+# Isaac Gym Preview 4 torch_utils (absent offline): the quaternion product legged_gym / walk-these-ways
+# rely on (go1_gym/envs/rewards/corl_rewards.py:156, 165), restated from the published library's
+# factored form; tests/test_vel_oracle.py checks it against a plain Hamilton product.
+def quat_mul(a, b):
+    assert a.shape == b.shape
+    shape = a.shape
+    a = a.reshape(-1, 4)
+    b = b.reshape(-1, 4)
+    x1, y1, z1, w1 = a[:, 0], a[:, 1], a[:, 2], a[:, 3]
+    x2, y2, z2, w2 = b[:, 0], b[:, 1], b[:, 2], b[:, 3]
+    ww = (z1 + x1) * (x2 + y2)
+    yy = (w1 - y1) * (w2 + z2)
+    zz = (w1 + y1) * (w2 - z2)
+    xx = ww + yy + zz
+    qq = 0.5 * (xx + (z1 - x1) * (x2 - y2))
+    w = qq - ww + (z1 - y1) * (y2 - z2)
+    x = qq - xx + (x1 + w1) * (x2 + w2)
+    y = qq - yy + (w1 - x1) * (y2 + z2)
+    z = qq - zz + (z1 + y1) * (w2 - x2)
+    return torch.stack([x, y, z, w], dim=-1).view(shape)
+
+
+def quat_conjugate(a):
+    shape = a.shape
+    a = a.reshape(-1, 4)
+    return torch.cat((-a[:, :3], a[:, -1:]), dim=-1).view(shape)
