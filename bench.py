@@ -260,6 +260,42 @@ def rollout_rate(n, dev, steps, warmup):
             "fused_policy": alg.fused is not None}
 
 
+def velocity_rate(n, dev, steps, warmup):
+    """BASELINE configs[1] (4096 Go1, plane, velocity_tracking reward): VecEnv.step of
+    HistoryWrapper(VelocityTrackingEasyEnv) -- the fused HIP velocity step (native integrator, CoRL rewards,
+    gait clock), the curriculum / history-shift launch (30-deep obs_history), the env's host bookkeeping --
+    with N(0,1) actions resident on the device; HIP events around the step kernel."""
+    import torch
+    from legged_tracking_amd import env as E, velocity as VEL
+    env = E.HistoryWrapper(VEL.VelocityTrackingEasyEnv(sim_device=str(dev), num_envs=n, seed=11))
+    env.reset()
+    env.get_observations()
+    ring = torch.randn((64, n, 12), device=dev, generator=torch.Generator(device=dev).manual_seed(7))
+    for k in range(warmup):
+        env.step(ring[k % 64])
+    torch.cuda.synchronize()
+    every = 4
+    ev = EventPairs((steps + every - 1) // every)
+    env.env.kernel_events.extend(ev.pair(k // every) if k % every == 0 else None for k in range(steps))
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.step(ring[k % 64])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    env.env.kernel_events.clear()
+    kms = float(np.mean([ev.ms(i) for i in range((steps + every - 1) // every)]))
+    ev.close()
+    assert torch.isfinite(env.env.obs_buf).all(), "non-finite observations"
+    resets = int(env.env.state["episode_length"].eq(0).sum())
+    env.env.close()
+    return {"value": n * steps / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+            "kernel_ms": kms, "envs_per_gpu": n, "dtype": "f32",
+            "what": "BASELINE configs[1]: VecEnv.step of HistoryWrapper(VelocityTrackingEasyEnv) on the plane, "
+                    "scripts/train_velocity_tracking.py config (CoRL rewards, gait commands, curriculum, 30-deep "
+                    "obs history); kernel_ms = go1_vel_step_kernel alone (HIP events on its dispatch)",
+            "envs_at_episode_start": resets}
+
+
 def learn_rate(n, dev, iters=4, warmup=1):
     """The whole training loop, as the reference's wandb train/fps measures it (ppo_cse/__init__.py:184:
     (it + 1) x num_envs x num_steps_per_env / elapsed): Runner iterations of rollout (24 x [PPO.act +
@@ -377,6 +413,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--no-learn", action="store_true", help="skip the whole-training-loop leg")
+    ap.add_argument("--no-velocity", action="store_true", help="skip the configs[1] velocity-tracking leg")
+    ap.add_argument("--velocity-only", action="store_true", help="profile helper: time only the velocity env")
     ap.add_argument("--learn-only", action="store_true", help="profile helper: time only Runner iterations")
     ap.add_argument("--rollout-only", action="store_true", help="profile helper: time only the rollout loop")
     ap.add_argument("--event-every", type=int, default=4,
@@ -411,6 +449,10 @@ def main():
     if args.rollout_only:
         torch.cuda.set_device(dev)
         print(json.dumps(rollout_rate(args.envs_per_gpu, dev, args.steps, args.warmup)))
+        return
+    if args.velocity_only:
+        torch.cuda.set_device(dev)
+        print(json.dumps(velocity_rate(args.envs_per_gpu, dev, args.steps, args.warmup)))
         return
     if args.learn_only:
         torch.cuda.set_device(dev)
@@ -535,6 +577,8 @@ def main():
             line["sweep"] = [env_sweep(int(x), dev) for x in args.sweep.split(",")]
         if not args.no_rollout and world == 1:
             line["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24))
+        if not args.no_velocity and world == 1:
+            line["velocity"] = velocity_rate(n, dev, steps=min(args.steps, 300), warmup=min(args.warmup, 30))
         if not args.no_learn and world == 1:
             line["learn"] = learn_rate(n, dev)
         if not args.no_cpu_baseline and world == 1:

@@ -1,0 +1,1714 @@
+// go1_device.h -- device code shared by the MI355X Go1 step kernels (go1_step.hip: trajectory
+// tracking; go1_velocity.hip: velocity tracking): Philox, lane-indexed selects, the actuator-net
+// MFMA groups, torch-order f32 math, the native articulated-body integrator with implicit penalty
+// contacts (phys_substep) and its helpers.  Included by one translation unit per library.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+
+#include "../../include/go1_mi355x.h"
+#include "go1_model_consts.h"
+#include "go1_spec.h"
+static_assert(GO1_MODEL_CONST_FLOATS == GO1_MODEL_FLOATS, "regenerate go1_model_consts.h");
+#include "pmath.h"
+
+#pragma clang fp contract(off)
+
+#ifdef GO1_ISA_MARKS  // section markers for static instruction accounting (tools/isa_sections.py)
+#define MARK(x) asm volatile("; MARK " #x)
+#elif defined(GO1_STAMPS)
+// Diagnostic build only (tools/stamps.py): every marker records (source line, s_memtime)
+// into a buffer of its own, read back by go1_debug_stamps.  Never built into the product.
+#define GO1_STAMP_WAVES 4096
+#define GO1_STAMP_SLOTS 160
+__device__ unsigned long long g_go1_stamps[GO1_STAMP_WAVES * GO1_STAMP_SLOTS];
+__shared__ unsigned s_go1_stamp_k;
+__device__ __forceinline__ void go1_stamp(unsigned line) {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned i = s_go1_stamp_k;
+  if (blockIdx.x < GO1_STAMP_WAVES && i < GO1_STAMP_SLOTS)
+    g_go1_stamps[blockIdx.x * GO1_STAMP_SLOTS + i] = ((unsigned long long)line << 48) | (t & 0xffffffffffffull);
+  s_go1_stamp_k = i + 1;
+  __builtin_amdgcn_sched_barrier(0);
+}
+#define MARK(x) go1_stamp(__LINE__)
+#else
+#define MARK(x)
+#endif
+#define NDOF 12
+#define NB 17
+#define EPB 16          // envs per block of the reset kernel (4 lanes per env)
+#define TPB 64          // one wave per block
+// LDS copy of the per-joint config arrays, contiguous in go1_config from default_dof_pos
+// (checked at go1_create): default_dof_pos, dof_pos_limits, torque_limits, hard_limits,
+// height_grid_x, height_grid_y, after the model block
+#define LDS_DDP (GO1_MODEL_FLOATS)
+#define LDS_DPL (LDS_DDP + 12)
+#define LDS_TL (LDS_DPL + 24)
+#define LDS_HL (LDS_TL + 12)
+#define LDS_GX (LDS_HL + 24)
+#define LDS_GY (LDS_GX + GO1_GRID_X)
+#define LDS_FLOATS (LDS_GY + GO1_GRID_Y)
+#define GO1_DIVERGED 1.0e4f
+static_assert(offsetof(go1_config, height_grid_y) - offsetof(go1_config, default_dof_pos) ==
+                  (LDS_GY - LDS_DDP) * sizeof(float),
+              "per-joint config arrays must be contiguous in go1_config");  // |state component| treated as a diverged integrator
+#define SEPB 4          // envs per wave of the step kernel (16 lanes per env: 4 roles x 4 legs)
+#define PI_F 3.14159265358979323846f
+#define TWO_PI_F 6.28318548202514648438f  // (float)(2*pi), torch's f32 scalar
+
+// ---------------------------------------------------------------- Philox
+__device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    // one v_mad_u64_u32 per product gives both halves (instead of v_mul_lo + v_mul_hi)
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t l0 = (uint32_t)p0, h0 = (uint32_t)(p0 >> 32), l1 = (uint32_t)p1, h1 = (uint32_t)(p1 >> 32);
+    uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = l1; c[2] = n2; c[3] = l0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+struct Rng {
+  const float* U;  // parity-mode uniforms or nullptr
+  uint64_t seed, step;
+  int e;    // local env index (parity-mode uniforms)
+  int gid;  // global env id (Philox counter): local index + go1_config.env_id_offset
+  int ustride;  // parity-mode uniform row width (go1_config.u_per_env)
+  __device__ float operator()(int slot) const {
+    if (U) return U[(size_t)e * ustride + slot];
+    uint32_t c[4] = {(uint32_t)gid, (uint32_t)slot >> 2, (uint32_t)step, (uint32_t)(step >> 32)};
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    return (float)(c[slot & 3] >> 8) * (1.0f / 16777216.0f);
+  }
+  // the four uniforms of slots 4 blk .. 4 blk + 3 (one Philox block), as operator() returns them
+  __device__ void quad(int blk, float* u) const {
+    if (U) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = U[(size_t)e * ustride + 4 * blk + k];
+      return;
+    }
+    uint32_t c[4] = {(uint32_t)gid, (uint32_t)blk, (uint32_t)step, (uint32_t)(step >> 32)};
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = (float)(c[k] >> 8) * (1.0f / 16777216.0f);
+  }
+};
+
+// ---------------------------------------------------------------- lane-indexed selects
+// a[i] for a lane-dependent i in 0..3 as two levels of bit-test selects (v_cndmask): an
+// equality chain (i == 0 ? .. : i == 1 ? ..) is turned into a switch with divergent branches
+__device__ __forceinline__ float sel4(int i, float a0, float a1, float a2, float a3) {
+  const bool lo = i & 1, hi = i & 2;
+  return hi ? (lo ? a3 : a2) : (lo ? a1 : a0);
+}
+__device__ __forceinline__ float sel3(int i, const float* a) { return sel4(i, a[0], a[1], a[2], a[2]); }
+
+// ---------------------------------------------------------------- quad helpers
+// sum over the quad (lanes xor 1, 2) in the order (l0 + l1) + (l2 + l3); DPP quad_perm
+// moves stay in the VALU (no LDS round trip)
+__device__ __forceinline__ float qsum(float v) {
+  // update_dpp(0, ., bound_ctrl) lets the compiler fold the move into the add (v_add_f32_dpp)
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));  // [1,0,3,2]
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));  // [2,3,0,1]
+  return v;
+}
+
+// sum over the four 16-lane rows, (r0 + r1) + (r2 + r3): gfx950 v_permlane16/32_swap
+__device__ __forceinline__ float rowsum4(float p) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+  p = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// N independent row sums stage by stage (all permlane16 swaps, then their adds, then the
+// permlane32 stage): one value at a time, every sum paid a register copy, a hazard nop and
+// the full swap latency, twice
+template <int N>
+__device__ __forceinline__ void rowsum4_n(float* v) {
+  float a[N], b[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+    a[i] = __uint_as_float(r[0]);
+    b[i] = __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = a[i] + b[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+    a[i] = __uint_as_float(r[0]);
+    b[i] = __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = a[i] + b[i];
+}
+
+// N values that two bodies split between the row pairs (body L on rows 0-1, body H on rows 2-3):
+// the permlane16 stage sums each pair, then one permlane32 swap hands every lane both results --
+// its two outputs are the low-half value (rows 0-1) and the high-half value (rows 2-3) on every
+// lane.  Three VALU per value where two full row sums cost eight.
+template <int N>
+__device__ __forceinline__ void pairsum_rows_n(const float* v, float* lo, float* hi) {
+  float a[N], b[N], s[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+    a[i] = __uint_as_float(r[0]);
+    b[i] = __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) s[i] = a[i] + b[i];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[i]), __float_as_uint(s[i]), false, false);
+    lo[i] = __uint_as_float(r[0]);
+    hi[i] = __uint_as_float(r[1]);
+  }
+}
+
+// ---------------------------------------------------------------- actuator net
+// eval_actuator_network (:1311-1320) on the matrix cores.  One "group" = 16
+// (env, joint) items; each item is carried by the 4 lanes {i, 16+i, 32+i, 48+i}
+// of a wave (i = lane & 15, q = lane >> 4), exactly the v_mfma_f32_16x16x4_f32
+// B-operand layout (B[k = q][item i]) and C/D layout (rows 4q..4q+3, column i).
+//   layer 1: D = W1pad(32x8) . X(8x16): 2 M-tiles x 2 K-steps = 4 MFMA
+//   layer 2: D = W2(32x32) . H1(32x16): each lane's layer-1 rows ARE its layer-2
+//            B operand when the K-steps run over (m, r) with k = 16 m + 4 q + r,
+//            so no data moves between the layers: 2 M-tiles x 8 K-steps = 16 MFMA
+//   layer 3: per-lane fma over its 8 rows, then two xor-shuffles (16, 32).
+// f32-input MFMA is bit-for-bit a k-ordered fmaf chain, and the oracle uses the
+// same k order (oracle/go1_oracle.c go1o_actuator_eval): torques are bit-identical.
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+struct MlpFrag {
+  float w1[2][2];  // [mo][s] = W1[16 mo + i][4 s + q]  (0 for k >= 6)
+  float w2[2][8];  // [mo][4 m + r] = W2[16 mo + i][16 m + 4 q + r]
+  f4 b1[2], b2[2]; // rows 4 q + r of tile mo
+  float w3[2][4];  // w3[16 mo + 4 q + r]
+  float b3;
+};
+
+__device__ __forceinline__ void mlp_load(const float* __restrict__ W, int lane, MlpFrag& F) {
+  const int i = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const int k = 4 * sk + q;
+      F.w1[mo][sk] = k < 6 ? W[(16 * mo + i) * 6 + k] : 0.0f;
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) F.w2[mo][4 * m + r] = W[224 + (16 * mo + i) * 32 + 16 * m + 4 * q + r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      F.b1[mo][r] = W[192 + 16 * mo + 4 * q + r];
+      F.b2[mo][r] = W[1248 + 16 * mo + 4 * q + r];
+      F.w3[mo][r] = W[1280 + 16 * mo + 4 * q + r];
+    }
+  }
+  F.b3 = W[1312];
+}
+
+// b0 = X[k = q][item], b1v = X[k = 4 + q][item] (0 for q >= 2).  Returns the torque
+// of item (lane & 15) in all four lanes of the item.  Needs all 64 lanes active.
+__device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v) {
+  f4 a1[2];
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+    a1[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][0], b0, F.b1[mo], 0, 0, 0);
+    a1[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][1], b1v, a1[mo], 0, 0, 0);
+  }
+  float h1[2][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      const f2 h = pm_softsign2(f2{a1[m][r], a1[m][r + 1]});
+      h1[m][r] = h.x;
+      h1[m][r + 1] = h.y;
+    }
+  f4 a2[2] = {F.b2[0], F.b2[1]};
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mo = 0; mo < 2; ++mo)
+        a2[mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w2[mo][4 * m + r], h1[m][r], a2[mo], 0, 0, 0);
+  float h2[2][4];
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo)
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      const f2 h = pm_softsign2(f2{a2[mo][r], a2[mo][r + 1]});
+      h2[mo][r] = h.x;
+      h2[mo][r + 1] = h.y;
+    }
+  float p = 0.0f;
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p = fmaf(F.w3[mo][r], h2[mo][r], p);
+  return rowsum4(p) + F.b3;
+}
+
+// The three groups of a sub-step (joints 0..2) at once, layer by layer: 6 independent
+// accumulator chains per layer keep the matrix pipe busy (one v_mfma_f32_16x16x4_f32 per
+// 32 cycles per SIMD), and the softsign VALU of one group issues under the MFMAs of the
+// next.  Each chain's k order is mlp_group's, so the torques are bit-identical to it.
+__device__ __forceinline__ void mlp_group3(const MlpFrag& F, const float* b0, const float* b1v, float* t) {
+  f4 a1[3][2];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) a1[g][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][0], b0[g], F.b1[mo], 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) a1[g][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w1[mo][1], b1v[g], a1[g][mo], 0, 0, 0);
+  float h1[3][2][4];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f2 h = pm_softsign2(f2{a1[g][m][r], a1[g][m][r + 1]});
+        h1[g][m][r] = h.x;
+        h1[g][m][r + 1] = h.y;
+      }
+  f4 a2[3][2];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) { a2[g][0] = F.b2[0]; a2[g][1] = F.b2[1]; }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int mo = 0; mo < 2; ++mo)
+          a2[g][mo] = __builtin_amdgcn_mfma_f32_16x16x4f32(F.w2[mo][4 * m + r], h1[g][m][r], a2[g][mo], 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    float p = 0.0f;
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo)
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f2 h = pm_softsign2(f2{a2[g][mo][r], a2[g][mo][r + 1]});
+        p = fmaf(F.w3[mo][r], h.x, p);
+        p = fmaf(F.w3[mo][r + 1], h.y, p);
+      }
+    t[g] = rowsum4(p) + F.b3;
+  }
+  // the matrix pipe takes one v_mfma_f32_16x16x4_f32 per 32 cycles and the wave may issue ~6 VALU
+  // instructions in that gap: layer 1 first, then each layer-2 MFMA followed by softsign work
+#pragma unroll
+  for (int i = 0; i < 12; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+  for (int i = 0; i < 48; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+  }
+}
+
+// ---------------------------------------------------------------- torch-order f32 math
+__device__ __forceinline__ void quat_rotate_inverse_f(const float* q, const float* v, float* out) {
+  float qw = q[3];
+  float s = 2.0f * (qw * qw) - 1.0f;
+  float a0 = v[0] * s, a1 = v[1] * s, a2 = v[2] * s;
+  float c0 = q[1] * v[2] - q[2] * v[1];
+  float c1 = q[2] * v[0] - q[0] * v[2];
+  float c2 = q[0] * v[1] - q[1] * v[0];
+  float b0 = c0 * qw * 2.0f, b1 = c1 * qw * 2.0f, b2 = c2 * qw * 2.0f;
+  float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+  float e0 = q[0] * d * 2.0f, e1 = q[1] * d * 2.0f, e2 = q[2] * d * 2.0f;
+  out[0] = a0 - b0 + e0;
+  out[1] = a1 - b1 + e1;
+  out[2] = a2 - b2 + e2;
+}
+
+__device__ __forceinline__ void quat_apply_yaw_inverse_f(const float* q, const float* v, float* out) {
+  float qy[4] = {0.0f, 0.0f, q[2], q[3]};
+  float n2 = fmaf(qy[3], qy[3], fmaf(qy[2], qy[2], fmaf(qy[1], qy[1], qy[0] * qy[0])));
+  float n = sqrtf(n2);
+  if (n < 1e-9f) n = 1e-9f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qy[i] = qy[i] / n;
+  quat_rotate_inverse_f(qy, v, out);
+}
+
+__device__ __forceinline__ float remainder_f(float a, float b) {
+  // fmodf is exact; so are its two cheap cases, which cover every angle this path wraps
+  // (|a| < 2 |b|): a itself for |a| < |b|, and sign(a) (|a| - |b|) for |b| <= |a| < 2 |b|
+  // (Sterbenz; the sign of a zero result is a's, as fmodf gives it).  The library's
+  // iterative fmodf runs only for the rare larger |a|.
+  const float aa = fabsf(a), ab = fabsf(b);
+  float m = aa < ab ? a : copysignf(aa - ab, a);
+  if (!(aa < 2.0f * ab)) m = fmodf(a, b);  // also NaN / inf inputs
+  if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
+  return m;
+}
+
+__device__ __forceinline__ float wrap_to_pi_f(float a) {
+  a = remainder_f(a, TWO_PI_F);
+  if (a > PI_F) a = a - TWO_PI_F;
+  return a;
+}
+
+__device__ __forceinline__ void quat_to_rpy_f(const float* q, float* rpy) {
+  float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+  float sinr = 2.0f * (qw * qx + qy * qz);
+  float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
+  float roll = pm_atan2f(sinr, cosr);
+  float sinp = 2.0f * (qw * qy - qz * qx);
+  float pitch = fabsf(sinp) >= 1.0f ? copysignf(PM_PIO2, sinp) : pm_asinf(sinp);
+  float siny = 2.0f * (qw * qz + qx * qy);
+  float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
+  float yaw = pm_atan2f(siny, cosy);
+  rpy[0] = wrap_to_pi_f(remainder_f(roll, TWO_PI_F));
+  rpy[1] = wrap_to_pi_f(remainder_f(pitch, TWO_PI_F));
+  rpy[2] = wrap_to_pi_f(remainder_f(yaw, TWO_PI_F));
+}
+
+__device__ __forceinline__ float norm2_f(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
+__device__ __forceinline__ float norm3_f(float x, float y, float z) { return sqrtf(fmaf(z, z, fmaf(y, y, x * x))); }
+__device__ __forceinline__ float sq_f(float x) { return x * x; }
+__device__ __forceinline__ float clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// =====================================================================
+//                  native articulated-body integrator (f32)
+// =====================================================================
+// Everything from here to the step kernel is integrator code (compared with the f64
+// oracle within a tolerance): FMA contraction on, including in the inlined helpers
+// (a pragma inside phys_substep alone does not reach them).
+#pragma clang fp contract(on)
+// Spatial vectors (angular; linear).  6x6 symmetric articulated inertia stored as
+// [[A, B], [B^T, C]], A and C symmetric (xx xy xz yy yz zz), B row-major 3x3.
+struct SI {
+  float a[6], b[9], c[6];
+};
+
+// Integrator-only fast math (hardware v_rcp_f32 / v_rsq_f32, ~1 ulp): the f32
+// integrator is compared with the f64 oracle within a tolerance, never bitwise.
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// hardware v_sin_f32 / v_cos_f32 on the angle in revolutions reduced to [0, 1) by v_fract_f32:
+// 5 issue slots instead of the portable polynomial's ~25 (integrator only; absolute error
+// ~1e-6, the step is compared with the f64 oracle within a tolerance)
+__device__ __forceinline__ void hw_sincosf(float x, float* s, float* c) {
+  const float r = __builtin_amdgcn_fractf(x * 0.159154943091895336f);
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+}
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+
+#define S3(m, i, j) m[((i) == 0 ? ((j) == 0 ? 0 : (j) == 1 ? 1 : 2) : (i) == 1 ? ((j) == 0 ? 1 : (j) == 1 ? 3 : 4) : ((j) == 0 ? 2 : (j) == 1 ? 4 : 5))]
+
+__device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
+  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+// y = M v for the symmetric spatial matrix
+__device__ __forceinline__ void si_mul(const SI& M, const float* v, float* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    float s = 0.0f, t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      s += S3(M.a, i, j) * v[j] + M.b[i * 3 + j] * v[3 + j];
+      t += M.b[j * 3 + i] * v[j] + S3(M.c, i, j) * v[3 + j];
+    }
+    o[i] = s;
+    o[3 + i] = t;
+  }
+}
+
+// y = M v for a v whose components ax and 3 + ax are zero (c_j of a joint about axis ax)
+__device__ __forceinline__ void si_mul_sparse(const SI& M, const float* v, int ax, float* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    float s = 0.0f, t = 0.0f;
+    bool fs = true, ft = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      s = fs ? S3(M.a, i, j) * v[j] : s + S3(M.a, i, j) * v[j];
+      t = ft ? M.b[j * 3 + i] * v[j] : t + M.b[j * 3 + i] * v[j];
+      fs = false; ft = false;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      s = s + M.b[i * 3 + j] * v[3 + j];
+      t = t + S3(M.c, i, j) * v[3 + j];
+    }
+    o[i] = s;
+    o[3 + i] = t;
+  }
+}
+
+__device__ __forceinline__ float si_get(const SI& M, int i, int j) {
+  if (i < 3 && j < 3) return S3(M.a, i, j);
+  if (i >= 3 && j >= 3) return S3(M.c, i - 3, j - 3);
+  if (i < 3) return M.b[i * 3 + (j - 3)];
+  return M.b[j * 3 + (i - 3)];
+}
+
+// rigid-body spatial inertia about the link origin
+__device__ __forceinline__ void rigid_si(const float* body, float mscale, SI& I) {
+  float m = body[0] * mscale;
+  float c0 = body[1], c1 = body[2], c2 = body[3];
+  float cc = c0 * c0 + c1 * c1 + c2 * c2;
+  I.a[0] = body[4] * mscale + m * (cc - c0 * c0);
+  I.a[1] = body[5] * mscale - m * c0 * c1;
+  I.a[2] = body[6] * mscale - m * c0 * c2;
+  I.a[3] = body[7] * mscale + m * (cc - c1 * c1);
+  I.a[4] = body[8] * mscale - m * c1 * c2;
+  I.a[5] = body[9] * mscale + m * (cc - c2 * c2);
+  // B = m c~
+  // structural zeros as -0.0: the compiler folds x + (-0.0) = x in si_add, not x + (+0.0)
+  I.b[0] = -0.0f; I.b[1] = -m * c2; I.b[2] = m * c1;
+  I.b[3] = m * c2; I.b[4] = -0.0f; I.b[5] = -m * c0;
+  I.b[6] = -m * c1; I.b[7] = m * c0; I.b[8] = -0.0f;
+  I.c[0] = m; I.c[1] = -0.0f; I.c[2] = -0.0f; I.c[3] = m; I.c[4] = -0.0f; I.c[5] = m;
+}
+
+// Rigid-body bias force v x* (I v) of a body (mass m, COM c, inertia Ic about the COM;
+// model layout) from its momentum, without building the 6x6 inertia:
+//   p = m (v + w x c),  L = Ic w + c x p,  v x* (L, p) = (w x L + v x p, w x p).
+__device__ __forceinline__ void rigid_bias(const float* body, float mscale, const float* vel, float* o) {
+  const float m = body[0] * mscale;
+  const float* c = body + 1;
+  const float* w = vel;
+  const float* v = vel + 3;
+  float wc[3], p[3], L[3], cp[3];
+  cross3(w, c, wc);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p[i] = m * (v[i] + wc[i]);
+  const float ixx = body[4] * mscale, ixy = body[5] * mscale, ixz = body[6] * mscale;
+  const float iyy = body[7] * mscale, iyz = body[8] * mscale, izz = body[9] * mscale;
+  cross3(c, p, cp);
+  L[0] = ixx * w[0] + ixy * w[1] + ixz * w[2] + cp[0];
+  L[1] = ixy * w[0] + iyy * w[1] + iyz * w[2] + cp[1];
+  L[2] = ixz * w[0] + iyz * w[1] + izz * w[2] + cp[2];
+  float a[3], b[3];
+  cross3(w, L, a);
+  cross3(v, p, b);
+  o[0] = a[0] + b[0]; o[1] = a[1] + b[1]; o[2] = a[2] + b[2];
+  cross3(w, p, o + 3);
+}
+
+// rigid_bias on a velocity given as (angular, linear) pairs, the result as pairs: the two
+// products with w, w x L and w x p, run as one packed cross product of w with the (L, p) pairs
+__device__ __forceinline__ void rigid_bias2(const float* body, const f2* vel, f2* o, float mscale = 1.0f) {
+  const float m = body[0] * mscale;
+  const float* c = body + 1;
+  const float w[3] = {vel[0].x, vel[1].x, vel[2].x}, v[3] = {vel[0].y, vel[1].y, vel[2].y};
+  float wc[3], p[3], L[3], cp[3], b[3];
+  cross3(w, c, wc);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p[i] = m * (v[i] + wc[i]);
+  const float ixx = body[4] * mscale, ixy = body[5] * mscale, ixz = body[6] * mscale;
+  const float iyy = body[7] * mscale, iyz = body[8] * mscale, izz = body[9] * mscale;
+  cross3(c, p, cp);
+  L[0] = ixx * w[0] + ixy * w[1] + ixz * w[2] + cp[0];
+  L[1] = ixy * w[0] + iyy * w[1] + iyz * w[2] + cp[1];
+  L[2] = ixz * w[0] + iyz * w[1] + izz * w[2] + cp[2];
+  const f2 X[3] = {f2{L[0], p[0]}, f2{L[1], p[1]}, f2{L[2], p[2]}};
+  cross3(v, p, b);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+    const f2 wx = w[i1] * X[i2] - w[i2] * X[i1];
+    o[i] = f2{wx.x + b[i], wx.y};
+  }
+}
+
+// force cross product v x* f
+__device__ __forceinline__ void crf(const float* v, const float* f, float* o) {
+  float a[3], b[3], c[3];
+  cross3(v, f, a);
+  cross3(v + 3, f + 3, b);
+  cross3(v, f + 3, c);
+  o[0] = a[0] + b[0]; o[1] = a[1] + b[1]; o[2] = a[2] + b[2];
+  o[3] = c[0]; o[4] = c[1]; o[5] = c[2];
+}
+
+// Revolute joint about coordinate axis ax (0 = x, 1 = y) by q: E = Rot(ax, q)^T maps
+// parent coordinates to child coordinates.  Only (c, s) is kept; every product with E
+// mixes two components.
+__device__ __forceinline__ void rE(int ax, float c, float s, const float* v, float* o) {  // o = E v
+  if (ax == 0) {
+    float y = c * v[1] + s * v[2], z = c * v[2] - s * v[1];
+    o[0] = v[0]; o[1] = y; o[2] = z;
+  } else {
+    float x = c * v[0] - s * v[2], z = s * v[0] + c * v[2];
+    o[0] = x; o[1] = v[1]; o[2] = z;
+  }
+}
+
+__device__ __forceinline__ void rET(int ax, float c, float s, const float* v, float* o) {  // o = E^T v
+  if (ax == 0) {
+    float y = c * v[1] - s * v[2], z = s * v[1] + c * v[2];
+    o[0] = v[0]; o[1] = y; o[2] = z;
+  } else {
+    float x = c * v[0] + s * v[2], z = c * v[2] - s * v[0];
+    o[0] = x; o[1] = v[1]; o[2] = z;
+  }
+}
+
+__device__ __forceinline__ void mat3_vec(const float* E, const float* v, float* o) {
+  float x = E[0] * v[0] + E[1] * v[1] + E[2] * v[2];
+  float y = E[3] * v[0] + E[4] * v[1] + E[5] * v[2];
+  float z = E[6] * v[0] + E[7] * v[1] + E[8] * v[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+__device__ __forceinline__ void mat3T_vec(const float* E, const float* v, float* o) {
+  float x = E[0] * v[0] + E[3] * v[1] + E[6] * v[2];
+  float y = E[1] * v[0] + E[4] * v[1] + E[7] * v[2];
+  float z = E[2] * v[0] + E[5] * v[1] + E[8] * v[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+
+// Joint offsets are sparse in the Go1 model (go1_create checks it): hip (x, y, 0), thigh
+// (0, y, 0), calf (0, 0, z).  `M` = mask of the components of r that may be non-zero
+// (bit i = component i), a constant after inlining and unrolling, so the products with
+// the zero components are never emitted (not even as 0 * x, which IEEE forbids folding).
+__host__ __device__ __forceinline__ constexpr int offset_mask(int j) { return j == 0 ? 3 : (j == 1 ? 2 : 4); }
+// which components of a x b can be non-zero, a and b with masks ma, mb
+__device__ __forceinline__ constexpr int cross_mask(int ma, int mb) {
+  int m = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int p = (i + 1) % 3, q = (i + 2) % 3;
+    if ((((ma >> p) & 1) && ((mb >> q) & 1)) || (((ma >> q) & 1) && ((mb >> p) & 1))) m |= 1 << i;
+  }
+  return m;
+}
+// component i of a x b (a_p b_q - a_q b_p) with only the terms the masks allow
+__device__ __forceinline__ float cross_c(int ma, int mb, int i, const float* a, const float* b) {
+  const int p = (i + 1) % 3, q = (i + 2) % 3;
+  const bool t1 = ((ma >> p) & 1) && ((mb >> q) & 1), t2 = ((ma >> q) & 1) && ((mb >> p) & 1);
+  if (t1 && t2) return a[p] * b[q] - a[q] * b[p];
+  if (t1) return a[p] * b[q];
+  if (t2) return -(a[q] * b[p]);
+  return 0.0f;
+}
+
+// motion transform parent -> child: (w, v) -> (E w, E (v - r x w)), r with mask M
+__device__ __forceinline__ void xm(int ax, float c, float s, int M, const float* r, const float* vin, float* vout) {
+  const int cm = cross_mask(M, 7);
+  float t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = ((cm >> i) & 1) ? vin[3 + i] - cross_c(M, 7, i, r, vin) : vin[3 + i];
+  rE(ax, c, s, vin, vout);
+  rE(ax, c, s, t, vout + 3);
+}
+
+// force transform child -> parent: (n, f) -> (E^T n + r x E^T f, E^T f), r with mask M
+__device__ __forceinline__ void xfT(int ax, float c, float s, int M, const float* r, const float* fin, float* fout) {
+  const int cm = cross_mask(M, 7);
+  float n[3], f[3];
+  rET(ax, c, s, fin, n);
+  rET(ax, c, s, fin + 3, f);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) fout[i] = ((cm >> i) & 1) ? n[i] + cross_c(M, 7, i, r, f) : n[i];
+  fout[3] = f[0]; fout[4] = f[1]; fout[5] = f[2];
+}
+
+// Q = E^T M E for a full 3x3 M (row-major): rows of M E are E^T(row of M), then E^T per column.
+__device__ __forceinline__ void rot_congruence(int ax, float c, float s, const float* M, float* Q) {
+  float N[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) rET(ax, c, s, M + 3 * i, N + 3 * i);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float col[3] = {N[j], N[3 + j], N[6 + j]}, out[3];
+    rET(ax, c, s, col, out);
+    Q[j] = out[0]; Q[3 + j] = out[1]; Q[6 + j] = out[2];
+  }
+}
+
+// Q = E^T M E for a symmetric M stored (xx xy xz yy yz zz) into a full 3x3 Q.  E^T rotates
+// the two indices (p, r) other than the axis f by R = [[c, -s'], [s', c]] (s' = s for x,
+// -s for y), so with c2 = c^2 - s'^2, s2 = 2 c s', h = (Mpp + Mrr) / 2, d = (Mpp - Mrr) / 2:
+//   Qff = Mff, Qfp = c Mfp - s' Mfr, Qfr = s' Mfp + c Mfr,
+//   Qpp = h + d c2 - Mpr s2, Qrr = h - d c2 + Mpr s2, Qpr = d s2 + Mpr c2.
+__device__ __forceinline__ void rot_congruence_sym(int ax, float c, float s, float c2, float s2, const float* m,
+                                                   float* Q) {
+  const int f = ax, pI = ax == 0 ? 1 : 0, rI = 2;
+  const float sp = ax == 0 ? s : -s;
+  auto at = [&](int i, int j) -> float { return S3(m, i, j); };
+  const float mff = at(f, f), mfp = at(f, pI), mfr = at(f, rI), mpp = at(pI, pI), mrr = at(rI, rI), mpr = at(pI, rI);
+  const float h = 0.5f * (mpp + mrr), d = 0.5f * (mpp - mrr);
+  const float qfp = c * mfp - sp * mfr, qfr = sp * mfp + c * mfr;
+  const float qpp = h + d * c2 - mpr * s2, qrr = h - d * c2 + mpr * s2, qpr = d * s2 + mpr * c2;
+  Q[f * 3 + f] = mff;
+  Q[f * 3 + pI] = qfp; Q[pI * 3 + f] = qfp;
+  Q[f * 3 + rI] = qfr; Q[rI * 3 + f] = qfr;
+  Q[pI * 3 + pI] = qpp; Q[rI * 3 + rI] = qrr;
+  Q[pI * 3 + rI] = qpr; Q[rI * 3 + pI] = qpr;
+}
+
+// X^T Ia X for X = [[E, 0], [-E r~, E]]: rotate the blocks by E^T(.)E, then translate by r
+// (mask M):  A'' = A' + r~ B'^T - B' r~ - r~ C' r~ ,  B'' = B' + r~ C' ,  C'' = C'.
+// RC = r~ C' has non-zero rows mc, BR = B' r~ non-zero columns mb, RCR = RC r~ both.
+__device__ __forceinline__ void xform_inertia(int ax, float cq, float sq, int M, const float* r, const SI& In,
+                                              SI& Out) {
+  float A[9], B[9], C[9];
+  const float sp = ax == 0 ? sq : -sq;
+  const float c2 = cq * cq - sp * sp, s2 = 2.0f * cq * sp;
+  rot_congruence_sym(ax, cq, sq, c2, s2, In.a, A);
+  rot_congruence(ax, cq, sq, In.b, B);
+  rot_congruence_sym(ax, cq, sq, c2, s2, In.c, C);
+  // translation, with (M r~) row i = (row i of M) x r and r~ B'^T = -(B' r~)^T
+  const int mc = cross_mask(M, 7), mb = cross_mask(7, M);
+  float RC[9], BR[9], RCR[9];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {  // r~ C': column j = r x C'[:, j]
+    const float col[3] = {C[j], C[3 + j], C[6 + j]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) RC[3 * i + j] = ((mc >> i) & 1) ? cross_c(M, 7, i, r, col) : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      BR[3 * i + j] = ((mb >> j) & 1) ? cross_c(7, M, j, B + 3 * i, r) : 0.0f;              // B' r~
+      RCR[3 * i + j] = ((mc >> i) & (mb >> j) & 1) ? cross_c(7, M, j, RC + 3 * i, r) : 0.0f;  // r~ C' r~
+    }
+  // upper triangle of A'' = A' - BR^T - BR - RCR (symmetric); zero terms are skipped
+  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int i = II[t], j = JJ[t];
+    float v = A[i * 3 + j];
+    if ((mb >> i) & 1) v -= BR[j * 3 + i];
+    if ((mb >> j) & 1) v -= BR[i * 3 + j];
+    if ((mc >> i) & (mb >> j) & 1) v -= RCR[i * 3 + j];
+    Out.a[t] = v;
+    Out.c[t] = C[i * 3 + j];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Out.b[3 * i + j] = ((mc >> i) & 1) ? B[3 * i + j] + RC[3 * i + j] : B[3 * i + j];
+}
+
+__device__ __forceinline__ void si_add(SI& A, const SI& B) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { A.a[i] += B.a[i]; A.c[i] += B.c[i]; }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) A.b[i] += B.b[i];
+}
+
+// 6x6 SPD solve (Cholesky), identical instruction stream in every lane of a quad
+__device__ __forceinline__ void solve6(const SI& M, const float* b, float* x) {
+  float L[21];
+#define LI(i, j) L[(i) * ((i) + 1) / 2 + (j)]
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      float s = si_get(M, i, j);
+#pragma unroll
+      for (int k = 0; k < j; ++k) s -= LI(i, k) * LI(j, k);
+      if (i == j) LI(i, i) = frsq(fmaxf(s, 1e-30f));  // holds 1 / L_ii
+      else LI(i, j) = s * LI(j, j);
+    }
+  float y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= LI(i, k) * y[k];
+    y[i] = s * LI(i, i);
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s -= LI(k, i) * x[k];
+    x[i] = s * LI(i, i);
+  }
+#undef LI
+}
+
+// ---- packed articulated-body algebra.  One wave alone issues a v_pk_fma_f32 (two FMAs) as
+// fast as a v_fma_f32 (tools/probes/pk_rate.hip), and a spatial quantity pairs up by itself:
+// a spatial vector is three (angular_i, linear_i) pairs, and a spatial inertia keeps its two
+// symmetric 3 x 3 blocks as six (A_t, C_t) pairs -- every rotation, rank-1 update and sum of the
+// articulated-body passes treats the two halves alike.  B (general 3 x 3) stays scalar.
+struct SIP {
+  f2 ac[6];
+  float b[9];
+};
+__host__ __device__ __forceinline__ constexpr int s3i(int i, int j) {
+  return i == 0 ? j : (i == 1 ? (j == 0 ? 1 : j + 2) : (j == 0 ? 2 : (j == 1 ? 4 : 5)));
+}
+
+__device__ __forceinline__ void rigid_sip(const float* body, float mscale, SIP& I) {
+  SI s;
+  rigid_si(body, mscale, s);
+#pragma unroll
+  for (int t = 0; t < 6; ++t) I.ac[t] = f2{s.a[t], s.c[t]};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) I.b[i] = s.b[i];
+}
+
+__device__ __forceinline__ void sip_add(SIP& A, const SIP& B) {
+#pragma unroll
+  for (int t = 0; t < 6; ++t) A.ac[t] += B.ac[t];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) A.b[i] += B.b[i];
+}
+
+// column ax of the 6 x 6 matrix as pairs: (A(i, ax), B^T(i, ax) = B(ax, i))
+__device__ __forceinline__ f2 sip_col(const SIP& M, int ax, int i) { return f2{M.ac[s3i(i, ax)].x, M.b[ax * 3 + i]}; }
+
+// y = M v for a v whose pair ax is zero (c_j of a joint about axis ax); v, y as pairs
+__device__ __forceinline__ void sip_mul_sparse(const SIP& M, const f2* v, int ax, f2* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    f2 st = f2{0.0f, 0.0f};
+    bool first = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      st = first ? M.ac[s3i(i, j)] * v[j] : st + M.ac[s3i(i, j)] * v[j];
+      first = false;
+    }
+    float s = st.x, t = st.y;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j == ax) continue;
+      s = s + M.b[i * 3 + j] * v[j].y;
+      t = t + M.b[j * 3 + i] * v[j].x;
+    }
+    o[i] = f2{s, t};
+  }
+}
+
+// E v (rE) and E^T v (rET) on pairs: both halves rotate by the same joint rotation
+__device__ __forceinline__ void rE2(int ax, float c, float s, const f2* v, f2* o) {
+  if (ax == 0) {
+    const f2 y = c * v[1] + s * v[2], z = c * v[2] - s * v[1];
+    o[0] = v[0]; o[1] = y; o[2] = z;
+  } else {
+    const f2 x = c * v[0] - s * v[2], z = s * v[0] + c * v[2];
+    o[0] = x; o[1] = v[1]; o[2] = z;
+  }
+}
+__device__ __forceinline__ void rET2(int ax, float c, float s, const f2* v, f2* o) {
+  if (ax == 0) {
+    const f2 y = c * v[1] - s * v[2], z = s * v[1] + c * v[2];
+    o[0] = v[0]; o[1] = y; o[2] = z;
+  } else {
+    const f2 x = c * v[0] + s * v[2], z = c * v[2] - s * v[0];
+    o[0] = x; o[1] = v[1]; o[2] = z;
+  }
+}
+
+// motion transform parent -> child on pairs: (w, v) -> (E w, E (v - r x w)), r with mask M
+__device__ __forceinline__ void xm2(int ax, float c, float s, int M, const float* r, const f2* vin, f2* vout) {
+  const int cm = cross_mask(M, 7);
+  const float w[3] = {vin[0].x, vin[1].x, vin[2].x};
+  f2 t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = f2{w[i], ((cm >> i) & 1) ? vin[i].y - cross_c(M, 7, i, r, w) : vin[i].y};
+  rE2(ax, c, s, t, vout);
+}
+
+// force transform child -> parent on pairs: (n, f) -> (E^T n + r x E^T f, E^T f), r with mask M
+__device__ __forceinline__ void xfT2(int ax, float c, float s, int M, const float* r, const f2* fin, f2* fout) {
+  const int cm = cross_mask(M, 7);
+  f2 nf[3];
+  rET2(ax, c, s, fin, nf);
+  const float f[3] = {nf[0].y, nf[1].y, nf[2].y};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) fout[i] = f2{((cm >> i) & 1) ? nf[i].x + cross_c(M, 7, i, r, f) : nf[i].x, f[i]};
+}
+
+// X^T Ia X (xform_inertia) with the A and C blocks rotated together as pairs
+__device__ __forceinline__ void xform_inertia2(int ax, float cq, float sq, int M, const float* r, const SIP& In,
+                                               SIP& Out) {
+  const float sp = ax == 0 ? sq : -sq;
+  const float c2 = cq * cq - sp * sp, s2 = 2.0f * cq * sp;
+  // rot_congruence_sym on (A, C) pairs
+  const int f = ax, pI = ax == 0 ? 1 : 0, rI = 2;
+  const f2 mff = In.ac[s3i(f, f)], mfp = In.ac[s3i(f, pI)], mfr = In.ac[s3i(f, rI)];
+  const f2 mpp = In.ac[s3i(pI, pI)], mrr = In.ac[s3i(rI, rI)], mpr = In.ac[s3i(pI, rI)];
+  const f2 h = 0.5f * (mpp + mrr), d = 0.5f * (mpp - mrr);
+  const f2 qfp = cq * mfp - sp * mfr, qfr = sp * mfp + cq * mfr;
+  const f2 qpp = h + d * c2 - mpr * s2, qrr = h - d * c2 + mpr * s2, qpr = d * s2 + mpr * c2;
+  f2 Q[9];
+  Q[f * 3 + f] = mff;
+  Q[f * 3 + pI] = qfp; Q[pI * 3 + f] = qfp;
+  Q[f * 3 + rI] = qfr; Q[rI * 3 + f] = qfr;
+  Q[pI * 3 + pI] = qpp; Q[rI * 3 + rI] = qrr;
+  Q[pI * 3 + rI] = qpr; Q[rI * 3 + pI] = qpr;
+  float B[9], C[9];
+  rot_congruence(ax, cq, sq, In.b, B);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) C[i] = Q[i].y;
+  // translation by r (xform_inertia): A'' = A' - BR^T - BR - RCR, B'' = B' + RC, C'' = C'
+  const int mc = cross_mask(M, 7), mb = cross_mask(7, M);
+  float RC[9], BR[9], RCR[9];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float col[3] = {C[j], C[3 + j], C[6 + j]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) RC[3 * i + j] = ((mc >> i) & 1) ? cross_c(M, 7, i, r, col) : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      BR[3 * i + j] = ((mb >> j) & 1) ? cross_c(7, M, j, B + 3 * i, r) : 0.0f;
+      RCR[3 * i + j] = ((mc >> i) & (mb >> j) & 1) ? cross_c(7, M, j, RC + 3 * i, r) : 0.0f;
+    }
+  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int i = II[t], j = JJ[t];
+    float v = Q[i * 3 + j].x;
+    if ((mb >> i) & 1) v -= BR[j * 3 + i];
+    if ((mb >> j) & 1) v -= BR[i * 3 + j];
+    if ((mc >> i) & (mb >> j) & 1) v -= RCR[i * 3 + j];
+    Out.ac[t] = f2{v, C[i * 3 + j]};
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Out.b[3 * i + j] = ((mc >> i) & 1) ? B[3 * i + j] + RC[3 * i + j] : B[3 * i + j];
+}
+
+__device__ __forceinline__ float sip_get(const SIP& M, int i, int j) {
+  if (i < 3 && j < 3) return M.ac[s3i(i, j)].x;
+  if (i >= 3 && j >= 3) return M.ac[s3i(i - 3, j - 3)].y;
+  if (i < 3) return M.b[i * 3 + (j - 3)];
+  return M.b[j * 3 + (i - 3)];
+}
+
+// 6x6 SPD solve (Cholesky) of the packed inertia, identical instruction stream in every lane
+__device__ __forceinline__ void solve6p(const SIP& M, const float* b, float* x) {
+  float L[21];
+#define LI(i, j) L[(i) * ((i) + 1) / 2 + (j)]
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      float s = sip_get(M, i, j);
+#pragma unroll
+      for (int k = 0; k < j; ++k) s -= LI(i, k) * LI(j, k);
+      if (i == j) LI(i, i) = frsq(fmaxf(s, 1e-30f));  // holds 1 / L_ii
+      else LI(i, j) = s * LI(j, j);
+    }
+  float y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= LI(i, k) * y[k];
+    y[i] = s * LI(i, i);
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s -= LI(k, i) * x[k];
+    x[i] = s * LI(i, i);
+  }
+#undef LI
+}
+
+__device__ __forceinline__ void quat_to_R(const float* q, float* R) {
+  float x = q[0], y = q[1], z = q[2], w = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
+  R[3] = 2 * (x * y + z * w); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+  R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+// Terrain view of one env.  `patch` is an LDS copy of the PSZX x PSZY cells around
+// the env's base at the start of the step, floor and ceiling interleaved, filled
+// once per step by the whole block; the integrator's contact queries hit it and
+// fall back to the HBM tile outside it (identical values: a pure cache).
+// 20 rows (x) x 16 columns (y): the legs' bounding box spans up to 14 cells in x and 12 in y
+// (p99 under N(0, 1) actions), the patch is placed on its centre, and the rows leave room for
+// the motion during the step
+#define PSZX 20
+#define PSZY 16
+static_assert(PSZY == 16 && PSZX % 2 == 0, "the LDS-DMA patch staging maps 2 rows of 16 cells to a wave");
+struct Terr {
+  const float* tile;  // (2, nx, ny) or nullptr
+  int nx, ny;
+  float hs;             // queries are relative to the env's terrain origin
+  const float2* patch;  // LDS, PSZX x PSZY (floor, ceiling) or nullptr
+  int pi0, pj0;
+};
+
+__device__ __forceinline__ float tile_at(const Terr& T, int layer, int i, int j) {
+  i = min(max(i, 0), T.nx - 1);
+  j = min(max(j, 0), T.ny - 1);
+  return T.tile[((size_t)layer * T.nx + i) * T.ny + j];
+}
+
+// floor (layer 1) and ceiling (layer 0) heights and gradients at world (x, y), bilinear
+__device__ __forceinline__ void height_query2(const Terr& T, float x, float y, float* hf, float* hc) {
+  if (!T.tile) {
+    hf[0] = 0.0f; hf[1] = 0.0f; hf[2] = 0.0f;
+    hc[0] = 1e9f; hc[1] = 0.0f; hc[2] = 0.0f;
+    return;
+  }
+  // bounded before the float -> int conversions (a diverged pose must not index memory)
+  const float ihs = frcp(T.hs);
+  const float u = fminf(fmaxf(x * ihs, -4.0f), (float)(T.nx + 4));
+  const float v = fminf(fmaxf(y * ihs, -4.0f), (float)(T.ny + 4));
+  const float fu = floorf(u), fv = floorf(v);
+  const int i = (int)fu, j = (int)fv;
+  const float a = u - fu, b = v - fv;
+  float2 c00, c10, c01, c11;
+  const int li = i - T.pi0, lj = j - T.pj0;
+  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
+    const float2* pp = T.patch + li * PSZY + lj;
+    c00 = pp[0]; c01 = pp[1]; c10 = pp[PSZY]; c11 = pp[PSZY + 1];
+  } else {
+    c00 = make_float2(tile_at(T, 1, i, j), tile_at(T, 0, i, j));
+    c10 = make_float2(tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j));
+    c01 = make_float2(tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1));
+    c11 = make_float2(tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1));
+  }
+  const float inv = ihs;
+  hf[0] = (1 - a) * (1 - b) * c00.x + a * (1 - b) * c10.x + (1 - a) * b * c01.x + a * b * c11.x;
+  hf[1] = ((1 - b) * (c10.x - c00.x) + b * (c11.x - c01.x)) * inv;
+  hf[2] = ((1 - a) * (c01.x - c00.x) + a * (c11.x - c10.x)) * inv;
+  hc[0] = (1 - a) * (1 - b) * c00.y + a * (1 - b) * c10.y + (1 - a) * b * c01.y + a * b * c11.y;
+  hc[1] = ((1 - b) * (c10.y - c00.y) + b * (c11.y - c01.y)) * inv;
+  hc[2] = ((1 - a) * (c01.y - c00.y) + a * (c11.y - c10.y)) * inv;
+}
+
+struct CP {
+  float k, d, kf, mu;
+};
+
+// ---- packed (v_pk_*_f32) contact: one wave issues a v_pk_fma_f32 (two FMAs) as fast as a
+// v_fma_f32 (tools/probes/pk_rate.hip), so the floor and ceiling layers of a point are
+// carried as the two halves of an f2 all the way from the bilinear patch to the force.
+__device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
+
+// (floor, ceiling) heights and gradients at world (x, y), bilinear, in two halves, so that the
+// corner reads are issued early and land while independent work runs (the articulated-inertia
+// chain of the sub-step): hq_fetch reads the four (floor, ceiling) corners -- the LDS patch stores
+// (floor, ceiling) per cell, i.e. already in f2 layout; the HBM tile outside it -- and hq_finish
+// interpolates.
+struct HQ {
+  f2 c00, c10, c01, c11;
+  float a, b;
+};
+__device__ __forceinline__ void hq_fetch(const Terr& T, float x, float y, HQ& q) {
+  if (!T.tile) {
+    q.c00 = q.c10 = q.c01 = q.c11 = f2{0.0f, 1e9f};
+    q.a = q.b = 0.0f;
+    return;
+  }
+  const float ihs = frcp(T.hs);
+  const float u = fminf(fmaxf(x * ihs, -4.0f), (float)(T.nx + 4));
+  const float v = fminf(fmaxf(y * ihs, -4.0f), (float)(T.ny + 4));
+  const float fu = floorf(u), fv = floorf(v);
+  const int i = (int)fu, j = (int)fv;
+  q.a = u - fu;
+  q.b = v - fv;
+#ifdef GO1_ABL_NO_FALLBACK  // ablation build only: every query from the (clamped) LDS patch
+  const int li = min(max(i - T.pi0, 0), PSZX - 2), lj = min(max(j - T.pj0, 0), PSZY - 2);
+#else
+  const int li = i - T.pi0, lj = j - T.pj0;
+#endif
+  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
+    const float2* pp = T.patch + li * PSZY + lj;
+    const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];
+    q.c00 = f2{q00.x, q00.y}; q.c01 = f2{q01.x, q01.y}; q.c10 = f2{q10.x, q10.y}; q.c11 = f2{q11.x, q11.y};
+  } else {
+    q.c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
+    q.c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
+    q.c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
+    q.c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
+  }
+}
+__device__ __forceinline__ void hq_finish(const Terr& T, const HQ& q, f2& h, f2& gx, f2& gy) {
+  const float ihs = frcp(T.hs);
+  const float a = q.a, b = q.b, a1 = 1.0f - a, b1 = 1.0f - b;
+  h = (a1 * b1) * q.c00 + (a * b1) * q.c10 + (a1 * b) * q.c01 + (a * b) * q.c11;
+  gx = (b1 * (q.c10 - q.c00) + b * (q.c11 - q.c01)) * ihs;
+  gy = (a1 * (q.c01 - q.c00) + a * (q.c11 - q.c10)) * ihs;
+}
+
+// penalty contact of a sphere (centre p, velocity pv, radius r) with the floor (pushes up)
+// and the ceiling (pushes down), both layers at once; F = floor + ceiling force
+__device__ __forceinline__ void sphere_contact_pk(const Terr& T, const HQ& q, const CP& C, const float* p,
+                                                  const float* pv, float r, float* F) {
+  f2 h, gx, gy;
+  hq_finish(T, q, h, gx, gy);
+  const f2 sg = f2{1.0f, -1.0f};
+  const f2 dv = sg * (h - p[2]) + r;  // floor: h + r - z, ceiling: z + r - h
+  f2 nx = -sg * gx, ny = -sg * gy;
+  f2 inv = nx * nx + ny * ny + 1.0f;
+  inv = f2{frsq(inv.x), frsq(inv.y)};
+  nx = nx * inv;
+  ny = ny * inv;
+  const f2 nz = sg * inv;
+  const f2 depth = dv * inv;
+  const f2 vn = pv[0] * nx + pv[1] * ny + pv[2] * nz;
+  const f2 fn = C.k * depth - C.d * vn;
+  const f2 vtx = pv[0] - vn * nx, vty = pv[1] - vn * ny, vtz = pv[2] - vn * nz;
+  const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
+  const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
+  const f2 vtn = vt2 * ivt;
+  const f2 cf = C.kf * vtn, cm = C.mu * fn;
+  const f2 ft = f2{fminf(cf.x, cm.x), fminf(cf.y, cm.y)};
+  const f2 fti = ft * ivt;
+  // a layer acts only in penetration with a compressive normal force
+  const bool ax = dv.x > 0.0f && fn.x > 0.0f, ay = dv.y > 0.0f && fn.y > 0.0f;
+  const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
+  const f2 sc = f2{(ax && vtn.x > 1e-9f) ? fti.x : 0.0f, (ay && vtn.y > 1e-9f) ? fti.y : 0.0f};
+  const f2 Fx = fa * nx - sc * vtx, Fy = fa * ny - sc * vty, Fz = fa * nz - sc * vtz;
+  F[0] = Fx.x + Fx.y;
+  F[1] = Fy.x + Fy.y;
+  F[2] = Fz.x + Fz.y;
+}
+
+// The same contact, linearly implicit in the point velocity (the integrator's scheme: one 5 ms step
+// per sim step, like PhysX's substeps = 1).  For an active layer the force at the end of the step,
+// k (depth - h vn') - d vn' (normal) and -c_t vt' (regularised friction, c_t = min(kf, mu fn / |vt|)
+// from the current state), with v' = v + h a_p, splits into an explicit force F and an added mass
+//   Mp = h (h k + d) n n^T + h c_t (I - n n^T)
+// on the point (world frame, summed over floor and ceiling; xx xy xz yy yz zz), which the caller
+// puts into the link's articulated inertia, so the ABA accelerations include the contact response.
+// oracle/go1_oracle.c sphere_contact_im is the f64 restatement.
+__device__ __forceinline__ void sphere_contact_im(const Terr& T, const HQ& q, const CP& C, const float* p,
+                                                  const float* pv, float r, float h, float* F, float* Mp) {
+  f2 hh, gx, gy;
+  hq_finish(T, q, hh, gx, gy);
+  const f2 sg = f2{1.0f, -1.0f};
+  const f2 dv = sg * (hh - p[2]) + r;  // floor: h + r - z, ceiling: z + r - h
+  f2 nx = -sg * gx, ny = -sg * gy;
+  f2 inv = nx * nx + ny * ny + 1.0f;
+  inv = f2{frsq(inv.x), frsq(inv.y)};
+  nx = nx * inv;
+  ny = ny * inv;
+  const f2 nz = sg * inv;
+  const f2 depth = dv * inv;
+  const f2 vn = pv[0] * nx + pv[1] * ny + pv[2] * nz;
+  const f2 fn0 = C.k * depth - C.d * vn;          // activation: compressive at the current state
+  const f2 fn = fn0 - (h * C.k) * vn;              // k depth - (h k + d) vn
+  const f2 vtx = pv[0] - vn * nx, vty = pv[1] - vn * ny, vtz = pv[2] - vn * nz;
+  const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
+  const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
+  const f2 vtn = vt2 * ivt;
+  const f2 cm = C.mu * fn0;
+  // c_t = min(kf, mu fn0 / |vt|); kf in the viscous limit |vt| -> 0
+  const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
+                   (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
+  const bool ax = dv.x > 0.0f && fn0.x > 0.0f, ay = dv.y > 0.0f && fn0.y > 0.0f;
+  const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
+  const f2 sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
+  const f2 Fx = fa * nx - sc * vtx, Fy = fa * ny - sc * vty, Fz = fa * nz - sc * vtz;
+  F[0] = Fx.x + Fx.y;
+  F[1] = Fy.x + Fy.y;
+  F[2] = Fz.x + Fz.y;
+  const float cn = h * (h * C.k + C.d);
+  const f2 cd = h * sc, cnd = f2{ax ? cn : 0.0f, ay ? cn : 0.0f} - cd;  // (cn - cd) on active layers
+  const f2 a = cnd * nx, b = cnd * ny, c = cnd * nz;
+  const f2 mxx = a * nx + cd, mxy = a * ny, mxz = a * nz, myy = b * ny + cd, myz = b * nz, mzz = c * nz + cd;
+  Mp[0] = mxx.x + mxx.y; Mp[1] = mxy.x + mxy.y; Mp[2] = mxz.x + mxz.y;
+  Mp[3] = myy.x + myy.y; Mp[4] = myz.x + myz.y; Mp[5] = mzz.x + mzz.y;
+}
+
+__device__ __forceinline__ void sphere_contact(const Terr& T, const CP& C, const float* p, const float* pv, float r,
+                                               float* F) {
+  F[0] = F[1] = F[2] = 0.0f;
+  float hq[2][3];
+  height_query2(T, p[0], p[1], hq[1], hq[0]);
+#pragma unroll
+  for (int layer = 1; layer >= 0; --layer) {
+    const float h = hq[layer][0], gx = hq[layer][1], gy = hq[layer][2];
+    float n[3], dv;
+    if (layer == 1) {
+      dv = h + r - p[2];
+      n[0] = -gx; n[1] = -gy; n[2] = 1.0f;
+    } else {
+      dv = p[2] + r - h;
+      n[0] = gx; n[1] = gy; n[2] = -1.0f;
+    }
+    if (dv <= 0.0f) continue;
+    const float inv = frsq(n[0] * n[0] + n[1] * n[1] + 1.0f);
+    n[0] *= inv; n[1] *= inv; n[2] *= inv;
+    const float depth = dv * inv;
+    const float vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
+    const float fn = C.k * depth - C.d * vn;
+    if (fn <= 0.0f) continue;
+    const float vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
+    const float vt2 = vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2];
+    const float ivt = frsq(fmaxf(vt2, 1e-18f));
+    const float vtn = vt2 * ivt;
+    const float ft = fminf(C.kf * vtn, C.mu * fn);
+    const float sc = vtn > 1e-9f ? ft * ivt : 0.0f;
+    F[0] += fn * n[0] - sc * vt[0];
+    F[1] += fn * n[1] - sc * vt[1];
+    F[2] += fn * n[2] - sc * vt[2];
+  }
+}
+
+__device__ __forceinline__ void point_kin(const float* Rb, const float* pb, const float* vb, const float* lp, float* pw,
+                                          float* vw) {
+  float wl[3], vl[3];
+  cross3(vb, lp, wl);
+  vl[0] = vb[3] + wl[0]; vl[1] = vb[4] + wl[1]; vl[2] = vb[5] + wl[2];
+  float t[3];
+  mat3_vec(Rb, lp, t);
+  pw[0] = pb[0] + t[0]; pw[1] = pb[1] + t[1]; pw[2] = pb[2] + t[2];
+  mat3_vec(Rb, vl, vw);
+}
+
+__device__ __forceinline__ void point_force(const float* Rb, const float* lp, const float* F, float* fs) {
+  float f[3], n[3];
+  mat3T_vec(Rb, F, f);
+  cross3(lp, f, n);
+  fs[0] += n[0]; fs[1] += n[1]; fs[2] += n[2]; fs[3] += f[0]; fs[4] += f[1]; fs[5] += f[2];
+}
+
+// Physical state of one env as held by one lane of its quad.
+// World position of this leg's foot body origin (rigid_body_state[:, feet, 0:3] after
+// the last sim step), the kinematic chain of phys_substep without velocities.
+__device__ void foot_world(const float* __restrict__ model, const float* root, const float* q, int leg, float* out) {
+  float Rp[9], pp[3] = {root[0], root[1], root[2]};
+  quat_to_R(root + 3, Rp);
+  const float* origin = model + 13 * 10 + leg * 9;
+  const float* foot = model + 13 * 10 + 4 * 9;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int ax = j == 0 ? 0 : 1;
+    float rw[3], sn, cn;
+    mat3_vec(Rp, origin + j * 3, rw);
+    pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];
+    pm_sincosf(q[j], &sn, &cn);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
+  }
+  float fw[3];
+  mat3_vec(Rp, foot, fw);
+  out[0] = pp[0] + fw[0]; out[1] = pp[1] + fw[1]; out[2] = pp[2] + fw[2];
+}
+
+// Centre (x, y) of the bounding box of the env's hips, knees and feet at the start of the
+// step: the terrain patch is placed on it rather than on the base (16 x 16 cells around the
+// base left ~6 % of the envs with a leg outside it, and one such lane sends its whole wave
+// through the HBM fallback of every contact query).  Hardware sin / cos: only the placement
+// of the patch depends on this, and the patch is a pure cache of the tile.
+__device__ __forceinline__ float quad_min(float v) {
+  v = fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true)));
+  return fminf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true)));
+}
+__device__ __forceinline__ float quad_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true)));
+  return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true)));
+}
+__device__ __forceinline__ void legs_bbox_centre(const float* pos, const float* quat, const float* q, int leg,
+                                                 float* cx, float* cy) {
+  const float sx = (leg & 2) ? -1.0f : 1.0f, sy = (leg & 1) ? -1.0f : 1.0f;
+  float Rp[9], pp[3] = {pos[0], pos[1], pos[2]};
+  quat_to_R(quat, Rp);
+  float xmin = 1e30f, xmax = -1e30f, ymin = 1e30f, ymax = -1e30f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float o[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = 30 + 3 * j + k, sp = GO1_LEG_SIGN[i];
+      o[k] = GO1_LEG_FL[i] * (sp == 0 ? 1.0f : (sp == 1 ? sx : (sp == 2 ? sy : sx * sy)));
+    }
+    float rw[3];
+    mat3_vec(Rp, o, rw);
+    pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];  // hip, thigh, calf (knee) origins
+    if (j != 1) {
+      xmin = fminf(xmin, pp[0]); xmax = fmaxf(xmax, pp[0]);
+      ymin = fminf(ymin, pp[1]); ymax = fmaxf(ymax, pp[1]);
+    }
+    float sn, cn;
+    __sincosf(q[j], &sn, &cn);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rE(j == 0 ? 0 : 1, cn, sn, Rp + 3 * a, Rp + 3 * a);
+  }
+  float fw[3];
+  mat3_vec(Rp, GO1_MODEL_F32 + 13 * 10 + 4 * 9, fw);  // foot offset in the calf frame
+  const float fx = pp[0] + fw[0], fy = pp[1] + fw[1];
+  xmin = quad_min(fminf(xmin, fx)); xmax = quad_max(fmaxf(xmax, fx));
+  ymin = quad_min(fminf(ymin, fy)); ymax = quad_max(fmaxf(ymax, fy));
+  *cx = 0.5f * (xmin + xmax);
+  *cy = 0.5f * (ymin + ymax);
+}
+
+// The config block through the constant address space: every uniform field read is a
+// scalar (SMEM) load.  Through a generic pointer the compiler cannot prove that the
+// kernel's stores leave the block unchanged, and emits vector loads, each a full memory
+// round trip at its first use (inside the sub-step loop too).
+typedef const __attribute__((address_space(4))) go1_config CCfg;
+
+struct Phys {
+  float pos[3], quat[4];  // base (replicated on the 16 lanes of the env)
+  f2 wv[3];               // base angular and linear velocity (world) as (w_i, v_i) pairs
+  float q[3], qd[3];                   // this lane's leg
+};
+
+// sum over the 4 roles of a leg (the four 16-lane rows), bitwise identical on every lane
+__device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
+
+// One integrator step of length h for the env of this lane.  Lane layout (16 per
+// env): lane = 16 role + 4 env + leg.  The four roles of a leg compute the leg's
+// kinematics and ABA passes redundantly (base quantities on all 16 lanes), and
+// split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
+// two per lane, so each wave has four envs and the whole grid fills every SIMD.
+// cf_out: this lane's reported contact forces (thigh, calf, foot of its leg; base).
+// `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
+// in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
+// because the physics keeps every VGPR busy, and LDS answers faster than the caches.
+__device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
+                                             float h, const float* g, float friction, float payload, const Terr& T,
+                                             int leg, int role, bool cf_out, float* cf_raw) {
+#pragma clang fp contract(on)
+  // Model constants are compile-time literals (go1_model_consts.h, checked against the
+  // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
+  // Per-leg floats are the FL values times the leg's mirror signs (loop-invariant products).
+  (void)lds;
+  const float* model = GO1_MODEL_F32;
+  const float msx = (leg & 2) ? -1.0f : 1.0f, msy = (leg & 1) ? -1.0f : 1.0f, msxy = msx * msy;
+  float LC[39];
+#pragma unroll
+  for (int i = 0; i < 39; ++i) {
+    const int p = GO1_LEG_SIGN[i];
+    LC[i] = p == 0 ? GO1_LEG_FL[i] : GO1_LEG_FL[i] * (p == 1 ? msx : (p == 2 ? msy : msxy));
+  }
+  MARK(phys_begin);
+  const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
+  float R[9];
+  quat_to_R(S.quat, R);
+  f2 vbp[3];  // base-frame (angular, linear) velocity pairs: R^T on both halves at once
+#pragma unroll
+  for (int i = 0; i < 3; ++i) vbp[i] = R[i] * S.wv[0] + R[3 + i] * S.wv[1] + R[6 + i] * S.wv[2];
+  const float vb[6] = {vbp[0].x, vbp[1].x, vbp[2].x, vbp[0].y, vbp[1].y, vbp[2].y};
+  const float* th = model + 13 * 10 + 4 * 9 + 3 + 1;  // trunk half extents
+  // ---- this leg: kinematics, rigid bias forces and gravity (hip -> calf)
+  const float* origin = LC + 30;
+  const float* foot = model + 13 * 10 + 4 * 9;
+  const float foot_r = foot[3];
+  const float thigh_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3];
+  const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
+  float cs[3][2];
+  float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
+  f2 cjp[3][3], pAp[3][3];  // c_j and the articulated bias force as (angular, linear) pairs
+  {
+    // link frame: rows 0 and 1 of the rotation as pairs over the column (row0_k, row1_k)
+    f2 R01[3], pp01 = f2{S.pos[0], S.pos[1]};
+    float R2[3], pp2 = S.pos[2];
+    f2 vp[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { R01[k] = f2{R[k], R[3 + k]}; R2[k] = R[6 + k]; }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) vp[i] = vbp[i];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int ax = j == 0 ? 0 : 1;
+      const float* r = origin + j * 3;
+      float sn, cn;
+      hw_sincosf(S.q[j], &sn, &cn);
+      cs[j][0] = cn; cs[j][1] = sn;
+      f2 vj[3];
+      xm2(ax, cn, sn, offset_mask(j), r, vp, vj);
+      vj[ax].x += S.qd[j];
+      // c_j = v_j x (S qd), S = unit axis ax: pair ax is exactly zero and never read
+      {
+        const float qdj = S.qd[j];
+        const int p1 = (ax + 1) % 3, p2 = (ax + 2) % 3;  // (w x e_ax)_p1 = w_p2, (.)_p2 = -w_p1
+        cjp[j][ax] = f2{0.0f, 0.0f};
+        cjp[j][p1] = vj[p2] * qdj;
+        cjp[j][p2] = -(vj[p1] * qdj);
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k)  // pp += Rp r over the components r may have
+        if ((offset_mask(j) >> k) & 1) { pp01 += R01[k] * r[k]; pp2 += R2[k] * r[k]; }
+      rE2(ax, cn, sn, R01, R01);
+      rE(ax, cn, sn, R2, R2);
+      // rigid bias force v x* I v about the link origin (gravity: a base acceleration, below)
+      rigid_bias2(LC + 10 * j, vj, pAp[j]);
+      if (j > 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { Rl[j - 1][k] = R01[k].x; Rl[j - 1][3 + k] = R01[k].y; Rl[j - 1][6 + k] = R2[k]; }
+        pl[j - 1][0] = pp01.x; pl[j - 1][1] = pp01.y; pl[j - 1][2] = pp2;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { vl[j - 1][i] = vj[i].x; vl[j - 1][3 + i] = vj[i].y; }
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) vp[i] = vj[i];
+    }
+  }
+  MARK(leg_kin_done);
+  // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
+  //      corner 2 leg, corner 2 leg + 1] -- world position / velocity, terrain corners, the explicit
+  //      force (body frame of the point's body) and the added mass of the implicit contact
+  // per lane: the leg's (thigh | calf) share in the row pair of its body and the trunk corner's share
+  float fleg[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
+  f2 Fpt[3] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};  // world forces of the lane's two points
+  const bool even = (role & 1) == 0;
+  // the contact inertias of this lane's points as one packed SIP per half (x, y = the two points):
+  // [[S M S^T, S M], [M S^T, M]] with M = Rs^T Mp Rs in the body frame, S = lp~
+  SIP cin[2];
+#ifndef GO1_ABL_NO_CONTACT
+  {
+    // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
+    // the body-frame force.  Points p: thigh 0-2, calf 3-4, foot 5 (on the calf), trunk corners
+    // 6-7 (2 leg, 2 leg + 1).  Rows (roles): 0 (thigh0, thigh1), 1 (thigh2, corner 6),
+    // 2 (calf0, calf1), 3 (foot, corner 7) -- x halves and the even rows' y halves belong to the
+    // thigh on rows 0-1 and to the calf on rows 2-3 (one pair reduction, pairsum_rows_n), the odd
+    // rows' y halves to the trunk
+    f2 Rs[9], lp[3], rr, pw[3], vw[3];
+    HQ qa, qb;
+    {
+      const bool lo_rows = role <= 1;  // x: thigh on rows 0-1, calf on rows 2-3; y: thigh, base, calf, base
+      f2 ps[3], vs[6];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+        Rs[i] = f2{lo_rows ? Rl[0][i] : Rl[1][i], even ? (lo_rows ? Rl[0][i] : Rl[1][i]) : R[i]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ps[i] = f2{lo_rows ? pl[0][i] : pl[1][i], even ? (lo_rows ? pl[0][i] : pl[1][i]) : S.pos[i]};
+#pragma unroll
+      for (int i = 0; i < 6; ++i) vs[i] = f2{lo_rows ? vl[0][i] : vl[1][i], even ? (lo_rows ? vl[0][i] : vl[1][i]) : vb[i]};
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int p = hh == 0 ? (role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5)))
+                              : (role == 0 ? 1 : (role == 1 ? 6 : (role == 2 ? 4 : 7)));
+        const bool on_thigh = p < 3, on_base = p >= 6;
+        const int cx = leg * 2 + (p - 6);
+        const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
+        lp[0][hh] = on_base ? ((cx & 1) ? th[0] : -th[0]) : (p == 5 ? foot[0] : 0.0f);
+        lp[1][hh] = on_base ? ((cx & 2) ? th[1] : -th[1]) : (p == 5 ? foot[1] : 0.0f);
+        lp[2][hh] = on_base ? ((cx & 4) ? th[2] : -th[2]) : (p == 5 ? foot[2] : lz);
+        rr[hh] = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
+      }
+      // point kinematics: v = R (v_lin + w x lp), p = p_body + R lp
+      const f2 wl[3] = {vs[1] * lp[2] - vs[2] * lp[1], vs[2] * lp[0] - vs[0] * lp[2], vs[0] * lp[1] - vs[1] * lp[0]};
+      const f2 vlin[3] = {vs[3] + wl[0], vs[4] + wl[1], vs[5] + wl[2]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pw[i] = ps[i] + Rs[3 * i] * lp[0] + Rs[3 * i + 1] * lp[1] + Rs[3 * i + 2] * lp[2];
+        vw[i] = Rs[3 * i] * vlin[0] + Rs[3 * i + 1] * vlin[1] + Rs[3 * i + 2] * vlin[2];
+      }
+      hq_fetch(T, pw[0].x, pw[1].x, qa);
+      hq_fetch(T, pw[0].y, pw[1].y, qb);
+    }
+    float Fa[3], Fb2[3], Ma[6], Mb[6];
+    {
+      const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
+      const float pb[3] = {pw[0].y, pw[1].y, pw[2].y}, vb2[3] = {vw[0].y, vw[1].y, vw[2].y};
+      sphere_contact_im(T, qa, C, pa, va, rr.x, h, Fa, Ma);
+      sphere_contact_im(T, qb, C, pb, vb2, rr.y, h, Fb2, Mb);
+    }
+    const f2 F[3] = {f2{Fa[0], Fb2[0]}, f2{Fa[1], Fb2[1]}, f2{Fa[2], Fb2[2]}};
+    // the ABA below solves for accelerations relative to free fall (gravity as a base
+    // acceleration), so the added mass would respond to a - g: the force it sees is F - Mp g
+    f2 Fd[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      Fd[i] = F[i] - (f2{Ma[s3i(i, 0)], Mb[s3i(i, 0)]} * g[0] + f2{Ma[s3i(i, 1)], Mb[s3i(i, 1)]} * g[1] +
+                      f2{Ma[s3i(i, 2)], Mb[s3i(i, 2)]} * g[2]);
+    // body-frame force f = R^T Fd and moment lp x f
+    f2 f6[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) f6[3 + j] = Rs[j] * Fd[0] + Rs[3 + j] * Fd[1] + Rs[6 + j] * Fd[2];
+    f6[0] = lp[1] * f6[5] - lp[2] * f6[4];
+    f6[1] = lp[2] * f6[3] - lp[0] * f6[5];
+    f6[2] = lp[0] * f6[4] - lp[1] * f6[3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      fleg[i] = f6[i].x + (even ? f6[i].y : 0.0f);
+      fbase[i] = even ? 0.0f : f6[i].y;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Fpt[i] = F[i];
+    // added masses into the body frame, M = Rs^T Mp Rs (both points as halves), then about the
+    // body origin: A = S M S^T, B = S M, C = M, S = lp~ (S v = lp x v)
+    const f2 Mw[6] = {f2{Ma[0], Mb[0]}, f2{Ma[1], Mb[1]}, f2{Ma[2], Mb[2]},
+                      f2{Ma[3], Mb[3]}, f2{Ma[4], Mb[4]}, f2{Ma[5], Mb[5]}};
+    f2 MR[9];  // Mp Rs (3 x 3, row-major)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        MR[3 * i + j] = Mw[s3i(i, 0)] * Rs[j] + Mw[s3i(i, 1)] * Rs[3 + j] + Mw[s3i(i, 2)] * Rs[6 + j];
+    f2 M[9];  // Rs^T (Mp Rs), symmetric
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = i; j < 3; ++j) {
+        M[3 * i + j] = Rs[i] * MR[j] + Rs[3 + i] * MR[3 + j] + Rs[6 + i] * MR[6 + j];
+        M[3 * j + i] = M[3 * i + j];
+      }
+    f2 SM[9];  // lp~ M: row i = lp x (column of M) components
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      SM[j] = lp[1] * M[6 + j] - lp[2] * M[3 + j];
+      SM[3 + j] = lp[2] * M[j] - lp[0] * M[6 + j];
+      SM[6 + j] = lp[0] * M[3 + j] - lp[1] * M[j];
+    }
+    // (S M) S^T: element (i, j) = (S M)_i . S_j row, S_j row = (lp x e)_j -> -(row i of SM) x lp
+    const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int i = II[k], j = JJ[k];
+      const f2* r = SM + 3 * i;
+      // (S M S^T)_ij = sum_l (SM)_il S_jl, S_j = (0, -lz, ly), (lz, 0, -lx), (-ly, lx, 0)
+      const f2 a = j == 0 ? r[2] * lp[1] - r[1] * lp[2] : (j == 1 ? r[0] * lp[2] - r[2] * lp[0] : r[1] * lp[0] - r[0] * lp[1]);
+      cin[0].ac[k][0] = a.x; cin[1].ac[k][0] = a.y;
+      cin[0].ac[k][1] = M[3 * i + j].x; cin[1].ac[k][1] = M[3 * i + j].y;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { cin[0].b[i] = SM[i].x; cin[1].b[i] = SM[i].y; }
+  }
+#else  // ablation build only: no contacts
+  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) cin[k].ac[t] = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 9; ++i) cin[k].b[i] = 0.0f;
+  }
+#endif
+  // the lane's contributions per body (thigh, calf, base), then summed over the leg's roles
+  SIP ci_th, ci_ca, ci_bs;
+  {
+    float lg[6 + 21], bs[6 + 21], th6[6 + 21], ca6[6 + 21];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { lg[i] = fleg[i]; bs[i] = fbase[i]; }
+#pragma unroll
+    for (int k = 0; k < 21; ++k) {
+      const float x = k < 12 ? cin[0].ac[k >> 1][k & 1] : cin[0].b[k - 12];
+      const float y = k < 12 ? cin[1].ac[k >> 1][k & 1] : cin[1].b[k - 12];
+      lg[6 + k] = x + (even ? y : 0.0f);  // thigh on rows 0-1, calf on rows 2-3
+      bs[6 + k] = even ? 0.0f : y;        // this leg's trunk corners
+    }
+    pairsum_rows_n<6 + 21>(lg, th6, ca6);
+    rowsum4_n<6 + 21>(bs);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pAp[1][i] -= f2{th6[i], th6[3 + i]};
+      pAp[2][i] -= f2{ca6[i], ca6[3 + i]};
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) fbase[i] = bs[i];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      ci_th.ac[k] = f2{th6[6 + 2 * k], th6[6 + 2 * k + 1]};
+      ci_ca.ac[k] = f2{ca6[6 + 2 * k], ca6[6 + 2 * k + 1]};
+      ci_bs.ac[k] = f2{bs[6 + 2 * k], bs[6 + 2 * k + 1]};
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { ci_th.b[i] = th6[18 + i]; ci_ca.b[i] = ca6[18 + i]; ci_bs.b[i] = bs[18 + i]; }
+  }
+  MARK(leg_kin_contacts_done);
+  // ---- backward pass calf -> hip (articulated inertias with the contact added masses, bias
+  //      forces with the explicit contact forces); the hip's inertia goes to the base
+  f2 Up[3][3];  // U = column ax of the articulated inertia, (angular, linear) pairs
+  float D[3], u[3];
+  SIP Ip;
+  f2 pp6[3];
+  {
+    SIP IA;
+    rigid_sip(LC + 20, 1.0f, IA);
+    sip_add(IA, ci_ca);
+#pragma unroll
+    for (int j = 2; j >= 0; --j) {
+      const int ax = j == 0 ? 0 : 1;
+      float t = tau[j];
+      // joint-limit spring-damper, implicit in the joint: the torque at the end of the
+      // sub-step, -k (q + h qd') - d qd' with qd' = qd + h qdd, moves (h d + h^2 k) qdd
+      // into the joint inertia D (unconditionally stable for any k, d)
+      const float lo = cfg->hard_limits[2 * j], hi = cfg->hard_limits[2 * j + 1];  // leg-uniform (go1_create)
+      const bool lim_on = S.q[j] > hi || S.q[j] < lo;
+      const float ex = S.q[j] > hi ? S.q[j] - hi : S.q[j] - lo;
+      const float kl = cfg->limit_stiffness, dl = cfg->limit_damping;
+      t -= lim_on ? kl * (ex + h * S.qd[j]) + dl * S.qd[j] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) Up[j][i] = sip_col(IA, ax, i);
+      D[j] = IA.ac[s3i(ax, ax)].x + (lim_on ? h * dl + h * h * kl : 0.0f);
+      u[j] = t - pAp[j][ax].x;
+      const float invD = frcp(D[j]);
+      D[j] = invD;  // the forward pass only needs 1 / D
+      f2 V[3];  // U / D
+#pragma unroll
+      for (int i = 0; i < 3; ++i) V[i] = Up[j][i] * invD;
+      SIP Ia;  // IA - U U^T / D: the A and C blocks as pairs, B scalar
+      const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Ia.ac[k] = IA.ac[k] - Up[j][II[k]] * V[JJ[k]];
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) Ia.b[a * 3 + b] = IA.b[a * 3 + b] - Up[j][a].x * V[b].y;
+      f2 Iac[3], pa[3], pt[3];
+      sip_mul_sparse(Ia, cjp[j], ax, Iac);
+      const float ud = u[j] * invD;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pa[i] = pAp[j][i] + Iac[i] + Up[j][i] * ud;
+      SIP It;
+      xform_inertia2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, Ia, It);
+      xfT2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, pa, pt);
+      if (j > 0) {
+        rigid_sip(LC + 10 * (j - 1), 1.0f, IA);
+        sip_add(IA, It);
+        if (j == 2) sip_add(IA, ci_th);  // the thigh's contact added masses
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
+      } else {
+        Ip = It;
+        sip_add(Ip, ci_bs);  // this leg's trunk corners: summed over the legs with the hips below
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pp6[i] = pt[i];
+      }
+    }
+  }
+  MARK(backward_done);
+  // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
+  const float* bb = model;
+  const float mscale = (bb[0] + payload) * frcp(bb[0]);
+  SIP I0;
+  rigid_sip(bb, mscale, I0);
+  f2 p0[3];
+  float gb[3];
+  rigid_bias2(bb, vbp, p0, mscale);
+  mat3T_vec(R, g, gb);  // gravity in the base frame: added to the relative base acceleration below
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Ip.ac[k] = f2{qsum(Ip.ac[k].x), qsum(Ip.ac[k].y)};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) pp6[i] = f2{qsum(pp6[i].x - fbase[i]), qsum(pp6[i].y - fbase[3 + i])};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Ip.b[i] = qsum(Ip.b[i]);
+  sip_add(I0, Ip);
+  float rhs[6], a0[6];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    rhs[i] = -(p0[i].x + pp6[i].x);
+    rhs[3 + i] = -(p0[i].y + pp6[i].y);
+  }
+  solve6p(I0, rhs, a0);
+  MARK(base_solve_done);
+  // ---- forward pass
+  float qdd[3];
+  {
+    f2 ap[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ap[i] = f2{a0[i], a0[3 + i]};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int ax = j == 0 ? 0 : 1;
+      f2 aj[3];
+      xm2(ax, cs[j][0], cs[j][1], offset_mask(j), origin + j * 3, ap, aj);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i != ax) aj[i] += cjp[j][i];  // pair ax of c_j is zero
+      const f2 ua = Up[j][0] * aj[0] + Up[j][1] * aj[1] + Up[j][2] * aj[2];
+      qdd[j] = (u[j] - (ua.x + ua.y)) * D[j];
+      aj[ax].x += qdd[j];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ap[i] = aj[i];
+    }
+  }
+  MARK(forward_done);
+  // ---- semi-implicit Euler (base identical in the quad)
+  float wxv[3];
+  cross3(vb, vb + 3, wxv);
+  // a0 is relative to free fall: the base's linear acceleration is a0_lin + g; (angular, linear)
+  // body-frame accelerations as pairs, rotated to the world and integrated together
+  f2 ab[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ab[i] = f2{a0[i], a0[3 + i] + gb[i] + wxv[i]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    S.wv[i] += h * (R[3 * i] * ab[0] + R[3 * i + 1] * ab[1] + R[3 * i + 2] * ab[2]);
+    S.pos[i] += h * S.wv[i].y;
+  }
+  {
+    const float w[3] = {S.wv[0].x, S.wv[1].x, S.wv[2].x};
+    const float wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    const float iwn = frsq(fmaxf(wn2, 1e-30f));
+    const float wn = wn2 * iwn;
+    const float thh = 0.5f * h * wn;
+    float sth, cth;
+    hw_sincosf(thh, &sth, &cth);
+    const float sc = thh > 1e-12f ? sth * iwn : 0.5f * h;
+    const float dq[4] = {w[0] * sc, w[1] * sc, w[2] * sc, cth};
+    float* q = S.quat;
+    float nq[4];
+    nq[3] = dq[3] * q[3] - dq[0] * q[0] - dq[1] * q[1] - dq[2] * q[2];
+    nq[0] = dq[3] * q[0] + dq[0] * q[3] + dq[1] * q[2] - dq[2] * q[1];
+    nq[1] = dq[3] * q[1] - dq[0] * q[2] + dq[1] * q[3] + dq[2] * q[0];
+    nq[2] = dq[3] * q[2] + dq[0] * q[1] - dq[1] * q[0] + dq[2] * q[3];
+    const float inv = frsq(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = nq[i] * inv;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    S.qd[j] += h * qdd[j];
+    S.q[j] += h * S.qd[j];
+  }
+  MARK(integrate_done);
+  // this lane's contact forces of the sub-step (the last sub-step's survive the loop); summed
+  // over the roles once, after the loop (cf_sum): no branch and no cross-lane work here
+  (void)cf_out;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    cf_raw[i] = Fpt[i].x;
+    cf_raw[3 + i] = Fpt[i].y;
+  }
+}
+
+// reported contact forces from the last sub-step's per-lane values: thigh, calf, foot of
+// the lane's leg (role sums) and the base (role and leg sums)
+__device__ __forceinline__ void cf_sum(const float* cf_raw, int role, float* cf_leg, float* cf_base) {
+  // cf_raw: world forces of the lane's two points (x, y); rows 0 (thigh, thigh), 1 (thigh, corner),
+  // 2 (calf, calf), 3 (foot, corner)
+  float v[12];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float x = cf_raw[i], y = cf_raw[3 + i];
+    v[i] = role == 0 ? x + y : (role == 1 ? x : 0.0f);  // thigh
+    v[3 + i] = role == 2 ? x + y : 0.0f;                 // calf
+    v[6 + i] = role == 3 ? x : 0.0f;                     // foot
+    v[9 + i] = (role & 1) ? y : 0.0f;                    // trunk corners
+  }
+  rowsum4_n<12>(v);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) cf_leg[i] = v[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) cf_base[i] = qsum(v[9 + i]);
+}
+
+#pragma clang fp contract(off)
+

@@ -1,0 +1,1260 @@
+// go1_velocity.hip -- MI355X (gfx950) fused Go1 velocity-tracking step + C ABI (include/go1_velocity.h).
+//
+// One go1_vel_step = one VelocityTrackingEasyEnv.step + HistoryWrapper.step
+// (go1_gym/envs/base/legged_robot_velocity_tracking.py, bare :N below) in two launches:
+//   go1_vel_step_kernel: 4 x [actuator-net torques (:925-964) -> the native articulated-body integrator
+//     of go1_device.h (phys_substep, plane terrain)] -> post-physics (:108-154): kinematics, the gait
+//     clock (_step_contact_targets :844-923), DR (:714-717), terminations (:156-166), the CoRL reward
+//     terms and command sums (:281-318, go1_gym/envs/rewards/corl_rewards.py), reset_idx's state part
+//     (:168-257), observations (:320-509), the epilogue (:144-149) and the appended obs_history row.
+//   go1_vel_curriculum_kernel: workgroup 0 runs _resample_commands (:728-842) for the envs the step reset
+//     (RewardThresholdCurriculum.update, Curriculum.sample: go1_gym/envs/base/curriculum.py) and patches
+//     their observed commands, then the interval resample of the next step ahead of time; the other
+//     workgroups shift the history (obs_history[:, 70:] -> the new buffer).
+// Lane layout of the step kernel as in go1_step.hip: 16 lanes per env = 4 legs x 4 roles, four envs per
+// one-wave block.  Post-physics arithmetic is f32 with contraction off in torch's operation order, the
+// transcendentals of the gait clock and the rewards via f64 (correctly rounded f32 but for rare double
+// roundings), so the results match oracle/vel_oracle.py to the ulp of numpy's own exp / sin / erf.
+#include "go1_device.h"
+#include "../../include/go1_velocity.h"
+
+typedef const __attribute__((address_space(4))) go1_vel_config VCfg;
+#define VLAG 2  // GO1_LAG_STEPS(decimation) for decimation 4..6 (go1_vel_create checks it)
+#define SQRT2_F 1.41421353816986083984f  // (float)math.sqrt(2)
+#define CAT_PRONK 0
+#define CAT_TROT 1
+#define CAT_PACE 2
+#define CAT_BOUND 3
+
+// ---------------------------------------------------------------- f64 draws (curriculum RandomState)
+struct RngD {
+  const double* U;  // parity mode (n_envs, GO1_VEL_D_PER_ENV) or nullptr
+  uint64_t seed, step;
+  int e, gid;
+  __device__ double operator()(int slot) const {
+    if (U) return U[(size_t)e * GO1_VEL_D_PER_ENV + slot];
+    // numpy's random_sample from two 32-bit words: (a >> 5, b >> 6) -> 53 bits
+    uint32_t c[4] = {(uint32_t)gid, 0x40000000u | ((uint32_t)slot >> 1), (uint32_t)step, (uint32_t)(step >> 32)};
+    philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t a = c[2 * (slot & 1)] >> 5, b = c[2 * (slot & 1) + 1] >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+  }
+};
+
+// ---------------------------------------------------------------- f32 helpers (torch order)
+__device__ __forceinline__ float sin_rn(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cos_rn(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float exp_rn(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float erf_rn(float x) { return (float)erf((double)x); }
+// torch.distributions.Normal(0, kappa).cdf: 0.5 (1 + erf((x - 0) (1 / kappa) / sqrt(2)))
+__device__ __forceinline__ float normal_cdf(float x, float inv_kappa) {
+  return 0.5f * (1.0f + erf_rn((x - 0.0f) * inv_kappa / SQRT2_F));
+}
+__device__ __forceinline__ float norm4_f(float a, float b, float c, float d) {
+  return sqrtf(fmaf(d, d, fmaf(c, c, fmaf(b, b, a * a))));
+}
+// isaacgym.torch_utils.quat_apply: b + w t + xyz x t, t = 2 (xyz x b)
+__device__ __forceinline__ void quat_apply_f(const float* a, const float* b, float* o) {
+  float t[3] = {(a[1] * b[2] - a[2] * b[1]) * 2.0f, (a[2] * b[0] - a[0] * b[2]) * 2.0f,
+                (a[0] * b[1] - a[1] * b[0]) * 2.0f};
+  float c[3] = {a[1] * t[2] - a[2] * t[1], a[2] * t[0] - a[0] * t[2], a[0] * t[1] - a[1] * t[0]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = (b[i] + a[3] * t[i]) + c[i];
+}
+__device__ __forceinline__ void normalize4_f(float* q) {
+  float n = norm4_f(q[0], q[1], q[2], q[3]);
+  if (n < 1e-9f) n = 1e-9f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = q[i] / n;
+}
+// quat_from_angle_axis for a unit coordinate axis (then quat_unit)
+__device__ __forceinline__ void quat_from_axis_f(float angle, int axis, float* q) {
+  const float th = angle / 2.0f, s = sin_rn(th), c = cos_rn(th);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) q[i] = (i == axis ? 1.0f : 0.0f) * s;
+  q[3] = c;
+  normalize4_f(q);
+}
+// isaacgym.torch_utils.quat_mul (the factored product)
+__device__ __forceinline__ void quat_mul_f(const float* a, const float* b, float* o) {
+  const float x1 = a[0], y1 = a[1], z1 = a[2], w1 = a[3], x2 = b[0], y2 = b[1], z2 = b[2], w2 = b[3];
+  const float ww = (z1 + x1) * (x2 + y2), yy = (w1 - y1) * (w2 + z2), zz = (w1 + y1) * (w2 - z2);
+  const float xx = ww + yy + zz;
+  const float qq = 0.5f * (xx + (z1 - x1) * (x2 - y2));
+  o[3] = qq - ww + (z1 - y1) * (y2 - z2);
+  o[0] = qq - xx + (x1 + w1) * (x2 + w2);
+  o[1] = qq - yy + (w1 - x1) * (y2 + z2);
+  o[2] = qq - zz + (z1 + y1) * (w2 - x2);
+}
+// the value of leg I's lane of this lane's quad (the legs of an (env, role)), DPP quad_perm broadcast
+template <int I>
+__device__ __forceinline__ float quad_at(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), I * 0x55, 0xF, 0xF, true));
+}
+// (((0 + t0) + t1) + t2) + t3: the reference's `reward = 0; for i: reward += t_i` over the four feet
+__device__ __forceinline__ float quad_seq_sum(float v) {
+  return (((0.0f + quad_at<0>(v)) + quad_at<1>(v)) + quad_at<2>(v)) + quad_at<3>(v);
+}
+// obs column without noise (noise_vec 0): v + (2u - 1) * 0 changes only a -0.0 (to +0.0 for u >= 0.5)
+__device__ __forceinline__ float noise_free(float v, bool add_noise, const Rng& rng, int slot) {
+  if (add_noise && v == 0.0f && signbit(v)) {
+    if (rng(slot) >= 0.5f) v = 0.0f;
+  }
+  return v;
+}
+
+// World position and velocity of this leg's foot body origin (rigid_body_state[:, feet, 0:3 / 7:10])
+// from the base state and the leg's joints: motion transforms down the chain (xm), then the foot
+// offset in the calf frame (point_kin).
+__device__ void foot_state(const float* root, const float* q, const float* qd, int leg, float* fp, float* fv) {
+  const float sx = (leg & 2) ? -1.0f : 1.0f, sy = (leg & 1) ? -1.0f : 1.0f;
+  float Rp[9], pp[3] = {root[0], root[1], root[2]}, vb[6];
+  quat_to_R(root + 3, Rp);
+  mat3T_vec(Rp, root + 10, vb);
+  mat3T_vec(Rp, root + 7, vb + 3);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float o[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = 30 + 3 * j + k, sp = GO1_LEG_SIGN[i];
+      o[k] = GO1_LEG_FL[i] * (sp == 0 ? 1.0f : (sp == 1 ? sx : (sp == 2 ? sy : sx * sy)));
+    }
+    const int ax = j == 0 ? 0 : 1;
+    float sn, cn, vj[6], rw[3];
+    pm_sincosf(q[j], &sn, &cn);
+    xm(ax, cn, sn, offset_mask(j), o, vb, vj);
+    vj[ax] += qd[j];
+    mat3_vec(Rp, o, rw);
+    pp[0] += rw[0]; pp[1] += rw[1]; pp[2] += rw[2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rE(ax, cn, sn, Rp + 3 * a, Rp + 3 * a);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) vb[i] = vj[i];
+  }
+  point_kin(Rp, pp, vb, GO1_MODEL_F32 + 13 * 10 + 4 * 9, fp, fv);
+}
+
+// reset_idx's state part for one env, on the lane of leg `leg` (:168-257 after _resample_commands):
+// _randomize_dof_props (:663-683), _reset_dofs (:966-981), _reset_root_states (:983-1019, plane: no
+// custom origins).  u(slot): the env's f32 uniforms.
+template <class U>
+__device__ void vel_reset_env(VCfg* v, const U& u, const float* eo, int leg, float* root, float* q, float* qd,
+                              float* strength, float* offset) {
+  const float s = u(GO1_VEL_U_RESET_DR) * v->strength_range + v->strength_lo;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int d = leg * 3 + j;
+    strength[j] = s;
+    offset[j] = u(GO1_VEL_U_RESET_DR + 1 + d) * v->offset_range + v->offset_lo;
+    q[j] = v->default_dof_pos[d] * (v->reset_dof_range * u(GO1_VEL_U_RESET_DOF + d) + v->reset_dof_lo);
+    qd[j] = 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 13; ++i) root[i] = v->base_init_state[i];
+  root[0] = root[0] + eo[0];
+  root[1] = root[1] + eo[1];
+  root[2] = root[2] + eo[2];
+  const float yaw = v->yaw_range * u(GO1_VEL_U_RESET_YAW) + v->yaw_lo;
+  quat_from_axis_f(yaw, 2, root + 3);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) root[7 + i] = v->reset_vel_range * u(GO1_VEL_U_RESET_VEL + i) + v->reset_vel_lo;
+}
+
+// =====================================================================
+//                          the fused step kernel
+// =====================================================================
+struct VArgs {
+  go1_vel_state st;
+  go1_vel_step_args a;
+  const float* env_origins;
+  int hist_w;  // obs_history row width (70 x history_len)
+};
+
+template <bool INJ>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) void go1_vel_step_kernel(
+    const go1_config* __restrict__ c_gen, const go1_vel_config* __restrict__ v_gen, VArgs K) {
+  CCfg* __restrict__ c = (CCfg*)c_gen;
+  VCfg* __restrict__ v = (VCfg*)v_gen;
+  const go1_vel_state& st = K.st;
+  const go1_vel_step_args& A = K.a;
+  const int lane = threadIdx.x & 63, leg = lane & 3, lq = lane >> 4;
+  const int role = lane >> 4, el = (lane >> 2) & 3, sub16 = 4 * role + leg;
+  const bool owner = role == 0;
+  const int e = blockIdx.x * SEPB + el;  // n % 16 == 0 (go1_vel_create)
+  MlpFrag F;
+  mlp_load(c_gen->actuator, lane, F);
+  const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset, GO1_VEL_U_PER_ENV};
+  const size_t d0 = (size_t)e * NDOF + leg * 3;
+  const int dec = c->decimation;
+  const float* lag_in = st.lag + (size_t)e * 12 * VLAG + leg * 3;
+  const int NT = v->n_terms;
+
+  // ---------------- load
+  float act[3], q[3], qd[3], eh[2][3], vh[2][3], strength[3], offset[3], dflt[3], tlim[3], lag_pre[VLAG][3];
+  float ldv[3], la[3], lla[3], ljpt[3], lljpt[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    act[j] = clampf(A.actions[d0 + j], -c->clip_actions, c->clip_actions);
+    q[j] = st.dof_pos[d0 + j];
+    qd[j] = st.dof_vel[d0 + j];
+    strength[j] = st.motor_strength[d0 + j];
+    offset[j] = st.motor_offset[d0 + j];
+    eh[0][j] = st.pos_err_hist[(size_t)e * 24 + leg * 3 + j];
+    eh[1][j] = st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j];
+    vh[0][j] = st.vel_hist[(size_t)e * 24 + leg * 3 + j];
+    vh[1][j] = st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j];
+    dflt[j] = c->default_dof_pos[leg * 3 + j];
+    tlim[j] = c->torque_limits[leg * 3 + j];
+#pragma unroll
+    for (int k = 0; k < VLAG; ++k) lag_pre[k][j] = lag_in[k * 12 + j];
+    ldv[j] = st.last_dof_vel[d0 + j];
+    la[j] = st.last_actions[d0 + j];
+    lla[j] = st.last_last_actions[d0 + j];
+    ljpt[j] = st.last_joint_pos_target[d0 + j];
+    lljpt[j] = st.last_last_joint_pos_target[d0 + j];
+  }
+  const float friction = st.friction[e], payload = st.payload[e], restitution = st.restitution[e];
+  const float eo_pre[3] = {K.env_origins[(size_t)e * 3], K.env_origins[(size_t)e * 3 + 1],
+                           K.env_origins[(size_t)e * 3 + 2]};
+  const int ep_in = st.episode_length[e];
+  const float gait_in = st.gait_indices[e];
+  const float lc_in = st.last_contacts[(size_t)e * 4 + leg];
+  float cmd[GO1_VEL_NUM_COMMANDS];
+#pragma unroll
+  for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) cmd[k] = st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + k];
+  // reward slots: lane sub16 holds slots sub16 and 16 + sub16 (command sums: NT + 5 of them, episode sums
+  // NT + 1: the terms, then "total")
+  const int NC = NT + GO1_VEL_SUM_EXTRA, NE = NT + 1;
+  float cs[2], es[2];
+  float my_scale[2];
+  int my_id[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = sub16 + 16 * h;
+    cs[h] = k < NC ? st.command_sums[(size_t)e * NC + k] : 0.0f;
+    es[h] = k < NE ? st.episode_sums[(size_t)e * NE + k] : 0.0f;
+    my_scale[h] = k < NT ? A.reward_scales[k] : 0.0f;
+    my_id[h] = k < NT ? v_gen->term_ids[k] : -1;
+  }
+  Phys P;
+  if (!INJ) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      P.pos[i] = st.root[(size_t)e * 13 + i];
+      P.wv[i] = f2{st.root[(size_t)e * 13 + 10 + i], st.root[(size_t)e * 13 + 7 + i]};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
+  }
+  const Terr T = {nullptr, 0, 0, 1.0f, nullptr, 0, 0};  // the plane: floor z = 0, no ceiling
+  float scaled[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    scaled[j] = act[j] * c->action_scale;
+    if (j == 0) scaled[j] = scaled[j] * c->hip_scale_reduction;
+  }
+
+  // ---------------- decimation loop (:76-82): lag ring pushed per sim step (:940-942)
+  float torque[3], tgt[3];
+  float cf_raw[6] = {0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
+  for (int sub = 0; sub < dec; ++sub) {
+    {
+      const int m = 6 - sub;
+      const int back = m <= 0 ? 0 : (m + dec - 1) / dec;
+      float xin[3][6];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        float lg = scaled[j];
+#pragma unroll
+        for (int k = 0; k < VLAG; ++k) lg = back == VLAG - k ? lag_pre[k][j] : lg;
+        tgt[j] = lg + dflt[j];
+        const float err = q[j] - tgt[j] + offset[j];
+        xin[j][0] = err; xin[j][1] = eh[0][j]; xin[j][2] = eh[1][j];
+        xin[j][3] = qd[j]; xin[j][4] = vh[0][j]; xin[j][5] = vh[1][j];
+      }
+      float tq[3] = {0.0f, 0.0f, 0.0f}, b0[3], b1v[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float* y = xin[j];
+        b0[j] = sel4(lq, y[0], y[1], y[2], y[3]);
+        b1v[j] = sel4(lq, y[4], y[5], 0.0f, 0.0f);
+      }
+      mlp_group3(F, b0, b1v, tq);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        eh[1][j] = eh[0][j];
+        eh[0][j] = xin[j][0];
+        vh[1][j] = vh[0][j];
+        vh[0][j] = qd[j];
+        torque[j] = clampf(tq[j] * strength[j], -tlim[j], tlim[j]);
+      }
+    }
+    if (INJ) {
+      const float* id = A.inj_dof + ((size_t)sub * c->n_envs + e) * NDOF * 2;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        q[j] = id[(leg * 3 + j) * 2];
+        qd[j] = id[(leg * 3 + j) * 2 + 1];
+      }
+    } else {
+      const float h = c->sim_dt / (float)c->n_internal;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) { P.q[j] = q[j]; P.qd[j] = qd[j]; }
+      for (int k = 0; k < c->n_internal; ++k) {
+        const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
+        phys_substep(c, nullptr, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }
+    }
+    if (A.dbg_torques && owner) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) A.dbg_torques[((size_t)sub * c->n_envs + e) * NDOF + leg * 3 + j] = torque[j];
+    }
+  }
+  float root[13], fp[3], fv[3];
+  if (INJ) {
+#pragma unroll
+    for (int i = 0; i < 13; ++i) root[i] = A.inj_root[(size_t)e * 13 + i];
+    const float* ic = A.inj_contact + (size_t)e * NB * 3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cf_base[i] = ic[i];
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cf_leg[b * 3 + i] = ic[(2 + leg * 4 + b) * 3 + i];
+    const float* ft = A.inj_feet + ((size_t)e * 4 + leg) * 6;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { fp[i] = ft[i]; fv[i] = ft[3 + i]; }
+  } else {
+    cf_sum(cf_raw, role, cf_leg, cf_base);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      root[i] = P.pos[i]; root[7 + i] = P.wv[i].y; root[10 + i] = P.wv[i].x;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) root[3 + i] = P.quat[i];
+    foot_state(root, q, qd, leg, fp, fv);
+  }
+  if (A.contact_forces && owner) {
+    float* o = A.contact_forces + (size_t)e * NB * 3;
+    if (leg == 0) { o[0] = cf_base[0]; o[1] = cf_base[1]; o[2] = cf_base[2]; }
+    float* ol = o + (1 + leg * 4) * 3;
+    ol[0] = 0.0f; ol[1] = 0.0f; ol[2] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) ol[3 + i] = cf_leg[i];
+  }
+
+  // ================= post_physics_step (:108-154), contraction off =================
+  const int ep = ep_in + 1;
+  float blv[3], bav[3], pg[3];
+  {
+    const float qb[4] = {root[3], root[4], root[5], root[6]};
+    quat_rotate_inverse_f(qb, root + 7, blv);
+    quat_rotate_inverse_f(qb, root + 10, bav);
+    quat_rotate_inverse_f(qb, A.gravity_vec, pg);
+  }
+  // ---- _step_contact_targets (:844-923): this lane's foot
+  const float gait = remainder_f(gait_in + v->dt * cmd[4], 1.0f);
+  float fi_raw;
+  {
+    const float ph = cmd[5], off = cmd[6], bnd = cmd[7];
+    const float f0 = ((gait + ph) + off) + bnd, f1 = gait + off, f2_ = gait + bnd, f3 = gait + ph;
+    fi_raw = leg == 0 ? f0 : (leg == 1 ? f1 : (leg == 2 ? f2_ : f3));
+  }
+  const float foot_idx = remainder_f(fi_raw, 1.0f);  // self.foot_indices
+  float fiw = fi_raw;
+  {
+    const float dur = cmd[8], r = remainder_f(fi_raw, 1.0f);
+    if (r < dur) fiw = r * (0.5f / dur);
+    else if (r > dur) fiw = 0.5f + (r - dur) * (0.5f / (1.0f - dur));
+  }
+  const float clock = sin_rn(TWO_PI_F * fiw);
+  float desired;
+  {
+    const float ik = 1.0f / v->kappa_gait_probs, r = remainder_f(fiw, 1.0f);
+    desired = normal_cdf(r, ik) * (1.0f - normal_cdf(r - 0.5f, ik)) +
+              normal_cdf(r - 1.0f, ik) * (1.0f - normal_cdf((r - 0.5f) - 1.0f, ik));
+  }
+  if (A.dbg_gait && owner) {
+    float* g = A.dbg_gait + (size_t)e * 12;
+    g[leg] = foot_idx;
+    g[4 + leg] = clock;
+    g[8 + leg] = desired;
+  }
+  // ---- DR every rand_interval (:714-717)
+  const bool dr_step = ep % v->rand_interval == 0;
+  if (dr_step) {
+    const float sv = rng(GO1_VEL_U_DR) * v->strength_range + v->strength_lo;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      strength[j] = sv;
+      offset[j] = rng(GO1_VEL_U_DR + 1 + leg * 3 + j) * v->offset_range + v->offset_lo;
+    }
+  }
+  // ---- check_termination (:156-166): base contact, time-out, body height (measured_heights = 0 on a plane)
+  const bool time_out = (float)ep > v->max_episode_length;
+  bool reset = norm3_f(cf_base[0], cf_base[1], cf_base[2]) > 1.0f || time_out;
+  if (v->use_terminal_body_height && root[2] < v->terminal_body_height) reset = true;
+  bool diverged = false;
+  if (!INJ) {  // native-integrator divergence guard (go1_step.hip): the env is reset, its rewards zeroed
+    bool finite = true;
+#pragma unroll
+    for (int i = 0; i < 13; ++i) finite = finite && fabsf(root[i]) < GO1_DIVERGED;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) finite = finite && fabsf(q[j]) < GO1_DIVERGED && fabsf(qd[j]) < GO1_DIVERGED;
+    diverged = qsum(finite ? 0.0f : 1.0f) != 0.0f;
+    if (diverged) reset = true;
+  }
+
+  // ---- compute_reward (:281-318): CoRLRewards terms filed by id in an LDS row per env
+  __shared__ float s_terms[SEPB][GO1_VT_COUNT];
+#define PUT(id, val)                           \
+  do {                                         \
+    const float v_ = (val);                    \
+    if (sub16 == 0) s_terms[el][(id)] = v_;    \
+  } while (0)
+  auto sum12 = [](const float* x) { return qsum((x[0] + x[1]) + x[2]); };
+  {
+    const float d0_ = cmd[0] - blv[0], d1_ = cmd[1] - blv[1];
+    PUT(GO1_VT_TRACKING_LIN_VEL, exp_rn(-(d0_ * d0_ + d1_ * d1_) / v->tracking_sigma));
+    const float dz = cmd[2] - bav[2];
+    PUT(GO1_VT_TRACKING_ANG_VEL, exp_rn(-(dz * dz) / v->tracking_sigma_yaw));
+  }
+  PUT(GO1_VT_LIN_VEL_Z, blv[2] * blv[2]);
+  PUT(GO1_VT_ANG_VEL_XY, bav[0] * bav[0] + bav[1] * bav[1]);
+  PUT(GO1_VT_ORIENTATION, pg[0] * pg[0] + pg[1] * pg[1]);
+  {
+    float x[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = torque[j] * torque[j];
+    PUT(GO1_VT_TORQUES, sum12(x));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = qd[j] * qd[j];
+    PUT(GO1_VT_DOF_VEL, sum12(x));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { const float a = (ldv[j] - qd[j]) / v->dt; x[j] = a * a; }
+    PUT(GO1_VT_DOF_ACC, sum12(x));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { const float a = la[j] - act[j]; x[j] = a * a; }
+    PUT(GO1_VT_ACTION_RATE, sum12(x));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int d = leg * 3 + j;
+      const float lo = fminf(q[j] - v->dof_pos_limits[2 * d], 0.0f);
+      const float hi = fmaxf(q[j] - v->dof_pos_limits[2 * d + 1], 0.0f);
+      x[j] = -lo + hi;
+    }
+    PUT(GO1_VT_DOF_POS_LIMITS, sum12(x));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { const float a = q[j] - v->default_dof_pos[leg * 3 + j]; x[j] = a * a; }
+    PUT(GO1_VT_DOF_POS, sum12(x));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float a = tgt[j] - ljpt[j];
+      x[j] = (a * a) * (la[j] != 0.0f ? 1.0f : 0.0f);
+    }
+    PUT(GO1_VT_ACTION_SMOOTHNESS_1, sum12(x));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float a = tgt[j] - 2.0f * ljpt[j] + lljpt[j];
+      x[j] = ((a * a) * (la[j] != 0.0f ? 1.0f : 0.0f)) * (lla[j] != 0.0f ? 1.0f : 0.0f);
+    }
+    PUT(GO1_VT_ACTION_SMOOTHNESS_2, sum12(x));
+  }
+  {  // collision on thighs and calves (penalize_contacts_on): integer counts, exact in any order
+    const float th = norm3_f(cf_leg[0], cf_leg[1], cf_leg[2]) > 0.1f ? 1.0f : 0.0f;
+    const float ca = norm3_f(cf_leg[3], cf_leg[4], cf_leg[5]) > 0.1f ? 1.0f : 0.0f;
+    PUT(GO1_VT_COLLISION, qsum(th) + qsum(ca));
+  }
+  {
+    const float d = root[2] - (cmd[3] + v->base_height_target);
+    PUT(GO1_VT_JUMP, -(d * d));
+  }
+  {
+    const float ff = norm3_f(cf_leg[6], cf_leg[7], cf_leg[8]);
+    const float tf = -(1.0f - desired) * (1.0f - exp_rn(-1.0f * (ff * ff) / v->gait_force_sigma));
+    PUT(GO1_VT_TRACKING_CONTACTS_SHAPED_FORCE, quad_seq_sum(tf) / 4.0f);
+    const float vv = norm3_f(fv[0], fv[1], fv[2]);
+    const float tv = -(desired * (1.0f - exp_rn(-1.0f * (vv * vv) / v->gait_vel_sigma)));
+    PUT(GO1_VT_TRACKING_CONTACTS_SHAPED_VEL, quad_seq_sum(tv) / 4.0f);
+  }
+  // feet_slip (corl:107-113) updates last_contacts when it is evaluated
+  const bool slip_live = [&] {
+    bool l = false;
+    for (int k = 0; k < NT; ++k) l = l || v->term_ids[k] == GO1_VT_FEET_SLIP;
+    return l;
+  }();
+  const bool contact = cf_leg[8] > 1.0f;
+  {
+    const bool filt = contact || lc_in != 0.0f;
+    const float sp = norm2_f(fv[0], fv[1]);
+    PUT(GO1_VT_FEET_SLIP, qsum((filt ? 1.0f : 0.0f) * (sp * sp)));
+  }
+  {  // feet_clearance_cmd_linear (corl:130-135)
+    const float phs = 1.0f - fabsf(1.0f - clampf(foot_idx * 2.0f - 1.0f, 0.0f, 1.0f) * 2.0f);
+    const float th = cmd[9] * phs + 0.02f;
+    const float d = th - fp[2];
+    PUT(GO1_VT_FEET_CLEARANCE_CMD_LINEAR, qsum((d * d) * (1.0f - desired)));
+  }
+  {  // orientation_control (corl:181-193)
+    float qr[4], qp[4], dq[4], dpg[3];
+    quat_from_axis_f(-cmd[11], 0, qr);
+    quat_from_axis_f(-cmd[10], 1, qp);
+    quat_mul_f(qr, qp, dq);
+    quat_rotate_inverse_f(dq, A.gravity_vec_after, dpg);
+    const float a = pg[0] - dpg[0], b = pg[1] - dpg[1];
+    PUT(GO1_VT_ORIENTATION_CONTROL, a * a + b * b);
+  }
+  {  // raibert_heuristic (corl:195-237)
+    const float rel[3] = {fp[0] - root[0], fp[1] - root[1], fp[2] - root[2]};
+    float qy[4] = {0.0f, 0.0f, -root[5], root[6]};  // quat_apply_yaw(quat_conjugate(base_quat), .)
+    normalize4_f(qy);
+    float fb[3];
+    quat_apply_f(qy, rel, fb);
+    const float w = cmd[12], ln = cmd[13];
+    const float ys = (leg & 1) ? -w / 2.0f : w / 2.0f;
+    const float xs = (leg & 2) ? -ln / 2.0f : ln / 2.0f;
+    const float phs = fabsf(1.0f - foot_idx * 2.0f) * 1.0f - 0.5f;
+    const float freq = cmd[4];
+    const float y_vel = cmd[2] * ln / 2.0f;
+    float yo = phs * y_vel * (0.5f / freq);
+    if (leg >= 2) yo = yo * -1.0f;
+    const float xo = phs * cmd[0] * (0.5f / freq);
+    const float ex = fabsf((xs + xo) - fb[0]), ey = fabsf((ys + yo) - fb[1]);
+    PUT(GO1_VT_RAIBERT_HEURISTIC, qsum(ex * ex + ey * ey));
+  }
+#undef PUT
+  // slot order (:289-301): rew += term * scale; pos / neg by the slot's fixed sign; episode and
+  // command sums per slot lane
+  __shared__ float s_r[SEPB][GO1_VEL_MAX_TERMS];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = sub16 + 16 * h;
+    if (k < NT) {
+      float t = s_terms[el][my_id[h]];
+      if (diverged) t = 0.0f;
+      if (A.dbg_terms) A.dbg_terms[(size_t)e * GO1_VEL_MAX_TERMS + k] = t;
+      const float r = t * my_scale[h];
+      s_r[el][k] = r;
+      es[h] = es[h] + r;
+      const bool shaped = my_id[h] == GO1_VT_TRACKING_CONTACTS_SHAPED_FORCE ||
+                          my_id[h] == GO1_VT_TRACKING_CONTACTS_SHAPED_VEL;
+      cs[h] = cs[h] + (shaped ? my_scale[h] + r : r);
+    }
+  }
+  float rew = 0.0f, pos = 0.0f, neg = 0.0f;
+  {
+    const uint32_t np = v->nonpos_slots;
+    for (int k = 0; k < NT; ++k) {
+      const float r = s_r[el][k];
+      rew = rew + r;
+      if ((np >> k) & 1u) neg = neg + r; else pos = pos + r;
+    }
+  }
+  if (v->reward_mode == 1) rew = rew < 0.0f ? 0.0f : rew;
+  else if (v->reward_mode == 2) rew = pos * exp_rn(neg / v->sigma_rew_neg);
+  if (diverged) rew = 0.0f;
+  // episode_sums["total"] (:306) and the command-sum extras (:314-318)
+  {
+    const float rx = blv[0] - cmd[0], rz = bav[2] - cmd[2];
+    const float extra[GO1_VEL_SUM_EXTRA] = {blv[0], bav[2], rx * rx, rz * rz, 1.0f};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = sub16 + 16 * h;
+      if (k == NT) es[h] = es[h] + rew;
+      if (k >= NT && k < NC && !diverged) cs[h] = cs[h] + extra[min(max(k - NT, 0), GO1_VEL_SUM_EXTRA - 1)];
+    }
+  }
+
+  // ---- reset_idx (:168-257) state part; the commands are resampled by the curriculum launch
+  float lla_out[3], la_obs[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) { la_obs[j] = la[j]; }
+  float gait_out = gait;
+  if (A.episode_log_count) {
+    const uint64_t rmask = __ballot(reset && owner && leg == 0);
+    if (rmask != 0ull) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(A.episode_log_count, __popcll(rmask));
+      base = __shfl(base, 0);
+      const int row = base + __popcll(rmask & ((1ull << (4 * el)) - 1ull));
+      if (reset && A.episode_log_cap > 0) {  // a ring: the newest rows overwrite the oldest
+        float* lg = A.episode_log + (size_t)(row % A.episode_log_cap) * (NE + 2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (sub16 + 16 * h < NE) lg[sub16 + 16 * h] = es[h];
+        if (sub16 == 0) { lg[NE] = (float)A.episode_log_tag; lg[NE + 1] = (float)e; }
+      }
+    }
+  }
+  if (reset) {
+    __shared__ float s_ru[SEPB][48];
+    // the reset's uniforms (slots 12 .. 59 = Philox blocks 3 .. 14): lane sub16 < 12 draws block 3 + sub16
+    if (sub16 < 12) {
+      float uq[4];
+      rng.quad(3 + sub16, uq);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_ru[el][4 * sub16 + k] = uq[k];
+    }
+    const float* ru = s_ru[el];
+    auto u = [ru](int slot) { return ru[slot - 12]; };
+    vel_reset_env(v, u, eo_pre, leg, root, q, qd, strength, offset);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) la_obs[j] = 0.0f;
+    gait_out = 0.0f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) es[h] = 0.0f;
+    if (diverged) {  // observe the post-reset pose; clear the actuator-net history of the diverged state
+      const float qb[4] = {root[3], root[4], root[5], root[6]};
+      quat_rotate_inverse_f(qb, A.gravity_vec, pg);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) eh[0][j] = eh[1][j] = vh[0][j] = vh[1][j] = 0.0f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) lla_out[j] = la_obs[j];  // epilogue: last_last_actions <- last_actions
+
+  // ---- compute_observations (:320-509): role r < 3 writes joint r's four columns, role 3 leg l the
+  // gravity component l (l < 3), commands l, l + 4, l + 8, l + 12 and the clock of foot l
+  float* o = A.obs + (size_t)e * GO1_VEL_NUM_OBS;
+  float* oh = A.obs_history_out ? A.obs_history_out + (size_t)e * K.hist_w + (K.hist_w - GO1_VEL_NUM_OBS) : nullptr;
+  const float clip = v->clip_obs;
+  const bool noisy = v->add_noise != 0;
+  auto put = [&](int i, float val) {
+    val = clampf(val, -clip, clip);
+    o[i] = val;
+    if (oh) oh[i] = val;
+  };
+  auto noise = [&](float val, int i, float u) { return noisy ? val + (2.0f * u - 1.0f) * v->noise_vec[i] : val; };
+  if (role < 3) {
+    const int j = role, d = leg * 3 + j;
+    const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act), lj = sel3(j, la_obs);
+    float uq = 0.0f, uv = 0.0f;
+    if (noisy) {
+      uq = rng(GO1_VEL_U_NOISE + 18 + d);
+      uv = rng(GO1_VEL_U_NOISE + 30 + d);
+    }
+    put(18 + d, noise((qj - v->default_dof_pos[d]) * v->obs_scale_dof_pos, 18 + d, uq));
+    put(30 + d, noise(qdj * v->obs_scale_dof_vel, 30 + d, uv));
+    put(42 + d, noise_free(aj, noisy, rng, GO1_VEL_U_NOISE + 42 + d));
+    put(54 + d, noise_free(lj, noisy, rng, GO1_VEL_U_NOISE + 54 + d));
+  } else {
+    if (leg < 3) {
+      const float g = sel3(leg, pg);
+      put(leg, noise(g, leg, noisy ? rng(GO1_VEL_U_NOISE + leg) : 0.0f));
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int k = leg + 4 * m;
+      if (k < GO1_VEL_NUM_COMMANDS) {
+        const float ck = sel4(leg, cmd[4 * m], cmd[4 * m + 1], cmd[4 * m + 2], cmd[4 * m + 3 < 15 ? 4 * m + 3 : 14]);
+        put(3 + k, noise_free(ck * v->cmd_scale[k], noisy, rng, GO1_VEL_U_NOISE + 3 + k));
+      }
+    }
+    put(66 + leg, noise_free(clock, noisy, rng, GO1_VEL_U_NOISE + 66 + leg));
+  }
+  if (sub16 == 0) {
+    float* pv = A.priv + (size_t)e * 2;
+    pv[0] = clampf((friction - v->priv_friction_shift) * v->priv_friction_scale, -clip, clip);
+    pv[1] = clampf((restitution - v->priv_rest_shift) * v->priv_rest_scale, -clip, clip);
+  }
+  if (A.aux) {
+    float* ax = A.aux + (size_t)e * GO1_VEL_AUX;
+    if (role == 3 && leg == 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { ax[i] = blv[i]; ax[3 + i] = bav[i]; }
+    }
+    if (role == 1) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ax[6 + leg * 3 + i] = fp[i];
+    }
+    if (owner) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        ax[18 + leg * 3 + i] = torque[i];
+        ax[30 + leg * 3 + i] = tgt[i];
+      }
+    }
+  }
+
+  // ---------------- write back (epilogue :144-149)
+  if (role < 3) {
+    const int j = role;
+    const size_t dj = d0 + j;
+    st.dof_pos[dj] = sel3(j, q);
+    st.dof_vel[dj] = sel3(j, qd);
+    st.last_dof_vel[dj] = sel3(j, qd);
+    st.last_actions[dj] = sel3(j, act);
+    st.last_last_actions[dj] = sel3(j, lla_out);
+    st.last_last_joint_pos_target[dj] = sel3(j, ljpt);
+    st.last_joint_pos_target[dj] = sel3(j, tgt);
+    if (reset || dr_step) {
+      st.motor_strength[dj] = sel3(j, strength);
+      st.motor_offset[dj] = sel3(j, offset);
+    }
+#pragma unroll
+    for (int k = 0; k < VLAG; ++k)
+      st.lag[(size_t)e * 12 * VLAG + k * 12 + leg * 3 + j] =
+          reset ? 0.0f : (k == VLAG - 1 ? sel3(j, scaled) : sel3(j, lag_pre[k + 1 < VLAG ? k + 1 : k]));
+    st.pos_err_hist[(size_t)e * 24 + leg * 3 + j] = sel3(j, eh[0]);
+    st.pos_err_hist[(size_t)e * 24 + 12 + leg * 3 + j] = sel3(j, eh[1]);
+    st.vel_hist[(size_t)e * 24 + leg * 3 + j] = sel3(j, vh[0]);
+    st.vel_hist[(size_t)e * 24 + 12 + leg * 3 + j] = sel3(j, vh[1]);
+  }
+  if (role == 3 && slip_live) st.last_contacts[(size_t)e * 4 + leg] = contact ? 1.0f : 0.0f;
+  if (role == 3 && leg == 0) {
+#pragma unroll
+    for (int i = 0; i < 13; ++i) st.root[(size_t)e * 13 + i] = root[i];
+    st.episode_length[e] = reset ? 0 : ep;
+    st.gait_indices[e] = gait_out;
+    A.rew[e] = rew;
+    A.reset[e] = reset;
+    A.time_out[e] = time_out;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = sub16 + 16 * h;
+    if (k < NC) st.command_sums[(size_t)e * NC + k] = cs[h];
+    if (k < NE) st.episode_sums[(size_t)e * NE + k] = es[h];
+  }
+}
+
+// explicit reset_idx(ids) state part (4 lanes per env, one per leg)
+__global__ __launch_bounds__(TPB) void go1_vel_reset_kernel(const go1_vel_config* __restrict__ v_gen,
+                                                            go1_vel_state st, const float* __restrict__ env_origins,
+                                                            const int32_t* __restrict__ ids, int n_ids, int n_envs,
+                                                            const float* __restrict__ U, uint64_t seed, uint64_t step,
+                                                            int env_id_offset, float* episode_log,
+                                                            int32_t* episode_log_count, int episode_log_cap,
+                                                            int episode_log_tag) {
+  VCfg* __restrict__ v = (VCfg*)v_gen;
+  const int leg = threadIdx.x & 3;
+  const int slot = blockIdx.x * EPB + (threadIdx.x >> 2);
+  if (slot >= n_ids) return;
+  const int e = ids[slot];
+  if (e < 0 || e >= n_envs) return;
+  const Rng rng = {U, seed, step, e, e + env_id_offset, GO1_VEL_U_PER_ENV};
+  const int NE = v->n_terms + 1;
+  if (leg == 0) {  // the episode log (:199-205) reads the sums, then reset_idx clears them
+    if (episode_log_count) {
+      const int row = atomicAdd(episode_log_count, 1);
+      if (episode_log_cap > 0) {
+        float* lg = episode_log + (size_t)(row % episode_log_cap) * (NE + 2);
+        for (int k = 0; k < NE; ++k) lg[k] = st.episode_sums[(size_t)e * NE + k];
+        lg[NE] = (float)episode_log_tag;
+        lg[NE + 1] = (float)e;
+      }
+    }
+    for (int k = 0; k < NE; ++k) st.episode_sums[(size_t)e * NE + k] = 0.0f;
+  }
+  float root[13], q[3], qd[3], strength[3], offset[3];
+  const float eo[3] = {env_origins[(size_t)e * 3], env_origins[(size_t)e * 3 + 1], env_origins[(size_t)e * 3 + 2]};
+  vel_reset_env(v, rng, eo, leg, root, q, qd, strength, offset);
+  const size_t d0 = (size_t)e * NDOF + leg * 3;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    st.dof_pos[d0 + j] = q[j];
+    st.dof_vel[d0 + j] = qd[j];
+    st.motor_strength[d0 + j] = strength[j];
+    st.motor_offset[d0 + j] = offset[j];
+    st.last_actions[d0 + j] = 0.0f;
+    st.last_last_actions[d0 + j] = 0.0f;
+    st.last_dof_vel[d0 + j] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < VLAG; ++k) st.lag[(size_t)e * 12 * VLAG + k * 12 + leg * 3 + j] = 0.0f;
+  }
+  if (leg == 0) {
+#pragma unroll
+    for (int i = 0; i < 13; ++i) st.root[(size_t)e * 13 + i] = root[i];
+    st.episode_length[e] = 0;
+    st.gait_indices[e] = 0.0f;
+  }
+}
+
+__global__ void go1_vel_mask_kernel(const int32_t* __restrict__ ids, int n_ids, int n, uint8_t* __restrict__ m) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_ids && ids[i] >= 0 && ids[i] < n) m[ids[i]] = 1;
+}
+
+// =====================================================================
+//        command curriculum (_resample_commands) + history shift
+// =====================================================================
+#define CK_THREADS 1024
+struct CArgs {
+  go1_vel_state st;
+  const double* grid;   // (GO1_VEL_N_KEYS, n_bins)
+  double* cdf;          // (GO1_VEL_N_CATEGORIES, n_bins): numpy's normalised cdf of each curriculum
+  int32_t* cdf_ok;      // [GO1_VEL_N_CATEGORIES]: cdf current for the weights
+  int n_envs, env_id_offset;
+  uint64_t seed;
+  // B kind: the envs of maskB (reset_idx's resample)
+  const uint8_t* maskB;
+  const float* UB;
+  const double* UDB;
+  uint64_t stepB;
+  // A kind: envs with (episode_length + 1) % resample_interval == 0 (the next step's interval resample)
+  int doA;
+  const float* UA;
+  const double* UDA;
+  uint64_t stepA;
+  // with B: extras["time_outs"] = time_out if some env was selected (:251-252), and the obs / obs_history
+  // command columns of the resampled envs
+  const uint8_t* time_out;
+  uint8_t* extras_time_outs;
+  float* obs;
+  float* hist_out;
+  const float* hist_in;
+  int hist_w;
+};
+
+// numpy's pairwise summation (np.add.reduce of a contiguous f64 array), PW_BLOCKSIZE 128
+template <int D>
+__device__ double np_pairwise_sum(const double* a, int n) {
+  if (D == 0 || n <= 128) {
+    if (n < 8) {
+      double r = 0.0;
+      for (int i = 0; i < n; ++i) r += a[i];
+      return r;
+    }
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a, n2) + np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a + n2, n - n2);
+}
+
+__device__ __forceinline__ float remainder1(float a) { return remainder_f(a, 1.0f); }
+
+// One resample (_resample_commands :728-842) of kind B (mask) or A (interval), by the whole workgroup.
+__device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs& K, bool kindB, int* s_hist,
+                               int* s_list, double* s_p, int* s_cnt, int* s_dirty) {
+  const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
+  const go1_vel_state& st = K.st;
+  const float* U = kindB ? K.UB : K.UA;
+  const double* UD = kindB ? K.UDB : K.UDA;
+  const uint64_t step = kindB ? K.stepB : K.stepA;
+  const int ucat = kindB ? GO1_VEL_U_CAT_B : GO1_VEL_U_CAT_A;
+  const int dch = kindB ? GO1_VEL_D_CHOICE_B : GO1_VEL_D_CHOICE_A;
+  const int NC = v->n_terms + GO1_VEL_SUM_EXTRA;
+  auto selected = [&](int e) {
+    return kindB ? K.maskB[e] != 0 : ((st.episode_length[e] + 1) % R == 0);
+  };
+  for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) s_hist[i] = 0;
+  if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
+  if (tid < GO1_VEL_N_CATEGORIES) s_dirty[tid] = 0;
+  __syncthreads();
+  // ---- RewardThresholdCurriculum.update per old category (:736-757, curriculum.py:135-154): success
+  // counts per (category, bin), and the list of the (category, bin) pairs that have any
+  for (int e = tid; e < n; e += CK_THREADS) {
+    if (!selected(e)) continue;
+    atomicAdd(s_cnt, 1);
+    const int cat = st.command_categories[e];
+    if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES || v->n_task == 0) continue;
+    bool ok = true;
+    for (int k = 0; k < v->n_task; ++k)
+      ok = ok && (st.command_sums[(size_t)e * NC + v->task_slot[k]] / v->curriculum_ep_len > v->task_threshold[k]);
+    const int b = st.command_bins[e];
+    if (ok && b >= 0 && b < nb) {
+      if (atomicAdd(&s_hist[cat * nb + b], 1) == 0) {
+        const int slot = atomicAdd(s_cnt + 1, 1);
+        s_list[slot] = cat * nb + b;  // at most GO1_VEL_N_CATEGORIES * nb distinct pairs
+      }
+    }
+  }
+  __syncthreads();
+  const int count = s_cnt[0], n_list = s_cnt[1];
+  if (count == 0) return;  // len(env_ids) == 0 (:730): nothing, not even the time-out rebinding
+  if (kindB && K.extras_time_outs)
+    for (int e = tid; e < n; e += CK_THREADS) K.extras_time_outs[e] = K.time_out[e];
+  // weights: cell j of category c gets +0.2 (clipped) once if it was a success bin and once per success
+  // env whose bin's neighbourhood holds it -- a sequence of identical clip(w + 0.2, 0, 1) steps, so the
+  // count decides the result whatever the order
+  if (n_list > 0) {
+    for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
+      const int cat = i / nb, j = i % nb;
+      int k = s_hist[i] > 0 ? 1 : 0;
+      for (int l = 0; l < n_list; ++l) {
+        const int cb = s_list[l];
+        if (cb / nb != cat) continue;
+        const int b = cb % nb;
+        bool adj = true;
+        for (int key = 0; key < GO1_VEL_N_KEYS; ++key) {
+          const double gb = K.grid[(size_t)key * nb + b], gj = K.grid[(size_t)key * nb + j], r = v->local_range[key];
+          adj = adj && gj >= gb - r && gj <= gb + r;
+        }
+        if (adj) k += s_hist[cb];
+      }
+      if (k > 0) {
+        double w = st.curriculum_weights[i];
+        for (int t = 0; t < k; ++t) w = fmin(fmax(w + 0.2, 0.0), 1.0);
+        st.curriculum_weights[i] = w;
+        s_dirty[cat] = 1;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- numpy rng.choice(p = w / w.sum()): cdf = cumsum(p) / cdf[-1], wave c for category c
+  {
+    const int wv = tid >> 6, ln = tid & 63;
+    if (wv < GO1_VEL_N_CATEGORIES && (s_dirty[wv] || !K.cdf_ok[wv])) {
+      const double* w = st.curriculum_weights + (size_t)wv * nb;
+      double* p = s_p + (size_t)wv * GO1_VEL_MAX_BINS;
+      double s = 0.0;
+      if (ln == 0) s = np_pairwise_sum<4>(w, nb);
+      s = __shfl(s, 0);
+      for (int j = ln; j < nb; j += 64) p[j] = w[j] / s;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if (ln == 0) {
+        double acc = 0.0;
+        for (int j = 0; j < nb; ++j) { acc += p[j]; p[j] = acc; }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double last = p[nb - 1];
+      for (int j = ln; j < nb; j += 64) K.cdf[(size_t)wv * nb + j] = p[j] / last;
+      if (ln == 0) K.cdf_ok[wv] = 1;
+    }
+  }
+  __syncthreads();
+  // ---- new category, cell and command per env (:759-842)
+  for (int e = tid; e < n; e += CK_THREADS) {
+    if (!selected(e)) continue;
+    const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
+    const RngD rngd = {UD, K.seed, step, e, e + K.env_id_offset};
+    const float uc = rng(ucat);
+    int cat = -1;
+    for (int i = 0; i < GO1_VEL_N_CATEGORIES; ++i)
+      if ((float)(0.25 * i) <= uc && uc < (float)(0.25 * (i + 1))) cat = i;
+    float cmd[GO1_VEL_NUM_COMMANDS];
+    for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) cmd[k] = st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + k];
+    if (cat >= 0) {
+      const double u0 = rngd(dch);
+      const double* cdf = K.cdf + (size_t)cat * nb;
+      int lo = 0, hi = nb;  // searchsorted(cdf, u0, side='right'): first j with cdf[j] > u0
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] <= u0) lo = mid + 1; else hi = mid;
+      }
+      const int idx = min(lo, nb - 1);
+      for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) {
+        const double cen = K.grid[(size_t)k * nb + idx], half = v->bin_sizes[k] / 2.0;
+        const double l = cen + half, h = cen - half;
+        cmd[k] = (float)(l + (h - l) * rngd(dch + 1 + k));
+      }
+      st.command_bins[e] = idx;
+      st.command_categories[e] = cat;
+      if (v->gaitwise_curricula) {
+        if (cat == CAT_PRONK) {
+          for (int k = 5; k < 8; ++k) cmd[k] = remainder1(cmd[k] / 2.0f - 0.25f);
+        } else if (cat == CAT_TROT) {
+          cmd[5] = cmd[5] / 2.0f + 0.25f; cmd[6] = 0.0f; cmd[7] = 0.0f;
+        } else if (cat == CAT_PACE) {
+          cmd[5] = 0.0f; cmd[6] = cmd[6] / 2.0f + 0.25f; cmd[7] = 0.0f;
+        } else {
+          cmd[5] = 0.0f; cmd[6] = 0.0f; cmd[7] = cmd[7] / 2.0f + 0.25f;
+        }
+      }
+    }
+    if (v->binary_phases)
+      for (int k = 5; k < 8; ++k) cmd[k] = remainder1(rintf(2.0f * cmd[k]) / 2.0f);
+    {
+      const float keep = norm2_f(cmd[0], cmd[1]) > 0.2f ? 1.0f : 0.0f;
+      cmd[0] = cmd[0] * keep;
+      cmd[1] = cmd[1] * keep;
+    }
+    for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + k] = cmd[k];
+    for (int k = 0; k < NC; ++k) st.command_sums[(size_t)e * NC + k] = 0.0f;
+    if (kindB && K.obs) {  // this step's observation of the resampled commands (:339)
+      const float clip = v->clip_obs;
+      for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) {
+        float val = cmd[k] * v->cmd_scale[k];
+        if (v->add_noise) val = val + (2.0f * rng(GO1_VEL_U_NOISE + 3 + k) - 1.0f) * v->noise_vec[3 + k];
+        val = clampf(val, -clip, clip);
+        K.obs[(size_t)e * GO1_VEL_NUM_OBS + 3 + k] = val;
+        if (K.hist_out) K.hist_out[(size_t)e * K.hist_w + K.hist_w - GO1_VEL_NUM_OBS + 3 + k] = val;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(CK_THREADS) void go1_vel_curriculum_kernel(const go1_vel_config* __restrict__ v_gen,
+                                                                        CArgs K) {
+  VCfg* __restrict__ v = (VCfg*)v_gen;
+  if (blockIdx.x > 0) {
+    // HistoryWrapper.step's shift (history_wrapper.py:22): new[:, :W - 70] = old[:, 70:], as f32 pairs
+    // (rows are 8-byte aligned: 70 x 4 B is not a multiple of 16)
+    if (!K.hist_in || !K.hist_out) return;
+    const int W = K.hist_w, W2 = (W - GO1_VEL_NUM_OBS) / 2;
+    const size_t total = (size_t)K.n_envs * W2;
+    for (size_t i = (size_t)(blockIdx.x - 1) * CK_THREADS + threadIdx.x; i < total;
+         i += (size_t)(gridDim.x - 1) * CK_THREADS) {
+      const size_t e = i / W2, k = i % W2;
+      const float2 val = *(const float2*)(K.hist_in + e * W + GO1_VEL_NUM_OBS + 2 * k);
+      *(float2*)(K.hist_out + e * W + 2 * k) = val;
+    }
+    return;
+  }
+  __shared__ int s_hist[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
+  __shared__ double s_p[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
+  __shared__ int s_list[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
+  __shared__ int s_cnt[2], s_dirty[GO1_VEL_N_CATEGORIES];
+  if (K.maskB) resample_phase(v, v_gen, K, true, s_hist, s_list, s_p, s_cnt, s_dirty);
+  if (K.doA) resample_phase(v, v_gen, K, false, s_hist, s_list, s_p, s_cnt, s_dirty);
+}
+
+// =====================================================================
+//                                C ABI
+// =====================================================================
+struct go1_vel_handle {
+  go1_config cfg;
+  go1_vel_config vcfg;
+  go1_config* d_cfg = nullptr;
+  go1_vel_config* d_vcfg = nullptr;
+  double* d_grid = nullptr;
+  double* d_cdf = nullptr;
+  int32_t* d_cdf_ok = nullptr;
+  uint8_t* d_mask = nullptr;  // reset_idx's env mask (stream-ordered reuse)
+  go1_vel_state st;
+  const float* env_origins = nullptr;
+  bool bound = false;
+};
+
+static thread_local std::string g_verr;
+static int vfail(int code, const std::string& msg) {
+  g_verr = msg;
+  return code;
+}
+#define VHIP_TRY(x)                                                                      \
+  do {                                                                                   \
+    hipError_t _e = (x);                                                                 \
+    if (_e != hipSuccess) return vfail(GO1_E_HIP, std::string(#x ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+static CArgs curriculum_args(go1_vel_handle* h) {
+  CArgs K;
+  memset(&K, 0, sizeof(K));
+  K.st = h->st;
+  K.grid = h->d_grid;
+  K.cdf = h->d_cdf;
+  K.cdf_ok = h->d_cdf_ok;
+  K.n_envs = h->cfg.n_envs;
+  K.env_id_offset = h->cfg.env_id_offset;
+  return K;
+}
+
+extern "C" {
+int go1_vel_abi_version(void) { return GO1_VEL_ABI_VERSION; }
+
+void go1_vel_abi_sizes(int64_t out[3]) {
+  out[0] = sizeof(go1_vel_config);
+  out[1] = sizeof(go1_vel_state);
+  out[2] = sizeof(go1_vel_step_args);
+}
+
+const char* go1_vel_last_error(void) { return g_verr.c_str(); }
+
+int go1_vel_create(const go1_config* cfg, const go1_vel_config* vel, const double* grid, go1_vel_handle** out) {
+  if (!cfg || !vel || !grid || !out) return vfail(GO1_E_ARG, "go1_vel_create: null argument");
+  if (cfg->n_envs <= 0 || cfg->n_envs % EPB != 0)
+    return vfail(GO1_E_ARG, "go1_vel_create: n_envs must be a positive multiple of 16");
+  if (vel->n_envs != cfg->n_envs) return vfail(GO1_E_ARG, "go1_vel_create: n_envs differs between the configs");
+  if (cfg->terrain_kind != 0) return vfail(GO1_E_ARG, "go1_vel_create: the velocity step runs on the plane");
+  if (cfg->n_internal <= 0 || GO1_LAG_STEPS(cfg->decimation) != VLAG)
+    return vfail(GO1_E_ARG, "go1_vel_create: decimation must be 4..6 (two stored lag steps)");
+  if (vel->n_terms < 0 || vel->n_terms > GO1_VEL_MAX_TERMS) return vfail(GO1_E_ARG, "go1_vel_create: n_terms");
+  for (int k = 0; k < vel->n_terms; ++k)
+    if (vel->term_ids[k] < 0 || vel->term_ids[k] >= GO1_VT_COUNT) return vfail(GO1_E_ARG, "go1_vel_create: term id");
+  if (vel->n_bins <= 0 || vel->n_bins > GO1_VEL_MAX_BINS) return vfail(GO1_E_ARG, "go1_vel_create: n_bins");
+  if (vel->resample_interval <= 0 || vel->rand_interval <= 0)
+    return vfail(GO1_E_ARG, "go1_vel_create: resample / rand interval");
+  if (vel->n_task < 0 || vel->n_task > 4) return vfail(GO1_E_ARG, "go1_vel_create: n_task");
+  if (vel->history_len < 1) return vfail(GO1_E_ARG, "go1_vel_create: history_len");
+  if (memcmp(cfg->model, GO1_MODEL_F32, sizeof(GO1_MODEL_F32)) != 0)
+    return vfail(GO1_E_ARG, "go1_vel_create: model block differs from the compiled Go1 model");
+  go1_vel_handle* h = new (std::nothrow) go1_vel_handle();
+  if (!h) return vfail(GO1_E_ARG, "go1_vel_create: out of host memory");
+  h->cfg = *cfg;
+  h->vcfg = *vel;
+  const size_t gsz = (size_t)GO1_VEL_N_KEYS * vel->n_bins * sizeof(double);
+  const size_t csz = (size_t)GO1_VEL_N_CATEGORIES * vel->n_bins * sizeof(double);
+  if (hipMalloc(&h->d_cfg, sizeof(go1_config)) != hipSuccess || hipMalloc(&h->d_vcfg, sizeof(go1_vel_config)) != hipSuccess ||
+      hipMalloc(&h->d_grid, gsz) != hipSuccess || hipMalloc(&h->d_cdf, csz) != hipSuccess ||
+      hipMalloc(&h->d_cdf_ok, GO1_VEL_N_CATEGORIES * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&h->d_mask, cfg->n_envs) != hipSuccess) {
+    go1_vel_destroy(h);
+    return vfail(GO1_E_HIP, "go1_vel_create: hipMalloc failed");
+  }
+  VHIP_TRY(hipMemcpy(h->d_cfg, cfg, sizeof(go1_config), hipMemcpyHostToDevice));
+  VHIP_TRY(hipMemcpy(h->d_vcfg, vel, sizeof(go1_vel_config), hipMemcpyHostToDevice));
+  VHIP_TRY(hipMemcpy(h->d_grid, grid, gsz, hipMemcpyHostToDevice));
+  VHIP_TRY(hipMemset(h->d_cdf_ok, 0, GO1_VEL_N_CATEGORIES * sizeof(int32_t)));
+  *out = h;
+  return GO1_OK;
+}
+
+int go1_vel_bind(go1_vel_handle* h, const go1_vel_state* s, const go1_plane* planes) {
+  if (!h || !s || !planes) return vfail(GO1_E_ARG, "go1_vel_bind: null argument");
+  const void* p[] = {s->root, s->dof_pos, s->dof_vel, s->last_actions, s->last_dof_vel, s->lag, s->pos_err_hist,
+                     s->vel_hist, s->motor_strength, s->motor_offset, s->friction, s->restitution, s->payload,
+                     s->episode_length, s->last_last_actions, s->last_joint_pos_target,
+                     s->last_last_joint_pos_target, s->commands, s->gait_indices, s->last_contacts,
+                     s->command_sums, s->episode_sums, s->command_bins, s->command_categories,
+                     s->curriculum_weights};
+  static_assert(sizeof(p) / sizeof(p[0]) == GO1_VEL_STATE_PLANES, "go1_vel_state planes");
+  static const char* names[GO1_VEL_STATE_PLANES] = {
+      "root", "dof_pos", "dof_vel", "last_actions", "last_dof_vel", "lag", "pos_err_hist", "vel_hist",
+      "motor_strength", "motor_offset", "friction", "restitution", "payload", "episode_length",
+      "last_last_actions", "last_joint_pos_target", "last_last_joint_pos_target", "commands", "gait_indices",
+      "last_contacts", "command_sums", "episode_sums", "command_bins", "command_categories", "curriculum_weights"};
+  const int64_t nt = h->vcfg.n_terms, n = h->cfg.n_envs;
+  const int64_t width[GO1_VEL_STATE_PLANES] = {13, 12, 12, 12, 12, 12 * VLAG, 24, 24, 12, 12, 1, 1, 1, 1, 12, 12, 12,
+                                               GO1_VEL_NUM_COMMANDS, 1, 4, nt + GO1_VEL_SUM_EXTRA, nt + 1, 1, 1,
+                                               h->vcfg.n_bins};
+  for (int i = 0; i < GO1_VEL_STATE_PLANES; ++i) {
+    const go1_plane& d = planes[i];
+    const int dt = (i == 13 || i == 22 || i == 23) ? GO1_DTYPE_I32 : (i == 24 ? GO1_DTYPE_F64 : GO1_DTYPE_F32);
+    const int64_t rows = i == 24 ? GO1_VEL_N_CATEGORIES : n;
+    if (!p[i]) return vfail(GO1_E_ARG, std::string("go1_vel_bind: state plane ") + names[i] + " is null");
+    if (d.rows != rows || d.cols != width[i] || d.dtype != dt)
+      return vfail(GO1_E_ARG, std::string("go1_vel_bind: state plane ") + names[i] + " must be (" +
+                                  std::to_string(rows) + ", " + std::to_string(width[i]) + ") " +
+                                  (dt == GO1_DTYPE_I32 ? "int32" : (dt == GO1_DTYPE_F64 ? "float64" : "float32")));
+    if (d.col_stride != 1 || (d.rows > 1 && d.row_stride != d.cols))
+      return vfail(GO1_E_ARG, std::string("go1_vel_bind: state plane ") + names[i] +
+                                  " is not dense row-major: pass a contiguous tensor");
+  }
+  h->st = *s;
+  h->bound = true;
+  VHIP_TRY(hipMemset(h->d_cdf_ok, 0, GO1_VEL_N_CATEGORIES * sizeof(int32_t)));  // new weights plane
+  return GO1_OK;
+}
+
+int go1_vel_set_origins(go1_vel_handle* h, const float* env_origins) {
+  if (!h || !env_origins) return vfail(GO1_E_ARG, "go1_vel_set_origins: null argument");
+  h->env_origins = env_origins;
+  return GO1_OK;
+}
+
+int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
+  if (!h || !a) return vfail(GO1_E_ARG, "go1_vel_step: null argument");
+  if (!h->bound || !h->env_origins) return vfail(GO1_E_STATE, "go1_vel_step: bind the state and set the origins first");
+  if (!a->actions || !a->obs || !a->priv || !a->rew || !a->reset || !a->time_out || !a->extras_time_outs)
+    return vfail(GO1_E_ARG, "go1_vel_step: actions and every output buffer are required");
+  const bool inj = a->inj_dof != nullptr;
+  if (inj && (!a->inj_root || !a->inj_contact || !a->inj_feet))
+    return vfail(GO1_E_ARG, "go1_vel_step: partial injected state");
+  if ((a->uniforms == nullptr) != (a->uniforms_f64 == nullptr))
+    return vfail(GO1_E_ARG, "go1_vel_step: parity mode needs both uniform arrays");
+  if (a->resample_next && a->uniforms && (!a->uniforms_next || !a->uniforms_f64_next))
+    return vfail(GO1_E_ARG, "go1_vel_step: parity mode resamples ahead with the next step's uniforms");
+  if ((a->obs_history_in == nullptr) != (a->obs_history_out == nullptr) ||
+      (a->obs_history_in && a->obs_history_in == a->obs_history_out))
+    return vfail(GO1_E_ARG, "go1_vel_step: obs_history in and out are two distinct buffers (or both NULL)");
+  if (a->episode_log_count && (!a->episode_log || a->episode_log_cap < 0))
+    return vfail(GO1_E_ARG, "go1_vel_step: a compact episode log needs episode_log and a capacity");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = h->cfg.n_envs;
+  VArgs K;
+  K.st = h->st;
+  K.a = *a;
+  K.env_origins = h->env_origins;
+  K.hist_w = GO1_VEL_NUM_OBS * h->vcfg.history_len;
+  hipEvent_t e0 = (hipEvent_t)a->ev_begin, e1 = (hipEvent_t)a->ev_end;
+  auto go = [&](auto kern) {
+    if (e0 || e1) hipExtLaunchKernelGGL(kern, dim3(n / SEPB), dim3(TPB), 0, s, e0, e1, 0, h->d_cfg, h->d_vcfg, K);
+    else hipLaunchKernelGGL(kern, dim3(n / SEPB), dim3(TPB), 0, s, h->d_cfg, h->d_vcfg, K);
+  };
+  if (inj) go(go1_vel_step_kernel<true>);
+  else go(go1_vel_step_kernel<false>);
+  VHIP_TRY(hipGetLastError());
+  CArgs C = curriculum_args(h);
+  C.seed = a->rng_seed;
+  C.maskB = a->reset;
+  C.UB = a->uniforms;
+  C.UDB = a->uniforms_f64;
+  C.stepB = a->rng_step;
+  C.doA = a->resample_next ? 1 : 0;
+  C.UA = a->uniforms_next;
+  C.UDA = a->uniforms_f64_next;
+  C.stepA = a->rng_step + 1;
+  C.time_out = a->time_out;
+  C.extras_time_outs = a->extras_time_outs;
+  C.obs = a->obs;
+  C.hist_in = a->obs_history_in;
+  C.hist_out = a->obs_history_out;
+  C.hist_w = K.hist_w;
+  const int shift_blocks = a->obs_history_in ? 1024 : 0;
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1 + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
+  VHIP_TRY(hipGetLastError());
+  return GO1_OK;
+}
+
+int go1_vel_resample(go1_vel_handle* h, const uint8_t* mask, const float* uniforms, const double* uniforms_f64,
+                     uint64_t rng_seed, uint64_t rng_step, void* stream) {
+  if (!h) return vfail(GO1_E_ARG, "go1_vel_resample: null handle");
+  if (!h->bound) return vfail(GO1_E_STATE, "go1_vel_resample: bind the state first");
+  if ((uniforms == nullptr) != (uniforms_f64 == nullptr))
+    return vfail(GO1_E_ARG, "go1_vel_resample: parity mode needs both uniform arrays");
+  CArgs C = curriculum_args(h);
+  C.seed = rng_seed;
+  if (mask) {
+    C.maskB = mask;
+    C.UB = uniforms;
+    C.UDB = uniforms_f64;
+    C.stepB = rng_step;
+  } else {
+    C.doA = 1;
+    C.UA = uniforms;
+    C.UDA = uniforms_f64;
+    C.stepA = rng_step;
+  }
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C);
+  VHIP_TRY(hipGetLastError());
+  return GO1_OK;
+}
+
+int go1_vel_reset_idx(go1_vel_handle* h, const int32_t* ids, int32_t n_ids, const float* uniforms,
+                      const double* uniforms_f64, uint64_t rng_seed, uint64_t rng_step, float* episode_log,
+                      int32_t* episode_log_count, int32_t episode_log_cap, int32_t episode_log_tag, void* stream) {
+  if (!h || (!ids && n_ids > 0) || n_ids < 0) return vfail(GO1_E_ARG, "go1_vel_reset_idx: bad argument");
+  if (!h->bound || !h->env_origins) return vfail(GO1_E_STATE, "go1_vel_reset_idx: bind the state and origins first");
+  if (n_ids == 0) return GO1_OK;  // (:178-179)
+  if (episode_log_count && !episode_log) return vfail(GO1_E_ARG, "go1_vel_reset_idx: episode_log missing");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = h->cfg.n_envs;
+  // _resample_commands first (:182): a mask of the ids for the curriculum launch
+  uint8_t* mask = h->d_mask;
+  VHIP_TRY(hipMemsetAsync(mask, 0, n, s));
+  hipLaunchKernelGGL(go1_vel_mask_kernel, dim3((n_ids + 255) / 256), dim3(256), 0, s, ids, n_ids, n, mask);
+  int rc = go1_vel_resample(h, mask, uniforms, uniforms_f64, rng_seed, rng_step, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(go1_vel_reset_kernel, dim3((n_ids + EPB - 1) / EPB), dim3(TPB), 0, s, h->d_vcfg, h->st,
+                     h->env_origins, ids, n_ids, n, uniforms, rng_seed, rng_step, h->cfg.env_id_offset, episode_log,
+                     episode_log_count, episode_log_cap, episode_log_tag);
+  VHIP_TRY(hipGetLastError());
+  return GO1_OK;
+}
+
+int go1_vel_destroy(go1_vel_handle* h) {
+  if (!h) return GO1_OK;
+  if (h->d_cfg) (void)hipFree(h->d_cfg);
+  if (h->d_vcfg) (void)hipFree(h->d_vcfg);
+  if (h->d_grid) (void)hipFree(h->d_grid);
+  if (h->d_cdf) (void)hipFree(h->d_cdf);
+  if (h->d_cdf_ok) (void)hipFree(h->d_cdf_ok);
+  if (h->d_mask) (void)hipFree(h->d_mask);
+  delete h;
+  return GO1_OK;
+}
+}  // extern "C"

@@ -766,6 +766,10 @@ class HistoryWrapper:
         # history length 1 with a distinct tensor: the step kernel writes obs_history (a copy of obs) itself
         self._tap = (self.obs_history_length == 1 and copy_history and hasattr(self.env, "_history_tap") and
                      self.env._history_tap())
+        # longer histories on an env that fuses the shift into its step (velocity.py: the step reads this
+        # wrapper's obs_history and writes cat(obs_history[:, num_obs:], obs) into a buffer of its own)
+        self._fused = (self.obs_history_length > 1 and hasattr(self.env, "attach_history") and
+                       self.env.attach_history(self.obs_history_length))
 
     def __getattr__(self, name):
         return getattr(self.env, name)
@@ -777,6 +781,11 @@ class HistoryWrapper:
             self.obs_history = torch.cat((self.obs_history[:, self.env.num_obs:], obs), dim=-1)
 
     def step(self, action):
+        if self._fused:
+            obs, rew, done, info = self.env.step(action, history_in=self.obs_history)
+            self.obs_history = self.env._last_hist
+            return {"obs": obs, "privileged_obs": info["privileged_obs"], "obs_history": self.obs_history}, rew, \
+                done, info
         obs, rew, done, info = self.env.step(action)
         privileged_obs = info["privileged_obs"]
         if self._tap:

@@ -355,12 +355,12 @@ def reward_terms(P, S, q):
             cf = q["contact"]
             t = [-(F(1) - q["desired"][:, i]) * (F(1) - np.exp(F(-1) * (ff * ff) / P.gait_force_sigma))
                  for i, ff in enumerate(norm3(cf[:, b, 0], cf[:, b, 1], cf[:, b, 2]) for b in FEET)]
-            v = (((t[0] + t[1]) + t[2]) + t[3]) / F(4)
+            v = ((((F(0) + t[0]) + t[1]) + t[2]) + t[3]) / F(4)  # reward = 0; reward += t_i (:70-75)
         elif name == "tracking_contacts_shaped_vel":
             fv = q["foot_vel"]
             t = [-(q["desired"][:, i] * (F(1) - np.exp(F(-1) * (vv * vv) / P.gait_vel_sigma)))
                  for i, vv in enumerate(norm3(fv[:, i, 0], fv[:, i, 1], fv[:, i, 2]) for i in range(4))]
-            v = (((t[0] + t[1]) + t[2]) + t[3]) / F(4)
+            v = ((((F(0) + t[0]) + t[1]) + t[2]) + t[3]) / F(4)
         elif name == "dof_pos":
             d = S["dof_pos"] - P.default
             v = sum12(d * d)

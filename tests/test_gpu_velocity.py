@@ -1,0 +1,278 @@
+"""The HIP velocity-tracking step (BASELINE configs[1]) against the oracle and the reference's fixtures.
+
+All through the C ABI (include/go1_velocity.h, legged_tracking_amd/_build/libgo1_velocity.so):
+
+* test_vel_step_replays_reference_fixture: tests/golden/vel_*.npz (the reference's VelocityTrackingEasyEnv
+  with injected physics and recorded draws, tests/golden/make_golden_vel.py) replayed step by step through
+  the kernel's parity mode (caller uniforms, injected dof / root / contact / feet).  Bit-exact: reset and
+  time-out masks, foot indices, torques, the resampled commands, bins, categories and curriculum weights,
+  the lag and every state plane the step copies.  Within 2e-6 of the oracle: the observations (the gait
+  clock is a sine), desired contact states, reward terms and sums (exp / erf), and 2e-5 of the reference.
+* test_vel_full_size_parity_with_oracle: 4096 envs (the configs[1] size) with synthetic injected physics and
+  host uniforms, episode lengths set so that time-outs, interval resamples and curriculum updates all occur.
+* test_vel_native_run_properties: the native integrator at 4096 envs for 200 steps (Philox draws): finite
+  state, commands inside the curriculum's cells, weights in [0, 1], the fused obs_history shift, extras.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from legged_tracking_amd import layout as L, vel_abi as VA, vel_layout as VL, velocity as VEL, velocity_config as V
+from oracle import vel_oracle as VO  # checker only
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = sorted(f for f in os.listdir(GOLDEN) if f.startswith("vel_") and f.endswith(".npz"))
+PLANES = ("root", "dof_pos", "dof_vel", "last_actions", "last_last_actions", "last_dof_vel", "lag", "pos_err_hist",
+          "vel_hist", "motor_strength", "motor_offset", "friction", "restitution", "payload", "episode_length",
+          "last_joint_pos_target", "last_last_joint_pos_target", "commands", "gait_indices", "last_contacts",
+          "command_sums", "episode_sums", "command_bins", "command_categories", "curriculum_weights")
+EXACT = ("episode_length", "command_bins", "command_categories", "curriculum_weights", "commands", "lag",
+         "last_contacts", "dof_pos", "dof_vel", "last_actions", "last_last_actions", "last_dof_vel", "pos_err_hist",
+         "vel_hist", "motor_strength", "motor_offset", "gait_indices", "last_joint_pos_target",
+         "last_last_joint_pos_target")
+DEV = "cuda:0"
+
+
+def make(n):
+    cfg = V.train_velocity_config(n_envs=n)
+    c, v, grid, w0, names, sum_keys = VEL.build_configs(cfg)
+    sim = VEL.VelNative(c, v, grid, w0, DEV)
+    return cfg, sim, VO.Params(cfg), names
+
+
+def load_state(sim, S):
+    for k in PLANES:
+        x = np.asarray(S[k])
+        if k == "lag":
+            x = L.lag_ring_to_stored(x.reshape(len(x), -1), 4)
+        t = sim.state[k]
+        t.copy_(torch.as_tensor(np.ascontiguousarray(x)).reshape(t.shape).to(t.dtype))
+
+
+def state_np(sim):
+    out = {k: v.cpu().numpy() for k, v in sim.state.items()}
+    out["lag"] = L.lag_stored_to_ring(out["lag"], 4)
+    return out
+
+
+def run_step(sim, P, names, n, actions, inj, u, ud, gvec, gvec_after, hist_in=None, hist_out=None):
+    """A-kind resample for this step, then go1_vel_step in parity mode (no ahead resample)."""
+    U = torch.as_tensor(u, dtype=torch.float32).to(DEV).contiguous()
+    UD = torch.as_tensor(ud, dtype=torch.float64).to(DEV).contiguous()
+    sim.resample(None, U, UD)
+    o = dict(obs=torch.zeros((n, VL.NUM_OBS), device=DEV), priv=torch.zeros((n, 2), device=DEV),
+             rew=torch.zeros(n, device=DEV), reset=torch.zeros(n, dtype=torch.bool, device=DEV),
+             time_out=torch.zeros(n, dtype=torch.bool, device=DEV),
+             terms=torch.zeros((n, VA.GO1_VEL_MAX_TERMS), device=DEV), gait=torch.zeros((n, 12), device=DEV),
+             torques=torch.zeros((4, n, 12), device=DEV), log=torch.zeros((4 * n, len(names) + 3), device=DEV),
+             log_count=torch.zeros(1, dtype=torch.int32, device=DEV))
+    it = {k: torch.as_tensor(np.ascontiguousarray(v, np.float32)).to(DEV) for k, v in inj.items()}
+    act = torch.as_tensor(np.ascontiguousarray(actions, np.float32)).to(DEV)
+    a = sim.args()
+    a.actions = act.data_ptr()
+    a.gravity_vec[:] = [float(x) for x in gvec]
+    a.gravity_vec_after[:] = [float(x) for x in gvec_after]
+    rs = np.zeros(VA.GO1_VEL_MAX_TERMS, np.float32)
+    rs[:len(names)] = [np.float32(P.scales[k]) for k in names]
+    a.reward_scales[:] = [float(x) for x in rs]
+    a.uniforms, a.uniforms_f64 = U.data_ptr(), UD.data_ptr()
+    a.resample_next = 0
+    a.inj_dof, a.inj_root, a.inj_contact, a.inj_feet = (it[k].data_ptr() for k in ("dof", "root", "contact", "feet"))
+    for k in ("obs", "priv", "rew", "reset", "time_out"):
+        setattr(a, k, o[k].data_ptr())
+    a.dbg_terms, a.dbg_gait, a.dbg_torques = o["terms"].data_ptr(), o["gait"].data_ptr(), o["torques"].data_ptr()
+    a.episode_log, a.episode_log_count, a.episode_log_cap, a.episode_log_tag = \
+        o["log"].data_ptr(), o["log_count"].data_ptr(), o["log"].shape[0], 7
+    if hist_in is not None:
+        a.obs_history_in, a.obs_history_out = hist_in.data_ptr(), hist_out.data_ptr()
+    sim.step(a)
+    torch.cuda.synchronize()
+    del U, UD, it, act
+    return {k: v.cpu().numpy() for k, v in o.items()}
+
+
+def compare(out, ref, S_gpu, S_ref, names, t, n_terms):
+    np.testing.assert_array_equal(out["reset"], ref["reset"], err_msg=f"step {t} reset")
+    np.testing.assert_array_equal(out["time_out"], ref["time_out"], err_msg=f"step {t} time_out")
+    np.testing.assert_array_equal(out["torques"][-1], ref["torques"], err_msg=f"step {t} torques")
+    np.testing.assert_array_equal(out["gait"][:, 0:4], ref["foot_indices"], err_msg=f"step {t} foot indices")
+    np.testing.assert_allclose(out["gait"][:, 4:8], ref["clock"], rtol=0, atol=2e-6, err_msg=f"step {t} clock")
+    np.testing.assert_allclose(out["gait"][:, 8:12], ref["desired"], rtol=0, atol=2e-6, err_msg=f"step {t} desired")
+    terms = np.stack([ref["terms"][k] for k in names], 1)
+    np.testing.assert_allclose(out["terms"][:, :n_terms], terms, rtol=2e-6, atol=1e-7, err_msg=f"step {t} terms")
+    np.testing.assert_allclose(out["rew"], ref["rew"], rtol=2e-6, atol=1e-9, err_msg=f"step {t} rew")
+    np.testing.assert_allclose(out["obs"], ref["obs"], rtol=0, atol=2e-6, err_msg=f"step {t} obs")
+    np.testing.assert_array_equal(out["priv"], ref["priv"])
+    for k in PLANES:
+        if k in EXACT:
+            np.testing.assert_array_equal(S_gpu[k], S_ref[k], err_msg=f"step {t} state {k}")
+        else:
+            np.testing.assert_allclose(S_gpu[k], S_ref[k], rtol=2e-6, atol=2e-6, err_msg=f"step {t} state {k}")
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_vel_step_replays_reference_fixture(name):
+    d = np.load(os.path.join(GOLDEN, name))
+    n = d["s0/obs"].shape[0]
+    cfg, sim, P, names = make(n)
+    eo = d["static/env_origins"].astype(np.float32)
+    sim.set_origins(eo)
+    hist_w = VL.NUM_OBS * cfg.env.num_observation_history
+    resets = resamples = 0
+    for t in range(int(d["meta/n_steps"])):
+        S = {k: np.array(d[f"s{t}/pre/{k}"]) for k in PLANES}
+        S["episode_length"] = S["episode_length"].astype(np.int32)
+        load_state(sim, S)
+        inj = dict(dof=d[f"s{t}/inj_dof"], root=d[f"s{t}/inj_root"], contact=d[f"s{t}/inj_contact"],
+                   feet=d[f"s{t}/inj_feet"])
+        u = np.nan_to_num(d[f"s{t}/uniforms"], nan=0.5).astype(np.float32)
+        ud = np.nan_to_num(d[f"s{t}/uniforms_f64"], nan=0.5)
+        hin = torch.randn((n, hist_w), device=DEV)
+        hout = torch.full((n, hist_w), float("nan"), device=DEV)
+        out = run_step(sim, P, names, n, d[f"s{t}/actions"], inj, u, ud, d[f"s{t}/gravity_vec"],
+                       d[f"s{t}/gravity_vec_after"], hin, hout)
+        S_ref = {k: v.copy() for k, v in S.items()}
+        S_ref["joint_pos_target"] = np.zeros((n, 12), np.float32)
+        ref = VO.step(P, S_ref, d[f"s{t}/actions"], inj, u, ud, d[f"s{t}/gravity_vec"], d[f"s{t}/gravity_vec_after"],
+                      eo)
+        compare(out, ref, state_np(sim), S_ref, names, t, len(names))
+        # against the reference itself
+        np.testing.assert_array_equal(out["reset"], d[f"s{t}/reset"])
+        np.testing.assert_array_equal(state_np(sim)["commands"], d[f"s{t}/post/commands"])
+        np.testing.assert_array_equal(state_np(sim)["curriculum_weights"], d[f"s{t}/post/curriculum_weights"])
+        np.testing.assert_allclose(out["obs"], d[f"s{t}/obs"], rtol=2e-5, atol=2e-5)
+        np.testing.assert_allclose(out["rew"], d[f"s{t}/rew"], rtol=1e-4, atol=1e-12)
+        # HistoryWrapper.step: cat(obs_history[:, 70:], obs)
+        h = hout.cpu().numpy()
+        np.testing.assert_array_equal(h[:, :hist_w - VL.NUM_OBS], hin.cpu().numpy()[:, VL.NUM_OBS:])
+        np.testing.assert_array_equal(h[:, hist_w - VL.NUM_OBS:], out["obs"])
+        # episode log rows (extras["train/episode"] means, :199-205)
+        cnt = int(out["log_count"][0])
+        assert cnt == int(d[f"s{t}/reset"].sum())
+        if cnt:
+            rows = out["log"][:cnt]
+            ne = len(names) + 1
+            assert (rows[:, ne] == 7).all()
+            rows = rows[np.argsort(rows[:, ne + 1])]
+            np.testing.assert_array_equal(rows[:, ne + 1], np.nonzero(d[f"s{t}/reset"])[0])
+            for i, k in enumerate(names + ["total"]):
+                np.testing.assert_allclose(np.float32(rows[:, i].mean(dtype=np.float32)), d[f"s{t}/episode/rew_{k}"],
+                                           rtol=1e-4, atol=1e-7)
+        resets += int(d[f"s{t}/reset"].sum())
+        resamples += len(d[f"s{t}/resample_A"])
+    assert resets > 0
+    sim.close()
+
+
+def synthetic_physics(rng, S, n):
+    """A random walk around the current state: (dof per sim step, root, contact, feet)."""
+    q = S["dof_pos"] + rng.normal(0, 0.05, (4, n, 12)).cumsum(0).astype(np.float32)
+    qd = rng.normal(0, 2.0, (4, n, 12)).astype(np.float32)
+    dof = np.stack([q, qd], -1).astype(np.float32)
+    root = S["root"].copy()
+    root[:, :3] += rng.normal(0, 0.02, (n, 3)).astype(np.float32)
+    root[:, 2] = np.clip(root[:, 2], 0.1, 0.5)
+    qu = root[:, 3:7] + rng.normal(0, 0.05, (n, 4)).astype(np.float32)
+    root[:, 3:7] = qu / np.linalg.norm(qu, axis=1, keepdims=True)
+    root[:, 7:13] = rng.normal(0, 0.5, (n, 6)).astype(np.float32)
+    contact = (rng.normal(0, 1, (n, 17, 3)) * (rng.random((n, 17, 1)) < 0.3) * 20).astype(np.float32)
+    contact[:, 0] *= rng.random((n, 1)) < 0.05  # a few base contacts terminate
+    feet = np.concatenate([root[:, None, :3] + rng.normal(0, 0.2, (n, 4, 3)), rng.normal(0, 0.5, (n, 4, 3))],
+                          -1).astype(np.float32)
+    feet[:, :, 2] = np.abs(feet[:, :, 2]) * 0.2
+    return dict(dof=dof, root=root, contact=contact, feet=feet)
+
+
+def test_vel_full_size_parity_with_oracle():
+    n = 4096
+    cfg, sim, P, names = make(n)
+    eo = VEL.plane_env_origins(n, cfg)
+    sim.set_origins(eo)
+    rng = np.random.default_rng(3)
+    # a state mid-training: episode lengths spread so that steps see time-outs (> 1000), interval
+    # resamples (ep + 1 == 500) and the curricula's updates (large task command sums)
+    S = {k: v.cpu().numpy().copy() for k, v in sim.state.items()}
+    S["lag"] = L.lag_stored_to_ring(S["lag"], 4)
+    S["root"][:, :3] = eo + np.float32([0, 0, 0.3])
+    S["root"][:, 6] = 1.0
+    S["dof_pos"][:] = P.default
+    S["episode_length"][:, 0] = rng.choice([0, 10, 498, 499, 999, 1000], n).astype(np.int32)
+    S["command_categories"][:, 0] = rng.integers(0, 4, n)
+    S["command_bins"][:, 0] = rng.choice(np.nonzero(P.w0)[0], n)
+    nt = len(names)
+    S["command_sums"][:, :nt] = (rng.random((n, nt)) * 2000 * np.float32([P.scales[k] for k in names])).astype(
+        np.float32)
+    S["commands"][:, :] = rng.uniform(-1, 1, (n, 15)).astype(np.float32)
+    S["commands"][:, 4] = 3.0
+    S["commands"][:, 8] = 0.5
+    S["last_actions"][:] = rng.normal(0, 1, (n, 12)).astype(np.float32)
+    S["motor_strength"][:] = 1.0
+    S["friction"][:] = rng.uniform(0.1, 3.0, (n, 1)).astype(np.float32)
+    n_changed = 0
+    for t in range(3):
+        load_state(sim, S)
+        inj = synthetic_physics(rng, S, n)
+        u = rng.random((n, VL.VU_PER_ENV)).astype(np.float32)
+        ud = rng.random((n, VL.VD_PER_ENV))
+        act = rng.normal(0, 1, (n, 12)).astype(np.float32)
+        g = np.float32([0, 0, -1])
+        out = run_step(sim, P, names, n, act, inj, u, ud, g, g)
+        S_ref = {k: v.copy() for k, v in S.items()}
+        S_ref["joint_pos_target"] = np.zeros((n, 12), np.float32)
+        w_before = S_ref["curriculum_weights"].copy()
+        ref = VO.step(P, S_ref, act, inj, u, ud, g, g, eo)
+        S_gpu = state_np(sim)
+        compare(out, ref, S_gpu, S_ref, names, t, nt)
+        n_changed += int((S_ref["curriculum_weights"] != w_before).sum())
+        assert out["reset"].any() and len(ref["resample_a"]) > 0
+        S = S_gpu
+        S["episode_length"][:, 0] = np.where(rng.random(n) < 0.2, 499, S["episode_length"][:, 0]).astype(np.int32)
+    assert n_changed > 0  # the curricula were updated
+    sim.close()
+
+
+def test_vel_native_run_properties():
+    from legged_tracking_amd.env import HistoryWrapper
+    n = 4096
+    env = HistoryWrapper(VEL.VelocityTrackingEasyEnv(sim_device=DEV, num_envs=n))
+    assert env._fused
+    obs = env.reset()
+    assert obs["obs_history"].shape == (n, 2100)
+    d = env.get_observations()
+    prev_hist = d["obs_history"].clone()
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    n_reset = 0
+    grid = env.env.curriculum_grid
+    for t in range(200):
+        act = torch.randn((n, 12), device=DEV, generator=gen)
+        o, rew, done, info = env.step(act)
+        h = o["obs_history"]
+        if t < 3:
+            torch.testing.assert_close(h[:, :-70], prev_hist[:, 70:], rtol=0, atol=0)
+            torch.testing.assert_close(h[:, -70:], o["obs"], rtol=0, atol=0)
+        prev_hist = h.clone()
+        n_reset += int(done.sum())
+    torch.cuda.synchronize()
+    st = {k: v.cpu().numpy() for k, v in env.env.state.items()}
+    for k in ("root", "dof_pos", "dof_vel", "commands", "command_sums", "episode_sums"):
+        assert np.isfinite(st[k]).all(), k
+    assert np.isfinite(o["obs"].cpu().numpy()).all() and np.abs(o["obs"].cpu().numpy()).max() <= 100
+    w = st["curriculum_weights"]
+    assert (w >= 0).all() and (w <= 1).all()
+    b = st["command_bins"][:, 0]
+    assert ((b >= 0) & (b < grid.shape[1])).all()
+    # resampled x velocity / yaw commands lie in their bin's cell (or were zeroed as small commands)
+    cmd = st["commands"]
+    cen = grid[:, b]
+    _, bs, _ = V.curriculum_grid(env.env.cfg)
+    for k in (2,):
+        assert (np.abs(cmd[:, k] - cen[k]) <= bs[k] / 2 + 1e-6).all()
+    assert set(np.unique(cmd[:, 5])) <= {0.0, 0.5} and set(np.unique(cmd[:, 8])) <= {0.5}
+    assert n_reset > 0
+    ep = info["train/episode"]
+    assert "rew_total" in ep and "command_area_trot" in ep
+    assert info["time_outs"].shape == (n,)
+    env.env.close()
