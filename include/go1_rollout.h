@@ -64,14 +64,16 @@ typedef struct go1_policy_layer {
      lo = f16(w - hi); record (t, g, lane = 16 q + m) = hi, then lo, of W[16 t + m][16 g + 4 q + r],
      r = 0..3 (16 bytes: the lane's A fragments of v_mfma_f32_16x16x16_f16 for both halves) */
   const void* w;
-  const float* b; /* [n padded to 16] */
+  const float* b;  /* [n padded to 16] */
+  const float* wf; /* (n, k) row-major f32, the unsplit weights: the f32 fallback of a workgroup whose
+                      activations leave the f16 split's range (|x| >= 65504) */
 } go1_policy_layer;
 typedef struct go1_policy_args {
   const float* obs_history;    /* (n, hist_dim) */
-  const float* privileged_obs; /* (n, 2) */
+  const float* privileged_obs; /* (n, num_priv) */
   float* action_mean;          /* (n, num_actions) */
   float* value;                /* (n) */
-  float* latent;               /* (n, 2) or NULL */
+  float* latent;               /* (n, num_priv) or NULL: the adaptation module's output */
   /* optional in-kernel Normal(mean, std).sample() + log_prob (NULL actions = skip) */
   const float* std;            /* (num_actions) */
   float* actions;              /* (n, num_actions) */
@@ -80,15 +82,15 @@ typedef struct go1_policy_args {
   uint64_t rng_seed, rng_step; /* Philox key / counter, one counter value per call */
   int32_t env_id_offset;       /* global id of row 0 (rank * n) */
   int32_t n_envs, hist_dim, num_actions;
+  int32_t num_priv;            /* privileged obs = latent width, 1 .. 8, hist_dim + num_priv <= 272 */
+  int32_t variant;             /* 0: per-net workgroups of 32 envs (default), 1: one workgroup of 16 envs
+                                  running all three nets; identical outputs (tests/test_rollout.py) */
+  int32_t* overflow;           /* optional: += workgroups that recomputed in f32 (the range guard) */
   go1_policy_layer layers[GO1_POLICY_LAYERS];
 } go1_policy_args;
 
 const char* go1_rollout_last_error(void);
 int go1_policy_forward(const go1_policy_args* args, void* stream);
-/* Which policy kernel go1_policy_forward launches: 1 = per-net workgroups of 32 envs (default),
- * 0 = one workgroup of 16 envs running all three nets.  Identical outputs (tests/test_rollout.py);
- * returns the previous setting. */
-int go1_policy_set_split(int split);
 int go1_record_transition(const go1_transition* tr, int32_t n_envs, float gamma, void* stream);
 /* rewards/values/returns/advantages: (T, n) f32; dones (T, n) u8; last_values (n);
  * stats: 2 f64 (sum, sum of squares of the raw advantages), overwritten. */

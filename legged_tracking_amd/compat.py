@@ -12,6 +12,12 @@ resolve to this package:
   go1_gym.envs.wrappers.history_wrapper.HistoryWrapper -> env.HistoryWrapper
   go1_gym_learn.ppo_cse{,.actor_critic,.ppo}          -> rollout (Runner, RunnerArgs, AC_Args, PPO_Args)
   wandb                                               -> no-op stand-in when wandb is not installed
+and, for scripts/train_velocity_tracking.py (BASELINE configs[1]):
+  go1_gym.envs.base.legged_robot_velocity_tracking_config.Cfg -> velocity_config.make_vel_cfg()
+  go1_gym.envs.go1.go1_config.config_go1              -> velocity_config.config_go1_vel
+  go1_gym.envs.go1.velocity_tracking.VelocityTrackingEasyEnv -> velocity.VelocityTrackingEasyEnv
+    (on the plane: configs[1] runs the velocity task on a plane, the script's own trimesh terrain is not on
+    the accelerated path; GO1_VEL_MESH=trimesh keeps the script's value and raises)
 
 Usage:
   python -m legged_tracking_amd.compat /path/to/legged_tracking/scripts/train.py --headless --old_ppo \\
@@ -54,7 +60,20 @@ def install(root_dir=None):
                 num_learning_iterations = min(num_learning_iterations, int(cap))
             return super().learn(num_learning_iterations, *a, **k)
 
+    from . import velocity as VEL, velocity_config as VC
+
+    class VelocityTrackingEasyEnv(VEL.VelocityTrackingEasyEnv):
+        def __init__(self, sim_device, headless, num_envs=None, prone=False, deploy=False, cfg=None,
+                     eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX"):
+            if os.environ.get("GO1_NUM_ENVS"):
+                num_envs = int(os.environ["GO1_NUM_ENVS"])
+            if cfg is not None and os.environ.get("GO1_VEL_MESH", "plane") == "plane":
+                cfg.terrain.mesh_type = "plane"
+            super().__init__(sim_device, headless, num_envs, prone, deploy, cfg, eval_cfg, initial_dynamics_dict,
+                             physics_engine)
+
     Cfg = CF.make_cfg()
+    VCfg = VC.make_vel_cfg()
     _module("isaacgym", gymapi=None, gymtorch=None, gymutil=None)
     _module("params_proto", PrefixProto=CF.PrefixProto, ParamsProto=CF.ParamsProto, Meta=type(CF.PrefixProto))
     root = root_dir or os.environ.get("GO1_GYM_ROOT", os.getcwd())
@@ -67,6 +86,9 @@ def install(root_dir=None):
     _module("go1_gym.envs.go1.go1_crawling", config_go1=CF.config_go1)
     _module("go1_gym.envs.go1.trajectory_tracking", TrajectoryTrackingEnv=TrajectoryTrackingEnv,
             LeggedRobot=E.LeggedRobot, Cfg=Cfg)
+    _module("go1_gym.envs.base.legged_robot_velocity_tracking_config", Cfg=VCfg)
+    _module("go1_gym.envs.go1.go1_config", config_go1=VC.config_go1_vel)
+    _module("go1_gym.envs.go1.velocity_tracking", VelocityTrackingEasyEnv=VelocityTrackingEasyEnv, Cfg=VCfg)
     _module("go1_gym.envs.wrappers")
     _module("go1_gym.envs.wrappers.history_wrapper", HistoryWrapper=E.HistoryWrapper)
     _module("go1_gym_learn")

@@ -192,18 +192,26 @@ struct Act {
 
 __device__ __forceinline__ float elu(float x) { return x > 0.0f ? x : expm1f(x); }
 
+// Range guard of the split: f16(x) overflows for |x| >= 65520 (and a NaN / inf input has no split), so a
+// value outside (-65504, 65504) sets the workgroup's flag; the workgroup then recomputes its envs in
+// f32 from the unsplit weights at its end (policy_fallback).  One compare per stored value.
+__device__ __forceinline__ void ovf_check(float v, int* ovf) {
+  if (!(fabsf(v) < 65504.0f)) *ovf = 1;
+}
 // four consecutive features 4 kq .. 4 kq + 3 of env c, split into the two planes
-__device__ __forceinline__ void act_store4(ActV d, int kq, int c, f4_t v) {
+__device__ __forceinline__ void act_store4(ActV d, int kq, int c, f4_t v, int* ovf) {
   h4_t h, l;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
+    ovf_check(v[r], ovf);
     h[r] = (_Float16)v[r];
     l[r] = (_Float16)(v[r] - (float)h[r]);
   }
   d.hi[kq * 16 + c] = h;
   d.lo[kq * 16 + c] = l;
 }
-__device__ __forceinline__ void act_store1(ActV d, int k, int c, float v) {
+__device__ __forceinline__ void act_store1(ActV d, int k, int c, float v, int* ovf) {
+  ovf_check(v, ovf);
   const _Float16 h = (_Float16)v;
   reinterpret_cast<_Float16*>(d.hi)[((k >> 2) * 16 + c) * 4 + (k & 3)] = h;
   reinterpret_cast<_Float16*>(d.lo)[((k >> 2) * 16 + c) * 4 + (k & 3)] = (_Float16)(v - (float)h);
@@ -261,7 +269,8 @@ __device__ __forceinline__ void policy_prefetch(const PolicyLayer* L, int tile0,
 
 template <int NT, int NL, int G, int D, bool PREFETCHED = false>
 __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, const ActV* src, int tile0, int tstride,
-                                             const ActV* dst, bool act, int lane, f4_t (*pre)[NL][NT] = nullptr) {
+                                             const ActV* dst, bool act, int lane, int* ovf,
+                                             f4_t (*pre)[NL][NT] = nullptr) {
   const int q = lane >> 4, c = lane & 15;
   f4_t acc[NL][NT], w[D][NL][NT];
 #pragma unroll
@@ -293,7 +302,7 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, const ActV* s
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = elu(v[r]);
       }
-      act_store4(dst[l], 4 * (tile0 + i * tstride) + q, c, v);
+      act_store4(dst[l], 4 * (tile0 + i * tstride) + q, c, v, ovf);
     }
 }
 
@@ -311,6 +320,76 @@ __device__ __forceinline__ f4_t tile_partial(const PolicyLayer& L, int Gs, int t
   for (int i = 0; i < NG; ++i)
     acc = mfma3(w[i], src.hi[(4 * (g0 + i) + q) * 16 + c], src.lo[(4 * (g0 + i) + q) * 16 + c], acc);
   return acc;
+}
+
+// ---------------------------------------------------------------- range guard: f32 fallback
+// y = act(W x + b) for one env, W (n_out, k_in) row-major f32, by the workgroup (output o on thread o)
+__device__ void dense_f32(const float* __restrict__ W, const float* __restrict__ b, int n_out, int k_in,
+                          const float* x, float* y, bool act) {
+  for (int o = threadIdx.x; o < n_out; o += blockDim.x) {
+    float acc = b[o];
+    const float* w = W + (size_t)o * k_in;
+    for (int k = 0; k < k_in; ++k) acc = fmaf(w[k], x[k], acc);
+    y[o] = act ? elu(acc) : acc;
+  }
+  __syncthreads();
+}
+
+// The envs [e0, e0 + ne) of a workgroup whose split activations left the f16 range, recomputed in f32
+// from the unsplit weights (layers[].wf): the adaptation module + actor (+ the Normal sample with the
+// same Philox draws) and / or the critic.  `buf`: >= 272 + 512 + 256 floats of LDS no longer in use.
+__device__ void policy_fallback(const go1_policy_args& P, int e0, int ne, bool actor, bool critic, float* buf) {
+  const go1_policy_layer* L = P.layers;
+  const int H = P.hist_dim, NP = P.num_priv, NA = P.num_actions;
+  float* x = buf;
+  float* ya = buf + PIN;
+  float* yb = ya + 512;
+  for (int e = 0; e < ne; ++e) {
+    const size_t ge = (size_t)(e0 + e);
+    for (int k = threadIdx.x; k < H; k += blockDim.x) x[k] = P.obs_history[ge * H + k];
+    __syncthreads();
+    if (actor) {
+      dense_f32(L[0].wf, L[0].b, 256, H, x, ya, true);
+      dense_f32(L[1].wf, L[1].b, 128, 256, ya, yb, true);
+      dense_f32(L[2].wf, L[2].b, NP, 128, yb, x + H, false);  // the latent, appended to the actor's input
+      if (P.latent && (int)threadIdx.x < NP) P.latent[ge * NP + threadIdx.x] = x[H + threadIdx.x];
+      dense_f32(L[3].wf, L[3].b, 512, H + NP, x, ya, true);
+      dense_f32(L[4].wf, L[4].b, 256, 512, ya, yb, true);
+      dense_f32(L[5].wf, L[5].b, 128, 256, yb, ya, true);
+      dense_f32(L[6].wf, L[6].b, NA, 128, ya, yb, false);
+      if (threadIdx.x == 0) {
+        float lp_q[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int f = 0; f < NA; ++f) {
+          P.action_mean[ge * NA + f] = yb[f];
+          if (P.actions) {
+            const float sd = P.std[f];
+            uint32_t ctr[4] = {(uint32_t)(ge + P.env_id_offset), (uint32_t)f, (uint32_t)P.rng_step,
+                               (uint32_t)(P.rng_step >> 32)};
+            philox4x32(ctr, (uint32_t)P.rng_seed, (uint32_t)(P.rng_seed >> 32));
+            const float u1 = ((float)(ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+            const float u2 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);
+            const float z = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+            P.actions[ge * NA + f] = yb[f] + sd * z;
+            P.action_sigma[ge * NA + f] = sd;
+            lp_q[f >> 2] += -0.5f * z * z - logf(sd) - 0.91893853320467274f;
+          }
+        }
+        if (P.actions) P.log_prob[ge] = (lp_q[0] + lp_q[1]) + (lp_q[2] + lp_q[3]);
+      }
+      __syncthreads();
+    }
+    if (critic) {
+      for (int k = threadIdx.x; k < NP; k += blockDim.x) x[H + k] = P.privileged_obs[ge * NP + k];
+      __syncthreads();
+      dense_f32(L[7].wf, L[7].b, 512, H + NP, x, ya, true);
+      dense_f32(L[8].wf, L[8].b, 256, 512, ya, yb, true);
+      dense_f32(L[9].wf, L[9].b, 128, 256, yb, ya, true);
+      dense_f32(L[10].wf, L[10].b, 1, 128, ya, yb, false);
+      if (threadIdx.x == 0) P.value[ge] = yb[0];
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0 && P.overflow) atomicAdd(P.overflow, 1);
 }
 
 #ifdef GO1_POLICY_STAMPS  // diagnostic build only (tools/policy_stamps.py): s_memtime per wave per phase
@@ -334,7 +413,10 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   const int e0 = blockIdx.x * 16;
   PSTAMP(0);
   const int ne = min(16, P.n_envs - e0);
+  const int NP = P.num_priv;
   const ActV va = xa.v(), vc = xc.v();
+  __shared__ int s_ovf;
+  if (tid == 0) s_ovf = 0;
 #ifndef GO1_POLICY_NO_EARLY
   // the adaptation module's first weight groups are in flight while the inputs are staged
   f4_t w_ad[8][1][1];
@@ -344,10 +426,10 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     const int e = idx / PIN, k = idx - e * PIN;
     float v = 0.0f;
     if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
-    act_store1(va, k, e, v);
+    act_store1(va, k, e, v, &s_ovf);
     act_store1(vc, k, e,
-               (e < ne && k >= P.hist_dim && k < P.hist_dim + 2) ? P.privileged_obs[(size_t)(e0 + e) * 2 + (k - P.hist_dim)]
-                                                                 : v);
+               (e < ne && k >= P.hist_dim && k < P.hist_dim + NP)
+                   ? P.privileged_obs[(size_t)(e0 + e) * NP + (k - P.hist_dim)] : v, &s_ovf);
   }
   __syncthreads();
   PSTAMP(1);
@@ -355,9 +437,9 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   const ActV vh1[2] = {h1[0].v(), h1[1].v()}, vh2[2] = {h2[0].v(), h2[1].v()};
   // adaptation module (xa rows >= hist_dim are still zero)
 #ifndef GO1_POLICY_NO_EARLY
-  policy_tiles<1, 1, PIN / 16, 8, true>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, w_ad);  // 256
+  policy_tiles<1, 1, PIN / 16, 8, true>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, &s_ovf, w_ad);  // 256
 #else
-  policy_tiles<1, 1, PIN / 16, 8>(Ls + 0, &va, wave, PW, &vh1[0], true, lane);  // 256
+  policy_tiles<1, 1, PIN / 16, 8>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, &s_ovf);  // 256
 #endif
   __syncthreads();
   PSTAMP(2);
@@ -377,12 +459,12 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
       f4_t v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = elu((b[r] + acc[r]) + scr[t][4 * q + r][c]);
-      act_store4(vh2[0], 4 * t + q, c, v);
+      act_store4(vh2[0], 4 * t + q, c, v, &s_ovf);
     }
   }
   __syncthreads();
   PSTAMP(3);
-  // 128 -> 2 (the latent): one K group per wave (8 waves), partials summed by wave 0
+  // 128 -> num_priv (the latent): one K group per wave (8 waves), partials summed by wave 0
   {
     float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1]);
     const int q = lane >> 4, c = lane & 15;
@@ -392,16 +474,17 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
       for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = acc[r];
     }
     __syncthreads();
-    if (wave == 0 && q == 0) {
-      float l0 = Ls[2].b[0], l1 = Ls[2].b[1];
+    if (wave == 0 && q < 2) {
 #pragma unroll
-      for (int w = 0; w < 8; ++w) { l0 += scr[w][0][c]; l1 += scr[w][1][c]; }
-      // features 0, 1: the latent, also the actor's inputs hist_dim, hist_dim + 1
-      act_store1(va, P.hist_dim, c, l0);
-      act_store1(va, P.hist_dim + 1, c, l1);
-      if (c < ne && P.latent) {
-        P.latent[(size_t)(e0 + c) * 2] = l0;
-        P.latent[(size_t)(e0 + c) * 2 + 1] = l1;
+      for (int r = 0; r < 4; ++r) {
+        const int f = 4 * q + r;  // latent feature f: also the actor's input hist_dim + f
+        if (f < NP) {
+          float l = Ls[2].b[f];
+#pragma unroll
+          for (int w = 0; w < 8; ++w) l += scr[w][f][c];
+          act_store1(va, P.hist_dim + f, c, l, &s_ovf);
+          if (c < ne && P.latent) P.latent[(size_t)(e0 + c) * NP + f] = l;
+        }
       }
     }
   }
@@ -411,18 +494,18 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   const PolicyLayer LA1[2] = {Ls[3], Ls[7]}, LA2[2] = {Ls[4], Ls[8]};
   {
     const ActV s1[2] = {va, vc};
-    policy_tiles<2, 2, PIN / 16, 3>(LA1, s1, wave, PW, vh1, true, lane);  // 512
+    policy_tiles<2, 2, PIN / 16, 3>(LA1, s1, wave, PW, vh1, true, lane, &s_ovf);  // 512
   }
   __syncthreads();
   PSTAMP(5);
-  policy_tiles<1, 2, 512 / 16, 6>(LA2, vh1, wave, PW, vh2, true, lane);  // 256
+  policy_tiles<1, 2, 512 / 16, 6>(LA2, vh1, wave, PW, vh2, true, lane, &s_ovf);  // 256
   __syncthreads();
   PSTAMP(6);
   {  // 256 -> 128, one tile per wave: waves 0-7 the actor's, 8-15 the critic's
     const bool critic = wave >= 8;
     const PolicyLayer L3 = critic ? Ls[9] : Ls[5];
     const ActV src = critic ? h2[1].v() : h2[0].v(), dst = critic ? h1[1].v() : h1[0].v();
-    policy_tiles<1, 1, 256 / 16, 8>(&L3, &src, wave & 7, 8, &dst, true, lane);
+    policy_tiles<1, 1, 256 / 16, 8>(&L3, &src, wave & 7, 8, &dst, true, lane, &s_ovf);
   }
   __syncthreads();
   PSTAMP(7);
@@ -496,6 +579,8 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     }
   }
   PSTAMP(8);
+  __syncthreads();
+  if (s_ovf) policy_fallback(P, e0, ne, true, true, reinterpret_cast<float*>(&h1[0]));
 }
 
 // ---------------------------------------------------------------- per-net workgroups
@@ -505,9 +590,6 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
 // workgroups run the adaptation module + actor (1.6 MB), the others the critic (1.2 MB), so a CU
 // streams at most 1.6 MB for twice the envs.  K order, tile split and partial-sum order are those
 // of policy_kernel, so the outputs are identical.
-#ifndef GO1_POLICY_SPLIT
-#define GO1_POLICY_SPLIT 1
-#endif
 constexpr int SE = 32;  // envs per workgroup of policy_kernel_split
 // weight groups in flight per wave, the 512-wide first layers and the 256-wide second: (4, 8), (6, 12),
 // (8, 12), (8, 16) all within 1 % of each other on the rollout loop (2 runs each), so not the limit
@@ -533,7 +615,7 @@ __device__ __forceinline__ void policy_group_e(const f4_t (&w)[NL][NT], const Ac
 
 template <int NT, int NL, int ET, int G, int D>
 __device__ __forceinline__ void policy_tiles_e(const PolicyLayer* L, const ActV (*src)[NL], int tile0, int tstride,
-                                               const ActV (*dst)[NL], bool act, int lane) {
+                                               const ActV (*dst)[NL], bool act, int lane, int* ovf) {
   const int q = lane >> 4, c = lane & 15;
   f4_t acc[ET][NL][NT], w[D][NL][NT];
 #pragma unroll
@@ -561,7 +643,7 @@ __device__ __forceinline__ void policy_tiles_e(const PolicyLayer* L, const ActV 
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = elu(v[r]);
         }
-        act_store4(dst[et][l], 4 * (tile0 + i * tstride) + q, c, v);
+        act_store4(dst[et][l], 4 * (tile0 + i * tstride) + q, c, v, ovf);
       }
 }
 
@@ -593,21 +675,24 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
   const bool critic = (int)blockIdx.x >= nblk;
   const int e0 = (critic ? (int)blockIdx.x - nblk : (int)blockIdx.x) * SE;
   const int ne = min(SE, P.n_envs - e0);
+  const int NP = P.num_priv;
   const ActV vx[2][1] = {{xin[0].v()}, {xin[1].v()}}, v1[2][1] = {{h1[0].v()}, {h1[1].v()}},
              v2[2][1] = {{h2[0].v()}, {h2[1].v()}};
+  __shared__ int s_ovf;
+  if (tid == 0) s_ovf = 0;
   for (int idx = tid; idx < SE * PIN; idx += 64 * PW) {
     const int e = idx / PIN, k = idx - e * PIN;
     float v = 0.0f;
     if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
-    if (critic && e < ne && k >= P.hist_dim && k < P.hist_dim + 2)
-      v = P.privileged_obs[(size_t)(e0 + e) * 2 + (k - P.hist_dim)];
-    act_store1(e < 16 ? vx[0][0] : vx[1][0], k, e & 15, v);  // no runtime index into vx (private memory)
+    if (critic && e < ne && k >= P.hist_dim && k < P.hist_dim + NP)
+      v = P.privileged_obs[(size_t)(e0 + e) * NP + (k - P.hist_dim)];
+    act_store1(e < 16 ? vx[0][0] : vx[1][0], k, e & 15, v, &s_ovf);  // no runtime index into vx (private memory)
   }
   __syncthreads();
   const PolicyLayer* Ls = P.layers;
   if (!critic) {
     // adaptation module 261 -> 256 (xin rows >= hist_dim are still zero)
-    policy_tiles_e<1, 1, 2, PIN / 16, 8>(Ls + 0, vx, wave, PW, v1, true, lane);
+    policy_tiles_e<1, 1, 2, PIN / 16, 8>(Ls + 0, vx, wave, PW, v1, true, lane, &s_ovf);
     __syncthreads();
     {  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7
       const int t = wave & 7, half = wave >> 3;
@@ -628,12 +713,12 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
           f4_t v;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = elu((b[r] + acc[et][r]) + scr[et][t][4 * q + r][c]);
-          act_store4(v2[et][0], 4 * t + q, c, v);
+          act_store4(v2[et][0], 4 * t + q, c, v, &s_ovf);
         }
       }
     }
     __syncthreads();
-    {  // 128 -> 2 (the latent): one K group per wave (8 waves), partials summed by waves 0 / 1
+    {  // 128 -> num_priv (the latent): one K group per wave (8 waves), partials summed by waves 0 / 1
       if (wave < 8) {
         const ActV src[2] = {v2[0][0], v2[1][0]};
         f4_t acc[2];
@@ -644,17 +729,19 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
           for (int r = 0; r < 4; ++r) scr[et][wave][4 * q + r][c] = acc[et][r];
       }
       __syncthreads();
-      if (wave < 2 && q == 0) {
+      if (wave < 2 && q < 2) {
         const int et = wave, e = 16 * et + c;
-        float l0 = Ls[2].b[0], l1 = Ls[2].b[1];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) { l0 += scr[et][w][0][c]; l1 += scr[et][w][1][c]; }
         const ActV d = et ? vx[1][0] : vx[0][0];
-        act_store1(d, P.hist_dim, c, l0);
-        act_store1(d, P.hist_dim + 1, c, l1);
-        if (e < ne && P.latent) {
-          P.latent[(size_t)(e0 + e) * 2] = l0;
-          P.latent[(size_t)(e0 + e) * 2 + 1] = l1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * q + r;
+          if (f < NP) {
+            float l = Ls[2].b[f];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) l += scr[et][w][f][c];
+            act_store1(d, P.hist_dim + f, c, l, &s_ovf);
+            if (e < ne && P.latent) P.latent[(size_t)(e0 + e) * NP + f] = l;
+          }
         }
       }
     }
@@ -662,11 +749,11 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
   }
   // actor (Ls 3-6) or critic (Ls 7-10), layer by layer
   const PolicyLayer* LN = Ls + (critic ? 7 : 3);
-  policy_tiles_e<2, 1, 2, PIN / 16, GO1_SPLIT_D1>(LN + 0, vx, wave, PW, v1, true, lane);  // 512
+  policy_tiles_e<2, 1, 2, PIN / 16, GO1_SPLIT_D1>(LN + 0, vx, wave, PW, v1, true, lane, &s_ovf);  // 512
   __syncthreads();
-  policy_tiles_e<1, 1, 2, 512 / 16, GO1_SPLIT_D2>(LN + 1, v1, wave, PW, v2, true, lane);  // 256
+  policy_tiles_e<1, 1, 2, 512 / 16, GO1_SPLIT_D2>(LN + 1, v1, wave, PW, v2, true, lane, &s_ovf);  // 256
   __syncthreads();
-  if (wave < 8) policy_tiles_e<1, 1, 2, 256 / 16, 8>(LN + 2, v2, wave, 8, v1, true, lane);  // 128 -> h1
+  if (wave < 8) policy_tiles_e<1, 1, 2, 256 / 16, 8>(LN + 2, v2, wave, 8, v1, true, lane, &s_ovf);  // 128 -> h1
   __syncthreads();
   if (wave < 8) {  // 128 -> num_actions / 1: one K group per wave, partials through LDS
     const ActV src[2] = {v1[0][0], v1[1][0]};
@@ -731,6 +818,8 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
       P.value[e0 + e] = acc[0];
     }
   }
+  __syncthreads();
+  if (s_ovf) policy_fallback(P, e0, ne, !critic, critic, reinterpret_cast<float*>(&h1[0]));
 }
 
 }  // namespace
@@ -771,23 +860,18 @@ int go1_gae(const float* rewards, const uint8_t* dones, const float* values, con
   return GO1_OK_RT;
 }
 
-static int g_policy_split = GO1_POLICY_SPLIT;
-int go1_policy_set_split(int split) {
-  const int prev = g_policy_split;
-  g_policy_split = split ? 1 : 0;
-  return prev;
-}
-
 int go1_policy_forward(const go1_policy_args* args, void* stream) {
   if (!args || args->n_envs <= 0 || !args->obs_history || !args->privileged_obs || !args->action_mean ||
       !args->value)
     return fail(GO1_RT_E_ARG, "go1_policy_forward: bad argument");
-  if (args->hist_dim + 2 > PIN || args->num_actions > 16)
-    return fail(GO1_RT_E_ARG, "go1_policy_forward: input / action width outside the compiled architecture");
+  if (args->num_priv < 1 || args->num_priv > 8 || args->hist_dim + args->num_priv > PIN || args->num_actions > 16)
+    return fail(GO1_RT_E_ARG, "go1_policy_forward: input / latent / action width outside the compiled architecture");
   for (int i = 0; i < GO1_POLICY_LAYERS; ++i)
-    if (!args->layers[i].w || !args->layers[i].b) return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer");
+    if (!args->layers[i].w || !args->layers[i].b || !args->layers[i].wf)
+      return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer (split, bias and f32 weights are required)");
+  if (args->variant != 0 && args->variant != 1) return fail(GO1_RT_E_ARG, "go1_policy_forward: variant");
   go1_policy_args P = *args;
-  if (g_policy_split)
+  if (P.variant == 0)
     hipLaunchKernelGGL(policy_kernel_split, dim3(2 * ((P.n_envs + SE - 1) / SE)), dim3(64 * PW), 0, (hipStream_t)stream, P);
   else
     hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(64 * PW), 0, (hipStream_t)stream, P);

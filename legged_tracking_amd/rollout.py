@@ -91,7 +91,7 @@ class _Transition(C.Structure):
 
 
 class _PolicyLayer(C.Structure):
-    _fields_ = [("w", C.c_void_p), ("b", C.c_void_p)]
+    _fields_ = [("w", C.c_void_p), ("b", C.c_void_p), ("wf", C.c_void_p)]
 
 
 class _PolicyArgs(C.Structure):
@@ -99,7 +99,8 @@ class _PolicyArgs(C.Structure):
                 ("value", C.c_void_p), ("latent", C.c_void_p), ("std", C.c_void_p), ("actions", C.c_void_p),
                 ("action_sigma", C.c_void_p), ("log_prob", C.c_void_p), ("rng_seed", C.c_uint64),
                 ("rng_step", C.c_uint64), ("env_id_offset", C.c_int32), ("n_envs", C.c_int32),
-                ("hist_dim", C.c_int32), ("num_actions", C.c_int32), ("layers", _PolicyLayer * 11)]
+                ("hist_dim", C.c_int32), ("num_actions", C.c_int32), ("num_priv", C.c_int32),
+                ("variant", C.c_int32), ("overflow", C.c_void_p), ("layers", _PolicyLayer * 11)]
 
 
 def _pack_linear(lin):
@@ -128,10 +129,13 @@ class FusedPolicy:
     """ActorCritic forward for the rollout (act + evaluate) in one HIP kernel
     (csrc/rollout.hip policy_kernel).  Re-pack after every optimiser step."""
 
-    def __init__(self, ac, lib):
+    def __init__(self, ac, lib, variant=0):
         self.ac = ac
         self.lib = lib
         self.packed = None
+        self.variant = variant  # 0: per-net workgroups of 32 envs, 1: one workgroup of 16 envs (go1_policy_args)
+        # workgroups that took the f32 fallback of the range guard (activations beyond f16's range)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=next(ac.parameters()).device)
 
     @staticmethod
     def supported(ac):
@@ -141,21 +145,26 @@ class FusedPolicy:
                                                        c[6])]
         except (IndexError, AttributeError):
             return False
-        h = ac.num_obs_history
-        want = [(256, h), (128, 256), (2, 128), (512, h + 2), (256, 512), (128, 256), (None, 128), (512, h + 2),
-                (256, 512), (128, 256), (1, 128)]
+        h, npv = ac.num_obs_history, ac.num_privileged_obs
+        want = [(256, h), (128, 256), (npv, 128), (512, h + npv), (256, 512), (128, 256), (None, 128),
+                (512, h + npv), (256, 512), (128, 256), (1, 128)]
         ok = all(w[0] in (None, s[0]) and w[1] == s[1] for s, w in zip(shapes, want))
-        return ok and h + 2 <= 272 and shapes[6][0] <= 16 and isinstance(a[1], nn.ELU) and ac.num_privileged_obs == 2
+        return ok and 1 <= npv <= 8 and h + npv <= 272 and shapes[6][0] <= 16 and isinstance(a[1], nn.ELU)
 
     def pack(self):
         ac = self.ac
         mods = [ac.adaptation_module[i] for i in (0, 2, 4)] + [ac.actor_body[i] for i in (0, 2, 4, 6)] + \
                [ac.critic_body[i] for i in (0, 2, 4, 6)]
         self.packed = [_pack_linear(m) for m in mods]
+        # the unsplit f32 weights for the range guard's fallback (the module's own tensors: an optimiser
+        # step updates them in place; the split copies are re-packed)
+        self.wf = [m.weight.detach().float().contiguous() for m in mods]
         self.na = ac.actor_body[6].out_features
-        self.args = _PolicyArgs(num_actions=self.na)
+        self.np = ac.num_privileged_obs
+        self.args = _PolicyArgs(num_actions=self.na, num_priv=self.np, overflow=self.overflow.data_ptr())
         for i, (w, b) in enumerate(self.packed):
             self.args.layers[i].w, self.args.layers[i].b = w.data_ptr(), b.data_ptr()
+            self.args.layers[i].wf = self.wf[i].data_ptr()
 
     def forward(self, obs_history, privileged_obs, sample=None):
         """-> (mean, value, latent) or, with sample = (rng_seed, rng_step, env_id_offset),
@@ -173,8 +182,9 @@ class FusedPolicy:
         dev = h.device
         mean = torch.empty(n, na, device=dev)
         value = torch.empty(n, 1, device=dev)
-        latent = torch.empty(n, 2, device=dev)
+        latent = torch.empty(n, self.np, device=dev)
         a = self.args
+        a.variant = self.variant
         a.obs_history, a.privileged_obs = h.data_ptr(), p.data_ptr()
         a.action_mean, a.value, a.latent = mean.data_ptr(), value.data_ptr(), latent.data_ptr()
         a.n_envs, a.hist_dim = n, h.shape[1]
@@ -210,7 +220,6 @@ class HipRolloutKernels:
         lib.go1_gae.argtypes = [C.c_void_p] * 7 + [C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_void_p]
         lib.go1_adv_normalize.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_int64, C.c_void_p]
         lib.go1_policy_forward.argtypes = [C.POINTER(_PolicyArgs), C.c_void_p]
-        lib.go1_policy_set_split.argtypes = [C.c_int]
         self.lib = lib
 
     def _chk(self, rc):
@@ -277,6 +286,39 @@ def get_activation(name):
     if name not in acts:
         raise ValueError(f"invalid activation function {name!r}")
     return acts[name]()
+
+
+class _LinearSplitK(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient is summed over K_SPLIT row chunks of the batch (one batched
+    GEMM, then a sum over the chunks): the mini-batch weight gradient dW = dY^T X is a tall-skinny
+    reduction (K = 24,576 samples, M x N <= 512 x 263), which one GEMM spreads over only a few dozen
+    workgroups of the 256 CUs; the batched form gives each chunk its own tiles.  Same value as
+    F.linear's backward up to the f32 summation order."""
+
+    K_SPLIT = 16
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        n, S = x.shape[0], _LinearSplitK.K_SPLIT
+        if n % S == 0 and n // S >= 256:
+            gw = torch.bmm(gy.view(S, n // S, -1).transpose(1, 2), x.view(S, n // S, -1)).sum(0)
+        else:
+            gw = gy.t() @ x
+        return gx, gw, gy.sum(0)
+
+
+def _mlp_train(seq, x):
+    """nn.Sequential of Linear / activation layers evaluated with _LinearSplitK (training mini-batches)."""
+    for m in seq:
+        x = _LinearSplitK.apply(x, m.weight, m.bias) if isinstance(m, nn.Linear) else m(x)
+    return x
 
 
 def _mlp(sizes, act):
@@ -358,6 +400,15 @@ class ActorCritic(nn.Module):
 
     def get_student_latent(self, observation_history):
         return self.adaptation_module(observation_history)
+
+    def update_distribution_train(self, observation_history):
+        """update_distribution for PPO.update's mini-batches (split-K weight gradients, _LinearSplitK)."""
+        latent = _mlp_train(self.adaptation_module, observation_history)
+        mean = _mlp_train(self.actor_body, torch.cat((observation_history, latent), dim=-1))
+        self.distribution = Normal(mean, mean * 0.0 + self.std, validate_args=False)
+
+    def evaluate_train(self, observation_history, privileged_observations):
+        return _mlp_train(self.critic_body, torch.cat((observation_history, privileged_observations), dim=-1))
 
 
 # ----------------------------------------------------------------------------- storage
@@ -604,9 +655,10 @@ class PPO:
         gen = self.storage.mini_batch_generator(A.num_mini_batches, A.num_learning_epochs)
         for (obs_b, critic_obs_b, priv_b, hist_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b,
              old_sigma_b, masks_b, bins_b) in gen:
-            ac.act(hist_b, masks=masks_b)
+            ac.update_distribution_train(hist_b)
+            ac.distribution.sample()  # ac.act's (unused) sample: the reference's torch RNG consumption (ppo.py:110)
             logp_b = ac.get_actions_log_prob(act_b)
-            value_b = ac.evaluate(hist_b, priv_b, masks=masks_b)
+            value_b = ac.evaluate_train(hist_b, priv_b)
             mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
             if A.desired_kl is not None and A.schedule == "adaptive":
                 with torch.inference_mode():
@@ -644,7 +696,7 @@ class PPO:
             acc[1] += surrogate_loss.detach()
             num_train = int(priv_b.shape[0] // 5 * 4)
             for _ in range(A.num_adaptation_module_substeps):
-                pred = ac.adaptation_module(hist_b)
+                pred = _mlp_train(ac.adaptation_module, hist_b)
                 with torch.no_grad():
                     target = priv_b
                 # every column (ppo.py:193: linspace(0, w - 1, w) as an index), or column 0

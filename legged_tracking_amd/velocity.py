@@ -622,6 +622,11 @@ class VelocityTrackingEasyEnv:
     def _flush_episode_log(self):
         pass
 
+    def _deferred_time_outs(self):
+        """extras["time_outs"] for the PPO record kernel: the curriculum launch of go1_vel_step already applied
+        the step's rebinding in stream order, so nothing is pending."""
+        return self._sim.extras_time_outs[: self.num_train_envs], None
+
     def _episode_extras(self):
         """extras["train/episode"] of the last step's reset_idx (:199-249): means of the episode sums over the
         envs reset by that step, the command range statistics and the curricula's areas."""

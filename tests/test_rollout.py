@@ -210,6 +210,110 @@ def test_fused_policy_kernel_matches_reference_actor_critic():
         np.testing.assert_allclose(v2.cpu().numpy(), vt.cpu().numpy(), rtol=1e-4, atol=1e-4)
 
 
+def _trained():
+    """The reference's trained checkpoint (6 privileged obs), tests/golden/make_trained_policy.py."""
+    d = G.load("trained_policy.npz")
+    npriv = d["in/priv"].shape[1]
+    ac = R.ActorCritic(261, npriv, 261, 12)
+    ac.load_state_dict({k[3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("sd/")})
+    return d, ac
+
+
+def test_trained_checkpoint_fixture_matches_the_torch_restatement():
+    d, ac = _trained()
+    h, p = torch.from_numpy(d["in/hist"]), torch.from_numpy(d["in/priv"])
+    with torch.no_grad():  # f32 CPU against the f64 record: tolerance relative to each output's scale
+        lat = ac.adaptation_module(h)
+        for got, k in ((lat, "latent"), (ac.actor_body(torch.cat((h, lat), -1)), "mean"),
+                       (ac.critic_body(torch.cat((h, p), -1)), "value")):
+            want = d["out/" + k]
+            np.testing.assert_allclose(got.numpy(), want, rtol=1e-5, atol=1e-5 * np.abs(want).max())
+
+
+@pytest.mark.gpu
+def test_fused_policy_kernel_runs_the_reference_trained_checkpoint():
+    """The fused 3xF16 kernel on the reference's only trained weights (6-wide latent, 267 actor / critic
+    inputs), both kernel variants, against the f64 forward of the checkpoint: the split keeps f32 accuracy
+    on trained (not just freshly initialised) weights."""
+    d, ac = _trained()
+    ac = ac.to("cuda:0")
+    pol = R.HipRolloutKernels().policy(ac)
+    assert pol is not None
+    h, p = (torch.from_numpy(d[x]).cuda() for x in ("in/hist", "in/priv"))
+    for variant in (0, 1):
+        pol.variant = variant
+        mean, value, latent = pol.forward(h, p)
+        torch.cuda.synchronize()
+        for got, k in ((latent, "latent"), (mean, "mean"), (value, "value")):
+            want = d["out/" + k]  # f64 record; f32 accuracy relative to the output's scale
+            np.testing.assert_allclose(got.cpu().numpy(), want, rtol=2e-5, atol=2e-5 * np.abs(want).max())
+    assert int(pol.overflow.item()) == 0
+
+
+def _split_values_max(ac, h, p):
+    """The largest |value| the fused kernel splits into f16 (hi, lo): inputs, the latent and every hidden
+    layer's output (the output layers' values are written unsplit)."""
+    vals = [h.abs().max(), p.abs().max()]
+    with torch.no_grad():
+        def run(seq, x):
+            for m in list(seq)[:-1]:
+                x = m(x)
+                if not isinstance(m, torch.nn.Linear):
+                    vals.append(x.abs().max())
+            return seq[-1](x)
+        lat = run(ac.adaptation_module, h)
+        vals.append(lat.abs().max())
+        run(ac.actor_body, torch.cat((h, lat), -1))
+        run(ac.critic_body, torch.cat((h, p), -1))
+    return max(float(v) for v in vals)
+
+
+@pytest.mark.gpu
+def test_fused_policy_range_guard():
+    """Split values near and beyond the f16 range of the 3xF16 split.  The first layers' weights are scaled
+    so that the largest value the kernel splits is 5e4 (inside f16's range: the split stays exact to f32,
+    no fallback) and 2e5 (beyond it: f16(x) would be inf; the workgroup's guard recomputes its envs in f32
+    from the unsplit weights).  Both match torch f32 (sampling included); only the second touches the
+    fallback counter."""
+    d = _fixture()
+    n = 64 + 7
+    g = torch.Generator(device="cuda").manual_seed(3)
+    h = torch.rand(n, 261, device="cuda", generator=g) + 0.5
+    p = torch.rand(n, 2, device="cuda", generator=g)
+    for target, expect_fallback in ((5.0e4, False), (2.0e5, True)):
+        base = _ac(d, "cuda:0")
+        with torch.no_grad():
+            for body in (base.actor_body, base.critic_body, base.adaptation_module):
+                body[0].weight.copy_(body[0].weight.abs())
+                body[0].bias.zero_()
+        lo, hi = 1.0, 1.0e4
+        for _ in range(60):  # bisect the layer-1 scale for the target maximum (monotone in the scale)
+            mid = (lo * hi) ** 0.5
+            ac = _ac(d, "cuda:0")
+            ac.load_state_dict(base.state_dict())
+            with torch.no_grad():
+                for body in (ac.actor_body, ac.critic_body, ac.adaptation_module):
+                    body[0].weight.mul_(mid)
+            lo, hi = (mid, hi) if _split_values_max(ac, h, p) < target else (lo, mid)
+        mx = _split_values_max(ac, h, p)
+        assert 0.95 * target < mx < 1.05 * target, mx
+        with torch.no_grad():
+            lt = ac.adaptation_module(h)
+            mt = ac.actor_body(torch.cat((h, lt), -1))
+            vt = ac.critic_body(torch.cat((h, p), -1))
+        pol = R.HipRolloutKernels().policy(ac)
+        for variant in (0, 1):
+            pol.variant = variant
+            pol.overflow.zero_()
+            mean, value, latent, actions, sigma, logp = pol.forward(h, p, sample=(5, 1, 0))
+            torch.cuda.synchronize()
+            for got, want in ((latent, lt), (mean, mt), (value, vt)):
+                scale = want.abs().max().item()
+                np.testing.assert_allclose(got.cpu().numpy(), want.cpu().numpy(), rtol=1e-4, atol=1e-5 * scale)
+            assert torch.isfinite(actions).all() and torch.isfinite(logp).all()
+            assert (int(pol.overflow.item()) > 0) == expect_fallback, (target, variant, int(pol.overflow.item()))
+
+
 @pytest.mark.gpu
 def test_split_policy_kernel_is_bit_identical_to_single_workgroup_kernel():
     """policy_kernel_split (a workgroup per net for 32 envs, weight fragments shared by two env
@@ -225,12 +329,9 @@ def test_split_policy_kernel_is_bit_identical_to_single_workgroup_kernel():
     h = torch.randn(n, 261, device="cuda", generator=g)
     p = torch.randn(n, 2, device="cuda", generator=g)
     outs = []
-    try:
-        for split in (1, 0):
-            k.lib.go1_policy_set_split(split)
-            outs.append([t.cpu().numpy() for t in pol.forward(h, p, sample=(123, 7, 0))])
-    finally:
-        k.lib.go1_policy_set_split(1)
+    for variant in (0, 1):  # per call (go1_policy_args.variant)
+        pol.variant = variant
+        outs.append([t.cpu().numpy() for t in pol.forward(h, p, sample=(123, 7, 0))])
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 
