@@ -7,16 +7,20 @@
 //     clock (_step_contact_targets :844-923), DR (:714-717), terminations (:156-166), the CoRL reward
 //     terms and command sums (:281-318, go1_gym/envs/rewards/corl_rewards.py), reset_idx's state part
 //     (:168-257), observations (:320-509), the epilogue (:144-149) and the appended obs_history row.
-//   go1_vel_curriculum_kernel: workgroup 0 runs _resample_commands (:728-842) for the envs the step reset
+//   go1_vel_curriculum_kernel: one workgroup runs _resample_commands (:728-842) for the envs the step reset
 //     (RewardThresholdCurriculum.update, Curriculum.sample: go1_gym/envs/base/curriculum.py) and patches
-//     their observed commands, then the interval resample of the next step ahead of time; the other
-//     workgroups shift the history (obs_history[:, 70:] -> the new buffer).
+//     their observed commands, then the interval resample of the next step ahead of time.
+//   go1_vel_hist_shift_kernel, on the handle's side stream beside the two: the history shift
+//     (obs_history[:, 70:] -> the new buffer).
 // Lane layout of the step kernel as in go1_step.hip: 16 lanes per env = 4 legs x 4 roles, four envs per
 // one-wave block.  Post-physics arithmetic is f32 with contraction off in torch's operation order, the
 // transcendentals of the gait clock and the rewards via f64 (correctly rounded f32 but for rare double
 // roundings), so the results match oracle/vel_oracle.py to the ulp of numpy's own exp / sin / erf.
 #include "go1_device.h"
 #include "../../include/go1_velocity.h"
+
+#include <algorithm>
+#include <vector>
 
 typedef const __attribute__((address_space(4))) go1_vel_config VCfg;
 #define VLAG 2  // GO1_LAG_STEPS(decimation) for decimation 4..6 (go1_vel_create checks it)
@@ -782,9 +786,27 @@ __global__ void go1_vel_mask_kernel(const int32_t* __restrict__ ids, int n_ids, 
 //        command curriculum (_resample_commands) + history shift
 // =====================================================================
 #define CK_THREADS 1024
+#ifdef GO1_VEL_STAMPS  // diagnostic build only (tools/vel_stamps.py): per section of block 0, cycle sums
+// [phase B / A][section] and the number of phases that ran with selected envs
+__device__ unsigned long long g_vstamps[2][16];
+#define VSTAMP(ph, k, t0)                                                            \
+  do {                                                                              \
+    if (threadIdx.x == 0) {                                                         \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                    \
+      atomicAdd(&g_vstamps[ph][k], t_ - t0);                                        \
+      t0 = t_;                                                                      \
+    }                                                                               \
+  } while (0)
+#else
+#define VSTAMP(ph, k, t0)
+#endif
+#define CK_BATCH 8
+#define CK_SEL_CAP 4096
 struct CArgs {
   go1_vel_state st;
   const double* grid;   // (GO1_VEL_N_KEYS, n_bins)
+  const int32_t* adj_ptr;  // neighbourhood table (CSR): cells adjacent to bin b are adj_idx[adj_ptr[b] ..]
+  const int32_t* adj_idx;
   double* cdf;          // (GO1_VEL_N_CATEGORIES, n_bins): numpy's normalised cdf of each curriculum
   int32_t* cdf_ok;      // [GO1_VEL_N_CATEGORIES]: cdf current for the weights
   int n_envs, env_id_offset;
@@ -807,6 +829,7 @@ struct CArgs {
   float* hist_out;
   const float* hist_in;
   int hist_w;
+  int hist_aligned;  // hist_w % 4 == 0 and both buffers 16-byte aligned: the shift moves 16-byte chunks
 };
 
 // numpy's pairwise summation (np.add.reduce of a contiguous f64 array), PW_BLOCKSIZE 128
@@ -836,7 +859,7 @@ __device__ __forceinline__ float remainder1(float a) { return remainder_f(a, 1.0
 
 // One resample (_resample_commands :728-842) of kind B (mask) or A (interval), by the whole workgroup.
 __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs& K, bool kindB, int* s_hist,
-                               int* s_list, double* s_p, int* s_cnt, int* s_dirty) {
+                               int* s_list, int* s_inc, double* s_p, int* s_sel, int* s_cnt, int* s_dirty) {
   const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
   const go1_vel_state& st = K.st;
   const float* U = kindB ? K.UB : K.UA;
@@ -845,6 +868,11 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
   const int ucat = kindB ? GO1_VEL_U_CAT_B : GO1_VEL_U_CAT_A;
   const int dch = kindB ? GO1_VEL_D_CHOICE_B : GO1_VEL_D_CHOICE_A;
   const int NC = v->n_terms + GO1_VEL_SUM_EXTRA;
+  const int ph = kindB ? 0 : 1;
+  (void)ph;
+#ifdef GO1_VEL_STAMPS
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
   auto selected = [&](int e) {
     return kindB ? K.maskB[e] != 0 : ((st.episode_length[e] + 1) % R == 0);
   };
@@ -852,13 +880,41 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
   if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
   if (tid < GO1_VEL_N_CATEGORIES) s_dirty[tid] = 0;
   __syncthreads();
+  // ---- env_ids: the selected envs, compacted into s_sel (the flags of CK_BATCH envs per thread are
+  // loaded before any is tested, so the scan costs one memory latency per CK_BATCH * CK_THREADS envs);
+  // beyond CK_SEL_CAP selected envs (a full reset) the loops below scan the flags again instead
+  for (int e0 = 0; e0 < n; e0 += CK_THREADS * CK_BATCH) {
+    bool sv[CK_BATCH];
+#pragma unroll
+    for (int k = 0; k < CK_BATCH; ++k) {
+      const int e = e0 + k * CK_THREADS + tid;
+      sv[k] = e < n && selected(e);
+    }
+#pragma unroll
+    for (int k = 0; k < CK_BATCH; ++k)
+      if (sv[k]) {
+        const int slot = atomicAdd(s_cnt, 1);
+        if (slot < CK_SEL_CAP) s_sel[slot] = e0 + k * CK_THREADS + tid;
+      }
+  }
+  __syncthreads();
+  VSTAMP(ph, 0, t0);
+  const int count = s_cnt[0];
+  if (count == 0) return;
+  VSTAMP(ph, 15, t0);  // len(env_ids) == 0 (:730): nothing, not even the time-out rebinding
+  auto for_selected = [&](auto&& fn) {
+    if (count <= CK_SEL_CAP) {
+      for (int i = tid; i < count; i += CK_THREADS) fn(s_sel[i]);
+    } else {
+      for (int e = tid; e < n; e += CK_THREADS)
+        if (selected(e)) fn(e);
+    }
+  };
   // ---- RewardThresholdCurriculum.update per old category (:736-757, curriculum.py:135-154): success
   // counts per (category, bin), and the list of the (category, bin) pairs that have any
-  for (int e = tid; e < n; e += CK_THREADS) {
-    if (!selected(e)) continue;
-    atomicAdd(s_cnt, 1);
+  for_selected([&](int e) {
     const int cat = st.command_categories[e];
-    if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES || v->n_task == 0) continue;
+    if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES || v->n_task == 0) return;
     bool ok = true;
     for (int k = 0; k < v->n_task; ++k)
       ok = ok && (st.command_sums[(size_t)e * NC + v->task_slot[k]] / v->curriculum_ep_len > v->task_threshold[k]);
@@ -869,153 +925,263 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
         s_list[slot] = cat * nb + b;  // at most GO1_VEL_N_CATEGORIES * nb distinct pairs
       }
     }
-  }
+  });
   __syncthreads();
-  const int count = s_cnt[0], n_list = s_cnt[1];
-  if (count == 0) return;  // len(env_ids) == 0 (:730): nothing, not even the time-out rebinding
+  VSTAMP(ph, 1, t0);
+  const int n_list = s_cnt[1];
   if (kindB && K.extras_time_outs)
     for (int e = tid; e < n; e += CK_THREADS) K.extras_time_outs[e] = K.time_out[e];
   // weights: cell j of category c gets +0.2 (clipped) once if it was a success bin and once per success
   // env whose bin's neighbourhood holds it -- a sequence of identical clip(w + 0.2, 0, 1) steps, so the
-  // count decides the result whatever the order
+  // count decides the result whatever the order.  Neighbourhoods come from the handle's table
+  // (get_local_bins, curriculum.py:123-133, evaluated on the host in the same f64 comparisons).
   if (n_list > 0) {
+    for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) s_inc[i] = 0;
+    __syncthreads();
+    for (int l = tid; l < n_list; l += CK_THREADS) {
+      const int cb = s_list[l], cat = cb / nb, b = cb % nb, h = s_hist[cb];
+      atomicAdd(&s_inc[cb], 1);  // weights[bin_inds[is_success]] += 0.2 (once per distinct bin)
+      for (int q = K.adj_ptr[b]; q < K.adj_ptr[b + 1]; ++q) atomicAdd(&s_inc[cat * nb + K.adj_idx[q]], h);
+    }
+    __syncthreads();
     for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
-      const int cat = i / nb, j = i % nb;
-      int k = s_hist[i] > 0 ? 1 : 0;
-      for (int l = 0; l < n_list; ++l) {
-        const int cb = s_list[l];
-        if (cb / nb != cat) continue;
-        const int b = cb % nb;
-        bool adj = true;
-        for (int key = 0; key < GO1_VEL_N_KEYS; ++key) {
-          const double gb = K.grid[(size_t)key * nb + b], gj = K.grid[(size_t)key * nb + j], r = v->local_range[key];
-          adj = adj && gj >= gb - r && gj <= gb + r;
-        }
-        if (adj) k += s_hist[cb];
-      }
+      const int k = s_inc[i];
       if (k > 0) {
         double w = st.curriculum_weights[i];
         for (int t = 0; t < k; ++t) w = fmin(fmax(w + 0.2, 0.0), 1.0);
         st.curriculum_weights[i] = w;
-        s_dirty[cat] = 1;
+        s_dirty[i / nb] = 1;
       }
     }
   }
   __syncthreads();
-  // ---- numpy rng.choice(p = w / w.sum()): cdf = cumsum(p) / cdf[-1], wave c for category c
+  VSTAMP(ph, 2, t0);
+  // ---- numpy rng.choice(p = w / w.sum()): cdf = cumsum(p) / cdf[-1], wave c for category c, in LDS
+  // (s_p); a category whose weights did not change reloads the cdf the handle keeps from its last
+  // computation.  The sampling below searches s_p.
   {
     const int wv = tid >> 6, ln = tid & 63;
-    if (wv < GO1_VEL_N_CATEGORIES && (s_dirty[wv] || !K.cdf_ok[wv])) {
-      const double* w = st.curriculum_weights + (size_t)wv * nb;
+    if (wv < GO1_VEL_N_CATEGORIES) {
       double* p = s_p + (size_t)wv * GO1_VEL_MAX_BINS;
-      double s = 0.0;
-      if (ln == 0) s = np_pairwise_sum<4>(w, nb);
-      s = __shfl(s, 0);
-      for (int j = ln; j < nb; j += 64) p[j] = w[j] / s;
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      if (ln == 0) {
-        double acc = 0.0;
-        for (int j = 0; j < nb; ++j) { acc += p[j]; p[j] = acc; }
+      if (s_dirty[wv] || !K.cdf_ok[wv]) {
+        const double* w = st.curriculum_weights + (size_t)wv * nb;
+        double t[GO1_VEL_MAX_BINS / 64];  // all of the lane's loads in flight before the LDS stores
+#pragma unroll
+        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? w[ln + 64 * i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
+          if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double s = 0.0;
+        if (ln == 0) s = np_pairwise_sum<4>(p, nb);
+        s = __shfl(s, 0);
+        for (int j = ln; j < nb; j += 64) p[j] = p[j] / s;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (ln == 0) {  // numpy's sequential cumsum: the adds are a dependent chain, the LDS reads of a
+                        // batch are issued ahead of it (in place, one read-write per element, it would wait
+                        // out the LDS latency at every element)
+          double acc = 0.0;
+          for (int j0 = 0; j0 < nb; j0 += 32) {
+            double t[32];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) t[i] = j0 + i < nb ? p[j0 + i] : 0.0;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) { acc += t[i]; t[i] = acc; }
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+              if (j0 + i < nb) p[j0 + i] = t[i];
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const double last = p[nb - 1];
+        for (int j = ln; j < nb; j += 64) {
+          const double c = p[j] / last;
+          p[j] = c;
+          K.cdf[(size_t)wv * nb + j] = c;
+        }
+        if (ln == 0) K.cdf_ok[wv] = 1;
+#ifdef GO1_VEL_STAMPS
+        if (ln == 0) atomicAdd(&g_vstamps[kindB ? 0 : 1][14], 1ull);
+#endif
+      } else {
+        const double* g = K.cdf + (size_t)wv * nb;
+        double t[GO1_VEL_MAX_BINS / 64];
+#pragma unroll
+        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? g[ln + 64 * i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
+          if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
       }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const double last = p[nb - 1];
-      for (int j = ln; j < nb; j += 64) K.cdf[(size_t)wv * nb + j] = p[j] / last;
-      if (ln == 0) K.cdf_ok[wv] = 1;
     }
   }
   __syncthreads();
-  // ---- new category, cell and command per env (:759-842)
-  for (int e = tid; e < n; e += CK_THREADS) {
-    if (!selected(e)) continue;
-    const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
-    const RngD rngd = {UD, K.seed, step, e, e + K.env_id_offset};
-    const float uc = rng(ucat);
-    int cat = -1;
-    for (int i = 0; i < GO1_VEL_N_CATEGORIES; ++i)
-      if ((float)(0.25 * i) <= uc && uc < (float)(0.25 * (i + 1))) cat = i;
-    float cmd[GO1_VEL_NUM_COMMANDS];
-    for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) cmd[k] = st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + k];
-    if (cat >= 0) {
-      const double u0 = rngd(dch);
-      const double* cdf = K.cdf + (size_t)cat * nb;
-      int lo = 0, hi = nb;  // searchsorted(cdf, u0, side='right'): first j with cdf[j] > u0
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (cdf[mid] <= u0) lo = mid + 1; else hi = mid;
+  VSTAMP(ph, 3, t0);
+  // ---- new category, cell and command per env (:759-842), 16 lanes per env: lane k < 15 draws and
+  // finishes command k (the gait rules and binary phases act per command; only the small-command rule
+  // pairs commands 0 and 1), lane 15 draws the choice and searches the cdf.  One Philox evaluation per
+  // lane instead of ~30 in sequence on one thread.
+  {
+    const int sub = tid & 15, grp = tid >> 4;
+    const bool listed = count <= CK_SEL_CAP;
+    const int n_iter = listed ? count : n;
+    for (int i0 = 0; i0 < n_iter; i0 += CK_THREADS / 16) {
+      const int i = i0 + grp;
+      int e = -1;
+      if (listed) {
+        if (i < count) e = s_sel[i];
+      } else if (i < n && selected(i)) {
+        e = i;
       }
-      const int idx = min(lo, nb - 1);
-      for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) {
-        const double cen = K.grid[(size_t)k * nb + idx], half = v->bin_sizes[k] / 2.0;
-        const double l = cen + half, h = cen - half;
-        cmd[k] = (float)(l + (h - l) * rngd(dch + 1 + k));
+      if (e < 0) continue;  // uniform over the env's 16 lanes
+      const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
+      const RngD rngd = {UD, K.seed, step, e, e + K.env_id_offset};
+      const float uc = rng(ucat);
+      int cat = -1;
+      for (int c = 0; c < GO1_VEL_N_CATEGORIES; ++c)
+        if ((float)(0.25 * c) <= uc && uc < (float)(0.25 * (c + 1))) cat = c;
+      float cmd = sub < GO1_VEL_NUM_COMMANDS ? st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] : 0.0f;
+      if (cat >= 0) {
+        const double u = rngd(sub < GO1_VEL_NUM_COMMANDS ? dch + 1 + sub : dch);
+        int idx = 0;
+        if (sub == 15) {
+          const double* cdf = s_p + (size_t)cat * GO1_VEL_MAX_BINS;
+          int lo = 0, hi = nb;  // searchsorted(cdf, u, side='right'): first j with cdf[j] > u
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
+          }
+          idx = min(lo, nb - 1);
+          st.command_bins[e] = idx;
+          st.command_categories[e] = cat;
+        }
+        idx = __shfl(idx, 15, 16);
+        if (sub < GO1_VEL_NUM_COMMANDS) {
+          const double cen = K.grid[(size_t)sub * nb + idx], half = v->bin_sizes[sub] / 2.0;
+          const double l = cen + half, h = cen - half;
+          cmd = (float)(l + (h - l) * u);
+          if (v->gaitwise_curricula && sub >= 5 && sub < 8) {
+            if (cat == CAT_PRONK) cmd = remainder1(cmd / 2.0f - 0.25f);
+            else if (sub - 5 == cat - 1) cmd = cmd / 2.0f + 0.25f;  // trot: 5, pace: 6, bound: 7
+            else cmd = 0.0f;
+          }
+        }
       }
-      st.command_bins[e] = idx;
-      st.command_categories[e] = cat;
-      if (v->gaitwise_curricula) {
-        if (cat == CAT_PRONK) {
-          for (int k = 5; k < 8; ++k) cmd[k] = remainder1(cmd[k] / 2.0f - 0.25f);
-        } else if (cat == CAT_TROT) {
-          cmd[5] = cmd[5] / 2.0f + 0.25f; cmd[6] = 0.0f; cmd[7] = 0.0f;
-        } else if (cat == CAT_PACE) {
-          cmd[5] = 0.0f; cmd[6] = cmd[6] / 2.0f + 0.25f; cmd[7] = 0.0f;
-        } else {
-          cmd[5] = 0.0f; cmd[6] = 0.0f; cmd[7] = cmd[7] / 2.0f + 0.25f;
+      if (v->binary_phases && sub >= 5 && sub < 8) cmd = remainder1(rintf(2.0f * cmd) / 2.0f);
+      {
+        const float c0 = __shfl(cmd, 0, 16), c1 = __shfl(cmd, 1, 16);
+        const float keep = norm2_f(c0, c1) > 0.2f ? 1.0f : 0.0f;
+        if (sub < 2) cmd = cmd * keep;
+      }
+      if (sub < GO1_VEL_NUM_COMMANDS) st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] = cmd;
+      for (int k = sub; k < NC; k += 16) st.command_sums[(size_t)e * NC + k] = 0.0f;
+      if (kindB && K.obs && sub < GO1_VEL_NUM_COMMANDS) {  // this step's observation of the resampled commands (:339)
+        const float clip = v->clip_obs;
+        float val = cmd * v->cmd_scale[sub];
+        if (v->add_noise) val = val + (2.0f * rng(GO1_VEL_U_NOISE + 3 + sub) - 1.0f) * v->noise_vec[3 + sub];
+        val = clampf(val, -clip, clip);
+        K.obs[(size_t)e * GO1_VEL_NUM_OBS + 3 + sub] = val;
+        if (K.hist_out) K.hist_out[(size_t)e * K.hist_w + K.hist_w - GO1_VEL_NUM_OBS + 3 + sub] = val;
+      }
+    }
+  }
+  __syncthreads();
+  VSTAMP(ph, 4, t0);
+}
+
+// HistoryWrapper.step's shift (history_wrapper.py:22): new[:, :W - 70] = old[:, 70:].  Its own launch, on
+// the handle's side stream beside the step kernel (nothing either reads or writes overlaps): a pure
+// HBM stream of 2 x 33 MB at 4096 envs x 30 observations, which in the curriculum launch slowed that
+// launch's latency-bound workgroup 0 through the memory system.
+#define SHIFT_THREADS 256
+__global__ __launch_bounds__(SHIFT_THREADS) void go1_vel_hist_shift_kernel(CArgs K) {
+  if (!K.hist_in || !K.hist_out) return;
+  const int W = K.hist_w, D = W - GO1_VEL_NUM_OBS;
+  const size_t G = (size_t)gridDim.x * SHIFT_THREADS;
+  const size_t g0 = (size_t)blockIdx.x * SHIFT_THREADS + threadIdx.x;
+  if (K.hist_aligned) {
+    // 16-byte chunks: rows are 16-byte aligned (W % 4 == 0), the source starts 70 = 4 x 17 + 2 floats in,
+    // so dest chunk i = (z, w) of aligned source chunk 17 + i and (x, y) of chunk 18 + i, which the next
+    // lane holds (lane 63 loads it).  Chunks per row padded to a multiple of 64 keep a wave in one row;
+    // four chunks per thread are loaded before any is stored (HBM latency x bandwidth needs them in flight).
+    // D = W - 70 is 2 mod 4: the last chunk of a row is half (its other half is the new obs row).
+    const int Cn = (D + 3) / 4, Cp = (Cn + 63) & ~63;
+    const size_t total = (size_t)K.n_envs * Cp;
+    const bool last_lane = (threadIdx.x & 63) == 63;
+    for (size_t t0 = g0; t0 < total; t0 += 4 * G) {
+      float4 own[4];
+      size_t ev[4];
+      int iv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t t = t0 + u * G;
+        ev[u] = t / Cp;
+        iv[u] = (int)(t % Cp);
+        own[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (t < total && iv[u] < Cn) own[u] = reinterpret_cast<const float4*>(K.hist_in + ev[u] * W)[17 + iv[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t t = t0 + u * G;  // t < total is uniform over the wave (total, G, t0 - lane: multiples of 64)
+        if (t >= total) break;
+        float nx = __shfl_down(own[u].x, 1), ny = __shfl_down(own[u].y, 1);
+        const int i = iv[u];
+        if (last_lane && i + 1 < Cn) {
+          const float4 o2 = reinterpret_cast<const float4*>(K.hist_in + ev[u] * W)[18 + i];
+          nx = o2.x;
+          ny = o2.y;
+        }
+        if (i < Cn) {
+          float* dst = K.hist_out + ev[u] * W + 4 * i;
+          if (4 * i + 4 <= D) *reinterpret_cast<float4*>(dst) = make_float4(own[u].z, own[u].w, nx, ny);
+          else *reinterpret_cast<float2*>(dst) = make_float2(own[u].z, own[u].w);
         }
       }
     }
-    if (v->binary_phases)
-      for (int k = 5; k < 8; ++k) cmd[k] = remainder1(rintf(2.0f * cmd[k]) / 2.0f);
-    {
-      const float keep = norm2_f(cmd[0], cmd[1]) > 0.2f ? 1.0f : 0.0f;
-      cmd[0] = cmd[0] * keep;
-      cmd[1] = cmd[1] * keep;
-    }
-    for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + k] = cmd[k];
-    for (int k = 0; k < NC; ++k) st.command_sums[(size_t)e * NC + k] = 0.0f;
-    if (kindB && K.obs) {  // this step's observation of the resampled commands (:339)
-      const float clip = v->clip_obs;
-      for (int k = 0; k < GO1_VEL_NUM_COMMANDS; ++k) {
-        float val = cmd[k] * v->cmd_scale[k];
-        if (v->add_noise) val = val + (2.0f * rng(GO1_VEL_U_NOISE + 3 + k) - 1.0f) * v->noise_vec[3 + k];
-        val = clampf(val, -clip, clip);
-        K.obs[(size_t)e * GO1_VEL_NUM_OBS + 3 + k] = val;
-        if (K.hist_out) K.hist_out[(size_t)e * K.hist_w + K.hist_w - GO1_VEL_NUM_OBS + 3 + k] = val;
-      }
-    }
+    return;
   }
-  __syncthreads();
+  // any other width / alignment: f32 pairs (rows are 8-byte aligned: 70 x 4 B is not a multiple of 16)
+  const int W2 = D / 2;
+  const size_t total = (size_t)K.n_envs * W2;
+  for (size_t i = g0; i < total; i += G) {
+    const size_t e = i / W2, k = i % W2;
+    const float2 val = *(const float2*)(K.hist_in + e * W + GO1_VEL_NUM_OBS + 2 * k);
+    *(float2*)(K.hist_out + e * W + 2 * k) = val;
+  }
 }
 
 __global__ __launch_bounds__(CK_THREADS) void go1_vel_curriculum_kernel(const go1_vel_config* __restrict__ v_gen,
                                                                         CArgs K) {
   VCfg* __restrict__ v = (VCfg*)v_gen;
-  if (blockIdx.x > 0) {
-    // HistoryWrapper.step's shift (history_wrapper.py:22): new[:, :W - 70] = old[:, 70:], as f32 pairs
-    // (rows are 8-byte aligned: 70 x 4 B is not a multiple of 16)
-    if (!K.hist_in || !K.hist_out) return;
-    const int W = K.hist_w, W2 = (W - GO1_VEL_NUM_OBS) / 2;
-    const size_t total = (size_t)K.n_envs * W2;
-    for (size_t i = (size_t)(blockIdx.x - 1) * CK_THREADS + threadIdx.x; i < total;
-         i += (size_t)(gridDim.x - 1) * CK_THREADS) {
-      const size_t e = i / W2, k = i % W2;
-      const float2 val = *(const float2*)(K.hist_in + e * W + GO1_VEL_NUM_OBS + 2 * k);
-      *(float2*)(K.hist_out + e * W + 2 * k) = val;
-    }
-    return;
-  }
   __shared__ int s_hist[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
   __shared__ double s_p[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
   __shared__ int s_list[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
+  __shared__ int s_inc[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
+  __shared__ int s_sel[CK_SEL_CAP];
   __shared__ int s_cnt[2], s_dirty[GO1_VEL_N_CATEGORIES];
-  if (K.maskB) resample_phase(v, v_gen, K, true, s_hist, s_list, s_p, s_cnt, s_dirty);
-  if (K.doA) resample_phase(v, v_gen, K, false, s_hist, s_list, s_p, s_cnt, s_dirty);
+  if (K.maskB) resample_phase(v, v_gen, K, true, s_hist, s_list, s_inc, s_p, s_sel, s_cnt, s_dirty);
+  if (K.doA) resample_phase(v, v_gen, K, false, s_hist, s_list, s_inc, s_p, s_sel, s_cnt, s_dirty);
 }
 
 // =====================================================================
 //                                C ABI
 // =====================================================================
+#ifdef GO1_VEL_STAMPS
+extern "C" int go1_vel_stamps(void* host, int reset) {
+  if (host && hipMemcpyFromSymbol(host, HIP_SYMBOL(g_vstamps), sizeof(g_vstamps), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return 1;
+  if (reset) {
+    static const unsigned long long z[2][16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_vstamps), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
 struct go1_vel_handle {
   go1_config cfg;
   go1_vel_config vcfg;
@@ -1025,6 +1191,12 @@ struct go1_vel_handle {
   double* d_cdf = nullptr;
   int32_t* d_cdf_ok = nullptr;
   uint8_t* d_mask = nullptr;  // reset_idx's env mask (stream-ordered reuse)
+  int32_t* d_adj_ptr = nullptr;  // neighbourhood table of the curriculum update (CSR over the bins)
+  int32_t* d_adj_idx = nullptr;
+  // the history shift's side stream and its two hand-off events (GO1_VEL_SHIFT_SIDE=0: the caller's stream)
+  hipStream_t s_shift = nullptr;
+  hipEvent_t ev_in = nullptr, ev_done = nullptr;
+  bool shift_side = true;
   go1_vel_state st;
   const float* env_origins = nullptr;
   bool bound = false;
@@ -1046,6 +1218,8 @@ static CArgs curriculum_args(go1_vel_handle* h) {
   memset(&K, 0, sizeof(K));
   K.st = h->st;
   K.grid = h->d_grid;
+  K.adj_ptr = h->d_adj_ptr;
+  K.adj_idx = h->d_adj_idx;
   K.cdf = h->d_cdf;
   K.cdf_ok = h->d_cdf_ok;
   K.n_envs = h->cfg.n_envs;
@@ -1095,9 +1269,40 @@ int go1_vel_create(const go1_config* cfg, const go1_vel_config* vel, const doubl
     go1_vel_destroy(h);
     return vfail(GO1_E_HIP, "go1_vel_create: hipMalloc failed");
   }
+  {
+    const char* side = getenv("GO1_VEL_SHIFT_SIDE");
+    h->shift_side = !(side && side[0] == '0');
+  }
+  if (h->shift_side && (hipStreamCreateWithFlags(&h->s_shift, hipStreamNonBlocking) != hipSuccess ||
+                        hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming) != hipSuccess ||
+                        hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming) != hipSuccess)) {
+    go1_vel_destroy(h);
+    return vfail(GO1_E_HIP, "go1_vel_create: side stream / events");
+  }
   VHIP_TRY(hipMemcpy(h->d_cfg, cfg, sizeof(go1_config), hipMemcpyHostToDevice));
   VHIP_TRY(hipMemcpy(h->d_vcfg, vel, sizeof(go1_vel_config), hipMemcpyHostToDevice));
   VHIP_TRY(hipMemcpy(h->d_grid, grid, gsz, hipMemcpyHostToDevice));
+  {  // get_local_bins (curriculum.py:123-133): cell j is adjacent to bin b when every key is within
+     // local_range -- the numpy comparisons grid[:, j] >= grid[:, b] - r and <= grid[:, b] + r in f64
+    const int nb = vel->n_bins;
+    std::vector<int32_t> ptr(nb + 1, 0), idx;
+    for (int b = 0; b < nb; ++b) {
+      for (int j = 0; j < nb; ++j) {
+        bool adj = true;
+        for (int k = 0; k < GO1_VEL_N_KEYS && adj; ++k) {
+          const double gb = grid[(size_t)k * nb + b], gj = grid[(size_t)k * nb + j], r = vel->local_range[k];
+          adj = gj >= gb - r && gj <= gb + r;
+        }
+        if (adj) idx.push_back(j);
+      }
+      ptr[b + 1] = (int32_t)idx.size();
+    }
+    if (idx.empty()) idx.push_back(0);
+    VHIP_TRY(hipMalloc(&h->d_adj_ptr, ptr.size() * sizeof(int32_t)));
+    VHIP_TRY(hipMalloc(&h->d_adj_idx, idx.size() * sizeof(int32_t)));
+    VHIP_TRY(hipMemcpy(h->d_adj_ptr, ptr.data(), ptr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    VHIP_TRY(hipMemcpy(h->d_adj_idx, idx.data(), idx.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   VHIP_TRY(hipMemset(h->d_cdf_ok, 0, GO1_VEL_N_CATEGORIES * sizeof(int32_t)));
   *out = h;
   return GO1_OK;
@@ -1170,6 +1375,25 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   K.a = *a;
   K.env_origins = h->env_origins;
   K.hist_w = GO1_VEL_NUM_OBS * h->vcfg.history_len;
+  CArgs C = curriculum_args(h);
+  C.hist_in = a->obs_history_in;
+  C.hist_out = a->obs_history_out;
+  C.hist_w = K.hist_w;
+  C.hist_aligned = C.hist_w % 4 == 0 && ((uintptr_t)C.hist_in % 16) == 0 && ((uintptr_t)C.hist_out % 16) == 0;
+  if (C.hist_in) {
+    // history shift: four 16-byte chunks per lane in flight, at most 8 workgroups per CU
+    const size_t chunks = (size_t)n * (size_t)((K.hist_w - GO1_VEL_NUM_OBS) / 4 + 64);
+    const int blocks = (int)std::min<size_t>(2048, std::max<size_t>(1, (chunks + 4 * SHIFT_THREADS - 1) / (4 * SHIFT_THREADS)));
+    hipStream_t ss = s;
+    if (h->shift_side) {  // after everything the caller queued before this step (hist_in's producer, hist_out's readers)
+      VHIP_TRY(hipEventRecord(h->ev_in, s));
+      VHIP_TRY(hipStreamWaitEvent(h->s_shift, h->ev_in, 0));
+      ss = h->s_shift;
+    }
+    hipLaunchKernelGGL(go1_vel_hist_shift_kernel, dim3(blocks), dim3(SHIFT_THREADS), 0, ss, C);
+    VHIP_TRY(hipGetLastError());
+    if (h->shift_side) VHIP_TRY(hipEventRecord(h->ev_done, h->s_shift));
+  }
   hipEvent_t e0 = (hipEvent_t)a->ev_begin, e1 = (hipEvent_t)a->ev_end;
   auto go = [&](auto kern) {
     if (e0 || e1) hipExtLaunchKernelGGL(kern, dim3(n / SEPB), dim3(TPB), 0, s, e0, e1, 0, h->d_cfg, h->d_vcfg, K);
@@ -1178,7 +1402,6 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   if (inj) go(go1_vel_step_kernel<true>);
   else go(go1_vel_step_kernel<false>);
   VHIP_TRY(hipGetLastError());
-  CArgs C = curriculum_args(h);
   C.seed = a->rng_seed;
   C.maskB = a->reset;
   C.UB = a->uniforms;
@@ -1191,12 +1414,9 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   C.time_out = a->time_out;
   C.extras_time_outs = a->extras_time_outs;
   C.obs = a->obs;
-  C.hist_in = a->obs_history_in;
-  C.hist_out = a->obs_history_out;
-  C.hist_w = K.hist_w;
-  const int shift_blocks = a->obs_history_in ? 1024 : 0;
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1 + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
   VHIP_TRY(hipGetLastError());
+  if (C.hist_in && h->shift_side) VHIP_TRY(hipStreamWaitEvent(s, h->ev_done, 0));  // obs_history_out complete
   return GO1_OK;
 }
 
@@ -1254,6 +1474,11 @@ int go1_vel_destroy(go1_vel_handle* h) {
   if (h->d_cdf) (void)hipFree(h->d_cdf);
   if (h->d_cdf_ok) (void)hipFree(h->d_cdf_ok);
   if (h->d_mask) (void)hipFree(h->d_mask);
+  if (h->d_adj_ptr) (void)hipFree(h->d_adj_ptr);
+  if (h->d_adj_idx) (void)hipFree(h->d_adj_idx);
+  if (h->s_shift) (void)hipStreamDestroy(h->s_shift);
+  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
+  if (h->ev_done) (void)hipEventDestroy(h->ev_done);
   delete h;
   return GO1_OK;
 }

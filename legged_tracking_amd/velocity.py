@@ -433,6 +433,10 @@ class VelocityTrackingEasyEnv:
         self._host_rng = np.random.default_rng(self.seed)
         self._rng_step = 0
         self._args = [None] * OUT_RING
+        self._args_grav = [None] * OUT_RING  # per output slot: the gravity versions / reward scales its args hold
+        self._args_rs = [None] * OUT_RING
+        self._grav_version = 0
+        self._gravity_interval_i = int(self._gravity_interval)
         self.extras = self._make_extras()
         self.kernel_events = deque()
         # the first step's interval resample (none unless episode lengths were set)
@@ -453,6 +457,7 @@ class VelocityTrackingEasyEnv:
             u = self._host_rng.random(3).astype(np.float32)
             self.gravities[:] = u * np.float32(hi - lo) + np.float32(lo)
         self._sim_gravity, self._gravity_vec = CF.gravity_state(self.gravities)
+        self._grav_version += 1
 
     @property
     def state(self):
@@ -560,20 +565,27 @@ class VelocityTrackingEasyEnv:
             args.episode_log_cap = self._log_cap
         # post_physics bookkeeping order (:120-121, :719-723): the step's gravity projection uses the vector
         # before this step's schedule, orientation_control the one after, the physics the sim gravity before
-        gvec, sgrav = self._gravity_vec.copy(), self._sim_gravity.copy()
+        # (_randomize_gravity replaces the arrays, so these references keep the values before it)
+        gvec, sgrav, vb = self._gravity_vec, self._sim_gravity, self._grav_version
         self.common_step_counter += 1
         c = self.common_step_counter
-        if c % int(self._gravity_interval) == 0:
+        gi = self._gravity_interval_i
+        if c % gi == 0:
             self._randomize_gravity()
-        if int(c - self._gravity_duration) % int(self._gravity_interval) == 0:
+        if int(c - self._gravity_duration) % gi == 0:
             self._randomize_gravity(np.zeros(3, np.float32))
         args.actions = a.data_ptr()
-        args.gravity_vec[:] = [float(x) for x in gvec]
-        args.gravity_vec_after[:] = [float(x) for x in self._gravity_vec]
-        args.sim_gravity[:] = [float(x) for x in sgrav]
-        rs = np.zeros(VA.GO1_VEL_MAX_TERMS, np.float32)
-        rs[:len(self.reward_names)] = [self.reward_scales[k] for k in self.reward_names]
-        args.reward_scales[:] = [float(x) for x in rs]
+        # the args of an output slot are rewritten only where they changed since that slot's last step
+        gkey = (vb, self._grav_version)
+        if self._args_grav[s] != gkey:
+            args.gravity_vec[:] = [float(x) for x in gvec]
+            args.gravity_vec_after[:] = [float(x) for x in self._gravity_vec]
+            args.sim_gravity[:] = [float(x) for x in sgrav]
+            self._args_grav[s] = gkey
+        rs = tuple(self.reward_scales[k] for k in self.reward_names)
+        if self._args_rs[s] != rs:
+            args.reward_scales[:] = [float(np.float32(x)) for x in rs] + [0.0] * (VA.GO1_VEL_MAX_TERMS - len(rs))
+            self._args_rs[s] = rs
         args.rng_seed, args.rng_step = self.seed, self._rng_step
         self._log_tag += 1
         args.episode_log_tag = self._log_tag

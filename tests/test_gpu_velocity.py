@@ -276,3 +276,26 @@ def test_vel_native_run_properties():
     assert "rew_total" in ep and "command_area_trot" in ep
     assert info["time_outs"].shape == (n,)
     env.env.close()
+
+
+def test_vel_runner_learns(tmp_path):
+    """scripts/train_velocity_tracking.py's loop (Runner.learn, ppo_cse/__init__.py) over the HIP velocity env:
+    rollout with the 30-deep history (2100 inputs: the policy runs on torch / hipBLASLt, the fused policy
+    kernel covers inputs up to 272), GAE and record kernels, PPO.update, checkpoints."""
+    from legged_tracking_amd import rollout as R
+    from legged_tracking_amd.env import HistoryWrapper
+    n = 512
+    env = HistoryWrapper(VEL.VelocityTrackingEasyEnv(sim_device=DEV, num_envs=n))
+    assert env.num_obs_history == 2100 and env.num_privileged_obs == 2
+    runner = R.Runner(env, device=DEV, save_dir=str(tmp_path))
+    assert runner.alg.fused is None  # 2100 history inputs: torch path for the policy
+    w0 = [p.detach().clone() for p in runner.alg.actor_critic.parameters()]
+    runner.learn(num_learning_iterations=2, init_at_random_ep_len=True)
+    torch.cuda.synchronize()
+    moved = sum(float((p.detach() - q).abs().max()) > 0 for p, q in zip(runner.alg.actor_critic.parameters(), w0))
+    assert moved > 0
+    for p in runner.alg.actor_critic.parameters():
+        assert torch.isfinite(p).all()
+    assert (tmp_path / "ac_weights.pt").exists() and (tmp_path / "body_latest.jit").exists()
+    assert runner.tot_timesteps == 2 * runner.num_steps_per_env * n
+    env.env.close()

@@ -1,6 +1,6 @@
 """Host-side cost of the env-only VecEnv.step loop (bench.py's headline loop), GPU box.
 
-  python tools/env_host_prof.py [steps]
+  python tools/env_host_prof.py [steps] [--velocity]   (--velocity: HistoryWrapper(VelocityTrackingEasyEnv))
 
 Prints the loop's wall time per step, the host enqueue time per step (the loop with the
 GPU kept busy by a long queue: time until the Python loop returns), and a cProfile of
@@ -18,11 +18,17 @@ import bench  # noqa: E402
 
 
 def main():
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    steps = int(args[0]) if args else 512
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     n = 4096
-    env = bench.make_env(n, 0, 1, dev)
+    if "--velocity" in sys.argv:
+        from legged_tracking_amd import env as E, velocity as VEL
+        env = E.HistoryWrapper(VEL.VelocityTrackingEasyEnv(sim_device=str(dev), num_envs=n, seed=11))
+        env.close = env.env.close
+    else:
+        env = bench.make_env(n, 0, 1, dev)
     env.reset()
     ring = torch.randn((64, n, 12), device=dev)
     for k in range(64):
