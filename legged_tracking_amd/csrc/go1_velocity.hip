@@ -7,11 +7,10 @@
 //     clock (_step_contact_targets :844-923), DR (:714-717), terminations (:156-166), the CoRL reward
 //     terms and command sums (:281-318, go1_gym/envs/rewards/corl_rewards.py), reset_idx's state part
 //     (:168-257), observations (:320-509), the epilogue (:144-149) and the appended obs_history row.
-//   go1_vel_curriculum_kernel: one workgroup runs _resample_commands (:728-842) for the envs the step reset
+//   go1_vel_curriculum_kernel: workgroup 0 runs _resample_commands (:728-842) for the envs the step reset
 //     (RewardThresholdCurriculum.update, Curriculum.sample: go1_gym/envs/base/curriculum.py) and patches
-//     their observed commands, then the interval resample of the next step ahead of time.
-//   go1_vel_hist_shift_kernel, on the handle's side stream beside the two: the history shift
-//     (obs_history[:, 70:] -> the new buffer).
+//     their observed commands, then the interval resample of the next step ahead of time; the other
+//     workgroups shift the history (obs_history[:, 70:] -> the new buffer).
 // Lane layout of the step kernel as in go1_step.hip: 16 lanes per env = 4 legs x 4 roles, four envs per
 // one-wave block.  Post-physics arithmetic is f32 with contraction off in torch's operation order, the
 // transcendentals of the gait clock and the rewards via f64 (correctly rounded f32 but for rare double
@@ -857,9 +856,73 @@ __device__ double np_pairwise_sum(const double* a, int n) {
 
 __device__ __forceinline__ float remainder1(float a) { return remainder_f(a, 1.0f); }
 
+// LDS of workgroup 0 (one allocation for the launch)
+struct CkShared {
+  int hist[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // success count per (category, bin)
+  double p[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // per category: the cdf the sampling searches
+  int list[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // distinct (category, bin) success pairs
+  int inc[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];   // +0.2 steps per weight cell
+  int sel[2][CK_SEL_CAP];                             // env_ids of the B and the A resample
+  int cnt[4];                                         // |sel B|, |sel A|, |list|, spare
+  int dirty[GO1_VEL_N_CATEGORIES];                    // weights changed in this phase
+  int pvalid[GO1_VEL_N_CATEGORIES];                   // p holds the cdf of the current weights
+};
+
+// The launch is latency-bound: a handful of envs per phase behind a chain of barrier-separated
+// sections, and a barrier waits out every memory access in flight.  So each section issues all the
+// memory reads it can at once: the prologue loads both phases' selection flags and the cached cdfs in
+// one round trip; a phase then costs the success counts (one round trip), the weight update (when some
+// env succeeded), the cdf of changed weights, and the sampling (commands and grid cells together).
+__device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
+  const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
+  for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.hist[i] = 0;
+  if (tid < 4) S.cnt[tid] = 0;
+  if (tid < GO1_VEL_N_CATEGORIES) S.dirty[tid] = 0;
+  __syncthreads();
+  // the cached cdfs (wave c: category c), whether or not a phase will need them
+  const int wv = tid >> 6, ln = tid & 63;
+  double t[GO1_VEL_MAX_BINS / 64];
+  int ok = 0;
+  if (wv < GO1_VEL_N_CATEGORIES) {
+    const double* g = K.cdf + (size_t)wv * nb;
+    ok = K.cdf_ok[wv];
+#pragma unroll
+    for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? g[ln + 64 * i] : 0.0;
+  }
+  // env_ids of both phases, compacted (the flags of CK_BATCH envs per thread loaded before any is tested);
+  // beyond CK_SEL_CAP selected envs (a full reset) a phase scans the flags again instead
+  for (int e0 = 0; e0 < n; e0 += CK_THREADS * CK_BATCH) {
+    bool sb[CK_BATCH], sa[CK_BATCH];
+#pragma unroll
+    for (int k = 0; k < CK_BATCH; ++k) {
+      const int e = e0 + k * CK_THREADS + tid;
+      sb[k] = K.maskB && e < n && K.maskB[e] != 0;
+      sa[k] = K.doA && e < n && (K.st.episode_length[e] + 1) % R == 0;
+    }
+#pragma unroll
+    for (int k = 0; k < CK_BATCH; ++k) {
+      if (sb[k]) {
+        const int slot = atomicAdd(&S.cnt[0], 1);
+        if (slot < CK_SEL_CAP) S.sel[0][slot] = e0 + k * CK_THREADS + tid;
+      }
+      if (sa[k]) {
+        const int slot = atomicAdd(&S.cnt[1], 1);
+        if (slot < CK_SEL_CAP) S.sel[1][slot] = e0 + k * CK_THREADS + tid;
+      }
+    }
+  }
+  if (wv < GO1_VEL_N_CATEGORIES) {
+    double* p = S.p + (size_t)wv * GO1_VEL_MAX_BINS;
+#pragma unroll
+    for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
+      if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
+    if (ln == 0) S.pvalid[wv] = ok;
+  }
+  __syncthreads();
+}
+
 // One resample (_resample_commands :728-842) of kind B (mask) or A (interval), by the whole workgroup.
-__device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs& K, bool kindB, int* s_hist,
-                               int* s_list, int* s_inc, double* s_p, int* s_sel, int* s_cnt, int* s_dirty) {
+__device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S) {
   const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
   const go1_vel_state& st = K.st;
   const float* U = kindB ? K.UB : K.UA;
@@ -876,35 +939,14 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
   auto selected = [&](int e) {
     return kindB ? K.maskB[e] != 0 : ((st.episode_length[e] + 1) % R == 0);
   };
-  for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) s_hist[i] = 0;
-  if (tid == 0) { s_cnt[0] = 0; s_cnt[1] = 0; }
-  if (tid < GO1_VEL_N_CATEGORIES) s_dirty[tid] = 0;
-  __syncthreads();
-  // ---- env_ids: the selected envs, compacted into s_sel (the flags of CK_BATCH envs per thread are
-  // loaded before any is tested, so the scan costs one memory latency per CK_BATCH * CK_THREADS envs);
-  // beyond CK_SEL_CAP selected envs (a full reset) the loops below scan the flags again instead
-  for (int e0 = 0; e0 < n; e0 += CK_THREADS * CK_BATCH) {
-    bool sv[CK_BATCH];
-#pragma unroll
-    for (int k = 0; k < CK_BATCH; ++k) {
-      const int e = e0 + k * CK_THREADS + tid;
-      sv[k] = e < n && selected(e);
-    }
-#pragma unroll
-    for (int k = 0; k < CK_BATCH; ++k)
-      if (sv[k]) {
-        const int slot = atomicAdd(s_cnt, 1);
-        if (slot < CK_SEL_CAP) s_sel[slot] = e0 + k * CK_THREADS + tid;
-      }
-  }
-  __syncthreads();
+  const int count = S.cnt[ph];
+  const int* sel = S.sel[ph];
   VSTAMP(ph, 0, t0);
-  const int count = s_cnt[0];
-  if (count == 0) return;
-  VSTAMP(ph, 15, t0);  // len(env_ids) == 0 (:730): nothing, not even the time-out rebinding
+  if (count == 0) return;  // len(env_ids) == 0 (:730): nothing, not even the time-out rebinding
+  VSTAMP(ph, 15, t0);
   auto for_selected = [&](auto&& fn) {
     if (count <= CK_SEL_CAP) {
-      for (int i = tid; i < count; i += CK_THREADS) fn(s_sel[i]);
+      for (int i = tid; i < count; i += CK_THREADS) fn(sel[i]);
     } else {
       for (int e = tid; e < n; e += CK_THREADS)
         if (selected(e)) fn(e);
@@ -920,104 +962,105 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
       ok = ok && (st.command_sums[(size_t)e * NC + v->task_slot[k]] / v->curriculum_ep_len > v->task_threshold[k]);
     const int b = st.command_bins[e];
     if (ok && b >= 0 && b < nb) {
-      if (atomicAdd(&s_hist[cat * nb + b], 1) == 0) {
-        const int slot = atomicAdd(s_cnt + 1, 1);
-        s_list[slot] = cat * nb + b;  // at most GO1_VEL_N_CATEGORIES * nb distinct pairs
+      if (atomicAdd(&S.hist[cat * nb + b], 1) == 0) {
+        const int slot = atomicAdd(&S.cnt[2], 1);
+        S.list[slot] = cat * nb + b;  // at most GO1_VEL_N_CATEGORIES * nb distinct pairs
       }
     }
   });
-  __syncthreads();
-  VSTAMP(ph, 1, t0);
-  const int n_list = s_cnt[1];
   if (kindB && K.extras_time_outs)
     for (int e = tid; e < n; e += CK_THREADS) K.extras_time_outs[e] = K.time_out[e];
+  __syncthreads();
+  VSTAMP(ph, 1, t0);
+  const int n_list = S.cnt[2];
   // weights: cell j of category c gets +0.2 (clipped) once if it was a success bin and once per success
   // env whose bin's neighbourhood holds it -- a sequence of identical clip(w + 0.2, 0, 1) steps, so the
   // count decides the result whatever the order.  Neighbourhoods come from the handle's table
   // (get_local_bins, curriculum.py:123-133, evaluated on the host in the same f64 comparisons).
   if (n_list > 0) {
-    for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) s_inc[i] = 0;
+    for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.inc[i] = 0;
     __syncthreads();
     for (int l = tid; l < n_list; l += CK_THREADS) {
-      const int cb = s_list[l], cat = cb / nb, b = cb % nb, h = s_hist[cb];
-      atomicAdd(&s_inc[cb], 1);  // weights[bin_inds[is_success]] += 0.2 (once per distinct bin)
-      for (int q = K.adj_ptr[b]; q < K.adj_ptr[b + 1]; ++q) atomicAdd(&s_inc[cat * nb + K.adj_idx[q]], h);
+      const int cb = S.list[l], cat = cb / nb, b = cb % nb, h = S.hist[cb];
+      atomicAdd(&S.inc[cb], 1);  // weights[bin_inds[is_success]] += 0.2 (once per distinct bin)
+      const int q0 = K.adj_ptr[b], q1 = K.adj_ptr[b + 1];
+      for (int q = q0; q < q1; q += 8) {  // eight neighbour indices in flight at a time
+        int j[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) j[u] = q + u < q1 ? K.adj_idx[q + u] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (j[u] >= 0) atomicAdd(&S.inc[cat * nb + j[u]], h);
+      }
     }
     __syncthreads();
     for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
-      const int k = s_inc[i];
+      const int k = S.inc[i];
       if (k > 0) {
         double w = st.curriculum_weights[i];
         for (int t = 0; t < k; ++t) w = fmin(fmax(w + 0.2, 0.0), 1.0);
         st.curriculum_weights[i] = w;
-        s_dirty[i / nb] = 1;
+        S.dirty[i / nb] = 1;
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
   VSTAMP(ph, 2, t0);
   // ---- numpy rng.choice(p = w / w.sum()): cdf = cumsum(p) / cdf[-1], wave c for category c, in LDS
-  // (s_p); a category whose weights did not change reloads the cdf the handle keeps from its last
-  // computation.  The sampling below searches s_p.
+  // (S.p), recomputed where the weights changed (or no cdf is cached), also into the handle's cache
   {
     const int wv = tid >> 6, ln = tid & 63;
-    if (wv < GO1_VEL_N_CATEGORIES) {
-      double* p = s_p + (size_t)wv * GO1_VEL_MAX_BINS;
-      if (s_dirty[wv] || !K.cdf_ok[wv]) {
-        const double* w = st.curriculum_weights + (size_t)wv * nb;
-        double t[GO1_VEL_MAX_BINS / 64];  // all of the lane's loads in flight before the LDS stores
+    if (wv < GO1_VEL_N_CATEGORIES && (S.dirty[wv] || !S.pvalid[wv])) {
+      double* p = S.p + (size_t)wv * GO1_VEL_MAX_BINS;
+      const double* w = st.curriculum_weights + (size_t)wv * nb;
+      double t[GO1_VEL_MAX_BINS / 64];  // all of the lane's loads in flight before the LDS stores
 #pragma unroll
-        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? w[ln + 64 * i] : 0.0;
+      for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? w[ln + 64 * i] : 0.0;
 #pragma unroll
-        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
-          if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double s = 0.0;
-        if (ln == 0) s = np_pairwise_sum<4>(p, nb);
-        s = __shfl(s, 0);
-        for (int j = ln; j < nb; j += 64) p[j] = p[j] / s;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (ln == 0) {  // numpy's sequential cumsum: the adds are a dependent chain, the LDS reads of a
-                        // batch are issued ahead of it (in place, one read-write per element, it would wait
-                        // out the LDS latency at every element)
-          double acc = 0.0;
-          for (int j0 = 0; j0 < nb; j0 += 32) {
-            double t[32];
+      for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
+        if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double s = 0.0;
+      if (ln == 0) s = np_pairwise_sum<4>(p, nb);
+      s = __shfl(s, 0);
+      for (int j = ln; j < nb; j += 64) p[j] = p[j] / s;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ln == 0) {  // numpy's sequential cumsum: the adds are a dependent chain, the LDS reads of a
+                      // batch are issued ahead of it (in place, one read-write per element, it would wait
+                      // out the LDS latency at every element)
+        double acc = 0.0;
+        for (int j0 = 0; j0 < nb; j0 += 32) {
+          double u[32];
 #pragma unroll
-            for (int i = 0; i < 32; ++i) t[i] = j0 + i < nb ? p[j0 + i] : 0.0;
+          for (int i = 0; i < 32; ++i) u[i] = j0 + i < nb ? p[j0 + i] : 0.0;
 #pragma unroll
-            for (int i = 0; i < 32; ++i) { acc += t[i]; t[i] = acc; }
+          for (int i = 0; i < 32; ++i) { acc += u[i]; u[i] = acc; }
 #pragma unroll
-            for (int i = 0; i < 32; ++i)
-              if (j0 + i < nb) p[j0 + i] = t[i];
-          }
+          for (int i = 0; i < 32; ++i)
+            if (j0 + i < nb) p[j0 + i] = u[i];
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const double last = p[nb - 1];
-        for (int j = ln; j < nb; j += 64) {
-          const double c = p[j] / last;
-          p[j] = c;
-          K.cdf[(size_t)wv * nb + j] = c;
-        }
-        if (ln == 0) K.cdf_ok[wv] = 1;
-#ifdef GO1_VEL_STAMPS
-        if (ln == 0) atomicAdd(&g_vstamps[kindB ? 0 : 1][14], 1ull);
-#endif
-      } else {
-        const double* g = K.cdf + (size_t)wv * nb;
-        double t[GO1_VEL_MAX_BINS / 64];
-#pragma unroll
-        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? g[ln + 64 * i] : 0.0;
-#pragma unroll
-        for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
-          if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double last = p[nb - 1];
+      for (int j = ln; j < nb; j += 64) {
+        const double c = p[j] / last;
+        p[j] = c;
+        K.cdf[(size_t)wv * nb + j] = c;
+      }
+      if (ln == 0) {
+        K.cdf_ok[wv] = 1;
+        S.pvalid[wv] = 1;
+        S.dirty[wv] = 0;
+      }
+#ifdef GO1_VEL_STAMPS
+      if (ln == 0) atomicAdd(&g_vstamps[kindB ? 0 : 1][14], 1ull);
+#endif
     }
   }
   __syncthreads();
@@ -1025,7 +1068,8 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
   // ---- new category, cell and command per env (:759-842), 16 lanes per env: lane k < 15 draws and
   // finishes command k (the gait rules and binary phases act per command; only the small-command rule
   // pairs commands 0 and 1), lane 15 draws the choice and searches the cdf.  One Philox evaluation per
-  // lane instead of ~30 in sequence on one thread.
+  // lane instead of ~30 in sequence on one thread; the env's old commands are loaded before the search,
+  // so they and the grid cells share one memory round trip.
   {
     const int sub = tid & 15, grp = tid >> 4;
     const bool listed = count <= CK_SEL_CAP;
@@ -1034,23 +1078,23 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
       const int i = i0 + grp;
       int e = -1;
       if (listed) {
-        if (i < count) e = s_sel[i];
+        if (i < count) e = sel[i];
       } else if (i < n && selected(i)) {
         e = i;
       }
       if (e < 0) continue;  // uniform over the env's 16 lanes
       const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
       const RngD rngd = {UD, K.seed, step, e, e + K.env_id_offset};
+      float cmd = sub < GO1_VEL_NUM_COMMANDS ? st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] : 0.0f;
       const float uc = rng(ucat);
       int cat = -1;
       for (int c = 0; c < GO1_VEL_N_CATEGORIES; ++c)
         if ((float)(0.25 * c) <= uc && uc < (float)(0.25 * (c + 1))) cat = c;
-      float cmd = sub < GO1_VEL_NUM_COMMANDS ? st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] : 0.0f;
       if (cat >= 0) {
         const double u = rngd(sub < GO1_VEL_NUM_COMMANDS ? dch + 1 + sub : dch);
         int idx = 0;
         if (sub == 15) {
-          const double* cdf = s_p + (size_t)cat * GO1_VEL_MAX_BINS;
+          const double* cdf = S.p + (size_t)cat * GO1_VEL_MAX_BINS;
           int lo = 0, hi = nb;  // searchsorted(cdf, u, side='right'): first j with cdf[j] > u
           while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -1090,20 +1134,21 @@ __device__ void resample_phase(VCfg* v, const go1_vel_config* v_gen, const CArgs
       }
     }
   }
+  // ready for the next phase: success counts and the pair list cleared
+  for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.hist[i] = 0;
+  if (tid == 0) S.cnt[2] = 0;
   __syncthreads();
   VSTAMP(ph, 4, t0);
 }
 
-// HistoryWrapper.step's shift (history_wrapper.py:22): new[:, :W - 70] = old[:, 70:].  Its own launch, on
-// the handle's side stream beside the step kernel (nothing either reads or writes overlaps): a pure
-// HBM stream of 2 x 33 MB at 4096 envs x 30 observations, which in the curriculum launch slowed that
-// launch's latency-bound workgroup 0 through the memory system.
-#define SHIFT_THREADS 256
-__global__ __launch_bounds__(SHIFT_THREADS) void go1_vel_hist_shift_kernel(CArgs K) {
+// HistoryWrapper.step's shift (history_wrapper.py:22): new[:, :W - 70] = old[:, 70:], by workgroups 1.. of
+// the curriculum launch (g0: the thread's index among them, G: their thread count).  A pure HBM stream of
+// 2 x 33 MB at 4096 envs x 30 observations.  Measured alternative, not kept: the shift as its own kernel on
+// a side stream beside the step kernel -- it overlapped (27 us under the 47 us step kernel), but the two
+// cross-stream hand-offs per step left ~11 us of idle GPU between steps: 70.6 against 69.1 us per step.
+__device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
   if (!K.hist_in || !K.hist_out) return;
   const int W = K.hist_w, D = W - GO1_VEL_NUM_OBS;
-  const size_t G = (size_t)gridDim.x * SHIFT_THREADS;
-  const size_t g0 = (size_t)blockIdx.x * SHIFT_THREADS + threadIdx.x;
   if (K.hist_aligned) {
     // 16-byte chunks: rows are 16-byte aligned (W % 4 == 0), the source starts 70 = 4 x 17 + 2 floats in,
     // so dest chunk i = (z, w) of aligned source chunk 17 + i and (x, y) of chunk 18 + i, which the next
@@ -1158,14 +1203,14 @@ __global__ __launch_bounds__(SHIFT_THREADS) void go1_vel_hist_shift_kernel(CArgs
 __global__ __launch_bounds__(CK_THREADS) void go1_vel_curriculum_kernel(const go1_vel_config* __restrict__ v_gen,
                                                                         CArgs K) {
   VCfg* __restrict__ v = (VCfg*)v_gen;
-  __shared__ int s_hist[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
-  __shared__ double s_p[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
-  __shared__ int s_list[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
-  __shared__ int s_inc[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];
-  __shared__ int s_sel[CK_SEL_CAP];
-  __shared__ int s_cnt[2], s_dirty[GO1_VEL_N_CATEGORIES];
-  if (K.maskB) resample_phase(v, v_gen, K, true, s_hist, s_list, s_inc, s_p, s_sel, s_cnt, s_dirty);
-  if (K.doA) resample_phase(v, v_gen, K, false, s_hist, s_list, s_inc, s_p, s_sel, s_cnt, s_dirty);
+  if (blockIdx.x > 0) {
+    hist_shift(K, (size_t)(blockIdx.x - 1) * CK_THREADS + threadIdx.x, (size_t)(gridDim.x - 1) * CK_THREADS);
+    return;
+  }
+  __shared__ CkShared S;
+  resample_prologue(v, K, S);
+  if (K.maskB) resample_phase(v, K, true, S);
+  if (K.doA) resample_phase(v, K, false, S);
 }
 
 // =====================================================================
@@ -1193,10 +1238,6 @@ struct go1_vel_handle {
   uint8_t* d_mask = nullptr;  // reset_idx's env mask (stream-ordered reuse)
   int32_t* d_adj_ptr = nullptr;  // neighbourhood table of the curriculum update (CSR over the bins)
   int32_t* d_adj_idx = nullptr;
-  // the history shift's side stream and its two hand-off events (GO1_VEL_SHIFT_SIDE=0: the caller's stream)
-  hipStream_t s_shift = nullptr;
-  hipEvent_t ev_in = nullptr, ev_done = nullptr;
-  bool shift_side = true;
   go1_vel_state st;
   const float* env_origins = nullptr;
   bool bound = false;
@@ -1269,16 +1310,7 @@ int go1_vel_create(const go1_config* cfg, const go1_vel_config* vel, const doubl
     go1_vel_destroy(h);
     return vfail(GO1_E_HIP, "go1_vel_create: hipMalloc failed");
   }
-  {
-    const char* side = getenv("GO1_VEL_SHIFT_SIDE");
-    h->shift_side = !(side && side[0] == '0');
-  }
-  if (h->shift_side && (hipStreamCreateWithFlags(&h->s_shift, hipStreamNonBlocking) != hipSuccess ||
-                        hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming) != hipSuccess ||
-                        hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming) != hipSuccess)) {
-    go1_vel_destroy(h);
-    return vfail(GO1_E_HIP, "go1_vel_create: side stream / events");
-  }
+
   VHIP_TRY(hipMemcpy(h->d_cfg, cfg, sizeof(go1_config), hipMemcpyHostToDevice));
   VHIP_TRY(hipMemcpy(h->d_vcfg, vel, sizeof(go1_vel_config), hipMemcpyHostToDevice));
   VHIP_TRY(hipMemcpy(h->d_grid, grid, gsz, hipMemcpyHostToDevice));
@@ -1380,20 +1412,6 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   C.hist_out = a->obs_history_out;
   C.hist_w = K.hist_w;
   C.hist_aligned = C.hist_w % 4 == 0 && ((uintptr_t)C.hist_in % 16) == 0 && ((uintptr_t)C.hist_out % 16) == 0;
-  if (C.hist_in) {
-    // history shift: four 16-byte chunks per lane in flight, at most 8 workgroups per CU
-    const size_t chunks = (size_t)n * (size_t)((K.hist_w - GO1_VEL_NUM_OBS) / 4 + 64);
-    const int blocks = (int)std::min<size_t>(2048, std::max<size_t>(1, (chunks + 4 * SHIFT_THREADS - 1) / (4 * SHIFT_THREADS)));
-    hipStream_t ss = s;
-    if (h->shift_side) {  // after everything the caller queued before this step (hist_in's producer, hist_out's readers)
-      VHIP_TRY(hipEventRecord(h->ev_in, s));
-      VHIP_TRY(hipStreamWaitEvent(h->s_shift, h->ev_in, 0));
-      ss = h->s_shift;
-    }
-    hipLaunchKernelGGL(go1_vel_hist_shift_kernel, dim3(blocks), dim3(SHIFT_THREADS), 0, ss, C);
-    VHIP_TRY(hipGetLastError());
-    if (h->shift_side) VHIP_TRY(hipEventRecord(h->ev_done, h->s_shift));
-  }
   hipEvent_t e0 = (hipEvent_t)a->ev_begin, e1 = (hipEvent_t)a->ev_end;
   auto go = [&](auto kern) {
     if (e0 || e1) hipExtLaunchKernelGGL(kern, dim3(n / SEPB), dim3(TPB), 0, s, e0, e1, 0, h->d_cfg, h->d_vcfg, K);
@@ -1414,9 +1432,13 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   C.time_out = a->time_out;
   C.extras_time_outs = a->extras_time_outs;
   C.obs = a->obs;
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
+  // workgroups 1..: the history shift, one per remaining CU (the launch's LDS allows one workgroup per CU),
+  // four 16-byte chunks in flight per lane; fewer for small batches
+  const size_t chunks = (size_t)n * (size_t)((K.hist_w - GO1_VEL_NUM_OBS) / 4 + 64);
+  const int shift_blocks =
+      C.hist_in ? (int)std::min<size_t>(255, std::max<size_t>(1, (chunks + 4 * CK_THREADS - 1) / (4 * CK_THREADS))) : 0;
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1 + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
   VHIP_TRY(hipGetLastError());
-  if (C.hist_in && h->shift_side) VHIP_TRY(hipStreamWaitEvent(s, h->ev_done, 0));  // obs_history_out complete
   return GO1_OK;
 }
 
@@ -1476,9 +1498,6 @@ int go1_vel_destroy(go1_vel_handle* h) {
   if (h->d_mask) (void)hipFree(h->d_mask);
   if (h->d_adj_ptr) (void)hipFree(h->d_adj_ptr);
   if (h->d_adj_idx) (void)hipFree(h->d_adj_idx);
-  if (h->s_shift) (void)hipStreamDestroy(h->s_shift);
-  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
-  if (h->ev_done) (void)hipEventDestroy(h->ev_done);
   delete h;
   return GO1_OK;
 }

@@ -670,6 +670,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
   __shared__ Act<256> h2[2];            // layer-2 outputs
   __shared__ float scr[2][8][16][16];   // [env tile] K-split partials
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  PSTAMP(0);
   const int q = lane >> 4, c = lane & 15;
   const int nblk = (P.n_envs + SE - 1) / SE;
   const bool critic = (int)blockIdx.x >= nblk;
@@ -689,11 +690,13 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
     act_store1(e < 16 ? vx[0][0] : vx[1][0], k, e & 15, v, &s_ovf);  // no runtime index into vx (private memory)
   }
   __syncthreads();
+  PSTAMP(1);
   const PolicyLayer* Ls = P.layers;
   if (!critic) {
     // adaptation module 261 -> 256 (xin rows >= hist_dim are still zero)
     policy_tiles_e<1, 1, 2, PIN / 16, 8>(Ls + 0, vx, wave, PW, v1, true, lane, &s_ovf);
     __syncthreads();
+    PSTAMP(2);
     {  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7
       const int t = wave & 7, half = wave >> 3;
       const ActV src[2] = {v1[0][0], v1[1][0]};
@@ -718,6 +721,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
       }
     }
     __syncthreads();
+    PSTAMP(3);
     {  // 128 -> num_priv (the latent): one K group per wave (8 waves), partials summed by waves 0 / 1
       if (wave < 8) {
         const ActV src[2] = {v2[0][0], v2[1][0]};
@@ -746,15 +750,23 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
       }
     }
     __syncthreads();
+    PSTAMP(4);
+  } else {
+    PSTAMP(2);
+    PSTAMP(3);
+    PSTAMP(4);
   }
   // actor (Ls 3-6) or critic (Ls 7-10), layer by layer
   const PolicyLayer* LN = Ls + (critic ? 7 : 3);
   policy_tiles_e<2, 1, 2, PIN / 16, GO1_SPLIT_D1>(LN + 0, vx, wave, PW, v1, true, lane, &s_ovf);  // 512
   __syncthreads();
+  PSTAMP(5);
   policy_tiles_e<1, 1, 2, 512 / 16, GO1_SPLIT_D2>(LN + 1, v1, wave, PW, v2, true, lane, &s_ovf);  // 256
   __syncthreads();
+  PSTAMP(6);
   if (wave < 8) policy_tiles_e<1, 1, 2, 256 / 16, 8>(LN + 2, v2, wave, 8, v1, true, lane, &s_ovf);  // 128 -> h1
   __syncthreads();
+  PSTAMP(7);
   if (wave < 8) {  // 128 -> num_actions / 1: one K group per wave, partials through LDS
     const ActV src[2] = {v1[0][0], v1[1][0]};
     f4_t part[2];
@@ -818,6 +830,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
       P.value[e0 + e] = acc[0];
     }
   }
+  PSTAMP(8);
   __syncthreads();
   if (s_ovf) policy_fallback(P, e0, ne, !critic, critic, reinterpret_cast<float*>(&h1[0]));
 }

@@ -1,7 +1,7 @@
 """Phase timing of the policy kernel (diagnostic build with -DGO1_POLICY_STAMPS).
 
   local:  hipcc ... -DGO1_POLICY_STAMPS -o legged_tracking_amd/_build/libgo1_rollout_stamps.so rollout.hip
-  gpurun: python tools/policy_stamps.py
+  gpurun: python tools/policy_stamps.py [--variant 1]   (default: variant 0, policy_kernel_split)
 
 Phases end at the kernel's barriers: 1 input staging, 2 adaptation L1, 3 adaptation L2,
 4 adaptation L3 (latent), 5 actor/critic L1, 6 L2, 7 L3, 8 output layer + sampling.
@@ -36,17 +36,29 @@ def main():
         for _ in range(5):
             alg.act(obs, priv, obs)
     torch.cuda.synchronize()
+    variant = int(sys.argv[sys.argv.index("--variant") + 1]) if "--variant" in sys.argv else 0
+    alg.fused.variant = variant
+    with torch.inference_mode():
+        for _ in range(5):
+            alg.act(obs, priv, obs)
+    torch.cuda.synchronize()
     lib = alg.fused.lib
     buf = np.zeros(512 * 16 * 12, np.uint64)
     assert lib.go1_policy_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
-    t = buf.reshape(512, 16, 12).astype(np.int64)[:256, :, :9]
-    t = t - t[:, :, :1].min(axis=1, keepdims=True)
-    ends = t.max(axis=1)  # (wg, 9): phase end = last wave through the barrier
-    d = np.diff(ends, axis=1).mean(axis=0)
-    life = ends[:, 8].mean()
-    print(f"workgroups {t.shape[0]}; mean lifetime {life:.0f} cycles")
-    for nm, v in zip(NAMES, d):
-        print(f"{nm:14s} {v:9.0f} {v / life:7.1%}")
+    t_all = buf.reshape(512, 16, 12).astype(np.int64)[:256, :, :9]
+    groups = [("all", t_all)] if variant else [("actor workgroups", t_all[:128]), ("critic workgroups", t_all[128:])]
+    for label, t in groups:
+        t = t - t[:, :, :1].min(axis=1, keepdims=True)
+        ends = t.max(axis=1)  # (wg, 9): phase end = last wave through the barrier
+        d = np.diff(ends, axis=1).mean(axis=0)
+        life = ends[:, 8].mean()
+        print(f"{label}: {t.shape[0]}; mean lifetime {life:.0f} cycles")
+        for nm, v in zip(NAMES, d):
+            print(f"  {nm:14s} {v:9.0f} {v / life:7.1%}")
+    # spread of the workgroups' start times (launch ramp) and end times
+    st = t_all[:, :, 0].min(axis=1)
+    en = t_all[:, :, 8].max(axis=1)
+    print(f"start spread {np.ptp(st)} cycles, end spread {np.ptp(en)}, first start -> last end {en.max() - st.min()}")
 
 
 if __name__ == "__main__":
