@@ -296,7 +296,7 @@ def velocity_rate(n, dev, steps, warmup):
             "envs_at_episode_start": resets}
 
 
-def learn_rate(n, dev, iters=4, warmup=1):
+def learn_rate(n, dev, iters=4, warmup=1, velocity=False):
     """The whole training loop, as the reference's wandb train/fps measures it (ppo_cse/__init__.py:184:
     (it + 1) x num_envs x num_steps_per_env / elapsed): Runner iterations of rollout (24 x [PPO.act +
     VecEnv.step + record]), compute_returns (GAE) and PPO.update (5 epochs x 4 mini-batches, Adam, the
@@ -304,7 +304,12 @@ def learn_rate(n, dev, iters=4, warmup=1):
     writes (every 400 iterations in the reference) are outside the timed iterations."""
     import torch
     from legged_tracking_amd import rollout as R
-    env = make_env(n, 0, 1, dev)
+    if velocity:  # configs[1]: scripts/train_velocity_tracking.py's env (30-deep history: torch policy path)
+        from legged_tracking_amd import env as E, velocity as VEL
+        env = E.HistoryWrapper(VEL.VelocityTrackingEasyEnv(sim_device=str(dev), num_envs=n, seed=11))
+        env.close = env.env.close
+    else:
+        env = make_env(n, 0, 1, dev)
     runner = R.Runner(env, device=dev, save_dir=None)
     alg, T = runner.alg, runner.num_steps_per_env
     od = env.get_observations()
@@ -332,6 +337,8 @@ def learn_rate(n, dev, iters=4, warmup=1):
     it_s = sum(split.values()) / iters
     return {"value": n * T / it_s, "unit": "env-steps/s", "ms_per_iteration": it_s * 1e3, "iterations": iters,
             "split_ms_per_iteration": {k: v / iters * 1e3 for k, v in split.items()},
+            "env": "VelocityTrackingEasyEnv (configs[1])" if velocity else "TrajectoryTrackingEnv (configs[2])",
+            "fused_policy": runner.alg.fused is not None,
             "what": f"Runner iteration at {n} envs: {T} rollout steps + GAE + PPO.update "
                     "(5 epochs x 4 mini-batches), env-steps/s as ppo_cse/__init__.py:184 computes train/fps; "
                     "BASELINE.md derives ~8,960 (A100) and ~27,300 (A40) whole-loop env-steps/s from the "
@@ -416,6 +423,8 @@ def main():
     ap.add_argument("--no-velocity", action="store_true", help="skip the configs[1] velocity-tracking leg")
     ap.add_argument("--velocity-only", action="store_true", help="profile helper: time only the velocity env")
     ap.add_argument("--learn-only", action="store_true", help="profile helper: time only Runner iterations")
+    ap.add_argument("--velocity-learn", action="store_true",
+                    help="profile helper: time Runner iterations over the configs[1] velocity env")
     ap.add_argument("--rollout-only", action="store_true", help="profile helper: time only the rollout loop")
     ap.add_argument("--event-every", type=int, default=4,
                     help="record the HIP event pair around every k-th step kernel of the timed loop")
@@ -454,9 +463,9 @@ def main():
         torch.cuda.set_device(dev)
         print(json.dumps(velocity_rate(args.envs_per_gpu, dev, args.steps, args.warmup)))
         return
-    if args.learn_only:
+    if args.learn_only or args.velocity_learn:
         torch.cuda.set_device(dev)
-        print(json.dumps(learn_rate(args.envs_per_gpu, dev)))
+        print(json.dumps(learn_rate(args.envs_per_gpu, dev, velocity=args.velocity_learn)))
         return
     dist = None
     if world > 1:

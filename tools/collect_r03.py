@@ -47,6 +47,27 @@ def probe(src, dst):
     json.dump(out, open(os.path.join(dst, "flop_probe.json"), "w"), indent=1)
 
 
+def policy_counters(src, dst):
+    """Per-launch means of the policy kernel's PMC passes (rollout loop)."""
+    acc = defaultdict(list)
+    for d in ("pol_sq", "pol_sq2", "pol_tcp", "pol_fetch"):
+        for f in glob.glob(os.path.join(src, d, "*counter_collection.csv")):
+            per = defaultdict(float)
+            for r in csv.DictReader(open(f)):
+                if "policy_kernel" in r["Kernel_Name"]:
+                    per[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
+            for (_, n), v in per.items():
+                acc[n].append(v)
+    if not acc:
+        return
+    mean = {n: sum(v) / len(v) for n, v in acc.items()}
+    out = {"kernel": "policy_kernel_split (rollout loop, 4096 envs)", "per_launch_mean": mean,
+           "launches_per_counter": {n: len(v) for n, v in acc.items()}}
+    if "TCP_TCC_READ_REQ_sum" in mean:
+        out["l2_to_cu_bytes_per_launch_128B_requests"] = mean["TCP_TCC_READ_REQ_sum"] * 128
+    json.dump(out, open(os.path.join(dst, "policy_counters.json"), "w"), indent=1)
+
+
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "prof_r03")
     dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "profiles", "r03")
@@ -58,6 +79,9 @@ def main():
                     "go1_step_kernel"], check=True, capture_output=True)
     stats(src, "rollout", dst, "rollout_kernel_stats.csv")
     stats(src, "learn", dst, "learn_kernel_stats.csv", keep_all=True)
+    stats(src, "vel", dst, "vel_kernel_stats.csv")
+    stats(src, "vel_learn", dst, "vel_learn_kernel_stats.csv", keep_all=True)
+    policy_counters(src, dst)
     probe(src, dst)
     b = os.path.join(src, "bench_full.log")
     if os.path.exists(b):

@@ -31,4 +31,12 @@ run flops 240 --pmc $FL --output-format csv -d "$OUT/flops" -o flops -- python3 
 run tcc 240 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/tcc" -o tcc -- python3 $B
 run rollout 240 --kernel-trace --stats --output-format csv -d "$OUT/rollout" -o rollout -- python3 "$ROOT/bench.py" --rollout-only --steps 120 --warmup 24
 run learn 300 --kernel-trace --stats --output-format csv -d "$OUT/learn" -o learn -- python3 "$ROOT/bench.py" --learn-only
-cd "$ROOT" && timeout -k 10 600 python bench.py --steps 500 --warmup 50 > "$OUT/bench_full.log" 2>&1; echo "bench rc=$?"
+# the velocity env (configs[1]): VecEnv.step loop and whole Runner iterations
+run vel 240 --kernel-trace --stats --output-format csv -d "$OUT/vel" -o vel -- python3 "$ROOT/bench.py" --velocity-only --steps 300 --warmup 30
+run vel_learn 400 --kernel-trace --stats --output-format csv -d "$OUT/vel_learn" -o vel_learn -- python3 "$ROOT/bench.py" --velocity-learn
+# the policy kernel under the rollout loop
+R="$ROOT/bench.py --rollout-only --steps 48 --warmup 8"
+run pol_sq 240 --pmc SQ_WAVES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU --output-format csv -d "$OUT/pol_sq" -o p -- python3 $R
+run pol_sq2 240 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT --output-format csv -d "$OUT/pol_sq2" -o p -- python3 $R
+run pol_tcp 240 --pmc TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d "$OUT/pol_tcp" -o p -- python3 $R
+run pol_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pol_fetch" -o p -- python3 $R
