@@ -40,3 +40,4 @@ run pol_sq 240 --pmc SQ_WAVES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY
 run pol_sq2 240 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT --output-format csv -d "$OUT/pol_sq2" -o p -- python3 $R
 run pol_tcp 240 --pmc TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d "$OUT/pol_tcp" -o p -- python3 $R
 run pol_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pol_fetch" -o p -- python3 $R
+cd "$ROOT" && timeout -k 10 600 python bench.py --steps 500 --warmup 50 > "$OUT/bench_full.log" 2>&1; echo "bench rc=$?"
