@@ -60,9 +60,9 @@ typedef struct go1_transition {
  * layers: a1 a2 a3 p1 p2 p3 p4 c1 c2 c3 c4). */
 #define GO1_POLICY_LAYERS 11
 typedef struct go1_policy_layer {
-  /* [n/16][k/16][64 lanes][8] f16 (n, k padded to 16): each weight w split into hi = f16(w) and
-     lo = f16(w - hi); record (t, g, lane = 16 q + m) = hi, then lo, of W[16 t + m][16 g + 4 q + r],
-     r = 0..3 (16 bytes: the lane's A fragments of v_mfma_f32_16x16x16_f16 for both halves) */
+  /* [n/16][k/32][64 lanes][16] f16 (n padded to 16, k to 32): each weight w split into hi = f16(w)
+     and lo = f16(w - hi); record (t, g, lane = 16 q + m) = hi, then lo, of W[16 t + m][32 g + 8 q + r],
+     r = 0..7 (32 bytes: the lane's A fragments of v_mfma_f32_16x16x32_f16 for both halves) */
   const void* w;
   const float* b;  /* [n padded to 16] */
   const float* wf; /* (n, k) row-major f32, the unsplit weights: the f32 fallback of a workgroup whose
@@ -82,7 +82,7 @@ typedef struct go1_policy_args {
   uint64_t rng_seed, rng_step; /* Philox key / counter, one counter value per call */
   int32_t env_id_offset;       /* global id of row 0 (rank * n) */
   int32_t n_envs, hist_dim, num_actions;
-  int32_t num_priv;            /* privileged obs = latent width, 1 .. 8, hist_dim + num_priv <= 272 */
+  int32_t num_priv;            /* privileged obs = latent width, 1 .. 8, hist_dim + num_priv <= 288 */
   int32_t variant;             /* 0: per-net workgroups of 32 envs (default), 1: one workgroup of 16 envs
                                   running all three nets; identical outputs (tests/test_rollout.py) */
   int32_t* overflow;           /* optional: += workgroups that recomputed in f32 (the range guard) */

@@ -160,33 +160,37 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
 //   critic:     [hist, priv](263)   -> 512 -> 256 -> 128 -> 1  (value)
 // ELU between layers.  f32 accuracy from f16 matrix cores ("3xF16"): every f32 weight and
 // activation x is split into hi = f16(x) and lo = f16(x - hi) (22 significant bits together),
-// and each 16-deep K group of a dot product is three v_mfma_f32_16x16x16_f16,
+// and each 32-deep K group of a dot product is three v_mfma_f32_16x16x32_f16,
 //   acc += Whi Xhi + Whi Xlo + Wlo Xhi
 // with products exact in f32 and f32 accumulation; the dropped Wlo Xlo term is ~2^-22 of the
-// product, below the f32 rounding of the sums.  Three f16 MFMAs (8 cycles each on gfx950) replace
-// four v_mfma_f32_16x16x4_f32 (32 cycles each) per 16 K values.  Weights are split and packed on
-// the host into fragment order: one 16-byte load per lane per (tile, K group) = 4 hi + 4 lo
-// halves, L2-resident (2.8 MB for all three nets).  Activations live in LDS already split, as
-// [k/4][env][4] halves (hi plane, then lo plane): a B fragment (k = 16 g + 4 q + r, env c) is one
-// 8-byte read per plane, and a layer's output tile (rows 4 q + r of env c) is one 8-byte write.
+// product, below the f32 rounding of the sums.  On gfx950 a 16x16x32 f16 MFMA issues in the 16
+// cycles of a 16x16x16 one (tools/probes/mfma_rate.hip: 16.3 cycles each, one wave), so the K=32 form
+// does twice the work per MFMA cycle.  Weights are split and packed on the host into fragment order:
+// 32 bytes per lane per (tile, K group) = 8 hi + 8 lo halves, L2-resident (2.8 MB for all three
+// nets).  Activations live in LDS already split, as [k/8][env][8] halves (hi plane, then lo plane): a
+// B fragment (k = 32 g + 8 q + r, env c) is one 16-byte read per plane, and a layer's output tile
+// (rows 4 q + r of env c) one 8-byte write.
 #ifndef GO1_POLICY_SCHED
 #define GO1_POLICY_SCHED 1
 #endif
-constexpr int PIN = 272;  // 261 / 263 inputs padded to a multiple of 16
+constexpr int PIN = 288;  // 261 / 263 inputs padded to a multiple of 32
 constexpr int PW = 16;    // waves per workgroup (four per SIMD)
 
-typedef go1_policy_layer PolicyLayer;  // w packed [n/16][k/16][64 lanes][4 hi + 4 lo halves], b [n padded to 16]
+typedef go1_policy_layer PolicyLayer;  // w packed [n/16][k/32][64 lanes][8 hi + 8 lo halves], b [n padded to 16]
 typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 h16_t __attribute__((ext_vector_type(16)));
+typedef float f8_t __attribute__((ext_vector_type(8)));  // one lane's weight fragment (32 bytes)
 
-// split activation planes in LDS: element (k, env c) at [k / 4][c][k % 4] of hi, and of lo
+// split activation planes in LDS: element (k, env c) at [k / 8][c][k % 8] of hi, and of lo
 struct ActV {
-  h4_t* hi;
-  h4_t* lo;
+  h8_t* hi;
+  h8_t* lo;
 };
 template <int K>
 struct Act {
-  h4_t hi[K / 4][16];
-  h4_t lo[K / 4][16];
+  h8_t hi[K / 8][16];
+  h8_t lo[K / 8][16];
   __device__ ActV v() { return ActV{&hi[0][0], &lo[0][0]}; }
 };
 
@@ -207,34 +211,34 @@ __device__ __forceinline__ void act_store4(ActV d, int kq, int c, f4_t v, int* o
     h[r] = (_Float16)v[r];
     l[r] = (_Float16)(v[r] - (float)h[r]);
   }
-  d.hi[kq * 16 + c] = h;
-  d.lo[kq * 16 + c] = l;
+  reinterpret_cast<h4_t*>(d.hi)[((kq >> 1) * 16 + c) * 2 + (kq & 1)] = h;
+  reinterpret_cast<h4_t*>(d.lo)[((kq >> 1) * 16 + c) * 2 + (kq & 1)] = l;
 }
 __device__ __forceinline__ void act_store1(ActV d, int k, int c, float v, int* ovf) {
   ovf_check(v, ovf);
   const _Float16 h = (_Float16)v;
-  reinterpret_cast<_Float16*>(d.hi)[((k >> 2) * 16 + c) * 4 + (k & 3)] = h;
-  reinterpret_cast<_Float16*>(d.lo)[((k >> 2) * 16 + c) * 4 + (k & 3)] = (_Float16)(v - (float)h);
+  reinterpret_cast<_Float16*>(d.hi)[((k >> 3) * 16 + c) * 8 + (k & 7)] = h;
+  reinterpret_cast<_Float16*>(d.lo)[((k >> 3) * 16 + c) * 8 + (k & 7)] = (_Float16)(v - (float)h);
 }
 
-// acc += W x over one 16-deep K group: w = (4 hi, 4 lo) halves of the lane's A fragment
-__device__ __forceinline__ f4_t mfma3(f4_t w, h4_t xh, h4_t xl, f4_t acc) {
-  typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
-  const h8_t wv = __builtin_bit_cast(h8_t, w);
-  const h4_t wh = {wv[0], wv[1], wv[2], wv[3]}, wl = {wv[4], wv[5], wv[6], wv[7]};
-  acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wl, xh, acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x16f16(wh, xl, acc, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x16f16(wh, xh, acc, 0, 0, 0);
+// acc += W x over one 32-deep K group: w = (8 hi, 8 lo) halves of the lane's A fragment
+__device__ __forceinline__ f4_t mfma3(f8_t w, h8_t xh, h8_t xl, f4_t acc) {
+  const h16_t wv = __builtin_bit_cast(h16_t, w);
+  const h8_t wh = __builtin_shufflevector(wv, wv, 0, 1, 2, 3, 4, 5, 6, 7);
+  const h8_t wl = __builtin_shufflevector(wv, wv, 8, 9, 10, 11, 12, 13, 14, 15);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc, 0, 0, 0);
 }
 
 template <int NT, int NL>
 __device__ __forceinline__ void policy_load(const PolicyLayer* L, int G, int g, int tile0, int tstride, int lane,
-                                            f4_t (&w)[NL][NT]) {
+                                            f8_t (&w)[NL][NT]) {
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
     for (int i = 0; i < NT; ++i)
-      w[l][i] = reinterpret_cast<const f4_t*>(L[l].w)[((size_t)(tile0 + i * tstride) * G + g) * 64 + lane];
+      w[l][i] = reinterpret_cast<const f8_t*>(L[l].w)[((size_t)(tile0 + i * tstride) * G + g) * 64 + lane];
 #if GO1_POLICY_SCHED
   // keep the prefetch where it is written: otherwise the scheduler sinks the loads next to
   // their MFMAs and the waits become vmcnt(1), exposing the L2 latency every group
@@ -243,11 +247,11 @@ __device__ __forceinline__ void policy_load(const PolicyLayer* L, int G, int g, 
 }
 
 template <int NT, int NL>
-__device__ __forceinline__ void policy_group(const f4_t (&w)[NL][NT], const ActV* src, int g, int q, int c,
+__device__ __forceinline__ void policy_group(const f8_t (&w)[NL][NT], const ActV* src, int g, int q, int c,
                                              f4_t (&acc)[NL][NT]) {
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
-    const h4_t xh = src[l].hi[(4 * g + q) * 16 + c], xl = src[l].lo[(4 * g + q) * 16 + c];
+    const h8_t xh = src[l].hi[(4 * g + q) * 16 + c], xl = src[l].lo[(4 * g + q) * 16 + c];
 #pragma unroll
     for (int i = 0; i < NT; ++i) acc[l][i] = mfma3(w[l][i], xh, xl, acc[l][i]);
   }
@@ -262,7 +266,7 @@ __device__ __forceinline__ void policy_group(const f4_t (&w)[NL][NT], const ActV
 // workgroup computes, so the adaptation module's can be in flight while the inputs are staged
 template <int NT, int NL, int G, int D>
 __device__ __forceinline__ void policy_prefetch(const PolicyLayer* L, int tile0, int tstride, int lane,
-                                                f4_t (&w)[D][NL][NT]) {
+                                                f8_t (&w)[D][NL][NT]) {
 #pragma unroll
   for (int g = 0; g < D && g < G; ++g) policy_load<NT, NL>(L, G, g, tile0, tstride, lane, w[g]);
 }
@@ -270,9 +274,10 @@ __device__ __forceinline__ void policy_prefetch(const PolicyLayer* L, int tile0,
 template <int NT, int NL, int G, int D, bool PREFETCHED = false>
 __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, const ActV* src, int tile0, int tstride,
                                              const ActV* dst, bool act, int lane, int* ovf,
-                                             f4_t (*pre)[NL][NT] = nullptr) {
+                                             f8_t (*pre)[NL][NT] = nullptr) {
   const int q = lane >> 4, c = lane & 15;
-  f4_t acc[NL][NT], w[D][NL][NT];
+  f4_t acc[NL][NT];
+  f8_t w[D][NL][NT];
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
@@ -312,9 +317,9 @@ __device__ __forceinline__ void policy_tiles(const PolicyLayer* L, const ActV* s
 template <int NG>
 __device__ __forceinline__ f4_t tile_partial(const PolicyLayer& L, int Gs, int tile, int g0, ActV src, int lane) {
   const int q = lane >> 4, c = lane & 15;
-  f4_t w[NG];
+  f8_t w[NG];
 #pragma unroll
-  for (int i = 0; i < NG; ++i) w[i] = reinterpret_cast<const f4_t*>(L.w)[((size_t)tile * Gs + g0 + i) * 64 + lane];
+  for (int i = 0; i < NG; ++i) w[i] = reinterpret_cast<const f8_t*>(L.w)[((size_t)tile * Gs + g0 + i) * 64 + lane];
   f4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int i = 0; i < NG; ++i)
@@ -337,7 +342,7 @@ __device__ void dense_f32(const float* __restrict__ W, const float* __restrict__
 
 // The envs [e0, e0 + ne) of a workgroup whose split activations left the f16 range, recomputed in f32
 // from the unsplit weights (layers[].wf): the adaptation module + actor (+ the Normal sample with the
-// same Philox draws) and / or the critic.  `buf`: >= 272 + 512 + 256 floats of LDS no longer in use.
+// same Philox draws) and / or the critic.  `buf`: >= PIN + 512 + 256 floats of LDS no longer in use.
 __device__ void policy_fallback(const go1_policy_args& P, int e0, int ne, bool actor, bool critic, float* buf) {
   const go1_policy_layer* L = P.layers;
   const int H = P.hist_dim, NP = P.num_priv, NA = P.num_actions;
@@ -419,8 +424,8 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   if (tid == 0) s_ovf = 0;
 #ifndef GO1_POLICY_NO_EARLY
   // the adaptation module's first weight groups are in flight while the inputs are staged
-  f4_t w_ad[8][1][1];
-  policy_prefetch<1, 1, PIN / 16, 8>(P.layers + 0, wave, PW, lane, w_ad);
+  f8_t w_ad[4][1][1];
+  policy_prefetch<1, 1, PIN / 32, 4>(P.layers + 0, wave, PW, lane, w_ad);
 #endif
   for (int idx = tid; idx < 16 * PIN; idx += 64 * PW) {
     const int e = idx / PIN, k = idx - e * PIN;
@@ -437,9 +442,9 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   const ActV vh1[2] = {h1[0].v(), h1[1].v()}, vh2[2] = {h2[0].v(), h2[1].v()};
   // adaptation module (xa rows >= hist_dim are still zero)
 #ifndef GO1_POLICY_NO_EARLY
-  policy_tiles<1, 1, PIN / 16, 8, true>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, &s_ovf, w_ad);  // 256
+  policy_tiles<1, 1, PIN / 32, 4, true>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, &s_ovf, w_ad);  // 256
 #else
-  policy_tiles<1, 1, PIN / 16, 8>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, &s_ovf);  // 256
+  policy_tiles<1, 1, PIN / 32, 4>(Ls + 0, &va, wave, PW, &vh1[0], true, lane, &s_ovf);  // 256
 #endif
   __syncthreads();
   PSTAMP(2);
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   {
     float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1]);
     const int q = lane >> 4, c = lane & 15, t = wave & 7, half = wave >> 3;
-    f4_t acc = tile_partial<8>(Ls[1], 16, t, 8 * half, vh1[0], lane);
+    f4_t acc = tile_partial<4>(Ls[1], 8, t, 4 * half, vh1[0], lane);
     if (half) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) scr[t][4 * q + r][c] = acc[r];
@@ -464,12 +469,12 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   }
   __syncthreads();
   PSTAMP(3);
-  // 128 -> num_priv (the latent): one K group per wave (8 waves), partials summed by wave 0
+  // 128 -> num_priv (the latent): one K group per wave (4 waves), partials summed by wave 0
   {
     float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[1]);
     const int q = lane >> 4, c = lane & 15;
-    if (wave < 8) {
-      const f4_t acc = tile_partial<1>(Ls[2], 8, 0, wave, vh2[0], lane);
+    if (wave < 4) {
+      const f4_t acc = tile_partial<1>(Ls[2], 4, 0, wave, vh2[0], lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = acc[r];
     }
@@ -481,7 +486,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
         if (f < NP) {
           float l = Ls[2].b[f];
 #pragma unroll
-          for (int w = 0; w < 8; ++w) l += scr[w][f][c];
+          for (int w = 0; w < 4; ++w) l += scr[w][f][c];
           act_store1(va, P.hist_dim + f, c, l, &s_ovf);
           if (c < ne && P.latent) P.latent[(size_t)(e0 + c) * NP + f] = l;
         }
@@ -494,30 +499,32 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   const PolicyLayer LA1[2] = {Ls[3], Ls[7]}, LA2[2] = {Ls[4], Ls[8]};
   {
     const ActV s1[2] = {va, vc};
-    policy_tiles<2, 2, PIN / 16, 3>(LA1, s1, wave, PW, vh1, true, lane, &s_ovf);  // 512
+    policy_tiles<2, 2, PIN / 32, 2>(LA1, s1, wave, PW, vh1, true, lane, &s_ovf);  // 512
   }
   __syncthreads();
   PSTAMP(5);
-  policy_tiles<1, 2, 512 / 16, 6>(LA2, vh1, wave, PW, vh2, true, lane, &s_ovf);  // 256
+  policy_tiles<1, 2, 512 / 32, 3>(LA2, vh1, wave, PW, vh2, true, lane, &s_ovf);  // 256
   __syncthreads();
   PSTAMP(6);
   {  // 256 -> 128, one tile per wave: waves 0-7 the actor's, 8-15 the critic's
     const bool critic = wave >= 8;
     const PolicyLayer L3 = critic ? Ls[9] : Ls[5];
     const ActV src = critic ? h2[1].v() : h2[0].v(), dst = critic ? h1[1].v() : h1[0].v();
-    policy_tiles<1, 1, 256 / 16, 8>(&L3, &src, wave & 7, 8, &dst, true, lane, &s_ovf);
+    policy_tiles<1, 1, 256 / 32, 4>(&L3, &src, wave & 7, 8, &dst, true, lane, &s_ovf);
   }
   __syncthreads();
   PSTAMP(7);
-  // 128 -> num_actions (actor, waves 0-7) and 128 -> 1 (critic, waves 8-15): one K group per
+  // 128 -> num_actions (actor, waves 0-3) and 128 -> 1 (critic, waves 8-11): one K group per
   // wave, partials through LDS (h2, free once the third layer has read it)
   {
     float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0]);
     const int q = lane >> 4, c = lane & 15;
     const bool critic = wave >= 8;
-    const f4_t part = tile_partial<1>(Ls[critic ? 10 : 6], 8, 0, wave & 7, critic ? h1[1].v() : h1[0].v(), lane);
+    if ((wave & 7) < 4) {
+      const f4_t part = tile_partial<1>(Ls[critic ? 10 : 6], 4, 0, wave & 7, critic ? h1[1].v() : h1[0].v(), lane);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = part[r];
+      for (int r = 0; r < 4; ++r) scr[wave][4 * q + r][c] = part[r];
+    }
   }
   __syncthreads();
   if (wave < 2) {
@@ -527,7 +534,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     {
       float(*scr)[16][16] = reinterpret_cast<float(*)[16][16]>(&h2[0]);
 #pragma unroll
-      for (int w = 0; w < 8; ++w)
+      for (int w = 0; w < 4; ++w)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] += scr[8 * wave + w][4 * q + r][c];
     }
@@ -590,24 +597,23 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
 // workgroups run the adaptation module + actor (1.6 MB), the others the critic (1.2 MB), so a CU
 // streams at most 1.6 MB for twice the envs.  K order, tile split and partial-sum order are those
 // of policy_kernel, so the outputs are identical.
-constexpr int SE = 32;  // envs per workgroup of policy_kernel_split
-// weight groups in flight per wave, the 512-wide first layers and the 256-wide second: (4, 8), (6, 12),
-// (8, 12), (8, 16) all within 1 % of each other on the rollout loop (2 runs each), so not the limit
+// weight groups (32 K values) in flight per wave, the 512-wide first layers and the 256-wide second
+// (16-deep groups, round 2: (4, 8), (6, 12), (8, 12), (8, 16) all within 1 %)
 #ifndef GO1_SPLIT_D1
-#define GO1_SPLIT_D1 6
+#define GO1_SPLIT_D1 3
 #endif
 #ifndef GO1_SPLIT_D2
-#define GO1_SPLIT_D2 12
+#define GO1_SPLIT_D2 6
 #endif
 
 template <int NT, int NL, int ET>
-__device__ __forceinline__ void policy_group_e(const f4_t (&w)[NL][NT], const ActV (*src)[NL], int g, int q, int c,
+__device__ __forceinline__ void policy_group_e(const f8_t (&w)[NL][NT], const ActV (*src)[NL], int g, int q, int c,
                                                f4_t (&acc)[ET][NL][NT]) {
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
     for (int et = 0; et < ET; ++et) {
-      const h4_t xh = src[et][l].hi[(4 * g + q) * 16 + c], xl = src[et][l].lo[(4 * g + q) * 16 + c];
+      const h8_t xh = src[et][l].hi[(4 * g + q) * 16 + c], xl = src[et][l].lo[(4 * g + q) * 16 + c];
 #pragma unroll
       for (int i = 0; i < NT; ++i) acc[et][l][i] = mfma3(w[l][i], xh, xl, acc[et][l][i]);
     }
@@ -617,7 +623,8 @@ template <int NT, int NL, int ET, int G, int D>
 __device__ __forceinline__ void policy_tiles_e(const PolicyLayer* L, const ActV (*src)[NL], int tile0, int tstride,
                                                const ActV (*dst)[NL], bool act, int lane, int* ovf) {
   const int q = lane >> 4, c = lane & 15;
-  f4_t acc[ET][NL][NT], w[D][NL][NT];
+  f4_t acc[ET][NL][NT];
+  f8_t w[D][NL][NT];
 #pragma unroll
   for (int l = 0; l < NL; ++l)
 #pragma unroll
@@ -652,9 +659,9 @@ template <int NG, int ET>
 __device__ __forceinline__ void tile_partial_e(const PolicyLayer& L, int Gs, int tile, int g0, const ActV* src, int lane,
                                                f4_t (&acc)[ET]) {
   const int q = lane >> 4, c = lane & 15;
-  f4_t w[NG];
+  f8_t w[NG];
 #pragma unroll
-  for (int i = 0; i < NG; ++i) w[i] = reinterpret_cast<const f4_t*>(L.w)[((size_t)tile * Gs + g0 + i) * 64 + lane];
+  for (int i = 0; i < NG; ++i) w[i] = reinterpret_cast<const f8_t*>(L.w)[((size_t)tile * Gs + g0 + i) * 64 + lane];
 #pragma unroll
   for (int et = 0; et < ET; ++et) acc[et] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -664,47 +671,101 @@ __device__ __forceinline__ void tile_partial_e(const PolicyLayer& L, int Gs, int
       acc[et] = mfma3(w[i], src[et].hi[(4 * (g0 + i) + q) * 16 + c], src[et].lo[(4 * (g0 + i) + q) * 16 + c], acc[et]);
 }
 
-__global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P) {
-  __shared__ Act<PIN> xin[2];           // [env tile] inputs (actor: history + latent; critic: history + priv)
-  __shared__ Act<512> h1[2];            // layer-1 outputs; layer 3 reuses them
-  __shared__ Act<256> h2[2];            // layer-2 outputs
-  __shared__ float scr[2][8][16][16];   // [env tile] K-split partials
+// LDS of policy_kernel_split: three env tiles of inputs and of 512-wide outputs.  Aliases (each used only
+// after a barrier that ends the previous use): the 256-wide L2 outputs live in the input planes (dead once
+// L1 has run); the adaptation module's L2 outputs in rows 256-383 of h1 (its L1 outputs hold rows 0-255);
+// K-split partials in a free input tile (actor: tile 2; critic, after L3: tiles 0-1).
+struct SplitLds {
+  Act<PIN> xin[3];
+  Act<512> h1[3];
+};
+typedef float Scr[8][16][16];  // the K-split partials of one env tile
+
+template <int ET, bool CRITIC>
+__device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S, int e0, int ne, int* s_ovf) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  PSTAMP(0);
   const int q = lane >> 4, c = lane & 15;
-  const int nblk = (P.n_envs + SE - 1) / SE;
-  const bool critic = (int)blockIdx.x >= nblk;
-  const int e0 = (critic ? (int)blockIdx.x - nblk : (int)blockIdx.x) * SE;
-  const int ne = min(SE, P.n_envs - e0);
   const int NP = P.num_priv;
-  const ActV vx[2][1] = {{xin[0].v()}, {xin[1].v()}}, v1[2][1] = {{h1[0].v()}, {h1[1].v()}},
-             v2[2][1] = {{h2[0].v()}, {h2[1].v()}};
-  __shared__ int s_ovf;
-  if (tid == 0) s_ovf = 0;
-  for (int idx = tid; idx < SE * PIN; idx += 64 * PW) {
-    const int e = idx / PIN, k = idx - e * PIN;
-    float v = 0.0f;
-    if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
-    if (critic && e < ne && k >= P.hist_dim && k < P.hist_dim + NP)
-      v = P.privileged_obs[(size_t)(e0 + e) * NP + (k - P.hist_dim)];
-    act_store1(e < 16 ? vx[0][0] : vx[1][0], k, e & 15, v, &s_ovf);  // no runtime index into vx (private memory)
+  ActV vx[ET][1], v1[ET][1], v2[ET][1];
+#pragma unroll
+  for (int et = 0; et < ET; ++et) {
+    vx[et][0] = S.xin[et].v();
+    v1[et][0] = S.h1[et].v();
+    v2[et][0] = S.xin[et].v();  // L2 outputs over the dead inputs
+  }
+  {
+    // inputs, in two passes through LDS (h1 is free until the first layer): the workgroup's history rows
+    // are one contiguous block of ne x H floats, read with coalesced loads (all of the thread's in flight)
+    // into a flat f32 copy; then each lane splits eight consecutive features of one env into one 16-byte
+    // record per plane, the lanes of a wave filling consecutive records (element-wise split stores hit
+    // the same LDS banks 8-16 times over: 12-16 k cycles of staging against ~3 k)
+    const int H = P.hist_dim;
+    float* flat = reinterpret_cast<float*>(&S.h1[0]);
+    constexpr int NI = (ET * 16 * PIN + 64 * PW - 1) / (64 * PW);
+    {
+      const float* src = P.obs_history + (size_t)e0 * H;
+      const int total = ne * H;
+      float v[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = tid + i * 64 * PW;
+        v[i] = j < total ? src[j] : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = tid + i * 64 * PW;
+        if (j < total) flat[j] = v[i];
+      }
+    }
+    __syncthreads();
+    constexpr int NC = PIN / 8, NTASK = ET * 16 * NC;
+    for (int t = tid; t < NTASK; t += 64 * PW) {
+      const int c = t & 15, rest = t >> 4, kc = rest % NC, et = rest / NC, e = 16 * et + c;
+      float x[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int k = 8 * kc + r;
+        float val = 0.0f;
+        if (e < ne) {
+          if (k < H) val = flat[e * H + k];
+          else if (CRITIC && k < H + NP) val = P.privileged_obs[(size_t)(e0 + e) * NP + (k - H)];
+        }
+        x[r] = val;
+      }
+      h8_t hi8, lo8;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        ovf_check(x[r], s_ovf);
+        hi8[r] = (_Float16)x[r];
+        lo8[r] = (_Float16)(x[r] - (float)hi8[r]);
+      }
+      S.xin[et].hi[kc][c] = hi8;
+      S.xin[et].lo[kc][c] = lo8;
+    }
   }
   __syncthreads();
   PSTAMP(1);
   const PolicyLayer* Ls = P.layers;
-  if (!critic) {
+  if constexpr (!CRITIC) {
+    static_assert(ET <= 2, "the actor's K-split partials use input tile 2");
+    Scr* scr = reinterpret_cast<Scr*>(&S.xin[2]);  // [et]
+    ActV va2[ET];  // adaptation L2 outputs: rows 256-383 of h1
+#pragma unroll
+    for (int et = 0; et < ET; ++et) va2[et] = ActV{&S.h1[et].hi[64][0], &S.h1[et].lo[64][0]};
     // adaptation module 261 -> 256 (xin rows >= hist_dim are still zero)
-    policy_tiles_e<1, 1, 2, PIN / 16, 8>(Ls + 0, vx, wave, PW, v1, true, lane, &s_ovf);
+    policy_tiles_e<1, 1, ET, PIN / 32, 4>(Ls + 0, vx, wave, PW, v1, true, lane, s_ovf);
     __syncthreads();
     PSTAMP(2);
     {  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7
       const int t = wave & 7, half = wave >> 3;
-      const ActV src[2] = {v1[0][0], v1[1][0]};
-      f4_t acc[2];
-      tile_partial_e<8, 2>(Ls[1], 16, t, 8 * half, src, lane, acc);
+      ActV src[ET];
+#pragma unroll
+      for (int et = 0; et < ET; ++et) src[et] = v1[et][0];
+      f4_t acc[ET];
+      tile_partial_e<4, ET>(Ls[1], 8, t, 4 * half, src, lane, acc);
       if (half) {
 #pragma unroll
-        for (int et = 0; et < 2; ++et)
+        for (int et = 0; et < ET; ++et)
 #pragma unroll
           for (int r = 0; r < 4; ++r) scr[et][t][4 * q + r][c] = acc[et][r];
       }
@@ -712,38 +773,36 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
       if (!half) {
         const f4_t b = *reinterpret_cast<const f4_t*>(Ls[1].b + 16 * t + 4 * q);
 #pragma unroll
-        for (int et = 0; et < 2; ++et) {
+        for (int et = 0; et < ET; ++et) {
           f4_t v;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = elu((b[r] + acc[et][r]) + scr[et][t][4 * q + r][c]);
-          act_store4(v2[et][0], 4 * t + q, c, v, &s_ovf);
+          act_store4(va2[et], 4 * t + q, c, v, s_ovf);
         }
       }
     }
     __syncthreads();
     PSTAMP(3);
-    {  // 128 -> num_priv (the latent): one K group per wave (8 waves), partials summed by waves 0 / 1
-      if (wave < 8) {
-        const ActV src[2] = {v2[0][0], v2[1][0]};
-        f4_t acc[2];
-        tile_partial_e<1, 2>(Ls[2], 8, 0, wave, src, lane, acc);
+    {  // 128 -> num_priv (the latent): one K group per wave (4 waves), partials summed by waves 0 .. ET-1
+      if (wave < 4) {
+        f4_t acc[ET];
+        tile_partial_e<1, ET>(Ls[2], 4, 0, wave, va2, lane, acc);
 #pragma unroll
-        for (int et = 0; et < 2; ++et)
+        for (int et = 0; et < ET; ++et)
 #pragma unroll
           for (int r = 0; r < 4; ++r) scr[et][wave][4 * q + r][c] = acc[et][r];
       }
       __syncthreads();
-      if (wave < 2 && q < 2) {
+      if (wave < ET && q < 2) {
         const int et = wave, e = 16 * et + c;
-        const ActV d = et ? vx[1][0] : vx[0][0];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int f = 4 * q + r;
           if (f < NP) {
             float l = Ls[2].b[f];
 #pragma unroll
-            for (int w = 0; w < 8; ++w) l += scr[et][w][f][c];
-            act_store1(d, P.hist_dim + f, c, l, &s_ovf);
+            for (int w = 0; w < 4; ++w) l += scr[et][w][f][c];
+            act_store1(S.xin[et].v(), P.hist_dim + f, c, l, s_ovf);
             if (e < ne && P.latent) P.latent[(size_t)(e0 + e) * NP + f] = l;
           }
         }
@@ -757,34 +816,38 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
     PSTAMP(4);
   }
   // actor (Ls 3-6) or critic (Ls 7-10), layer by layer
-  const PolicyLayer* LN = Ls + (critic ? 7 : 3);
-  policy_tiles_e<2, 1, 2, PIN / 16, GO1_SPLIT_D1>(LN + 0, vx, wave, PW, v1, true, lane, &s_ovf);  // 512
+  const PolicyLayer* LN = Ls + (CRITIC ? 7 : 3);
+  policy_tiles_e<2, 1, ET, PIN / 32, GO1_SPLIT_D1>(LN + 0, vx, wave, PW, v1, true, lane, s_ovf);  // 512
   __syncthreads();
   PSTAMP(5);
-  policy_tiles_e<1, 1, 2, 512 / 16, GO1_SPLIT_D2>(LN + 1, v1, wave, PW, v2, true, lane, &s_ovf);  // 256
+  policy_tiles_e<1, 1, ET, 512 / 32, GO1_SPLIT_D2>(LN + 1, v1, wave, PW, v2, true, lane, s_ovf);  // 256
   __syncthreads();
   PSTAMP(6);
-  if (wave < 8) policy_tiles_e<1, 1, 2, 256 / 16, 8>(LN + 2, v2, wave, 8, v1, true, lane, &s_ovf);  // 128 -> h1
+  if (wave < 8) policy_tiles_e<1, 1, ET, 256 / 32, 4>(LN + 2, v2, wave, 8, v1, true, lane, s_ovf);  // 128 -> h1
   __syncthreads();
   PSTAMP(7);
-  if (wave < 8) {  // 128 -> num_actions / 1: one K group per wave, partials through LDS
-    const ActV src[2] = {v1[0][0], v1[1][0]};
-    f4_t part[2];
-    tile_partial_e<1, 2>(LN[3], 8, 0, wave, src, lane, part);
+  // 128 -> num_actions / 1: one K group per wave, partials through LDS (the inputs' planes, dead now)
+  Scr* scr = CRITIC ? reinterpret_cast<Scr*>(&S.xin[0]) : reinterpret_cast<Scr*>(&S.xin[2]);
+  if (wave < 4) {
+    ActV src[ET];
 #pragma unroll
-    for (int et = 0; et < 2; ++et)
+    for (int et = 0; et < ET; ++et) src[et] = v1[et][0];
+    f4_t part[ET];
+    tile_partial_e<1, ET>(LN[3], 4, 0, wave, src, lane, part);
+#pragma unroll
+    for (int et = 0; et < ET; ++et)
 #pragma unroll
       for (int r = 0; r < 4; ++r) scr[et][wave][4 * q + r][c] = part[et][r];
   }
   __syncthreads();
-  if (wave < 2) {
+  if (wave < ET) {
     const int et = wave, e = 16 * et + c;
     f4_t acc = *reinterpret_cast<const f4_t*>(LN[3].b + 4 * q);
 #pragma unroll
-    for (int w = 0; w < 8; ++w)
+    for (int w = 0; w < 4; ++w)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[r] += scr[et][w][4 * q + r][c];
-    if (!critic) {
+    if constexpr (!CRITIC) {
       if (P.actions) {
         float lp = 0.0f;
         f4_t a4, s4;
@@ -832,7 +895,32 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
   }
   PSTAMP(8);
   __syncthreads();
-  if (s_ovf) policy_fallback(P, e0, ne, !critic, critic, reinterpret_cast<float*>(&h1[0]));
+  if (*s_ovf) policy_fallback(P, e0, ne, !CRITIC, CRITIC, reinterpret_cast<float*>(&S.h1[0]));
+}
+
+// envs per workgroup: actor workgroups (adaptation module + actor, 1.6 MB of split weights) take SPLIT_ET_A
+// env tiles, critic workgroups (1.2 MB) SPLIT_ET_C, so the two kinds take about as long
+#ifndef GO1_SPLIT_ET_A
+#define GO1_SPLIT_ET_A 2
+#endif
+#ifndef GO1_SPLIT_ET_C
+#define GO1_SPLIT_ET_C 3
+#endif
+constexpr int SE_A = 16 * GO1_SPLIT_ET_A, SE_C = 16 * GO1_SPLIT_ET_C;
+
+__global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P) {
+  __shared__ SplitLds S;
+  __shared__ int s_ovf;
+  PSTAMP(0);
+  if (threadIdx.x == 0) s_ovf = 0;
+  const int na = (P.n_envs + SE_A - 1) / SE_A;
+  if ((int)blockIdx.x < na) {
+    const int e0 = blockIdx.x * SE_A;
+    split_body<GO1_SPLIT_ET_A, false>(P, S, e0, min(SE_A, P.n_envs - e0), &s_ovf);
+  } else {
+    const int e0 = (blockIdx.x - na) * SE_C;
+    split_body<GO1_SPLIT_ET_C, true>(P, S, e0, min(SE_C, P.n_envs - e0), &s_ovf);
+  }
 }
 
 }  // namespace
@@ -885,7 +973,8 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
   if (args->variant != 0 && args->variant != 1) return fail(GO1_RT_E_ARG, "go1_policy_forward: variant");
   go1_policy_args P = *args;
   if (P.variant == 0)
-    hipLaunchKernelGGL(policy_kernel_split, dim3(2 * ((P.n_envs + SE - 1) / SE)), dim3(64 * PW), 0, (hipStream_t)stream, P);
+    hipLaunchKernelGGL(policy_kernel_split, dim3((P.n_envs + SE_A - 1) / SE_A + (P.n_envs + SE_C - 1) / SE_C),
+                       dim3(64 * PW), 0, (hipStream_t)stream, P);
   else
     hipLaunchKernelGGL(policy_kernel, dim3((P.n_envs + 15) / 16), dim3(64 * PW), 0, (hipStream_t)stream, P);
   RT_TRY(hipGetLastError());

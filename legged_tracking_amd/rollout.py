@@ -106,13 +106,13 @@ class _PolicyArgs(C.Structure):
 def _pack_linear(lin):
     """nn.Linear -> (weights split and packed for csrc/rollout.hip's 3xF16 MFMA, bias padded to 16).
 
-    Every weight w is split into hi = f16(w) and lo = f16(w - hi).  Packed as 16-byte records
-    [n/16][k/16][lane = 16 q + m][hi r = 0..3, lo r = 0..3] of W[16 t + m][16 g + 4 q + r]: lane
-    (m, q) of output tile t reads one record per 16-deep K group g -- its A fragments of
-    v_mfma_f32_16x16x16_f16 (rows m, k = 4 q .. 4 q + 3) for both halves of the split."""
+    Every weight w is split into hi = f16(w) and lo = f16(w - hi).  Packed as 32-byte records
+    [n/16][k/32][lane = 16 q + m][hi r = 0..7, lo r = 0..7] of W[16 t + m][32 g + 8 q + r]: lane
+    (m, q) of output tile t reads one record per 32-deep K group g -- its A fragments of
+    v_mfma_f32_16x16x32_f16 (row m, k = 8 q .. 8 q + 7) for both halves of the split."""
     W, b = lin.weight.detach().float(), lin.bias.detach().float()
     n, k = W.shape
-    npad, kpad = -(-n // 16) * 16, -(-k // 16) * 16
+    npad, kpad = -(-n // 16) * 16, -(-k // 32) * 32
     Wp = torch.zeros(npad, kpad, device=W.device, dtype=torch.float32)
     Wp[:n, :k] = W
     bp = torch.zeros(npad, device=W.device, dtype=torch.float32)
@@ -121,7 +121,7 @@ def _pack_linear(lin):
     lo = (Wp - hi.float()).to(torch.float16)
     # [t, m, g, q, r] -> [t, g, q, m, r], then hi and lo side by side in the last dimension
     def frag(x):
-        return x.view(npad // 16, 16, kpad // 16, 4, 4).permute(0, 2, 3, 1, 4)
+        return x.view(npad // 16, 16, kpad // 32, 4, 8).permute(0, 2, 3, 1, 4)
     return torch.cat([frag(hi), frag(lo)], dim=-1).contiguous(), bp
 
 
@@ -149,7 +149,7 @@ class FusedPolicy:
         want = [(256, h), (128, 256), (npv, 128), (512, h + npv), (256, 512), (128, 256), (None, 128),
                 (512, h + npv), (256, 512), (128, 256), (1, 128)]
         ok = all(w[0] in (None, s[0]) and w[1] == s[1] for s, w in zip(shapes, want))
-        return ok and 1 <= npv <= 8 and h + npv <= 272 and shapes[6][0] <= 16 and isinstance(a[1], nn.ELU)
+        return ok and 1 <= npv <= 8 and h + npv <= 288 and shapes[6][0] <= 16 and isinstance(a[1], nn.ELU)
 
     def pack(self):
         ac = self.ac

@@ -46,9 +46,13 @@ def main():
     buf = np.zeros(512 * 16 * 12, np.uint64)
     assert lib.go1_policy_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
     t_all = buf.reshape(512, 16, 12).astype(np.int64)[:256, :, :9]
-    groups = [("all", t_all)] if variant else [("actor workgroups", t_all[:128]), ("critic workgroups", t_all[128:])]
+    used = t_all[:, 0, 0] != 0  # workgroups of the launch (the stamp buffer holds 256)
+    na = -(-n // (16 * int(os.environ.get("GO1_SPLIT_ET_A", "2"))))
+    groups = [("all", t_all[used])] if variant else [("actor workgroups", t_all[:na][used[:na]]),
+                                                     ("critic workgroups", t_all[na:][used[na:]])]
     for label, t in groups:
         t = t - t[:, :, :1].min(axis=1, keepdims=True)
+        print(f"{label}: wave start spread within a workgroup: mean {t[:, :, 0].max(axis=1).mean():.0f} cycles")
         ends = t.max(axis=1)  # (wg, 9): phase end = last wave through the barrier
         d = np.diff(ends, axis=1).mean(axis=0)
         life = ends[:, 8].mean()
@@ -56,8 +60,8 @@ def main():
         for nm, v in zip(NAMES, d):
             print(f"  {nm:14s} {v:9.0f} {v / life:7.1%}")
     # spread of the workgroups' start times (launch ramp) and end times
-    st = t_all[:, :, 0].min(axis=1)
-    en = t_all[:, :, 8].max(axis=1)
+    st = t_all[used][:, :, 0].min(axis=1)
+    en = t_all[used][:, :, 8].max(axis=1)
     print(f"start spread {np.ptp(st)} cycles, end spread {np.ptp(en)}, first start -> last end {en.max() - st.min()}")
 
 
