@@ -619,9 +619,10 @@ __device__ __forceinline__ void policy_group_e(const f8_t (&w)[NL][NT], const Ac
     }
 }
 
-template <int NT, int NL, int ET, int G, int D>
+template <int NT, int NL, int ET, int G, int D, bool PREFETCHED = false>
 __device__ __forceinline__ void policy_tiles_e(const PolicyLayer* L, const ActV (*src)[NL], int tile0, int tstride,
-                                               const ActV (*dst)[NL], bool act, int lane, int* ovf) {
+                                               const ActV (*dst)[NL], bool act, int lane, int* ovf,
+                                               f8_t (*pre)[NL][NT] = nullptr) {
   const int q = lane >> 4, c = lane & 15;
   f4_t acc[ET][NL][NT];
   f8_t w[D][NL][NT];
@@ -633,7 +634,16 @@ __device__ __forceinline__ void policy_tiles_e(const PolicyLayer* L, const ActV 
 #pragma unroll
       for (int et = 0; et < ET; ++et) acc[et][l][i] = b;
     }
-  policy_prefetch<NT, NL, G, D>(L, tile0, tstride, lane, w);
+  if constexpr (PREFETCHED) {
+#pragma unroll
+    for (int g = 0; g < D; ++g)
+#pragma unroll
+      for (int l = 0; l < NL; ++l)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) w[g][l][i] = pre[g][l][i];
+  } else {
+    policy_prefetch<NT, NL, G, D>(L, tile0, tstride, lane, w);
+  }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     policy_group_e<NT, NL, ET>(w[g % D], src, g, q, c, acc);
@@ -655,13 +665,24 @@ __device__ __forceinline__ void policy_tiles_e(const PolicyLayer* L, const ActV 
 }
 
 // tile_partial for ET env tiles sharing the weight fragments
-template <int NG, int ET>
-__device__ __forceinline__ void tile_partial_e(const PolicyLayer& L, int Gs, int tile, int g0, const ActV* src, int lane,
-                                               f4_t (&acc)[ET]) {
-  const int q = lane >> 4, c = lane & 15;
-  f8_t w[NG];
+// the NG weight fragments of a tile_partial_e, loaded ahead (they depend on nothing the workgroup computes)
+template <int NG>
+__device__ __forceinline__ void partial_load(const PolicyLayer& L, int Gs, int tile, int g0, int lane, f8_t (&w)[NG]) {
 #pragma unroll
   for (int i = 0; i < NG; ++i) w[i] = reinterpret_cast<const f8_t*>(L.w)[((size_t)tile * Gs + g0 + i) * 64 + lane];
+}
+
+template <int NG, int ET>
+__device__ __forceinline__ void tile_partial_e(const PolicyLayer& L, int Gs, int tile, int g0, const ActV* src, int lane,
+                                               f4_t (&acc)[ET], const f8_t* pre = nullptr) {
+  const int q = lane >> 4, c = lane & 15;
+  f8_t w[NG];
+  if (pre) {
+#pragma unroll
+    for (int i = 0; i < NG; ++i) w[i] = pre[i];
+  } else {
+    partial_load<NG>(L, Gs, tile, g0, lane, w);
+  }
 #pragma unroll
   for (int et = 0; et < ET; ++et) acc[et] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -673,13 +694,18 @@ __device__ __forceinline__ void tile_partial_e(const PolicyLayer& L, int Gs, int
 
 // LDS of policy_kernel_split: three env tiles of inputs and of 512-wide outputs.  Aliases (each used only
 // after a barrier that ends the previous use): the 256-wide L2 outputs live in the input planes (dead once
-// L1 has run); the adaptation module's L2 outputs in rows 256-383 of h1 (its L1 outputs hold rows 0-255);
-// K-split partials in a free input tile (actor: tile 2; critic, after L3: tiles 0-1).
+// L1 has run); the adaptation module's L2 outputs in rows 256-383 of h1 (its L1 outputs hold rows 0-255)
+// and its K-split partials in rows 384-511; the output layer's partials in the input planes.
 struct SplitLds {
   Act<PIN> xin[3];
   Act<512> h1[3];
 };
-typedef float Scr[8][16][16];  // the K-split partials of one env tile
+typedef float Scr[4][16][16];  // the output layer's K-split partials of one env tile
+
+// Workgroup barrier over LDS only: waits for this wave's LDS operations, not for its global loads, so
+// weight fragments requested ahead of a barrier stay in flight across it (__syncthreads' release fence
+// waits for every memory operation).  policy_kernel_split never reads global memory it writes.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int ET, bool CRITIC>
 __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S, int e0, int ne, int* s_ovf) {
@@ -693,6 +719,15 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
     v1[et][0] = S.h1[et].v();
     v2[et][0] = S.xin[et].v();  // L2 outputs over the dead inputs
   }
+  // Every layer's first weight fragments are requested before the barrier that ends the previous phase
+  // (they depend on nothing the workgroup computes), so a layer starts with its weights landed instead
+  // of one L2 round trip after the barrier; the first layer's during the input staging.
+  const PolicyLayer* Ls = P.layers;
+  const PolicyLayer* LN = Ls + (CRITIC ? 7 : 3);
+  f8_t pa1[4][1][1];                   // actor: adaptation module L1
+  f8_t pl1[GO1_SPLIT_D1][1][2];        // actor / critic L1
+  if constexpr (!CRITIC) policy_prefetch<1, 1, PIN / 32, 4>(Ls + 0, wave, PW, lane, pa1);
+  else policy_prefetch<2, 1, PIN / 32, GO1_SPLIT_D1>(LN + 0, wave, PW, lane, pl1);
   {
     // inputs, in two passes through LDS (h1 is free until the first layer): the workgroup's history rows
     // are one contiguous block of ne x H floats, read with coalesced loads (all of the thread's in flight)
@@ -717,7 +752,7 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
         if (j < total) flat[j] = v[i];
       }
     }
-    __syncthreads();
+    lds_barrier();
     constexpr int NC = PIN / 8, NTASK = ET * 16 * NC;
     for (int t = tid; t < NTASK; t += 64 * PW) {
       const int c = t & 15, rest = t >> 4, kc = rest % NC, et = rest / NC, e = 16 * et + c;
@@ -743,56 +778,63 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
       S.xin[et].lo[kc][c] = lo8;
     }
   }
-  __syncthreads();
+  lds_barrier();
   PSTAMP(1);
-  const PolicyLayer* Ls = P.layers;
   if constexpr (!CRITIC) {
-    static_assert(ET <= 2, "the actor's K-split partials use input tile 2");
-    Scr* scr = reinterpret_cast<Scr*>(&S.xin[2]);  // [et]
+    // K-split partials of the adaptation module: 16 x 16 blocks in rows 384-511 of h1 (block t < 4 in
+    // the hi plane, t >= 4 in the lo plane), free until the actor's L1
+    auto blk = [&](int et, int t) -> float(*)[16] {
+      return reinterpret_cast<float(*)[16]>(t < 4 ? &S.h1[et].hi[384 / 8][0] : &S.h1[et].lo[384 / 8][0]) + 16 * (t & 3);
+    };
     ActV va2[ET];  // adaptation L2 outputs: rows 256-383 of h1
 #pragma unroll
-    for (int et = 0; et < ET; ++et) va2[et] = ActV{&S.h1[et].hi[64][0], &S.h1[et].lo[64][0]};
+    for (int et = 0; et < ET; ++et) va2[et] = ActV{&S.h1[et].hi[256 / 8][0], &S.h1[et].lo[256 / 8][0]};
     // adaptation module 261 -> 256 (xin rows >= hist_dim are still zero)
-    policy_tiles_e<1, 1, ET, PIN / 32, 4>(Ls + 0, vx, wave, PW, v1, true, lane, s_ovf);
-    __syncthreads();
+    policy_tiles_e<1, 1, ET, PIN / 32, 4, true>(Ls + 0, vx, wave, PW, v1, true, lane, s_ovf, pa1);
+    f8_t pa2[4];
+    partial_load<4>(Ls[1], 8, wave & 7, 4 * (wave >> 3), lane, pa2);
+    lds_barrier();
     PSTAMP(2);
+    f8_t pa3[1];
+    if (wave < 4) partial_load<1>(Ls[2], 4, 0, wave, lane, pa3);
     {  // 256 -> 128: waves w and w + 8 take the two K halves of tile w & 7
       const int t = wave & 7, half = wave >> 3;
       ActV src[ET];
 #pragma unroll
       for (int et = 0; et < ET; ++et) src[et] = v1[et][0];
       f4_t acc[ET];
-      tile_partial_e<4, ET>(Ls[1], 8, t, 4 * half, src, lane, acc);
+      tile_partial_e<4, ET>(Ls[1], 8, t, 4 * half, src, lane, acc, pa2);
       if (half) {
 #pragma unroll
         for (int et = 0; et < ET; ++et)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) scr[et][t][4 * q + r][c] = acc[et][r];
+          for (int r = 0; r < 4; ++r) blk(et, t)[4 * q + r][c] = acc[et][r];
       }
-      __syncthreads();
+      lds_barrier();
       if (!half) {
         const f4_t b = *reinterpret_cast<const f4_t*>(Ls[1].b + 16 * t + 4 * q);
 #pragma unroll
         for (int et = 0; et < ET; ++et) {
           f4_t v;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = elu((b[r] + acc[et][r]) + scr[et][t][4 * q + r][c]);
+          for (int r = 0; r < 4; ++r) v[r] = elu((b[r] + acc[et][r]) + blk(et, t)[4 * q + r][c]);
           act_store4(va2[et], 4 * t + q, c, v, s_ovf);
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     PSTAMP(3);
     {  // 128 -> num_priv (the latent): one K group per wave (4 waves), partials summed by waves 0 .. ET-1
+      policy_prefetch<2, 1, PIN / 32, GO1_SPLIT_D1>(LN + 0, wave, PW, lane, pl1);  // the actor's L1
       if (wave < 4) {
         f4_t acc[ET];
-        tile_partial_e<1, ET>(Ls[2], 4, 0, wave, va2, lane, acc);
+        tile_partial_e<1, ET>(Ls[2], 4, 0, wave, va2, lane, acc, pa3);
 #pragma unroll
         for (int et = 0; et < ET; ++et)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) scr[et][wave][4 * q + r][c] = acc[et][r];
+          for (int r = 0; r < 4; ++r) blk(et, wave)[4 * q + r][c] = acc[et][r];
       }
-      __syncthreads();
+      lds_barrier();
       if (wave < ET && q < 2) {
         const int et = wave, e = 16 * et + c;
 #pragma unroll
@@ -801,14 +843,14 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
           if (f < NP) {
             float l = Ls[2].b[f];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) l += scr[et][w][f][c];
+            for (int w = 0; w < 4; ++w) l += blk(et, w)[f][c];
             act_store1(S.xin[et].v(), P.hist_dim + f, c, l, s_ovf);
             if (e < ne && P.latent) P.latent[(size_t)(e0 + e) * NP + f] = l;
           }
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     PSTAMP(4);
   } else {
     PSTAMP(2);
@@ -816,30 +858,35 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
     PSTAMP(4);
   }
   // actor (Ls 3-6) or critic (Ls 7-10), layer by layer
-  const PolicyLayer* LN = Ls + (CRITIC ? 7 : 3);
-  policy_tiles_e<2, 1, ET, PIN / 32, GO1_SPLIT_D1>(LN + 0, vx, wave, PW, v1, true, lane, s_ovf);  // 512
-  __syncthreads();
+  policy_tiles_e<2, 1, ET, PIN / 32, GO1_SPLIT_D1, true>(LN + 0, vx, wave, PW, v1, true, lane, s_ovf, pl1);  // 512
+  f8_t pl2[GO1_SPLIT_D2][1][1];
+  policy_prefetch<1, 1, 512 / 32, GO1_SPLIT_D2>(LN + 1, wave, PW, lane, pl2);
+  lds_barrier();
   PSTAMP(5);
-  policy_tiles_e<1, 1, ET, 512 / 32, GO1_SPLIT_D2>(LN + 1, v1, wave, PW, v2, true, lane, s_ovf);  // 256
-  __syncthreads();
+  policy_tiles_e<1, 1, ET, 512 / 32, GO1_SPLIT_D2, true>(LN + 1, v1, wave, PW, v2, true, lane, s_ovf, pl2);  // 256
+  f8_t pl3[4][1][1];
+  if (wave < 8) policy_prefetch<1, 1, 256 / 32, 4>(LN + 2, wave, 8, lane, pl3);
+  lds_barrier();
   PSTAMP(6);
-  if (wave < 8) policy_tiles_e<1, 1, ET, 256 / 32, 4>(LN + 2, v2, wave, 8, v1, true, lane, s_ovf);  // 128 -> h1
-  __syncthreads();
+  f8_t pl4[1];
+  if (wave < 4) partial_load<1>(LN[3], 4, 0, wave, lane, pl4);
+  if (wave < 8) policy_tiles_e<1, 1, ET, 256 / 32, 4, true>(LN + 2, v2, wave, 8, v1, true, lane, s_ovf, pl3);  // 128 -> h1
+  lds_barrier();
   PSTAMP(7);
   // 128 -> num_actions / 1: one K group per wave, partials through LDS (the inputs' planes, dead now)
-  Scr* scr = CRITIC ? reinterpret_cast<Scr*>(&S.xin[0]) : reinterpret_cast<Scr*>(&S.xin[2]);
+  Scr* scr = reinterpret_cast<Scr*>(&S.xin[0]);  // [et], over the dead input planes
   if (wave < 4) {
     ActV src[ET];
 #pragma unroll
     for (int et = 0; et < ET; ++et) src[et] = v1[et][0];
     f4_t part[ET];
-    tile_partial_e<1, ET>(LN[3], 4, 0, wave, src, lane, part);
+    tile_partial_e<1, ET>(LN[3], 4, 0, wave, src, lane, part, pl4);
 #pragma unroll
     for (int et = 0; et < ET; ++et)
 #pragma unroll
       for (int r = 0; r < 4; ++r) scr[et][wave][4 * q + r][c] = part[et][r];
   }
-  __syncthreads();
+  lds_barrier();
   if (wave < ET) {
     const int et = wave, e = 16 * et + c;
     f4_t acc = *reinterpret_cast<const f4_t*>(LN[3].b + 4 * q);
@@ -899,7 +946,8 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
 }
 
 // envs per workgroup: actor workgroups (adaptation module + actor, 1.6 MB of split weights) take SPLIT_ET_A
-// env tiles, critic workgroups (1.2 MB) SPLIT_ET_C, so the two kinds take about as long
+// env tiles, critic workgroups (1.2 MB) SPLIT_ET_C, so the two kinds take about as long (4096 envs: actor
+// 65.8 k / critic 58.5 k cycles; with 3 + 3 tiles the actor workgroups grew to 84 k: 39 against 32.5 us)
 #ifndef GO1_SPLIT_ET_A
 #define GO1_SPLIT_ET_A 2
 #endif
