@@ -296,7 +296,7 @@ def velocity_rate(n, dev, steps, warmup):
             "envs_at_episode_start": resets}
 
 
-def learn_rate(n, dev, iters=4, warmup=1, velocity=False):
+def learn_rate(n, dev, iters=6, warmup=2, velocity=False):
     """The whole training loop, as the reference's wandb train/fps measures it (ppo_cse/__init__.py:184:
     (it + 1) x num_envs x num_steps_per_env / elapsed): Runner iterations of rollout (24 x [PPO.act +
     VecEnv.step + record]), compute_returns (GAE) and PPO.update (5 epochs x 4 mini-batches, Adam, the

@@ -523,9 +523,21 @@ class PPO:
         self.actor_critic = actor_critic.to(device)
         self.storage = None
         self.kernels = kernels
-        self.optimizer = torch.optim.Adam(self.actor_critic.parameters(), lr=PPO_Args.learning_rate)
-        self.adaptation_module_optimizer = torch.optim.Adam(self.actor_critic.parameters(),
-                                                            lr=PPO_Args.adaptation_module_learning_rate)
+        # On the GPU: fused Adam (one kernel per step instead of a foreach chain), its learning rate a device
+        # tensor so that the adaptive schedule (ppo.py:124-136) runs on the device -- no host sync per
+        # mini-batch; the rate is computed in f64 as the reference's Python floats are, and the f32 copy the
+        # kernel reads is the value the foreach path would cast to.  On the CPU: the reference's path.
+        self._dev_lr = torch.device(device).type == "cuda" and os.environ.get("GO1_PPO_FUSED", "1") != "0"
+        params = list(self.actor_critic.parameters())
+        if self._dev_lr:
+            self._lr64 = torch.tensor(PPO_Args.learning_rate, dtype=torch.float64, device=device)
+            self._lr32 = torch.tensor(PPO_Args.learning_rate, dtype=torch.float32, device=device)
+            self.optimizer = torch.optim.Adam(params, lr=self._lr32, fused=True)
+            self.adaptation_module_optimizer = torch.optim.Adam(params, lr=PPO_Args.adaptation_module_learning_rate,
+                                                                fused=True)
+        else:
+            self.optimizer = torch.optim.Adam(params, lr=PPO_Args.learning_rate)
+            self.adaptation_module_optimizer = torch.optim.Adam(params, lr=PPO_Args.adaptation_module_learning_rate)
         self.transition = RolloutStorage.Transition()
         self.learning_rate = PPO_Args.learning_rate
         self.fused = None  # FusedPolicy once the storage (and its kernels) exist
@@ -670,6 +682,15 @@ class PPO:
                         kl_mean = kl_mean.clone()
                         torch.distributed.all_reduce(kl_mean)
                         kl_mean /= _world()
+                if self._dev_lr:
+                    with torch.no_grad():
+                        k, lr = kl_mean.double(), self._lr64
+                        new = torch.where(k > A.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
+                                          torch.where((k < A.desired_kl / 2.0) & (k > 0.0),
+                                                      torch.clamp(lr * 1.5, max=1e-2), lr))
+                        self._lr64.copy_(new)
+                        self._lr32.copy_(new)
+                else:
                     kl_mean = float(kl_mean)
                     if kl_mean > A.desired_kl * 2.0:
                         self.learning_rate = max(1e-5, self.learning_rate / 1.5)
@@ -715,6 +736,8 @@ class PPO:
         if self.fused is not None:
             self.fused.pack()  # the rollout kernel reads the updated weights
         mean_value_loss, mean_surrogate_loss, mean_adapt, mean_adapt_test = (float(x) for x in acc.cpu())
+        if self._dev_lr:
+            self.learning_rate = float(self._lr64)
         return (mean_value_loss / n_up, mean_surrogate_loss / n_up, mean_adapt / n_ad, 0.0, 0.0,
                 mean_adapt_test / n_ad, 0.0, 0.0)
 
