@@ -194,7 +194,26 @@ struct Act {
   __device__ ActV v() { return ActV{&hi[0][0], &lo[0][0]}; }
 };
 
-__device__ __forceinline__ float elu(float x) { return x > 0.0f ? x : expm1f(x); }
+// ELU's negative branch through the hardware exponential (v_exp_f32): exp(x) - 1 loses relative accuracy
+// only where |x| is tiny, where its absolute error stays ~6e-8 (the outputs are checked at 2e-5 of their
+// scale against f64); expm1f's range reduction cost ~25 instructions per value on the workgroups' tails
+__device__ __forceinline__ float elu(float x) { return x > 0.0f ? x : __expf(x) - 1.0f; }
+
+// Normal(0, 1) draws of actions 4 q .. 4 q + 3 of global env gid: one Philox4x32-10 block keyed by
+// (env, action group, step), two Box-Muller pairs on the hardware log2 / sqrt / sin / cos (v_sin / v_cos
+// take revolutions).  The samples are the kernel's own stream (the reference draws from torch's generator).
+__device__ __forceinline__ void normal4(uint32_t gid, int q, uint64_t step, uint64_t seed, float z[4]) {
+  uint32_t ctr[4] = {gid, (uint32_t)q, (uint32_t)step, (uint32_t)(step >> 32)};
+  philox4x32(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float u1 = ((float)(ctr[2 * p] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+    const float u2 = (float)(ctr[2 * p + 1] >> 8) * (1.0f / 16777216.0f);       // [0, 1)
+    const float r = __builtin_amdgcn_sqrtf(-2.0f * 0.69314718055994531f * __builtin_amdgcn_logf(u1));
+    z[2 * p] = r * __builtin_amdgcn_cosf(u2);
+    z[2 * p + 1] = r * __builtin_amdgcn_sinf(u2);
+  }
+}
 
 // Range guard of the split: f16(x) overflows for |x| >= 65520 (and a NaN / inf input has no split), so a
 // value outside (-65504, 65504) sets the workgroup's flag; the workgroup then recomputes its envs in
@@ -342,12 +361,13 @@ __device__ void dense_f32(const float* __restrict__ W, const float* __restrict__
 
 // The envs [e0, e0 + ne) of a workgroup whose split activations left the f16 range, recomputed in f32
 // from the unsplit weights (layers[].wf): the adaptation module + actor (+ the Normal sample with the
-// same Philox draws) and / or the critic.  `buf`: >= PIN + 512 + 256 floats of LDS no longer in use.
+// same Philox draws) and / or the critic.  `buf`: >= hist_dim + num_priv (rounded up to 32) + 768 floats of
+// LDS no longer in use.
 __device__ void policy_fallback(const go1_policy_args& P, int e0, int ne, bool actor, bool critic, float* buf) {
   const go1_policy_layer* L = P.layers;
   const int H = P.hist_dim, NP = P.num_priv, NA = P.num_actions;
   float* x = buf;
-  float* ya = buf + PIN;
+  float* ya = buf + ((H + NP + 31) & ~31);
   float* yb = ya + 512;
   for (int e = 0; e < ne; ++e) {
     const size_t ge = (size_t)(e0 + e);
@@ -364,19 +384,16 @@ __device__ void policy_fallback(const go1_policy_args& P, int e0, int ne, bool a
       dense_f32(L[6].wf, L[6].b, NA, 128, ya, yb, false);
       if (threadIdx.x == 0) {
         float lp_q[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float zq[4];
         for (int f = 0; f < NA; ++f) {
           P.action_mean[ge * NA + f] = yb[f];
           if (P.actions) {
             const float sd = P.std[f];
-            uint32_t ctr[4] = {(uint32_t)(ge + P.env_id_offset), (uint32_t)f, (uint32_t)P.rng_step,
-                               (uint32_t)(P.rng_step >> 32)};
-            philox4x32(ctr, (uint32_t)P.rng_seed, (uint32_t)(P.rng_seed >> 32));
-            const float u1 = ((float)(ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
-            const float u2 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);
-            const float z = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+            if ((f & 3) == 0) normal4((uint32_t)(ge + P.env_id_offset), f >> 2, P.rng_step, P.rng_seed, zq);
+            const float z = zq[f & 3];
             P.actions[ge * NA + f] = yb[f] + sd * z;
             P.action_sigma[ge * NA + f] = sd;
-            lp_q[f >> 2] += -0.5f * z * z - logf(sd) - 0.91893853320467274f;
+            lp_q[f >> 2] += -0.5f * z * z - __logf(sd) - 0.91893853320467274f;
           }
         }
         if (P.actions) P.log_prob[ge] = (lp_q[0] + lp_q[1]) + (lp_q[2] + lp_q[3]);
@@ -541,23 +558,20 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
     if (wave == 0 && P.actions) {
       // Normal(mean, std).sample() and its log_prob summed over the actions
       // (actor_critic.py:137-145), Box-Muller on Philox4x32-10 uniforms keyed by
-      // (global env, action, step): row q, element r is action f = 4 q + r of env c
+      // (global env, action group q, step): row q, element r is action f = 4 q + r of env c (normal4)
       float lp = 0.0f;
       f4_t a4, s4;
+      float z4[4];
+      normal4((uint32_t)(e0 + c + P.env_id_offset), q, P.rng_step, P.rng_seed, z4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int f = 4 * q + r;
         const bool real = f < P.num_actions;
         const float sd = real ? P.std[f] : 1.0f;
-        uint32_t ctr[4] = {(uint32_t)(e0 + c + P.env_id_offset), (uint32_t)f, (uint32_t)P.rng_step,
-                           (uint32_t)(P.rng_step >> 32)};
-        philox4x32(ctr, (uint32_t)P.rng_seed, (uint32_t)(P.rng_seed >> 32));
-        const float u1 = ((float)(ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
-        const float u2 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);
-        const float z = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+        const float z = z4[r];
         a4[r] = acc[r] + sd * z;
         s4[r] = sd;
-        if (real) lp += -0.5f * z * z - logf(sd) - 0.91893853320467274f;  // log sqrt(2 pi)
+        if (real) lp += -0.5f * z * z - __logf(sd) - 0.91893853320467274f;  // log sqrt(2 pi)
       }
       // sum over the four rows (actions 0-3, 4-7, 8-11, 12-15 of the env)
       auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(lp), __float_as_uint(lp), false, false);
@@ -721,76 +735,173 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
   }
   // Every layer's first weight fragments are requested before the barrier that ends the previous phase
   // (they depend on nothing the workgroup computes), so a layer starts with its weights landed instead
-  // of one L2 round trip after the barrier; the first layer's during the input staging.
+  // of one L2 round trip after the barrier.
   const PolicyLayer* Ls = P.layers;
   const PolicyLayer* LN = Ls + (CRITIC ? 7 : 3);
-  f8_t pa1[4][1][1];                   // actor: adaptation module L1
-  f8_t pl1[GO1_SPLIT_D1][1][2];        // actor / critic L1
-  if constexpr (!CRITIC) policy_prefetch<1, 1, PIN / 32, 4>(Ls + 0, wave, PW, lane, pa1);
-  else policy_prefetch<2, 1, PIN / 32, GO1_SPLIT_D1>(LN + 0, wave, PW, lane, pl1);
-  {
-    // inputs, in two passes through LDS (h1 is free until the first layer): the workgroup's history rows
-    // are one contiguous block of ne x H floats, read with coalesced loads (all of the thread's in flight)
-    // into a flat f32 copy; then each lane splits eight consecutive features of one env into one 16-byte
-    // record per plane, the lanes of a wave filling consecutive records (element-wise split stores hit
-    // the same LDS banks 8-16 times over: 12-16 k cycles of staging against ~3 k)
-    const int H = P.hist_dim;
-    float* flat = reinterpret_cast<float*>(&S.h1[0]);
+  // First layers, K-streamed in chunks of CG groups (PIN inputs) through the input planes: the adaptation
+  // module's L1 over the history (GA groups), the actor's / critic's L1 over [history, latent | priv] (GL
+  // groups).  The actor's groups from gl = H / 32 on hold latent inputs: they run after the adaptation
+  // module, from the last chunk's planes (the host guarantees they lie in it).  One chunk when the inputs
+  // fit PIN (the README configuration); the velocity task's 30-deep history (2,100) takes eight.
+  const int H = P.hist_dim, KIN = H + NP;
+  const int GA = (H + 31) / 32, GL = (KIN + 31) / 32, gl = H / 32;
+  constexpr int CG = PIN / 32;
+  const int nch = (GL + CG - 1) / CG, g_last = CG * (nch - 1);
+  const int g_pass = CRITIC ? GL : gl;  // L1 groups of the chunk pass
+  // the f32 staging copy (h1 is free until the L1 epilogue); one chunk: the workgroup's rows are one
+  // contiguous block of ne x H floats, copied with coalesced loads from one base pointer (all of the
+  // thread's in flight) before the accumulators are live
+  float* flat = reinterpret_cast<float*>(&S.h1[0]);
+  const int fs = nch == 1 ? H : PIN;
+  if (nch == 1) {
     constexpr int NI = (ET * 16 * PIN + 64 * PW - 1) / (64 * PW);
-    {
-      const float* src = P.obs_history + (size_t)e0 * H;
-      const int total = ne * H;
+    const float* src = P.obs_history + (size_t)e0 * H;
+    const int total = ne * H;
+    float v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = tid + i * 64 * PW;
+      v[i] = j < total ? src[j] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = tid + i * 64 * PW;
+      if (j < total) flat[j] = v[i];
+    }
+  }
+  f4_t accA[ET], accL[ET][2];
+  {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f4_t b = *reinterpret_cast<const f4_t*>(LN[0].b + 16 * (wave + i * PW) + 4 * q);
+#pragma unroll
+      for (int et = 0; et < ET; ++et) accL[et][i] = b;
+    }
+    if constexpr (!CRITIC) {
+      const f4_t b = *reinterpret_cast<const f4_t*>(Ls[0].b + 16 * wave + 4 * q);
+#pragma unroll
+      for (int et = 0; et < ET; ++et) accA[et] = b;
+    }
+  }
+  for (int ch = 0; ch < nch; ++ch) {
+    const int g0 = CG * ch, k0 = 32 * g0;
+    // inputs of the chunk, in two passes through LDS: coalesced loads of each env's window (all of the
+    // thread's in flight) into a flat f32 copy; then each lane splits eight consecutive features of one
+    // env into one 16-byte record per plane, the lanes of a wave filling consecutive records
+    // (element-wise split stores hit the same LDS banks 8-16 times over)
+    // the f32 copy holds the history part of the chunk: rows of fs floats (one chunk: copied above)
+    if (nch > 1) {
+      // thread -> (env, column phase): TPE threads per env row, one row pointer per thread (per-element
+      // addresses would be hoisted out of the chunk loop and spill)
+      constexpr int TPE = (64 * PW) / (ET * 16), NI = (PIN + TPE - 1) / TPE;
+      const int e = tid / TPE, kk = tid - e * TPE;
+      const bool live = e < ET * 16;
+      const bool row = live && e < ne;
+      const float* src = P.obs_history + (size_t)(e0 + (row ? e : 0)) * H;
       float v[NI];
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
-        const int j = tid + i * 64 * PW;
-        v[i] = j < total ? src[j] : 0.0f;
+        const int kc = kk + TPE * i, k = k0 + kc;
+        v[i] = (row && kc < PIN && k < H) ? src[k] : 0.0f;
       }
+      if (live) {
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int j = tid + i * 64 * PW;
-        if (j < total) flat[j] = v[i];
+        for (int i = 0; i < NI; ++i) {
+          const int kc = kk + TPE * i;
+          if (kc < PIN) flat[e * PIN + kc] = v[i];
+        }
       }
     }
     lds_barrier();
-    constexpr int NC = PIN / 8, NTASK = ET * 16 * NC;
-    for (int t = tid; t < NTASK; t += 64 * PW) {
-      const int c = t & 15, rest = t >> 4, kc = rest % NC, et = rest / NC, e = 16 * et + c;
-      float x[8];
+    {
+      constexpr int NC = PIN / 8, NTASK = ET * 16 * NC;
+      for (int t = tid; t < NTASK; t += 64 * PW) {
+        const int c = t & 15, rest = t >> 4, kc = rest % NC, et = rest / NC, e = 16 * et + c;
+        h8_t hi8, lo8;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int k = 8 * kc + r;
-        float val = 0.0f;
-        if (e < ne) {
-          if (k < H) val = flat[e * H + k];
-          else if (CRITIC && k < H + NP) val = P.privileged_obs[(size_t)(e0 + e) * NP + (k - H)];
+        for (int r = 0; r < 8; ++r) {
+          const int kl = 8 * kc + r, k = k0 + kl;
+          float x = 0.0f;
+          if (e < ne) {
+            if (k < H) x = flat[e * fs + kl];
+            else if (CRITIC && k < KIN) x = P.privileged_obs[(size_t)(e0 + e) * NP + (k - H)];
+          }
+          ovf_check(x, s_ovf);
+          hi8[r] = (_Float16)x;
+          lo8[r] = (_Float16)(x - (float)hi8[r]);
         }
-        x[r] = val;
+        S.xin[et].hi[kc][c] = hi8;
+        S.xin[et].lo[kc][c] = lo8;
       }
-      h8_t hi8, lo8;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        ovf_check(x[r], s_ovf);
-        hi8[r] = (_Float16)x[r];
-        lo8[r] = (_Float16)(x[r] - (float)hi8[r]);
-      }
-      S.xin[et].hi[kc][c] = hi8;
-      S.xin[et].lo[kc][c] = lo8;
     }
+    lds_barrier();
+    if (ch == 0) PSTAMP(1);
+    // the chunk's groups (uniform runtime bounds, no predicated MFMAs): [g0, gb) feed the adaptation
+    // module (actor) and L1; the next group's fragments are requested before this group's MFMAs
+    {
+      const int g1 = min(g0 + CG, GL), gb = CRITIC ? g1 : min(gl, g1);
+      // fragments two groups ahead: two register sets, the loop body unrolled by two
+      f8_t wA0, wL00, wL01, wA1, wL10, wL11;
+      auto load0 = [&](int g) {
+        if constexpr (!CRITIC) wA0 = reinterpret_cast<const f8_t*>(Ls[0].w)[((size_t)wave * GA + g) * 64 + lane];
+        wL00 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)wave * GL + g) * 64 + lane];
+        wL01 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)(wave + PW) * GL + g) * 64 + lane];
+      };
+      auto load1 = [&](int g) {
+        if constexpr (!CRITIC) wA1 = reinterpret_cast<const f8_t*>(Ls[0].w)[((size_t)wave * GA + g) * 64 + lane];
+        wL10 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)wave * GL + g) * 64 + lane];
+        wL11 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)(wave + PW) * GL + g) * 64 + lane];
+      };
+      auto group = [&](int gi, const f8_t& a, const f8_t& l0, const f8_t& l1) {
+#pragma unroll
+        for (int et = 0; et < ET; ++et) {
+          const h8_t xh = S.xin[et].hi[4 * gi + q][c], xl = S.xin[et].lo[4 * gi + q][c];
+          if constexpr (!CRITIC) accA[et] = mfma3(a, xh, xl, accA[et]);
+          accL[et][0] = mfma3(l0, xh, xl, accL[et][0]);
+          accL[et][1] = mfma3(l1, xh, xl, accL[et][1]);
+        }
+      };
+      if (g0 < gb) load0(g0);
+      if (g0 + 1 < gb) load1(g0 + 1);
+      for (int g = g0; g < gb; g += 2) {
+        group(g - g0, wA0, wL00, wL01);
+        if (g + 2 < gb) load0(g + 2);
+        if (g + 1 < gb) {
+          group(g + 1 - g0, wA1, wL10, wL11);
+          if (g + 3 < gb) load1(g + 3);
+        }
+      }
+      if constexpr (!CRITIC) {  // the history's last, partial group (adaptation module only; the actor's
+        if (GA > gl && gl >= g0 && gl < g1) {  // L1 takes it with the latent)
+          const f8_t a = reinterpret_cast<const f8_t*>(Ls[0].w)[((size_t)wave * GA + gl) * 64 + lane];
+#pragma unroll
+          for (int et = 0; et < ET; ++et)
+            accA[et] = mfma3(a, S.xin[et].hi[4 * (gl - g0) + q][c], S.xin[et].lo[4 * (gl - g0) + q][c], accA[et]);
+        }
+      }
+    }
+    if (ch + 1 < nch) lds_barrier();  // the next chunk's staging overwrites the planes and the copy
   }
-  lds_barrier();
-  PSTAMP(1);
+  // no barrier: the copy in h1 was last read before the last chunk's MFMAs (every wave has passed that
+  // barrier), so each wave stores its first-layer outputs as soon as its own MFMAs are done, overlapping the
+  // other waves' MFMAs (a barrier here made every wave run its ELUs at the same time)
   if constexpr (!CRITIC) {
+    // adaptation module epilogue: ELU, split into h1 rows 0-255
+#pragma unroll
+    for (int et = 0; et < ET; ++et) {
+      f4_t v = accA[et];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = elu(v[r]);
+      act_store4(v1[et][0], 4 * wave + q, c, v, s_ovf);
+    }
     // K-split partials of the adaptation module: 16 x 16 blocks in rows 384-511 of h1 (block t < 4 in
-    // the hi plane, t >= 4 in the lo plane), free until the actor's L1
+    // the hi plane, t >= 4 in the lo plane), free until the actor's L1 epilogue
     auto blk = [&](int et, int t) -> float(*)[16] {
       return reinterpret_cast<float(*)[16]>(t < 4 ? &S.h1[et].hi[384 / 8][0] : &S.h1[et].lo[384 / 8][0]) + 16 * (t & 3);
     };
     ActV va2[ET];  // adaptation L2 outputs: rows 256-383 of h1
 #pragma unroll
     for (int et = 0; et < ET; ++et) va2[et] = ActV{&S.h1[et].hi[256 / 8][0], &S.h1[et].lo[256 / 8][0]};
-    // adaptation module 261 -> 256 (xin rows >= hist_dim are still zero)
-    policy_tiles_e<1, 1, ET, PIN / 32, 4, true>(Ls + 0, vx, wave, PW, v1, true, lane, s_ovf, pa1);
     f8_t pa2[4];
     partial_load<4>(Ls[1], 8, wave & 7, 4 * (wave >> 3), lane, pa2);
     lds_barrier();
@@ -825,7 +936,6 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
     lds_barrier();
     PSTAMP(3);
     {  // 128 -> num_priv (the latent): one K group per wave (4 waves), partials summed by waves 0 .. ET-1
-      policy_prefetch<2, 1, PIN / 32, GO1_SPLIT_D1>(LN + 0, wave, PW, lane, pl1);  // the actor's L1
       if (wave < 4) {
         f4_t acc[ET];
         tile_partial_e<1, ET>(Ls[2], 4, 0, wave, va2, lane, acc, pa3);
@@ -844,7 +954,7 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
             float l = Ls[2].b[f];
 #pragma unroll
             for (int w = 0; w < 4; ++w) l += blk(et, w)[f][c];
-            act_store1(S.xin[et].v(), P.hist_dim + f, c, l, s_ovf);
+            act_store1(S.xin[et].v(), H + f - 32 * g_last, c, l, s_ovf);  // the last chunk's planes
             if (e < ne && P.latent) P.latent[(size_t)(e0 + e) * NP + f] = l;
           }
         }
@@ -852,13 +962,34 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
     }
     lds_barrier();
     PSTAMP(4);
+    // the actor's L1 groups that hold the latent
+    for (int g = gl; g < GL; ++g) {
+      const int gi = g - g_last;
+      f8_t w[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) w[i] = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)(wave + i * PW) * GL + g) * 64 + lane];
+#pragma unroll
+      for (int et = 0; et < ET; ++et) {
+        const h8_t xh = S.xin[et].hi[4 * gi + q][c], xl = S.xin[et].lo[4 * gi + q][c];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) accL[et][i] = mfma3(w[i], xh, xl, accL[et][i]);
+      }
+    }
   } else {
     PSTAMP(2);
     PSTAMP(3);
     PSTAMP(4);
   }
-  // actor (Ls 3-6) or critic (Ls 7-10), layer by layer
-  policy_tiles_e<2, 1, ET, PIN / 32, GO1_SPLIT_D1, true>(LN + 0, vx, wave, PW, v1, true, lane, s_ovf, pl1);  // 512
+  // actor (Ls 3-6) or critic (Ls 7-10), layer by layer; L1 epilogue: ELU, split into h1
+#pragma unroll
+  for (int et = 0; et < ET; ++et)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f4_t v = accL[et][i];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = elu(v[r]);
+      act_store4(v1[et][0], 4 * (wave + i * PW) + q, c, v, s_ovf);
+    }
   f8_t pl2[GO1_SPLIT_D2][1][1];
   policy_prefetch<1, 1, 512 / 32, GO1_SPLIT_D2>(LN + 1, wave, PW, lane, pl2);
   lds_barrier();
@@ -898,20 +1029,17 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
       if (P.actions) {
         float lp = 0.0f;
         f4_t a4, s4;
+        float z4[4];
+        normal4((uint32_t)(e0 + e + P.env_id_offset), q, P.rng_step, P.rng_seed, z4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int f = 4 * q + r;
           const bool real = f < P.num_actions;
           const float sd = real ? P.std[f] : 1.0f;
-          uint32_t ctr[4] = {(uint32_t)(e0 + e + P.env_id_offset), (uint32_t)f, (uint32_t)P.rng_step,
-                             (uint32_t)(P.rng_step >> 32)};
-          philox4x32(ctr, (uint32_t)P.rng_seed, (uint32_t)(P.rng_seed >> 32));
-          const float u1 = ((float)(ctr[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
-          const float u2 = (float)(ctr[1] >> 8) * (1.0f / 16777216.0f);
-          const float z = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+          const float z = z4[r];
           a4[r] = acc[r] + sd * z;
           s4[r] = sd;
-          if (real) lp += -0.5f * z * z - logf(sd) - 0.91893853320467274f;  // log sqrt(2 pi)
+          if (real) lp += -0.5f * z * z - __logf(sd) - 0.91893853320467274f;  // log sqrt(2 pi)
         }
         auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(lp), __float_as_uint(lp), false, false);
         lp = __uint_as_float(x[0]) + __uint_as_float(x[1]);
@@ -1013,8 +1141,18 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
   if (!args || args->n_envs <= 0 || !args->obs_history || !args->privileged_obs || !args->action_mean ||
       !args->value)
     return fail(GO1_RT_E_ARG, "go1_policy_forward: bad argument");
-  if (args->num_priv < 1 || args->num_priv > 8 || args->hist_dim + args->num_priv > PIN || args->num_actions > 16)
+  if (args->num_priv < 1 || args->num_priv > 8 || args->hist_dim < 1 || args->num_actions > 16)
     return fail(GO1_RT_E_ARG, "go1_policy_forward: input / latent / action width outside the compiled architecture");
+  {
+    // variant 1 stages all inputs at once (PIN); variant 0 streams them in chunks of PIN, and the actor's
+    // groups that hold the latent must lie in the last chunk (its planes receive the latent)
+    const int kin = args->hist_dim + args->num_priv, gl = args->hist_dim / 32, GL = (kin + 31) / 32;
+    const int g_last = (PIN / 32) * ((GL + PIN / 32 - 1) / (PIN / 32) - 1);
+    if (args->variant == 1 && kin > PIN)
+      return fail(GO1_RT_E_ARG, "go1_policy_forward: variant 1 takes at most 288 history + privileged inputs");
+    if (gl < g_last || kin > 16384)
+      return fail(GO1_RT_E_ARG, "go1_policy_forward: history width not supported by the chunked first layers");
+  }
   for (int i = 0; i < GO1_POLICY_LAYERS; ++i)
     if (!args->layers[i].w || !args->layers[i].b || !args->layers[i].wf)
       return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer (split, bias and f32 weights are required)");

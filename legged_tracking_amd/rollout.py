@@ -149,7 +149,12 @@ class FusedPolicy:
         want = [(256, h), (128, 256), (npv, 128), (512, h + npv), (256, 512), (128, 256), (None, 128),
                 (512, h + npv), (256, 512), (128, 256), (1, 128)]
         ok = all(w[0] in (None, s[0]) and w[1] == s[1] for s, w in zip(shapes, want))
-        return ok and 1 <= npv <= 8 and h + npv <= 288 and shapes[6][0] <= 16 and isinstance(a[1], nn.ELU)
+        # any history width for the default launch (inputs streamed in chunks of 288), as long as the
+        # 32-wide groups that hold the latent sit in the last chunk (go1_policy_forward checks the same)
+        kin, gl, GL = h + npv, h // 32, -(-(h + npv) // 32)
+        g_last = 9 * (-(-GL // 9) - 1)
+        return (ok and 1 <= npv <= 8 and kin <= 16384 and gl >= g_last and shapes[6][0] <= 16
+                and isinstance(a[1], nn.ELU))
 
     def pack(self):
         ac = self.ac

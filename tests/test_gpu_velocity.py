@@ -280,15 +280,15 @@ def test_vel_native_run_properties():
 
 def test_vel_runner_learns(tmp_path):
     """scripts/train_velocity_tracking.py's loop (Runner.learn, ppo_cse/__init__.py) over the HIP velocity env:
-    rollout with the 30-deep history (2100 inputs: the policy runs on torch / hipBLASLt, the fused policy
-    kernel covers inputs up to 272), GAE and record kernels, PPO.update, checkpoints."""
+    rollout with the 30-deep history (2100 inputs, streamed through the fused policy kernel in chunks of
+    288), GAE and record kernels, PPO.update, checkpoints."""
     from legged_tracking_amd import rollout as R
     from legged_tracking_amd.env import HistoryWrapper
     n = 512
     env = HistoryWrapper(VEL.VelocityTrackingEasyEnv(sim_device=DEV, num_envs=n))
     assert env.num_obs_history == 2100 and env.num_privileged_obs == 2
     runner = R.Runner(env, device=DEV, save_dir=str(tmp_path))
-    assert runner.alg.fused is None  # 2100 history inputs: torch path for the policy
+    assert runner.alg.fused is not None  # the fused policy kernel streams the 2,100 history inputs
     w0 = [p.detach().clone() for p in runner.alg.actor_critic.parameters()]
     runner.learn(num_learning_iterations=2, init_at_random_ep_len=True)
     torch.cuda.synchronize()

@@ -453,3 +453,37 @@ def test_runner_learn_on_gpu_through_hip_env_and_rollout_kernels(tmp_path):
     sd = torch.load(tmp_path / "checkpoints" / "ac_weights.pt", weights_only=True, map_location="cpu")
     assert set(sd) == set(after)
     assert env.extras["diverged"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hist,npriv", [(2100, 2), (1020, 6), (70, 2)])
+def test_fused_policy_kernel_streams_long_histories(hist, npriv):
+    """The default launch streams the first layers' inputs in chunks of 288 (the velocity task's 30-deep
+    history: 2,100 inputs, BASELINE configs[1]; a 1,020-wide history whose 6-wide latent straddles two
+    32-input groups; a short one): against an f64 forward of the same weights, a ragged batch, and the
+    single-workgroup variant refusing what it cannot stage."""
+    torch.manual_seed(3)
+    ac = R.ActorCritic(70, npriv, hist, 12).to("cuda:0")
+    pol = R.HipRolloutKernels().policy(ac)
+    assert pol is not None
+    n = 1000 + 25
+    g = torch.Generator(device="cuda").manual_seed(5)
+    h = torch.randn(n, hist, device="cuda", generator=g)
+    p = torch.randn(n, npriv, device="cuda", generator=g)
+    mean, value, latent = pol.forward(h, p)
+    torch.cuda.synchronize()
+    ac64 = R.ActorCritic(70, npriv, hist, 12).double()
+    ac64.load_state_dict({k: v.double().cpu() for k, v in ac.state_dict().items()})
+    with torch.no_grad():
+        h64, p64 = h.double().cpu(), p.double().cpu()
+        lt = ac64.adaptation_module(h64)
+        mt = ac64.actor_body(torch.cat((h64, lt), -1))
+        vt = ac64.critic_body(torch.cat((h64, p64), -1))
+    for got, want in ((latent, lt), (mean, mt), (value, vt)):
+        want = want.numpy()
+        np.testing.assert_allclose(got.cpu().numpy(), want, rtol=2e-5, atol=2e-5 * np.abs(want).max())
+    assert int(pol.overflow.item()) == 0
+    if hist + npriv > 288:
+        pol.variant = 1
+        with pytest.raises(RuntimeError, match="variant 1"):
+            pol.forward(h, p)
