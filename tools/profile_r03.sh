@@ -41,3 +41,5 @@ run pol_sq2 240 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS 
 run pol_tcp 240 --pmc TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d "$OUT/pol_tcp" -o p -- python3 $R
 run pol_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pol_fetch" -o p -- python3 $R
 cd "$ROOT" && timeout -k 10 600 python bench.py --steps 500 --warmup 50 > "$OUT/bench_full.log" 2>&1; echo "bench rc=$?"
+# whole-loop traces are tens of MB: keep their stats only (gpurun copies back at most 64 MiB)
+rm -f "$OUT"/learn/*_kernel_trace.csv "$OUT"/vel_learn/*_kernel_trace.csv
