@@ -1616,7 +1616,13 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     rhs[i] = -(p0[i].x + pp6[i].x);
     rhs[3 + i] = -(p0[i].y + pp6[i].y);
   }
+#ifdef GO1_ABL_NO_BASESOLVE  // ablation build only: the base's 6x6 solve replaced by a diagonal scaling
+#pragma unroll
+  for (int i = 0; i < 6; ++i) a0[i] = rhs[i] * 0.05f;
+  (void)I0;
+#else
   solve6p(I0, rhs, a0);
+#endif
   MARK(base_solve_done);
   // ---- forward pass
   float qdd[3];
