@@ -51,7 +51,7 @@ extern "C" {
 #define GO1_MAX_TRAJ 16    /* waypoints per trajectory (Cfg.commands.traj_length) */
 #define GO1_U_NOISE 47     /* parity-mode uniform slots: 0..46 reset / DR draws, then one per obs column
                               (compute_observations noise, :472-473), then the trajectory draws */
-#define GO1_MODEL_FLOATS 175
+#define GO1_MODEL_FLOATS 178
 #define GO1_ACTUATOR_FLOATS 1313 /* w1[32][6] b1[32] w2[32][32] b2[32] w3[32] b3[1] */
 #define GO1_GRID_X 21
 #define GO1_GRID_Y 11

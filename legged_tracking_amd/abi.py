@@ -19,7 +19,7 @@ def lag_steps(decimation):
     return (GO1_LAG_SLOTS + int(decimation) - 1) // int(decimation)
 GO1_MAX_TRAJ = 16
 GO1_U_NOISE = 47
-GO1_MODEL_FLOATS = 175
+GO1_MODEL_FLOATS = 178
 GO1_ACTUATOR_FLOATS = 1313
 GO1_GRID_X = 21
 GO1_GRID_Y = 11

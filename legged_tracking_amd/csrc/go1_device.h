@@ -1187,6 +1187,108 @@ __device__ __forceinline__ void point_kin(const float* Rb, const float* pb, cons
   mat3_vec(Rb, vl, vw);
 }
 
+// Hip capsule contact (model.py HIP_CAPSULE_*: the two ends of the capsule's segment as spheres of its
+// radius on the hip link's y axis, oracle/go1_oracle.c phys_substep j == 0).  Every role lane of a leg
+// evaluates its own leg's hip (redundantly over the four roles, like the leg's ABA: no cross-lane
+// sums), the two spheres in the halves of f2.  A wave whose hip spheres all clear both layers (the
+// contact's own penetration test, evaluated first) skips the force and the added mass, which are then
+// exactly zero (as the oracle computes them): on open ground and with the trunk level the hips never
+// touch, and the skip costs the kinematics and one height query.
+// Adds the added mass to the hip's articulated inertia IA and the force to its bias force pA (hip
+// frame, (angular, linear) pairs); Fw = the world force, the hip's reported contact force.
+__device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const float* R, const float* pos,
+                                            const f2* vbp, const float* org, float cq, float sq, float qd0,
+                                            f2 yy, float hr, float h, const float* g, SIP& IA, f2* pA,
+                                            float* Fw) {
+  Fw[0] = Fw[1] = Fw[2] = 0.0f;
+  // sphere centres from the hip joint, base frame: Rx(q) (0, y, 0) = (0, c y, s y)
+  const f2 rby = cq * yy, rbz = sq * yy;
+  // base frame: p = org + r, v = v_b + w_b x org + (w_b + qd e_x) x r
+  const float w0 = vbp[0].x, w1 = vbp[1].x, w2 = vbp[2].x, wh0 = w0 + qd0;
+  const float vo0 = vbp[0].y + (w1 * org[2] - w2 * org[1]);
+  const float vo1 = vbp[1].y + (w2 * org[0] - w0 * org[2]);
+  const float vo2 = vbp[2].y + (w0 * org[1] - w1 * org[0]);
+  const f2 pb[3] = {f2s(org[0]), org[1] + rby, org[2] + rbz};
+  const f2 vpb[3] = {vo0 + (w1 * rbz - w2 * rby), vo1 - wh0 * rbz, vo2 + wh0 * rby};
+  f2 pw[3], vw[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    pw[i] = pos[i] + (R[3 * i] * pb[0] + R[3 * i + 1] * pb[1] + R[3 * i + 2] * pb[2]);
+    vw[i] = R[3 * i] * vpb[0] + R[3 * i + 1] * vpb[1] + R[3 * i + 2] * vpb[2];
+  }
+  HQ qa, qb;
+  hq_fetch(T, pw[0].x, pw[1].x, qa);
+  hq_fetch(T, pw[0].y, pw[1].y, qb);
+  auto near = [&](const HQ& q, float z) {  // sphere_contact_im's own penetration test, bit for bit
+    f2 hh, gx, gy;
+    hq_finish(T, q, hh, gx, gy);
+    const f2 dv = f2{1.0f, -1.0f} * (hh - z) + hr;
+    return dv.x > 0.0f || dv.y > 0.0f;
+  };
+  if (!__any(near(qa, pw[2].x) || near(qb, pw[2].y))) return;
+  float Fa[3], Fb[3], Ma[6], Mb[6];
+  {
+    const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
+    const float pb2[3] = {pw[0].y, pw[1].y, pw[2].y}, vb2[3] = {vw[0].y, vw[1].y, vw[2].y};
+    sphere_contact_im(T, qa, C, pa, va, hr, h, Fa, Ma);
+    sphere_contact_im(T, qb, C, pb2, vb2, hr, h, Fb, Mb);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Fw[i] = Fa[i] + Fb[i];
+  // the force the added mass sees is F - Mp g (accelerations relative to free fall, as the leg points)
+  const f2 Mw[6] = {f2{Ma[0], Mb[0]}, f2{Ma[1], Mb[1]}, f2{Ma[2], Mb[2]},
+                    f2{Ma[3], Mb[3]}, f2{Ma[4], Mb[4]}, f2{Ma[5], Mb[5]}};
+  f2 Fd[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    Fd[i] = f2{Fa[i], Fb[i]} - (Mw[s3i(i, 0)] * g[0] + Mw[s3i(i, 1)] * g[1] + Mw[s3i(i, 2)] * g[2]);
+  // hip link rotation (world <- hip): R Rx(q), columns R0, c R1 + s R2, c R2 - s R1
+  float Rh[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    Rh[3 * i] = R[3 * i];
+    Rh[3 * i + 1] = cq * R[3 * i + 1] + sq * R[3 * i + 2];
+    Rh[3 * i + 2] = cq * R[3 * i + 2] - sq * R[3 * i + 1];
+  }
+  // hip-frame force f = Rh^T Fd and moment lp x f with lp = (0, y, 0): (y fz, 0, -y fx)
+  f2 f[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) f[j] = Rh[j] * Fd[0] + Rh[3 + j] * Fd[1] + Rh[6 + j] * Fd[2];
+  const f2 m0 = yy * f[2], m2 = -(yy * f[0]);
+  pA[0] -= f2{m0.x + m0.y, f[0].x + f[0].y};
+  pA[1] -= f2{0.0f, f[1].x + f[1].y};
+  pA[2] -= f2{m2.x + m2.y, f[2].x + f[2].y};
+  // added mass M = Rh^T Mp Rh about the hip origin, S = lp~: S M S^T has (0,0) y^2 M22, (0,2) -y^2 M20,
+  // (2,2) y^2 M00 and zeros elsewhere; S M has rows (y M2., 0, -y M0.)
+  f2 MR[9], M[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      MR[3 * i + j] = Mw[s3i(i, 0)] * Rh[j] + Mw[s3i(i, 1)] * Rh[3 + j] + Mw[s3i(i, 2)] * Rh[6 + j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = i; j < 3; ++j) {
+      M[3 * i + j] = Rh[i] * MR[j] + Rh[3 + i] * MR[3 + j] + Rh[6 + i] * MR[6 + j];
+      M[3 * j + i] = M[3 * i + j];
+    }
+  const f2 y2 = yy * yy;
+  const f2 A[6] = {y2 * M[8], f2s(0.0f), -(y2 * M[6]), f2s(0.0f), f2s(0.0f), y2 * M[0]};  // 00 01 02 11 12 22
+  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const f2 c = M[3 * II[k] + JJ[k]];
+    IA.ac[k] += f2{A[k].x + A[k].y, c.x + c.y};
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const f2 b0 = yy * M[6 + j], b2 = -(yy * M[j]);
+    IA.b[j] += b0.x + b0.y;
+    IA.b[6 + j] += b2.x + b2.y;
+  }
+}
+
 __device__ __forceinline__ void point_force(const float* Rb, const float* lp, const float* F, float* fs) {
   float f[3], n[3];
   mat3T_vec(Rb, F, f);
@@ -1285,7 +1387,7 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // kinematics and ABA passes redundantly (base quantities on all 16 lanes), and
 // split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
 // two per lane, so each wave has four envs and the whole grid fills every SIMD.
-// cf_out: this lane's reported contact forces (thigh, calf, foot of its leg; base).
+// cf_raw: this lane's reported contact forces (its two points; its leg's hip).
 // `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
 // in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
@@ -1320,6 +1422,9 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   const float foot_r = foot[3];
   const float thigh_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3];
   const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
+  const float hip_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 2];
+  const float hip_y0 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 3], hip_y1 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 4];
+  float Fhip[3] = {0.0f, 0.0f, 0.0f};  // the hip capsule's world force (the leg's, on every role)
   float cs[3][2];
   float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
   f2 cjp[3][3], pAp[3][3];  // c_j and the articulated bias force as (angular, linear) pairs
@@ -1491,7 +1596,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     for (int i = 0; i < 9; ++i) { cin[0].b[i] = SM[i].x; cin[1].b[i] = SM[i].y; }
   }
 #else  // ablation build only: no contacts
-  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
+  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)hip_r; (void)hip_y0; (void)hip_y1; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
 #pragma unroll
@@ -1585,6 +1690,13 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
         if (j == 2) sip_add(IA, ci_th);  // the thigh's contact added masses
 #pragma unroll
         for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
+#ifndef GO1_ABL_NO_CONTACT
+#ifndef GO1_ABL_NO_HIP  // ablation build only: no hip capsules
+        if (j == 1)  // the hip capsule's contact, on the hip's inertia and bias force
+          hip_contact(T, C, R, S.pos, vbp, origin, cs[0][0], cs[0][1], S.qd[0], msy * f2{hip_y0, hip_y1}, hip_r, h,
+                      g, IA, pAp[0], Fhip);
+#endif
+#endif
       } else {
         Ip = It;
         sip_add(Ip, ci_bs);  // this leg's trunk corners: summed over the legs with the hips below
@@ -1621,7 +1733,17 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   for (int i = 0; i < 6; ++i) a0[i] = rhs[i] * 0.05f;
   (void)I0;
 #else
+#ifdef GO1_ABL_NO_CHOL  // ablation build only: the Cholesky alone compiled out, its inputs kept live
+  float tr = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) tr += I0.ac[k].x + I0.ac[k].y;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) tr += I0.b[k];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) a0[i] = rhs[i] * tr * 1e-3f;
+#else
   solve6p(I0, rhs, a0);
+#endif
 #endif
   MARK(base_solve_done);
   // ---- forward pass
@@ -1692,14 +1814,15 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   for (int i = 0; i < 3; ++i) {
     cf_raw[i] = Fpt[i].x;
     cf_raw[3 + i] = Fpt[i].y;
+    cf_raw[6 + i] = Fhip[i];
   }
 }
 
 // reported contact forces from the last sub-step's per-lane values: thigh, calf, foot of
-// the lane's leg (role sums) and the base (role and leg sums)
-__device__ __forceinline__ void cf_sum(const float* cf_raw, int role, float* cf_leg, float* cf_base) {
+// the lane's leg (role sums), the base (role and leg sums) and the leg's hip
+__device__ __forceinline__ void cf_sum(const float* cf_raw, int role, float* cf_leg, float* cf_base, float* cf_hip) {
   // cf_raw: world forces of the lane's two points (x, y); rows 0 (thigh, thigh), 1 (thigh, corner),
-  // 2 (calf, calf), 3 (foot, corner)
+  // 2 (calf, calf), 3 (foot, corner); then the leg's hip (already whole on every role)
   float v[12];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -1713,7 +1836,10 @@ __device__ __forceinline__ void cf_sum(const float* cf_raw, int role, float* cf_
 #pragma unroll
   for (int i = 0; i < 9; ++i) cf_leg[i] = v[i];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) cf_base[i] = qsum(v[9 + i]);
+  for (int i = 0; i < 3; ++i) {
+    cf_base[i] = qsum(v[9 + i]);
+    cf_hip[i] = cf_raw[6 + i];
+  }
 }
 
 #pragma clang fp contract(off)

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // ---------------- decimation loop (:76-82): lag ring pushed per sim step (:940-942)
   float torque[3], tgt[3];
-  float cf_raw[6] = {0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3];
+  float cf_raw[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
   for (int sub = 0; sub < dec; ++sub) {
     {
       const int m = 6 - sub;
@@ -322,7 +322,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int i = 0; i < 13; ++i) root[i] = A.inj_root[(size_t)e * 13 + i];
     const float* ic = A.inj_contact + (size_t)e * NB * 3;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) cf_base[i] = ic[i];
+    for (int i = 0; i < 3; ++i) {
+      cf_base[i] = ic[i];
+      cf_hip[i] = ic[(1 + leg * 4) * 3 + i];
+    }
 #pragma unroll
     for (int b = 0; b < 3; ++b)
 #pragma unroll
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 3; ++i) { fp[i] = ft[i]; fv[i] = ft[3 + i]; }
   } else {
-    cf_sum(cf_raw, role, cf_leg, cf_base);
+    cf_sum(cf_raw, role, cf_leg, cf_base, cf_hip);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       root[i] = P.pos[i]; root[7 + i] = P.wv[i].y; root[10 + i] = P.wv[i].x;
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float* o = A.contact_forces + (size_t)e * NB * 3;
     if (leg == 0) { o[0] = cf_base[0]; o[1] = cf_base[1]; o[2] = cf_base[2]; }
     float* ol = o + (1 + leg * 4) * 3;
-    ol[0] = 0.0f; ol[1] = 0.0f; ol[2] = 0.0f;
+    ol[0] = cf_hip[0]; ol[1] = cf_hip[1]; ol[2] = cf_hip[2];
 #pragma unroll
     for (int i = 0; i < 9; ++i) ol[3 + i] = cf_leg[i];
   }

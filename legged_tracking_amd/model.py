@@ -38,6 +38,14 @@ FOOT = dict(mass=0.06, com=(0.0, 0.0, -0.213), inertia=(9.6e-06, 0.0, 0.0, 9.6e-
 TRUNK_BOX = (0.3762, 0.0935, 0.114)       # go1.urdf:54-56
 THIGH_BOX_HALF_WIDTH = 0.0245 / 2         # go1.urdf:148-153 (0.213 x 0.0245 x 0.034)
 CALF_BOX_HALF_WIDTH = 0.016 / 2           # go1.urdf:176-181
+# hip collision cylinder, axis along the hip link's y, centred 0.045 m outboard of the hip joint
+# (go1.urdf:106-111 FR at y = -0.045, :229-234 FL at +0.045); Isaac Gym's
+# replace_cylinder_with_capsule (legged_robot_trajectory_tracking_config.py:214-215) makes it a capsule of
+# the same radius whose segment is the cylinder's axis (half length 0.02).  A capsule's deepest point
+# against a locally planar surface is an end of its segment, so the native model carries the two
+# segment ends as spheres of the capsule's radius (FL values; y mirrors with the side).
+HIP_CAPSULE_RADIUS = 0.046
+HIP_CAPSULE_Y = (0.045 - 0.02, 0.045 + 0.02)
 
 
 def _mirror(body, sx, sy):
@@ -103,8 +111,9 @@ def joint_origins(leg):
 # Per body: mass, com[3], inertia about COM [xx, xy, xz, yy, yz, zz] (10 floats)
 # Base first, then per leg (FL, FR, RL, RR): hip, thigh, calf   -> 13 bodies x 10
 # Then per leg: hip origin[3], thigh origin[3], calf origin[3]  -> 4 x 9
-# Then foot offset[3], foot radius, trunk half extents[3], thigh radius, calf radius
-MODEL_FLOATS = 13 * 10 + 4 * 9 + 3 + 1 + 3 + 1 + 1  # 175
+# Then foot offset[3], foot radius, trunk half extents[3], thigh radius, calf radius,
+# hip capsule radius, hip capsule segment ends y[2] (FL)
+MODEL_FLOATS = 13 * 10 + 4 * 9 + 3 + 1 + 3 + 1 + 1 + 1 + 2  # 178
 
 
 def model_block() -> np.ndarray:
@@ -125,6 +134,8 @@ def model_block() -> np.ndarray:
     out.extend([TRUNK_BOX[0] / 2, TRUNK_BOX[1] / 2, TRUNK_BOX[2] / 2])
     out.append(THIGH_BOX_HALF_WIDTH)
     out.append(CALF_BOX_HALF_WIDTH)
+    out.append(HIP_CAPSULE_RADIUS)
+    out.extend(HIP_CAPSULE_Y)
     a = np.asarray(out, dtype=np.float64)
     assert a.shape == (MODEL_FLOATS,), a.shape
     return a

@@ -206,6 +206,7 @@ typedef struct {
   Body leg[4][3];
   real origin[4][3][3]; /* joint origins in parent frame */
   real foot[3], foot_r, trunk_half[3], thigh_r, calf_r;
+  real hip_r, hip_y[2]; /* hip capsule: radius, segment ends on the hip link's y axis (FL; mirrored by side) */
 } Model;
 
 static void load_model(const go1_config* c, Model* M) {
@@ -232,6 +233,9 @@ static void load_model(const go1_config* c, Model* M) {
   for (int i = 0; i < 3; ++i) M->trunk_half[i] = p[k++];
   M->thigh_r = p[k++];
   M->calf_r = p[k++];
+  M->hip_r = p[k++];
+  M->hip_y[0] = p[k++];
+  M->hip_y[1] = p[k++];
 }
 
 static void cross3(const real* a, const real* b, real* o) {
@@ -518,6 +522,9 @@ static void sphere_contact(const TerrainView* T, const ContactParams* C, const r
  *   thigh: (0,0,-0.071), (0,0,-0.142), knee (0,0,-0.213)   radius thigh_r
  *   calf : (0,0,-0.071), (0,0,-0.142)                     radius calf_r
  *   foot : foot offset (calf frame)                        radius foot_r
+ *   hip  : (0, +-hip_y[0], 0), (0, +-hip_y[1], 0)            radius hip_r (the ends of the hip
+ *          capsule's segment, go1.urdf:106-111 as a capsule per replace_cylinder_with_capsule;
+ *          the sign is the leg's side)
  * Trunk: the 8 corners of the collision box (radius 0). */
 #define N_THIGH_PTS 3
 #define N_CALF_PTS 2
@@ -642,7 +649,22 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       cross3(B->com, fg, cg);
       for (int i = 0; i < 3; ++i) { fext[i] += cg[i]; fext[3 + i] += fg[i]; }
       int body_idx = 1 + l * 4 + j; /* hip, thigh, calf */
-      if (j == 1) {
+      if (j == 0) {
+        const real sy = (l & 1) ? -1.0 : 1.0; /* legs FL, FR, RL, RR */
+        for (int p = 0; p < 2; ++p) {
+          real lp[3] = {0, sy * M->hip_y[p], 0}, pw[3], vw[3], F[3];
+          point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
+          if (g_implicit_contact) {
+            real Mp[3][3] = {{0}};
+            sphere_contact_im(T, &C, pw, vw, M->hip_r, F, h, Mp);
+            point_inertia(Rw[j], lp, Mp, &IA[j]);
+          } else {
+            sphere_contact(T, &C, pw, vw, M->hip_r, F);
+          }
+          point_force(Rw[j], lp, F, fext);
+          if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
+        }
+      } else if (j == 1) {
         for (int p = 0; p < N_THIGH_PTS; ++p) {
           real lp[3] = {0, 0, THIGH_PTS_Z[p]}, pw[3], vw[3], F[3];
           point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);

@@ -17,7 +17,8 @@ Scenarios (plane terrain, 64 envs, random orientation / velocities / joint angle
     COM falls with g).  Measured 4.2e-4 relative (HIP and oracle).  Bound 1e-3.
   * static stance (gravity, actuator net holding the default pose, zero actions), 150 env steps:
     the base settles (measured height 0.263 m, |v| 5e-4 m/s) and the reported contact forces carry
-    the weight (measured sum F_z / M g = 1.000), HIP and oracle alike.  Bounds: height in
+    the weight (measured sum F_z / M g = 1.000), HIP and oracle alike, with the hip capsules clear
+    of the plane (no hip force; tests/test_hip_capsule.py has the hips in contact).  Bounds: height in
     (0.20, 0.40) m, |v| < 5e-2, |sum F_z / M g - 1| < 2 %.
 """
 import numpy as np
@@ -79,6 +80,7 @@ def _stance(backend):
     hist = []
     for t, (s, cf, reset) in enumerate(_roll(backend, *_args(backend, c, td, ter, st, scales), 150, GZ)):
         assert not reset.any()
+        assert np.abs(cf.reshape(st.n, 17, 3)[:, 1::4]).max() == 0.0  # the hip capsules clear the plane
         if t >= 130:
             hist.append((s["root"].copy(), cf.sum(axis=1)[:, 2]))
     z = np.array([h[0][:, 2] for h in hist])
