@@ -526,13 +526,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   MARK(post_kin_done);
   // DR every rand_interval (:822-824)
+  // slots 34 .. 46 = Philox blocks 8 .. 11: lane sub16 < 4 of the env draws block 8 + sub16 and the
+  // env's lanes read their slots back from LDS (one evaluation per lane instead of four in a row; one
+  // wave per block: its LDS operations complete in order)
+  __shared__ float s_u[SEPB][32];
   const bool dr_step = ep % CI(rand_interval) == 0;
   if (dr_step) {
-    const float sv = rng(34) * CI(strength_range) + CI(strength_lo);
+    if (sub16 < 4) {
+      float uq[4];
+      rng.quad(8 + sub16, uq);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_u[el][4 * sub16 + k] = uq[k];
+    }
+    const float sv = s_u[el][34 - 32] * CI(strength_range) + CI(strength_lo);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       strength[j] = sv;
-      offset[j] = rng(35 + leg * 3 + j) * CI(offset_range) + CI(offset_lo);
+      offset[j] = s_u[el][35 + leg * 3 + j - 32] * CI(offset_range) + CI(offset_lo);
     }
   }
   const float rel_norm = norm2_f(rel_lin[0], rel_lin[1]);
@@ -822,18 +832,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float* o = A.obs + (size_t)e * NO;
   float* oh = A.obs_history ? A.obs_history + (size_t)e * NO : nullptr;  // optional second copy
   const float clip = CI(clip_obs);
-  // noise uniforms rng(47 + i) (:472-473): every lane draws exactly two Philox blocks, the
-  // same two-block code path in all lanes (the per-value calls of the two store branches
-  // ran five Philox evaluations per wave, one after the other): role r < 3 needs slots
-  // 52 + d (dof pos) and 64 + d (dof vel), role 3 slots 47, 48, 49 (gravity)
+  // noise uniforms rng(47 + i) (:472-473): the env's observed noisy columns use slots 47 .. 49
+  // (gravity), 52 .. 63 (dof pos) and 64 .. 75 (dof vel), i.e. Philox blocks 11 .. 18: lane
+  // sub16 < 8 draws block 11 + sub16 into LDS (one evaluation per lane; it was two), and role
+  // r < 3 reads slots 52 + d and 64 + d, role 3 slots 47, 48, 49
   const int dn = leg * 3 + (role < 3 ? role : 0);
-  float uA[4], uB[4];
-  {
-    const int sa = role < 3 ? 52 + dn : 44, sb = role < 3 ? 64 + dn : 48;
-    if (CI(add_noise)) {
-      rng.quad(sa >> 2, uA);
-      rng.quad(sb >> 2, uB);
+  float un = 0.0f, uv = 0.0f, ug[3] = {0.0f, 0.0f, 0.0f};
+  if (CI(add_noise)) {
+    if (sub16 < 8) {
+      float uq[4];
+      rng.quad(11 + sub16, uq);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_u[el][4 * sub16 + k] = uq[k];
     }
+    un = s_u[el][52 + dn - 44];
+    uv = s_u[el][64 + dn - 44];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ug[i] = s_u[el][47 + i - 44];
   }
   auto put = [&](int i, float v, float nv, float u, bool noisy) {
     if (noisy && CI(add_noise)) v = v + (2.0f * u - 1.0f) * nv;
@@ -844,9 +859,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // role r < 3 writes joint r of its leg; role 3 of leg 0 writes gravity and commands, role 3
   // of leg 1 the episode progress (timestep_in_obs, :375-377: post-reset episode length)
   if (role == 3 && leg == 0) {
-    put(0, pg[0], CI(noise_gravity), uA[3], true);
-    put(1, pg[1], CI(noise_gravity), uB[0], true);
-    put(2, pg[2], CI(noise_gravity), uB[1], true);
+    put(0, pg[0], CI(noise_gravity), ug[0], true);
+    put(1, pg[1], CI(noise_gravity), ug[1], true);
+    put(2, pg[2], CI(noise_gravity), ug[2], true);
     put(3, cmd[0] * 1.0f, 0.0f, 0.0f, false);
     put(4, cmd[1] * 1.0f, 0.0f, 0.0f, false);
   }
@@ -855,8 +870,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (role < 3) {
     const int j = role, d = dn;
     const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act);
-    const float un = sel4((52 + d) & 3, uA[0], uA[1], uA[2], uA[3]);
-    const float uv = sel4((64 + d) & 3, uB[0], uB[1], uB[2], uB[3]);
     put(5 + d, (qj - s_phys[LDS_DDP + d]) * CI(obs_scale_dof_pos), CI(noise_dof_pos), un, true);
     put(17 + d, qdj * CI(obs_scale_dof_vel), CI(noise_dof_vel), uv, true);
     put(29 + d, aj, 0.0f, 0.0f, false);

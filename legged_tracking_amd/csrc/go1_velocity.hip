@@ -390,13 +390,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     g[8 + leg] = desired;
   }
   // ---- DR every rand_interval (:714-717)
+  // slots 2 .. 14 = Philox blocks 0 .. 3: lane sub16 < 4 of the env draws block sub16 into LDS and the
+  // env's lanes read their slots back (one evaluation per lane instead of four in a row; one wave per
+  // block: its LDS operations complete in order)
+  __shared__ float s_u[SEPB][48];
   const bool dr_step = ep % v->rand_interval == 0;
   if (dr_step) {
-    const float sv = rng(GO1_VEL_U_DR) * v->strength_range + v->strength_lo;
+    if (sub16 < 4) {
+      float uq[4];
+      rng.quad(sub16, uq);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_u[el][4 * sub16 + k] = uq[k];
+    }
+    const float sv = s_u[el][GO1_VEL_U_DR] * v->strength_range + v->strength_lo;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       strength[j] = sv;
-      offset[j] = rng(GO1_VEL_U_DR + 1 + leg * 3 + j) * v->offset_range + v->offset_lo;
+      offset[j] = s_u[el][GO1_VEL_U_DR + 1 + leg * 3 + j] * v->offset_range + v->offset_lo;
     }
   }
   // ---- check_termination (:156-166): base contact, time-out, body height (measured_heights = 0 on a plane)
@@ -634,14 +644,25 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (oh) oh[i] = val;
   };
   auto noise = [&](float val, int i, float u) { return noisy ? val + (2.0f * u - 1.0f) * v->noise_vec[i] : val; };
+  // the noisy columns' uniforms (gravity 0 .. 2, dof pos 18 .. 29, dof vel 30 .. 41: slots 47 .. 88 =
+  // Philox blocks 11 .. 22): lane sub16 < 12 draws block 11 + sub16 into LDS
+  float uq = 0.0f, uv = 0.0f, ugr = 0.0f;
+  if (noisy) {
+    if (sub16 < 12) {
+      float u4[4];
+      rng.quad(11 + sub16, u4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_u[el][4 * sub16 + k] = u4[k];
+    }
+    const int d = leg * 3 + (role < 3 ? role : 0);
+    uq = s_u[el][GO1_VEL_U_NOISE + 18 + d - 44];
+    uv = s_u[el][GO1_VEL_U_NOISE + 30 + d - 44];
+    ugr = s_u[el][GO1_VEL_U_NOISE + (leg < 3 ? leg : 0) - 44];
+  }
+  static_assert(GO1_VEL_U_NOISE == 47 && GO1_VEL_U_DR + 13 <= 16, "the shared noise / DR Philox blocks");
   if (role < 3) {
     const int j = role, d = leg * 3 + j;
     const float qj = sel3(j, q), qdj = sel3(j, qd), aj = sel3(j, act), lj = sel3(j, la_obs);
-    float uq = 0.0f, uv = 0.0f;
-    if (noisy) {
-      uq = rng(GO1_VEL_U_NOISE + 18 + d);
-      uv = rng(GO1_VEL_U_NOISE + 30 + d);
-    }
     put(18 + d, noise((qj - v->default_dof_pos[d]) * v->obs_scale_dof_pos, 18 + d, uq));
     put(30 + d, noise(qdj * v->obs_scale_dof_vel, 30 + d, uv));
     put(42 + d, noise_free(aj, noisy, rng, GO1_VEL_U_NOISE + 42 + d));
@@ -649,7 +670,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   } else {
     if (leg < 3) {
       const float g = sel3(leg, pg);
-      put(leg, noise(g, leg, noisy ? rng(GO1_VEL_U_NOISE + leg) : 0.0f));
+      put(leg, noise(g, leg, ugr));
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
