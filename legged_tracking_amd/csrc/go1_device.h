@@ -1219,71 +1219,97 @@ __device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const fl
   HQ qa, qb;
   hq_fetch(T, pw[0].x, pw[1].x, qa);
   hq_fetch(T, pw[0].y, pw[1].y, qb);
-  auto near = [&](const HQ& q, float z) {  // sphere_contact_im's own penetration test, bit for bit
-    f2 hh, gx, gy;
-    hq_finish(T, q, hh, gx, gy);
-    const f2 dv = f2{1.0f, -1.0f} * (hh - z) + hr;
-    return dv.x > 0.0f || dv.y > 0.0f;
-  };
-  if (!__any(near(qa, pw[2].x) || near(qb, pw[2].y))) return;
-  float Fa[3], Fb[3], Ma[6], Mb[6];
+  // heights and gradients with the spheres in the halves: layer L = 0 floor (.x of hq_finish), 1 ceiling
+  f2 hl[2], gxl[2], gyl[2];
   {
-    const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
-    const float pb2[3] = {pw[0].y, pw[1].y, pw[2].y}, vb2[3] = {vw[0].y, vw[1].y, vw[2].y};
-    sphere_contact_im(T, qa, C, pa, va, hr, h, Fa, Ma);
-    sphere_contact_im(T, qb, C, pb2, vb2, hr, h, Fb, Mb);
+    f2 ha, gxa, gya, hb, gxb, gyb;
+    hq_finish(T, qa, ha, gxa, gya);
+    hq_finish(T, qb, hb, gxb, gyb);
+    hl[0] = f2{ha.x, hb.x}; gxl[0] = f2{gxa.x, gxb.x}; gyl[0] = f2{gya.x, gyb.x};
+    hl[1] = f2{ha.y, hb.y}; gxl[1] = f2{gxa.y, gxb.y}; gyl[1] = f2{gya.y, gyb.y};
   }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) Fw[i] = Fa[i] + Fb[i];
-  // the force the added mass sees is F - Mp g (accelerations relative to free fall, as the leg points)
-  const f2 Mw[6] = {f2{Ma[0], Mb[0]}, f2{Ma[1], Mb[1]}, f2{Ma[2], Mb[2]},
-                    f2{Ma[3], Mb[3]}, f2{Ma[4], Mb[4]}, f2{Ma[5], Mb[5]}};
-  f2 Fd[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-    Fd[i] = f2{Fa[i], Fb[i]} - (Mw[s3i(i, 0)] * g[0] + Mw[s3i(i, 1)] * g[1] + Mw[s3i(i, 2)] * g[2]);
-  // hip link rotation (world <- hip): R Rx(q), columns R0, c R1 + s R2, c R2 - s R1
-  float Rh[9];
+  // the penetration test of sphere_contact_im: floor h + r - z, ceiling z + r - h
+  const f2 dvl[2] = {(hl[0] - pw[2]) + hr, (pw[2] - hl[1]) + hr};
+  if (!__any(dvl[0].x > 0.0f || dvl[0].y > 0.0f || dvl[1].x > 0.0f || dvl[1].y > 0.0f)) return;
+  // The contact of sphere_contact_im (the oracle's sphere_contact_im), evaluated in the hip frame: with
+  // m = Rh^T n the force is sum_L fa m - sc Rh^T vt and the added mass sum_L (cn - cd) m m^T + cd I
+  // (the rotation leaves I alone), so neither Mp nor F needs the 3x3 sandwich into the link frame.
+  float Rh[9];  // hip link rotation (world <- hip): R Rx(q), columns R0, c R1 + s R2, c R2 - s R1
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     Rh[3 * i] = R[3 * i];
     Rh[3 * i + 1] = cq * R[3 * i + 1] + sq * R[3 * i + 2];
     Rh[3 * i + 2] = cq * R[3 * i + 2] - sq * R[3 * i + 1];
   }
-  // hip-frame force f = Rh^T Fd and moment lp x f with lp = (0, y, 0): (y fz, 0, -y fx)
+  f2 vh[3];  // sphere velocities, hip frame
+#pragma unroll
+  for (int j = 0; j < 3; ++j) vh[j] = Rh[j] * vw[0] + Rh[3 + j] * vw[1] + Rh[6 + j] * vw[2];
+  float gh[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) gh[j] = Rh[j] * g[0] + Rh[3 + j] * g[1] + Rh[6 + j] * g[2];
+  f2 Fh[3] = {f2s(0.0f), f2s(0.0f), f2s(0.0f)}, M[6] = {f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f)};
+  f2 cds = f2s(0.0f);
+  f2 Fwx = f2s(0.0f), Fwy = f2s(0.0f), Fwz = f2s(0.0f);
+  const float cn = h * (h * C.k + C.d);
+#pragma unroll
+  for (int L = 0; L < 2; ++L) {
+    const float sg = L == 0 ? 1.0f : -1.0f;
+    f2 nx = -sg * gxl[L], ny = -sg * gyl[L];
+    f2 inv = nx * nx + ny * ny + 1.0f;
+    inv = f2{frsq(inv.x), frsq(inv.y)};
+    nx = nx * inv;
+    ny = ny * inv;
+    const f2 nz = sg * inv;
+    const f2 depth = dvl[L] * inv;
+    const f2 vn = vw[0] * nx + vw[1] * ny + vw[2] * nz;
+    const f2 fn0 = C.k * depth - C.d * vn;
+    const f2 fn = fn0 - (h * C.k) * vn;
+    const f2 vtx = vw[0] - vn * nx, vty = vw[1] - vn * ny, vtz = vw[2] - vn * nz;
+    const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
+    const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
+    const f2 vtn = vt2 * ivt;
+    const f2 cm = C.mu * fn0;
+    const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
+                     (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
+    const bool ax = dvl[L].x > 0.0f && fn0.x > 0.0f, ay = dvl[L].y > 0.0f && fn0.y > 0.0f;
+    const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
+    const f2 sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
+    Fwx += fa * nx - sc * vtx;  // the reported world force
+    Fwy += fa * ny - sc * vty;
+    Fwz += fa * nz - sc * vtz;
+    f2 m[3];  // the normal in the hip frame
+#pragma unroll
+    for (int j = 0; j < 3; ++j) m[j] = Rh[j] * nx + Rh[3 + j] * ny + Rh[6 + j] * nz;
+    // F = fa n - sc (v - vn n) = (fa + sc vn) n - sc v
+    const f2 fs = fa + sc * vn;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Fh[j] += fs * m[j] - sc * vh[j];
+    const f2 cd = h * sc, cnd = f2{ax ? cn : 0.0f, ay ? cn : 0.0f} - cd;
+    cds += cd;
+    const f2 am[3] = {cnd * m[0], cnd * m[1], cnd * m[2]};
+    M[0] += am[0] * m[0]; M[1] += am[0] * m[1]; M[2] += am[0] * m[2];
+    M[3] += am[1] * m[1]; M[4] += am[1] * m[2]; M[5] += am[2] * m[2];
+  }
+  M[0] += cds; M[3] += cds; M[5] += cds;
+  Fw[0] = Fwx.x + Fwx.y; Fw[1] = Fwy.x + Fwy.y; Fw[2] = Fwz.x + Fwz.y;
+  // the force the added mass sees is F - M g (accelerations relative to free fall, as the leg points);
+  // moment lp x f with lp = (0, y, 0): (y fz, 0, -y fx)
   f2 f[3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) f[j] = Rh[j] * Fd[0] + Rh[3 + j] * Fd[1] + Rh[6 + j] * Fd[2];
+  for (int i = 0; i < 3; ++i) f[i] = Fh[i] - (M[s3i(i, 0)] * gh[0] + M[s3i(i, 1)] * gh[1] + M[s3i(i, 2)] * gh[2]);
   const f2 m0 = yy * f[2], m2 = -(yy * f[0]);
   pA[0] -= f2{m0.x + m0.y, f[0].x + f[0].y};
   pA[1] -= f2{0.0f, f[1].x + f[1].y};
   pA[2] -= f2{m2.x + m2.y, f[2].x + f[2].y};
-  // added mass M = Rh^T Mp Rh about the hip origin, S = lp~: S M S^T has (0,0) y^2 M22, (0,2) -y^2 M20,
-  // (2,2) y^2 M00 and zeros elsewhere; S M has rows (y M2., 0, -y M0.)
-  f2 MR[9], M[9];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      MR[3 * i + j] = Mw[s3i(i, 0)] * Rh[j] + Mw[s3i(i, 1)] * Rh[3 + j] + Mw[s3i(i, 2)] * Rh[6 + j];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = i; j < 3; ++j) {
-      M[3 * i + j] = Rh[i] * MR[j] + Rh[3 + i] * MR[3 + j] + Rh[6 + i] * MR[6 + j];
-      M[3 * j + i] = M[3 * i + j];
-    }
+  // about the hip origin, S = lp~: S M S^T has (0,0) y^2 M22, (0,2) -y^2 M20, (2,2) y^2 M00 and zeros
+  // elsewhere; S M has rows (y M2., 0, -y M0.); C = M
   const f2 y2 = yy * yy;
-  const f2 A[6] = {y2 * M[8], f2s(0.0f), -(y2 * M[6]), f2s(0.0f), f2s(0.0f), y2 * M[0]};  // 00 01 02 11 12 22
-  const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
+  const f2 A[6] = {y2 * M[5], f2s(0.0f), -(y2 * M[2]), f2s(0.0f), f2s(0.0f), y2 * M[0]};  // 00 01 02 11 12 22
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const f2 c = M[3 * II[k] + JJ[k]];
-    IA.ac[k] += f2{A[k].x + A[k].y, c.x + c.y};
-  }
+  for (int k = 0; k < 6; ++k) IA.ac[k] += f2{A[k].x + A[k].y, M[k].x + M[k].y};
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const f2 b0 = yy * M[6 + j], b2 = -(yy * M[j]);
+    const f2 b0 = yy * M[s3i(2, j)], b2 = -(yy * M[s3i(0, j)]);
     IA.b[j] += b0.x + b0.y;
     IA.b[6 + j] += b2.x + b2.y;
   }
@@ -1692,9 +1718,12 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
         for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
 #ifndef GO1_ABL_NO_CONTACT
 #ifndef GO1_ABL_NO_HIP  // ablation build only: no hip capsules
-        if (j == 1)  // the hip capsule's contact, on the hip's inertia and bias force
+        if (j == 1) {  // the hip capsule's contact, on the hip's inertia and bias force
+          MARK(hip_begin);
           hip_contact(T, C, R, S.pos, vbp, origin, cs[0][0], cs[0][1], S.qd[0], msy * f2{hip_y0, hip_y1}, hip_r, h,
                       g, IA, pAp[0], Fhip);
+          MARK(hip_done);
+        }
 #endif
 #endif
       } else {

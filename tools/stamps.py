@@ -39,7 +39,7 @@ def main():
     scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
     grav, gvec = CF.gravity_state(rng.uniform(-1, 1, 3))
     ring = torch.randn((8, n, 12), device=dev)
-    for k in range(30):
+    for k in range(int(os.environ.get('GO1_STAMPS_STEPS', '30'))):
         g.step(ring[k % 8], gvec, grav, scales, rng_seed=11, rng_step=1 + k)
     torch.cuda.synchronize()
     lib = native.lib()
@@ -56,15 +56,19 @@ def main():
     tot = collections.Counter()
     cnt = collections.Counter()
     life = []
+    per_wave = []  # per wave: section -> cycles (the tail analysis below)
     for w in range(nw):
         k = int(np.count_nonzero(line[w]))
         if k < 2:
             continue
         life.append(t[w, k - 1] - t[w, 0])
+        pw = collections.Counter()
         for i in range(k - 1):
             nm = name.get(int(line[w, i]), str(line[w, i]))
             tot[nm] += int(t[w, i + 1] - t[w, i])
+            pw[nm] += int(t[w, i + 1] - t[w, i])
             cnt[nm] += 1
+        per_wave.append(pw)
     L = float(np.mean(life))
     lf = np.array(life, np.float64)
     print(f"wave lifetime cycles: p50 {np.percentile(lf, 50):.0f}  p90 {np.percentile(lf, 90):.0f}  "
@@ -75,6 +79,16 @@ def main():
     print(f"{'section (after marker)':28s} {'cycles/wave':>12s} {'share':>7s} {'execs':>6s}")
     for nm, v in sorted(tot.items(), key=lambda x: -x[1]):
         print(f"{nm:28s} {v / len(life):12.0f} {v / len(life) / L:7.1%} {cnt[nm] / len(life):6.1f}")
+    # the launch lasts as long as its slowest waves: where do the slowest 5 % spend their extra cycles?
+    order = np.argsort(lf)
+    slow = order[-max(1, len(lf) // 20):]
+    mid = order[len(lf) // 4: 3 * len(lf) // 4]
+    print(f"\nslowest 5 % of waves ({len(slow)}): mean lifetime {lf[slow].mean():.0f} vs the middle half "
+          f"{lf[mid].mean():.0f} cycles; extra cycles per section:")
+    secs = sorted(tot)
+    extra = {nm: np.mean([per_wave[i][nm] for i in slow]) - np.mean([per_wave[i][nm] for i in mid]) for nm in secs}
+    for nm, v in sorted(extra.items(), key=lambda x: -x[1])[:12]:
+        print(f"{nm:28s} {v:+12.0f}")
 
 
 if __name__ == "__main__":
