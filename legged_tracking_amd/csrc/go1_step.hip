@@ -347,6 +347,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float torque[3], tgt[3];
   float cf_raw[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
   for (int sub = 0; sub < dec; ++sub) {
+    MARK(sub_begin);
     // _compute_torques (:957-996)
     {
       // inputs of this lane's three joints ...
@@ -410,6 +411,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const float h = c->sim_dt / (float)c->n_internal;
 #pragma unroll
       for (int j = 0; j < 3; ++j) { P.q[j] = q[j]; P.qd[j] = qd[j]; }
+      MARK(phys_call);
 #ifndef GO1_ABL_NO_PHYS
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
@@ -420,6 +422,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
 #pragma unroll
       for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }
+      MARK(phys_returned);
     }
     if (A.dbg_torques && owner) {
 #pragma unroll
