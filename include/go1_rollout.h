@@ -8,6 +8,8 @@
  *   go1_adv_normalize()      <- rollout_storage.py:89-90 (global normalisation; the
  *                               caller may all-reduce the 2 f64 statistics across ranks
  *                               between the two calls)
+ *   go1_colsum()             <- the bias gradients of PPO.update's backward (ppo.py:155-157),
+ *                               torch's grad_output.sum(0) in F.linear's backward
  *
  * All pointers are device pointers owned by the caller; every call is
  * asynchronous on the given HIP stream and returns 0 or a negative code.
@@ -101,6 +103,10 @@ int go1_gae(const float* rewards, const uint8_t* dones, const float* values, con
             void* stream);
 /* advantages <- (a - mean) / (std + 1e-8); count = number of samples the stats cover (all ranks). */
 int go1_adv_normalize(float* advantages, const double* stats, double count, int64_t total, void* stream);
+/* out[c] = sum over rows of x[r][c], x row-major (rows, cols) f32, deterministic (fixed partition and order):
+ * the PPO update's bias gradients (PPO.update, ppo.py:155-157 backward; torch's grad_output.sum(0)).
+ * partial: scratch of parts x cols floats, 1 <= parts <= min(rows, 65535). */
+int go1_colsum(const float* x, int64_t rows, int32_t cols, float* partial, int32_t parts, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1101,6 +1101,52 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel_split(go1_policy_args P
 
 }  // namespace
 
+// ------------------------------------------------------------------ column sums (bias gradients)
+// out[c] = sum_r x[r][c] of a row-major (R, C) f32 matrix, deterministic: pass 1 sums row partition p of 64
+// columns per workgroup (4 row groups x 64 columns, each lane a fixed stride-4 row order, the 4 groups added
+// in order through LDS) into partial[p][c]; pass 2 adds the partitions in order.  The PPO update's bias
+// gradients (dL/db = column sums of dL/dy over the 24,576-sample mini-batch): torch's sum(0) takes 18-24 us
+// for 24,576 x 512 (tools/reduce_bench.py), 2-3x the HBM time of the 50 MB it reads.
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ x, int64_t R, int C, int64_t RP,
+                                                          float* __restrict__ partial) {
+  __shared__ float s[4][64];
+  const int t = threadIdx.x, cl = t & 63, rg = t >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int64_t r0 = (int64_t)blockIdx.y * RP, r1 = r0 + RP < R ? r0 + RP : R;
+  float acc = 0.0f;
+  if (c < C) {
+    // eight rows in flight per lane (independent loads), added in row order
+    int64_t r = r0 + rg;
+    for (; r + 28 < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = x[(r + 4 * k) * C + c];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+    for (; r < r1; r += 4) acc += x[r * C + c];
+  }
+  s[rg][cl] = acc;
+  __syncthreads();
+  if (rg == 0 && c < C) partial[(int64_t)blockIdx.y * C + c] = ((s[0][cl] + s[1][cl]) + s[2][cl]) + s[3][cl];
+}
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial, int P, int C,
+                                                           float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float acc = 0.0f;
+  int p = 0;
+  for (; p + 8 <= P; p += 8) {  // eight partitions in flight, added in order
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = partial[(int64_t)(p + k) * C + c];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k];
+  }
+  for (; p < P; ++p) acc += partial[(int64_t)p * C + c];
+  out[c] = acc;
+}
+
 extern "C" {
 
 #ifdef GO1_POLICY_STAMPS
@@ -1174,6 +1220,19 @@ int go1_adv_normalize(float* advantages, const double* stats, double count, int6
   blocks = blocks > 4096 ? 4096 : blocks;
   hipLaunchKernelGGL(adv_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, advantages, stats,
                      count, (size_t)total);
+  RT_TRY(hipGetLastError());
+  return GO1_OK_RT;
+}
+
+int go1_colsum(const float* x, int64_t rows, int32_t cols, float* partial, int32_t parts, float* out, void* stream) {
+  if (!x || !partial || !out || rows < 1 || cols < 1 || parts < 1 || parts > 65535 || parts > rows)
+    return fail(GO1_RT_E_ARG, "go1_colsum: bad argument");
+  const int64_t rp = (rows + parts - 1) / parts;
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)parts), dim3(256), 0,
+                     (hipStream_t)stream, x, rows, cols, rp, partial);
+  RT_TRY(hipGetLastError());
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     partial, parts, cols, out);
   RT_TRY(hipGetLastError());
   return GO1_OK_RT;
 }

@@ -293,6 +293,36 @@ def get_activation(name):
     return acts[name]()
 
 
+_COLSUM_LIB = []  # [ctypes lib or None], loaded on first use
+
+
+def _colsum(g):
+    """Column sums of a (rows, cols) gradient (the bias gradient) with the deterministic HIP kernel
+    (go1_colsum); torch's sum(0) off the GPU or without the library."""
+    if not g.is_cuda or g.dim() != 2 or not g.is_contiguous() or g.dtype != torch.float32 or g.shape[0] < 64 or \
+            os.environ.get("GO1_COLSUM", "1") == "0":
+        return g.sum(0)
+    if not _COLSUM_LIB:
+        lib = None
+        if os.path.exists(LIB_PATH):
+            lib = C.CDLL(LIB_PATH)
+            lib.go1_colsum.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+            lib.go1_rollout_last_error.restype = C.c_char_p
+        _COLSUM_LIB.append(lib)
+    lib = _COLSUM_LIB[0]
+    if lib is None:
+        return g.sum(0)
+    rows, cols = g.shape
+    parts = max(1, min(512 // ((cols + 63) // 64), rows // 256, 64))
+    part = torch.empty((parts, cols), dtype=torch.float32, device=g.device)
+    out = torch.empty(cols, dtype=torch.float32, device=g.device)
+    rc = lib.go1_colsum(g.data_ptr(), rows, cols, part.data_ptr(), parts, out.data_ptr(),
+                        C.c_void_p(torch.cuda.current_stream(g.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError(lib.go1_rollout_last_error().decode())
+    return out
+
+
 class _LinearSplitK(torch.autograd.Function):
     """y = x W^T + b whose weight gradient is summed over K_SPLIT row chunks of the batch (one batched
     GEMM, then a sum over the chunks): the mini-batch weight gradient dW = dY^T X is a tall-skinny
@@ -316,7 +346,7 @@ class _LinearSplitK(torch.autograd.Function):
             gw = torch.bmm(gy.view(S, n // S, -1).transpose(1, 2), x.view(S, n // S, -1)).sum(0)
         else:
             gw = gy.t() @ x
-        return gx, gw, gy.sum(0)
+        return gx, gw, _colsum(gy)
 
 
 def _mlp_train(seq, x):
@@ -534,12 +564,20 @@ class PPO:
         # kernel reads is the value the foreach path would cast to.  On the CPU: the reference's path.
         self._dev_lr = torch.device(device).type == "cuda" and os.environ.get("GO1_PPO_FUSED", "1") != "0"
         params = list(self.actor_critic.parameters())
+        # The mini-batch step (forward, backward, gradient clip, both Adam steps, the adaptive rate) is
+        # captured once into a HIP graph and replayed for every later mini-batch (GO1_PPO_GRAPH=0: eager):
+        # it is ~150 small launches whose host issue left the GPU idle between them.  One rank only (the
+        # gradient all-reduce stays eager).
+        self._graph_on = self._dev_lr and os.environ.get("GO1_PPO_GRAPH", "1") != "0"
+        self._graph = None
+        self._graph_warm = 0
         if self._dev_lr:
             self._lr64 = torch.tensor(PPO_Args.learning_rate, dtype=torch.float64, device=device)
             self._lr32 = torch.tensor(PPO_Args.learning_rate, dtype=torch.float32, device=device)
-            self.optimizer = torch.optim.Adam(params, lr=self._lr32, fused=True)
+            cap = self._graph_on
+            self.optimizer = torch.optim.Adam(params, lr=self._lr32, fused=True, capturable=cap)
             self.adaptation_module_optimizer = torch.optim.Adam(params, lr=PPO_Args.adaptation_module_learning_rate,
-                                                                fused=True)
+                                                                fused=True, capturable=cap)
         else:
             self.optimizer = torch.optim.Adam(params, lr=PPO_Args.learning_rate)
             self.adaptation_module_optimizer = torch.optim.Adam(params, lr=PPO_Args.adaptation_module_learning_rate)
@@ -663,78 +701,144 @@ class PPO:
             p.grad.copy_(flat[off:off + k].view_as(p.grad))
             off += k
 
-    def update(self):
+    def _minibatch_step(self, batch, acc, sample=True):
+        """One mini-batch of PPO.update (ppo.py:107-201): the surrogate / value / entropy loss and its Adam step,
+        the adaptive learning rate, then the adaptation-module regression step(s).  Loss values accumulate
+        into `acc` on the device.  sample=False leaves out ac.act's unused sample (the graphed loop draws it
+        outside the graph: torch's generator cannot be advanced inside a HIP capture here)."""
         A = PPO_Args
         ac = self.actor_critic
-        # the loss means accumulate on the device (ppo.py:186-187, 200-201 call .item() per mini-batch:
-        # a host sync each); one copy at the end.  The adaptive-LR rule's KL stays a host read.
-        acc = torch.zeros(4, dtype=torch.float32, device=self.device)  # value, surrogate, adapt, adapt_test
-        gen = self.storage.mini_batch_generator(A.num_mini_batches, A.num_learning_epochs)
-        for (obs_b, critic_obs_b, priv_b, hist_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b,
-             old_sigma_b, masks_b, bins_b) in gen:
-            ac.update_distribution_train(hist_b)
+        (obs_b, critic_obs_b, priv_b, hist_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b,
+         old_sigma_b) = batch
+        ac.update_distribution_train(hist_b)
+        if sample:
             ac.distribution.sample()  # ac.act's (unused) sample: the reference's torch RNG consumption (ppo.py:110)
-            logp_b = ac.get_actions_log_prob(act_b)
-            value_b = ac.evaluate_train(hist_b, priv_b)
-            mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
-            if A.desired_kl is not None and A.schedule == "adaptive":
-                with torch.inference_mode():
-                    kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.0e-5) +
-                                   (torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) /
-                                   (2.0 * torch.square(sigma_b)) - 0.5, axis=-1)
-                    kl_mean = torch.mean(kl)
-                    if _world() > 1:
-                        kl_mean = kl_mean.clone()
-                        torch.distributed.all_reduce(kl_mean)
-                        kl_mean /= _world()
-                if self._dev_lr:
-                    with torch.no_grad():
-                        k, lr = kl_mean.double(), self._lr64
-                        new = torch.where(k > A.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
-                                          torch.where((k < A.desired_kl / 2.0) & (k > 0.0),
-                                                      torch.clamp(lr * 1.5, max=1e-2), lr))
-                        self._lr64.copy_(new)
-                        self._lr32.copy_(new)
-                else:
-                    kl_mean = float(kl_mean)
-                    if kl_mean > A.desired_kl * 2.0:
-                        self.learning_rate = max(1e-5, self.learning_rate / 1.5)
-                    elif A.desired_kl / 2.0 > kl_mean > 0.0:
-                        self.learning_rate = min(1e-2, self.learning_rate * 1.5)
-                    for g in self.optimizer.param_groups:
-                        g["lr"] = self.learning_rate
-            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
-            surrogate = -torch.squeeze(adv_b) * ratio
-            surrogate_clipped = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - A.clip_param, 1.0 + A.clip_param)
-            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
-            if A.use_clipped_value_loss:
-                value_clipped = target_v_b + (value_b - target_v_b).clamp(-A.clip_param, A.clip_param)
-                value_loss = torch.max((value_b - ret_b).pow(2), (value_clipped - ret_b).pow(2)).mean()
-            else:
-                value_loss = (ret_b - value_b).pow(2).mean()
-            loss = surrogate_loss + A.value_loss_coef * value_loss - A.entropy_coef * entropy_b.mean()
-            self.optimizer.zero_grad()
-            loss.backward()
-            self._allreduce_grads()
-            nn.utils.clip_grad_norm_(ac.parameters(), A.max_grad_norm)
-            self.optimizer.step()
-            acc[0] += value_loss.detach()
-            acc[1] += surrogate_loss.detach()
-            num_train = int(priv_b.shape[0] // 5 * 4)
-            for _ in range(A.num_adaptation_module_substeps):
-                pred = _mlp_train(ac.adaptation_module, hist_b)
+        logp_b = ac.get_actions_log_prob(act_b)
+        value_b = ac.evaluate_train(hist_b, priv_b)
+        mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
+        if A.desired_kl is not None and A.schedule == "adaptive":
+            with torch.inference_mode():
+                kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.0e-5) +
+                               (torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) /
+                               (2.0 * torch.square(sigma_b)) - 0.5, axis=-1)
+                kl_mean = torch.mean(kl)
+                if _world() > 1:
+                    kl_mean = kl_mean.clone()
+                    torch.distributed.all_reduce(kl_mean)
+                    kl_mean /= _world()
+            if self._dev_lr:
                 with torch.no_grad():
-                    target = priv_b
-                # every column (ppo.py:193: linspace(0, w - 1, w) as an index), or column 0
-                sel = 0 if A.selective_adaptation_module_loss else slice(None)
-                adapt_loss = F.mse_loss(pred[:num_train, sel], target[:num_train, sel])
-                adapt_test = F.mse_loss(pred[num_train:, sel], target[num_train:, sel])
-                self.adaptation_module_optimizer.zero_grad()
-                adapt_loss.backward()
-                self._allreduce_grads()
-                self.adaptation_module_optimizer.step()
-                acc[2] += adapt_loss.detach()
-                acc[3] += adapt_test.detach()
+                    k, lr = kl_mean.double(), self._lr64
+                    new = torch.where(k > A.desired_kl * 2.0, torch.clamp(lr / 1.5, min=1e-5),
+                                      torch.where((k < A.desired_kl / 2.0) & (k > 0.0),
+                                                  torch.clamp(lr * 1.5, max=1e-2), lr))
+                    self._lr64.copy_(new)
+                    self._lr32.copy_(new)
+            else:
+                kl_mean = float(kl_mean)
+                if kl_mean > A.desired_kl * 2.0:
+                    self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+                elif A.desired_kl / 2.0 > kl_mean > 0.0:
+                    self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+                for g in self.optimizer.param_groups:
+                    g["lr"] = self.learning_rate
+        ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+        surrogate = -torch.squeeze(adv_b) * ratio
+        surrogate_clipped = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - A.clip_param, 1.0 + A.clip_param)
+        surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+        if A.use_clipped_value_loss:
+            value_clipped = target_v_b + (value_b - target_v_b).clamp(-A.clip_param, A.clip_param)
+            value_loss = torch.max((value_b - ret_b).pow(2), (value_clipped - ret_b).pow(2)).mean()
+        else:
+            value_loss = (ret_b - value_b).pow(2).mean()
+        loss = surrogate_loss + A.value_loss_coef * value_loss - A.entropy_coef * entropy_b.mean()
+        self.optimizer.zero_grad()
+        loss.backward()
+        self._allreduce_grads()
+        nn.utils.clip_grad_norm_(ac.parameters(), A.max_grad_norm)
+        self.optimizer.step()
+        acc[0] += value_loss.detach()
+        acc[1] += surrogate_loss.detach()
+        num_train = int(priv_b.shape[0] // 5 * 4)
+        for _ in range(A.num_adaptation_module_substeps):
+            pred = _mlp_train(ac.adaptation_module, hist_b)
+            with torch.no_grad():
+                target = priv_b
+            # every column (ppo.py:193: linspace(0, w - 1, w) as an index), or column 0
+            sel = 0 if A.selective_adaptation_module_loss else slice(None)
+            adapt_loss = F.mse_loss(pred[:num_train, sel], target[:num_train, sel])
+            adapt_test = F.mse_loss(pred[num_train:, sel], target[num_train:, sel])
+            self.adaptation_module_optimizer.zero_grad()
+            adapt_loss.backward()
+            self._allreduce_grads()
+            self.adaptation_module_optimizer.step()
+            acc[2] += adapt_loss.detach()
+            acc[3] += adapt_test.detach()
+
+    GRAPH_WARMUP = 3  # eager mini-batches (on a side stream) before the capture: lazy handles and optimizer state
+
+    def _graphed_minibatches(self, acc):
+        """The mini-batch loop of update() with the step replayed from a HIP graph: the batch is gathered inside the
+        graph from the storage with a static index buffer, so a mini-batch costs one index copy and one replay."""
+        A = PPO_Args
+        st = self.storage
+        batch = st.num_envs * st.num_transitions_per_env
+        mb = batch // A.num_mini_batches
+        indices = torch.randperm(A.num_mini_batches * mb, device=self.device)  # mini_batch_generator's draw
+        flat = [x.flatten(0, 1) for x in (st.observations, st.observations, st.privileged_observations,
+                                         st.observation_histories, st.actions, st.values, st.advantages,
+                                         st.returns, st.actions_log_prob, st.mu, st.sigma)]
+        if self._graph is not None and self._graph_key != (mb, tuple(x.data_ptr() for x in flat)):
+            self._graph = None  # new storage: capture again
+            self._graph_warm = 0
+        if self._graph is None and self._graph_warm == 0:
+            self._graph_idx = torch.empty(mb, dtype=torch.int64, device=self.device)
+            self._graph_acc = torch.zeros(4, dtype=torch.float32, device=self.device)
+        idx, gacc = self._graph_idx, self._graph_acc
+        # ac.act's unused sample per mini-batch, drawn before each step with the same shape: the same torch
+        # generator advance as the eager loop's (the values are discarded there too)
+        na = st.actions.shape[-1]
+        if getattr(self, "_graph_draw", None) is None or self._graph_draw[0].shape != (mb, na):
+            self._graph_draw = (torch.zeros(mb, na, device=self.device), torch.ones(mb, na, device=self.device))
+
+        def step():
+            self._minibatch_step([x[idx] for x in flat], gacc, sample=False)
+
+        for _ in range(A.num_learning_epochs):
+            for i in range(A.num_mini_batches):
+                idx.copy_(indices[i * mb:(i + 1) * mb])
+                torch.normal(*self._graph_draw)
+                if self._graph is not None:
+                    self._graph.replay()
+                elif self._graph_warm < self.GRAPH_WARMUP:
+                    side = torch.cuda.Stream(self.device)
+                    side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(side):
+                        step()
+                    torch.cuda.current_stream(self.device).wait_stream(side)
+                    self._graph_warm += 1
+                else:
+                    torch.cuda.synchronize(self.device)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        step()
+                    self._graph = g
+                    self._graph_key = (mb, tuple(x.data_ptr() for x in flat))
+                    g.replay()  # the capture recorded the step without running it
+        acc += gacc
+        gacc.zero_()
+
+    def update(self):
+        A = PPO_Args
+        # the loss means accumulate on the device (ppo.py:186-187, 200-201 call .item() per mini-batch:
+        # a host sync each); one copy at the end.
+        acc = torch.zeros(4, dtype=torch.float32, device=self.device)  # value, surrogate, adapt, adapt_test
+        if self._graph_on and _world() == 1:
+            self._graphed_minibatches(acc)
+        else:
+            gen = self.storage.mini_batch_generator(A.num_mini_batches, A.num_learning_epochs)
+            for b in gen:
+                self._minibatch_step(b[:11], acc)
         n_up = A.num_learning_epochs * A.num_mini_batches
         n_ad = n_up * A.num_adaptation_module_substeps
         self.storage.clear()

@@ -487,3 +487,45 @@ def test_fused_policy_kernel_streams_long_histories(hist, npriv):
         pol.variant = 1
         with pytest.raises(RuntimeError, match="variant 1"):
             pol.forward(h, p)
+
+
+@pytest.mark.gpu
+def test_ppo_update_graph_replays_the_eager_update(monkeypatch):
+    """The HIP-graph mini-batch step (PPO._graphed_minibatches: 3 eager warm-up mini-batches, one capture,
+    replays) computes the eager update: two consecutive updates from the reference fixture's storage, with
+    the graph captured in the first and replayed through the second, against GO1_PPO_GRAPH=0."""
+    d = _fixture()
+    runs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GO1_PPO_GRAPH", flag)
+        alg, losses = _ppo_update_from_fixture(d, "cuda:0", R.HipRolloutKernels())
+        assert (alg._graph is not None) == (flag == "1")
+        st = alg.storage
+        for k in ("observations", "privileged_observations", "observation_histories", "actions", "values",
+                  "returns", "actions_log_prob", "advantages", "mu", "sigma", "rewards"):
+            getattr(st, k).copy_(torch.from_numpy(d["upd/storage/" + k]))
+        st.step = st.num_transitions_per_env
+        torch.manual_seed(5)
+        losses2 = alg.update()
+        runs[flag] = (losses, losses2, alg.learning_rate,
+                      {k: v.detach().cpu().numpy() for k, v in alg.actor_critic.state_dict().items()})
+    e, g = runs["0"], runs["1"]
+    np.testing.assert_allclose(np.array(g[0] + g[1]), np.array(e[0] + e[1]), rtol=1e-5, atol=1e-7)
+    assert g[2] == e[2]
+    dmax = max(float(np.abs(g[3][k] - e[3][k]).max()) for k in e[3])
+    print(f"\ngraph vs eager after two updates: max |dw| {dmax:.2e}")
+    assert dmax <= 1e-5, dmax
+
+
+@pytest.mark.gpu
+def test_colsum_kernel_matches_f64_sums_and_is_deterministic():
+    """go1_colsum (the bias gradients of PPO.update's backward) against f64 column sums, ragged shapes included;
+    two calls agree bit for bit (fixed partition and order)."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for rows, cols in ((24576, 512), (24576, 12), (24577, 1), (1000, 70), (64, 3), (4096, 2100)):
+        x = torch.randn(rows, cols, device="cuda", generator=g)
+        got = R._colsum(x)
+        ref = x.double().sum(0)
+        scale = x.double().abs().sum(0)
+        assert ((got.double() - ref).abs() <= 1e-6 * scale + 1e-6).all(), (rows, cols)
+        assert torch.equal(got, R._colsum(x))

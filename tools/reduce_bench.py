@@ -1,6 +1,12 @@
 """Micro-benchmark of the PPO update's reductions (GPU): the split-K weight-gradient sum over 16 chunks and the
 bias-gradient column sum, as torch .sum(0) against a ones-vector GEMV (hipBLASLt).  python tools/reduce_bench.py"""
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from legged_tracking_amd import rollout as R  # noqa: E402
 
 
 def bench(f, it=200):
@@ -29,7 +35,8 @@ def main():
     for shape in [(24576, 512), (24576, 256), (24576, 128), (24576, 12)]:
         g = torch.randn(shape, device=dev)
         ones = torch.ones(1, shape[0], device=dev)
-        print(f"column sum {shape}: sum(0) {bench(lambda: g.sum(0)):.1f} us, ones@ {bench(lambda: ones @ g):.1f} us")
+        print(f"column sum {shape}: sum(0) {bench(lambda: g.sum(0)):.1f} us, ones@ {bench(lambda: ones @ g):.1f} us, "
+              f"go1_colsum {bench(lambda: R._colsum(g)):.1f} us")
 
 
 if __name__ == "__main__":
