@@ -52,6 +52,8 @@ typedef struct go1_transition {
   const int32_t* time_outs_flag;
   const uint8_t* time_outs_pending;
   uint8_t* time_outs_dst;
+  int64_t obs_history_ld;         /* row stride of obs_history in floats (0: num_obs_history), e.g. a window of
+                                     the velocity env's wider history rows (go1_velocity.h obs_history_out_ld) */
 } go1_transition;
 
 /* Fused policy inference (ActorCritic.act / evaluate, actor_critic.py:121-150) for the
@@ -91,6 +93,7 @@ typedef struct go1_policy_args {
                                   running all three nets; identical outputs (tests/test_rollout.py) */
   int32_t* overflow;           /* optional: += workgroups that recomputed in f32 (the range guard) */
   go1_policy_layer layers[GO1_POLICY_LAYERS];
+  int64_t hist_ld;             /* row stride of obs_history in floats (0: hist_dim; >= hist_dim) */
 } go1_policy_args;
 
 const char* go1_rollout_last_error(void);

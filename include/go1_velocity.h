@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GO1_VEL_ABI_VERSION 1
+#define GO1_VEL_ABI_VERSION 2
 #define GO1_VEL_NUM_COMMANDS 15  /* x, y, yaw vel, body height, gait freq, phase, offset, bound, duration,
                                     footswing height, body pitch, body roll, stance width, stance length, aux */
 #define GO1_VEL_NUM_OBS 70       /* gravity 3, commands 15, dof pos 12, dof vel 12, actions 12, last actions 12,
@@ -194,8 +194,12 @@ typedef struct go1_vel_step_args {
   uint8_t* time_out;                /* (n_envs) */
   uint8_t* extras_time_outs;        /* (n_envs): time_out, rebound only on steps with a reset (:251-252) */
   float* contact_forces;            /* (n_envs, 17, 3) or NULL */
-  const float* obs_history_in;      /* (n_envs, 70 x history_len) or NULL (no history output) */
-  float* obs_history_out;           /* cat(in[:, 70:], obs) (HistoryWrapper.step), another buffer */
+  const float* obs_history_in;      /* (n_envs, 70 x history_len) rows obs_history_in_ld apart, or NULL (no
+                                       history output) */
+  float* obs_history_out;           /* cat(in[:, 70:], obs) (HistoryWrapper.step), rows obs_history_out_ld apart:
+                                       another buffer, or in + 70 with the same row stride (a sliding window
+                                       over rows wider than the history: the shift is the identity and skipped,
+                                       only the new observation is written) */
   float* aux;                       /* (n_envs, GO1_VEL_AUX) or NULL */
   /* compact episode log, a ring: each env reset this step writes n_terms + 3 floats (n_terms + 1 episode
      sums, tag, env index) at row atomicAdd(*episode_log_count, 1) % episode_log_cap */
@@ -209,6 +213,8 @@ typedef struct go1_vel_step_args {
   float* dbg_gait;                  /* (n_envs, 12): foot_indices 4, clock_inputs 4, desired_contact_states 4 */
   void* ev_begin;                   /* optional hipEvent_t pair around the step kernel */
   void* ev_end;
+  int64_t obs_history_in_ld;        /* row strides of obs_history_in / _out in floats (0: 70 x history_len); */
+  int64_t obs_history_out_ld;       /* >= 70 x history_len, the window of a row is contiguous (ABI v2) */
 } go1_vel_step_args;
 
 typedef struct go1_vel_handle go1_vel_handle;

@@ -171,7 +171,8 @@ struct VArgs {
   go1_vel_state st;
   go1_vel_step_args a;
   const float* env_origins;
-  int hist_w;  // obs_history row width (70 x history_len)
+  int hist_w;      // obs_history row width (70 x history_len)
+  int64_t hist_ld; // obs_history_out row stride (floats)
 };
 
 template <bool INJ>
@@ -635,7 +636,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // ---- compute_observations (:320-509): role r < 3 writes joint r's four columns, role 3 leg l the
   // gravity component l (l < 3), commands l, l + 4, l + 8, l + 12 and the clock of foot l
   float* o = A.obs + (size_t)e * GO1_VEL_NUM_OBS;
-  float* oh = A.obs_history_out ? A.obs_history_out + (size_t)e * K.hist_w + (K.hist_w - GO1_VEL_NUM_OBS) : nullptr;
+  float* oh = A.obs_history_out ? A.obs_history_out + (size_t)e * K.hist_ld + (K.hist_w - GO1_VEL_NUM_OBS) : nullptr;
   const float clip = v->clip_obs;
   const bool noisy = v->add_noise != 0;
   auto put = [&](int i, float val) {
@@ -851,8 +852,9 @@ struct CArgs {
   float* obs;
   float* hist_out;
   const float* hist_in;
+  int64_t ld_in, ld_out;  // row strides (floats)
   int hist_w;
-  int hist_aligned;  // hist_w % 4 == 0 and both buffers 16-byte aligned: the shift moves 16-byte chunks
+  int hist_aligned;  // hist_w and both strides % 4 == 0, both buffers 16-byte aligned: 16-byte chunks
 };
 
 // numpy's pairwise summation (np.add.reduce of a contiguous f64 array), PW_BLOCKSIZE 128
@@ -1154,7 +1156,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
         if (v->add_noise) val = val + (2.0f * rng(GO1_VEL_U_NOISE + 3 + sub) - 1.0f) * v->noise_vec[3 + sub];
         val = clampf(val, -clip, clip);
         K.obs[(size_t)e * GO1_VEL_NUM_OBS + 3 + sub] = val;
-        if (K.hist_out) K.hist_out[(size_t)e * K.hist_w + K.hist_w - GO1_VEL_NUM_OBS + 3 + sub] = val;
+        if (K.hist_out) K.hist_out[(size_t)e * K.ld_out + K.hist_w - GO1_VEL_NUM_OBS + 3 + sub] = val;
       }
     }
   }
@@ -1173,6 +1175,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
 __device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
   if (!K.hist_in || !K.hist_out) return;
   const int W = K.hist_w, D = W - GO1_VEL_NUM_OBS;
+  const size_t Li = (size_t)K.ld_in, Lo = (size_t)K.ld_out;
   if (K.hist_aligned) {
     // 16-byte chunks: rows are 16-byte aligned (W % 4 == 0), the source starts 70 = 4 x 17 + 2 floats in,
     // so dest chunk i = (z, w) of aligned source chunk 17 + i and (x, y) of chunk 18 + i, which the next
@@ -1192,7 +1195,7 @@ __device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
         ev[u] = t / Cp;
         iv[u] = (int)(t % Cp);
         own[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (t < total && iv[u] < Cn) own[u] = reinterpret_cast<const float4*>(K.hist_in + ev[u] * W)[17 + iv[u]];
+        if (t < total && iv[u] < Cn) own[u] = reinterpret_cast<const float4*>(K.hist_in + ev[u] * Li)[17 + iv[u]];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -1201,12 +1204,12 @@ __device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
         float nx = __shfl_down(own[u].x, 1), ny = __shfl_down(own[u].y, 1);
         const int i = iv[u];
         if (last_lane && i + 1 < Cn) {
-          const float4 o2 = reinterpret_cast<const float4*>(K.hist_in + ev[u] * W)[18 + i];
+          const float4 o2 = reinterpret_cast<const float4*>(K.hist_in + ev[u] * Li)[18 + i];
           nx = o2.x;
           ny = o2.y;
         }
         if (i < Cn) {
-          float* dst = K.hist_out + ev[u] * W + 4 * i;
+          float* dst = K.hist_out + ev[u] * Lo + 4 * i;
           if (4 * i + 4 <= D) *reinterpret_cast<float4*>(dst) = make_float4(own[u].z, own[u].w, nx, ny);
           else *reinterpret_cast<float2*>(dst) = make_float2(own[u].z, own[u].w);
         }
@@ -1219,8 +1222,8 @@ __device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
   const size_t total = (size_t)K.n_envs * W2;
   for (size_t i = g0; i < total; i += G) {
     const size_t e = i / W2, k = i % W2;
-    const float2 val = *(const float2*)(K.hist_in + e * W + GO1_VEL_NUM_OBS + 2 * k);
-    *(float2*)(K.hist_out + e * W + 2 * k) = val;
+    const float2 val = *(const float2*)(K.hist_in + e * Li + GO1_VEL_NUM_OBS + 2 * k);
+    *(float2*)(K.hist_out + e * Lo + 2 * k) = val;
   }
 }
 
@@ -1419,9 +1422,17 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
     return vfail(GO1_E_ARG, "go1_vel_step: parity mode needs both uniform arrays");
   if (a->resample_next && a->uniforms && (!a->uniforms_next || !a->uniforms_f64_next))
     return vfail(GO1_E_ARG, "go1_vel_step: parity mode resamples ahead with the next step's uniforms");
+  const int hist_w = GO1_VEL_NUM_OBS * h->vcfg.history_len;
+  const int64_t ld_in = a->obs_history_in_ld ? a->obs_history_in_ld : hist_w;
+  const int64_t ld_out = a->obs_history_out_ld ? a->obs_history_out_ld : hist_w;
   if ((a->obs_history_in == nullptr) != (a->obs_history_out == nullptr) ||
       (a->obs_history_in && a->obs_history_in == a->obs_history_out))
     return vfail(GO1_E_ARG, "go1_vel_step: obs_history in and out are two distinct buffers (or both NULL)");
+  if (a->obs_history_in && (ld_in < hist_w || ld_out < hist_w || (hist_w & 1) || (ld_in & 1) || (ld_out & 1) ||
+                            ((uintptr_t)a->obs_history_in & 7) || ((uintptr_t)a->obs_history_out & 7)))
+    return vfail(GO1_E_ARG, "go1_vel_step: obs_history row strides >= 70 x history_len, even, rows 8-byte aligned");
+  // out = in + 70 with the same stride: a sliding window, new[:, :W - 70] IS old[:, 70:] (no shift)
+  const bool window = a->obs_history_in && ld_in == ld_out && a->obs_history_out == a->obs_history_in + GO1_VEL_NUM_OBS;
   if (a->episode_log_count && (!a->episode_log || a->episode_log_cap < 0))
     return vfail(GO1_E_ARG, "go1_vel_step: a compact episode log needs episode_log and a capacity");
   hipStream_t s = (hipStream_t)stream;
@@ -1430,12 +1441,16 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   K.st = h->st;
   K.a = *a;
   K.env_origins = h->env_origins;
-  K.hist_w = GO1_VEL_NUM_OBS * h->vcfg.history_len;
+  K.hist_w = hist_w;
+  K.hist_ld = ld_out;
   CArgs C = curriculum_args(h);
-  C.hist_in = a->obs_history_in;
+  C.hist_in = window ? nullptr : a->obs_history_in;
   C.hist_out = a->obs_history_out;
+  C.ld_in = ld_in;
+  C.ld_out = ld_out;
   C.hist_w = K.hist_w;
-  C.hist_aligned = C.hist_w % 4 == 0 && ((uintptr_t)C.hist_in % 16) == 0 && ((uintptr_t)C.hist_out % 16) == 0;
+  C.hist_aligned = C.hist_w % 4 == 0 && ld_in % 4 == 0 && ld_out % 4 == 0 && ((uintptr_t)C.hist_in % 16) == 0 &&
+                   ((uintptr_t)C.hist_out % 16) == 0;
   hipEvent_t e0 = (hipEvent_t)a->ev_begin, e1 = (hipEvent_t)a->ev_end;
   auto go = [&](auto kern) {
     if (e0 || e1) hipExtLaunchKernelGGL(kern, dim3(n / SEPB), dim3(TPB), 0, s, e0, e1, 0, h->d_cfg, h->d_vcfg, K);

@@ -122,10 +122,26 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
                        {tr.actions_log_prob, tr.st_actions_log_prob, (int64_t)n}};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t hld = tr.obs_history_ld, hw = tr.num_obs_history;
 #pragma unroll
   for (int s = 0; s < 7; ++s) {
     const Seg g = segs[s];
     if (!g.src) continue;
+    if (s == 2 && hld != hw) {  // a row-strided history window: rows of hw floats, hld apart
+      if (((hw | hld) & 1) == 0 && ((((uintptr_t)g.src) | ((uintptr_t)g.dst)) & 7) == 0) {
+        const int64_t w2 = hw >> 1, n2 = (int64_t)n * w2;
+        for (int64_t i = tid; i < n2; i += stride) {
+          const int64_t r = i / w2, c = i - r * w2;
+          reinterpret_cast<float2*>(g.dst)[i] = *reinterpret_cast<const float2*>(g.src + r * hld + 2 * c);
+        }
+      } else {
+        for (int64_t i = tid; i < g.n; i += stride) {
+          const int64_t r = i / hw;
+          g.dst[i] = g.src[r * hld + (i - r * hw)];
+        }
+      }
+      continue;
+    }
     const bool vec = ((((uintptr_t)g.src) | ((uintptr_t)g.dst)) & 15) == 0;
     if (vec) {
       const int64_t n4 = g.n >> 2;
@@ -371,7 +387,7 @@ __device__ void policy_fallback(const go1_policy_args& P, int e0, int ne, bool a
   float* yb = ya + 512;
   for (int e = 0; e < ne; ++e) {
     const size_t ge = (size_t)(e0 + e);
-    for (int k = threadIdx.x; k < H; k += blockDim.x) x[k] = P.obs_history[ge * H + k];
+    for (int k = threadIdx.x; k < H; k += blockDim.x) x[k] = P.obs_history[ge * P.hist_ld + k];
     __syncthreads();
     if (actor) {
       dense_f32(L[0].wf, L[0].b, 256, H, x, ya, true);
@@ -447,7 +463,7 @@ __global__ __launch_bounds__(64 * PW) void policy_kernel(go1_policy_args P) {
   for (int idx = tid; idx < 16 * PIN; idx += 64 * PW) {
     const int e = idx / PIN, k = idx - e * PIN;
     float v = 0.0f;
-    if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_dim + k];
+    if (e < ne && k < P.hist_dim) v = P.obs_history[(size_t)(e0 + e) * P.hist_ld + k];
     act_store1(va, k, e, v, &s_ovf);
     act_store1(vc, k, e,
                (e < ne && k >= P.hist_dim && k < P.hist_dim + NP)
@@ -755,13 +771,22 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
   const int fs = nch == 1 ? H : PIN;
   if (nch == 1) {
     constexpr int NI = (ET * 16 * PIN + 64 * PW - 1) / (64 * PW);
-    const float* src = P.obs_history + (size_t)e0 * H;
+    const int64_t LD = P.hist_ld;
+    const float* src = P.obs_history + (size_t)e0 * LD;
     const int total = ne * H;
     float v[NI];
+    if (LD == H) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int j = tid + i * 64 * PW;
-      v[i] = j < total ? src[j] : 0.0f;
+      for (int i = 0; i < NI; ++i) {
+        const int j = tid + i * 64 * PW;
+        v[i] = j < total ? src[j] : 0.0f;
+      }
+    } else {  // rows of a wider buffer (row-strided window)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int j = tid + i * 64 * PW, r = j / H;
+        v[i] = j < total ? src[(size_t)r * LD + (j - r * H)] : 0.0f;
+      }
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -797,7 +822,7 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
       const int e = tid / TPE, kk = tid - e * TPE;
       const bool live = e < ET * 16;
       const bool row = live && e < ne;
-      const float* src = P.obs_history + (size_t)(e0 + (row ? e : 0)) * H;
+      const float* src = P.obs_history + (size_t)(e0 + (row ? e : 0)) * P.hist_ld;
       float v[NI];
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -1162,10 +1187,14 @@ int go1_record_transition(const go1_transition* tr, int32_t n_envs, float gamma,
   if (!tr || n_envs <= 0) return fail(GO1_RT_E_ARG, "go1_record_transition: bad argument");
   if (!tr->rewards || !tr->dones || !tr->values || !tr->st_rewards || !tr->st_dones || !tr->st_values)
     return fail(GO1_RT_E_ARG, "go1_record_transition: rewards / dones / values are required");
+  if (tr->obs_history && tr->obs_history_ld != 0 && tr->obs_history_ld < tr->num_obs_history)
+    return fail(GO1_RT_E_ARG, "go1_record_transition: obs_history_ld < num_obs_history");
+  go1_transition T = *tr;
+  if (T.obs_history_ld == 0) T.obs_history_ld = T.num_obs_history;
   int64_t big = (int64_t)n_envs * (tr->num_obs + tr->num_obs_history);
   int blocks = (int)((big / 4 + 255) / 256);
   blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
-  hipLaunchKernelGGL(record_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *tr, n_envs, gamma);
+  hipLaunchKernelGGL(record_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, T, n_envs, gamma);
   RT_TRY(hipGetLastError());
   return GO1_OK_RT;
 }
@@ -1203,7 +1232,10 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
     if (!args->layers[i].w || !args->layers[i].b || !args->layers[i].wf)
       return fail(GO1_RT_E_ARG, "go1_policy_forward: missing layer (split, bias and f32 weights are required)");
   if (args->variant != 0 && args->variant != 1) return fail(GO1_RT_E_ARG, "go1_policy_forward: variant");
+  if (args->hist_ld != 0 && args->hist_ld < args->hist_dim)
+    return fail(GO1_RT_E_ARG, "go1_policy_forward: hist_ld < hist_dim");
   go1_policy_args P = *args;
+  if (P.hist_ld == 0) P.hist_ld = P.hist_dim;
   if (P.variant == 0)
     hipLaunchKernelGGL(policy_kernel_split, dim3((P.n_envs + SE_A - 1) / SE_A + (P.n_envs + SE_C - 1) / SE_C),
                        dim3(64 * PW), 0, (hipStream_t)stream, P);

@@ -87,7 +87,8 @@ class _Transition(C.Structure):
                                           "st_sigma", "st_actions_log_prob", "st_values", "st_rewards",
                                           "st_dones")] + [
         ("num_obs", C.c_int32), ("num_priv", C.c_int32), ("num_obs_history", C.c_int32), ("num_actions", C.c_int32),
-        ("time_outs_flag", C.c_void_p), ("time_outs_pending", C.c_void_p), ("time_outs_dst", C.c_void_p)]
+        ("time_outs_flag", C.c_void_p), ("time_outs_pending", C.c_void_p), ("time_outs_dst", C.c_void_p),
+        ("obs_history_ld", C.c_int64)]
 
 
 class _PolicyLayer(C.Structure):
@@ -100,7 +101,8 @@ class _PolicyArgs(C.Structure):
                 ("action_sigma", C.c_void_p), ("log_prob", C.c_void_p), ("rng_seed", C.c_uint64),
                 ("rng_step", C.c_uint64), ("env_id_offset", C.c_int32), ("n_envs", C.c_int32),
                 ("hist_dim", C.c_int32), ("num_actions", C.c_int32), ("num_priv", C.c_int32),
-                ("variant", C.c_int32), ("overflow", C.c_void_p), ("layers", _PolicyLayer * 11)]
+                ("variant", C.c_int32), ("overflow", C.c_void_p), ("layers", _PolicyLayer * 11),
+                ("hist_ld", C.c_int64)]
 
 
 def _pack_linear(lin):
@@ -178,8 +180,8 @@ class FusedPolicy:
             self.pack()
         h = obs_history.detach()
         p = privileged_obs.detach()
-        if not h.is_contiguous():
-            h = h.contiguous()
+        if h.dim() != 2 or h.stride(1) != 1 or h.stride(0) < h.shape[1]:
+            h = h.contiguous()  # row-strided windows (the velocity env's history) are read in place
         if not p.is_contiguous():
             p = p.contiguous()
         n = h.shape[0]
@@ -192,7 +194,7 @@ class FusedPolicy:
         a.variant = self.variant
         a.obs_history, a.privileged_obs = h.data_ptr(), p.data_ptr()
         a.action_mean, a.value, a.latent = mean.data_ptr(), value.data_ptr(), latent.data_ptr()
-        a.n_envs, a.hist_dim = n, h.shape[1]
+        a.n_envs, a.hist_dim, a.hist_ld = n, h.shape[1], h.stride(0)
         out = (mean, value, latent)
         if sample is not None:
             actions = torch.empty(n, na, device=dev)
@@ -259,8 +261,12 @@ class HipRolloutKernels:
                 continue
             if v.dtype == torch.bool:
                 v = v.view(torch.uint8)
-            if not v.is_contiguous():
+            if k == "obs_history" and v.dim() == 2 and v.stride(1) == 1 and v.stride(0) >= v.shape[1]:
+                t.obs_history_ld = v.stride(0)  # a row-strided window is copied row by row
+            elif not v.is_contiguous():
                 v = v.contiguous()
+            if k == "obs_history" and v.is_contiguous():
+                t.obs_history_ld = 0
             keep.append(v)
             setattr(t, k, v.data_ptr())
         for k, buf in st._tr_dst:

@@ -7,7 +7,7 @@ import ctypes as C
 
 from . import vel_layout as VL
 
-GO1_VEL_ABI_VERSION = 1
+GO1_VEL_ABI_VERSION = 2
 GO1_VEL_NUM_COMMANDS = VL.NUM_COMMANDS
 GO1_VEL_NUM_OBS = VL.NUM_OBS
 GO1_VEL_MAX_TERMS = VL.MAX_TERMS
@@ -98,4 +98,5 @@ class Go1VelStepArgs(C.Structure):
         ("contact_forces", P), ("obs_history_in", P), ("obs_history_out", P), ("aux", P),
         ("episode_log", P), ("episode_log_count", P), ("episode_log_cap", I32), ("episode_log_tag", I32),
         ("dbg_torques", P), ("dbg_terms", P), ("dbg_gait", P), ("ev_begin", P), ("ev_end", P),
+        ("obs_history_in_ld", C.c_int64), ("obs_history_out_ld", C.c_int64),
     ]

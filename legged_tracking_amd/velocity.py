@@ -30,7 +30,10 @@ from . import abi, config as CF, layout as L, vel_abi as VA, vel_layout as VL, v
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GO1_VEL_LIB_OVERRIDE") or os.path.join(HERE, "_build", "libgo1_velocity.so")
 OUT_RING = 4
-HIST_RING = 3
+# obs_history windows per wide buffer: the history lives in rows of width W + 70 x HIST_WINDOW, and each step
+# returns the next W-wide window of the row (go1_vel_step's sliding-window form, no shift); the rows are
+# rewound -- the last W - 70 columns shifted into the other buffer -- once every HIST_WINDOW steps
+HIST_WINDOW = 32
 _lib = None
 
 
@@ -417,8 +420,8 @@ class VelocityTrackingEasyEnv:
         self._reset = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
         self._time_out = torch.zeros((OUT_RING, n), dtype=torch.bool, device=dev)
         self._slot = 0
-        self._hist = None  # HIST_RING (n, 70 x history) buffers when a HistoryWrapper attaches
-        self._hist_slot = 0
+        self._hist = None  # 2 wide (n, 70 x (history + HIST_WINDOW)) buffers when a HistoryWrapper attaches
+        self._hist_buf, self._hist_off = 0, 0  # buffer and window (in observations) of the last returned history
         self._last_hist = None
         # compact episode log: one row per reset env (n_terms + 1 sums, tag, env)
         self._log_cap = max(4 * n, 1024)
@@ -535,13 +538,38 @@ class VelocityTrackingEasyEnv:
 
     # ---------------------------------------------------------------- history (HistoryWrapper fusion)
     def attach_history(self, length):
-        """Fuse HistoryWrapper.step's shift-and-append into the step: the env keeps HIST_RING buffers of
-        (n, length x num_obs); go1_vel_step reads the wrapper's current history and writes the next."""
+        """Fuse HistoryWrapper.step's shift-and-append into the step.  The env keeps two buffers of rows
+        70 x (length + HIST_WINDOW) wide; the history a step returns is a (n, 70 x length) window of one of
+        them (row stride 70 x (length + HIST_WINDOW), inner stride 1): the next step's window starts one
+        observation further, so cat(obs_history[:, 70:], obs) is only the new observation written past the
+        window's end (history_wrapper.py:22 without moving 33 MB per step at 4096 envs x 30).  Every
+        HIST_WINDOW steps, or when the caller hands in a history that is not the last window, the step
+        shifts it into the start of the other buffer.  A returned window keeps its values for HIST_WINDOW
+        further steps; the wrapper's in-place zeroing (reset / reset_idx) writes through to the following
+        windows, as it would to the reference's tensor."""
         if length != self._vcfg.history_len:
             return False
         if self._hist is None:
-            self._hist = torch.zeros((HIST_RING, self.num_envs, length * self.num_obs), device=self.device)
+            self._hist = torch.zeros((2, self.num_envs, (length + HIST_WINDOW) * self.num_obs), device=self.device)
         return True
+
+    def _history_windows(self, history_in):
+        """-> (in, in_ld, out view) of this step's history (see attach_history)."""
+        no, W = self.num_obs, self._vcfg.history_len * self.num_obs
+        last = self._last_hist
+        if (last is not None and history_in.data_ptr() == last.data_ptr() and history_in.stride() == last.stride()
+                and self._hist_off < HIST_WINDOW):
+            self._hist_off += 1
+            o = self._hist_off * no
+            return history_in, history_in.stride(0), self._hist[self._hist_buf][:, o:o + W]
+        if history_in.shape != (self.num_envs, W) or history_in.stride(1) != 1:
+            history_in = history_in.contiguous()
+        if history_in.untyped_storage().data_ptr() == self._hist.untyped_storage().data_ptr() and \
+                (last is None or history_in.data_ptr() != last.data_ptr()):
+            history_in = history_in.clone()  # an older window: it may lie where the rewind writes
+        self._hist_buf ^= 1
+        self._hist_off = 0
+        return history_in, history_in.stride(0), self._hist[self._hist_buf][:, :W]
 
     # ---------------------------------------------------------------- step
     def step(self, actions, history_in=None):
@@ -591,12 +619,10 @@ class VelocityTrackingEasyEnv:
         args.episode_log_tag = self._log_tag
         hist = None
         if history_in is not None and self._hist is not None:
-            slot = self._hist_slot
-            if self._hist[slot].data_ptr() == history_in.data_ptr():
-                slot = (slot + 1) % HIST_RING
-            hist = self._hist[slot]
-            self._hist_slot = (slot + 1) % HIST_RING
-            args.obs_history_in, args.obs_history_out = history_in.data_ptr(), hist.data_ptr()
+            hin, ld_in, hist = self._history_windows(history_in)
+            args.obs_history_in, args.obs_history_out = hin.data_ptr(), hist.data_ptr()
+            args.obs_history_in_ld, args.obs_history_out_ld = ld_in, hist.stride(0)
+            self._hist_in_keep = hin  # alive until the launch is enqueued
         else:
             args.obs_history_in = args.obs_history_out = None
         events = self.kernel_events.popleft() if self.kernel_events else None

@@ -246,13 +246,26 @@ def test_vel_native_run_properties():
     gen = torch.Generator(device=DEV).manual_seed(0)
     n_reset = 0
     grid = env.env.curriculum_grid
+    # the history is a sliding window over wider rows (velocity.py attach_history): every step is
+    # cat(prev[:, 70:], obs) exactly, across the rewinds every HIST_WINDOW steps; a returned window keeps
+    # its values for HIST_WINDOW steps (unless written in place); the wrapper's reset_idx zeroing reaches
+    # the following windows
+    old = []
     for t in range(200):
         act = torch.randn((n, 12), device=DEV, generator=gen)
         o, rew, done, info = env.step(act)
         h = o["obs_history"]
-        if t < 3:
-            torch.testing.assert_close(h[:, :-70], prev_hist[:, 70:], rtol=0, atol=0)
-            torch.testing.assert_close(h[:, -70:], o["obs"], rtol=0, atol=0)
+        torch.testing.assert_close(h[:, :-70], prev_hist[:, 70:], rtol=0, atol=0)
+        torch.testing.assert_close(h[:, -70:], o["obs"], rtol=0, atol=0)
+        old.append((h, h.clone()))
+        if len(old) > VEL.HIST_WINDOW:
+            w, c = old.pop(0)
+            assert torch.equal(w, c)
+        if t == 77:
+            ids = torch.arange(0, n, 97, device=DEV)
+            env.obs_history[ids, :] = 0
+            h = env.obs_history
+            old.clear()  # the zeroing also reaches the earlier windows' overlapping columns (shared rows)
         prev_hist = h.clone()
         n_reset += int(done.sum())
     torch.cuda.synchronize()

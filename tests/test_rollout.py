@@ -529,3 +529,49 @@ def test_colsum_kernel_matches_f64_sums_and_is_deterministic():
         scale = x.double().abs().sum(0)
         assert ((got.double() - ref).abs() <= 1e-6 * scale + 1e-6).all(), (rows, cols)
         assert torch.equal(got, R._colsum(x))
+
+
+@pytest.mark.gpu
+def test_policy_and_record_read_row_strided_history_windows():
+    """The velocity env returns obs_history as a window of wider rows (row stride > width, velocity.py
+    attach_history): the fused policy kernel (both launches) and the record kernel read it in place and
+    give exactly what they give for the same history made contiguous."""
+    torch.manual_seed(4)
+    n, hist, npriv, wide = 777, 2100, 2, 2100 + 70 * 5
+    ac = R.ActorCritic(70, npriv, hist, 12).to("cuda:0")
+    kern = R.HipRolloutKernels()
+    pol = kern.policy(ac)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    buf = torch.randn(n, wide, device="cuda", generator=g)
+    for off in (0, 70, 350):  # 16-byte aligned and 8-byte aligned window starts
+        win = buf[:, off:off + hist]
+        assert not win.is_contiguous() and win.stride() == (wide, 1)
+        p = torch.randn(n, npriv, device="cuda", generator=g)
+        got = pol.forward(win, p)
+        want = pol.forward(win.contiguous(), p)
+        for a, b in zip(got, want):
+            assert torch.equal(a, b)
+    # the single-workgroup variant (one 288-input chunk: the strided-block staging path)
+    ac2 = R.ActorCritic(70, npriv, 210, 12).to("cuda:0")
+    pol2 = kern.policy(ac2)
+    pol2.variant = 1
+    win2 = buf[:, 70:280]
+    p = torch.randn(n, npriv, device="cuda", generator=g)
+    for a, b in zip(pol2.forward(win2, p), pol2.forward(win2.contiguous(), p)):
+        assert torch.equal(a, b)
+    pol2.variant = 0
+    for a, b in zip(pol2.forward(win2, p), pol2.forward(win2.contiguous(), p)):
+        assert torch.equal(a, b)
+    # record: the storage row equals the window
+    st = R.RolloutStorage(n, 2, [70], [npriv], [hist], [12], device="cuda:0", kernels=kern)
+    for step, off in enumerate((70, 140)):
+        t = R.RolloutStorage.Transition()
+        t.observations = torch.randn(n, 70, device="cuda", generator=g)
+        t.privileged_observations = torch.randn(n, npriv, device="cuda", generator=g)
+        t.observation_histories = buf[:, off:off + hist]
+        t.actions = t.action_mean = t.action_sigma = torch.randn(n, 12, device="cuda", generator=g)
+        t.actions_log_prob = t.values = t.rewards = torch.randn(n, device="cuda", generator=g)
+        t.dones = torch.zeros(n, dtype=torch.bool, device="cuda")
+        st.add_transitions(t, 0.99)
+        torch.cuda.synchronize()
+        assert torch.equal(st.observation_histories[step], buf[:, off:off + hist])
