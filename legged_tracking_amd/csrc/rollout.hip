@@ -1225,6 +1225,10 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
     const int g_last = (PIN / 32) * ((GL + PIN / 32 - 1) / (PIN / 32) - 1);
     if (args->variant == 1 && kin > PIN)
       return fail(GO1_RT_E_ARG, "go1_policy_forward: variant 1 takes at most 288 history + privileged inputs");
+    // variant 1 walks PIN / 32 K groups of the packed first layers (compile-time G): the packing
+    // (ceil(k / 32) groups per output tile) must have exactly that many, or its reads leave the buffer
+    if (args->variant == 1 && (args->hist_dim + 31) / 32 != PIN / 32)
+      return fail(GO1_RT_E_ARG, "go1_policy_forward: variant 1 needs 257..288 history inputs (9 packed K groups)");
     if (gl < g_last || kin > 16384)
       return fail(GO1_RT_E_ARG, "go1_policy_forward: history width not supported by the chunked first layers");
   }

@@ -551,11 +551,16 @@ def test_policy_and_record_read_row_strided_history_windows():
         want = pol.forward(win.contiguous(), p)
         for a, b in zip(got, want):
             assert torch.equal(a, b)
-    # the single-workgroup variant (one 288-input chunk: the strided-block staging path)
-    ac2 = R.ActorCritic(70, npriv, 210, 12).to("cuda:0")
+    # the single-workgroup variant (one 288-input chunk: the strided-block staging path); it walks exactly
+    # nine packed K groups, so a narrower history is refused at the boundary before any launch
+    narrow = kern.policy(R.ActorCritic(70, npriv, 210, 12).to("cuda:0"))
+    narrow.variant = 1
+    with pytest.raises(RuntimeError, match="variant 1"):
+        narrow.forward(buf[:, 70:280], torch.randn(n, npriv, device="cuda", generator=g))
+    ac2 = R.ActorCritic(70, npriv, 265, 12).to("cuda:0")
     pol2 = kern.policy(ac2)
     pol2.variant = 1
-    win2 = buf[:, 70:280]
+    win2 = buf[:, 70:335]
     p = torch.randn(n, npriv, device="cuda", generator=g)
     for a, b in zip(pol2.forward(win2, p), pol2.forward(win2.contiguous(), p)):
         assert torch.equal(a, b)
