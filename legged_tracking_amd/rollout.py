@@ -808,7 +808,9 @@ class PPO:
             self._graph_draw = (torch.zeros(mb, na, device=self.device), torch.ones(mb, na, device=self.device))
 
         def step():
-            self._minibatch_step([x[idx] for x in flat], gacc, sample=False)
+            # the generator's obs and critic-obs batches (flat[0:2]) are never read by the step (the nets take the
+            # history and the privileged obs): not gathered, two index kernels less per mini-batch
+            self._minibatch_step([None, None] + [x[idx] for x in flat[2:]], gacc, sample=False)
 
         for _ in range(A.num_learning_epochs):
             for i in range(A.num_mini_batches):
