@@ -86,7 +86,7 @@ typedef struct go1_policy_args {
   uint64_t rng_seed, rng_step; /* Philox key / counter, one counter value per call */
   int32_t env_id_offset;       /* global id of row 0 (rank * n) */
   int32_t n_envs, hist_dim, num_actions;
-  int32_t num_priv;            /* privileged obs = latent width, 1 .. 8.  variant 1: 257 <= hist_dim and hist_dim + num_priv <= 288
+  int32_t num_priv;            /* privileged obs = latent width, 1 .. 8.  variant 1: 257 <= hist_dim <= 288 - num_priv
                                   (it walks exactly nine packed K groups; anything else is GO1_RT_E_ARG);
                                   variant 0 streams the inputs in chunks of 288 (hist_dim + num_priv <= 16384,
                                   the groups of 32 that hold the latent inside the last chunk) */

@@ -202,7 +202,8 @@ typedef struct go1_vel_step_args {
                                        only the new observation is written) */
   float* aux;                       /* (n_envs, GO1_VEL_AUX) or NULL */
   /* compact episode log, a ring: each env reset this step writes n_terms + 3 floats (n_terms + 1 episode
-     sums, tag, env index) at row atomicAdd(*episode_log_count, 1) % episode_log_cap */
+     sums, tag, env index) at row (uint32) atomicAdd(*episode_log_count, 1) % episode_log_cap; the tag is
+     stored as its int32 bits (exact for every tag; read the column as int32), the env index as a float */
   float* episode_log;
   int32_t* episode_log_count;
   int32_t episode_log_cap;

@@ -30,6 +30,7 @@ import os
 import runpy
 import sys
 import types
+import warnings
 
 from . import config as CF
 
@@ -67,7 +68,12 @@ def install(root_dir=None):
                      eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX"):
             if os.environ.get("GO1_NUM_ENVS"):
                 num_envs = int(os.environ["GO1_NUM_ENVS"])
-            if cfg is not None and os.environ.get("GO1_VEL_MESH", "plane") == "plane":
+            if cfg is not None and os.environ.get("GO1_VEL_MESH", "plane") == "plane" and \
+                    cfg.terrain.mesh_type != "plane":
+                warnings.warn(f"legged_tracking_amd.compat: the velocity script's terrain mesh_type "
+                              f"{cfg.terrain.mesh_type!r} is replaced by 'plane' (BASELINE configs[1]; the script's "
+                              f"own terrain is not on the accelerated path). Set GO1_VEL_MESH=trimesh to keep it "
+                              f"(the env then raises NotImplementedError).", RuntimeWarning, stacklevel=2)
                 cfg.terrain.mesh_type = "plane"
             super().__init__(sim_device, headless, num_envs, prone, deploy, cfg, eval_cfg, initial_dynamics_dict,
                              physics_engine)

@@ -598,11 +598,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       base = __shfl(base, 0);
       const int row = base + __popcll(rmask & ((1ull << (4 * el)) - 1ull));
       if (reset && A.episode_log_cap > 0) {  // a ring: the newest rows overwrite the oldest
-        float* lg = A.episode_log + (size_t)(row % A.episode_log_cap) * (NE + 2);
+        float* lg = A.episode_log + (size_t)((uint32_t)row % (uint32_t)A.episode_log_cap) * (NE + 2);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
           if (sub16 + 16 * h < NE) lg[sub16 + 16 * h] = es[h];
-        if (sub16 == 0) { lg[NE] = (float)A.episode_log_tag; lg[NE + 1] = (float)e; }
+        if (sub16 == 0) { lg[NE] = __int_as_float(A.episode_log_tag); lg[NE + 1] = (float)e; }
       }
     }
   }
@@ -769,9 +769,9 @@ __global__ __launch_bounds__(TPB) void go1_vel_reset_kernel(const go1_vel_config
     if (episode_log_count) {
       const int row = atomicAdd(episode_log_count, 1);
       if (episode_log_cap > 0) {
-        float* lg = episode_log + (size_t)(row % episode_log_cap) * (NE + 2);
+        float* lg = episode_log + (size_t)((uint32_t)row % (uint32_t)episode_log_cap) * (NE + 2);
         for (int k = 0; k < NE; ++k) lg[k] = st.episode_sums[(size_t)e * NE + k];
-        lg[NE] = (float)episode_log_tag;
+        lg[NE] = __int_as_float(episode_log_tag);
         lg[NE + 1] = (float)e;
       }
     }

@@ -1223,12 +1223,13 @@ int go1_policy_forward(const go1_policy_args* args, void* stream) {
     // groups that hold the latent must lie in the last chunk (its planes receive the latent)
     const int kin = args->hist_dim + args->num_priv, gl = args->hist_dim / 32, GL = (kin + 31) / 32;
     const int g_last = (PIN / 32) * ((GL + PIN / 32 - 1) / (PIN / 32) - 1);
-    if (args->variant == 1 && kin > PIN)
-      return fail(GO1_RT_E_ARG, "go1_policy_forward: variant 1 takes at most 288 history + privileged inputs");
-    // variant 1 walks PIN / 32 K groups of the packed first layers (compile-time G): the packing
-    // (ceil(k / 32) groups per output tile) must have exactly that many, or its reads leave the buffer
-    if (args->variant == 1 && (args->hist_dim + 31) / 32 != PIN / 32)
-      return fail(GO1_RT_E_ARG, "go1_policy_forward: variant 1 needs 257..288 history inputs (9 packed K groups)");
+    // variant 1 stages all inputs at once (kin <= PIN) and walks PIN / 32 K groups of the packed first layers
+    // (compile-time G): the packing (ceil(k / 32) groups per output tile) must have exactly that many, or its
+    // reads leave the buffer.  Together: 257 <= hist_dim <= 288 - num_priv.
+    if (args->variant == 1 && (kin > PIN || (args->hist_dim + 31) / 32 != PIN / 32))
+      return fail(GO1_RT_E_ARG, "go1_policy_forward: variant 1 needs hist_dim in 257.." +
+                                    std::to_string(PIN - args->num_priv) + " (288 - num_priv; 9 packed K groups), got " +
+                                    std::to_string(args->hist_dim));
     if (gl < g_last || kin > 16384)
       return fail(GO1_RT_E_ARG, "go1_policy_forward: history width not supported by the chunked first layers");
   }

@@ -802,7 +802,9 @@ class HistoryWrapper:
 
     def reset_idx(self, env_ids):
         ret = self.env.reset_idx(env_ids)
-        if self._alias or self._tap:  # never zero rows of the env's obs / its output ring in place
+        # never zero rows of the env's obs / its output ring in place; a fused window shares columns with the
+        # windows returned before it (velocity.py), so it is cloned too: the next step then takes the rewind path
+        if self._alias or self._tap or self._fused:
             self.obs_history = self.obs_history.clone()
         self.obs_history[env_ids, :] = 0
         return ret
@@ -810,7 +812,7 @@ class HistoryWrapper:
     def reset(self):
         ret = self.env.reset()
         privileged_obs = self.env.get_privileged_observations()
-        if self._alias or self._tap:
+        if self._alias or self._tap or self._fused:
             self.obs_history = torch.zeros_like(self.obs_history)
         else:
             self.obs_history[:, :] = 0

@@ -783,6 +783,16 @@ class PPO:
 
     GRAPH_WARMUP = 3  # eager mini-batches (on a side stream) before the capture: lazy handles and optimizer state
 
+    _ARG_KEYS = ("clip_param", "value_loss_coef", "use_clipped_value_loss", "entropy_coef", "max_grad_norm",
+                 "desired_kl", "schedule", "num_adaptation_module_substeps", "selective_adaptation_module_loss")
+
+    def _torch_graph_key(self, mb, flat):
+        """What a captured mini-batch step bakes in: the batch size, the storage it gathers from, the PPO_Args
+        scalars of the loss / clip / schedule, and the optimizers' state tensors (load_state_dict replaces them)."""
+        opt_state = tuple(id(t) for o in (self.optimizer, self.adaptation_module_optimizer)
+                          for s in o.state.values() for t in s.values() if isinstance(t, torch.Tensor))
+        return (mb, tuple(x.data_ptr() for x in flat), tuple(getattr(PPO_Args, k) for k in self._ARG_KEYS), opt_state)
+
     def _graphed_minibatches(self, acc):
         """The mini-batch loop of update() with the step replayed from a HIP graph: the batch is gathered inside the
         graph from the storage with a static index buffer, so a mini-batch costs one index copy and one replay."""
@@ -794,8 +804,9 @@ class PPO:
         flat = [x.flatten(0, 1) for x in (st.observations, st.observations, st.privileged_observations,
                                          st.observation_histories, st.actions, st.values, st.advantages,
                                          st.returns, st.actions_log_prob, st.mu, st.sigma)]
-        if self._graph is not None and self._graph_key != (mb, tuple(x.data_ptr() for x in flat)):
-            self._graph = None  # new storage: capture again
+        key = self._torch_graph_key(mb, flat)
+        if self._graph is not None and self._graph_key != key:
+            self._graph = None  # new storage, PPO_Args or optimizer state: capture again
             self._graph_warm = 0
         if self._graph is None and self._graph_warm == 0:
             self._graph_idx = torch.empty(mb, dtype=torch.int64, device=self.device)
@@ -812,27 +823,36 @@ class PPO:
             # history and the privileged obs): not gathered, two index kernels less per mini-batch
             self._minibatch_step([None, None] + [x[idx] for x in flat[2:]], gacc, sample=False)
 
+        # warm-up and capture run on ONE persistent side stream: the parameters' AccumulateGrad nodes are created
+        # there and every later backward (warm-up, capture) runs on the same stream (a fresh stream per warm-up
+        # mini-batch made torch warn about a stream mismatch of the accumulation)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        side = self._side
         for _ in range(A.num_learning_epochs):
             for i in range(A.num_mini_batches):
                 idx.copy_(indices[i * mb:(i + 1) * mb])
                 torch.normal(*self._graph_draw)
                 if self._graph is not None:
                     self._graph.replay()
-                elif self._graph_warm < self.GRAPH_WARMUP:
-                    side = torch.cuda.Stream(self.device)
-                    side.wait_stream(torch.cuda.current_stream(self.device))
+                    continue
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                if self._graph_warm < self.GRAPH_WARMUP:
                     with torch.cuda.stream(side):
                         step()
-                    torch.cuda.current_stream(self.device).wait_stream(side)
                     self._graph_warm += 1
                 else:
                     torch.cuda.synchronize(self.device)
+                    for p in self.actor_critic.parameters():
+                        p.grad = None
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
+                    with torch.cuda.graph(g, stream=side):
                         step()
                     self._graph = g
-                    self._graph_key = (mb, tuple(x.data_ptr() for x in flat))
-                    g.replay()  # the capture recorded the step without running it
+                    self._graph_key = self._torch_graph_key(mb, flat)  # the optimizer state exists by now
+                    with torch.cuda.stream(side):
+                        g.replay()  # the capture recorded the step without running it
+                torch.cuda.current_stream(self.device).wait_stream(side)
         acc += gacc
         gacc.zero_()
 

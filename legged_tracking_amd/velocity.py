@@ -672,7 +672,8 @@ class VelocityTrackingEasyEnv:
         rows = self._log[:cnt].cpu().numpy()
         ne = len(self.episode_keys)
         if cnt:  # the latest reset's rows (the reference rebuilds the dict at each reset_idx, :199-205)
-            rows = rows[rows[:, ne] == rows[:, ne].max()]
+            tags = np.ascontiguousarray(rows[:, ne]).view(np.int32)  # the kernels store the tag's int32 bits
+            rows = rows[tags == tags.max()]
         out = {}
         if rows.shape[0]:
             rows = rows[np.argsort(rows[:, ne + 1], kind="stable")]

@@ -102,3 +102,5 @@ def test_reference_velocity_train_script_reaches_the_velocity_env(tmp_path):
                        timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "VEL_ENV_OK 4096 plane 19" in r.stdout, r.stdout[-2000:]
+    # the rewrite of the script's trimesh terrain is announced, never silent
+    assert "mesh_type 'trimesh' is replaced by 'plane'" in r.stderr, r.stderr[-2000:]

@@ -494,26 +494,41 @@ def test_ppo_update_graph_replays_the_eager_update(monkeypatch):
     """The HIP-graph mini-batch step (PPO._graphed_minibatches: 3 eager warm-up mini-batches, one capture,
     replays) computes the eager update: two consecutive updates from the reference fixture's storage, with
     the graph captured in the first and replayed through the second, against GO1_PPO_GRAPH=0."""
+    import warnings
     d = _fixture()
     runs = {}
+    clip0 = R.PPO_Args.clip_param
     for flag in ("0", "1"):
         monkeypatch.setenv("GO1_PPO_GRAPH", flag)
-        alg, losses = _ppo_update_from_fixture(d, "cuda:0", R.HipRolloutKernels())
-        assert (alg._graph is not None) == (flag == "1")
-        st = alg.storage
-        for k in ("observations", "privileged_observations", "observation_histories", "actions", "values",
-                  "returns", "actions_log_prob", "advantages", "mu", "sigma", "rewards"):
-            getattr(st, k).copy_(torch.from_numpy(d["upd/storage/" + k]))
-        st.step = st.num_transitions_per_env
-        torch.manual_seed(5)
-        losses2 = alg.update()
-        runs[flag] = (losses, losses2, alg.learning_rate,
+        with warnings.catch_warnings(record=True) as wrec:
+            warnings.simplefilter("always")
+            alg, losses = _ppo_update_from_fixture(d, "cuda:0", R.HipRolloutKernels())
+            assert (alg._graph is not None) == (flag == "1")
+            st = alg.storage
+            out = [losses]
+            for upd in range(2):
+                for k in ("observations", "privileged_observations", "observation_histories", "actions", "values",
+                          "returns", "actions_log_prob", "advantages", "mu", "sigma", "rewards"):
+                    getattr(st, k).copy_(torch.from_numpy(d["upd/storage/" + k]))
+                st.step = st.num_transitions_per_env
+                torch.manual_seed(5 + upd)
+                g_before = alg._graph
+                if upd == 1:  # a PPO_Args change between updates: the captured step must not replay stale values
+                    R.PPO_Args.clip_param = 0.15
+                try:
+                    out.append(alg.update())
+                finally:
+                    R.PPO_Args.clip_param = clip0
+                if flag == "1":
+                    assert (alg._graph is g_before) == (upd == 0), "replayed across updates, recaptured on a change"
+        assert not [w for w in wrec if "AccumulateGrad" in str(w.message)], [str(w.message) for w in wrec]
+        runs[flag] = (out, alg.learning_rate,
                       {k: v.detach().cpu().numpy() for k, v in alg.actor_critic.state_dict().items()})
     e, g = runs["0"], runs["1"]
-    np.testing.assert_allclose(np.array(g[0] + g[1]), np.array(e[0] + e[1]), rtol=1e-5, atol=1e-7)
-    assert g[2] == e[2]
-    dmax = max(float(np.abs(g[3][k] - e[3][k]).max()) for k in e[3])
-    print(f"\ngraph vs eager after two updates: max |dw| {dmax:.2e}")
+    np.testing.assert_allclose(np.array(sum(g[0], ())), np.array(sum(e[0], ())), rtol=1e-5, atol=1e-7)
+    assert g[1] == e[1]
+    dmax = max(float(np.abs(g[2][k] - e[2][k]).max()) for k in e[2])
+    print(f"\ngraph vs eager after three updates (PPO_Args changed before the third): max |dw| {dmax:.2e}")
     assert dmax <= 1e-5, dmax
 
 
