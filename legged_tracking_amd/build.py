@@ -20,6 +20,7 @@ LIBS = {
     "libgo1_mi355x.so": (["go1_step.hip", "go1_terrain.hip"],
                          ["pmath.h", "go1_device.h", "go1_model_consts.h", "go1_spec.h", os.path.join(INC, "go1_mi355x.h")], STEP_FLAGS),
     "libgo1_rollout.so": (["rollout.hip"], [os.path.join(INC, "go1_rollout.h")], []),
+    "libgo1_ppo.so": (["ppo_update.hip"], [os.path.join(INC, "go1_ppo.h")], []),
     "libgo1_velocity.so": (["go1_velocity.hip"],
                            ["pmath.h", "go1_device.h", "go1_model_consts.h", os.path.join(INC, "go1_mi355x.h"),
                             os.path.join(INC, "go1_velocity.h")], STEP_FLAGS),

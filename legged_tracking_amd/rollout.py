@@ -856,8 +856,38 @@ class PPO:
         acc += gacc
         gacc.zero_()
 
+    def _engine_on(self):
+        """The hand-written HIP update (ppo_engine.PPOEngine, csrc/ppo_update.hip) on the GPU for the default
+        architecture; GO1_PPO_ENGINE=0 selects the torch autograd update (A/B)."""
+        if torch.device(self.device).type != "cuda" or os.environ.get("GO1_PPO_ENGINE", "1") == "0":
+            return False
+        from . import ppo_engine
+        return ppo_engine.supported(self.actor_critic)
+
     def update(self):
         A = PPO_Args
+        n_up = A.num_learning_epochs * A.num_mini_batches
+        n_ad = n_up * A.num_adaptation_module_substeps
+        if self._engine_on() and A.num_adaptation_module_substeps == 1:
+            from . import ppo_engine
+            if getattr(self, "_engine", None) is None:
+                self._engine = ppo_engine.PPOEngine(self)
+            sums, lr = self._engine.update(A, A.num_mini_batches, A.num_learning_epochs, _world(),
+                                           use_graph=self._graph_on,
+                                           split=os.environ.get("GO1_PPO_SPLIT", "0") == "1")
+            self.learning_rate = lr
+            for g in self.optimizer.param_groups:
+                if isinstance(g["lr"], torch.Tensor):
+                    g["lr"].fill_(lr)
+                else:
+                    g["lr"] = lr
+            if self._dev_lr:
+                self._lr64.fill_(lr)
+                self._lr32.fill_(lr)
+            self.storage.clear()
+            if self.fused is not None:
+                self.fused.pack()  # the rollout kernel reads the updated weights
+            return (sums[0] / n_up, sums[1] / n_up, sums[2] / n_ad, 0.0, 0.0, sums[3] / n_ad, 0.0, 0.0)
         # the loss means accumulate on the device (ppo.py:186-187, 200-201 call .item() per mini-batch:
         # a host sync each); one copy at the end.
         acc = torch.zeros(4, dtype=torch.float32, device=self.device)  # value, surrogate, adapt, adapt_test
@@ -867,8 +897,6 @@ class PPO:
             gen = self.storage.mini_batch_generator(A.num_mini_batches, A.num_learning_epochs)
             for b in gen:
                 self._minibatch_step(b[:11], acc)
-        n_up = A.num_learning_epochs * A.num_mini_batches
-        n_ad = n_up * A.num_adaptation_module_substeps
         self.storage.clear()
         if self.fused is not None:
             self.fused.pack()  # the rollout kernel reads the updated weights

@@ -415,17 +415,20 @@ def test_ppo_update_matches_reference_on_cpu():
 
 
 @pytest.mark.gpu
-def test_ppo_update_matches_reference_on_gpu():
+@pytest.mark.parametrize("engine", ["1", "0"])
+def test_ppo_update_matches_reference_on_gpu(engine, monkeypatch):
     """MI355X: the update's GEMMs run on hipBLASLt with another reduction order than the CPU's.  Adam
     normalises each gradient component, so a component whose gradient is near zero can step by up
     to the learning rate in either direction on either side: the weights may differ by at most the
     schedule's total step, sum_t lr_t < 1e-3 / (1 - 1 / 1.5) = 3e-3 (the adaptive KL rule divides lr
     by 1.5 per minibatch here); 99.99 % of the 700k weights agree within 1e-4, the losses within
     1e-3 relative, and the KL schedule takes the same decisions."""
+    monkeypatch.setenv("GO1_PPO_ENGINE", engine)  # 1: the HIP update engine (default), 0: torch autograd
     d = _fixture()
     alg, losses = _ppo_update_from_fixture(d, "cuda:0", R.HipRolloutKernels())
+    assert (getattr(alg, "_engine", None) is not None) == (engine == "1")
     w = _check_update(d, alg, losses, rtol_loss=1e-3, atol_w=1e-4, atol_max=3e-3)
-    print(f"\nPPO.update on the GPU vs the reference (CPU): max |dw| {w:.2e}")
+    print(f"\nPPO.update on the GPU ({'engine' if engine == '1' else 'torch'}) vs the reference (CPU): max |dw| {w:.2e}")
 
 
 @pytest.mark.gpu
@@ -495,6 +498,7 @@ def test_ppo_update_graph_replays_the_eager_update(monkeypatch):
     replays) computes the eager update: two consecutive updates from the reference fixture's storage, with
     the graph captured in the first and replayed through the second, against GO1_PPO_GRAPH=0."""
     import warnings
+    monkeypatch.setenv("GO1_PPO_ENGINE", "0")  # the torch autograd update's graph (the engine: test_ppo_engine.py)
     d = _fixture()
     runs = {}
     clip0 = R.PPO_Args.clip_param
