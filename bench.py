@@ -220,13 +220,30 @@ def env_sweep(n, dev, steps=100, warmup=10):
             "kernel_ms": kms, "kernel_loop_env_steps_per_s": n * steps / kdt}
 
 
-def rollout_rate(n, dev, steps, warmup):
+def _max_over_ranks(x, world):
+    """The slowest rank's value (the whole job's time) at world > 1 (RCCL all-reduce MAX)."""
+    if world == 1:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _barrier(world):
+    if world > 1:
+        import torch
+        torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+
+def rollout_rate(n, dev, steps, warmup, rank=0, world=1):
     """Secondary line (SURVEY 8(d) "report both env-only and rollout (act + step) rates"): the
     Runner's rollout loop -- fused PPO.act kernel, env.step through TrajectoryTrackingEnv /
-    HistoryWrapper, transition record kernel -- at n envs."""
+    HistoryWrapper, transition record kernel -- at n envs per rank (every rank runs it at world > 1)."""
     import torch
     from legged_tracking_amd import rollout as R
-    env = make_env(n, 0, 1, dev)
+    env = make_env(n, rank, world, dev)
     ac = R.ActorCritic(env.num_obs, env.num_privileged_obs, env.num_obs_history, env.num_actions).to(dev)
     alg = R.PPO(ac, device=dev)
     T = 24
@@ -248,15 +265,17 @@ def rollout_rate(n, dev, steps, warmup):
         for _ in range(warmup):
             one()
         torch.cuda.synchronize()
+        _barrier(world)
         t0 = time.perf_counter()
         for _ in range(steps):
             one()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     env.close()
-    return {"value": n * steps / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+    dt = _max_over_ranks(dt, world)
+    return {"value": n * world * steps / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
             "what": "PPO.act (fused MFMA adaptation+actor+critic kernel, Normal sample) + TrajectoryTrackingEnv.step "
-                    "+ HistoryWrapper + process_env_step record kernel, 1 GPU",
+                    f"+ HistoryWrapper + process_env_step record kernel, {world} GPU(s), slowest rank's time",
             "fused_policy": alg.fused is not None}
 
 
@@ -296,7 +315,7 @@ def velocity_rate(n, dev, steps, warmup):
             "envs_at_episode_start": resets}
 
 
-def learn_rate(n, dev, iters=6, warmup=2, velocity=False):
+def learn_rate(n, dev, iters=6, warmup=2, velocity=False, rank=0, world=1):
     """The whole training loop, as the reference's wandb train/fps measures it (ppo_cse/__init__.py:184:
     (it + 1) x num_envs x num_steps_per_env / elapsed): Runner iterations of rollout (24 x [PPO.act +
     VecEnv.step + record]), compute_returns (GAE) and PPO.update (5 epochs x 4 mini-batches, Adam, the
@@ -309,7 +328,7 @@ def learn_rate(n, dev, iters=6, warmup=2, velocity=False):
         env = E.HistoryWrapper(VEL.VelocityTrackingEasyEnv(sim_device=str(dev), num_envs=n, seed=11))
         env.close = env.env.close
     else:
-        env = make_env(n, 0, 1, dev)
+        env = make_env(n, rank, world, dev)
     runner = R.Runner(env, device=dev, save_dir=None)
     alg, T = runner.alg, runner.num_steps_per_env
     od = env.get_observations()
@@ -318,6 +337,8 @@ def learn_rate(n, dev, iters=6, warmup=2, velocity=False):
     split = {"rollout": 0.0, "gae": 0.0, "update": 0.0}
     for it in range(warmup + iters):
         torch.cuda.synchronize()
+        if it == warmup:
+            _barrier(world)
         t0 = time.perf_counter()
         with torch.inference_mode():
             obs, priv, hist, _ = runner.rollout(obs, priv, hist)
@@ -334,8 +355,11 @@ def learn_rate(n, dev, iters=6, warmup=2, velocity=False):
             split["gae"] += t2 - t1
             split["update"] += t3 - t2
     env.close()
-    it_s = sum(split.values()) / iters
-    return {"value": n * T / it_s, "unit": "env-steps/s", "ms_per_iteration": it_s * 1e3, "iterations": iters,
+    # at world > 1 the ranks meet in the gradient / KL / advantage all-reduces; the job runs at the slowest rank
+    it_s = _max_over_ranks(sum(split.values()), world) / iters
+    split = {k: _max_over_ranks(v, world) for k, v in split.items()}
+    return {"value": n * world * T / it_s, "unit": "env-steps/s", "ms_per_iteration": it_s * 1e3, "iterations": iters,
+            "world": world, "update": getattr(alg, "_engine", None) is not None and "hip-engine" or "torch",
             "split_ms_per_iteration": {k: v / iters * 1e3 for k, v in split.items()},
             "env": "VelocityTrackingEasyEnv (configs[1])" if velocity else "TrajectoryTrackingEnv (configs[2])",
             "fused_policy": runner.alg.fused is not None,
@@ -529,6 +553,14 @@ def main():
     elapsed = max(p[0] for p in per_rank)
     kernel_ms = max(p[1] for p in per_rank)
     kdt = max(p[2] for p in per_rank)
+    # the rollout loop and the whole training loop run on every rank (RCCL all-reduces inside the timed
+    # learn iterations at world > 1); rank 0 reports the slowest rank's time
+    legs = {}
+    if not args.no_rollout:
+        legs["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24), rank=rank,
+                                       world=world)
+    if not args.no_learn:
+        legs["learn"] = learn_rate(n, dev, rank=rank, world=world)
 
     if rank == 0:
         value = n_global * args.steps / elapsed
@@ -584,12 +616,12 @@ def main():
         }
         if args.sweep:
             line["sweep"] = [env_sweep(int(x), dev) for x in args.sweep.split(",")]
-        if not args.no_rollout and world == 1:
-            line["rollout"] = rollout_rate(n, dev, steps=min(args.steps, 240), warmup=min(args.warmup, 24))
+        for k, v in legs.items():
+            line[k] = v
         if not args.no_velocity and world == 1:
-            line["velocity"] = velocity_rate(n, dev, steps=min(args.steps, 300), warmup=min(args.warmup, 30))
-        if not args.no_learn and world == 1:
-            line["learn"] = learn_rate(n, dev)
+            # at least two full 32-step history windows (velocity.py HIST_WINDOW), whatever --steps is
+            line["velocity"] = velocity_rate(n, dev, steps=max(2 * 32, min(args.steps, 300)),
+                                             warmup=min(args.warmup, 30))
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(n, budget_s=args.cpu_budget)
         print(json.dumps(line), flush=True)

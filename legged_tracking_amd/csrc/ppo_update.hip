@@ -161,25 +161,34 @@ __global__ __launch_bounds__(256, 2) void xw_kernel(XwLaunch L) {
   // staging: per instruction 8 rows x 32 k; lane -> row (lane >> 1) & 7, float4 k4 = 2 (lane >> 4) + (lane & 1)
   const int srow = (lane >> 1) & 7, k4 = ((lane >> 4) << 1) | (lane & 1);
   const int mrow0 = mt * TB + w * 32 + srow;  // row of instruction it: mrow0 + 8 it
-  const float* abase = P.a + (size_t)mrow0 * P.lda + 4 * k4;
-  const size_t astep = (size_t)8 * P.lda;
+  // every load is unconditional (rows clamped to M - 1, columns to the row's last 16 bytes) and out-of-range
+  // values are zeroed afterwards: a load under a branch makes hipcc wait for it (vmcnt(0)) right away
+  const float* arow[4];
+  float rmask[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int m = mrow0 + 8 * it;
+    arow[it] = P.a + (size_t)min(m, M - 1) * P.lda;
+    rmask[it] = m < M ? 1.0f : 0.0f;
+  }
+  const int kmax = (int)P.lda - 4;
   f4_t st[4];
+  int stk = 0;  // first column of the staged group: the masks are applied in store(), after the MFMAs, so that the
+                // loads stay in flight across them
   auto load = [&](int g) {
-    const int k = g * 32 + 4 * k4;
+    const int k = g * 32 + 4 * k4, kc = min(k, kmax);
+    stk = k;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      f4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (mrow0 + 8 * it < M && k < P.k0) v = *reinterpret_cast<const f4_t*>(abase + it * astep + g * 32);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = k + i < P.k0 ? v[i] : 0.0f;
-      st[it] = v;
-    }
+    for (int it = 0; it < 4; ++it) st[it] = *reinterpret_cast<const f4_t*>(arow[it] + kc);
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
+      f4_t v = st[it];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (stk + i < P.k0) ? v[i] * rmask[it] : 0.0f;
       h4_t hi, lo;
-      split4(st[it], sa, hi, lo);
+      split4(v, sa, hi, lo);
       const int row = w * 32 + it * 8 + srow;
       reinterpret_cast<h4_t*>(&sA[buf][0][k4 >> 1][row])[k4 & 1] = hi;
       reinterpret_cast<h4_t*>(&sA[buf][1][k4 >> 1][row])[k4 & 1] = lo;
@@ -213,23 +222,60 @@ __global__ __launch_bounds__(256, 2) void xw_kernel(XwLaunch L) {
   load(0);
   store(0);
 #if PPO_XW_V == 1
-  // weight fragments one group ahead in registers
+  // weight fragments and the A tile of the next group in flight across this group's MFMAs: every load is
+  // unconditional (the last group re-loads itself), the LDS store of the staged group follows the MFMAs
   h8_t wh0[4], wl0[4], wh1[4], wl1[4];
   loadw(0, wh0, wl0);
   __syncthreads();
   auto body = [&](int g, int cur, h8_t (&wh)[4], h8_t (&wl)[4], h8_t (&nwh)[4], h8_t (&nwl)[4]) {
-    const bool more = g + 1 < G;
-    if (more) {
-      loadw(g + 1, nwh, nwl);
-      load(g + 1);
-    }
+    const int gn = min(g + 1, G - 1);
+    loadw(gn, nwh, nwl);
+    load(gn);
     mma(cur, wh, wl);
-    if (more) store(cur ^ 1);
+    store(cur ^ 1);
     __syncthreads();
   };
   for (int g = 0; g < G; g += 2) {
     body(g, 0, wh0, wl0, wh1, wl1);
     if (g + 1 < G) body(g + 1, 1, wh1, wl1, wh0, wl0);
+  }
+#elif PPO_XW_V == 2
+  // weight tile through LDS: each thread stages 4 x 16 bytes of the next group's 16 KiB image with the A tile
+  __shared__ h8_t sW[2][2][4][TB];  // [buffer][plane][q][n]
+  const h8_t* wsrc = P.w + nt * TB + (tid & 31) + (size_t)(tid >> 5) * npad;  // chunk (plane, q) = tid >> 5
+  h8_t wst[4];
+  auto loadw2 = [&](int g) {
+    const h8_t* p = wsrc + (size_t)g * 8 * npad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wst[i] = p[32 * i];
+  };
+  auto storew2 = [&](int buf) {
+    h8_t* d = &sW[buf][0][0][0] + (size_t)(tid >> 5) * TB + (tid & 31);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[32 * i] = wst[i];
+  };
+  loadw2(0);
+  storew2(0);
+  __syncthreads();
+  for (int g = 0; g < G; ++g) {
+    const int cur = g & 1;
+    const bool more = g + 1 < G;
+    if (more) {
+      loadw2(g + 1);
+      load(g + 1);
+    }
+    h8_t wh[4], wl[4];
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      wh[tn] = sW[cur][0][q][wn * 64 + tn * 16 + c];
+      wl[tn] = sW[cur][1][q][wn * 64 + tn * 16 + c];
+    }
+    mma(cur, wh, wl);
+    if (more) {
+      store(cur ^ 1);
+      storew2(cur ^ 1);
+    }
+    __syncthreads();
   }
 #else
   __syncthreads();
@@ -382,36 +428,39 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgLaunch L) {
   const int nkt = max(0, min(4, (P.k0 - kw0 + 15) >> 4));
   // staging: instruction j covers rows 2 j, 2 j + 1 of the wave's 8; lane -> row + (lane >> 5), float4 lane & 31
   const int col4 = lane & 31;
-  const int kx = tk * TB + 4 * col4;
+  const int kx = tk * TB + 4 * col4, kxc = min(kx, (int)P.ldx - 4);
   const int rsub = w * 8 + (lane >> 5);  // + 2 j
-  const float* xb = P.x + (size_t)rsub * P.ldx + kx;
-  const float* db = P.d + (size_t)rsub * P.ldd + tn * TB + 4 * col4;
+  const float* xb = P.x + kxc;
+  const float* db = P.d + tn * TB + 4 * col4;
   f4_t sxv[4], sdv[4];
+  int sm0 = 0;
+  // unconditional loads (rows clamped); out-of-range values are zeroed in store(), after the MFMAs (xw_kernel)
   auto load = [&](int m0) {
+    sm0 = m0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int m = m0 + rsub + 2 * j;
-      f4_t vx = {0.0f, 0.0f, 0.0f, 0.0f}, vd = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (m < m_hi) {
-        if (kx < P.k0) vx = *reinterpret_cast<const f4_t*>(xb + (size_t)(m0 + 2 * j) * P.ldx);
-        vd = *reinterpret_cast<const f4_t*>(db + (size_t)(m0 + 2 * j) * P.ldd);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) vx[i] = kx + i < P.k0 ? vx[i] : 0.0f;
-      sxv[j] = vx;
-      sdv[j] = vd;
+      const int mc = min(m0 + rsub + 2 * j, L.M - 1);
+      sxv[j] = *reinterpret_cast<const f4_t*>(xb + (size_t)mc * P.ldx);
+      sdv[j] = *reinterpret_cast<const f4_t*>(db + (size_t)mc * P.ldd);
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = rsub + 2 * j;
+      const float rm = sm0 + r < m_hi ? 1.0f : 0.0f;
+      f4_t vx = sxv[j], vd = sdv[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        vx[i] = kx + i < P.k0 ? vx[i] * rm : 0.0f;
+        vd[i] = vd[i] * rm;
+      }
       const int off = img_off(r, col4);
       h4_t hi, lo;
-      split4(sxv[j], sx, hi, lo);
+      split4(vx, sx, hi, lo);
       *reinterpret_cast<h4_t*>(&sX[buf][0][off]) = hi;
       *reinterpret_cast<h4_t*>(&sX[buf][1][off]) = lo;
-      split4(sdv[j], sd, hi, lo);
+      split4(vd, sd, hi, lo);
       *reinterpret_cast<h4_t*>(&sD[buf][0][off]) = hi;
       *reinterpret_cast<h4_t*>(&sD[buf][1][off]) = lo;
     }
@@ -1209,7 +1258,8 @@ enum MaxSlot {
 enum WSlot { W_A0 = 0, W_A2, W_P0, W_P2, W_P4, W_C0, W_C2, W_C4, W_N };
 
 struct Lay {
-  int H, P, A, M, MP, MT, HB, S, chunk, ldg, bw;
+  int H, P, A, M, MP, MT, HB, ldg, bw;
+  int S[2], chunk[2];  // weight-gradient row split per phase (about two workgroups per CU in one round)
   int64_t np_total, np_adapt;
   // parameter offsets (floats) in state_dict order
   int64_t pw[11], pb[11], pstd;
@@ -1237,10 +1287,6 @@ bool make_layout(const go1_ppo_dims* d, Lay& L, std::string& err) {
   L.HB = std::min(HEAD_BLOCKS, cdiv(L.M, 4));
   L.ldg = cdiv(L.H + 2 * L.P, 4) * 4;  // [hist, latent, priv]
   L.bw = cdiv(3 * L.A + 4, 4) * 4;     // [actions, mu, sigma, logp, adv, ret, values]
-  int S = L.MP / 256;
-  S = S >= 16 ? 16 : (S >= 8 ? 8 : (S < 1 ? 1 : S));
-  L.chunk = cdiv(cdiv(L.M, S), 32) * 32;
-  L.S = cdiv(L.M, L.chunk);
   // parameters
   const int64_t H = L.H, P = L.P, A = L.A;
   const int64_t wsz[11] = {HA1 * H, HA2 * HA1, P * HA2, H1 * (H + P), H2 * H1, H3 * H2, A * H3,
@@ -1297,6 +1343,22 @@ bool make_layout(const go1_ppo_dims* d, Lay& L, std::string& err) {
   L.apart = take((size_t)ADAPT_BLOCKS * adapt_stride(L.P) * F);
   // weight-gradient partials [S][n][kpad] and weight images (4 bytes per element: hi + lo halves)
   const int wn[W_N] = {HA1, HA2, H1, H2, H3, H1, H2, H3};
+  // the row split of each phase's grouped weight-gradient launch: ~512 workgroups, chunks of >= 64 rows
+  {
+    const int wk0[W_N] = {L.H, HA1, L.H + L.P, H1, H2, L.H + 2 * L.P, H1, H2};
+    int tiles[2] = {0, 0};
+    for (int i = 0; i < W_N; ++i) {
+      const int t = cdiv(wk0[i], TB) * (wn[i] / TB);
+      tiles[0] += t;
+      if (i == W_A0 || i == W_A2) tiles[1] += t;
+    }
+    for (int ph = 0; ph < 2; ++ph) {
+      int S = (512 + tiles[ph] / 2) / tiles[ph];
+      S = std::max(1, std::min(std::min(S, 64), L.M / 64));
+      L.chunk[ph] = cdiv(cdiv(L.M, S), 32) * 32;
+      L.S[ph] = cdiv(L.M, L.chunk[ph]);
+    }
+  }
   // GEMM columns: the actor's first layer reads [hist, latent], the critic's [hist, latent, priv] (zero weights on
   // the latent columns), the adaptation module's [hist]
   const int wk[W_N] = {L.H, HA1, L.H + L.P, H1, H2, L.H + 2 * L.P, H1, H2};
@@ -1305,7 +1367,8 @@ bool make_layout(const go1_ppo_dims* d, Lay& L, std::string& err) {
     L.wk[i] = wk[i];
     const int kpad = cdiv(wk[i], TB) * TB;
     L.wpart_stride[i] = (int64_t)wn[i] * kpad;
-    L.wpart[i] = take((size_t)L.S * wn[i] * kpad * F);
+    const int S = (i == W_A0 || i == W_A2) ? std::max(L.S[0], L.S[1]) : L.S[0];
+    L.wpart[i] = take((size_t)S * wn[i] * kpad * F);
     L.img[i] = take((size_t)cdiv(wk[i], 32) * 32 * wn[i] * 4);
     // transposed images for the layers the backward crosses: a2 (adaptation L2), p2, p4, c2, c4
     const bool tr = i == W_A2 || i == W_P2 || i == W_P4 || i == W_C2 || i == W_C4;
@@ -1404,7 +1467,7 @@ WgProb wg_prob(const Ctx& C, int wslot, const float* x, int64_t ldx, int k0, con
   return p;
 }
 
-int launch_wg(const Ctx& C, WgProb* ps, int np) {
+int launch_wg(const Ctx& C, WgProb* ps, int np, int phase) {
   WgLaunch L{};
   int total = 0;
   for (int i = 0; i < np; ++i) {
@@ -1414,8 +1477,8 @@ int launch_wg(const Ctx& C, WgProb* ps, int np) {
   }
   L.nprob = np;
   L.M = C.L.M;
-  L.S = C.L.S;
-  L.chunk = C.L.chunk;
+  L.S = C.L.S[phase];
+  L.chunk = C.L.chunk[phase];
   L.total = total;
   hipLaunchKernelGGL(wgrad_kernel, dim3(total * L.S), dim3(256), 0, C.s, L);
   PPO_TRY(hipGetLastError());
@@ -1448,10 +1511,10 @@ int launch_reduce(const Ctx& C, SegBuilder& B) {
 }
 
 // weight-gradient segment of W slot i (partials [S][n][kpad]) into the flat gradient of parameter pi (row stride ldd)
-void seg_w(const Ctx& C, SegBuilder& B, int wslot, int pi, int ldd) {
+void seg_w(const Ctx& C, SegBuilder& B, int wslot, int pi, int ldd, int phase) {
   const int n = C.L.wn[wslot], k = C.L.wk[wslot];
   const int kpad = cdiv(k, TB) * TB;
-  B.add(C.gW(pi), C.at<float>(C.L.wpart[wslot]), n, k, kpad, C.L.S, C.L.wpart_stride[wslot], ldd);
+  B.add(C.gW(pi), C.at<float>(C.L.wpart[wslot]), n, k, kpad, C.L.S[phase], C.L.wpart_stride[wslot], ldd);
 }
 
 int pack_weights(const Ctx& C, bool adaptation_only, bool zero_max) {
@@ -1551,13 +1614,13 @@ int adapt_backward_l2(const Ctx& C) {
                    nullptr);
 }
 
-void adapt_segments(const Ctx& C, SegBuilder& SB) {
+void adapt_segments(const Ctx& C, SegBuilder& SB, int phase) {
   const Lay& L = C.L;
   const int P = L.P, as = adapt_stride(P);
   const float* ap = C.at<float>(L.apart);
-  seg_w(C, SB, W_A0, IA0, L.H);
+  seg_w(C, SB, W_A0, IA0, L.H, phase);
   SB.add(C.gB(IA0), C.at<float>(L.cs1a), 1, HA1, 0, L.MT, HA1);
-  seg_w(C, SB, W_A2, IA2, HA1);
+  seg_w(C, SB, W_A2, IA2, HA1, phase);
   SB.add(C.gB(IA2), ap + P * 128 + P, 1, HA2, 0, L.HB, as);
   SB.add(C.gW(IA4), ap, 1, P * 128, 0, L.HB, as);
   SB.add(C.gB(IA4), ap + P * 128, 1, P, 0, L.HB, as);
@@ -1675,7 +1738,7 @@ int grad_phase0(const Ctx& C) {
     ps[5] = wg_prob(C, W_C4, c2, H2, H2, C.mx(MX_C2), d3c, H3, H3, C.mx(MX_D3C));
     ps[6] = wg_prob(C, W_A0, G, L.ldg, H, C.mx(MX_G), d1a, HA1, HA1, C.mx(MX_D1A));
     ps[7] = wg_prob(C, W_A2, a1a, HA1, HA1, C.mx(MX_A1A), d2a, HA2, HA2, C.mx(MX_D2A));
-    if ((rc = launch_wg(C, ps, 8))) return rc;
+    if ((rc = launch_wg(C, ps, 8, 0))) return rc;
   }
   // ---- partials -> flat gradient (+ aux: surrogate, value, KL sums)
   SegBuilder SB;
@@ -1684,25 +1747,25 @@ int grad_phase0(const Ctx& C) {
   const int o_db4p = A * 128, o_db3p = o_db4p + A, o_dW4c = o_db3p + 128, o_db4c = o_dW4c + 128, o_db3c = o_db4c + 1,
             o_dstd = o_db3c + 128, o_loss = o_dstd + A;
   SB.add(b->grads, hp + o_loss, 1, 3, 0, L.HB, hs);
-  adapt_segments(C, SB);
-  seg_w(C, SB, W_P0, IP0, H + P);
+  adapt_segments(C, SB, 0);
+  seg_w(C, SB, W_P0, IP0, H + P, 0);
   SB.add(C.gB(IP0), C.at<float>(L.cs1p), 1, H1, 0, L.MT, H1);
-  seg_w(C, SB, W_P2, IP2, H1);
+  seg_w(C, SB, W_P2, IP2, H1, 0);
   SB.add(C.gB(IP2), C.at<float>(L.cs2p), 1, H2, 0, L.MT, H2);
-  seg_w(C, SB, W_P4, IP4, H2);
+  seg_w(C, SB, W_P4, IP4, H2, 0);
   SB.add(C.gB(IP4), hp + o_db3p, 1, H3, 0, L.HB, hs);
   SB.add(C.gW(IP6), hp, 1, A * 128, 0, L.HB, hs);
   SB.add(C.gB(IP6), hp + o_db4p, 1, A, 0, L.HB, hs);
   {  // the critic's first layer: G's hist columns, then its priv columns (the latent columns' gradient is dropped)
     const int kpad = cdiv(H + 2 * P, TB) * TB;
     const float* wp = C.at<float>(L.wpart[W_C0]);
-    SB.add(C.gW(IC0), wp, H1, H, kpad, L.S, L.wpart_stride[W_C0], H + P);
-    SB.add(C.gW(IC0) + H, wp + H + P, H1, P, kpad, L.S, L.wpart_stride[W_C0], H + P);
+    SB.add(C.gW(IC0), wp, H1, H, kpad, L.S[0], L.wpart_stride[W_C0], H + P);
+    SB.add(C.gW(IC0) + H, wp + H + P, H1, P, kpad, L.S[0], L.wpart_stride[W_C0], H + P);
   }
   SB.add(C.gB(IC0), C.at<float>(L.cs1c), 1, H1, 0, L.MT, H1);
-  seg_w(C, SB, W_C2, IC2, H1);
+  seg_w(C, SB, W_C2, IC2, H1, 0);
   SB.add(C.gB(IC2), C.at<float>(L.cs2c), 1, H2, 0, L.MT, H2);
-  seg_w(C, SB, W_C4, IC4, H2);
+  seg_w(C, SB, W_C4, IC4, H2, 0);
   SB.add(C.gB(IC4), hp + o_db3c, 1, H3, 0, L.HB, hs);
   SB.add(C.gW(IC6), hp + o_dW4c, 1, 128, 0, L.HB, hs);
   SB.add(C.gB(IC6), hp + o_db4c, 1, 1, 0, L.HB, hs);
@@ -1726,13 +1789,13 @@ int grad_phase1(const Ctx& C) {
     ps[0] = wg_prob(C, W_A0, C.at<float>(L.G), L.ldg, L.H, C.mx(MX_G), C.at<float>(L.d1a), HA1, HA1, C.mx(MX_D1A));
     ps[1] = wg_prob(C, W_A2, C.at<float>(L.a1a), HA1, HA1, C.mx(MX_A1A), C.at<float>(L.d2a), HA2, HA2,
                     C.mx(MX_D2A));
-    if ((rc = launch_wg(C, ps, 2))) return rc;
+    if ((rc = launch_wg(C, ps, 2, 1))) return rc;
   }
   SegBuilder SB;
   const int as = adapt_stride(P);
   const float* ap = C.at<float>(L.apart);
   SB.add(b->grads + 3, ap + P * 128 + P + 128, 1, 2, 0, L.HB, as);  // aux[3], aux[4]: adaptation loss sums
-  adapt_segments(C, SB);
+  adapt_segments(C, SB, 1);
   return launch_reduce(C, SB);
 }
 
