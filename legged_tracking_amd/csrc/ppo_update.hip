@@ -104,7 +104,23 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // ELU (alpha = 1) as torch's kernel: x > 0 ? x : expm1(x); its derivative from the output a: 1 or a + 1 = exp(x)
-__device__ __forceinline__ float elu(float z) { return z > 0.0f ? z : expm1f(z); }
+// expm1 for z <= 0 in ~14 instructions (ocml's expm1f is ~40, which made the ELU epilogue VALU-bound):
+// z in [-0.5, 0]: degree-9 Taylor polynomial (truncation < 2^-27 relative); z < -0.5: exp(z) - 1 on v_exp_f32
+// (|result| > 0.39, so the exp's ~1 ulp error stays ~2^-23 relative).  Within 2 ulp of expm1f on z <= 0.
+__device__ __forceinline__ float expm1_neg(float z) {
+  float p = 1.0f / 362880.0f;
+  p = fmaf(p, z, 1.0f / 40320.0f);
+  p = fmaf(p, z, 1.0f / 5040.0f);
+  p = fmaf(p, z, 1.0f / 720.0f);
+  p = fmaf(p, z, 1.0f / 120.0f);
+  p = fmaf(p, z, 1.0f / 24.0f);
+  p = fmaf(p, z, 1.0f / 6.0f);
+  p = fmaf(p, z, 0.5f);
+  const float small = fmaf(p * z, z, z);
+  const float big = __builtin_amdgcn_exp2f(z * 1.44269504f) - 1.0f;
+  return z >= -0.5f ? small : big;
+}
+__device__ __forceinline__ float elu(float z) { return z > 0.0f ? z : expm1_neg(z); }
 __device__ __forceinline__ float delu_from_out(float a) { return a > 0.0f ? 1.0f : a + 1.0f; }
 
 // ------------------------------------------------------------------ xw: C = act(A W^T + b) / (A W^T) * ELU'
@@ -142,14 +158,30 @@ struct XwLaunch {
 
 enum { EPI_LIN = 0, EPI_ELU = 1, EPI_DELU = 2 };
 
+#ifndef PPO_XW_LB
+#define PPO_XW_LB 2
+#endif
 #ifndef PPO_XW_V
-#define PPO_XW_V 0  // 0: weight fragments loaded at the start of their K group; 1: one group ahead
+#define PPO_XW_V 1  // 0: weight fragments loaded at the start of their K group; 1: one group ahead; 2: through LDS
+#endif
+
+#ifdef PPO_STAMPS  // diagnostic build only (tools/xw_stamps.py): s_memrealtime per workgroup at kernel start,
+                   // after the first staged group, after the K loop and after the epilogue
+__device__ unsigned long long g_xw_stamps[8192][4];
+#define XW_STAMP(i)                                                                                   \
+  do {                                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_xw_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define XW_STAMP(i)
 #endif
 
 template <int EPI>
-__global__ __launch_bounds__(256, 2) void xw_kernel(XwLaunch L) {
+__global__ __launch_bounds__(256, PPO_XW_LB) void xw_kernel(XwLaunch L) {
+  XW_STAMP(0);
   __shared__ h8_t sA[2][2][4][TB];  // [buffer][plane][q][row]: 32 KiB
   __shared__ float sRed[2][64];
+  __shared__ uint32_t sMax[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = lane >> 4, c = lane & 15;
   int t = blockIdx.x;
   if ((L.total & 7) == 0) t = (t & 7) * (L.total >> 3) + (t >> 3);  // one XCD walks consecutive row tiles
@@ -229,16 +261,28 @@ __global__ __launch_bounds__(256, 2) void xw_kernel(XwLaunch L) {
   __syncthreads();
   auto body = [&](int g, int cur, h8_t (&wh)[4], h8_t (&wl)[4], h8_t (&nwh)[4], h8_t (&nwl)[4]) {
     const int gn = min(g + 1, G - 1);
+#ifndef PPO_XW_NOW  // timing experiments only: PPO_XW_NOW / NOA / NOMMA drop the weight loads / A loads / MFMAs
     loadw(gn, nwh, nwl);
+#else
+    (void)nwh; (void)nwl;
+#endif
+#ifndef PPO_XW_NOA
     load(gn);
+#endif
+#ifndef PPO_XW_NOMMA
     mma(cur, wh, wl);
+#else
+    if (g < 0) mma(cur, wh, wl);
+#endif
     store(cur ^ 1);
     __syncthreads();
   };
+  XW_STAMP(1);
   for (int g = 0; g < G; g += 2) {
     body(g, 0, wh0, wl0, wh1, wl1);
     if (g + 1 < G) body(g + 1, 1, wh1, wl1, wh0, wl0);
   }
+  XW_STAMP(2);
 #elif PPO_XW_V == 2
   // weight tile through LDS: each thread stages 4 x 16 bytes of the next group's 16 KiB image with the A tile
   __shared__ h8_t sW[2][2][4][TB];  // [buffer][plane][q][n]
@@ -321,11 +365,17 @@ __global__ __launch_bounds__(256, 2) void xw_kernel(XwLaunch L) {
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) amax = max(amax, absbits(v[i]));
+#ifdef PPO_XW_NOSTORE  // timing experiment: no C stores
+      if (v[0] != v[0] && v[1] == 12345.0f)
+#endif
       *reinterpret_cast<f4_t*>(P.c + (size_t)m * P.ldc + n) = v;
     }
   }
   amax = wave_max_u32(amax);
-  if (lane == 0 && P.cmax) atomicMax(P.cmax, amax);
+  if (lane == 0) sMax[w] = amax;  // one atomic per workgroup (a single address takes them one at a time)
+  __syncthreads();
+  if (tid == 0 && P.cmax) atomicMax(P.cmax, max(max(sMax[0], sMax[1]), max(sMax[2], sMax[3])));
+  XW_STAMP(3);
   if (EPI == EPI_DELU && P.colsum) {
     // column sums of this tile in a fixed order: the 16 rows of a lane group (xor tree), then wm = 0 + wm = 1
 #pragma unroll
@@ -534,49 +584,63 @@ struct GatherArgs {
   uint32_t* mx;
 };
 
-// grid (M rows, 2): y = 0 writes the row of G, y = 1 the row of B
+// A wave gathers four rows at a time (rows strided over the grid): the four storage indices come in one load,
+// then every element load of the four rows is issued (clamped addresses, selects afterwards) before any store.
+// One atomicMax per workgroup: a max per row-block would serialise ~M atomics on one address.
+constexpr int GATHER_BLOCKS_MAX = 1024;
 __global__ __launch_bounds__(256) void gather_kernel(GatherArgs g) {
   __shared__ uint32_t red[4];
-  const int m = blockIdx.x;
-  const int64_t r = g.idx[m];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int M = g.M, H = g.H, P = g.P, A = g.A, ldg = g.ldg, bw = g.bw;
+  const int nwaves = gridDim.x * 4;
   uint32_t mb = 0u;
-  if (blockIdx.y == 0) {
-    const float* __restrict__ src = g.hist + r * g.hld;
-    const float* __restrict__ pr = g.priv + r * g.P;
-    float* __restrict__ dst = g.G + (size_t)m * g.ldg;
-    for (int k = threadIdx.x; k < g.ldg; k += 256) {
-      float v = 0.0f;
-      if (k < g.H)
-        v = src[k];
-      else if (k >= g.H + g.P && k < g.H + 2 * g.P)
-        v = pr[k - g.H - g.P];
-      dst[k] = v;
-      mb = max(mb, absbits(v));
+  for (int m0 = (blockIdx.x * 4 + w) * 4; m0 < M; m0 += nwaves * 4) {
+    const int64_t ri = g.idx[min(m0 + (lane & 3), M - 1)];
+    int64_t r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = __shfl(ri, j);
+    for (int k0 = 0; k0 < ldg; k0 += 64) {
+      const int k = k0 + lane;
+      const int kh = min(k, H - 1), kp = min(max(k - H - P, 0), P - 1);
+      const bool in_h = k < H, in_p = k >= H + P && k < H + 2 * P;
+      float vh[4], vp[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vh[j] = g.hist[r[j] * g.hld + kh];
+        vp[j] = g.priv[r[j] * P + kp];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = in_h ? vh[j] : (in_p ? vp[j] : 0.0f);
+        if (m0 + j < M && k < ldg) {
+          g.G[(size_t)(m0 + j) * ldg + k] = v;
+          mb = max(mb, absbits(v));
+        }
+      }
     }
-  } else {
-    const int k = threadIdx.x, A = g.A;
-    if (k < g.bw) {
-      float v = 0.0f;
-      if (k < A)
-        v = g.act[r * A + k];
-      else if (k < 2 * A)
-        v = g.mu[r * A + k - A];
-      else if (k < 3 * A)
-        v = g.sigma[r * A + k - 2 * A];
-      else if (k == 3 * A)
-        v = g.logp[r];
-      else if (k == 3 * A + 1)
-        v = g.adv[r];
-      else if (k == 3 * A + 2)
-        v = g.ret[r];
-      else if (k == 3 * A + 3)
-        v = g.val[r];
-      g.B[(size_t)m * g.bw + k] = v;
+    // B rows: [actions A, mu A, sigma A, logp, adv, ret, values, 0 ...] (bw <= 64 columns)
+    {
+      const int k = lane;
+      const int seg = k < A ? 0 : (k < 2 * A ? 1 : (k < 3 * A ? 2 : 3));
+      const int ka = min(k - seg * A, A - 1);
+      const float* srcA = seg == 0 ? g.act : (seg == 1 ? g.mu : g.sigma);
+      const int t = k - 3 * A;  // 0: logp, 1: adv, 2: ret, 3: values
+      const float* srcS = t == 0 ? g.logp : (t == 1 ? g.adv : (t == 2 ? g.ret : g.val));
+      float va[4], vs[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        va[j] = srcA[r[j] * A + max(ka, 0)];
+        vs[j] = srcS[r[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = seg < 3 ? va[j] : (t < 4 ? vs[j] : 0.0f);
+        if (m0 + j < M && k < bw) g.B[(size_t)(m0 + j) * bw + k] = v;
+      }
     }
-    return;
   }
   mb = wave_max_u32(mb);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mb;
+  if (lane == 0) red[w] = mb;
   __syncthreads();
   if (threadIdx.x == 0) {
     mb = max(max(red[0], red[1]), max(red[2], red[3]));
@@ -1343,7 +1407,8 @@ bool make_layout(const go1_ppo_dims* d, Lay& L, std::string& err) {
   L.apart = take((size_t)ADAPT_BLOCKS * adapt_stride(L.P) * F);
   // weight-gradient partials [S][n][kpad] and weight images (4 bytes per element: hi + lo halves)
   const int wn[W_N] = {HA1, HA2, H1, H2, H3, H1, H2, H3};
-  // the row split of each phase's grouped weight-gradient launch: ~512 workgroups, chunks of >= 64 rows
+  // the row split of each phase's grouped weight-gradient launch: at most 512 workgroups (two per CU with the
+  // launch's 64 KiB of LDS: one more would start a second round), chunks of >= 64 rows
   {
     const int wk0[W_N] = {L.H, HA1, L.H + L.P, H1, H2, L.H + 2 * L.P, H1, H2};
     int tiles[2] = {0, 0};
@@ -1353,7 +1418,7 @@ bool make_layout(const go1_ppo_dims* d, Lay& L, std::string& err) {
       if (i == W_A0 || i == W_A2) tiles[1] += t;
     }
     for (int ph = 0; ph < 2; ++ph) {
-      int S = (512 + tiles[ph] / 2) / tiles[ph];
+      int S = 512 / tiles[ph];
       S = std::max(1, std::min(std::min(S, 64), L.M / 64));
       L.chunk[ph] = cdiv(cdiv(L.M, S), 32) * 32;
       L.S[ph] = cdiv(L.M, L.chunk[ph]);
@@ -1658,7 +1723,7 @@ int grad_phase0(const Ctx& C) {
     ga.G = G;
     ga.B = Bb;
     ga.mx = C.mx(MX_G);
-    hipLaunchKernelGGL(gather_kernel, dim3(L.M, 2), dim3(256), 0, C.s, ga);
+    hipLaunchKernelGGL(gather_kernel, dim3(std::min(cdiv(L.M, 16), GATHER_BLOCKS_MAX)), dim3(256), 0, C.s, ga);
     PPO_TRY(hipGetLastError());
   }
   float *a1a = C.at<float>(L.a1a);
@@ -1891,6 +1956,11 @@ int go1_ppo_step(const go1_ppo_dims* d, const go1_ppo_bufs* b, int32_t phase, vo
   return step_phase(C, phase);
 }
 
+#ifdef PPO_STAMPS
+extern "C" int go1_ppo_xw_stamps(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xw_stamps), sizeof(g_xw_stamps), 0, hipMemcpyDeviceToHost) != hipSuccess;
+}
+#endif
 // ---- test entry points: one GEMM of each kind on caller tensors (x rows 16-byte aligned: k % 4 == 0 or padded)
 int go1_ppo_test_linear(const float* x, int64_t rows, int32_t k, const float* w, const float* bias, int32_t n,
                         int32_t elu, float* y, void* work, int64_t work_bytes, int32_t reps, void* stream) {

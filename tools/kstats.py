@@ -9,7 +9,7 @@ div = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 d = collections.defaultdict(list)
 for r in rows:
     nm = r["Kernel_Name"]
-    short = nm.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")[-40:]
+    short = nm.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[-40:]
     key = (short, r["Grid_Size_X"], r["Workgroup_Size_X"], r["LDS_Block_Size"], r["VGPR_Count"])
     d[key].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 tot = sum(sum(v) for v in d.values())

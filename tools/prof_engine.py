@@ -1,5 +1,6 @@
 import sys, time, torch
-sys.path.insert(0, '.')
+import os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from legged_tracking_amd import rollout as R
 torch.manual_seed(0)
 n, T = 4096, 24
