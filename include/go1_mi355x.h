@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GO1_ABI_VERSION 5
+#define GO1_ABI_VERSION 6
 
 #define GO1_NUM_DOF 12
 #define GO1_NUM_BODIES 17
@@ -185,6 +185,15 @@ typedef struct go1_config {
   float height_grid_x[GO1_GRID_X], height_grid_y[GO1_GRID_Y];
   /* native contact / joint-limit model (no reference equivalent: PhysX is closed) */
   float contact_stiffness, contact_damping, friction_damping, limit_stiffness, limit_damping;
+  /* restitution (PhysX's restitution with the default average combine and bounce threshold): a point
+   * approaching a surface faster than bounce_threshold gets a separating velocity target
+   * e * |vn|, e = (state.restitution + terrain_restitution) / 2
+   * (legged_robot_trajectory_tracking.py:676 / :1421-1428, config bounce_threshold_velocity :369) */
+  float terrain_restitution, bounce_threshold;
+  /* self-collision (asset.self_collisions == 0, go1_crawling.py:44): the calf and foot spheres against the
+   * other legs' thigh / calf / foot spheres and the trunk box, explicit penalty springs; stiffness 0
+   * disables them (self_collisions == 1) */
+  float self_stiffness, self_damping;
   float model[GO1_MODEL_FLOATS];
   float actuator[GO1_ACTUATOR_FLOATS];
 } go1_config;

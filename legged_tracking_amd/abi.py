@@ -5,7 +5,7 @@ checks sizes and offsets against the compiled library's expectations.
 """
 import ctypes as C
 
-GO1_ABI_VERSION = 5
+GO1_ABI_VERSION = 6
 GO1_NUM_DOF = 12
 GO1_NUM_BODIES = 17
 GO1_MAX_TERMS = 16
@@ -77,7 +77,8 @@ class Go1Config(C.Structure):
         ("default_dof_pos", F * 12), ("dof_pos_limits", F * 24), ("torque_limits", F * 12),
         ("hard_limits", F * 24), ("height_grid_x", F * GO1_GRID_X), ("height_grid_y", F * GO1_GRID_Y),
         ("contact_stiffness", F), ("contact_damping", F), ("friction_damping", F), ("limit_stiffness", F),
-        ("limit_damping", F),
+        ("limit_damping", F), ("terrain_restitution", F), ("bounce_threshold", F), ("self_stiffness", F),
+        ("self_damping", F),
         ("model", F * GO1_MODEL_FLOATS), ("actuator", F * GO1_ACTUATOR_FLOATS),
     ]
 

@@ -682,8 +682,23 @@ def f32(x):
 # integrator step per sim step (as PhysX's substeps = 1, legged_robot_trajectory_tracking_config.py:
 # 355-356): the contacts are linearly implicit (added masses in the articulated inertias), which keeps
 # the penalty contact stable at that step (tools/implicit_contact_study.py)
+# Self-collision springs are explicit (the two bodies sit in different legs' ABA chains, so no added mass
+# couples them): 2000 N/m and 10 N.s/m keep h w = 0.7 and h d / m = 0.5 on a 0.1 kg link at 5 ms.
 PHYSICS = dict(contact_stiffness=2.0e4, contact_damping=80.0, friction_damping=60.0,
-               limit_stiffness=2000.0, limit_damping=20.0, n_internal=1)
+               limit_stiffness=2000.0, limit_damping=20.0, n_internal=1, self_stiffness=2000.0, self_damping=10.0)
+
+
+def set_contact_fields(c, cfg, physics):
+    """The native contact model's go1_config fields: penalty constants, restitution (the terrain's
+    cfg.terrain.restitution, PhysX's bounce threshold cfg.sim.physx.bounce_threshold_velocity) and the
+    self-collision springs (asset.self_collisions == 0 enables them, Isaac Gym's bitwise filter convention)."""
+    for k in ("contact_stiffness", "contact_damping", "friction_damping", "limit_stiffness", "limit_damping"):
+        setattr(c, k, float(physics[k]))
+    c.terrain_restitution = f32(_get(cfg, "terrain.restitution", 0.0))
+    c.bounce_threshold = f32(_get(cfg, "sim.physx.bounce_threshold_velocity", 0.5))
+    on = int(_get(cfg, "asset.self_collisions", 0)) == 0
+    c.self_stiffness = float(physics["self_stiffness"]) if on else 0.0
+    c.self_damping = float(physics["self_damping"]) if on else 0.0
 
 
 def _get(cfg, path, default=None):
@@ -977,8 +992,7 @@ def build_abi_config(cfg, n_envs=None, physics=None, actuator=None, hf_shape=(80
         c.height_grid_x[i] = f32(v)
     for i, v in enumerate(np.asarray(t.measured_points_y, np.float64)):
         c.height_grid_y[i] = f32(v)
-    for k in ("contact_stiffness", "contact_damping", "friction_damping", "limit_stiffness", "limit_damping"):
-        setattr(c, k, float(physics[k]))
+    set_contact_fields(c, cfg, physics)
     for i, v in enumerate(M.model_block()):
         c.model[i] = float(v)
     w = actuator if actuator is not None else load_actuator()

@@ -14,6 +14,7 @@
 
 #include "../../include/go1_mi355x.h"
 #include "go1_model_consts.h"
+#include "go1_selfpairs.h"
 #include "go1_spec.h"
 static_assert(GO1_MODEL_CONST_FLOATS == GO1_MODEL_FLOATS, "regenerate go1_model_consts.h");
 #include "pmath.h"
@@ -1007,6 +1008,7 @@ __device__ __forceinline__ void height_query2(const Terr& T, float x, float y, f
 
 struct CP {
   float k, d, kf, mu;
+  float e, vb;  // restitution (the env's and the terrain's, averaged) and the bounce threshold
 };
 
 // ---- packed (v_pk_*_f32) contact: one wave issues a v_pk_fma_f32 (two FMAs) as fast as a
@@ -1094,6 +1096,19 @@ __device__ __forceinline__ void sphere_contact_pk(const Terr& T, const HQ& q, co
   F[2] = Fz.x + Fz.y;
 }
 
+// Restitution.  PhysX bounces a contact whose relative velocity exceeds the bounce threshold with the
+// coefficient e (the average of the two shapes').  A penalty contact has no impact event to attach a velocity
+// target to (no per-contact state), so e acts on the dissipation of the rebound: while a point separates
+// faster than the threshold, the explicit part of the normal force gets + e (h k + d) vn, i.e. the fraction e
+// of the linearly implicit contact's damping (the physical d and the h k of the implicit spring) is handed
+// back; the added mass h (h k + d) n n^T stays, so the velocity update keeps a contraction factor
+// (m + e c) / (m + c) <= 1 (c = h (h k + d)): no e in [0, 1] adds energy (tests/test_self_collision.py).
+// e = 0 leaves the force bit for bit as before.
+__device__ __forceinline__ f2 restitute(const CP& C, float h, f2 vn, f2 fn) {
+  const float cr = (h * C.k + C.d) * C.e;
+  return f2{(C.e > 0.0f && vn.x > C.vb) ? fn.x + cr * vn.x : fn.x, (C.e > 0.0f && vn.y > C.vb) ? fn.y + cr * vn.y : fn.y};
+}
+
 // The same contact, linearly implicit in the point velocity (the integrator's scheme: one 5 ms step
 // per sim step, like PhysX's substeps = 1).  For an active layer the force at the end of the step,
 // k (depth - h vn') - d vn' (normal) and -c_t vt' (regularised friction, c_t = min(kf, mu fn / |vt|)
@@ -1117,7 +1132,7 @@ __device__ __forceinline__ void sphere_contact_im(const Terr& T, const HQ& q, co
   const f2 depth = dv * inv;
   const f2 vn = pv[0] * nx + pv[1] * ny + pv[2] * nz;
   const f2 fn0 = C.k * depth - C.d * vn;          // activation: compressive at the current state
-  const f2 fn = fn0 - (h * C.k) * vn;              // k depth - (h k + d) vn
+  const f2 fn = restitute(C, h, vn, fn0 - (h * C.k) * vn);  // k depth - (h k + d) vn [+ e (h k + d) vn]
   const f2 vtx = pv[0] - vn * nx, vty = pv[1] - vn * ny, vtz = pv[2] - vn * nz;
   const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
   const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
@@ -1250,7 +1265,6 @@ __device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const fl
   f2 Fh[3] = {f2s(0.0f), f2s(0.0f), f2s(0.0f)}, M[6] = {f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f)};
   f2 cds = f2s(0.0f);
   f2 Fwx = f2s(0.0f), Fwy = f2s(0.0f), Fwz = f2s(0.0f);
-  const float cn = h * (h * C.k + C.d);
 #pragma unroll
   for (int L = 0; L < 2; ++L) {
     const float sg = L == 0 ? 1.0f : -1.0f;
@@ -1263,7 +1277,8 @@ __device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const fl
     const f2 depth = dvl[L] * inv;
     const f2 vn = vw[0] * nx + vw[1] * ny + vw[2] * nz;
     const f2 fn0 = C.k * depth - C.d * vn;
-    const f2 fn = fn0 - (h * C.k) * vn;
+    const f2 fn = restitute(C, h, vn, fn0 - (h * C.k) * vn);
+    const float cn = h * (h * C.k + C.d);
     const f2 vtx = vw[0] - vn * nx, vty = vw[1] - vn * ny, vtz = vw[2] - vn * nz;
     const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
     const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
@@ -1413,13 +1428,212 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // kinematics and ABA passes redundantly (base quantities on all 16 lanes), and
 // split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
 // two per lane, so each wave has four envs and the whole grid fills every SIMD.
-// cf_raw: this lane's reported contact forces (its two points; its leg's hip).
+// cf_raw: this lane's reported contact forces (its two points; its leg's hip; the trunk's self-collision
+// reaction of the lane's box pairs).
 // `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
 // in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
+// ---- self-collision (asset.self_collisions == 0, go1_crawling.py:44; oracle/go1_oracle.c self_forces)
+// Spheres leg * 6 + s (s: thigh 0-2, calf 3-4, foot 5, the contact points below); the 162 sphere pairs and
+// per-sphere slot lists in go1_selfpairs.h (tools/gen_selfpairs.py): the calf and foot spheres against the
+// other legs' spheres; and the calf and foot spheres against the trunk box.  Explicit penalty springs on the
+// overlap, fn = ks pen - ds vn (compressive only), no friction, no added mass (the two bodies sit in
+// different legs' ABA chains).
+// Broad phase in registers: each lane bounds its leg (thigh joint, knee, foot, grown by the largest sphere
+// radius) by an AABB, swaps the four legs' boxes over the quad (DPP) and tests the six leg pairs and the
+// trunk's world AABB; a wave whose envs have no overlapping pair is done.  Otherwise, per env in LDS: the 24
+// spheres as (pos, r), (vel, 0); each lane tests its share of the pairs (k, k + 16, ... for env-local lane k)
+// of the overlapping leg pairs; if some sphere pair overlaps anywhere in the wave, each lane writes the force
+// of each of its pairs (zero when apart) into the pair's slot and every sphere's owner sums its slots in the
+// table's order -- the force on a sphere does not depend on which lane evaluated which pair, and a pair's two
+// spheres get exactly opposite forces.  The box pairs are evaluated by the sphere's own lane.
+#define SELF_ENV_FLOATS (24 * 8 + SELF_NPAIRS_PAD * 4)
+
+// force on sphere A (world) of the pair (A, B); zero when apart or when the spring no longer compresses
+__device__ __forceinline__ void self_sphere_force(const float4 A, const float4 Av, const float4 B, const float4 Bv,
+                                                  float ks, float ds, float* F) {
+  const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z;
+  const float dd = d0 * d0 + d1 * d1 + d2 * d2, rs = A.w + B.w;
+  const float inv = dd > 1e-18f ? frsq(dd) : 0.0f;
+  const float n0 = dd > 1e-18f ? d0 * inv : 0.0f, n1 = dd > 1e-18f ? d1 * inv : 0.0f,
+              n2 = dd > 1e-18f ? d2 * inv : 1.0f;
+  const float pen = rs - dd * inv;
+  const float vn = (Av.x - Bv.x) * n0 + (Av.y - Bv.y) * n1 + (Av.z - Bv.z) * n2;
+  float fn = ks * pen - ds * vn;
+  fn = (dd < rs * rs && fn > 0.0f) ? fn : 0.0f;
+  F[0] = fn * n0; F[1] = fn * n1; F[2] = fn * n2;
+}
+
+// sphere A against the trunk box (half extents th about the base origin): the force on A (world) added to F
+// and the trunk's reaction wrench (base frame, (moment, force) about the base origin) added to wb
+__device__ __forceinline__ void self_box_force(const float4 A, const float4 Av, const float* R, const float* pos,
+                                               const float* vb, const float* th, float ks, float ds, float* F,
+                                               float* wb) {
+  const float w0 = A.x - pos[0], w1 = A.y - pos[1], w2 = A.z - pos[2];
+  float c[3], q[3], d[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) c[i] = R[i] * w0 + R[3 + i] * w1 + R[6 + i] * w2;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { q[i] = fminf(fmaxf(c[i], -th[i]), th[i]); d[i] = c[i] - q[i]; }
+  const float dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+  float nb[3], pen;
+  if (dd > 0.0f) {
+    const float inv = frsq(dd);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) nb[i] = d[i] * inv;
+    pen = A.w - dd * inv;
+  } else {  // centre inside: out through the nearest face (lowest axis on ties)
+    const float m0 = th[0] - fabsf(c[0]), m1 = th[1] - fabsf(c[1]), m2 = th[2] - fabsf(c[2]);
+    const int ax = (m0 <= m1 && m0 <= m2) ? 0 : (m1 <= m2 ? 1 : 2);
+    const float sg = c[ax] >= 0.0f ? 1.0f : -1.0f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) nb[i] = i == ax ? sg : 0.0f;
+    q[ax] = sg * th[ax];
+    pen = A.w + (ax == 0 ? m0 : (ax == 1 ? m1 : m2));
+  }
+  // the trunk's velocity at q (base frame v + w x q), relative normal velocity in the base frame
+  const float vq0 = vb[3] + (vb[1] * q[2] - vb[2] * q[1]);
+  const float vq1 = vb[4] + (vb[2] * q[0] - vb[0] * q[2]);
+  const float vq2 = vb[5] + (vb[0] * q[1] - vb[1] * q[0]);
+  float va[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) va[i] = R[i] * Av.x + R[3 + i] * Av.y + R[6 + i] * Av.z;
+  const float vn = (va[0] - vq0) * nb[0] + (va[1] - vq1) * nb[1] + (va[2] - vq2) * nb[2];
+  float fn = ks * pen - ds * vn;
+  fn = (dd < A.w * A.w && fn > 0.0f) ? fn : 0.0f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) F[i] += fn * (R[3 * i] * nb[0] + R[3 * i + 1] * nb[1] + R[3 * i + 2] * nb[2]);
+  const float f0 = -fn * nb[0], f1 = -fn * nb[1], f2v = -fn * nb[2];
+  wb[0] += q[1] * f2v - q[2] * f1;
+  wb[1] += q[2] * f0 - q[0] * f2v;
+  wb[2] += q[0] * f1 - q[1] * f0;
+  wb[3] += f0; wb[4] += f1; wb[5] += f2v;
+}
+
+template <int D>
+__device__ __forceinline__ float quad_xor(float v) {  // the value of lane ^ D within the quad (DPP quad_perm)
+  constexpr int c = D == 1 ? 0xB1 : (D == 2 ? 0x4E : 0x1B);
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), c, 0xF, 0xF, true));
+}
+__device__ __forceinline__ int quad_or(int v) {
+  v |= __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true);
+  return v | __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);
+}
+
+// sc: this env's LDS scratch (SELF_ENV_FLOATS); the leg's thigh joint, knee and foot (world); the lane's
+// spheres p0 (x halves of pw / vw / rr) and p1 (y halves; -1: a trunk corner).  Fs: the self-contact world
+// forces on the lane's two points, wb: the trunk reaction wrench of the lane's box contacts (base frame, summed
+// over the env's lanes by the caller).
+__device__ __forceinline__ void self_collide(CCfg* __restrict__ cfg, float* sc, int leg, int role, const float* pth,
+                                             const float* pkn, const float* pft, float rmax, const f2* pw,
+                                             const f2* vw, f2 rr, const float* R, const float* pos,
+                                             const float* vb, const float* th, float Fs[2][3], float* wb) {
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) Fs[hh][0] = Fs[hh][1] = Fs[hh][2] = 0.0f;
+  // ---- broad phase: the legs' AABBs, the trunk's world AABB
+  float lo[3], hi[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    lo[i] = fminf(fminf(pth[i], pkn[i]), pft[i]) - rmax;
+    hi[i] = fmaxf(fmaxf(pth[i], pkn[i]), pft[i]) + rmax;
+  }
+  int mask = 0;  // bit lp: leg pair lp overlaps (go1_selfpairs.h order); bit 6 + leg: the leg meets the trunk box
+  float olo[3][3], ohi[3][3];  // the boxes of legs leg ^ 1, ^ 2, ^ 3
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    olo[0][i] = quad_xor<1>(lo[i]); ohi[0][i] = quad_xor<1>(hi[i]);
+    olo[1][i] = quad_xor<2>(lo[i]); ohi[1][i] = quad_xor<2>(hi[i]);
+    olo[2][i] = quad_xor<3>(lo[i]); ohi[2][i] = quad_xor<3>(hi[i]);
+  }
+#pragma unroll
+  for (int dl = 1; dl < 4; ++dl) {
+    bool ov = true;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ov = ov && lo[i] <= ohi[dl - 1][i] && olo[dl - 1][i] <= hi[i];
+    const int o = leg ^ dl, la = min(leg, o), lb = max(leg, o);
+    const int lp = la == 0 ? lb - 1 : (la == 1 ? lb + 1 : 5);
+    mask |= ov ? (1 << lp) : 0;
+  }
+  {
+    bool ov = true;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float e = fabsf(R[3 * i]) * th[0] + fabsf(R[3 * i + 1]) * th[1] + fabsf(R[3 * i + 2]) * th[2];
+      ov = ov && lo[i] <= pos[i] + e && pos[i] - e <= hi[i];
+    }
+    mask |= ov ? (64 << leg) : 0;
+  }
+  mask = quad_or(mask);
+  if (!__any(mask != 0)) return;
+  // ---- narrow phase
+  const float ks = cfg->self_stiffness, ds = cfg->self_damping;
+  const int k = 4 * role + leg;
+  const int p0 = role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5));
+  const int p1 = role == 0 ? 1 : (role == 2 ? 4 : -1);
+  // the trunk box, by the lane of the sphere (calf and foot spheres: x halves of roles 2, 3, y half of role 2)
+  if ((mask >> (6 + leg)) & 1) {
+    if (role >= 2)
+      self_box_force(make_float4(pw[0].x, pw[1].x, pw[2].x, rr.x), make_float4(vw[0].x, vw[1].x, vw[2].x, 0.0f),
+                     R, pos, vb, th, ks, ds, Fs[0], wb);
+    if (role == 2)
+      self_box_force(make_float4(pw[0].y, pw[1].y, pw[2].y, rr.y), make_float4(vw[0].y, vw[1].y, vw[2].y, 0.0f),
+                     R, pos, vb, th, ks, ds, Fs[1], wb);
+  }
+  if (!__any((mask & 63) != 0)) return;
+  float4* P = reinterpret_cast<float4*>(sc);
+  float4* FS = reinterpret_cast<float4*>(sc + 24 * 8);
+  P[(leg * 6 + p0) * 2] = make_float4(pw[0].x, pw[1].x, pw[2].x, rr.x);
+  P[(leg * 6 + p0) * 2 + 1] = make_float4(vw[0].x, vw[1].x, vw[2].x, 0.0f);
+  if (p1 >= 0) {
+    P[(leg * 6 + p1) * 2] = make_float4(pw[0].y, pw[1].y, pw[2].y, rr.y);
+    P[(leg * 6 + p1) * 2 + 1] = make_float4(vw[0].y, vw[1].y, vw[2].y, 0.0f);
+  }
+  __syncthreads();
+  constexpr int NT = SELF_NPAIRS_PAD / 16;
+  unsigned act = 0u;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int i = k + 16 * t;
+    if (i < SELF_NPAIRS && ((mask >> (i / 27)) & 1)) {
+      const unsigned e = SELF_PAIR[i];
+      const float4 A = P[2 * (e & 0xffu)], B = P[2 * (e >> 8)];
+      const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
+      act |= (d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << t) : 0u;
+    }
+  }
+  if (!__any(act != 0u)) return;
+  // some sphere pair of the wave overlaps: every slot of the block written, then the owners' sums
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float F[3] = {0.0f, 0.0f, 0.0f};
+    if ((act >> t) & 1u) {
+      const unsigned e = SELF_PAIR[k + 16 * t], a = e & 0xffu, b = e >> 8;
+      self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
+    }
+    FS[k + 16 * t] = make_float4(F[0], F[1], F[2], 0.0f);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int p = hh == 0 ? p0 : p1;
+    if (p < 0) continue;
+    const short* sl = SELF_SLOT[leg * 6 + p];
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+    for (int j = 0; j < SELF_SLOTS; ++j) {
+      const int v = sl[j];
+      if (v < 0) break;
+      const float4 f = FS[v >> 1];
+      const float sg = (v & 1) ? -1.0f : 1.0f;
+      s0 += sg * f.x; s1 += sg * f.y; s2 += sg * f.z;
+    }
+    Fs[hh][0] += s0; Fs[hh][1] += s1; Fs[hh][2] += s2;
+  }
+}
+
 __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
-                                             float h, const float* g, float friction, float payload, const Terr& T,
-                                             int leg, int role, bool cf_out, float* cf_raw) {
+                                             float h, const float* g, float friction, float restitution,
+                                             float payload, const Terr& T, int leg, int role, bool cf_out,
+                                             float* cf_raw, float* self_sc) {
 #pragma clang fp contract(on)
   // Model constants are compile-time literals (go1_model_consts.h, checked against the
   // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
@@ -1434,7 +1648,8 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     LC[i] = p == 0 ? GO1_LEG_FL[i] : GO1_LEG_FL[i] * (p == 1 ? msx : (p == 2 ? msy : msxy));
   }
   MARK(phys_begin);
-  const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
+  const CP C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction,
+                0.5f * (restitution + cfg->terrain_restitution), cfg->bounce_threshold};
   float R[9];
   quat_to_R(S.quat, R);
   f2 vbp[3];  // base-frame (angular, linear) velocity pairs: R^T on both halves at once
@@ -1506,6 +1721,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   // per lane: the leg's (thigh | calf) share in the row pair of its body and the trunk corner's share
   float fleg[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
   f2 Fpt[3] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};  // world forces of the lane's two points
+  float Fbs[3] = {0.0f, 0.0f, 0.0f};  // world reaction force on the trunk of the lane's self-collision box pairs
   const bool even = (role & 1) == 0;
   // the contact inertias of this lane's points as one packed SIP per half (x, y = the two points):
   // [[S M S^T, S M], [M S^T, M]] with M = Rs^T Mp Rs in the body frame, S = lp~
@@ -1553,6 +1769,18 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       hq_fetch(T, pw[0].x, pw[1].x, qa);
       hq_fetch(T, pw[0].y, pw[1].y, qb);
     }
+    // self-collision while the terrain reads land: world forces on the lane's two spheres, the trunk's
+    // reaction wrench of the lane's box pairs into its trunk share
+    float Fs[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}}, wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (cfg->self_stiffness > 0.0f) {
+      float pft[3];  // the foot centre (calf frame offset), for the leg's bounding box
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pft[i] = pl[1][i] + Rl[1][3 * i] * foot[0] + Rl[1][3 * i + 1] * foot[1] + Rl[1][3 * i + 2] * foot[2];
+      self_collide(cfg, self_sc, leg, role, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), pw, vw, rr, R,
+                   S.pos, vb, th, Fs, wb);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
+    }
     float Fa[3], Fb2[3], Ma[6], Mb[6];
     {
       const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
@@ -1560,6 +1788,8 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       sphere_contact_im(T, qa, C, pa, va, rr.x, h, Fa, Ma);
       sphere_contact_im(T, qb, C, pb, vb2, rr.y, h, Fb2, Mb);
     }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { Fa[i] += Fs[0][i]; Fb2[i] += Fs[1][i]; }
     const f2 F[3] = {f2{Fa[0], Fb2[0]}, f2{Fa[1], Fb2[1]}, f2{Fa[2], Fb2[2]}};
     // the ABA below solves for accelerations relative to free fall (gravity as a base
     // acceleration), so the added mass would respond to a - g: the force it sees is F - Mp g
@@ -1578,7 +1808,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       fleg[i] = f6[i].x + (even ? f6[i].y : 0.0f);
-      fbase[i] = even ? 0.0f : f6[i].y;
+      fbase[i] = (even ? 0.0f : f6[i].y) + wb[i];
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) Fpt[i] = F[i];
@@ -1844,6 +2074,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     cf_raw[i] = Fpt[i].x;
     cf_raw[3 + i] = Fpt[i].y;
     cf_raw[6 + i] = Fhip[i];
+    cf_raw[9 + i] = Fbs[i];
   }
 }
 
@@ -1859,7 +2090,7 @@ __device__ __forceinline__ void cf_sum(const float* cf_raw, int role, float* cf_
     v[i] = role == 0 ? x + y : (role == 1 ? x : 0.0f);  // thigh
     v[3 + i] = role == 2 ? x + y : 0.0f;                 // calf
     v[6 + i] = role == 3 ? x : 0.0f;                     // foot
-    v[9 + i] = (role & 1) ? y : 0.0f;                    // trunk corners
+    v[9 + i] = ((role & 1) ? y : 0.0f) + cf_raw[9 + i];  // trunk corners, self-collision reactions
   }
   rowsum4_n<12>(v);
 #pragma unroll

@@ -260,6 +260,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   Terr T = {nullptr, CI(hf_nx), CI(hf_ny), CI(horizontal_scale), nullptr, 0, 0};
   __shared__ float2 s_patch[SEPB][PSZX * PSZY];
   __shared__ float s_phys[(LDS_FLOATS + 63) / 64 * 64];
+  __shared__ __attribute__((aligned(16))) float s_self[SEPB][SELF_ENV_FLOATS];  // self-collision scratch
   // Block = one wave, so LDS needs no barrier here (a wave's LDS operations execute in
   // order).  The model block and the terrain patches are staged with LDS-DMA
   // (global_load_lds: no VGPR round trip, no __syncthreads fence draining the state loads);
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // (:973), so sub-step s reads the slot s+1 of the incoming ring and the ring
   // leaves the step as [old4, old5, old6, scaled x 4].
   float torque[3], tgt[3];
-  float cf_raw[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
+  float cf_raw[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
   for (int sub = 0; sub < dec; ++sub) {
     MARK(sub_begin);
     // _compute_torques (:957-996)
@@ -415,7 +416,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #ifndef GO1_ABL_NO_PHYS
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
-        phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw);
+        phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, restitution, payload, T, leg, role, last,
+                     cf_raw, s_self[el]);
       }
 #else
       P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];

@@ -219,6 +219,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     lljpt[j] = st.last_last_joint_pos_target[d0 + j];
   }
   const float friction = st.friction[e], payload = st.payload[e], restitution = st.restitution[e];
+  __shared__ __attribute__((aligned(16))) float s_self[SEPB][SELF_ENV_FLOATS];  // self-collision scratch
   const float eo_pre[3] = {K.env_origins[(size_t)e * 3], K.env_origins[(size_t)e * 3 + 1],
                            K.env_origins[(size_t)e * 3 + 2]};
   const int ep_in = st.episode_length[e];
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // ---------------- decimation loop (:76-82): lag ring pushed per sim step (:940-942)
   float torque[3], tgt[3];
-  float cf_raw[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
+  float cf_raw[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
   for (int sub = 0; sub < dec; ++sub) {
     {
       const int m = 6 - sub;
@@ -307,7 +308,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int j = 0; j < 3; ++j) { P.q[j] = q[j]; P.qd[j] = qd[j]; }
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
-        phys_substep(c, nullptr, P, torque, h, A.sim_gravity, friction, payload, T, leg, role, last, cf_raw);
+        phys_substep(c, nullptr, P, torque, h, A.sim_gravity, friction, restitution, payload, T, leg, role, last,
+                     cf_raw, s_self[el]);
       }
 #pragma unroll
       for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }

@@ -160,8 +160,7 @@ def build_configs(cfg, n_envs=None, physics=None, env_id_offset=0, history_len=N
         c.torque_limits[i] = f32(L.TORQUE_LIMIT)
         lo, hi = L.JOINT_LIMITS[i % 3]
         c.hard_limits[2 * i], c.hard_limits[2 * i + 1] = f32(lo), f32(hi)
-    for k in ("contact_stiffness", "contact_damping", "friction_damping", "limit_stiffness", "limit_damping"):
-        setattr(c, k, float(physics[k]))
+    CF.set_contact_fields(c, cfg, physics)
     from . import model as M
     for i, x in enumerate(M.model_block()):
         c.model[i] = float(x)

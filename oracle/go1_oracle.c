@@ -405,6 +405,7 @@ static void height_query(const TerrainView* T, int layer, real x, real y, real* 
 
 typedef struct {
   real k, d, kf, mu;
+  real e, vb; /* restitution (env and terrain averaged, PhysX's default combine) and the bounce threshold */
 } ContactParams;
 
 /* The integrator's contact scheme (go1_step.hip sphere_contact_im): contact forces linearly
@@ -443,6 +444,9 @@ static void sphere_contact_im(const TerrainView* T, const ContactParams* C, cons
     real fn0 = C->k * depth - C->d * vn;
     if (fn0 <= 0.0) continue;
     real fn = C->k * depth - (h * C->k + C->d) * vn;
+    /* restitution: separating faster than the bounce threshold, the fraction e of the contact's damping
+       (h k + d) is handed back (go1_device.h restitute) */
+    if (C->e > 0.0 && vn > C->vb) fn += C->e * (h * C->k + C->d) * vn;
     real vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
     real vtn = sqrt(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
     real ct = C->kf;
@@ -557,11 +561,71 @@ static void point_force(real Rb[3][3], const real* lp, const real* F, real* fs) 
   for (int i = 0; i < 3; ++i) { fs[i] += n[i]; fs[3 + i] += f[i]; }
 }
 
+/* Self-collision (asset.self_collisions == 0, go1_crawling.py:44; go1_device.h self_collide): spheres
+ * leg * 6 + s (s: thigh points 0-2, calf points 3-4, foot 5); pairs: for legs la < lb every (a, b) with a or
+ * b a calf / foot sphere, and every calf / foot sphere against the trunk box (half extents trunk_half about
+ * the base origin).  Explicit penalty springs fn = ks pen - ds vn on the overlap, compressive only, no
+ * friction; the force on the lower sphere id is computed, the other sphere gets its negative, the trunk the
+ * box pairs' reaction. */
+static void self_sphere_force(const real* pa, const real* va, real ra, const real* pb, const real* vb, real rb,
+                              real ks, real ds, real* F) {
+  real d[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+  real dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2], rs = ra + rb;
+  F[0] = F[1] = F[2] = 0.0;
+  if (!(dd < rs * rs)) return;
+  real dist = sqrt(dd), n[3] = {0.0, 0.0, 1.0};
+  if (dd > 1e-18) for (int i = 0; i < 3; ++i) n[i] = d[i] / dist;
+  else dist = 0.0;
+  real vn = (va[0] - vb[0]) * n[0] + (va[1] - vb[1]) * n[1] + (va[2] - vb[2]) * n[2];
+  real fn = ks * (rs - dist) - ds * vn;
+  if (fn <= 0.0) return;
+  for (int i = 0; i < 3; ++i) F[i] = fn * n[i];
+}
+
+/* sphere (world pa, va, radius r) against the trunk box: force on the sphere (world) and the trunk's
+ * reaction wrench (base frame, (moment, force) about the base origin) added to wb */
+static void self_box_force(const real* pa, const real* va, real r, real R[3][3], const real* pos, const real* vbase,
+                           const real* th, real ks, real ds, real* F, real* wb) {
+  real c[3], q[3], d[3], nb[3], pen;
+  F[0] = F[1] = F[2] = 0.0;
+  for (int i = 0; i < 3; ++i) c[i] = R[0][i] * (pa[0] - pos[0]) + R[1][i] * (pa[1] - pos[1]) + R[2][i] * (pa[2] - pos[2]);
+  for (int i = 0; i < 3; ++i) { q[i] = fmin(fmax(c[i], -th[i]), th[i]); d[i] = c[i] - q[i]; }
+  real dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+  if (!(dd < r * r)) return;
+  if (dd > 0.0) {
+    real dist = sqrt(dd);
+    for (int i = 0; i < 3; ++i) nb[i] = d[i] / dist;
+    pen = r - dist;
+  } else { /* centre inside: out through the nearest face, lowest axis on ties */
+    real m[3];
+    for (int i = 0; i < 3; ++i) m[i] = th[i] - fabs(c[i]);
+    int ax = (m[0] <= m[1] && m[0] <= m[2]) ? 0 : (m[1] <= m[2] ? 1 : 2);
+    real sg = c[ax] >= 0.0 ? 1.0 : -1.0;
+    for (int i = 0; i < 3; ++i) nb[i] = i == ax ? sg : 0.0;
+    q[ax] = sg * th[ax];
+    pen = r + m[ax];
+  }
+  real vq[3], w[3] = {vbase[0], vbase[1], vbase[2]}, wq[3];
+  cross3(w, q, wq);
+  for (int i = 0; i < 3; ++i) vq[i] = vbase[3 + i] + wq[i];
+  real vab[3];
+  for (int i = 0; i < 3; ++i) vab[i] = R[0][i] * va[0] + R[1][i] * va[1] + R[2][i] * va[2];
+  real vn = (vab[0] - vq[0]) * nb[0] + (vab[1] - vq[1]) * nb[1] + (vab[2] - vq[2]) * nb[2];
+  real fn = ks * pen - ds * vn;
+  if (fn <= 0.0) return;
+  for (int i = 0; i < 3; ++i) F[i] = fn * (R[i][0] * nb[0] + R[i][1] * nb[1] + R[i][2] * nb[2]);
+  real fb[3] = {-fn * nb[0], -fn * nb[1], -fn * nb[2]}, tq[3];
+  cross3(q, fb, tq);
+  for (int i = 0; i < 3; ++i) { wb[i] += tq[i]; wb[3 + i] += fb[i]; }
+}
+
 /* One integrator step of length h with torques tau.  Writes net contact forces
  * per reported body (17 x 3, world) into cf (may be NULL). */
 static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, const real* tau, real h,
-                         const real* g, real friction, real payload, const TerrainView* T, real* cf) {
-  ContactParams C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction};
+                         const real* g, real friction, real restitution, real payload, const TerrainView* T,
+                         real* cf) {
+  ContactParams C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction,
+                     0.5 * (restitution + (real)cfg->terrain_restitution), cfg->bounce_threshold};
   real R[3][3];
   quat_to_R(S->quat, R);
   real vb[6]; /* base spatial velocity, body coords */
@@ -606,13 +670,13 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
 
   /* per-leg quantities kept for the forward pass */
   real E[4][3][3][3], vj[4][3][6], cj[4][3][6], U[4][3][6], D[4][3], u[4][3];
+  real Rw_all[4][3][3][3], pw_all[4][3][3];
   for (int l = 0; l < 4; ++l) {
     real Rp[3][3], pp[3], vp[6];
     memcpy(Rp, R, sizeof(Rp));
     memcpy(pp, S->pos, sizeof(pp));
     memcpy(vp, vb, sizeof(vp));
-    M6 IA[3];
-    real pA[3][6], Rw[3][3][3], pw_[3][3];
+    real (*Rw)[3][3] = Rw_all[l], (*pw_)[3] = pw_all[l];
     for (int j = 0; j < 3; ++j) {
       int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
       const real* r = M->origin[l][j];
@@ -636,6 +700,50 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       memcpy(pp, pw_[j], sizeof(pp));
       memcpy(vp, vj[l][j], sizeof(vp));
     }
+  }
+  /* self-collision forces on the thigh / calf / foot spheres and the trunk's reaction wrench */
+  real Fself[24][3], wself[6] = {0, 0, 0, 0, 0, 0};
+  memset(Fself, 0, sizeof(Fself));
+  if (cfg->self_stiffness > 0.0f) {
+    real SP[24][3], SV[24][3], SR[24];
+    for (int l = 0; l < 4; ++l)
+      for (int s6 = 0; s6 < 6; ++s6) {
+        int j = s6 < 3 ? 1 : 2;
+        real lp[3] = {0, 0, 0};
+        if (s6 < 3) lp[2] = THIGH_PTS_Z[s6];
+        else if (s6 < 5) lp[2] = CALF_PTS_Z[s6 - 3];
+        else { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
+        point_kin(Rw_all[l][j], pw_all[l][j], vj[l][j], lp, SP[l * 6 + s6], SV[l * 6 + s6]);
+        SR[l * 6 + s6] = s6 < 3 ? M->thigh_r : (s6 < 5 ? M->calf_r : M->foot_r);
+      }
+    const real ks = cfg->self_stiffness, ds = cfg->self_damping;
+    for (int la = 0; la < 4; ++la)
+      for (int lb = la + 1; lb < 4; ++lb)
+        for (int a = 0; a < 6; ++a)
+          for (int b = 0; b < 6; ++b) {
+            if (a < 3 && b < 3) continue;
+            int ia = la * 6 + a, ib = lb * 6 + b;
+            real F[3];
+            self_sphere_force(SP[ia], SV[ia], SR[ia], SP[ib], SV[ib], SR[ib], ks, ds, F);
+            for (int i = 0; i < 3; ++i) { Fself[ia][i] += F[i]; Fself[ib][i] -= F[i]; }
+          }
+    for (int l = 0; l < 4; ++l)
+      for (int s6 = 3; s6 < 6; ++s6) {
+        int ia = l * 6 + s6;
+        real F[3];
+        real wb[6] = {0, 0, 0, 0, 0, 0};
+        self_box_force(SP[ia], SV[ia], SR[ia], R, S->pos, vb, M->trunk_half, ks, ds, F, wb);
+        for (int i = 0; i < 6; ++i) wself[i] += wb[i];
+        for (int i = 0; i < 3; ++i) Fself[ia][i] += F[i];
+        /* the trunk's reported contact force includes the reaction (world frame) */
+        if (cf) for (int i = 0; i < 3; ++i) cf[i] += R[i][0] * wb[3] + R[i][1] * wb[4] + R[i][2] * wb[5];
+      }
+    for (int i = 0; i < 6; ++i) pA0[i] -= wself[i];
+  }
+  for (int l = 0; l < 4; ++l) {
+    M6 IA[3];
+    real pA[3][6];
+    real (*Rw)[3][3] = Rw_all[l], (*pw_)[3] = pw_all[l];
     /* rigid inertias, bias forces, gravity and contact */
     for (int j = 0; j < 3; ++j) {
       const Body* B = &M->leg[l][j];
@@ -675,6 +783,7 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
           } else {
             sphere_contact(T, &C, pw, vw, M->thigh_r, F);
           }
+          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 6 + p][i];
           point_force(Rw[j], lp, F, fext);
           if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
         }
@@ -692,6 +801,7 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
           } else {
             sphere_contact(T, &C, pw, vw, r, F);
           }
+          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 6 + 3 + p][i];
           point_force(Rw[j], lp, F, fext);
           int bi = p < N_CALF_PTS ? body_idx : body_idx + 1; /* foot body reported separately */
           if (cf) for (int i = 0; i < 3; ++i) cf[bi * 3 + i] += F[i];
@@ -787,10 +897,66 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
   }
 }
 
+/* Mechanical energy of a state (physics invariant tests): the kinetic energy of the 13 rigid bodies plus
+ * their potential energy in the gravity field g (world), with the integrator's kinematics and inertias. */
+double go1o_energy(const go1_config* cfg, const double* pos, const double* quat, const double* v, const double* w,
+                   const double* q, const double* qd, const double* g, double payload) {
+  Model M;
+  load_model(cfg, &M);
+  real R[3][3], qt[4] = {quat[0], quat[1], quat[2], quat[3]};
+  quat_to_R(qt, R);
+  real vb[6];
+  for (int i = 0; i < 3; ++i) {
+    vb[i] = R[0][i] * w[0] + R[1][i] * w[1] + R[2][i] * w[2];
+    vb[3 + i] = R[0][i] * v[0] + R[1][i] * v[1] + R[2][i] * v[2];
+  }
+  real mscale = (M.base.mass + payload) / M.base.mass, e = 0.0;
+  M6 I;
+  real hm[6];
+  rigid_inertia(&M.base, mscale, &I);
+  m6_vec(&I, vb, hm);
+  for (int i = 0; i < 6; ++i) e += 0.5 * vb[i] * hm[i];
+  for (int i = 0; i < 3; ++i) {
+    real ci = pos[i] + R[i][0] * M.base.com[0] + R[i][1] * M.base.com[1] + R[i][2] * M.base.com[2];
+    e -= M.base.mass * mscale * g[i] * ci;
+  }
+  for (int l = 0; l < 4; ++l) {
+    real Rp[3][3], pp[3], vp[6];
+    memcpy(Rp, R, sizeof(Rp));
+    for (int i = 0; i < 3; ++i) pp[i] = pos[i];
+    memcpy(vp, vb, sizeof(vp));
+    for (int j = 0; j < 3; ++j) {
+      int ax = j == 0 ? 0 : 1, dof = l * 3 + j;
+      const real* r = M.origin[l][j];
+      real E[3][3], vj[6], Rw[3][3], pw[3];
+      joint_E(ax, q[dof], E);
+      xform_motion(E, r, vp, vj);
+      vj[ax] += qd[dof];
+      for (int i = 0; i < 3; ++i) {
+        pw[i] = pp[i] + Rp[i][0] * r[0] + Rp[i][1] * r[1] + Rp[i][2] * r[2];
+        for (int k = 0; k < 3; ++k) Rw[i][k] = Rp[i][0] * E[k][0] + Rp[i][1] * E[k][1] + Rp[i][2] * E[k][2];
+      }
+      const Body* B = &M.leg[l][j];
+      rigid_inertia(B, 1.0, &I);
+      m6_vec(&I, vj, hm);
+      for (int i = 0; i < 6; ++i) e += 0.5 * vj[i] * hm[i];
+      for (int i = 0; i < 3; ++i) {
+        real ci = pw[i] + Rw[i][0] * B->com[0] + Rw[i][1] * B->com[1] + Rw[i][2] * B->com[2];
+        e -= B->mass * g[i] * ci;
+      }
+      memcpy(Rp, Rw, sizeof(Rp));
+      memcpy(pp, pw, sizeof(pp));
+      memcpy(vp, vj, sizeof(vp));
+    }
+  }
+  return (double)e;
+}
+
 /* exposed for the physics invariant tests: run n substeps of length h on a
  * state given as doubles; tiles may be NULL (plane) */
 void go1o_physics(const go1_config* cfg, double* pos, double* quat, double* v, double* w, double* q, double* qd,
-                  const double* tau, int n_sub, double h, const double* g, double friction, double payload,
+                  const double* tau, int n_sub, double h, const double* g, double friction, double restitution,
+                  double payload,
                   const float* tile, double ox, double oy, double* cf_out) {
   Model M;
   load_model(cfg, &M);
@@ -800,7 +966,7 @@ void go1o_physics(const go1_config* cfg, double* pos, double* quat, double* v, d
   for (int i = 0; i < 4; ++i) S.quat[i] = quat[i];
   for (int d = 0; d < NDOF; ++d) { S.q[d] = q[d]; S.qd[d] = qd[d]; tr[d] = tau[d]; }
   TerrainView T = {tile, cfg->hf_nx, cfg->hf_ny, ox, oy, cfg->horizontal_scale};
-  for (int i = 0; i < n_sub; ++i) phys_substep(&M, cfg, &S, tr, (real)h, gr, (real)friction, (real)payload, &T, cfr);
+  for (int i = 0; i < n_sub; ++i) phys_substep(&M, cfg, &S, tr, (real)h, gr, (real)friction, (real)restitution, (real)payload, &T, cfr);
   for (int i = 0; i < 3; ++i) { pos[i] = S.pos[i]; v[i] = S.v[i]; w[i] = S.w[i]; }
   for (int i = 0; i < 4; ++i) quat[i] = S.quat[i];
   for (int d = 0; d < NDOF; ++d) { q[d] = S.q[d]; qd[d] = S.qd[d]; }
@@ -1060,7 +1226,7 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
       TerrainView T = {tile, c->hf_nx, c->hf_ny, 0, 0, c->horizontal_scale};
       real h = (real)c->sim_dt / c->n_internal;
       for (int k = 0; k < c->n_internal; ++k)
-        phys_substep(M, c, &S, tau, h, g, st->friction[e], st->payload[e], &T, cfd);
+        phys_substep(M, c, &S, tau, h, g, st->friction[e], st->restitution[e], st->payload[e], &T, cfd);
       for (int d = 0; d < NDOF; ++d) { dp[d] = (float)S.q[d]; dv[d] = (float)S.qd[d]; }
       for (int i = 0; i < NB * 3; ++i) cf[i] = (float)cfd[i];
     }

@@ -39,9 +39,39 @@ def lib(precision="f64"):
         _lib.go1o_uniform.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
         _lib.go1o_uniform.restype = C.c_float
         _lib.go1o_physics.argtypes = [C.POINTER(abi.Go1Config)] + [C.c_void_p] * 7 + [
-            C.c_int, C.c_double, C.c_void_p, C.c_double, C.c_double, C.c_void_p, C.c_double, C.c_double,
-            C.c_void_p]
+            C.c_int, C.c_double, C.c_void_p, C.c_double, C.c_double, C.c_double, C.c_void_p, C.c_double,
+            C.c_double, C.c_void_p]
+        _lib.go1o_energy.argtypes = [C.POINTER(abi.Go1Config)] + [C.c_void_p] * 7 + [C.c_double]
+        _lib.go1o_energy.restype = C.c_double
     return _lib
+
+
+def _d(x, n):
+    return np.ascontiguousarray(np.asarray(x, np.float64).reshape(n))
+
+
+def physics(cfg, body, tau, n_sub, h, g, friction, restitution, payload, tile=None, origin=(0.0, 0.0)):
+    """n_sub integrator steps of length h on one env's state given as a dict of f64 arrays (pos 3, quat 4 xyzw,
+    v 3, w 3 world; q 12, qd 12), updated in place; returns the last step's reported contact forces (17, 3).
+    tile: one (2, hf_nx, hf_ny) heightfield at `origin`, or None for the plane."""
+    b = {k: _d(body[k], n) for k, n in (("pos", 3), ("quat", 4), ("v", 3), ("w", 3), ("q", 12), ("qd", 12))}
+    t, gg = _d(tau, 12), _d(g, 3)
+    cf = np.zeros(17 * 3, np.float64)
+    tl = None if tile is None else np.ascontiguousarray(tile, np.float32)
+    lib().go1o_physics(C.byref(cfg), *(b[k].ctypes.data for k in ("pos", "quat", "v", "w", "q", "qd")),
+                       t.ctypes.data, int(n_sub), float(h), gg.ctypes.data, float(friction), float(restitution),
+                       float(payload), None if tl is None else tl.ctypes.data, float(origin[0]), float(origin[1]),
+                       cf.ctypes.data)
+    body.update(b)
+    return cf.reshape(17, 3)
+
+
+def energy(cfg, body, g, payload):
+    """Kinetic + potential energy of one env's state (dict as `physics`) in the gravity field g."""
+    b = {k: _d(body[k], n) for k, n in (("pos", 3), ("quat", 4), ("v", 3), ("w", 3), ("q", 12), ("qd", 12))}
+    gg = _d(g, 3)
+    return lib().go1o_energy(C.byref(cfg), *(b[k].ctypes.data for k in ("pos", "quat", "v", "w", "q", "qd")),
+                             gg.ctypes.data, float(payload))
 
 
 class _Readme:

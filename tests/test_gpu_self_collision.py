@@ -1,0 +1,77 @@
+"""Self-collision and restitution on the GPU step against the f64 oracle (CPU invariants of the same
+model in tests/test_self_collision.py).  One-step comparisons with the integrator bounds of
+tests/test_gpu_parity.py (check_integrator_step) on states built to exercise the new terms:
+  * legs in random poses within the joint limits, some with the front feet crossed under the trunk, the base
+    held 1 m above the plane (every reported force is then a self-contact force);
+  * the robot dropped onto the plane at up to 2.5 m/s with restitution 0..1, through the rebound.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from legged_tracking_amd import config as CF, layout as L, native  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from tests.test_gpu_parity import DEV, _dev, _sim_setup, check_integrator_step  # noqa: E402
+
+
+def _run(c, td, ter, st, rng, steps, act_scale=1.0, grav=(0.0, 0.0, 0.0), act=None):
+    g = native.Go1Native(c, DEV)
+    g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    gr, gvec = CF.gravity_state(list(grav))
+    scales = np.zeros(c.n_terms, np.float32)
+    forces = []
+    n = c.n_envs
+    for t in range(steps):
+        g.state.load(st.arrays)
+        a = (act_scale * rng.normal(0, 1, (n, 12))).astype(np.float32) if act is None else act.astype(np.float32)
+        g.step(_dev(a), gvec, gr, scales, rng_seed=5, rng_step=200 + t)
+        torch.cuda.synchronize()
+        out = O.step(c, st, ter, a, gvec, gr, scales, rng_seed=5, rng_step=200 + t, debug=False)
+        gs = g.state.numpy()
+        cf = g.contact_forces.cpu().numpy()
+        check_integrator_step(gs, st, cf, out["contact_forces"], g.reset.cpu().numpy().astype(bool),
+                              out["reset"].astype(bool))
+        forces.append(cf)
+        st = O.NpState(n, gs, c)
+    return np.stack(forces)
+
+
+def test_self_collision_step_vs_oracle():
+    n = 256
+    cfg, c, td, ter, st, rng = _sim_setup(n, "plane")
+    c.camera_zero = 0
+    assert c.self_stiffness > 0
+    lim = np.array([L.JOINT_LIMITS[j % 3] for j in range(12)])
+    q = rng.uniform(lim[:, 0], lim[:, 1], (n, 12)).astype(np.float32)
+    # a quarter of the envs with the front feet crossing under the trunk (tests/test_self_collision.py)
+    k = n // 4
+    q[:k] = [0.1, 0.8, -1.5, -0.1, 0.8, -1.5, 0.1, 1.0, -1.5, -0.1, 1.0, -1.5]
+    q[:k, 0] = -rng.uniform(0.30, 0.42, k)
+    q[:k, 3] = rng.uniform(0.30, 0.42, k)
+    st["dof_pos"][:] = q
+    st["dof_vel"][:] = 0.0
+    st["root"][:, 2] = st["root"][:, 2] + 1.0  # 1 m above the plane
+    st["episode_length"][:, 0] = 10
+    # actions that hold each pose (joint targets default + action_scale (x hip reduction) * action)
+    scale = np.float32(c.action_scale) * np.array([c.hip_scale_reduction, 1.0, 1.0] * 4, np.float32)
+    hold = (q - np.array(c.default_dof_pos, np.float32)) / scale
+    forces = _run(c, td, ter, st, rng, 3, act=np.clip(hold, -9.0, 9.0))
+    # every reported force is a self-contact force here: opposite pairs sum to zero per env
+    np.testing.assert_allclose(forces.sum(axis=2), 0.0, atol=2e-3)
+    touching = (np.abs(forces).max(axis=(0, 2, 3)) > 0)
+    assert touching[:k].mean() > 0.9 and touching.sum() > k + 5, (touching[:k].mean(), touching.sum())
+
+
+def test_restitution_step_vs_oracle():
+    n = 256
+    cfg, c, td, ter, st, rng = _sim_setup(n, "plane")
+    c.camera_zero = 0
+    st["restitution"][:, 0] = rng.uniform(0.0, 1.0, n).astype(np.float32)
+    st["root"][:, 2] = st["root"][:, 2] + rng.uniform(0.0, 0.05, n).astype(np.float32)
+    st["root"][:, 9] = -rng.uniform(0.5, 2.5, n).astype(np.float32)  # falling
+    st["episode_length"][:, 0] = 10
+    forces = _run(c, td, ter, st, rng, 4, act_scale=0.5, grav=(0.0, 0.0, 0.0))
+    assert (np.abs(forces).max(axis=(0, 2, 3)) > 0).mean() > 0.9

