@@ -1447,7 +1447,7 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // of each of its pairs (zero when apart) into the pair's slot and every sphere's owner sums its slots in the
 // table's order -- the force on a sphere does not depend on which lane evaluated which pair, and a pair's two
 // spheres get exactly opposite forces.  The box pairs are evaluated by the sphere's own lane.
-#define SELF_ENV_FLOATS (24 * 8 + SELF_NPAIRS_PAD * 4)
+#define SELF_ENV_FLOATS (24 * 8 + SELF_NPAIRS_PAD * 4)  // spheres, pair slots
 
 // force on sphere A (world) of the pair (A, B); zero when apart or when the spring no longer compresses
 __device__ __forceinline__ void self_sphere_force(const float4 A, const float4 Av, const float4 B, const float4 Bv,
@@ -1520,97 +1520,65 @@ __device__ __forceinline__ int quad_or(int v) {
   return v | __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);
 }
 
-// sc: this env's LDS scratch (SELF_ENV_FLOATS); the leg's thigh joint, knee and foot (world); the lane's
-// spheres p0 (x halves of pw / vw / rr) and p1 (y halves; -1: a trunk corner).  Fs: the self-contact world
-// forces on the lane's two points, wb: the trunk reaction wrench of the lane's box contacts (base frame, summed
-// over the env's lanes by the caller).
-__device__ __forceinline__ void self_collide(CCfg* __restrict__ cfg, float* sc, int leg, int role, const float* pth,
-                                             const float* pkn, const float* pft, float rmax, const f2* pw,
-                                             const f2* vw, f2 rr, const float* R, const float* pos,
-                                             const float* vb, const float* th, float Fs[2][3], float* wb) {
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) Fs[hh][0] = Fs[hh][1] = Fs[hh][2] = 0.0f;
-  // ---- broad phase: the legs' AABBs, the trunk's world AABB
-  float lo[3], hi[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    lo[i] = fminf(fminf(pth[i], pkn[i]), pft[i]) - rmax;
-    hi[i] = fmaxf(fmaxf(pth[i], pkn[i]), pft[i]) + rmax;
-  }
-  int mask = 0;  // bit lp: leg pair lp overlaps (go1_selfpairs.h order); bit 6 + leg: the leg meets the trunk box
-  float olo[3][3], ohi[3][3];  // the boxes of legs leg ^ 1, ^ 2, ^ 3
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    olo[0][i] = quad_xor<1>(lo[i]); ohi[0][i] = quad_xor<1>(hi[i]);
-    olo[1][i] = quad_xor<2>(lo[i]); ohi[1][i] = quad_xor<2>(hi[i]);
-    olo[2][i] = quad_xor<3>(lo[i]); ohi[2][i] = quad_xor<3>(hi[i]);
-  }
-#pragma unroll
-  for (int dl = 1; dl < 4; ++dl) {
-    bool ov = true;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) ov = ov && lo[i] <= ohi[dl - 1][i] && olo[dl - 1][i] <= hi[i];
-    const int o = leg ^ dl, la = min(leg, o), lb = max(leg, o);
-    const int lp = la == 0 ? lb - 1 : (la == 1 ? lb + 1 : 5);
-    mask |= ov ? (1 << lp) : 0;
-  }
-  {
-    bool ov = true;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float e = fabsf(R[3 * i]) * th[0] + fabsf(R[3 * i + 1]) * th[1] + fabsf(R[3 * i + 2]) * th[2];
-      ov = ov && lo[i] <= pos[i] + e && pos[i] - e <= hi[i];
-    }
-    mask |= ov ? (64 << leg) : 0;
-  }
-  mask = quad_or(mask);
-  if (!__any(mask != 0)) return;
-  // ---- narrow phase
+// Narrow phase (a wave whose broad phase found a candidate; inline: out of line, the call's saves and
+// restores of the step kernel's ~500 live registers cost more than the narrow phase itself).  sc: this env's
+// LDS scratch, the spheres already written (self_put); the lane's spheres p0 / p1 (-1: a trunk corner).
+// Work per candidate leg pair: its 27 sphere pairs over the env's 16 lanes (two rounds).  Fs: the
+// self-contact world forces on the lane's two points (x, y halves), wb: the trunk reaction wrench of the
+// lane's box contacts (base frame, summed over the env's lanes by the caller).
+__device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
+                                           const float* R, const float* pos, const float* vb, const float* th,
+                                           float Fs[2][3], float* wb) {
   const float ks = cfg->self_stiffness, ds = cfg->self_damping;
   const int k = 4 * role + leg;
   const int p0 = role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5));
   const int p1 = role == 0 ? 1 : (role == 2 ? 4 : -1);
-  // the trunk box, by the lane of the sphere (calf and foot spheres: x halves of roles 2, 3, y half of role 2)
-  if ((mask >> (6 + leg)) & 1) {
-    if (role >= 2)
-      self_box_force(make_float4(pw[0].x, pw[1].x, pw[2].x, rr.x), make_float4(vw[0].x, vw[1].x, vw[2].x, 0.0f),
-                     R, pos, vb, th, ks, ds, Fs[0], wb);
-    if (role == 2)
-      self_box_force(make_float4(pw[0].y, pw[1].y, pw[2].y, rr.y), make_float4(vw[0].y, vw[1].y, vw[2].y, 0.0f),
-                     R, pos, vb, th, ks, ds, Fs[1], wb);
-  }
-  if (!__any((mask & 63) != 0)) return;
   float4* P = reinterpret_cast<float4*>(sc);
   float4* FS = reinterpret_cast<float4*>(sc + 24 * 8);
-  P[(leg * 6 + p0) * 2] = make_float4(pw[0].x, pw[1].x, pw[2].x, rr.x);
-  P[(leg * 6 + p0) * 2 + 1] = make_float4(vw[0].x, vw[1].x, vw[2].x, 0.0f);
-  if (p1 >= 0) {
-    P[(leg * 6 + p1) * 2] = make_float4(pw[0].y, pw[1].y, pw[2].y, rr.y);
-    P[(leg * 6 + p1) * 2 + 1] = make_float4(vw[0].y, vw[1].y, vw[2].y, 0.0f);
+  // the trunk box, by the lane of the sphere (calf and foot spheres: x halves of roles 2, 3, y half of role 2)
+  if ((mask >> (6 + leg)) & 1) {
+    if (role >= 2) {
+      const int a = leg * 6 + p0;
+      self_box_force(P[2 * a], P[2 * a + 1], R, pos, vb, th, ks, ds, Fs[0], wb);
+    }
+    if (role == 2) {
+      const int a = leg * 6 + p1;
+      self_box_force(P[2 * a], P[2 * a + 1], R, pos, vb, th, ks, ds, Fs[1], wb);
+    }
   }
-  __syncthreads();
-  constexpr int NT = SELF_NPAIRS_PAD / 16;
-  unsigned act = 0u;
+  if (!__any((mask & 63) != 0)) return;
+  unsigned act = 0u;  // bit 2 lp + t: this lane's pair t of leg pair lp overlaps
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int i = k + 16 * t;
-    if (i < SELF_NPAIRS && ((mask >> (i / 27)) & 1)) {
-      const unsigned e = SELF_PAIR[i];
-      const float4 A = P[2 * (e & 0xffu)], B = P[2 * (e >> 8)];
-      const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
-      act |= (d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << t) : 0u;
+  for (int lp = 0; lp < 6; ++lp) {
+    if (!__any((mask >> lp) & 1)) continue;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = k + 16 * t;
+      if (j < 27 && ((mask >> lp) & 1)) {
+        const unsigned e = SELF_PAIR[lp * 27 + j];
+        const float4 A = P[2 * (e & 0xffu)], B = P[2 * (e >> 8)];
+        const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
+        act |= (d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << (2 * lp + t)) : 0u;
+      }
     }
   }
   if (!__any(act != 0u)) return;
-  // some sphere pair of the wave overlaps: every slot of the block written, then the owners' sums
+  // some sphere pair of the wave overlaps: every slot of the candidate leg pairs written, then the owners' sums
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    float F[3] = {0.0f, 0.0f, 0.0f};
-    if ((act >> t) & 1u) {
-      const unsigned e = SELF_PAIR[k + 16 * t], a = e & 0xffu, b = e >> 8;
-      self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
+  for (int lp = 0; lp < 6; ++lp) {
+    if (!__any((mask >> lp) & 1)) continue;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int j = k + 16 * t;
+      if (j < 27 && ((mask >> lp) & 1)) {
+        float F[3] = {0.0f, 0.0f, 0.0f};
+        if ((act >> (2 * lp + t)) & 1u) {
+          const unsigned e = SELF_PAIR[lp * 27 + j], a = e & 0xffu, b = e >> 8;
+          self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
+        }
+        FS[lp * 27 + j] = make_float4(F[0], F[1], F[2], 0.0f);
+      }
     }
-    FS[k + 16 * t] = make_float4(F[0], F[1], F[2], 0.0f);
   }
   __syncthreads();
 #pragma unroll
@@ -1622,12 +1590,58 @@ __device__ __forceinline__ void self_collide(CCfg* __restrict__ cfg, float* sc, 
     for (int j = 0; j < SELF_SLOTS; ++j) {
       const int v = sl[j];
       if (v < 0) break;
+      if (!((mask >> ((v >> 1) / 27)) & 1)) continue;  // a leg pair without candidates: no slot written
       const float4 f = FS[v >> 1];
       const float sg = (v & 1) ? -1.0f : 1.0f;
       s0 += sg * f.x; s1 += sg * f.y; s2 += sg * f.z;
     }
     Fs[hh][0] += s0; Fs[hh][1] += s1; Fs[hh][2] += s2;
   }
+}
+
+// the lane's spheres into this env's LDS scratch (x half p0; y half p1 unless a trunk corner)
+__device__ __forceinline__ void self_put(float* sc, int leg, int role, const f2* pw, const f2* vw, f2 rr) {
+  const int p0 = role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5));
+  const int p1 = role == 0 ? 1 : (role == 2 ? 4 : -1);
+  float4* P = reinterpret_cast<float4*>(sc);
+  P[(leg * 6 + p0) * 2] = make_float4(pw[0].x, pw[1].x, pw[2].x, rr.x);
+  P[(leg * 6 + p0) * 2 + 1] = make_float4(vw[0].x, vw[1].x, vw[2].x, 0.0f);
+  if (p1 >= 0) {
+    P[(leg * 6 + p1) * 2] = make_float4(pw[0].y, pw[1].y, pw[2].y, rr.y);
+    P[(leg * 6 + p1) * 2 + 1] = make_float4(vw[0].y, vw[1].y, vw[2].y, 0.0f);
+  }
+}
+
+// Broad phase, in registers, in the trunk frame (where the legs keep their places whatever the trunk's
+// pose; world-axis boxes of a yawed trunk overlap every leg): bit lp of the result = leg pair lp's boxes overlap
+// (go1_selfpairs.h order), bit 6 + leg = the leg's calf (knee to foot) box meets the trunk box; the same mask on
+// the env's 16 lanes.  Boxes: the thigh joint, knee and foot grown by the largest sphere radius.
+__device__ __forceinline__ int self_broad(int leg, const float* pth, const float* pkn, const float* pft, float rmax,
+                                          const float* R, const float* pos, const float* th) {
+  float b[3][3];  // the three points in the trunk frame, R^T (p - pos)
+  const float* pts[3] = {pth, pkn, pft};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float w0 = pts[k][0] - pos[0], w1 = pts[k][1] - pos[1], w2 = pts[k][2] - pos[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) b[k][i] = R[i] * w0 + R[3 + i] * w1 + R[6 + i] * w2;
+  }
+  bool o1 = true, o2 = true, o3 = true, ob = true;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float clo = fminf(b[1][i], b[2][i]) - rmax, chi = fmaxf(b[1][i], b[2][i]) + rmax;  // the calf
+    const float lo = fminf(b[0][i], clo), hi = fmaxf(b[0][i], chi);
+    o1 = o1 && lo <= quad_xor<1>(hi) && quad_xor<1>(lo) <= hi;
+    o2 = o2 && lo <= quad_xor<2>(hi) && quad_xor<2>(lo) <= hi;
+    o3 = o3 && lo <= quad_xor<3>(hi) && quad_xor<3>(lo) <= hi;
+    ob = ob && clo <= th[i] && -th[i] <= chi;
+  }
+  // leg pairs (leg, leg ^ d): lp(0,1) = 0, (0,2) = 1, (0,3) = 2, (1,2) = 3, (1,3) = 4, (2,3) = 5
+  const int lp1 = (leg >> 1) ? 5 : 0;                         // (0,1) / (2,3)
+  const int lp2 = (leg & 1) ? 4 : 1;                          // (0,2) / (1,3)
+  const int lp3 = (leg == 0 || leg == 3) ? 2 : 3;             // (0,3) / (1,2)
+  int mask = (o1 ? 1 << lp1 : 0) | (o2 ? 1 << lp2 : 0) | (o3 ? 1 << lp3 : 0) | (ob ? 64 << leg : 0);
+  return quad_or(mask);
 }
 
 __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
@@ -1776,8 +1790,12 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       float pft[3];  // the foot centre (calf frame offset), for the leg's bounding box
 #pragma unroll
       for (int i = 0; i < 3; ++i) pft[i] = pl[1][i] + Rl[1][3 * i] * foot[0] + Rl[1][3 * i + 1] * foot[1] + Rl[1][3 * i + 2] * foot[2];
-      self_collide(cfg, self_sc, leg, role, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), pw, vw, rr, R,
-                   S.pos, vb, th, Fs, wb);
+      const int mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), R, S.pos, th);
+      if (__any(mask != 0)) {
+        self_put(self_sc, leg, role, pw, vw, rr);
+        __syncthreads();
+        self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
+      }
 #pragma unroll
       for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
     }

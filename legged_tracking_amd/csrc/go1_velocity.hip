@@ -7,10 +7,11 @@
 //     clock (_step_contact_targets :844-923), DR (:714-717), terminations (:156-166), the CoRL reward
 //     terms and command sums (:281-318, go1_gym/envs/rewards/corl_rewards.py), reset_idx's state part
 //     (:168-257), observations (:320-509), the epilogue (:144-149) and the appended obs_history row.
-//   go1_vel_curriculum_kernel: workgroup 0 runs _resample_commands (:728-842) for the envs the step reset
-//     (RewardThresholdCurriculum.update, Curriculum.sample: go1_gym/envs/base/curriculum.py) and patches
-//     their observed commands, then the interval resample of the next step ahead of time; the other
-//     workgroups shift the history (obs_history[:, 70:] -> the new buffer).
+//   go1_vel_curriculum_kernel: workgroups 0 .. nblk - 1 run _resample_commands (:728-842) for the envs the
+//     step reset (RewardThresholdCurriculum.update, Curriculum.sample: go1_gym/envs/base/curriculum.py) and
+//     patch their observed commands, then the interval resample of the next step ahead of time, the per-env
+//     draws split over the workgroups; the other workgroups shift the history (obs_history[:, 70:] -> the
+//     new buffer) when the sliding window rewinds.
 // Lane layout of the step kernel as in go1_step.hip: 16 lanes per env = 4 legs x 4 roles, four envs per
 // one-wave block.  Post-physics arithmetic is f32 with contraction off in torch's operation order, the
 // transcendentals of the gait clock and the rewards via f64 (correctly rounded f32 but for rare double
@@ -817,7 +818,7 @@ __global__ void go1_vel_mask_kernel(const int32_t* __restrict__ ids, int n_ids, 
 __device__ unsigned long long g_vstamps[2][16];
 #define VSTAMP(ph, k, t0)                                                            \
   do {                                                                              \
-    if (threadIdx.x == 0) {                                                         \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                                      \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                    \
       atomicAdd(&g_vstamps[ph][k], t_ - t0);                                        \
       t0 = t_;                                                                      \
@@ -836,6 +837,8 @@ struct CArgs {
   double* cdf;          // (GO1_VEL_N_CATEGORIES, n_bins): numpy's normalised cdf of each curriculum
   int32_t* cdf_ok;      // [GO1_VEL_N_CATEGORIES]: cdf current for the weights
   int n_envs, env_id_offset;
+  int nblk;             // curriculum workgroups (blocks 0 .. nblk - 1; the rest shift the history)
+  int* done;            // their completion count (zero between launches)
   uint64_t seed;
   // B kind: the envs of maskB (reset_idx's resample)
   const uint8_t* maskB;
@@ -884,74 +887,127 @@ __device__ double np_pairwise_sum(const double* a, int n) {
 
 __device__ __forceinline__ float remainder1(float a) { return remainder_f(a, 1.0f); }
 
-// LDS of workgroup 0 (one allocation for the launch)
+// LDS of a curriculum workgroup (one allocation for the launch)
 struct CkShared {
   int hist[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // success count per (category, bin)
   double p[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // per category: the cdf the sampling searches
+  double w[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // the curriculum weights (committed by the last workgroup)
   int list[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // distinct (category, bin) success pairs
   int inc[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];   // +0.2 steps per weight cell
-  int sel[2][CK_SEL_CAP];                             // env_ids of the B and the A resample
-  int cnt[4];                                         // |sel B|, |sel A|, |list|, spare
+  int sel[2][CK_SEL_CAP];                             // env_ids of the B and the A resample, ascending
+  int wsum[2][CK_THREADS / 64];                       // per-wave selection counts of the ordered compaction
+  int cnt[4];                                         // |sel B|, |sel A|, |list|, last-workgroup flag
   int dirty[GO1_VEL_N_CATEGORIES];                    // weights changed in this phase
   int pvalid[GO1_VEL_N_CATEGORIES];                   // p holds the cdf of the current weights
+  int rec[GO1_VEL_N_CATEGORIES];                      // p recomputed in this launch (the cache to commit)
 };
 
-// The launch is latency-bound: a handful of envs per phase behind a chain of barrier-separated
-// sections, and a barrier waits out every memory access in flight.  So each section issues all the
-// memory reads it can at once: the prologue loads both phases' selection flags and the cached cdfs in
-// one round trip; a phase then costs the success counts (one round trip), the weight update (when some
-// env succeeded), the cdf of changed weights, and the sampling (commands and grid cells together).
+// The curriculum runs on K.nblk workgroups.  Everything _resample_commands computes for the batch as a whole --
+// the selections, the success counts, the weight update and the cdf -- is computed by every workgroup from the
+// same inputs (identical results, no cross-workgroup hand-off); the per-env work (the draws, the commands, the
+// observation patch) is split: the env at position i of a phase's ascending list belongs to workgroup
+// i % nblk.  The last workgroup to finish commits the weights and the cdf cache.  An env selected by both
+// phases is written by phase A only (its phase-B commands reach this step's observation; the state the
+// reference's second resample overwrites is never written twice by two workgroups), and phase A's success
+// check for it recomputes the category and bin phase B drew (a pure function of its draws and phase B's cdf).
+__device__ __forceinline__ bool selectedB(const CArgs& K, int e) { return K.maskB && K.maskB[e] != 0; }
+__device__ __forceinline__ bool selectedA(const CArgs& K, int e, int R) {
+  return K.doA && (K.st.episode_length[e] + 1) % R == 0;
+}
+
+// The launch is latency-bound: a handful of envs per phase behind a chain of barrier-separated sections, and
+// a barrier waits out every memory access in flight.  So each section issues all the memory reads it can at
+// once: the prologue loads both phases' selection flags, the cached cdfs and the weights in one round trip;
+// a phase then costs the success counts (one round trip), the weight update (when some env succeeded), the
+// cdf of changed weights, and the sampling (commands and grid cells together).
 __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
   const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
+  const int lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.hist[i] = 0;
   if (tid < 4) S.cnt[tid] = 0;
-  if (tid < GO1_VEL_N_CATEGORIES) S.dirty[tid] = 0;
-  __syncthreads();
-  // the cached cdfs (wave c: category c), whether or not a phase will need them
-  const int wv = tid >> 6, ln = tid & 63;
+  if (tid < GO1_VEL_N_CATEGORIES) { S.dirty[tid] = 0; S.rec[tid] = 0; }
+  // the cached cdfs (wave c) and the weights (wave 4 + c), whether or not a phase will need them
   double t[GO1_VEL_MAX_BINS / 64];
   int ok = 0;
-  if (wv < GO1_VEL_N_CATEGORIES) {
-    const double* g = K.cdf + (size_t)wv * nb;
-    ok = K.cdf_ok[wv];
+  if (wv < 2 * GO1_VEL_N_CATEGORIES) {
+    const int c = wv & 3;
+    const double* g = (wv < GO1_VEL_N_CATEGORIES ? K.cdf : K.st.curriculum_weights) + (size_t)c * nb;
+    if (wv < GO1_VEL_N_CATEGORIES) ok = K.cdf_ok[c];
 #pragma unroll
-    for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? g[ln + 64 * i] : 0.0;
+    for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = lane + 64 * i < nb ? g[lane + 64 * i] : 0.0;
   }
-  // env_ids of both phases, compacted (the flags of CK_BATCH envs per thread loaded before any is tested);
-  // beyond CK_SEL_CAP selected envs (a full reset) a phase scans the flags again instead
+  // env_ids of both phases, compacted in ascending order (per-wave ballots, then an exclusive scan of the
+  // wave counts; the flags of CK_BATCH envs per thread are loaded before any is tested); beyond CK_SEL_CAP
+  // selected envs (a full reset) a phase scans the flags again instead
+  int base[2] = {0, 0};
   for (int e0 = 0; e0 < n; e0 += CK_THREADS * CK_BATCH) {
     bool sb[CK_BATCH], sa[CK_BATCH];
 #pragma unroll
     for (int k = 0; k < CK_BATCH; ++k) {
       const int e = e0 + k * CK_THREADS + tid;
-      sb[k] = K.maskB && e < n && K.maskB[e] != 0;
-      sa[k] = K.doA && e < n && (K.st.episode_length[e] + 1) % R == 0;
+      sb[k] = e < n && selectedB(K, e);
+      sa[k] = e < n && selectedA(K, e, R);
     }
 #pragma unroll
     for (int k = 0; k < CK_BATCH; ++k) {
+      const uint64_t mb = __ballot(sb[k]), ma = __ballot(sa[k]);
+      if (lane == 0) { S.wsum[0][wv] = __popcll(mb); S.wsum[1][wv] = __popcll(ma); }
+      __syncthreads();
+      int ob = base[0], oa = base[1], tb = 0, ta = 0;
+      for (int w = 0; w < CK_THREADS / 64; ++w) {
+        const int cb = S.wsum[0][w], ca = S.wsum[1][w];
+        if (w < wv) { ob += cb; oa += ca; }
+        tb += cb; ta += ca;
+      }
+      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      const int e = e0 + k * CK_THREADS + tid;
       if (sb[k]) {
-        const int slot = atomicAdd(&S.cnt[0], 1);
-        if (slot < CK_SEL_CAP) S.sel[0][slot] = e0 + k * CK_THREADS + tid;
+        const int slot = ob + __popcll(mb & below);
+        if (slot < CK_SEL_CAP) S.sel[0][slot] = e;
       }
       if (sa[k]) {
-        const int slot = atomicAdd(&S.cnt[1], 1);
-        if (slot < CK_SEL_CAP) S.sel[1][slot] = e0 + k * CK_THREADS + tid;
+        const int slot = oa + __popcll(ma & below);
+        if (slot < CK_SEL_CAP) S.sel[1][slot] = e;
       }
+      base[0] += tb;
+      base[1] += ta;
+      __syncthreads();  // wsum is rewritten by the next batch
     }
   }
-  if (wv < GO1_VEL_N_CATEGORIES) {
-    double* p = S.p + (size_t)wv * GO1_VEL_MAX_BINS;
+  if (tid == 0) { S.cnt[0] = base[0]; S.cnt[1] = base[1]; }
+  if (wv < 2 * GO1_VEL_N_CATEGORIES) {
+    const int c = wv & 3;
+    double* dst = (wv < GO1_VEL_N_CATEGORIES ? S.p : S.w) + (size_t)c * GO1_VEL_MAX_BINS;
 #pragma unroll
     for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
-      if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
-    if (ln == 0) S.pvalid[wv] = ok;
+      if (lane + 64 * i < nb) dst[lane + 64 * i] = t[i];
+    if (lane == 0 && wv < GO1_VEL_N_CATEGORIES) S.pvalid[c] = ok;
   }
   __syncthreads();
+}
+
+// searchsorted(cdf, u, side='right') clipped to the last bin (numpy's choice)
+__device__ __forceinline__ int cdf_search(const double* cdf, int nb, double u) {
+  int lo = 0, hi = nb;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
+  }
+  return min(lo, nb - 1);
+}
+
+// the category draw of a resample: category c when 0.25 c <= u < 0.25 (c + 1) (as f32), -1 otherwise
+__device__ __forceinline__ int draw_category(float uc) {
+  int cat = -1;
+  for (int c = 0; c < GO1_VEL_N_CATEGORIES; ++c)
+    if ((float)(0.25 * c) <= uc && uc < (float)(0.25 * (c + 1))) cat = c;
+  return cat;
 }
 
 // One resample (_resample_commands :728-842) of kind B (mask) or A (interval), by the whole workgroup.
 __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S) {
   const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
+  const int blk = blockIdx.x, nblk = K.nblk;
   const go1_vel_state& st = K.st;
   const float* U = kindB ? K.UB : K.UA;
   const double* UD = kindB ? K.UDB : K.UDA;
@@ -960,20 +1016,18 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   const int dch = kindB ? GO1_VEL_D_CHOICE_B : GO1_VEL_D_CHOICE_A;
   const int NC = v->n_terms + GO1_VEL_SUM_EXTRA;
   const int ph = kindB ? 0 : 1;
-  (void)ph;
 #ifdef GO1_VEL_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-  auto selected = [&](int e) {
-    return kindB ? K.maskB[e] != 0 : ((st.episode_length[e] + 1) % R == 0);
-  };
+  auto selected = [&](int e) { return kindB ? selectedB(K, e) : selectedA(K, e, R); };
   const int count = S.cnt[ph];
   const int* sel = S.sel[ph];
   VSTAMP(ph, 0, t0);
   if (count == 0) return;  // len(env_ids) == 0 (:730): nothing, not even the time-out rebinding
   VSTAMP(ph, 15, t0);
+  const bool listed = count <= CK_SEL_CAP;
   auto for_selected = [&](auto&& fn) {
-    if (count <= CK_SEL_CAP) {
+    if (listed) {
       for (int i = tid; i < count; i += CK_THREADS) fn(sel[i]);
     } else {
       for (int e = tid; e < n; e += CK_THREADS)
@@ -983,12 +1037,29 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   // ---- RewardThresholdCurriculum.update per old category (:736-757, curriculum.py:135-154): success
   // counts per (category, bin), and the list of the (category, bin) pairs that have any
   for_selected([&](int e) {
-    const int cat = st.command_categories[e];
-    if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES || v->n_task == 0) return;
+    if (v->n_task == 0) return;
+    int cat, b;
     bool ok = true;
-    for (int k = 0; k < v->n_task; ++k)
-      ok = ok && (st.command_sums[(size_t)e * NC + v->task_slot[k]] / v->curriculum_ep_len > v->task_threshold[k]);
-    const int b = st.command_bins[e];
+    if (!kindB && selectedB(K, e)) {
+      // phase B resampled this env: its sums are zero and its category / bin are phase B's draws, recomputed
+      // here from phase B's uniforms and cdf (S.p still holds it: phase A's cdf comes after these counts)
+      const Rng rng = {K.UB, K.seed, K.stepB, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
+      const RngD rngd = {K.UDB, K.seed, K.stepB, e, e + K.env_id_offset};
+      cat = draw_category(rng(GO1_VEL_U_CAT_B));
+      if (cat >= 0) {
+        b = cdf_search(S.p + (size_t)cat * GO1_VEL_MAX_BINS, nb, rngd(GO1_VEL_D_CHOICE_B));
+      } else {
+        cat = st.command_categories[e];
+        b = st.command_bins[e];
+      }
+      for (int k = 0; k < v->n_task; ++k) ok = ok && (0.0f / v->curriculum_ep_len > v->task_threshold[k]);
+    } else {
+      cat = st.command_categories[e];
+      b = st.command_bins[e];
+      for (int k = 0; k < v->n_task; ++k)
+        ok = ok && (st.command_sums[(size_t)e * NC + v->task_slot[k]] / v->curriculum_ep_len > v->task_threshold[k]);
+    }
+    if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES) return;
     if (ok && b >= 0 && b < nb) {
       if (atomicAdd(&S.hist[cat * nb + b], 1) == 0) {
         const int slot = atomicAdd(&S.cnt[2], 1);
@@ -996,8 +1067,8 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
       }
     }
   });
-  if (kindB && K.extras_time_outs)
-    for (int e = tid; e < n; e += CK_THREADS) K.extras_time_outs[e] = K.time_out[e];
+  if (kindB && K.extras_time_outs)  // this workgroup's share of the rebinding
+    for (int e = blk * CK_THREADS + tid; e < n; e += nblk * CK_THREADS) K.extras_time_outs[e] = K.time_out[e];
   __syncthreads();
   VSTAMP(ph, 1, t0);
   const int n_list = S.cnt[2];
@@ -1025,28 +1096,24 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
     for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
       const int k = S.inc[i];
       if (k > 0) {
-        double w = st.curriculum_weights[i];
+        const int c = i / nb;
+        double w = S.w[(size_t)c * GO1_VEL_MAX_BINS + (i - c * nb)];
         for (int t = 0; t < k; ++t) w = fmin(fmax(w + 0.2, 0.0), 1.0);
-        st.curriculum_weights[i] = w;
-        S.dirty[i / nb] = 1;
+        S.w[(size_t)c * GO1_VEL_MAX_BINS + (i - c * nb)] = w;
+        S.dirty[c] = 1;
       }
     }
     __syncthreads();
   }
   VSTAMP(ph, 2, t0);
   // ---- numpy rng.choice(p = w / w.sum()): cdf = cumsum(p) / cdf[-1], wave c for category c, in LDS
-  // (S.p), recomputed where the weights changed (or no cdf is cached), also into the handle's cache
+  // (S.p), recomputed where the weights changed (or no cdf is cached)
   {
     const int wv = tid >> 6, ln = tid & 63;
     if (wv < GO1_VEL_N_CATEGORIES && (S.dirty[wv] || !S.pvalid[wv])) {
       double* p = S.p + (size_t)wv * GO1_VEL_MAX_BINS;
-      const double* w = st.curriculum_weights + (size_t)wv * nb;
-      double t[GO1_VEL_MAX_BINS / 64];  // all of the lane's loads in flight before the LDS stores
-#pragma unroll
-      for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = ln + 64 * i < nb ? w[ln + 64 * i] : 0.0;
-#pragma unroll
-      for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
-        if (ln + 64 * i < nb) p[ln + 64 * i] = t[i];
+      const double* w = S.w + (size_t)wv * GO1_VEL_MAX_BINS;
+      for (int j = ln; j < nb; j += 64) p[j] = w[j];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1076,61 +1143,53 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const double last = p[nb - 1];
-      for (int j = ln; j < nb; j += 64) {
-        const double c = p[j] / last;
-        p[j] = c;
-        K.cdf[(size_t)wv * nb + j] = c;
-      }
+      for (int j = ln; j < nb; j += 64) p[j] = p[j] / last;
       if (ln == 0) {
-        K.cdf_ok[wv] = 1;
         S.pvalid[wv] = 1;
+        S.rec[wv] = 1;
         S.dirty[wv] = 0;
       }
 #ifdef GO1_VEL_STAMPS
-      if (ln == 0) atomicAdd(&g_vstamps[kindB ? 0 : 1][14], 1ull);
+      if (ln == 0 && blk == 0) atomicAdd(&g_vstamps[kindB ? 0 : 1][14], 1ull);
 #endif
     }
   }
   __syncthreads();
   VSTAMP(ph, 3, t0);
-  // ---- new category, cell and command per env (:759-842), 16 lanes per env: lane k < 15 draws and
-  // finishes command k (the gait rules and binary phases act per command; only the small-command rule
-  // pairs commands 0 and 1), lane 15 draws the choice and searches the cdf.  One Philox evaluation per
-  // lane instead of ~30 in sequence on one thread; the env's old commands are loaded before the search,
-  // so they and the grid cells share one memory round trip.
+  // ---- new category, cell and command per env (:759-842), this workgroup's envs (list positions
+  // blk, blk + nblk, ...; env ids e % nblk == blk beyond the list capacity), 16 lanes per env: lane k < 15
+  // draws and finishes command k (the gait rules and binary phases act per command; only the small-command
+  // rule pairs commands 0 and 1), lane 15 draws the choice and searches the cdf.  One Philox evaluation per
+  // lane instead of ~30 in sequence on one thread; the env's old commands are loaded before the search, so
+  // they and the grid cells share one memory round trip.
   {
     const int sub = tid & 15, grp = tid >> 4;
-    const bool listed = count <= CK_SEL_CAP;
-    const int n_iter = listed ? count : n;
-    for (int i0 = 0; i0 < n_iter; i0 += CK_THREADS / 16) {
+    const int n_own = listed ? (count > blk ? (count - blk + nblk - 1) / nblk : 0)
+                             : (n > blk ? (n - blk + nblk - 1) / nblk : 0);
+    for (int i0 = 0; i0 < n_own; i0 += CK_THREADS / 16) {
       const int i = i0 + grp;
       int e = -1;
-      if (listed) {
-        if (i < count) e = sel[i];
-      } else if (i < n && selected(i)) {
-        e = i;
+      if (i < n_own) {
+        const int pos = blk + i * nblk;
+        if (listed) e = sel[pos];
+        else if (selected(pos)) e = pos;
       }
       if (e < 0) continue;  // uniform over the env's 16 lanes
+      // an env phase A resamples again: phase A writes its state, phase B only its observed commands
+      const bool state_out = !(kindB && selectedA(K, e, R));
       const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
       const RngD rngd = {UD, K.seed, step, e, e + K.env_id_offset};
       float cmd = sub < GO1_VEL_NUM_COMMANDS ? st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] : 0.0f;
-      const float uc = rng(ucat);
-      int cat = -1;
-      for (int c = 0; c < GO1_VEL_N_CATEGORIES; ++c)
-        if ((float)(0.25 * c) <= uc && uc < (float)(0.25 * (c + 1))) cat = c;
+      const int cat = draw_category(rng(ucat));
       if (cat >= 0) {
         const double u = rngd(sub < GO1_VEL_NUM_COMMANDS ? dch + 1 + sub : dch);
         int idx = 0;
         if (sub == 15) {
-          const double* cdf = S.p + (size_t)cat * GO1_VEL_MAX_BINS;
-          int lo = 0, hi = nb;  // searchsorted(cdf, u, side='right'): first j with cdf[j] > u
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
+          idx = cdf_search(S.p + (size_t)cat * GO1_VEL_MAX_BINS, nb, u);
+          if (state_out) {
+            st.command_bins[e] = idx;
+            st.command_categories[e] = cat;
           }
-          idx = min(lo, nb - 1);
-          st.command_bins[e] = idx;
-          st.command_categories[e] = cat;
         }
         idx = __shfl(idx, 15, 16);
         if (sub < GO1_VEL_NUM_COMMANDS) {
@@ -1150,8 +1209,10 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
         const float keep = norm2_f(c0, c1) > 0.2f ? 1.0f : 0.0f;
         if (sub < 2) cmd = cmd * keep;
       }
-      if (sub < GO1_VEL_NUM_COMMANDS) st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] = cmd;
-      for (int k = sub; k < NC; k += 16) st.command_sums[(size_t)e * NC + k] = 0.0f;
+      if (state_out) {
+        if (sub < GO1_VEL_NUM_COMMANDS) st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] = cmd;
+        for (int k = sub; k < NC; k += 16) st.command_sums[(size_t)e * NC + k] = 0.0f;
+      }
       if (kindB && K.obs && sub < GO1_VEL_NUM_COMMANDS) {  // this step's observation of the resampled commands (:339)
         const float clip = v->clip_obs;
         float val = cmd * v->cmd_scale[sub];
@@ -1167,6 +1228,29 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   if (tid == 0) S.cnt[2] = 0;
   __syncthreads();
   VSTAMP(ph, 4, t0);
+}
+
+// The last curriculum workgroup to finish writes the weights and the recomputed cdfs (every workgroup holds
+// the same values; all of them have read the old ones by then).  Release: every workgroup's reads and writes
+// precede its ticket; acquire: the last one sees every other workgroup done before it writes.
+__device__ void resample_commit(VCfg* v, const CArgs& K, CkShared& S) {
+  const int tid = threadIdx.x, nb = v->n_bins;
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int old = __hip_atomic_fetch_add(K.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S.cnt[3] = old == K.nblk - 1;
+    if (S.cnt[3]) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!S.cnt[3]) return;
+  for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
+    const int c = i / nb, j = i - c * nb;
+    K.st.curriculum_weights[i] = S.w[(size_t)c * GO1_VEL_MAX_BINS + j];
+    if (S.rec[c]) K.cdf[i] = S.p[(size_t)c * GO1_VEL_MAX_BINS + j];
+  }
+  if (tid < GO1_VEL_N_CATEGORIES && S.rec[tid]) K.cdf_ok[tid] = 1;
+  if (tid == 0) *K.done = 0;  // the next launch's count (stream order)
 }
 
 // HistoryWrapper.step's shift (history_wrapper.py:22): new[:, :W - 70] = old[:, 70:], by workgroups 1.. of
@@ -1232,14 +1316,15 @@ __device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
 __global__ __launch_bounds__(CK_THREADS) void go1_vel_curriculum_kernel(const go1_vel_config* __restrict__ v_gen,
                                                                         CArgs K) {
   VCfg* __restrict__ v = (VCfg*)v_gen;
-  if (blockIdx.x > 0) {
-    hist_shift(K, (size_t)(blockIdx.x - 1) * CK_THREADS + threadIdx.x, (size_t)(gridDim.x - 1) * CK_THREADS);
+  if ((int)blockIdx.x >= K.nblk) {
+    hist_shift(K, (size_t)(blockIdx.x - K.nblk) * CK_THREADS + threadIdx.x, (size_t)(gridDim.x - K.nblk) * CK_THREADS);
     return;
   }
   __shared__ CkShared S;
   resample_prologue(v, K, S);
   if (K.maskB) resample_phase(v, K, true, S);
   if (K.doA) resample_phase(v, K, false, S);
+  resample_commit(v, K, S);
 }
 
 // =====================================================================
@@ -1267,6 +1352,7 @@ struct go1_vel_handle {
   uint8_t* d_mask = nullptr;  // reset_idx's env mask (stream-ordered reuse)
   int32_t* d_adj_ptr = nullptr;  // neighbourhood table of the curriculum update (CSR over the bins)
   int32_t* d_adj_idx = nullptr;
+  int32_t* d_done = nullptr;     // completion count of the curriculum workgroups (zero between launches)
   go1_vel_state st;
   const float* env_origins = nullptr;
   bool bound = false;
@@ -1283,6 +1369,9 @@ static int vfail(int code, const std::string& msg) {
     if (_e != hipSuccess) return vfail(GO1_E_HIP, std::string(#x ": ") + hipGetErrorString(_e)); \
   } while (0)
 
+// curriculum workgroups: the per-env sampling splits over them (a 4096-env resample: 128 envs each)
+static int curriculum_blocks(int n) { return std::max(1, std::min(32, n / 128)); }
+
 static CArgs curriculum_args(go1_vel_handle* h) {
   CArgs K;
   memset(&K, 0, sizeof(K));
@@ -1294,6 +1383,8 @@ static CArgs curriculum_args(go1_vel_handle* h) {
   K.cdf_ok = h->d_cdf_ok;
   K.n_envs = h->cfg.n_envs;
   K.env_id_offset = h->cfg.env_id_offset;
+  K.nblk = curriculum_blocks(h->cfg.n_envs);
+  K.done = h->d_done;
   return K;
 }
 
@@ -1335,7 +1426,7 @@ int go1_vel_create(const go1_config* cfg, const go1_vel_config* vel, const doubl
   if (hipMalloc(&h->d_cfg, sizeof(go1_config)) != hipSuccess || hipMalloc(&h->d_vcfg, sizeof(go1_vel_config)) != hipSuccess ||
       hipMalloc(&h->d_grid, gsz) != hipSuccess || hipMalloc(&h->d_cdf, csz) != hipSuccess ||
       hipMalloc(&h->d_cdf_ok, GO1_VEL_N_CATEGORIES * sizeof(int32_t)) != hipSuccess ||
-      hipMalloc(&h->d_mask, cfg->n_envs) != hipSuccess) {
+      hipMalloc(&h->d_mask, cfg->n_envs) != hipSuccess || hipMalloc(&h->d_done, sizeof(int32_t)) != hipSuccess) {
     go1_vel_destroy(h);
     return vfail(GO1_E_HIP, "go1_vel_create: hipMalloc failed");
   }
@@ -1365,6 +1456,7 @@ int go1_vel_create(const go1_config* cfg, const go1_vel_config* vel, const doubl
     VHIP_TRY(hipMemcpy(h->d_adj_idx, idx.data(), idx.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }
   VHIP_TRY(hipMemset(h->d_cdf_ok, 0, GO1_VEL_N_CATEGORIES * sizeof(int32_t)));
+  VHIP_TRY(hipMemset(h->d_done, 0, sizeof(int32_t)));
   *out = h;
   return GO1_OK;
 }
@@ -1473,12 +1565,13 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   C.time_out = a->time_out;
   C.extras_time_outs = a->extras_time_outs;
   C.obs = a->obs;
-  // workgroups 1..: the history shift, one per remaining CU (the launch's LDS allows one workgroup per CU),
-  // four 16-byte chunks in flight per lane; fewer for small batches
+  // workgroups nblk..: the history shift, one per remaining CU (the launch's LDS allows one workgroup per
+  // CU), four 16-byte chunks in flight per lane; fewer for small batches
   const size_t chunks = (size_t)n * (size_t)((K.hist_w - GO1_VEL_NUM_OBS) / 4 + 64);
   const int shift_blocks =
-      C.hist_in ? (int)std::min<size_t>(255, std::max<size_t>(1, (chunks + 4 * CK_THREADS - 1) / (4 * CK_THREADS))) : 0;
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1 + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
+      C.hist_in ? (int)std::min<size_t>(256 - C.nblk, std::max<size_t>(1, (chunks + 4 * CK_THREADS - 1) / (4 * CK_THREADS)))
+                : 0;
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
   VHIP_TRY(hipGetLastError());
   return GO1_OK;
 }
@@ -1502,7 +1595,7 @@ int go1_vel_resample(go1_vel_handle* h, const uint8_t* mask, const float* unifor
     C.UDA = uniforms_f64;
     C.stepA = rng_step;
   }
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(1), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C);
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C);
   VHIP_TRY(hipGetLastError());
   return GO1_OK;
 }
@@ -1531,6 +1624,7 @@ int go1_vel_reset_idx(go1_vel_handle* h, const int32_t* ids, int32_t n_ids, cons
 
 int go1_vel_destroy(go1_vel_handle* h) {
   if (!h) return GO1_OK;
+  if (h->d_done) (void)hipFree(h->d_done);
   if (h->d_cfg) (void)hipFree(h->d_cfg);
   if (h->d_vcfg) (void)hipFree(h->d_vcfg);
   if (h->d_grid) (void)hipFree(h->d_grid);

@@ -155,7 +155,7 @@ def test_vel_step_replays_reference_fixture(name):
         if cnt:
             rows = out["log"][:cnt]
             ne = len(names) + 1
-            assert (rows[:, ne] == 7).all()
+            assert (np.ascontiguousarray(rows[:, ne]).view(np.int32) == 7).all()  # the tag's int32 bits
             rows = rows[np.argsort(rows[:, ne + 1])]
             np.testing.assert_array_equal(rows[:, ne + 1], np.nonzero(d[f"s{t}/reset"])[0])
             for i, k in enumerate(names + ["total"]):
