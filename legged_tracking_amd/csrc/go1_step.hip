@@ -258,7 +258,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int i = 0; i < 4; ++i) P.quat[i] = st.root[(size_t)e * 13 + 3 + i];
   }
   Terr T = {nullptr, CI(hf_nx), CI(hf_ny), CI(horizontal_scale), nullptr, 0, 0};
-  __shared__ float2 s_patch[SEPB][PSZX * PSZY];
+  // +8 float2 per env: the four envs' patches start 16 banks apart (unpadded they start on the same bank, and
+  // the legs sit at similar cells of their env-centred patches: the corner reads of different envs collided)
+  __shared__ float2 s_patch[SEPB][PSZX * PSZY + 8];
   __shared__ float s_phys[(LDS_FLOATS + 63) / 64 * 64];
   __shared__ __attribute__((aligned(16))) float s_self[SEPB][SELF_ENV_FLOATS];  // self-collision scratch
   // Block = one wave, so LDS needs no barrier here (a wave's LDS operations execute in

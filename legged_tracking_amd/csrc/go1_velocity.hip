@@ -900,6 +900,7 @@ struct CkShared {
   int dirty[GO1_VEL_N_CATEGORIES];                    // weights changed in this phase
   int pvalid[GO1_VEL_N_CATEGORIES];                   // p holds the cdf of the current weights
   int rec[GO1_VEL_N_CATEGORIES];                      // p recomputed in this launch (the cache to commit)
+  int wchg;                                           // some weight changed in this launch
 };
 
 // The curriculum runs on K.nblk workgroups.  Everything _resample_commands computes for the batch as a whole --
@@ -922,10 +923,14 @@ __device__ __forceinline__ bool selectedA(const CArgs& K, int e, int R) {
 // cdf of changed weights, and the sampling (commands and grid cells together).
 __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
   const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
+#ifdef GO1_VEL_STAMPS
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
   const int lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.hist[i] = 0;
   if (tid < 4) S.cnt[tid] = 0;
   if (tid < GO1_VEL_N_CATEGORIES) { S.dirty[tid] = 0; S.rec[tid] = 0; }
+  if (tid == 0) S.wchg = 0;
   // the cached cdfs (wave c) and the weights (wave 4 + c), whether or not a phase will need them
   double t[GO1_VEL_MAX_BINS / 64];
   int ok = 0;
@@ -933,46 +938,61 @@ __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
     const int c = wv & 3;
     const double* g = (wv < GO1_VEL_N_CATEGORIES ? K.cdf : K.st.curriculum_weights) + (size_t)c * nb;
     if (wv < GO1_VEL_N_CATEGORIES) ok = K.cdf_ok[c];
+    // unconditional loads (index clamped): a load under a condition makes hipcc wait for it right away
 #pragma unroll
-    for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = lane + 64 * i < nb ? g[lane + 64 * i] : 0.0;
+    for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = g[min(lane + 64 * i, nb - 1)];
   }
-  // env_ids of both phases, compacted in ascending order (per-wave ballots, then an exclusive scan of the
-  // wave counts; the flags of CK_BATCH envs per thread are loaded before any is tested); beyond CK_SEL_CAP
-  // selected envs (a full reset) a phase scans the flags again instead
+  // env_ids of both phases, compacted in ascending order: thread t takes a contiguous run of envs (its flags
+  // loaded before any is tested), one block-wide exclusive scan of the (B, A) counts places each run; beyond
+  // CK_SEL_CAP selected envs (a full reset) a phase scans the flags again instead
   int base[2] = {0, 0};
   for (int e0 = 0; e0 < n; e0 += CK_THREADS * CK_BATCH) {
+    const int span = min(CK_THREADS * CK_BATCH, n - e0), per = (span + CK_THREADS - 1) / CK_THREADS;
+    const int eb = e0 + tid * per;
     bool sb[CK_BATCH], sa[CK_BATCH];
+    int v = 0;
+    // the flags of the run: unconditional loads at clamped indices (no wait per load), then the tests
+    const uint8_t* mB = K.maskB ? K.maskB : reinterpret_cast<const uint8_t*>(K.st.episode_length);
+    uint8_t fb[CK_BATCH];
+    int el[CK_BATCH];
 #pragma unroll
     for (int k = 0; k < CK_BATCH; ++k) {
-      const int e = e0 + k * CK_THREADS + tid;
-      sb[k] = e < n && selectedB(K, e);
-      sa[k] = e < n && selectedA(K, e, R);
+      const int ec = min(eb + k, n - 1);
+      fb[k] = mB[ec];
+      el[k] = K.st.episode_length[ec];
     }
 #pragma unroll
     for (int k = 0; k < CK_BATCH; ++k) {
-      const uint64_t mb = __ballot(sb[k]), ma = __ballot(sa[k]);
-      if (lane == 0) { S.wsum[0][wv] = __popcll(mb); S.wsum[1][wv] = __popcll(ma); }
-      __syncthreads();
-      int ob = base[0], oa = base[1], tb = 0, ta = 0;
-      for (int w = 0; w < CK_THREADS / 64; ++w) {
-        const int cb = S.wsum[0][w], ca = S.wsum[1][w];
-        if (w < wv) { ob += cb; oa += ca; }
-        tb += cb; ta += ca;
-      }
-      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-      const int e = e0 + k * CK_THREADS + tid;
-      if (sb[k]) {
-        const int slot = ob + __popcll(mb & below);
-        if (slot < CK_SEL_CAP) S.sel[0][slot] = e;
-      }
-      if (sa[k]) {
-        const int slot = oa + __popcll(ma & below);
-        if (slot < CK_SEL_CAP) S.sel[1][slot] = e;
-      }
-      base[0] += tb;
-      base[1] += ta;
-      __syncthreads();  // wsum is rewritten by the next batch
+      const int e = eb + k;
+      const bool ok = k < per && e < e0 + span;
+      sb[k] = ok && K.maskB != nullptr && fb[k] != 0;
+      sa[k] = ok && K.doA && (el[k] + 1) % R == 0;
+      v += (sb[k] ? 1 : 0) + (sa[k] ? 1 << 16 : 0);
     }
+    int inc = v;  // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o);
+      inc += lane >= o ? u : 0;
+    }
+    if (lane == 63) S.wsum[0][wv] = inc;
+    __syncthreads();
+    int pre = 0, tot = 0;
+    for (int w = 0; w < CK_THREADS / 64; ++w) {
+      const int c = S.wsum[0][w];
+      pre += w < wv ? c : 0;
+      tot += c;
+    }
+    const int ex = pre + inc - v;
+    int ob = base[0] + (ex & 0xffff), oa = base[1] + (ex >> 16);
+#pragma unroll
+    for (int k = 0; k < CK_BATCH; ++k) {
+      if (sb[k]) { if (ob < CK_SEL_CAP) S.sel[0][ob] = eb + k; ++ob; }
+      if (sa[k]) { if (oa < CK_SEL_CAP) S.sel[1][oa] = eb + k; ++oa; }
+    }
+    base[0] += tot & 0xffff;
+    base[1] += tot >> 16;
+    __syncthreads();  // wsum is rewritten by the next pass
   }
   if (tid == 0) { S.cnt[0] = base[0]; S.cnt[1] = base[1]; }
   if (wv < 2 * GO1_VEL_N_CATEGORIES) {
@@ -984,6 +1004,7 @@ __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
     if (lane == 0 && wv < GO1_VEL_N_CATEGORIES) S.pvalid[c] = ok;
   }
   __syncthreads();
+  VSTAMP(0, 10, t0);
 }
 
 // searchsorted(cdf, u, side='right') clipped to the last bin (numpy's choice)
@@ -1056,8 +1077,12 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
     } else {
       cat = st.command_categories[e];
       b = st.command_bins[e];
-      for (int k = 0; k < v->n_task; ++k)
-        ok = ok && (st.command_sums[(size_t)e * NC + v->task_slot[k]] / v->curriculum_ep_len > v->task_threshold[k]);
+      float sm[4];  // every task's sum loaded (slot clamped) before any is tested
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sm[k] = st.command_sums[(size_t)e * NC + v->task_slot[min(k, v->n_task - 1)]];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < v->n_task) ok = ok && (sm[k] / v->curriculum_ep_len > v->task_threshold[k]);
     }
     if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES) return;
     if (ok && b >= 0 && b < nb) {
@@ -1101,6 +1126,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
         for (int t = 0; t < k; ++t) w = fmin(fmax(w + 0.2, 0.0), 1.0);
         S.w[(size_t)c * GO1_VEL_MAX_BINS + (i - c * nb)] = w;
         S.dirty[c] = 1;
+        S.wchg = 1;
       }
     }
     __syncthreads();
@@ -1179,7 +1205,9 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
       const bool state_out = !(kindB && selectedA(K, e, R));
       const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
       const RngD rngd = {UD, K.seed, step, e, e + K.env_id_offset};
-      float cmd = sub < GO1_VEL_NUM_COMMANDS ? st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + sub] : 0.0f;
+      const int subc = min(sub, GO1_VEL_NUM_COMMANDS - 1);  // clamped: unconditional loads
+      float cmd = st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + subc];
+      if (sub >= GO1_VEL_NUM_COMMANDS) cmd = 0.0f;
       const int cat = draw_category(rng(ucat));
       if (cat >= 0) {
         const double u = rngd(sub < GO1_VEL_NUM_COMMANDS ? dch + 1 + sub : dch);
@@ -1192,8 +1220,8 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
           }
         }
         idx = __shfl(idx, 15, 16);
+        const double cen = K.grid[(size_t)subc * nb + idx], half = v->bin_sizes[subc] / 2.0;
         if (sub < GO1_VEL_NUM_COMMANDS) {
-          const double cen = K.grid[(size_t)sub * nb + idx], half = v->bin_sizes[sub] / 2.0;
           const double l = cen + half, h = cen - half;
           cmd = (float)(l + (h - l) * u);
           if (v->gaitwise_curricula && sub >= 5 && sub < 8) {
@@ -1236,6 +1264,12 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
 __device__ void resample_commit(VCfg* v, const CArgs& K, CkShared& S) {
   const int tid = threadIdx.x, nb = v->n_bins;
   __syncthreads();
+  // every workgroup takes the same decisions: with no weight changed and no cdf recomputed there is nothing
+  // to commit, and none of them takes a ticket
+  if (!S.wchg && !S.rec[0] && !S.rec[1] && !S.rec[2] && !S.rec[3]) return;
+#ifdef GO1_VEL_STAMPS
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const int old = __hip_atomic_fetch_add(K.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1246,11 +1280,14 @@ __device__ void resample_commit(VCfg* v, const CArgs& K, CkShared& S) {
   if (!S.cnt[3]) return;
   for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
     const int c = i / nb, j = i - c * nb;
-    K.st.curriculum_weights[i] = S.w[(size_t)c * GO1_VEL_MAX_BINS + j];
-    if (S.rec[c]) K.cdf[i] = S.p[(size_t)c * GO1_VEL_MAX_BINS + j];
+    if (S.rec[c]) {  // a category whose weights changed had its cdf recomputed
+      K.st.curriculum_weights[i] = S.w[(size_t)c * GO1_VEL_MAX_BINS + j];
+      K.cdf[i] = S.p[(size_t)c * GO1_VEL_MAX_BINS + j];
+    }
   }
   if (tid < GO1_VEL_N_CATEGORIES && S.rec[tid]) K.cdf_ok[tid] = 1;
   if (tid == 0) *K.done = 0;  // the next launch's count (stream order)
+  VSTAMP(0, 11, t0);
 }
 
 // HistoryWrapper.step's shift (history_wrapper.py:22): new[:, :W - 70] = old[:, 70:], by workgroups 1.. of

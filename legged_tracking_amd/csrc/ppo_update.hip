@@ -120,7 +120,10 @@ __device__ __forceinline__ float expm1_neg(float z) {
   const float big = __builtin_amdgcn_exp2f(z * 1.44269504f) - 1.0f;
   return z >= -0.5f ? small : big;
 }
-__device__ __forceinline__ float elu(float z) { return z > 0.0f ? z : expm1_neg(z); }
+__device__ __forceinline__ float elu(float z) {
+  const float e = expm1_neg(fminf(z, 0.0f));  // unconditionally: a select, not a branch per value
+  return z > 0.0f ? z : e;
+}
 __device__ __forceinline__ float delu_from_out(float a) { return a > 0.0f ? 1.0f : a + 1.0f; }
 
 // ------------------------------------------------------------------ xw: C = act(A W^T + b) / (A W^T) * ELU'
@@ -188,8 +191,8 @@ __global__ __launch_bounds__(256, PPO_XW_LB) void xw_kernel(XwLaunch L) {
   const XwProb& P = (L.nprob > 1 && t >= L.p[1].tile0) ? L.p[1] : L.p[0];
   const int lt = t - P.tile0, mt = lt / P.tiles_n, nt = lt - mt * P.tiles_n;
   const int wm = w & 1, wn = w >> 1, M = L.M;
-  const int eA = scale_exp(P.amax2 ? max(*P.amax, *P.amax2) : *P.amax), eW = *P.wexp;
-  const float sa = pow2f(eA);
+  int eA = 0, eW = 0;  // the operands' scale exponents: read after the first group's loads are issued
+  float sa = 1.0f;
   // staging: per instruction 8 rows x 32 k; lane -> row (lane >> 1) & 7, float4 k4 = 2 (lane >> 4) + (lane & 1)
   const int srow = (lane >> 1) & 7, k4 = ((lane >> 4) << 1) | (lane & 1);
   const int mrow0 = mt * TB + w * 32 + srow;  // row of instruction it: mrow0 + 8 it
@@ -233,6 +236,12 @@ __global__ __launch_bounds__(256, PPO_XW_LB) void xw_kernel(XwLaunch L) {
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = (f4_t){0.0f, 0.0f, 0.0f, 0.0f};
+  // the F epilogue's bias, loaded now: a load at the epilogue would be waited for right there
+  f4_t bias4[4];
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn)
+    bias4[tn] = EPI != EPI_DELU ? *reinterpret_cast<const f4_t*>(P.bias + nt * TB + wn * 64 + tn * 16 + 4 * q)
+                                : (f4_t){0.0f, 0.0f, 0.0f, 0.0f};
   const int G = P.G;
   auto loadw = [&](int g, h8_t (&wh)[4], h8_t (&wl)[4]) {
     const h8_t* wg = wrow + (size_t)g * 8 * npad;
@@ -252,12 +261,18 @@ __global__ __launch_bounds__(256, PPO_XW_LB) void xw_kernel(XwLaunch L) {
     }
   };
   load(0);
-  store(0);
 #if PPO_XW_V == 1
   // weight fragments and the A tile of the next group in flight across this group's MFMAs: every load is
   // unconditional (the last group re-loads itself), the LDS store of the staged group follows the MFMAs
   h8_t wh0[4], wl0[4], wh1[4], wl1[4];
   loadw(0, wh0, wl0);
+#endif
+  // the max |x| records (one dependent round trip) after the first group's loads are in flight
+  eA = scale_exp(P.amax2 ? max(*P.amax, *P.amax2) : *P.amax);
+  eW = *P.wexp;
+  sa = pow2f(eA);
+  store(0);
+#if PPO_XW_V == 1
   __syncthreads();
   auto body = [&](int g, int cur, h8_t (&wh)[4], h8_t (&wl)[4], h8_t (&nwh)[4], h8_t (&nwl)[4]) {
     const int gn = min(g + 1, G - 1);
@@ -303,11 +318,9 @@ __global__ __launch_bounds__(256, PPO_XW_LB) void xw_kernel(XwLaunch L) {
   __syncthreads();
   for (int g = 0; g < G; ++g) {
     const int cur = g & 1;
-    const bool more = g + 1 < G;
-    if (more) {
-      loadw2(g + 1);
-      load(g + 1);
-    }
+    const int gn = min(g + 1, G - 1);  // unconditional: the last group re-loads itself into the idle buffer
+    loadw2(gn);
+    load(gn);
     h8_t wh[4], wl[4];
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) {
@@ -315,10 +328,8 @@ __global__ __launch_bounds__(256, PPO_XW_LB) void xw_kernel(XwLaunch L) {
       wl[tn] = sW[cur][1][q][wn * 64 + tn * 16 + c];
     }
     mma(cur, wh, wl);
-    if (more) {
-      store(cur ^ 1);
-      storew2(cur ^ 1);
-    }
+    store(cur ^ 1);
+    storew2(cur ^ 1);
     __syncthreads();
   }
 #else
@@ -334,41 +345,51 @@ __global__ __launch_bounds__(256, PPO_XW_LB) void xw_kernel(XwLaunch L) {
     __syncthreads();
   }
 #endif
-  // epilogue
+  // epilogue.  The D form's ELU' operand: the next column block's rows are requested while this one is
+  // finished (clamped rows, unconditional: a load under the row test would be waited for at once); rows past
+  // M only skip their store.
   const int sh = -(eA + eW);
   uint32_t amax = 0u;
   f4_t csum[4];
+  f4_t ap[2][4];
+  auto load_ap = [&](int tn, f4_t (&a)[4]) {
+    const int n = nt * TB + wn * 64 + tn * 16 + 4 * q;
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm) {
+      const int mc = min(mt * TB + wm * 64 + tm * 16 + c, M - 1);
+      a[tm] = *reinterpret_cast<const f4_t*>(P.aprev + (size_t)mc * P.ldp + n);
+    }
+  };
+  if (EPI == EPI_DELU) load_ap(0, ap[0]);
 #pragma unroll
   for (int tn = 0; tn < 4; ++tn) {
+    if (EPI == EPI_DELU && tn + 1 < 4) load_ap(tn + 1, ap[(tn + 1) & 1]);
     csum[tn] = (f4_t){0.0f, 0.0f, 0.0f, 0.0f};
     const int n = nt * TB + wn * 64 + tn * 16 + 4 * q;
-    f4_t bias4 = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (EPI != EPI_DELU) bias4 = *reinterpret_cast<const f4_t*>(P.bias + n);
 #pragma unroll
     for (int tm = 0; tm < 4; ++tm) {
       const int m = mt * TB + wm * 64 + tm * 16 + c;
-      if (m >= M) continue;
+      const bool in = m < M;
       f4_t v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = ldexpf(acc[tn][tm][i], sh);
       if (EPI == EPI_DELU) {
-        const f4_t ap = *reinterpret_cast<const f4_t*>(P.aprev + (size_t)m * P.ldp + n);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] * delu_from_out(ap[i]);
+        for (int i = 0; i < 4; ++i) v[i] = in ? v[i] * delu_from_out(ap[tn & 1][tm][i]) : 0.0f;
         csum[tn] += v;
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float z = v[i] + bias4[i];
+          const float z = v[i] + bias4[tn][i];
           v[i] = EPI == EPI_ELU ? elu(z) : z;
         }
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) amax = max(amax, absbits(v[i]));
+      for (int i = 0; i < 4; ++i) amax = max(amax, in ? absbits(v[i]) : 0u);
 #ifdef PPO_XW_NOSTORE  // timing experiment: no C stores
       if (v[0] != v[0] && v[1] == 12345.0f)
 #endif
-      *reinterpret_cast<f4_t*>(P.c + (size_t)m * P.ldc + n) = v;
+      if (in) *reinterpret_cast<f4_t*>(P.c + (size_t)m * P.ldc + n) = v;
     }
   }
   amax = wave_max_u32(amax);
@@ -482,24 +503,28 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgLaunch L) {
   const int rsub = w * 8 + (lane >> 5);  // + 2 j
   const float* xb = P.x + kxc;
   const float* db = P.d + tn * TB + 4 * col4;
-  f4_t sxv[4], sdv[4];
-  int sm0 = 0;
-  // unconditional loads (rows clamped); out-of-range values are zeroed in store(), after the MFMAs (xw_kernel)
-  auto load = [&](int m0) {
-    sm0 = m0;
+  // two register slots: the rows of group g + 1 are in flight while group g is multiplied, and group g + 2 is
+  // requested before group g + 1 is split into LDS (every load unconditional: rows clamped, the last group
+  // re-loaded past the end; out-of-range values zeroed in store(), after the MFMAs)
+  f4_t sxv[2][4], sdv[2][4];
+  int sm0[2] = {0, 0};
+  const int ng = (m_hi - m_lo + 31) >> 5;
+  auto load = [&](int slot, int g) {
+    const int m0 = m_lo + min(g, ng - 1) * 32;
+    sm0[slot] = m0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int mc = min(m0 + rsub + 2 * j, L.M - 1);
-      sxv[j] = *reinterpret_cast<const f4_t*>(xb + (size_t)mc * P.ldx);
-      sdv[j] = *reinterpret_cast<const f4_t*>(db + (size_t)mc * P.ldd);
+      sxv[slot][j] = *reinterpret_cast<const f4_t*>(xb + (size_t)mc * P.ldx);
+      sdv[slot][j] = *reinterpret_cast<const f4_t*>(db + (size_t)mc * P.ldd);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int slot, int buf) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = rsub + 2 * j;
-      const float rm = sm0 + r < m_hi ? 1.0f : 0.0f;
-      f4_t vx = sxv[j], vd = sdv[j];
+      const float rm = sm0[slot] + r < m_hi ? 1.0f : 0.0f;
+      f4_t vx = sxv[slot][j], vd = sdv[slot][j];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         vx[i] = kx + i < P.k0 ? vx[i] * rm : 0.0f;
@@ -520,34 +545,43 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgLaunch L) {
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int bq = 0; bq < 4; ++bq) acc[a][bq] = (f4_t){0.0f, 0.0f, 0.0f, 0.0f};
-  const int ng = (m_hi - m_lo + 31) >> 5;
-  if (ng > 0) {
-    load(m_lo);
-    store(0);
-    __syncthreads();
-    for (int g = 0; g < ng; ++g) {
-      const int cur = g & 1;
-      const bool more = g + 1 < ng;
-      if (more) load(m_lo + (g + 1) * 32);
-      if (nkt > 0) {
-        h8_t dh[4], dl[4];
+  auto mma = [&](int cur) {
+    if (nkt > 0) {
+      h8_t dh[4], dl[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dh[j] = tr_frag(sD[cur][0], wn * 64 + j * 16, q, c);
-          dl[j] = tr_frag(sD[cur][1], wn * 64 + j * 16, q, c);
-        }
+      for (int j = 0; j < 4; ++j) {
+        dh[j] = tr_frag(sD[cur][0], wn * 64 + j * 16, q, c);
+        dl[j] = tr_frag(sD[cur][1], wn * 64 + j * 16, q, c);
+      }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (i < nkt) {
-            const h8_t xh = tr_frag(sX[cur][0], wk * 64 + i * 16, q, c);
-            const h8_t xl = tr_frag(sX[cur][1], wk * 64 + i * 16, q, c);
+      for (int i = 0; i < 4; ++i) {
+        if (i < nkt) {
+          const h8_t xh = tr_frag(sX[cur][0], wk * 64 + i * 16, q, c);
+          const h8_t xl = tr_frag(sX[cur][1], wk * 64 + i * 16, q, c);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma3(xh, xl, dh[j], dl[j], acc[i][j]);
-          }
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma3(xh, xl, dh[j], dl[j], acc[i][j]);
         }
       }
-      if (more) store(cur ^ 1);
+    }
+  };
+  if (ng > 0) {
+    load(0, 0);
+    store(0, 0);
+    load(1, 1);
+    __syncthreads();
+    for (int g = 0; g < ng; g += 2) {
+      // slot 1 holds group g + 1; slot 0 is free
+      load(0, g + 2);
+      mma(0);
+      store(1, 1);
       __syncthreads();
+      if (g + 1 < ng) {
+        // slot 0 holds group g + 2; slot 1 is free
+        load(1, g + 3);
+        mma(1);
+        store(0, 0);
+        __syncthreads();
+      }
     }
   }
   const int sh = -(eX + eD);
