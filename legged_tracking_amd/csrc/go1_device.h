@@ -1526,9 +1526,10 @@ __device__ __forceinline__ int quad_or(int v) {
 // Work per candidate leg pair: its 27 sphere pairs over the env's 16 lanes (two rounds).  Fs: the
 // self-contact world forces on the lane's two points (x, y halves), wb: the trunk reaction wrench of the
 // lane's box contacts (base frame, summed over the env's lanes by the caller).
-__device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
-                                           const float* R, const float* pos, const float* vb, const float* th,
-                                           float Fs[2][3], float* wb) {
+__device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, const unsigned short* tpair,
+                                           const short* tslot, int leg, int role, int mask, const float* R,
+                                           const float* pos, const float* vb, const float* th, float Fs[2][3],
+                                           float* wb) {
   const float ks = cfg->self_stiffness, ds = cfg->self_damping;
   const int k = 4 * role + leg;
   const int p0 = role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5));
@@ -1555,7 +1556,7 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
     for (int t = 0; t < 2; ++t) {
       const int j = k + 16 * t;
       if (j < 27 && ((mask >> lp) & 1)) {
-        const unsigned e = SELF_PAIR[lp * 27 + j];
+        const unsigned e = tpair[lp * 27 + j];
         const float4 A = P[2 * (e & 0xffu)], B = P[2 * (e >> 8)];
         const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
         act |= (d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << (2 * lp + t)) : 0u;
@@ -1573,7 +1574,7 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
       if (j < 27 && ((mask >> lp) & 1)) {
         float F[3] = {0.0f, 0.0f, 0.0f};
         if ((act >> (2 * lp + t)) & 1u) {
-          const unsigned e = SELF_PAIR[lp * 27 + j], a = e & 0xffu, b = e >> 8;
+          const unsigned e = tpair[lp * 27 + j], a = e & 0xffu, b = e >> 8;
           self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
         }
         FS[lp * 27 + j] = make_float4(F[0], F[1], F[2], 0.0f);
@@ -1585,7 +1586,7 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
   for (int hh = 0; hh < 2; ++hh) {
     const int p = hh == 0 ? p0 : p1;
     if (p < 0) continue;
-    const short* sl = SELF_SLOT[leg * 6 + p];
+    const short* sl = tslot + (leg * 6 + p) * SELF_SLOTS;
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
     for (int j = 0; j < SELF_SLOTS; ++j) {
       const int v = sl[j];
@@ -1597,6 +1598,14 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
     }
     Fs[hh][0] += s0; Fs[hh][1] += s1; Fs[hh][2] += s2;
   }
+}
+
+// the pair and slot tables (go1_selfpairs.h) copied into LDS once per launch: read from constant memory inside
+// the narrow phase, every entry is a vector load with a full memory latency
+#define SELF_TAB_SHORTS (SELF_NPAIRS_PAD + 24 * SELF_SLOTS)
+__device__ __forceinline__ void self_tables_to_lds(unsigned short* tab, int lane) {
+  for (int i = lane; i < SELF_NPAIRS_PAD; i += 64) tab[i] = SELF_PAIR[i];
+  for (int i = lane; i < 24 * SELF_SLOTS; i += 64) tab[SELF_NPAIRS_PAD + i] = (unsigned short)(&SELF_SLOT[0][0])[i];
 }
 
 // the lane's spheres into this env's LDS scratch (x half p0; y half p1 unless a trunk corner)
@@ -1647,7 +1656,7 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
 __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
                                              float h, const float* g, float friction, float restitution,
                                              float payload, const Terr& T, int leg, int role, bool cf_out,
-                                             float* cf_raw, float* self_sc) {
+                                             float* cf_raw, float* self_sc, const unsigned short* self_tab) {
 #pragma clang fp contract(on)
   // Model constants are compile-time literals (go1_model_consts.h, checked against the
   // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
@@ -1794,7 +1803,8 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       if (__any(mask != 0)) {
         self_put(self_sc, leg, role, pw, vw, rr);
         __syncthreads();
-        self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
+        self_narrow(cfg, self_sc, self_tab, reinterpret_cast<const short*>(self_tab + SELF_NPAIRS_PAD), leg, role,
+                    mask, R, S.pos, vb, th, Fs, wb);
       }
 #pragma unroll
       for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
