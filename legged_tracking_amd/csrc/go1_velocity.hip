@@ -916,7 +916,21 @@ struct CkShared {
   int pvalid[GO1_VEL_N_CATEGORIES];                   // p holds the cdf of the current weights
   int rec[GO1_VEL_N_CATEGORIES];                      // p recomputed in this launch (the cache to commit)
   int wchg;                                           // some weight changed in this launch
+  int wloaded;                                        // w holds the weights (loaded on first need)
 };
+
+// the weights into LDS, once per launch, when a phase first needs them (called by the whole workgroup)
+__device__ void ensure_weights(VCfg* v, const CArgs& K, CkShared& S) {
+  if (S.wloaded) return;
+  const int nb = v->n_bins;
+  for (int i = threadIdx.x; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
+    const int c = i / nb;
+    S.w[(size_t)c * GO1_VEL_MAX_BINS + (i - c * nb)] = K.st.curriculum_weights[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) S.wloaded = 1;
+  __syncthreads();
+}
 
 // The curriculum runs on K.nblk workgroups.  Everything _resample_commands computes for the batch as a whole --
 // the selections, the success counts, the weight update and the cdf -- is computed by every workgroup from the
@@ -945,13 +959,13 @@ __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
   for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.hist[i] = 0;
   if (tid < 4) S.cnt[tid] = 0;
   if (tid < GO1_VEL_N_CATEGORIES) { S.dirty[tid] = 0; S.rec[tid] = 0; }
-  if (tid == 0) S.wchg = 0;
+  if (tid == 0) { S.wchg = 0; S.wloaded = 0; }
   // the cached cdfs (wave c) and the weights (wave 4 + c), whether or not a phase will need them
   double t[GO1_VEL_MAX_BINS / 64];
   int ok = 0;
-  if (wv < 2 * GO1_VEL_N_CATEGORIES) {
+  if (wv < GO1_VEL_N_CATEGORIES) {  // the weights are loaded only when a phase needs them (ensure_weights)
     const int c = wv & 3;
-    const double* g = (wv < GO1_VEL_N_CATEGORIES ? K.cdf : K.st.curriculum_weights) + (size_t)c * nb;
+    const double* g = K.cdf + (size_t)c * nb;
     if (wv < GO1_VEL_N_CATEGORIES) ok = K.cdf_ok[c];
     // unconditional loads (index clamped): a load under a condition makes hipcc wait for it right away
 #pragma unroll
@@ -1010,9 +1024,9 @@ __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
     __syncthreads();  // wsum is rewritten by the next pass
   }
   if (tid == 0) { S.cnt[0] = base[0]; S.cnt[1] = base[1]; }
-  if (wv < 2 * GO1_VEL_N_CATEGORIES) {
+  if (wv < GO1_VEL_N_CATEGORIES) {
     const int c = wv & 3;
-    double* dst = (wv < GO1_VEL_N_CATEGORIES ? S.p : S.w) + (size_t)c * GO1_VEL_MAX_BINS;
+    double* dst = S.p + (size_t)c * GO1_VEL_MAX_BINS;
 #pragma unroll
     for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
       if (lane + 64 * i < nb) dst[lane + 64 * i] = t[i];
@@ -1117,6 +1131,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   // count decides the result whatever the order.  Neighbourhoods come from the handle's table
   // (get_local_bins, curriculum.py:123-133, evaluated on the host in the same f64 comparisons).
   if (n_list > 0) {
+    ensure_weights(v, K, S);
     for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.inc[i] = 0;
     __syncthreads();
     for (int l = tid; l < n_list; l += CK_THREADS) {
@@ -1149,6 +1164,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   VSTAMP(ph, 2, t0);
   // ---- numpy rng.choice(p = w / w.sum()): cdf = cumsum(p) / cdf[-1], wave c for category c, in LDS
   // (S.p), recomputed where the weights changed (or no cdf is cached)
+  if (!S.pvalid[0] || !S.pvalid[1] || !S.pvalid[2] || !S.pvalid[3]) ensure_weights(v, K, S);  // uniform
   {
     const int wv = tid >> 6, ln = tid & 63;
     if (wv < GO1_VEL_N_CATEGORIES && (S.dirty[wv] || !S.pvalid[wv])) {
@@ -1421,8 +1437,8 @@ static int vfail(int code, const std::string& msg) {
     if (_e != hipSuccess) return vfail(GO1_E_HIP, std::string(#x ": ") + hipGetErrorString(_e)); \
   } while (0)
 
-// curriculum workgroups: the per-env sampling splits over them (a 4096-env resample: 128 envs each)
-static int curriculum_blocks(int n) { return std::max(1, std::min(32, n / 128)); }
+// curriculum workgroups: the per-env sampling splits over them (a 4096-env resample: 256 envs each)
+static int curriculum_blocks(int n) { return std::max(1, std::min(16, n / 256)); }
 
 static CArgs curriculum_args(go1_vel_handle* h) {
   CArgs K;
