@@ -40,6 +40,9 @@ def counters(src, match="go1_step_kernel"):
     per = defaultdict(list)
     meta = {}
     for f in sorted(glob.glob(os.path.join(src, "*", "*counter_collection.csv"))):
+        # the pol_* passes profile the rollout loop (whose step kernel runs beside the policy kernel)
+        if os.path.basename(os.path.dirname(f)).startswith("pol_") != match.startswith("policy"):
+            continue
         acc = defaultdict(float)
         with open(f) as fh:
             for row in csv.DictReader(fh):

@@ -2,7 +2,7 @@
 # Round-4 profile set (gpurun): available counters, the FLOP-counter calibration probe, kernel trace
 # + PMC passes of the step kernel under the bench loop, and the kernel traces of the rollout loop
 # and of whole Runner iterations (learn).  One counter set per pass, never combined with tracing.
-# Output: gpurun_out/prof_r04/.  A pass that fails fast (rc 1/2: e.g. a counter name the pool's
+# Output: gpurun_out/prof_r04/.  Argument 1 / 2: the step-kernel passes / the rest (one gpurun call each).  A pass that fails fast (rc 1/2: e.g. a counter name the pool's
 # rocprofv3 does not know) is reported and skipped; a timeout / signal ends the script.
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$ROOT/gpurun_out/prof_r04"
@@ -18,6 +18,8 @@ run() {  # name, timeout, rocprofv3 args... -- program...
   if [ $rc -ge 124 ]; then exit $rc; fi
   return 0
 }
+PART="${1:-all}"
+if [ "$PART" != 2 ]; then
 timeout -k 10 60 rocprofv3 --list-avail > "$OUT/list_avail.txt" 2>&1; echo "list rc=$?"
 FL="SQ_WAVES SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_MFMA_MOPS_F32"
 run probe_flops 60 --pmc $FL --output-format csv -d "$OUT/probe_flops" -o probe -- "$ROOT/tools/probes/flop_count"
@@ -29,6 +31,8 @@ run sq 240 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU
 run sq2 240 --pmc SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY --output-format csv -d "$OUT/sq2" -o sq2 -- python3 $B
 run flops 240 --pmc $FL --output-format csv -d "$OUT/flops" -o flops -- python3 $B
 run tcc 240 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/tcc" -o tcc -- python3 $B
+fi
+if [ "$PART" != 1 ]; then
 run engine 240 --kernel-trace --stats --output-format csv -d "$OUT/engine" -o engine -- python3 "$ROOT/tools/prof_engine.py"
 run lds 240 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE --output-format csv -d "$OUT/lds" -o lds -- python3 $B
 run rollout 240 --kernel-trace --stats --output-format csv -d "$OUT/rollout" -o rollout -- python3 "$ROOT/bench.py" --rollout-only --steps 120 --warmup 24
@@ -45,3 +49,4 @@ run pol_fetch 240 --pmc FETCH_SIZE --output-format csv -d "$OUT/pol_fetch" -o p 
 cd "$ROOT" && timeout -k 10 600 python bench.py --steps 500 --warmup 50 > "$OUT/bench_full.log" 2>&1; echo "bench rc=$?"
 # whole-loop traces are tens of MB: keep their stats only (gpurun copies back at most 64 MiB)
 rm -f "$OUT"/learn/*_kernel_trace.csv "$OUT"/vel_learn/*_kernel_trace.csv
+fi
