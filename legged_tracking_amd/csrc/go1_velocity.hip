@@ -852,6 +852,8 @@ struct CArgs {
   double* cdf;          // (GO1_VEL_N_CATEGORIES, n_bins): numpy's normalised cdf of each curriculum
   int32_t* cdf_ok;      // [GO1_VEL_N_CATEGORIES]: cdf current for the weights
   int n_envs, env_id_offset;
+  int nb, R;            // v->n_bins, v->resample_interval as kernel arguments: the prologue's first loads
+                        // (flags, cached cdfs) then wait on no load of the config block
   int nblk;             // curriculum workgroups (blocks 0 .. nblk - 1; the rest shift the history)
   int* done;            // their completion count (zero between launches)
   uint64_t seed;
@@ -922,7 +924,7 @@ struct CkShared {
 // the weights into LDS, once per launch, when a phase first needs them (called by the whole workgroup)
 __device__ void ensure_weights(VCfg* v, const CArgs& K, CkShared& S) {
   if (S.wloaded) return;
-  const int nb = v->n_bins;
+  const int nb = K.nb;
   for (int i = threadIdx.x; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
     const int c = i / nb;
     S.w[(size_t)c * GO1_VEL_MAX_BINS + (i - c * nb)] = K.st.curriculum_weights[i];
@@ -951,7 +953,7 @@ __device__ __forceinline__ bool selectedA(const CArgs& K, int e, int R) {
 // a phase then costs the success counts (one round trip), the weight update (when some env succeeded), the
 // cdf of changed weights, and the sampling (commands and grid cells together).
 __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
-  const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
+  const int tid = threadIdx.x, n = K.n_envs, nb = K.nb, R = K.R;
 #ifdef GO1_VEL_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1056,7 +1058,7 @@ __device__ __forceinline__ int draw_category(float uc) {
 
 // One resample (_resample_commands :728-842) of kind B (mask) or A (interval), by the whole workgroup.
 __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S) {
-  const int tid = threadIdx.x, n = K.n_envs, nb = v->n_bins, R = v->resample_interval;
+  const int tid = threadIdx.x, n = K.n_envs, nb = K.nb, R = K.R;
   const int blk = blockIdx.x, nblk = K.nblk;
   const go1_vel_state& st = K.st;
   const float* U = kindB ? K.UB : K.UA;
@@ -1293,7 +1295,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
 // the same values; all of them have read the old ones by then).  Release: every workgroup's reads and writes
 // precede its ticket; acquire: the last one sees every other workgroup done before it writes.
 __device__ void resample_commit(VCfg* v, const CArgs& K, CkShared& S) {
-  const int tid = threadIdx.x, nb = v->n_bins;
+  const int tid = threadIdx.x, nb = K.nb;
   __syncthreads();
   // every workgroup takes the same decisions: with no weight changed and no cdf recomputed there is nothing
   // to commit, and none of them takes a ticket
@@ -1451,6 +1453,8 @@ static CArgs curriculum_args(go1_vel_handle* h) {
   K.cdf_ok = h->d_cdf_ok;
   K.n_envs = h->cfg.n_envs;
   K.env_id_offset = h->cfg.env_id_offset;
+  K.nb = h->vcfg.n_bins;
+  K.R = h->vcfg.resample_interval;
   K.nblk = curriculum_blocks(h->cfg.n_envs);
   K.done = h->d_done;
   return K;
