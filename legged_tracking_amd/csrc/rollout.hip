@@ -769,23 +769,47 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
   // thread's in flight) before the accumulators are live
   float* flat = reinterpret_cast<float*>(&S.h1[0]);
   const int fs = nch == 1 ? H : PIN;
+  // L1 weight fragments, two groups ahead (two register sets, the group loop unrolled by two)
+  f8_t wA0, wL00, wL01, wA1, wL10, wL11;
+  auto load0 = [&](int g) {
+    if constexpr (!CRITIC) wA0 = reinterpret_cast<const f8_t*>(Ls[0].w)[((size_t)wave * GA + g) * 64 + lane];
+    wL00 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)wave * GL + g) * 64 + lane];
+    wL01 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)(wave + PW) * GL + g) * 64 + lane];
+  };
+  auto load1 = [&](int g) {
+    if constexpr (!CRITIC) wA1 = reinterpret_cast<const f8_t*>(Ls[0].w)[((size_t)wave * GA + g) * 64 + lane];
+    wL10 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)wave * GL + g) * 64 + lane];
+    wL11 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)(wave + PW) * GL + g) * 64 + lane];
+  };
+  // the first chunk's first two groups are requested before the inputs: they depend on nothing the workgroup
+  // computes, so the weight stream starts under the input loads' latency instead of after the staging
+#ifndef GO1_POLICY_L1_EARLY
+#define GO1_POLICY_L1_EARLY 1
+#endif
+  if (GO1_POLICY_L1_EARLY) {
+    const int gb0 = CRITIC ? min(CG, GL) : min(gl, min(CG, GL));
+    if (0 < gb0) load0(0);
+    if (1 < gb0) load1(1);
+#if GO1_POLICY_SCHED
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
   if (nch == 1) {
     constexpr int NI = (ET * 16 * PIN + 64 * PW - 1) / (64 * PW);
     const int64_t LD = P.hist_ld;
     const float* src = P.obs_history + (size_t)e0 * LD;
     const int total = ne * H;
     float v[NI];
+    // unconditional loads at clamped indices: a load under a condition is waited for right after it is
+    // issued (one HBM round trip per load instead of one for all)
     if (LD == H) {
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int j = tid + i * 64 * PW;
-        v[i] = j < total ? src[j] : 0.0f;
-      }
+      for (int i = 0; i < NI; ++i) v[i] = src[min(tid + i * 64 * PW, total - 1)];
     } else {  // rows of a wider buffer (row-strided window)
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
-        const int j = tid + i * 64 * PW, r = j / H;
-        v[i] = j < total ? src[(size_t)r * LD + (j - r * H)] : 0.0f;
+        const int j = min(tid + i * 64 * PW, total - 1), r = j / H;
+        v[i] = src[(size_t)r * LD + (j - r * H)];
       }
     }
 #pragma unroll
@@ -793,6 +817,16 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
       const int j = tid + i * 64 * PW;
       if (j < total) flat[j] = v[i];
     }
+    PSTAMP(9);
+  }
+  // the critic's privileged inputs into LDS behind the f32 copy (one clamped load per thread; the split
+  // passes read them from there)
+  float* pflat = flat + ET * 16 * PIN;
+  static_assert(ET * 16 * (PIN + 8) * sizeof(float) <= sizeof(SplitLds::h1), "f32 staging exceeds h1");
+  if constexpr (CRITIC) {
+    const int t = min(tid, ET * 16 * NP - 1), e = t / NP;
+    const float x = P.privileged_obs[(size_t)(e0 + min(e, ne - 1)) * NP + (t - e * NP)];
+    if (tid < ET * 16 * NP) pflat[tid] = x;
   }
   f4_t accA[ET], accL[ET][2];
   {
@@ -825,9 +859,10 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
       const float* src = P.obs_history + (size_t)(e0 + (row ? e : 0)) * P.hist_ld;
       float v[NI];
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
+      for (int i = 0; i < NI; ++i) {  // unconditional loads (index clamped), then the mask
         const int kc = kk + TPE * i, k = k0 + kc;
-        v[i] = (row && kc < PIN && k < H) ? src[k] : 0.0f;
+        const float x = src[min(k, H - 1)];
+        v[i] = (row && kc < PIN && k < H) ? x : 0.0f;
       }
       if (live) {
 #pragma unroll
@@ -838,6 +873,7 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
       }
     }
     lds_barrier();
+    if (ch == 0) PSTAMP(10);
     {
       constexpr int NC = PIN / 8, NTASK = ET * 16 * NC;
       for (int t = tid; t < NTASK; t += 64 * PW) {
@@ -849,7 +885,7 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
           float x = 0.0f;
           if (e < ne) {
             if (k < H) x = flat[e * fs + kl];
-            else if (CRITIC && k < KIN) x = P.privileged_obs[(size_t)(e0 + e) * NP + (k - H)];
+            else if (CRITIC && k < KIN) x = pflat[e * NP + (k - H)];
           }
           ovf_check(x, s_ovf);
           hi8[r] = (_Float16)x;
@@ -865,18 +901,6 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
     // module (actor) and L1; the next group's fragments are requested before this group's MFMAs
     {
       const int g1 = min(g0 + CG, GL), gb = CRITIC ? g1 : min(gl, g1);
-      // fragments two groups ahead: two register sets, the loop body unrolled by two
-      f8_t wA0, wL00, wL01, wA1, wL10, wL11;
-      auto load0 = [&](int g) {
-        if constexpr (!CRITIC) wA0 = reinterpret_cast<const f8_t*>(Ls[0].w)[((size_t)wave * GA + g) * 64 + lane];
-        wL00 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)wave * GL + g) * 64 + lane];
-        wL01 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)(wave + PW) * GL + g) * 64 + lane];
-      };
-      auto load1 = [&](int g) {
-        if constexpr (!CRITIC) wA1 = reinterpret_cast<const f8_t*>(Ls[0].w)[((size_t)wave * GA + g) * 64 + lane];
-        wL10 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)wave * GL + g) * 64 + lane];
-        wL11 = reinterpret_cast<const f8_t*>(LN[0].w)[((size_t)(wave + PW) * GL + g) * 64 + lane];
-      };
       auto group = [&](int gi, const f8_t& a, const f8_t& l0, const f8_t& l1) {
 #pragma unroll
         for (int et = 0; et < ET; ++et) {
@@ -886,8 +910,10 @@ __device__ __forceinline__ void split_body(const go1_policy_args& P, SplitLds& S
           accL[et][1] = mfma3(l1, xh, xl, accL[et][1]);
         }
       };
-      if (g0 < gb) load0(g0);
-      if (g0 + 1 < gb) load1(g0 + 1);
+      if (ch > 0 || !GO1_POLICY_L1_EARLY) {  // the first chunk's were requested before the staging
+        if (g0 < gb) load0(g0);
+        if (g0 + 1 < gb) load1(g0 + 1);
+      }
       for (int g = g0; g < gb; g += 2) {
         group(g - g0, wA0, wL00, wL01);
         if (g + 2 < gb) load0(g + 2);

@@ -45,7 +45,8 @@ def main():
     lib = alg.fused.lib
     buf = np.zeros(512 * 16 * 12, np.uint64)
     assert lib.go1_policy_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
-    t_all = buf.reshape(512, 16, 12).astype(np.int64)[:256, :, :9]
+    t_full = buf.reshape(512, 16, 12).astype(np.int64)[:256]
+    t_all = t_full[:, :, :9]
     used = t_all[:, 0, 0] != 0  # workgroups of the launch (the stamp buffer holds 256)
     na = -(-n // (16 * int(os.environ.get("GO1_SPLIT_ET_A", "2"))))
     groups = [("all", t_all[used])] if variant else [("actor workgroups", t_all[:na][used[:na]]),
@@ -59,6 +60,13 @@ def main():
         print(f"{label}: {t.shape[0]}; mean lifetime {life:.0f} cycles")
         for nm, v in zip(NAMES, d):
             print(f"  {nm:14s} {v:9.0f} {v / life:7.1%}")
+    # inside the staging: 9 = the f32 copy stored (the input loads landed), 10 = past the barrier after it
+    tf = t_full[used]
+    t0 = tf[:, :, :1].min(axis=1)
+    for k, nm in ((9, "inputs landed"), (10, "copy barrier")):
+        if (tf[:, :, k] != 0).all():
+            print(f"  staging: {nm:14s} at {(tf[:, :, k].max(axis=1) - t0[:, 0]).mean():9.0f} cycles (last wave)")
+    print(f"  wave start -> first stamp of wave: mean spread {(tf[:, :, 0] - t0).mean():.0f}")
     # spread of the workgroups' start times (launch ramp) and end times
     st = t_all[used][:, :, 0].min(axis=1)
     en = t_all[used][:, :, 8].max(axis=1)
