@@ -845,25 +845,27 @@ __device__ unsigned long long g_vstamps[2][16];
 #define CK_BATCH 8
 #define CK_SEL_CAP 4096
 struct CArgs {
+  // the prologue's inputs lead (a launch that preloads the first kernel-argument dwords into registers has them
+  // without a load)
+  int n_envs, nb, R;    // nb, R: v->n_bins, v->resample_interval (no load of the config block in the prologue)
+  int doA;              // A kind below: the next step's interval resample
+  const uint8_t* maskB; // B kind below: reset_idx's envs
+  const int32_t* episode_length;  // st.episode_length
+  double* cdf;          // (GO1_VEL_N_CATEGORIES, n_bins): numpy's normalised cdf of each curriculum
+  int32_t* cdf_ok;      // [GO1_VEL_N_CATEGORIES]: cdf current for the weights
   go1_vel_state st;
   const double* grid;   // (GO1_VEL_N_KEYS, n_bins)
   const int32_t* adj_ptr;  // neighbourhood table (CSR): cells adjacent to bin b are adj_idx[adj_ptr[b] ..]
   const int32_t* adj_idx;
-  double* cdf;          // (GO1_VEL_N_CATEGORIES, n_bins): numpy's normalised cdf of each curriculum
-  int32_t* cdf_ok;      // [GO1_VEL_N_CATEGORIES]: cdf current for the weights
-  int n_envs, env_id_offset;
-  int nb, R;            // v->n_bins, v->resample_interval as kernel arguments: the prologue's first loads
-                        // (flags, cached cdfs) then wait on no load of the config block
+  int env_id_offset;
   int nblk;             // curriculum workgroups (blocks 0 .. nblk - 1; the rest shift the history)
   int* done;            // their completion count (zero between launches)
   uint64_t seed;
   // B kind: the envs of maskB (reset_idx's resample)
-  const uint8_t* maskB;
   const float* UB;
   const double* UDB;
   uint64_t stepB;
   // A kind: envs with (episode_length + 1) % resample_interval == 0 (the next step's interval resample)
-  int doA;
   const float* UA;
   const double* UDA;
   uint64_t stepA;
@@ -952,8 +954,12 @@ __device__ __forceinline__ bool selectedA(const CArgs& K, int e, int R) {
 // once: the prologue loads both phases' selection flags, the cached cdfs and the weights in one round trip;
 // a phase then costs the success counts (one round trip), the weight update (when some env succeeded), the
 // cdf of changed weights, and the sampling (commands and grid cells together).
-__device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
-  const int tid = threadIdx.x, n = K.n_envs, nb = K.nb, R = K.R;
+// The prologue's inputs come as the launch's leading scalar arguments (pn .. pcdf_ok, the same values as the
+// CArgs fields): with kernel-argument preloading they arrive in registers with the wave.
+__device__ __forceinline__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S, int pn, int pnb, int pR,
+                                                  int pdoA, const uint8_t* pmaskB, const int32_t* pel,
+                                                  const double* pcdf, const int32_t* pcdf_ok) {
+  const int tid = threadIdx.x, n = pn, nb = pnb, R = pR;
 #ifdef GO1_VEL_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -967,8 +973,8 @@ __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
   int ok = 0;
   if (wv < GO1_VEL_N_CATEGORIES) {  // the weights are loaded only when a phase needs them (ensure_weights)
     const int c = wv & 3;
-    const double* g = K.cdf + (size_t)c * nb;
-    if (wv < GO1_VEL_N_CATEGORIES) ok = K.cdf_ok[c];
+    const double* g = pcdf + (size_t)c * nb;
+    if (wv < GO1_VEL_N_CATEGORIES) ok = pcdf_ok[c];
     // unconditional loads (index clamped): a load under a condition makes hipcc wait for it right away
 #pragma unroll
     for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = g[min(lane + 64 * i, nb - 1)];
@@ -983,21 +989,21 @@ __device__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S) {
     bool sb[CK_BATCH], sa[CK_BATCH];
     int v = 0;
     // the flags of the run: unconditional loads at clamped indices (no wait per load), then the tests
-    const uint8_t* mB = K.maskB ? K.maskB : reinterpret_cast<const uint8_t*>(K.st.episode_length);
+    const uint8_t* mB = pmaskB ? pmaskB : reinterpret_cast<const uint8_t*>(pel);
     uint8_t fb[CK_BATCH];
     int el[CK_BATCH];
 #pragma unroll
     for (int k = 0; k < CK_BATCH; ++k) {
       const int ec = min(eb + k, n - 1);
       fb[k] = mB[ec];
-      el[k] = K.st.episode_length[ec];
+      el[k] = pel[ec];
     }
 #pragma unroll
     for (int k = 0; k < CK_BATCH; ++k) {
       const int e = eb + k;
       const bool ok = k < per && e < e0 + span;
-      sb[k] = ok && K.maskB != nullptr && fb[k] != 0;
-      sa[k] = ok && K.doA && (el[k] + 1) % R == 0;
+      sb[k] = ok && pmaskB != nullptr && fb[k] != 0;
+      sa[k] = ok && pdoA && (el[k] + 1) % R == 0;
       v += (sb[k] ? 1 : 0) + (sa[k] ? 1 << 16 : 0);
     }
     int inc = v;  // inclusive scan over the wave
@@ -1384,6 +1390,9 @@ __device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
 }
 
 __global__ __launch_bounds__(CK_THREADS) void go1_vel_curriculum_kernel(const go1_vel_config* __restrict__ v_gen,
+                                                                        int pn, int pnb, int pR, int pdoA,
+                                                                        const uint8_t* pmaskB, const int32_t* pel,
+                                                                        const double* pcdf, const int32_t* pcdf_ok,
                                                                         CArgs K) {
   VCfg* __restrict__ v = (VCfg*)v_gen;
   if ((int)blockIdx.x >= K.nblk) {
@@ -1391,7 +1400,7 @@ __global__ __launch_bounds__(CK_THREADS) void go1_vel_curriculum_kernel(const go
     return;
   }
   __shared__ CkShared S;
-  resample_prologue(v, K, S);
+  resample_prologue(v, K, S, pn, pnb, pR, pdoA, pmaskB, pel, pcdf, pcdf_ok);
   if (K.maskB) resample_phase(v, K, true, S);
   if (K.doA) resample_phase(v, K, false, S);
   resample_commit(v, K, S);
@@ -1446,6 +1455,7 @@ static CArgs curriculum_args(go1_vel_handle* h) {
   CArgs K;
   memset(&K, 0, sizeof(K));
   K.st = h->st;
+  K.episode_length = h->st.episode_length;
   K.grid = h->d_grid;
   K.adj_ptr = h->d_adj_ptr;
   K.adj_idx = h->d_adj_idx;
@@ -1643,7 +1653,8 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   const int shift_blocks =
       C.hist_in ? (int)std::min<size_t>(256 - C.nblk, std::max<size_t>(1, (chunks + 4 * CK_THREADS - 1) / (4 * CK_THREADS)))
                 : 0;
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C);
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C.n_envs, C.nb, C.R, C.doA,
+                     C.maskB, C.episode_length, C.cdf, C.cdf_ok, C);
   VHIP_TRY(hipGetLastError());
   return GO1_OK;
 }
@@ -1667,7 +1678,8 @@ int go1_vel_resample(go1_vel_handle* h, const uint8_t* mask, const float* unifor
     C.UDA = uniforms_f64;
     C.stepA = rng_step;
   }
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C);
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C.n_envs, C.nb, C.R, C.doA,
+                     C.maskB, C.episode_length, C.cdf, C.cdf_ok, C);
   VHIP_TRY(hipGetLastError());
   return GO1_OK;
 }

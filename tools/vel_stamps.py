@@ -1,7 +1,7 @@
 """Section timing of the velocity curriculum launch's block 0 (diagnostic build with -DGO1_VEL_STAMPS).
 
   local:  hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off -fno-slp-vectorize \\
-              -DGO1_VEL_STAMPS -o legged_tracking_amd/_build/libgo1_velocity_stamps.so \\
+              -mllvm -amdgpu-kernarg-preload-count=16 -DGO1_VEL_STAMPS -o legged_tracking_amd/_build/libgo1_velocity_stamps.so \\
               legged_tracking_amd/csrc/go1_velocity.hip
   gpurun: python tools/vel_stamps.py
 
@@ -16,7 +16,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["GO1_VEL_LIB_OVERRIDE"] = os.path.join(ROOT, "legged_tracking_amd", "_build", "libgo1_velocity_stamps.so")
+os.environ["GO1_VEL_LIB_OVERRIDE"] = os.environ.get("VEL_STAMPS_LIB") or os.path.join(ROOT, "legged_tracking_amd", "_build", "libgo1_velocity_stamps.so")
 NAMES = {0: "scan (all phases)", 15: "count>0 entry", 1: "success hist", 2: "weights update", 3: "cdf",
          4: "sampling", 14: "cdf recomputes (count)", 10: "prologue (phase B row: every launch)",
          11: "commit (phase B row, launches that commit)"}
