@@ -1213,7 +1213,7 @@ __device__ __forceinline__ void point_kin(const float* Rb, const float* pb, cons
 // frame, (angular, linear) pairs); Fw = the world force, the hip's reported contact force.
 __device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const float* R, const float* pos,
                                             const f2* vbp, const float* org, float cq, float sq, float qd0,
-                                            f2 yy, float hr, float h, const float* g, SIP& IA, f2* pA,
+                                            f2 yy, float hr, float h, const float* g, int role, SIP& IA, f2* pA,
                                             float* Fw) {
   Fw[0] = Fw[1] = Fw[2] = 0.0f;
   // sphere centres from the hip joint, base frame: Rx(q) (0, y, 0) = (0, c y, s y)
@@ -1262,19 +1262,21 @@ __device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const fl
   float gh[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) gh[j] = Rh[j] * g[0] + Rh[3 + j] * g[1] + Rh[6 + j] * g[2];
-  f2 Fh[3] = {f2s(0.0f), f2s(0.0f), f2s(0.0f)}, M[6] = {f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f), f2s(0.0f)};
-  f2 cds = f2s(0.0f);
-  f2 Fwx = f2s(0.0f), Fwy = f2s(0.0f), Fwz = f2s(0.0f);
-#pragma unroll
-  for (int L = 0; L < 2; ++L) {
-    const float sg = L == 0 ? 1.0f : -1.0f;
-    f2 nx = -sg * gxl[L], ny = -sg * gyl[L];
+  // The two layers split over the role rows: rows 0 and 2 evaluate the floor (L = 0), rows 1 and 3 the
+  // ceiling (L = 1), both spheres packed; each sum over the layers is the row pair's sum (one permlane16
+  // swap), the same addition in every row (x + y = y + x) as one lane walking both layers.
+  const bool ceil_row = (role & 1) != 0;
+  const float sg = ceil_row ? -1.0f : 1.0f;
+  const f2 gxL = ceil_row ? gxl[1] : gxl[0], gyL = ceil_row ? gyl[1] : gyl[0], dvL = ceil_row ? dvl[1] : dvl[0];
+  f2 Fh[3], M[6], cds, Fwx, Fwy, Fwz;
+  {
+    f2 nx = -sg * gxL, ny = -sg * gyL;
     f2 inv = nx * nx + ny * ny + 1.0f;
     inv = f2{frsq(inv.x), frsq(inv.y)};
     nx = nx * inv;
     ny = ny * inv;
     const f2 nz = sg * inv;
-    const f2 depth = dvl[L] * inv;
+    const f2 depth = dvL * inv;
     const f2 vn = vw[0] * nx + vw[1] * ny + vw[2] * nz;
     const f2 fn0 = C.k * depth - C.d * vn;
     const f2 fn = restitute(C, h, vn, fn0 - (h * C.k) * vn);
@@ -1286,24 +1288,39 @@ __device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const fl
     const f2 cm = C.mu * fn0;
     const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
                      (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
-    const bool ax = dvl[L].x > 0.0f && fn0.x > 0.0f, ay = dvl[L].y > 0.0f && fn0.y > 0.0f;
+    const bool ax = dvL.x > 0.0f && fn0.x > 0.0f, ay = dvL.y > 0.0f && fn0.y > 0.0f;
     const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
     const f2 sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
-    Fwx += fa * nx - sc * vtx;  // the reported world force
-    Fwy += fa * ny - sc * vty;
-    Fwz += fa * nz - sc * vtz;
+    Fwx = fa * nx - sc * vtx;  // the reported world force
+    Fwy = fa * ny - sc * vty;
+    Fwz = fa * nz - sc * vtz;
     f2 m[3];  // the normal in the hip frame
 #pragma unroll
     for (int j = 0; j < 3; ++j) m[j] = Rh[j] * nx + Rh[3 + j] * ny + Rh[6 + j] * nz;
     // F = fa n - sc (v - vn n) = (fa + sc vn) n - sc v
     const f2 fs = fa + sc * vn;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) Fh[j] += fs * m[j] - sc * vh[j];
+    for (int j = 0; j < 3; ++j) Fh[j] = fs * m[j] - sc * vh[j];
     const f2 cd = h * sc, cnd = f2{ax ? cn : 0.0f, ay ? cn : 0.0f} - cd;
-    cds += cd;
+    cds = cd;
     const f2 am[3] = {cnd * m[0], cnd * m[1], cnd * m[2]};
-    M[0] += am[0] * m[0]; M[1] += am[0] * m[1]; M[2] += am[0] * m[2];
-    M[3] += am[1] * m[1]; M[4] += am[1] * m[2]; M[5] += am[2] * m[2];
+    M[0] = am[0] * m[0]; M[1] = am[0] * m[1]; M[2] = am[0] * m[2];
+    M[3] = am[1] * m[1]; M[4] = am[1] * m[2]; M[5] = am[2] * m[2];
+  }
+  {
+    auto pair = [](f2& v) {
+      auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.x), __float_as_uint(v.x), false, false);
+      auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.y), __float_as_uint(v.y), false, false);
+      v = f2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+    };
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pair(Fh[j]);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pair(M[k]);
+    pair(cds);
+    pair(Fwx);
+    pair(Fwy);
+    pair(Fwz);
   }
   M[0] += cds; M[3] += cds; M[5] += cds;
   Fw[0] = Fwx.x + Fwx.y; Fw[1] = Fwy.x + Fwy.y; Fw[2] = Fwz.x + Fwz.y;
@@ -1979,7 +1996,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
         if (j == 1) {  // the hip capsule's contact, on the hip's inertia and bias force
           MARK(hip_begin);
           hip_contact(T, C, R, S.pos, vbp, origin, cs[0][0], cs[0][1], S.qd[0], msy * f2{hip_y0, hip_y1}, hip_r, h,
-                      g, IA, pAp[0], Fhip);
+                      g, role, IA, pAp[0], Fhip);
           MARK(hip_done);
         }
 #endif
