@@ -148,7 +148,6 @@ class PPOEngine:
         self._graph_key = None
         self._import_optimizer_state()
         self._install_optimizer_views()
-        self.packed = False
 
     # ------------------------------------------------------------------ helpers
     def _chk(self, rc):
@@ -180,6 +179,22 @@ class PPOEngine:
             for name, p in self._param_list(ad):
                 opt.state[p] = {"step": self.steps[k], "exp_avg": v1[name], "exp_avg_sq": v2[name]}
         self._state_ptrs = self._optimizer_state_ptrs()
+
+    def release_optimizer_state(self):
+        """Give every parameter's optimizer state its own tensors again (copies of the engine's), before a torch
+        optimizer steps them: the views share one `step` per optimizer, which a torch Adam would increment once
+        per parameter.  The next engine update imports the state back (_sync_external_changes)."""
+        alg = self.alg
+        for opt, (m1, m2), k, ad in ((alg.optimizer, (self.exp_avg, self.exp_avg_sq), 0, False),
+                                     (alg.adaptation_module_optimizer, (self.ad_exp_avg, self.ad_exp_avg_sq), 1, True)):
+            g = opt.defaults
+            on_dev = bool(g.get("fused") or g.get("capturable"))
+            v1, v2 = self._views(m1, ad), self._views(m2, ad)
+            for name, p in self._param_list(ad):
+                step = self.steps[k].detach().clone()
+                opt.state[p] = {"step": step if on_dev else step.cpu(), "exp_avg": v1[name].clone(),
+                                "exp_avg_sq": v2[name].clone()}
+        self._state_ptrs = None
 
     def _optimizer_state_ptrs(self):
         alg = self.alg
@@ -215,8 +230,6 @@ class PPOEngine:
         if self._optimizer_state_ptrs() != self._state_ptrs:
             self._import_optimizer_state()
             self._install_optimizer_views()
-        if relink:
-            self.packed = False
         return ac
 
     def _write_hyper(self, A, world):
@@ -245,7 +258,6 @@ class PPOEngine:
         self._chk(self.lib.go1_ppo_workspace_bytes(C.byref(dims), C.byref(nb)))
         if self.work is None or self.work.numel() < nb.value:
             self.work = torch.zeros(nb.value + 256, dtype=torch.uint8, device=self.device)
-            self.packed = False
             self.graphs = None
         self.dims = dims
         b = self.bufs
@@ -273,7 +285,6 @@ class PPOEngine:
     # ------------------------------------------------------------------ the C-ABI calls
     def pack(self):
         self._chk(self.lib.go1_ppo_pack(C.byref(self.dims), C.byref(self.bufs), self._stream()))
-        self.packed = True
 
     def grad(self, phase):
         self._chk(self.lib.go1_ppo_grad(C.byref(self.dims), C.byref(self.bufs), phase, self._stream()))
@@ -310,8 +321,9 @@ class PPOEngine:
         mb = batch // num_mini_batches
         key = self._bind(st, mb)
         self._write_hyper(A, world)
-        if not self.packed:
-            self.pack()
+        # the f16 fragment images from the current weights, every update: an in-place write to the parameters
+        # (load_state_dict, a torch-path update, std.data edits) keeps their storage, so no pointer check sees it
+        self.pack()
         self.losses.zero_()
         indices = torch.randperm(num_mini_batches * mb, device=self.device)  # mini_batch_generator's draw
         draw = getattr(self, "_draw", None)

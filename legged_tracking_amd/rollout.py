@@ -888,6 +888,8 @@ class PPO:
             if self.fused is not None:
                 self.fused.pack()  # the rollout kernel reads the updated weights
             return (sums[0] / n_up, sums[1] / n_up, sums[2] / n_ad, 0.0, 0.0, sums[3] / n_ad, 0.0, 0.0)
+        if getattr(self, "_engine", None) is not None:
+            self._engine.release_optimizer_state()  # torch's Adam steps per-parameter state of its own
         # the loss means accumulate on the device (ppo.py:186-187, 200-201 call .item() per mini-batch:
         # a host sync each); one copy at the end.
         acc = torch.zeros(4, dtype=torch.float32, device=self.device)  # value, surrogate, adapt, adapt_test
