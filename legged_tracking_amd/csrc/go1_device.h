@@ -1812,7 +1812,11 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     // self-collision while the terrain reads land: world forces on the lane's two spheres, the trunk's
     // reaction wrench of the lane's box pairs into its trunk share
     float Fs[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}}, wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#ifndef GO1_ABL_NO_SELF  // ablation build only: no self-collision
     if (cfg->self_stiffness > 0.0f) {
+#else
+    if (false) {
+#endif
       float pft[3];  // the foot centre (calf frame offset), for the leg's bounding box
 #pragma unroll
       for (int i = 0; i < 3; ++i) pft[i] = pl[1][i] + Rl[1][3 * i] * foot[0] + Rl[1][3 * i + 1] * foot[1] + Rl[1][3 * i + 2] * foot[2];

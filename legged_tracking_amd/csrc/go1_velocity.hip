@@ -20,6 +20,7 @@
 #include "../../include/go1_velocity.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 typedef const __attribute__((address_space(4))) go1_vel_config VCfg;
@@ -174,6 +175,13 @@ struct VArgs {
   const float* env_origins;
   int hist_w;      // obs_history row width (70 x history_len)
   int64_t hist_ld; // obs_history_out row stride (floats)
+  // the curriculum launch's selection lists (CkRec, B = this step's resets, A = the next step's interval
+  // resample, n_envs each) and their counts (B low, A high word); czero: the other slot's counts, cleared here
+  // (the launch that read them has completed, stream order)
+  int4* clist;
+  unsigned long long* ccnt;
+  unsigned long long* czero;
+  int doA;
 };
 
 template <bool INJ>
@@ -235,6 +243,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int ep_in = st.episode_length[e];
   const float gait_in = st.gait_indices[e];
   const float lc_in = st.last_contacts[(size_t)e * 4 + leg];
+  // the curriculum's record of the env (category and bin before the resample), with the prologue loads
+  const int cat_in = st.command_categories[e], bin_in = st.command_bins[e];
   // reward slots: lane sub16 holds slots sub16 and 16 + sub16 (command sums: NT + 5 of them, episode sums
   // NT + 1: the terms, then "total")
   const int NC = NT + GO1_VEL_SUM_EXTRA, NE = NT + 1;
@@ -725,6 +735,42 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   }
 
+  // ---- the curriculum launch's selection lists.  A record per selected env: (env, category, bin, success)
+  // -- RewardThresholdCurriculum.update's inputs (:736-757, curriculum.py:135-154) over this step's command
+  // sums -- so the curriculum's workgroups never read the command state they rewrite (a late
+  // workgroup counting after another one's sampling).  B: this step's resets (:168 -> :182); A: the next
+  // step's interval resample, (episode_length + 1) % resample_interval == 0 (:702-704).  One 64-bit atomic per
+  // wave with a selected env; the lists are in atomic order (the curriculum's results do not depend on it).
+  if (K.clist) {
+    bool fail = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k < v->n_task) {
+        const int slot = v->task_slot[k];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (sub16 + 16 * h == slot && !(cs[h] / v->curriculum_ep_len > v->task_threshold[k])) fail = true;
+      }
+    }
+    const uint64_t fails = __ballot(fail);
+    const bool ok = ((fails >> (4 * el)) & 0x000F000F000F000Full) == 0ull;
+    const bool lead = lane == 4 * el;  // role 0, leg 0 of the env
+    const int ep_out = reset ? 0 : ep;
+    const bool selB = lead && reset, selA = lead && K.doA && (ep_out + 1) % v->resample_interval == 0;
+    const uint64_t mB = __ballot(selB), mA = __ballot(selA);
+    if ((mB | mA) != 0ull) {
+      unsigned long long base = 0ull;
+      if (lane == 0)
+        base = atomicAdd(K.ccnt, (unsigned long long)__popcll(mB) | ((unsigned long long)__popcll(mA) << 32));
+      const uint32_t bB = (uint32_t)__shfl((int)(uint32_t)base, 0), bA = (uint32_t)__shfl((int)(uint32_t)(base >> 32), 0);
+      const uint64_t below = (1ull << lane) - 1ull;
+      const int4 rec = make_int4(e, cat_in, bin_in, ok ? 1 : 0);
+      if (selB) K.clist[bB + __popcll(mB & below)] = rec;
+      if (selA) K.clist[(size_t)c->n_envs + bA + __popcll(mA & below)] = rec;
+    }
+    if (blockIdx.x == 0 && lane == 0) *K.czero = 0ull;
+  }
+
   // ---------------- write back (epilogue :144-149)
   if (role < 3) {
     const int j = role;
@@ -842,8 +888,10 @@ __device__ unsigned long long g_vstamps[2][16];
 #else
 #define VSTAMP(ph, k, t0)
 #endif
-#define CK_BATCH 8
-#define CK_SEL_CAP 4096
+#define CK_PRE 1024  // list records prefetched into LDS per phase (one per thread); the rest read from memory
+// the curriculum's record of a selected env: (env, command category, command bin, success of every task over the
+// episode's command sums) -- written by the step kernel (or go1_vel_list_kernel) before the launch
+typedef int4 CkRec;
 struct CArgs {
   // the prologue's inputs lead (a launch that preloads the first kernel-argument dwords into registers has them
   // without a load)
@@ -853,6 +901,8 @@ struct CArgs {
   const int32_t* episode_length;  // st.episode_length
   double* cdf;          // (GO1_VEL_N_CATEGORIES, n_bins): numpy's normalised cdf of each curriculum
   int32_t* cdf_ok;      // [GO1_VEL_N_CATEGORIES]: cdf current for the weights
+  const CkRec* list;    // the selection lists: B at [0, n_envs), A at [n_envs, 2 n_envs)
+  const unsigned long long* cnt;  // their lengths: B low word, A high word
   go1_vel_state st;
   const double* grid;   // (GO1_VEL_N_KEYS, n_bins)
   const int32_t* adj_ptr;  // neighbourhood table (CSR): cells adjacent to bin b are adj_idx[adj_ptr[b] ..]
@@ -879,6 +929,8 @@ struct CArgs {
   int64_t ld_in, ld_out;  // row strides (floats)
   int hist_w;
   int hist_aligned;  // hist_w and both strides % 4 == 0, both buffers 16-byte aligned: 16-byte chunks
+  uint32_t delay;    // test knob (GO1_VEL_CK_DELAY, 0 in use): workgroups 1.. wait this many s_memtime ticks before
+                     // their success counts, so workgroup 0 samples (writes the command state) first
 };
 
 // numpy's pairwise summation (np.add.reduce of a contiguous f64 array), PW_BLOCKSIZE 128
@@ -913,12 +965,11 @@ struct CkShared {
   double w[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // the curriculum weights (committed by the last workgroup)
   int list[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];  // distinct (category, bin) success pairs
   int inc[GO1_VEL_N_CATEGORIES * GO1_VEL_MAX_BINS];   // +0.2 steps per weight cell
-  int sel[2][CK_SEL_CAP];                             // env_ids of the B and the A resample, ascending
-  int wsum[2][CK_THREADS / 64];                       // per-wave selection counts of the ordered compaction
-  int cnt[4];                                         // |sel B|, |sel A|, |list|, last-workgroup flag
+  CkRec rec[2][CK_PRE];                               // the first CK_PRE records of the B and the A list
+  int cnt[4];                                         // |list B|, |list A|, |pairs|, last-workgroup flag
   int dirty[GO1_VEL_N_CATEGORIES];                    // weights changed in this phase
   int pvalid[GO1_VEL_N_CATEGORIES];                   // p holds the cdf of the current weights
-  int rec[GO1_VEL_N_CATEGORIES];                      // p recomputed in this launch (the cache to commit)
+  int rec_[GO1_VEL_N_CATEGORIES];                     // p recomputed in this launch (the cache to commit)
   int wchg;                                           // some weight changed in this launch
   int wloaded;                                        // w holds the weights (loaded on first need)
 };
@@ -951,97 +1002,55 @@ __device__ __forceinline__ bool selectedA(const CArgs& K, int e, int R) {
 
 // The launch is latency-bound: a handful of envs per phase behind a chain of barrier-separated sections, and
 // a barrier waits out every memory access in flight.  So each section issues all the memory reads it can at
-// once: the prologue loads both phases' selection flags, the cached cdfs and the weights in one round trip;
-// a phase then costs the success counts (one round trip), the weight update (when some env succeeded), the
-// cdf of changed weights, and the sampling (commands and grid cells together).
-// The prologue's inputs come as the launch's leading scalar arguments (pn .. pcdf_ok, the same values as the
-// CArgs fields): with kernel-argument preloading they arrive in registers with the wave.
-__device__ __forceinline__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S, int pn, int pnb, int pR,
-                                                  int pdoA, const uint8_t* pmaskB, const int32_t* pel,
+// once: the prologue loads the list lengths, the first CK_PRE records of both lists (at clamped positions,
+// before their lengths are known) and the cached cdfs in one round trip; a phase then costs the success counts
+// (LDS only), the weight update (when some env succeeded), the cdf of changed weights, and the sampling
+// (commands and grid cells together).
+// The prologue's inputs come as the launch's leading scalar arguments (the same values as the CArgs fields):
+// with kernel-argument preloading they arrive in registers with the wave.
+__device__ __forceinline__ void resample_prologue(VCfg* v, const CArgs& K, CkShared& S, int pn, int pnb,
+                                                  const unsigned long long* pcnt, const CkRec* plist,
                                                   const double* pcdf, const int32_t* pcdf_ok) {
-  const int tid = threadIdx.x, n = pn, nb = pnb, R = pR;
+  const int tid = threadIdx.x, n = pn, nb = pnb;
 #ifdef GO1_VEL_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
   const int lane = tid & 63, wv = tid >> 6;
+  const unsigned long long cc = *pcnt;
+  const CkRec rB = plist[min(tid, n - 1)], rA = plist[(size_t)n + min(tid, n - 1)];
   for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.hist[i] = 0;
-  if (tid < 4) S.cnt[tid] = 0;
-  if (tid < GO1_VEL_N_CATEGORIES) { S.dirty[tid] = 0; S.rec[tid] = 0; }
-  if (tid == 0) { S.wchg = 0; S.wloaded = 0; }
-  // the cached cdfs (wave c) and the weights (wave 4 + c), whether or not a phase will need them
+  if (tid < GO1_VEL_N_CATEGORIES) { S.dirty[tid] = 0; S.rec_[tid] = 0; }
+  if (tid == 0) { S.wchg = 0; S.wloaded = 0; S.cnt[2] = 0; S.cnt[3] = 0; }
+  // the cached cdfs (wave c), whether or not a phase will need them
   double t[GO1_VEL_MAX_BINS / 64];
   int ok = 0;
   if (wv < GO1_VEL_N_CATEGORIES) {  // the weights are loaded only when a phase needs them (ensure_weights)
     const int c = wv & 3;
     const double* g = pcdf + (size_t)c * nb;
-    if (wv < GO1_VEL_N_CATEGORIES) ok = pcdf_ok[c];
+    ok = pcdf_ok[c];
     // unconditional loads (index clamped): a load under a condition makes hipcc wait for it right away
 #pragma unroll
     for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i) t[i] = g[min(lane + 64 * i, nb - 1)];
   }
-  // env_ids of both phases, compacted in ascending order: thread t takes a contiguous run of envs (its flags
-  // loaded before any is tested), one block-wide exclusive scan of the (B, A) counts places each run; beyond
-  // CK_SEL_CAP selected envs (a full reset) a phase scans the flags again instead
-  int base[2] = {0, 0};
-  for (int e0 = 0; e0 < n; e0 += CK_THREADS * CK_BATCH) {
-    const int span = min(CK_THREADS * CK_BATCH, n - e0), per = (span + CK_THREADS - 1) / CK_THREADS;
-    const int eb = e0 + tid * per;
-    bool sb[CK_BATCH], sa[CK_BATCH];
-    int v = 0;
-    // the flags of the run: unconditional loads at clamped indices (no wait per load), then the tests
-    const uint8_t* mB = pmaskB ? pmaskB : reinterpret_cast<const uint8_t*>(pel);
-    uint8_t fb[CK_BATCH];
-    int el[CK_BATCH];
-#pragma unroll
-    for (int k = 0; k < CK_BATCH; ++k) {
-      const int ec = min(eb + k, n - 1);
-      fb[k] = mB[ec];
-      el[k] = pel[ec];
-    }
-#pragma unroll
-    for (int k = 0; k < CK_BATCH; ++k) {
-      const int e = eb + k;
-      const bool ok = k < per && e < e0 + span;
-      sb[k] = ok && pmaskB != nullptr && fb[k] != 0;
-      sa[k] = ok && pdoA && (el[k] + 1) % R == 0;
-      v += (sb[k] ? 1 : 0) + (sa[k] ? 1 << 16 : 0);
-    }
-    int inc = v;  // inclusive scan over the wave
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(inc, o);
-      inc += lane >= o ? u : 0;
-    }
-    if (lane == 63) S.wsum[0][wv] = inc;
-    __syncthreads();
-    int pre = 0, tot = 0;
-    for (int w = 0; w < CK_THREADS / 64; ++w) {
-      const int c = S.wsum[0][w];
-      pre += w < wv ? c : 0;
-      tot += c;
-    }
-    const int ex = pre + inc - v;
-    int ob = base[0] + (ex & 0xffff), oa = base[1] + (ex >> 16);
-#pragma unroll
-    for (int k = 0; k < CK_BATCH; ++k) {
-      if (sb[k]) { if (ob < CK_SEL_CAP) S.sel[0][ob] = eb + k; ++ob; }
-      if (sa[k]) { if (oa < CK_SEL_CAP) S.sel[1][oa] = eb + k; ++oa; }
-    }
-    base[0] += tot & 0xffff;
-    base[1] += tot >> 16;
-    __syncthreads();  // wsum is rewritten by the next pass
-  }
-  if (tid == 0) { S.cnt[0] = base[0]; S.cnt[1] = base[1]; }
+  const int nB = (int)(uint32_t)cc, nA = (int)(uint32_t)(cc >> 32);
+  if (tid == 0) { S.cnt[0] = nB; S.cnt[1] = nA; }
+  if (tid < nB) S.rec[0][tid] = rB;
+  if (tid < nA) S.rec[1][tid] = rA;
   if (wv < GO1_VEL_N_CATEGORIES) {
     const int c = wv & 3;
     double* dst = S.p + (size_t)c * GO1_VEL_MAX_BINS;
 #pragma unroll
     for (int i = 0; i < GO1_VEL_MAX_BINS / 64; ++i)
       if (lane + 64 * i < nb) dst[lane + 64 * i] = t[i];
-    if (lane == 0 && wv < GO1_VEL_N_CATEGORIES) S.pvalid[c] = ok;
+    if (lane == 0) S.pvalid[c] = ok;
   }
   __syncthreads();
   VSTAMP(0, 10, t0);
+}
+
+// record i of a phase's list (ph 0: B, 1: A)
+__device__ __forceinline__ CkRec ck_rec(const CArgs& K, const CkShared& S, int ph, int i) {
+  return i < CK_PRE ? S.rec[ph][i] : K.list[(size_t)ph * K.n_envs + i];
 }
 
 // searchsorted(cdf, u, side='right') clipped to the last bin (numpy's choice)
@@ -1077,58 +1086,44 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
 #ifdef GO1_VEL_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-  auto selected = [&](int e) { return kindB ? selectedB(K, e) : selectedA(K, e, R); };
   const int count = S.cnt[ph];
-  const int* sel = S.sel[ph];
   VSTAMP(ph, 0, t0);
   if (count == 0) return;  // len(env_ids) == 0 (:730): nothing, not even the time-out rebinding
   VSTAMP(ph, 15, t0);
-  const bool listed = count <= CK_SEL_CAP;
-  auto for_selected = [&](auto&& fn) {
-    if (listed) {
-      for (int i = tid; i < count; i += CK_THREADS) fn(sel[i]);
-    } else {
-      for (int e = tid; e < n; e += CK_THREADS)
-        if (selected(e)) fn(e);
-    }
-  };
+  if (K.delay && blk > 0) {  // test knob only (tests/test_gpu_velocity.py)
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t1 < (unsigned long long)K.delay) __builtin_amdgcn_s_sleep(16);
+  }
   // ---- RewardThresholdCurriculum.update per old category (:736-757, curriculum.py:135-154): success
-  // counts per (category, bin), and the list of the (category, bin) pairs that have any
-  for_selected([&](int e) {
-    if (v->n_task == 0) return;
-    int cat, b;
-    bool ok = true;
+  // counts per (category, bin), and the list of the (category, bin) pairs that have any.  The inputs come
+  // from the records (the state at the end of the step), never from the command state the sampling rewrites.
+  for (int i = tid; i < count; i += CK_THREADS) {
+    if (v->n_task == 0) break;
+    const CkRec r = ck_rec(K, S, ph, i);
+    const int e = r.x;
+    int cat = r.y, b = r.z;
+    bool ok = r.w != 0;
     if (!kindB && selectedB(K, e)) {
       // phase B resampled this env: its sums are zero and its category / bin are phase B's draws, recomputed
       // here from phase B's uniforms and cdf (S.p still holds it: phase A's cdf comes after these counts)
       const Rng rng = {K.UB, K.seed, K.stepB, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
       const RngD rngd = {K.UDB, K.seed, K.stepB, e, e + K.env_id_offset};
-      cat = draw_category(rng(GO1_VEL_U_CAT_B));
-      if (cat >= 0) {
+      const int cb = draw_category(rng(GO1_VEL_U_CAT_B));
+      if (cb >= 0) {
+        cat = cb;
         b = cdf_search(S.p + (size_t)cat * GO1_VEL_MAX_BINS, nb, rngd(GO1_VEL_D_CHOICE_B));
-      } else {
-        cat = st.command_categories[e];
-        b = st.command_bins[e];
       }
+      ok = true;
       for (int k = 0; k < v->n_task; ++k) ok = ok && (0.0f / v->curriculum_ep_len > v->task_threshold[k]);
-    } else {
-      cat = st.command_categories[e];
-      b = st.command_bins[e];
-      float sm[4];  // every task's sum loaded (slot clamped) before any is tested
-#pragma unroll
-      for (int k = 0; k < 4; ++k) sm[k] = st.command_sums[(size_t)e * NC + v->task_slot[min(k, v->n_task - 1)]];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (k < v->n_task) ok = ok && (sm[k] / v->curriculum_ep_len > v->task_threshold[k]);
     }
-    if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES) return;
+    if (cat < 0 || cat >= GO1_VEL_N_CATEGORIES) continue;
     if (ok && b >= 0 && b < nb) {
       if (atomicAdd(&S.hist[cat * nb + b], 1) == 0) {
         const int slot = atomicAdd(&S.cnt[2], 1);
         S.list[slot] = cat * nb + b;  // at most GO1_VEL_N_CATEGORIES * nb distinct pairs
       }
     }
-  });
+  }
   if (kindB && K.extras_time_outs)  // this workgroup's share of the rebinding
     for (int e = blk * CK_THREADS + tid; e < n; e += nblk * CK_THREADS) K.extras_time_outs[e] = K.time_out[e];
   __syncthreads();
@@ -1211,7 +1206,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
       for (int j = ln; j < nb; j += 64) p[j] = p[j] / last;
       if (ln == 0) {
         S.pvalid[wv] = 1;
-        S.rec[wv] = 1;
+        S.rec_[wv] = 1;
         S.dirty[wv] = 0;
       }
 #ifdef GO1_VEL_STAMPS
@@ -1229,17 +1224,11 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   // they and the grid cells share one memory round trip.
   {
     const int sub = tid & 15, grp = tid >> 4;
-    const int n_own = listed ? (count > blk ? (count - blk + nblk - 1) / nblk : 0)
-                             : (n > blk ? (n - blk + nblk - 1) / nblk : 0);
+    const int n_own = count > blk ? (count - blk + nblk - 1) / nblk : 0;
     for (int i0 = 0; i0 < n_own; i0 += CK_THREADS / 16) {
       const int i = i0 + grp;
-      int e = -1;
-      if (i < n_own) {
-        const int pos = blk + i * nblk;
-        if (listed) e = sel[pos];
-        else if (selected(pos)) e = pos;
-      }
-      if (e < 0) continue;  // uniform over the env's 16 lanes
+      if (i >= n_own) continue;  // uniform over the env's 16 lanes
+      const int e = ck_rec(K, S, ph, blk + i * nblk).x;
       // an env phase A resamples again: phase A writes its state, phase B only its observed commands
       const bool state_out = !(kindB && selectedA(K, e, R));
       const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
@@ -1305,7 +1294,7 @@ __device__ void resample_commit(VCfg* v, const CArgs& K, CkShared& S) {
   __syncthreads();
   // every workgroup takes the same decisions: with no weight changed and no cdf recomputed there is nothing
   // to commit, and none of them takes a ticket
-  if (!S.wchg && !S.rec[0] && !S.rec[1] && !S.rec[2] && !S.rec[3]) return;
+  if (!S.wchg && !S.rec_[0] && !S.rec_[1] && !S.rec_[2] && !S.rec_[3]) return;
 #ifdef GO1_VEL_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1319,12 +1308,12 @@ __device__ void resample_commit(VCfg* v, const CArgs& K, CkShared& S) {
   if (!S.cnt[3]) return;
   for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
     const int c = i / nb, j = i - c * nb;
-    if (S.rec[c]) {  // a category whose weights changed had its cdf recomputed
+    if (S.rec_[c]) {  // a category whose weights changed had its cdf recomputed
       K.st.curriculum_weights[i] = S.w[(size_t)c * GO1_VEL_MAX_BINS + j];
       K.cdf[i] = S.p[(size_t)c * GO1_VEL_MAX_BINS + j];
     }
   }
-  if (tid < GO1_VEL_N_CATEGORIES && S.rec[tid]) K.cdf_ok[tid] = 1;
+  if (tid < GO1_VEL_N_CATEGORIES && S.rec_[tid]) K.cdf_ok[tid] = 1;
   if (tid == 0) *K.done = 0;  // the next launch's count (stream order)
   VSTAMP(0, 11, t0);
 }
@@ -1390,20 +1379,69 @@ __device__ void hist_shift(const CArgs& K, size_t g0, size_t G) {
 }
 
 __global__ __launch_bounds__(CK_THREADS) void go1_vel_curriculum_kernel(const go1_vel_config* __restrict__ v_gen,
-                                                                        int pn, int pnb, int pR, int pdoA,
-                                                                        const uint8_t* pmaskB, const int32_t* pel,
-                                                                        const double* pcdf, const int32_t* pcdf_ok,
-                                                                        CArgs K) {
+                                                                        int pn, int pnb,
+                                                                        const unsigned long long* pcnt,
+                                                                        const CkRec* plist, const double* pcdf,
+                                                                        const int32_t* pcdf_ok, CArgs K) {
   VCfg* __restrict__ v = (VCfg*)v_gen;
   if ((int)blockIdx.x >= K.nblk) {
     hist_shift(K, (size_t)(blockIdx.x - K.nblk) * CK_THREADS + threadIdx.x, (size_t)(gridDim.x - K.nblk) * CK_THREADS);
     return;
   }
   __shared__ CkShared S;
-  resample_prologue(v, K, S, pn, pnb, pR, pdoA, pmaskB, pel, pcdf, pcdf_ok);
+  resample_prologue(v, K, S, pn, pnb, pcnt, plist, pcdf, pcdf_ok);
   if (K.maskB) resample_phase(v, K, true, S);
   if (K.doA) resample_phase(v, K, false, S);
   resample_commit(v, K, S);
+}
+
+// The selection lists of an explicit resample (go1_vel_resample: reset_idx's mask, or the interval envs) in
+// ascending env order, one workgroup: thread t takes a contiguous run of envs, a block-wide scan places the
+// runs.  The records carry the state the curriculum's success counts read.
+__global__ __launch_bounds__(CK_THREADS) void go1_vel_list_kernel(const go1_vel_config* __restrict__ v_gen, CArgs K,
+                                                                  CkRec* list, unsigned long long* cnt) {
+  VCfg* __restrict__ v = (VCfg*)v_gen;
+  __shared__ int wsum[2][CK_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, n = K.n_envs, R = K.R;
+  const int NC = v->n_terms + GO1_VEL_SUM_EXTRA;
+  const int per = (n + CK_THREADS - 1) / CK_THREADS, eb = tid * per;
+  int cb = 0, ca = 0;
+  for (int k = 0; k < per; ++k) {
+    const int e = eb + k;
+    if (e < n) {
+      cb += selectedB(K, e) ? 1 : 0;
+      ca += selectedA(K, e, R) ? 1 : 0;
+    }
+  }
+  int ib = cb, ia = ca;  // inclusive scans over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int ub = __shfl_up(ib, o), ua = __shfl_up(ia, o);
+    ib += lane >= o ? ub : 0;
+    ia += lane >= o ? ua : 0;
+  }
+  if (lane == 63) { wsum[0][wv] = ib; wsum[1][wv] = ia; }
+  __syncthreads();
+  int ob = ib - cb, oa = ia - ca, totb = 0, tota = 0;
+  for (int w = 0; w < CK_THREADS / 64; ++w) {
+    ob += w < wv ? wsum[0][w] : 0;
+    oa += w < wv ? wsum[1][w] : 0;
+    totb += wsum[0][w];
+    tota += wsum[1][w];
+  }
+  for (int k = 0; k < per; ++k) {
+    const int e = eb + k;
+    if (e >= n) break;
+    const bool sb = selectedB(K, e), sa = selectedA(K, e, R);
+    if (!sb && !sa) continue;
+    bool ok = true;
+    for (int t = 0; t < v->n_task; ++t)
+      ok = ok && (K.st.command_sums[(size_t)e * NC + v->task_slot[t]] / v->curriculum_ep_len > v->task_threshold[t]);
+    const CkRec r = make_int4(e, K.st.command_categories[e], K.st.command_bins[e], ok ? 1 : 0);
+    if (sb) list[ob++] = r;
+    if (sa) list[(size_t)n + oa++] = r;
+  }
+  if (tid == 0) *cnt = (unsigned long long)(uint32_t)totb | ((unsigned long long)(uint32_t)tota << 32);
 }
 
 // =====================================================================
@@ -1432,6 +1470,10 @@ struct go1_vel_handle {
   int32_t* d_adj_ptr = nullptr;  // neighbourhood table of the curriculum update (CSR over the bins)
   int32_t* d_adj_idx = nullptr;
   int32_t* d_done = nullptr;     // completion count of the curriculum workgroups (zero between launches)
+  CkRec* d_clist = nullptr;      // selection lists: 3 slots (steps alternate 0 / 1, explicit resamples 2) x (B, A)
+  unsigned long long* d_ccnt = nullptr;  // their lengths per slot (B low word, A high word)
+  int slot = 0;                  // the next step's slot
+  uint32_t ck_delay = 0;         // CArgs.delay (GO1_VEL_CK_DELAY at create; tests only)
   go1_vel_state st;
   const float* env_origins = nullptr;
   bool bound = false;
@@ -1467,6 +1509,7 @@ static CArgs curriculum_args(go1_vel_handle* h) {
   K.R = h->vcfg.resample_interval;
   K.nblk = curriculum_blocks(h->cfg.n_envs);
   K.done = h->d_done;
+  K.delay = h->ck_delay;
   return K;
 }
 
@@ -1503,12 +1546,15 @@ int go1_vel_create(const go1_config* cfg, const go1_vel_config* vel, const doubl
   if (!h) return vfail(GO1_E_ARG, "go1_vel_create: out of host memory");
   h->cfg = *cfg;
   h->vcfg = *vel;
+  if (const char* d = getenv("GO1_VEL_CK_DELAY")) h->ck_delay = (uint32_t)strtoul(d, nullptr, 10);
   const size_t gsz = (size_t)GO1_VEL_N_KEYS * vel->n_bins * sizeof(double);
   const size_t csz = (size_t)GO1_VEL_N_CATEGORIES * vel->n_bins * sizeof(double);
   if (hipMalloc(&h->d_cfg, sizeof(go1_config)) != hipSuccess || hipMalloc(&h->d_vcfg, sizeof(go1_vel_config)) != hipSuccess ||
       hipMalloc(&h->d_grid, gsz) != hipSuccess || hipMalloc(&h->d_cdf, csz) != hipSuccess ||
       hipMalloc(&h->d_cdf_ok, GO1_VEL_N_CATEGORIES * sizeof(int32_t)) != hipSuccess ||
-      hipMalloc(&h->d_mask, cfg->n_envs) != hipSuccess || hipMalloc(&h->d_done, sizeof(int32_t)) != hipSuccess) {
+      hipMalloc(&h->d_mask, cfg->n_envs) != hipSuccess || hipMalloc(&h->d_done, sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&h->d_clist, (size_t)6 * cfg->n_envs * sizeof(CkRec)) != hipSuccess ||
+      hipMalloc(&h->d_ccnt, 3 * sizeof(unsigned long long)) != hipSuccess) {
     go1_vel_destroy(h);
     return vfail(GO1_E_HIP, "go1_vel_create: hipMalloc failed");
   }
@@ -1539,6 +1585,8 @@ int go1_vel_create(const go1_config* cfg, const go1_vel_config* vel, const doubl
   }
   VHIP_TRY(hipMemset(h->d_cdf_ok, 0, GO1_VEL_N_CATEGORIES * sizeof(int32_t)));
   VHIP_TRY(hipMemset(h->d_done, 0, sizeof(int32_t)));
+  VHIP_TRY(hipMemset(h->d_ccnt, 0, 3 * sizeof(unsigned long long)));
+  VHIP_TRY(hipMemset(h->d_clist, 0, (size_t)6 * cfg->n_envs * sizeof(CkRec)));
   *out = h;
   return GO1_OK;
 }
@@ -1619,7 +1667,15 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   K.env_origins = h->env_origins;
   K.hist_w = hist_w;
   K.hist_ld = ld_out;
+  const int slot = h->slot;
+  h->slot ^= 1;
+  K.clist = h->d_clist + (size_t)slot * 2 * n;
+  K.ccnt = h->d_ccnt + slot;
+  K.czero = h->d_ccnt + (slot ^ 1);
+  K.doA = a->resample_next ? 1 : 0;
   CArgs C = curriculum_args(h);
+  C.list = K.clist;
+  C.cnt = K.ccnt;
   C.hist_in = window ? nullptr : a->obs_history_in;
   C.hist_out = a->obs_history_out;
   C.ld_in = ld_in;
@@ -1653,8 +1709,8 @@ int go1_vel_step(go1_vel_handle* h, const go1_vel_step_args* a, void* stream) {
   const int shift_blocks =
       C.hist_in ? (int)std::min<size_t>(256 - C.nblk, std::max<size_t>(1, (chunks + 4 * CK_THREADS - 1) / (4 * CK_THREADS)))
                 : 0;
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C.n_envs, C.nb, C.R, C.doA,
-                     C.maskB, C.episode_length, C.cdf, C.cdf_ok, C);
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk + shift_blocks), dim3(CK_THREADS), 0, s, h->d_vcfg, C.n_envs, C.nb,
+                     C.cnt, C.list, C.cdf, C.cdf_ok, C);
   VHIP_TRY(hipGetLastError());
   return GO1_OK;
 }
@@ -1678,8 +1734,13 @@ int go1_vel_resample(go1_vel_handle* h, const uint8_t* mask, const float* unifor
     C.UDA = uniforms_f64;
     C.stepA = rng_step;
   }
-  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C.n_envs, C.nb, C.R, C.doA,
-                     C.maskB, C.episode_length, C.cdf, C.cdf_ok, C);
+  // the lists (slot 2) from the mask / the interval condition, then the curriculum on them
+  C.list = h->d_clist + (size_t)4 * C.n_envs;
+  C.cnt = h->d_ccnt + 2;
+  hipLaunchKernelGGL(go1_vel_list_kernel, dim3(1), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C,
+                     const_cast<CkRec*>(C.list), const_cast<unsigned long long*>(C.cnt));
+  hipLaunchKernelGGL(go1_vel_curriculum_kernel, dim3(C.nblk), dim3(CK_THREADS), 0, (hipStream_t)stream, h->d_vcfg, C.n_envs, C.nb,
+                     C.cnt, C.list, C.cdf, C.cdf_ok, C);
   VHIP_TRY(hipGetLastError());
   return GO1_OK;
 }
@@ -1709,6 +1770,8 @@ int go1_vel_reset_idx(go1_vel_handle* h, const int32_t* ids, int32_t n_ids, cons
 int go1_vel_destroy(go1_vel_handle* h) {
   if (!h) return GO1_OK;
   if (h->d_done) (void)hipFree(h->d_done);
+  if (h->d_clist) (void)hipFree(h->d_clist);
+  if (h->d_ccnt) (void)hipFree(h->d_ccnt);
   if (h->d_cfg) (void)hipFree(h->d_cfg);
   if (h->d_vcfg) (void)hipFree(h->d_vcfg);
   if (h->d_grid) (void)hipFree(h->d_grid);

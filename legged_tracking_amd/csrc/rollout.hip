@@ -14,6 +14,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "../../include/go1_rollout.h"
@@ -166,6 +169,60 @@ __global__ __launch_bounds__(256) void record_kernel(go1_transition tr, int n, f
     tr.st_rewards[e] = r;
     tr.st_values[e] = v;
     tr.st_dones[e] = tr.dones[e] ? 1 : 0;
+  }
+}
+
+// The same copies with one 16-byte chunk per thread and each workgroup on one segment (block ranges per
+// segment, chosen on the host when every buffer is 16-byte aligned and the history is contiguous): every
+// thread issues its single load at once instead of walking the segments one round trip after the other.
+#define REC_MAX_SEGS 8
+struct RecPlan {
+  const float4* src[REC_MAX_SEGS];
+  float4* dst[REC_MAX_SEGS];
+  float4* dst2[REC_MAX_SEGS];  // a second destination (obs_history aliasing obs: one read feeds both rows)
+  int64_t nf[REC_MAX_SEGS];    // floats
+  int first[REC_MAX_SEGS + 1]; // first workgroup of each segment; first[nseg] = the env columns' first
+  int nseg;
+};
+__global__ __launch_bounds__(256) void record_flat_kernel(RecPlan P, go1_transition tr, int n, float gamma) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (b >= P.first[P.nseg]) {  // per-env columns: bootstrap reward, value, done
+    const int64_t e = (int64_t)(b - P.first[P.nseg]) * 256 + t;
+    if (e >= n) return;
+    // every column requested before any is used (both time-out arrays: the flag picks one afterwards)
+    const float v = tr.values[e];
+    float r = tr.rewards[e];
+    const uint8_t d = tr.dones[e];
+    const uint8_t* tn_p = tr.time_outs ? tr.time_outs : tr.dones;
+    const uint8_t* tp_p = tr.time_outs_pending ? tr.time_outs_pending : tr.dones;
+    const uint8_t tn = tn_p[e], tp = tp_p[e];
+    const bool rebind = tr.time_outs_flag && *tr.time_outs_flag != 0;
+    if (rebind ? tr.time_outs_pending != nullptr : tr.time_outs != nullptr) {
+      const uint8_t tt = rebind ? tp : tn;
+      if (rebind && tr.time_outs_dst) tr.time_outs_dst[e] = tt;
+      r = r + gamma * (v * (tt ? 1.0f : 0.0f));
+    }
+    tr.st_rewards[e] = r;
+    tr.st_values[e] = v;
+    tr.st_dones[e] = d ? 1 : 0;
+    return;
+  }
+  int s = 0;  // the workgroup's segment (uniform)
+  while (s + 1 < P.nseg && b >= P.first[s + 1]) ++s;
+  const int64_t k = (int64_t)(b - P.first[s]) * 256 + t, n4 = P.nf[s] >> 2;
+  const float4* src = P.src[s];
+  float4* dst = P.dst[s];
+  float4* dst2 = P.dst2[s];
+  if (k < n4) {
+    const float4 v = src[k];
+    dst[k] = v;
+    if (dst2) dst2[k] = v;
+  }
+  const int rem = (int)(P.nf[s] & 3);
+  if (b == P.first[s] && t < rem) {  // the last nf % 4 floats
+    const float x = reinterpret_cast<const float*>(src)[4 * n4 + t];
+    reinterpret_cast<float*>(dst)[4 * n4 + t] = x;
+    if (dst2) reinterpret_cast<float*>(dst2)[4 * n4 + t] = x;
   }
 }
 
@@ -1217,6 +1274,41 @@ int go1_record_transition(const go1_transition* tr, int32_t n_envs, float gamma,
     return fail(GO1_RT_E_ARG, "go1_record_transition: obs_history_ld < num_obs_history");
   go1_transition T = *tr;
   if (T.obs_history_ld == 0) T.obs_history_ld = T.num_obs_history;
+  {  // the flat form when every buffer is 16-byte aligned and the history contiguous
+    const Seg segs[7] = {{T.obs, T.st_obs, (int64_t)n_envs * T.num_obs},
+                         {T.privileged_obs, T.st_privileged_obs, (int64_t)n_envs * T.num_priv},
+                         {T.obs_history, T.st_obs_history, (int64_t)n_envs * T.num_obs_history},
+                         {T.actions, T.st_actions, (int64_t)n_envs * T.num_actions},
+                         {T.mu, T.st_mu, (int64_t)n_envs * T.num_actions},
+                         {T.sigma, T.st_sigma, (int64_t)n_envs * T.num_actions},
+                         {T.actions_log_prob, T.st_actions_log_prob, (int64_t)n_envs}};
+    const char* fe = std::getenv("GO1_RECORD_FLAT");  // "0": the segment-walking kernel (A/B)
+    bool flat = T.obs_history_ld == T.num_obs_history && !(fe && fe[0] == '0');
+    for (int i = 0; i < 7; ++i)
+      if (segs[i].src && segs[i].n > 0)
+        flat = flat && ((((uintptr_t)segs[i].src) | ((uintptr_t)segs[i].dst)) & 15) == 0;
+    if (flat) {
+      RecPlan P;
+      memset(&P, 0, sizeof(P));
+      const bool alias = T.obs && T.obs_history == T.obs && T.num_obs == T.num_obs_history;
+      int blk = 0;
+      for (int i = 0; i < 7; ++i) {
+        if (!segs[i].src || segs[i].n <= 0 || (i == 2 && alias)) continue;
+        const int s = P.nseg++;
+        P.src[s] = reinterpret_cast<const float4*>(segs[i].src);
+        P.dst[s] = reinterpret_cast<float4*>(segs[i].dst);
+        P.dst2[s] = (i == 0 && alias) ? reinterpret_cast<float4*>(T.st_obs_history) : nullptr;
+        P.nf[s] = segs[i].n;
+        P.first[s] = blk;
+        blk += (int)std::max<int64_t>(1, ((segs[i].n >> 2) + 255) / 256);
+      }
+      P.first[P.nseg] = blk;
+      blk += (n_envs + 255) / 256;
+      hipLaunchKernelGGL(record_flat_kernel, dim3(blk), dim3(256), 0, (hipStream_t)stream, P, T, n_envs, gamma);
+      RT_TRY(hipGetLastError());
+      return GO1_OK_RT;
+    }
+  }
   int64_t big = (int64_t)n_envs * (tr->num_obs + tr->num_obs_history);
   int blocks = (int)((big / 4 + 255) / 256);
   blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);

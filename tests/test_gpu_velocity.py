@@ -186,7 +186,14 @@ def synthetic_physics(rng, S, n):
     return dict(dof=dof, root=root, contact=contact, feet=feet)
 
 
-def test_vel_full_size_parity_with_oracle():
+@pytest.mark.parametrize("delay", [0, 400000])
+def test_vel_full_size_parity_with_oracle(delay, monkeypatch):
+    """delay > 0: the curriculum launch's workgroups 1..15 wait ~0.1-0.2 ms (GO1_VEL_CK_DELAY, s_memtime ticks)
+    before their success counts, so workgroup 0 has sampled its envs -- rewritten their categories, bins and
+    command sums -- by then (the counts must not read state another workgroup writes in the same
+    launch; they read the step kernel's records).  Weights, bins and commands stay bit-exact."""
+    if delay:
+        monkeypatch.setenv("GO1_VEL_CK_DELAY", str(delay))
     n = 4096
     cfg, sim, P, names = make(n)
     eo = VEL.plane_env_origins(n, cfg)

@@ -599,3 +599,43 @@ def test_policy_and_record_read_row_strided_history_windows():
         st.add_transitions(t, 0.99)
         torch.cuda.synchronize()
         assert torch.equal(st.observation_histories[step], buf[:, off:off + hist])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,alias", [(4096, False), (4096, True), (777, False), (16, True)])
+def test_record_flat_kernel_equals_segment_kernel(n, alias, monkeypatch):
+    """process_env_step's record (rollout_storage.py:76-90 add_transitions + the time-out bootstrap ppo.py:85-87):
+    the flat kernel (one 16-byte chunk per thread, a segment per workgroup; the default when every buffer is
+    16-byte aligned) writes exactly what the segment-walking kernel (GO1_RECORD_FLAT=0) writes -- with obs and
+    obs_history one tensor (the README configuration: history depth 1) or two, ragged sizes, time-outs."""
+    kern = R.HipRolloutKernels()
+    nh = 261
+    g = torch.Generator(device="cuda").manual_seed(n + alias)
+    outs = {}
+    data = []
+    for step in range(3):
+        t = R.RolloutStorage.Transition()
+        t.observations = torch.randn(n, nh, device="cuda", generator=g)
+        t.observation_histories = t.observations if alias else torch.randn(n, nh, device="cuda", generator=g)
+        t.privileged_observations = torch.randn(n, 2, device="cuda", generator=g)
+        t.actions = torch.randn(n, 12, device="cuda", generator=g)
+        t.action_mean = torch.randn(n, 12, device="cuda", generator=g)
+        t.action_sigma = torch.rand(n, 12, device="cuda", generator=g)
+        t.actions_log_prob = torch.randn(n, device="cuda", generator=g)
+        t.values = torch.randn(n, 1, device="cuda", generator=g)
+        t.rewards = torch.randn(n, device="cuda", generator=g)
+        t.dones = torch.rand(n, device="cuda", generator=g) < 0.1
+        t.time_outs = torch.rand(n, device="cuda", generator=g) < 0.5
+        data.append(t)
+    for flat in ("1", "0"):
+        monkeypatch.setenv("GO1_RECORD_FLAT", flat)
+        st = R.RolloutStorage(n, 3, [nh], [2], [nh], [12], device="cuda:0", kernels=kern)
+        for t in data:
+            st.add_transitions(t, 0.99)
+        torch.cuda.synchronize()
+        outs[flat] = {k: getattr(st, k).clone() for k in ("observations", "privileged_observations",
+                                                          "observation_histories", "actions", "mu", "sigma",
+                                                          "actions_log_prob", "values", "rewards", "dones")}
+    for k, v in outs["0"].items():
+        assert torch.equal(outs["1"][k], v), k
+    assert torch.equal(outs["1"]["observations"][1], data[1].observations)
