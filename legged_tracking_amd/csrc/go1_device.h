@@ -14,7 +14,6 @@
 
 #include "../../include/go1_mi355x.h"
 #include "go1_model_consts.h"
-#include "go1_selfpairs.h"
 #include "go1_spec.h"
 static_assert(GO1_MODEL_CONST_FLOATS == GO1_MODEL_FLOATS, "regenerate go1_model_consts.h");
 #include "pmath.h"
@@ -1435,7 +1434,108 @@ struct Phys {
   float pos[3], quat[4];  // base (replicated on the 16 lanes of the env)
   f2 wv[3];               // base angular and linear velocity (world) as (w_i, v_i) pairs
   float q[3], qd[3];                   // this lane's leg
+  int face[2];            // the trunk faces' contact vertices of the control step (face_scan), -1: none
 };
+
+// ---- the trunk box's faces against the heightfields (go1.urdf:53-58, the 0.3762 x 0.0935 x 0.114
+// box; tunnel_fn.py:99-163, the ceiling's downward wedges).  The 8 box corners are contact points of the sub-step
+// (above); a wedge apex or ridge that enters a face between its corners is a grid vertex of the heightfield
+// inside the face's footprint (bilinear cells: a face's deepest point against them is a vertex or on the
+// footprint's boundary).  Once per control step, the env's 16 lanes scan the 10 x 8 vertices around the trunk
+// (5 each, both layers in the halves: floor against the bottom face, ceiling against the top face) and keep, per
+// face, the deepest vertex inside the footprint; depths are compared quantised to 1e-5 m, ties go to the lowest
+// window position, so the choice is a lexicographic maximum (associative: the same in any reduction order, and
+// the oracle's).  Every sim step a penalty force acts at the two chosen vertices (face_force).
+#define FACE_Q 1.0e-5f
+__device__ __forceinline__ int face_key_max(int v) {  // max over the env's 16 lanes (quad, then the rows)
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true));
+  auto a = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  v = max((int)a[0], (int)a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  return max((int)b[0], (int)b[1]);
+}
+__device__ __forceinline__ void face_scan(const Terr& T, const float* R, const float* pos, const float* th, int sub16,
+                                          int* sel) {
+  const float ihs = frcp(T.hs);
+  const bool xl = fabsf(R[0]) >= fabsf(R[3]);  // the window's long side along the world axis nearer the trunk's x
+  const int ci = (int)floorf(fminf(fmaxf(pos[0] * ihs, -16000.0f), 16000.0f));
+  const int cj = (int)floorf(fminf(fmaxf(pos[1] * ihs, -16000.0f), 16000.0f));
+  int key[2] = {-1, -1};
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int v = sub16 + 16 * u, a = v % 10, b = v / 10;
+    const int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+    const int li = i - T.pi0, lj = j - T.pj0;
+    const bool inp = li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
+    const float2 hv = T.patch[min(max(li, 0), PSZX - 1) * PSZY + min(max(lj, 0), PSZY - 1)];
+    const float dx = (float)i * T.hs - pos[0], dy = (float)j * T.hs - pos[1];
+    const f2 dz = f2{hv.x, hv.y} - pos[2];
+    const f2 cx = (R[0] * dx + R[3] * dy) + R[6] * dz, cy = (R[1] * dx + R[4] * dy) + R[7] * dz,
+             cz = (R[2] * dx + R[5] * dy) + R[8] * dz;
+    const f2 pen = f2{cz.x + th[2], th[2] - cz.y};  // floor vertex above the bottom face / ceiling below the top
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const bool in = inp && fabsf(cx[hh]) <= th[0] && fabsf(cy[hh]) <= th[1] && pen[hh] > 0.0f;
+      const int q = (int)fminf(pen[hh] * (1.0f / FACE_Q), 1.0e6f);
+      const int k = in ? (q << 7) | (127 - v) : -1;
+      key[hh] = max(key[hh], k);
+    }
+  }
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int k = face_key_max(key[hh]);
+    const int v = 127 - (k & 127), a = v % 10, b = v / 10;
+    const int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+    sel[hh] = k < 0 ? -1 : ((i + 16384) << 16) | (j + 16384);
+  }
+}
+// the penalty force of the two chosen vertices at the current pose (explicit: the trunk's 5 kg keep h sqrt(k / m)
+// = 0.3 and h d / m = 0.08): normal k depth - d vn along the face normal (base frame +z on the bottom face, -z on
+// the top), regularised Coulomb friction as the point contacts, nothing when the vertex left the footprint.
+// Adds the base-frame wrench (angular, linear pairs) to w and the world force to Fw.
+__device__ __forceinline__ void face_force(const Terr& T, const CP& C, const float* R, const float* pos, const float* vb,
+                                           const float* th, const int* sel, f2* w, float* Fw) {
+  f2 cx, cy, cz;
+  bool ok[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int i = (sel[hh] >> 16) - 16384, j = (sel[hh] & 0xffff) - 16384;
+    const int li = i - T.pi0, lj = j - T.pj0;
+    ok[hh] = sel[hh] >= 0 && li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
+    const float2 hv = T.patch[min(max(li, 0), PSZX - 1) * PSZY + min(max(lj, 0), PSZY - 1)];
+    const float dx = (float)i * T.hs - pos[0], dy = (float)j * T.hs - pos[1], dz = (hh == 0 ? hv.x : hv.y) - pos[2];
+    cx[hh] = (R[0] * dx + R[3] * dy) + R[6] * dz;
+    cy[hh] = (R[1] * dx + R[4] * dy) + R[7] * dz;
+    cz[hh] = (R[2] * dx + R[5] * dy) + R[8] * dz;
+  }
+  const f2 pen = f2{cz.x + th[2], th[2] - cz.y};
+  bool act[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) act[hh] = ok[hh] && fabsf(cx[hh]) <= th[0] && fabsf(cy[hh]) <= th[1] && pen[hh] > 0.0f;
+  if (!__any(act[0] || act[1])) return;
+  const f2 nz = f2{1.0f, -1.0f};
+  // the trunk's velocity at the vertex, base frame: v + w x c
+  const f2 vx = vb[3] + (vb[1] * cz - vb[2] * cy), vy = vb[4] + (vb[2] * cx - vb[0] * cz), vz = vb[5] + (vb[0] * cy - vb[1] * cx);
+  const f2 depth = f2{fminf(pen.x, 2.0f * th[2]), fminf(pen.y, 2.0f * th[2])};
+  const f2 vn = vz * nz;
+  const f2 fn = C.k * depth - C.d * vn;
+  const f2 vt2 = vx * vx + vy * vy;
+  const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
+  const f2 vtn = vt2 * ivt, cm = C.mu * fn;
+  const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
+                   (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
+  const bool ax = act[0] && fn.x > 0.0f, ay = act[1] && fn.y > 0.0f;
+  const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f}, sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
+  const f2 Fx = -(sc * vx), Fy = -(sc * vy), Fz = fa * nz;
+  const f2 mx = cy * Fz - cz * Fy, my = cz * Fx - cx * Fz, mz = cx * Fy - cy * Fx;
+  w[0] += f2{mx.x + mx.y, Fx.x + Fx.y};
+  w[1] += f2{my.x + my.y, Fy.x + Fy.y};
+  w[2] += f2{mz.x + mz.y, Fz.x + Fz.y};
+  const float F[3] = {Fx.x + Fx.y, Fy.x + Fy.y, Fz.x + Fz.y};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Fw[i] += R[3 * i] * F[0] + R[3 * i + 1] * F[1] + R[3 * i + 2] * F[2];
+}
 
 // sum over the 4 roles of a leg (the four 16-lane rows), bitwise identical on every lane
 __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
@@ -1450,21 +1550,29 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
 // in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
 // because the physics keeps every VGPR busy, and LDS answers faster than the caches.
-// ---- self-collision (asset.self_collisions == 0, go1_crawling.py:44; oracle/go1_oracle.c self_forces)
-// Spheres leg * 6 + s (s: thigh 0-2, calf 3-4, foot 5, the contact points below); the 162 sphere pairs and
-// per-sphere slot lists in go1_selfpairs.h (tools/gen_selfpairs.py): the calf and foot spheres against the
-// other legs' spheres; and the calf and foot spheres against the trunk box.  Explicit penalty springs on the
-// overlap, fn = ks pen - ds vn (compressive only), no friction, no added mass (the two bodies sit in
-// different legs' ABA chains).
-// Broad phase in registers: each lane bounds its leg (thigh joint, knee, foot, grown by the largest sphere
-// radius) by an AABB, swaps the four legs' boxes over the quad (DPP) and tests the six leg pairs and the
-// trunk's world AABB; a wave whose envs have no overlapping pair is done.  Otherwise, per env in LDS: the 24
-// spheres as (pos, r), (vel, 0); each lane tests its share of the pairs (k, k + 16, ... for env-local lane k)
-// of the overlapping leg pairs; if some sphere pair overlaps anywhere in the wave, each lane writes the force
-// of each of its pairs (zero when apart) into the pair's slot and every sphere's owner sums its slots in the
-// table's order -- the force on a sphere does not depend on which lane evaluated which pair, and a pair's two
-// spheres get exactly opposite forces.  The box pairs are evaluated by the sphere's own lane.
-#define SELF_ENV_FLOATS (24 * 8 + SELF_NPAIRS_PAD * 4)  // spheres, pair slots
+// ---- self-collision (asset.self_collisions == 0, go1_crawling.py:44: Isaac Gym collides every pair of bodies no
+// joint connects; oracle/go1_oracle.c phys_substep).  Spheres leg * 8 + s (s: thigh 0-2, calf 3-4, foot 5 -- the
+// contact points below -- and the hip capsule's ends 6-7).  Pairs: every sphere of leg la against every sphere of
+// leg lb (la < lb: 64 per leg pair, pair j = 8 a + b of group lp); within a leg the links two joints apart (hip
+// capsule vs calf and foot, thigh vs foot: SELF_SAME_A / _B); the thigh, calf and foot spheres against the trunk
+// box (the hip is the trunk's neighbour).  Explicit penalty springs on the overlap, fn = ks pen - ds vn
+// (compressive only), no friction, no added mass (the bodies sit in different ABA chains, or two joints apart).
+// Broad phase in registers: each lane bounds its leg (thigh joint, knee, foot, hip-capsule ends, grown by their
+// radii) by an AABB in the trunk frame, swaps the four legs' boxes over the quad (DPP) and tests the six leg pairs,
+// the trunk box and the leg's own folded links; a wave whose envs have no candidate is done.  Otherwise, per env in
+// LDS: the 32 spheres as (pos, r), (vel, 0); one candidate group at a time (wave-uniform), the env's 16 lanes
+// evaluate the group's pairs (j = k, k + 16, ... for env-local lane k) into the group's force slots, and each
+// sphere's owner sums its slots in a fixed order -- the force on a sphere does not depend on which lane evaluated
+// which pair, and a pair's two spheres get exactly opposite forces.  Sphere owners: role 0 (thigh 0, thigh 1),
+// role 1 (thigh 2, hip end 6), role 2 (calf 0, calf 1), role 3 (foot, hip end 7).  The box pairs are evaluated by
+// the sphere's own lane.
+#define SELF_NSAME 9
+#define SELF_ENV_FLOATS (32 * 8 + 64 * 4 + 48 * 4)  // spheres, one group's pair forces, the same-leg pair forces
+__device__ __forceinline__ constexpr int self_same_a(int p) { return p < 3 ? 6 : (p < 6 ? 7 : p - 6); }
+__device__ __forceinline__ constexpr int self_same_b(int p) { return p < 6 ? 3 + p % 3 : 5; }
+// the lane's spheres: x half s0, y half s1
+__device__ __forceinline__ int self_s0(int role) { return role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5)); }
+__device__ __forceinline__ int self_s1(int role) { return role == 0 ? 1 : (role == 1 ? 6 : (role == 2 ? 4 : 7)); }
 
 // force on sphere A (world) of the pair (A, B); zero when apart or when the spring no longer compresses
 __device__ __forceinline__ void self_sphere_force(const float4 A, const float4 Av, const float4 B, const float4 Bv,
@@ -1537,112 +1645,131 @@ __device__ __forceinline__ int quad_or(int v) {
   return v | __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);
 }
 
+// leg pairs lp: (0,1) = 0, (0,2) = 1, (0,3) = 2, (1,2) = 3, (1,3) = 4, (2,3) = 5
+__device__ __forceinline__ constexpr int self_la(int lp) { return lp < 3 ? 0 : (lp < 5 ? 1 : 2); }
+__device__ __forceinline__ constexpr int self_lb(int lp) { return lp < 3 ? lp + 1 : (lp < 5 ? lp - 1 : 3); }
+
 // Narrow phase (a wave whose broad phase found a candidate; inline: out of line, the call's saves and
 // restores of the step kernel's ~500 live registers cost more than the narrow phase itself).  sc: this env's
-// LDS scratch, the spheres already written (self_put); the lane's spheres p0 / p1 (-1: a trunk corner).
-// Work per candidate leg pair: its 27 sphere pairs over the env's 16 lanes (two rounds).  Fs: the
-// self-contact world forces on the lane's two points (x, y halves), wb: the trunk reaction wrench of the
-// lane's box contacts (base frame, summed over the env's lanes by the caller).
-__device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, const unsigned short* tpair,
-                                           const short* tslot, int leg, int role, int mask, const float* R,
-                                           const float* pos, const float* vb, const float* th, float Fs[2][3],
-                                           float* wb) {
+// LDS scratch, the spheres already written (self_put).  Fs: the self-contact world forces on the lane's two
+// spheres (x, y halves), wb: the trunk reaction wrench of the lane's box contacts (base frame, summed over the
+// env's lanes by the caller).
+__device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
+                                           const float* R, const float* pos, const float* vb, const float* th,
+                                           float Fs[2][3], float* wb) {
   const float ks = cfg->self_stiffness, ds = cfg->self_damping;
   const int k = 4 * role + leg;
-  const int p0 = role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5));
-  const int p1 = role == 0 ? 1 : (role == 2 ? 4 : -1);
+  const int s0 = self_s0(role), s1 = self_s1(role);
   float4* P = reinterpret_cast<float4*>(sc);
-  float4* FS = reinterpret_cast<float4*>(sc + 24 * 8);
-  // the trunk box, by the lane of the sphere (calf and foot spheres: x halves of roles 2, 3, y half of role 2)
+  float4* FS = reinterpret_cast<float4*>(sc + 32 * 8);
+  float4* FS2 = reinterpret_cast<float4*>(sc + 32 * 8 + 64 * 4);
+  // the trunk box, by the lane of the sphere (thigh, calf and foot: every x half, the y halves of roles 0 and 2)
   if ((mask >> (6 + leg)) & 1) {
-    if (role >= 2) {
-      const int a = leg * 6 + p0;
-      self_box_force(P[2 * a], P[2 * a + 1], R, pos, vb, th, ks, ds, Fs[0], wb);
-    }
-    if (role == 2) {
-      const int a = leg * 6 + p1;
-      self_box_force(P[2 * a], P[2 * a + 1], R, pos, vb, th, ks, ds, Fs[1], wb);
-    }
+    self_box_force(P[2 * (leg * 8 + s0)], P[2 * (leg * 8 + s0) + 1], R, pos, vb, th, ks, ds, Fs[0], wb);
+    if ((role & 1) == 0) self_box_force(P[2 * (leg * 8 + s1)], P[2 * (leg * 8 + s1) + 1], R, pos, vb, th, ks, ds, Fs[1], wb);
   }
-  if (!__any((mask & 63) != 0)) return;
-  unsigned act = 0u;  // bit 2 lp + t: this lane's pair t of leg pair lp overlaps
+  // the cross-leg groups, one at a time through the group's 64 force slots
 #pragma unroll
   for (int lp = 0; lp < 6; ++lp) {
     if (!__any((mask >> lp) & 1)) continue;
+    const int la = self_la(lp), lb = self_lb(lp);
+    const bool on = (mask >> lp) & 1;
+    unsigned act = 0u;  // bit t: this lane's pair k + 16 t overlaps
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < 4; ++t) {
       const int j = k + 16 * t;
-      if (j < 27 && ((mask >> lp) & 1)) {
-        const unsigned e = tpair[lp * 27 + j];
-        const float4 A = P[2 * (e & 0xffu)], B = P[2 * (e >> 8)];
-        const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
-        act |= (d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << (2 * lp + t)) : 0u;
+      const float4 A = P[2 * (la * 8 + (j >> 3))], B = P[2 * (lb * 8 + (j & 7))];
+      const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
+      act |= (on && d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << t) : 0u;
+    }
+    if (!__any(act != 0u)) continue;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = k + 16 * t;
+      float F[3] = {0.0f, 0.0f, 0.0f};
+      if ((act >> t) & 1u) {
+        const int a = la * 8 + (j >> 3), b = lb * 8 + (j & 7);
+        self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
+      }
+      FS[j] = make_float4(F[0], F[1], F[2], 0.0f);
+    }
+    __syncthreads();
+    if (on && (leg == la || leg == lb)) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int s = hh == 0 ? s0 : s1;
+        float x = 0.0f, y = 0.0f, z = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float4 f = leg == la ? FS[8 * s + u] : FS[8 * u + s];
+          x += f.x; y += f.y; z += f.z;
+        }
+        const float sg = leg == la ? 1.0f : -1.0f;
+        Fs[hh][0] += sg * x; Fs[hh][1] += sg * y; Fs[hh][2] += sg * z;
       }
     }
+    __syncthreads();  // the slots are rewritten by the next group
   }
-  if (!__any(act != 0u)) return;
-  // some sphere pair of the wave overlaps: every slot of the candidate leg pairs written, then the owners' sums
+  // the same-leg pairs: 4 legs x 9 over the env's 16 lanes
+  if (__any(((mask >> 10) & 15) != 0)) {
+    unsigned act = 0u;
 #pragma unroll
-  for (int lp = 0; lp < 6; ++lp) {
-    if (!__any((mask >> lp) & 1)) continue;
+    for (int t = 0; t < 3; ++t) {
+      const int j = k + 16 * t, l2 = j / SELF_NSAME, p = j - SELF_NSAME * l2;
+      if (j < 4 * SELF_NSAME && ((mask >> (10 + l2)) & 1)) {
+        const float4 A = P[2 * (l2 * 8 + self_same_a(p))], B = P[2 * (l2 * 8 + self_same_b(p))];
+        const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
+        act |= (d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << t) : 0u;
+      }
+    }
+    if (__any(act != 0u)) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int j = k + 16 * t;
-      if (j < 27 && ((mask >> lp) & 1)) {
+      for (int t = 0; t < 3; ++t) {
+        const int j = k + 16 * t, l2 = j / SELF_NSAME, p = j - SELF_NSAME * l2;
         float F[3] = {0.0f, 0.0f, 0.0f};
-        if ((act >> (2 * lp + t)) & 1u) {
-          const unsigned e = tpair[lp * 27 + j], a = e & 0xffu, b = e >> 8;
+        if ((act >> t) & 1u) {
+          const int a = l2 * 8 + self_same_a(p), b = l2 * 8 + self_same_b(p);
           self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
         }
-        FS[lp * 27 + j] = make_float4(F[0], F[1], F[2], 0.0f);
+        if (j < 4 * SELF_NSAME) FS2[j] = make_float4(F[0], F[1], F[2], 0.0f);
       }
-    }
-  }
-  __syncthreads();
+      __syncthreads();
+      if ((mask >> (10 + leg)) & 1) {
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    const int p = hh == 0 ? p0 : p1;
-    if (p < 0) continue;
-    const short* sl = tslot + (leg * 6 + p) * SELF_SLOTS;
-    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
-    for (int j = 0; j < SELF_SLOTS; ++j) {
-      const int v = sl[j];
-      if (v < 0) break;
-      if (!((mask >> ((v >> 1) / 27)) & 1)) continue;  // a leg pair without candidates: no slot written
-      const float4 f = FS[v >> 1];
-      const float sg = (v & 1) ? -1.0f : 1.0f;
-      s0 += sg * f.x; s1 += sg * f.y; s2 += sg * f.z;
+        for (int hh = 0; hh < 2; ++hh) {
+          const int s = hh == 0 ? s0 : s1;
+#pragma unroll
+          for (int p = 0; p < SELF_NSAME; ++p) {
+            const float sg = self_same_a(p) == s ? 1.0f : (self_same_b(p) == s ? -1.0f : 0.0f);
+            const float4 f = FS2[SELF_NSAME * leg + p];
+            Fs[hh][0] += sg * f.x; Fs[hh][1] += sg * f.y; Fs[hh][2] += sg * f.z;
+          }
+        }
+      }
+      __syncthreads();
     }
-    Fs[hh][0] += s0; Fs[hh][1] += s1; Fs[hh][2] += s2;
   }
 }
 
-// the pair and slot tables (go1_selfpairs.h) copied into LDS once per launch: read from constant memory inside
-// the narrow phase, every entry is a vector load with a full memory latency
-#define SELF_TAB_SHORTS (SELF_NPAIRS_PAD + 24 * SELF_SLOTS)
-__device__ __forceinline__ void self_tables_to_lds(unsigned short* tab, int lane) {
-  for (int i = lane; i < SELF_NPAIRS_PAD; i += 64) tab[i] = SELF_PAIR[i];
-  for (int i = lane; i < 24 * SELF_SLOTS; i += 64) tab[SELF_NPAIRS_PAD + i] = (unsigned short)(&SELF_SLOT[0][0])[i];
-}
-
-// the lane's spheres into this env's LDS scratch (x half p0; y half p1 unless a trunk corner)
-__device__ __forceinline__ void self_put(float* sc, int leg, int role, const f2* pw, const f2* vw, f2 rr) {
-  const int p0 = role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5));
-  const int p1 = role == 0 ? 1 : (role == 2 ? 4 : -1);
+// the lane's spheres into this env's LDS scratch (x half s0, y half s1)
+__device__ __forceinline__ void self_put(float* sc, int leg, int role, const float* p0, const float* v0, float r0,
+                                         const float* p1, const float* v1, float r1) {
   float4* P = reinterpret_cast<float4*>(sc);
-  P[(leg * 6 + p0) * 2] = make_float4(pw[0].x, pw[1].x, pw[2].x, rr.x);
-  P[(leg * 6 + p0) * 2 + 1] = make_float4(vw[0].x, vw[1].x, vw[2].x, 0.0f);
-  if (p1 >= 0) {
-    P[(leg * 6 + p1) * 2] = make_float4(pw[0].y, pw[1].y, pw[2].y, rr.y);
-    P[(leg * 6 + p1) * 2 + 1] = make_float4(vw[0].y, vw[1].y, vw[2].y, 0.0f);
-  }
+  const int a = leg * 8 + self_s0(role), b = leg * 8 + self_s1(role);
+  P[2 * a] = make_float4(p0[0], p0[1], p0[2], r0);
+  P[2 * a + 1] = make_float4(v0[0], v0[1], v0[2], 0.0f);
+  P[2 * b] = make_float4(p1[0], p1[1], p1[2], r1);
+  P[2 * b + 1] = make_float4(v1[0], v1[1], v1[2], 0.0f);
 }
 
 // Broad phase, in registers, in the trunk frame (where the legs keep their places whatever the trunk's
-// pose; world-axis boxes of a yawed trunk overlap every leg): bit lp of the result = leg pair lp's boxes overlap
-// (go1_selfpairs.h order), bit 6 + leg = the leg's calf (knee to foot) box meets the trunk box; the same mask on
-// the env's 16 lanes.  Boxes: the thigh joint, knee and foot grown by the largest sphere radius.
+// pose; world-axis boxes of a yawed trunk overlap every leg): bit lp of the result = leg pair lp's boxes overlap,
+// bit 6 + leg = the leg's thigh and calf box meets the trunk box, bit 10 + leg = the leg's own links two joints
+// apart may touch (the hip capsule's ends against the calf / foot box, the thigh against the foot); the same mask
+// on the env's 16 lanes.  pth, pkn, pft: the thigh joint, knee and foot (world); hc0, hc1: the hip capsule's ends
+// in the trunk frame.
 __device__ __forceinline__ int self_broad(int leg, const float* pth, const float* pkn, const float* pft, float rmax,
+                                          float rthigh, float rfoot, const float* hc0, const float* hc1, float rhip,
                                           const float* R, const float* pos, const float* th) {
   float b[3][3];  // the three points in the trunk frame, R^T (p - pos)
   const float* pts[3] = {pth, pkn, pft};
@@ -1652,28 +1779,33 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
 #pragma unroll
     for (int i = 0; i < 3; ++i) b[k][i] = R[i] * w0 + R[3 + i] * w1 + R[6 + i] * w2;
   }
-  bool o1 = true, o2 = true, o3 = true, ob = true;
+  bool o1 = true, o2 = true, o3 = true, ob = true, ohc = true, otf = true;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const float clo = fminf(b[1][i], b[2][i]) - rmax, chi = fmaxf(b[1][i], b[2][i]) + rmax;  // the calf
-    const float lo = fminf(b[0][i], clo), hi = fmaxf(b[0][i], chi);
+    const float clo = fminf(b[1][i], b[2][i]) - rmax, chi = fmaxf(b[1][i], b[2][i]) + rmax;  // knee .. foot
+    const float tlo = fminf(b[0][i], clo), thi = fmaxf(b[0][i], chi);                       // + the thigh joint
+    const float hlo = fminf(hc0[i], hc1[i]) - rhip, hhi = fmaxf(hc0[i], hc1[i]) + rhip;     // the hip capsule
+    const float lo = fminf(tlo, hlo), hi = fmaxf(thi, hhi);
     o1 = o1 && lo <= quad_xor<1>(hi) && quad_xor<1>(lo) <= hi;
     o2 = o2 && lo <= quad_xor<2>(hi) && quad_xor<2>(lo) <= hi;
     o3 = o3 && lo <= quad_xor<3>(hi) && quad_xor<3>(lo) <= hi;
-    ob = ob && clo <= th[i] && -th[i] <= chi;
+    ob = ob && tlo <= th[i] && -th[i] <= thi;
+    ohc = ohc && hlo <= chi && clo <= hhi;
+    const float t0 = fminf(b[0][i], b[1][i]) - rthigh, t1 = fmaxf(b[0][i], b[1][i]) + rthigh;  // the thigh
+    otf = otf && t0 <= b[2][i] + rfoot && b[2][i] - rfoot <= t1;
   }
-  // leg pairs (leg, leg ^ d): lp(0,1) = 0, (0,2) = 1, (0,3) = 2, (1,2) = 3, (1,3) = 4, (2,3) = 5
   const int lp1 = (leg >> 1) ? 5 : 0;                         // (0,1) / (2,3)
   const int lp2 = (leg & 1) ? 4 : 1;                          // (0,2) / (1,3)
   const int lp3 = (leg == 0 || leg == 3) ? 2 : 3;             // (0,3) / (1,2)
-  int mask = (o1 ? 1 << lp1 : 0) | (o2 ? 1 << lp2 : 0) | (o3 ? 1 << lp3 : 0) | (ob ? 64 << leg : 0);
+  int mask = (o1 ? 1 << lp1 : 0) | (o2 ? 1 << lp2 : 0) | (o3 ? 1 << lp3 : 0) | (ob ? 64 << leg : 0) |
+             ((ohc || otf) ? 1024 << leg : 0);
   return quad_or(mask);
 }
 
 __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
                                              float h, const float* g, float friction, float restitution,
                                              float payload, const Terr& T, int leg, int role, bool cf_out,
-                                             float* cf_raw, float* self_sc, const unsigned short* self_tab) {
+                                             float* cf_raw, float* self_sc, bool face_scan_now) {
 #pragma clang fp contract(on)
   // Model constants are compile-time literals (go1_model_consts.h, checked against the
   // model block by go1_create): no LDS reads or waits for them inside the sub-step loop.
@@ -1706,6 +1838,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   const float hip_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 2];
   const float hip_y0 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 3], hip_y1 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 4];
   float Fhip[3] = {0.0f, 0.0f, 0.0f};  // the hip capsule's world force (the leg's, on every role)
+  float FhS[3] = {0.0f, 0.0f, 0.0f};   // its self-contact part
   float cs[3][2];
   float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
   f2 cjp[3][3], pAp[3][3];  // c_j and the articulated bias force as (angular, linear) pairs
@@ -1820,12 +1953,53 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       float pft[3];  // the foot centre (calf frame offset), for the leg's bounding box
 #pragma unroll
       for (int i = 0; i < 3; ++i) pft[i] = pl[1][i] + Rl[1][3 * i] * foot[0] + Rl[1][3 * i + 1] * foot[1] + Rl[1][3 * i + 2] * foot[2];
-      const int mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), R, S.pos, th);
+      // the hip capsule's ends in the trunk frame: the hip joint + Rx(q_hip) (0, y, 0)
+      const f2 hy = msy * f2{hip_y0, hip_y1};
+      const f2 hcy = origin[1] + cs[0][0] * hy, hcz = origin[2] + cs[0][1] * hy;
+      const float hc0[3] = {origin[0], hcy.x, hcz.x}, hc1[3] = {origin[0], hcy.y, hcz.y};
+      const int mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), thigh_r, foot_r, hc0,
+                                  hc1, hip_r, R, S.pos, th);
       if (__any(mask != 0)) {
-        self_put(self_sc, leg, role, pw, vw, rr);
+        // the lane's second sphere: point b of the contact pass, or on roles 1 and 3 an end of the hip capsule
+        // (world p = pos + R c, v = R (v_b + w_b x c + qd_hip e_x x (c - hip joint)))
+        const bool odd = (role & 1) != 0;
+        const float* hc = role == 1 ? hc0 : hc1;
+        float p1[3], v1[3];
+        {
+          const float rx = hc[1] - origin[1], rz = hc[2] - origin[2];  // e_x x (0, ry, rz) = (0, -rz, ry)
+          const float vh[3] = {vb[3] + (vb[1] * hc[2] - vb[2] * hc[1]), vb[4] + (vb[2] * hc[0] - vb[0] * hc[2]) - S.qd[0] * rz,
+                               vb[5] + (vb[0] * hc[1] - vb[1] * hc[0]) + S.qd[0] * rx};
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const float ph = S.pos[i] + (R[3 * i] * hc[0] + R[3 * i + 1] * hc[1] + R[3 * i + 2] * hc[2]);
+            const float vw_h = R[3 * i] * vh[0] + R[3 * i + 1] * vh[1] + R[3 * i + 2] * vh[2];
+            p1[i] = odd ? ph : pw[i].y;
+            v1[i] = odd ? vw_h : vw[i].y;
+          }
+        }
+        const float p0[3] = {pw[0].x, pw[1].x, pw[2].x}, v0[3] = {vw[0].x, vw[1].x, vw[2].x};
+        self_put(self_sc, leg, role, p0, v0, rr.x, p1, v1, odd ? hip_r : rr.y);
         __syncthreads();
-        self_narrow(cfg, self_sc, self_tab, reinterpret_cast<const short*>(self_tab + SELF_NPAIRS_PAD), leg, role,
-                    mask, R, S.pos, vb, th, Fs, wb);
+        self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
+        // the hip ends' forces (y halves of roles 1 and 3) on the hip link: hip-frame force f = Rh^T F and
+        // moment (0, y, 0) x f, summed over the leg's rows (every role runs the leg's ABA)
+        float hv[8];
+        {
+          const float F0 = odd ? Fs[1][0] : 0.0f, F1 = odd ? Fs[1][1] : 0.0f, F2 = odd ? Fs[1][2] : 0.0f;
+          const float r0 = R[0] * F0 + R[3] * F1 + R[6] * F2, r1 = R[1] * F0 + R[4] * F1 + R[7] * F2,
+                      r2 = R[2] * F0 + R[5] * F1 + R[8] * F2;
+          const float fh1 = cs[0][0] * r1 + cs[0][1] * r2, fh2 = cs[0][0] * r2 - cs[0][1] * r1;
+          const float y = role == 1 ? hy.x : hy.y;
+          hv[0] = y * fh2; hv[1] = -(y * r0); hv[2] = r0; hv[3] = fh1; hv[4] = fh2;
+          hv[5] = F0; hv[6] = F1; hv[7] = F2;
+        }
+        rowsum4_n<8>(hv);
+        pAp[0][0] -= f2{hv[0], hv[2]};
+        pAp[0][1] -= f2{0.0f, hv[3]};
+        pAp[0][2] -= f2{hv[1], hv[4]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) FhS[i] = hv[5 + i];
+        if (odd) { Fs[1][0] = 0.0f; Fs[1][1] = 0.0f; Fs[1][2] = 0.0f; }  // not the trunk corner's
       }
 #pragma unroll
       for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
@@ -2014,6 +2188,13 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     }
   }
   MARK(backward_done);
+  // ---- the trunk faces (face_scan / face_force): the vertices once per control step, the force every sim step
+  f2 wface[3] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
+  float Fface[3] = {0.0f, 0.0f, 0.0f};
+  if (T.patch) {  // the tunnel; on the plane the corners are the faces' deepest points
+    if (face_scan_now) face_scan(T, R, S.pos, th, 4 * role + leg, S.face);
+    face_force(T, C, R, S.pos, vb, th, S.face, wface, Fface);
+  }
   // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
   const float* bb = model;
   const float mscale = (bb[0] + payload) * frcp(bb[0]);
@@ -2026,7 +2207,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
 #pragma unroll
   for (int k = 0; k < 6; ++k) Ip.ac[k] = f2{qsum(Ip.ac[k].x), qsum(Ip.ac[k].y)};
 #pragma unroll
-  for (int i = 0; i < 3; ++i) pp6[i] = f2{qsum(pp6[i].x - fbase[i]), qsum(pp6[i].y - fbase[3 + i])};
+  for (int i = 0; i < 3; ++i) pp6[i] = f2{qsum(pp6[i].x - fbase[i]), qsum(pp6[i].y - fbase[3 + i])} - wface[i];
 #pragma unroll
   for (int i = 0; i < 9; ++i) Ip.b[i] = qsum(Ip.b[i]);
   sip_add(I0, Ip);
@@ -2122,8 +2303,8 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   for (int i = 0; i < 3; ++i) {
     cf_raw[i] = Fpt[i].x;
     cf_raw[3 + i] = Fpt[i].y;
-    cf_raw[6 + i] = Fhip[i];
-    cf_raw[9 + i] = Fbs[i];
+    cf_raw[6 + i] = Fhip[i] + FhS[i];
+    cf_raw[9 + i] = Fbs[i] + (role == 0 && leg == 0 ? Fface[i] : 0.0f);  // summed over the env's lanes (cf_sum)
   }
 }
 

@@ -263,7 +263,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ float2 s_patch[SEPB][PSZX * PSZY + 8];
   __shared__ float s_phys[(LDS_FLOATS + 63) / 64 * 64];
   __shared__ __attribute__((aligned(16))) float s_self[SEPB][SELF_ENV_FLOATS];  // self-collision scratch
-  __shared__ unsigned short s_selftab[SELF_TAB_SHORTS];  // the self-collision pair tables, staged with the model
   // Block = one wave, so LDS needs no barrier here (a wave's LDS operations execute in
   // order).  The model block and the terrain patches are staged with LDS-DMA
   // (global_load_lds: no VGPR round trip, no __syncthreads fence draining the state loads);
@@ -288,22 +287,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int i = 64 * k + lane;
       mv[k] = i < GO1_MODEL_FLOATS ? c_gen->model[i] : c_gen->default_dof_pos[min(i, LDS_FLOATS - 1) - GO1_MODEL_FLOATS];
     }
-    unsigned short tv[(SELF_TAB_SHORTS + 63) / 64];  // the pair tables (clamped unconditional loads)
-#pragma unroll
-    for (int k = 0; k < (SELF_TAB_SHORTS + 63) / 64; ++k) {
-      const int i = 64 * k + lane;
-      const unsigned short a = SELF_PAIR[min(i, SELF_NPAIRS_PAD - 1)];
-      const unsigned short b = (unsigned short)(&SELF_SLOT[0][0])[min(max(i - SELF_NPAIRS_PAD, 0), 24 * SELF_SLOTS - 1)];
-      tv[k] = i < SELF_NPAIRS_PAD ? a : b;
-    }
     MARK(pro_loads_issued);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     MARK(pro_loads_landed);
 #pragma unroll
     for (int k = 0; k < (LDS_FLOATS + 63) / 64; ++k) s_phys[64 * k + lane] = mv[k];  // padded to 64
-#pragma unroll
-    for (int k = 0; k < (SELF_TAB_SHORTS + 63) / 64; ++k)
-      if (64 * k + lane < SELF_TAB_SHORTS) s_selftab[64 * k + lane] = tv[k];
   }
   if (CI(terrain_kind) == 1) {
     T.tile = K.ter.tiles + (size_t)tix * 2 * CI(hf_nx) * CI(hf_ny);
@@ -431,7 +419,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
         phys_substep(c, s_phys, P, torque, h, A.sim_gravity, friction, restitution, payload, T, leg, role, last,
-                     cf_raw, s_self[el], s_selftab);
+                     cf_raw, s_self[el], sub == 0 && k == 0);
       }
 #else
       P.qd[0] += 1e-4f * torque[0]; P.qd[1] += 1e-4f * torque[1]; P.qd[2] += 1e-4f * torque[2];

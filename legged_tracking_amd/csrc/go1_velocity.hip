@@ -229,15 +229,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const float friction = st.friction[e], payload = st.payload[e], restitution = st.restitution[e];
   __shared__ __attribute__((aligned(16))) float s_self[SEPB][SELF_ENV_FLOATS];  // self-collision scratch
-  __shared__ unsigned short s_selftab[SELF_TAB_SHORTS];  // the self-collision pair tables
-  unsigned short tv[(SELF_TAB_SHORTS + 63) / 64];  // loaded with the prologue (clamped, unconditional)
-#pragma unroll
-  for (int k = 0; k < (SELF_TAB_SHORTS + 63) / 64; ++k) {
-    const int i = 64 * k + lane;
-    const unsigned short a = SELF_PAIR[min(i, SELF_NPAIRS_PAD - 1)];
-    const unsigned short b = (unsigned short)(&SELF_SLOT[0][0])[min(max(i - SELF_NPAIRS_PAD, 0), 24 * SELF_SLOTS - 1)];
-    tv[k] = i < SELF_NPAIRS_PAD ? a : b;
-  }
   const float eo_pre[3] = {K.env_origins[(size_t)e * 3], K.env_origins[(size_t)e * 3 + 1],
                            K.env_origins[(size_t)e * 3 + 2]};
   const int ep_in = st.episode_length[e];
@@ -277,10 +268,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (j == 0) scaled[j] = scaled[j] * c->hip_scale_reduction;
   }
 
-  // block = one wave: the table's LDS writes precede every read in the wave's program order
-#pragma unroll
-  for (int k = 0; k < (SELF_TAB_SHORTS + 63) / 64; ++k)
-    if (64 * k + lane < SELF_TAB_SHORTS) s_selftab[64 * k + lane] = tv[k];
   // ---------------- decimation loop (:76-82): lag ring pushed per sim step (:940-942)
   float torque[3], tgt[3];
   float cf_raw[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
@@ -330,7 +317,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int k = 0; k < c->n_internal; ++k) {
         const bool last = (sub == dec - 1) && (k == c->n_internal - 1);
         phys_substep(c, nullptr, P, torque, h, A.sim_gravity, friction, restitution, payload, T, leg, role, last,
-                     cf_raw, s_self[el], s_selftab);
+                     cf_raw, s_self[el], sub == 0 && k == 0);
       }
 #pragma unroll
       for (int j = 0; j < 3; ++j) { q[j] = P.q[j]; qd[j] = P.qd[j]; }

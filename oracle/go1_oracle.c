@@ -538,6 +538,7 @@ static const real CALF_PTS_Z[N_CALF_PTS] = {-0.071, -0.142};
 typedef struct {
   real pos[3], quat[4], v[3], w[3];
   real q[NDOF], qd[NDOF];
+  int face[2]; /* the trunk faces' contact vertices of the control step (face_scan), -1: none */
 } PhysState;
 
 /* world pose/velocity of a point given body pose (Rb, pb) and body spatial velocity
@@ -561,12 +562,17 @@ static void point_force(real Rb[3][3], const real* lp, const real* F, real* fs) 
   for (int i = 0; i < 3; ++i) { fs[i] += n[i]; fs[3 + i] += f[i]; }
 }
 
-/* Self-collision (asset.self_collisions == 0, go1_crawling.py:44; go1_device.h self_collide): spheres
- * leg * 6 + s (s: thigh points 0-2, calf points 3-4, foot 5); pairs: for legs la < lb every (a, b) with a or
- * b a calf / foot sphere, and every calf / foot sphere against the trunk box (half extents trunk_half about
- * the base origin).  Explicit penalty springs fn = ks pen - ds vn on the overlap, compressive only, no
- * friction; the force on the lower sphere id is computed, the other sphere gets its negative, the trunk the
- * box pairs' reaction. */
+/* Self-collision (asset.self_collisions == 0, go1_crawling.py:44: Isaac Gym collides every pair of bodies that
+ * no joint connects; go1_device.h self_narrow): spheres leg * 8 + s (s: thigh points 0-2, calf points 3-4, foot 5,
+ * hip-capsule ends 6-7, the contact spheres of phys_substep); pairs: every sphere of leg la against every sphere
+ * of leg lb (la < lb, 64 per leg pair), within a leg the links two joints apart (hip capsule vs calf and foot,
+ * thigh vs foot: SELF_SAME_A / _B), and the thigh / calf / foot spheres against the trunk box (half extents
+ * trunk_half about the base origin; the hip is the trunk's neighbour).  Explicit penalty springs
+ * fn = ks pen - ds vn on the overlap, compressive only, no friction; the force on the first sphere of a pair is
+ * computed, the other gets its negative, the trunk the box pairs' reaction. */
+#define SELF_NSAME 9
+static const int SELF_SAME_A[SELF_NSAME] = {6, 6, 6, 7, 7, 7, 0, 1, 2};
+static const int SELF_SAME_B[SELF_NSAME] = {3, 4, 5, 3, 4, 5, 5, 5, 5};
 static void self_sphere_force(const real* pa, const real* va, real ra, const real* pb, const real* vb, real rb,
                               real ks, real ds, real* F) {
   real d[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
@@ -619,11 +625,67 @@ static void self_box_force(const real* pa, const real* va, real r, real R[3][3],
   for (int i = 0; i < 3; ++i) { wb[i] += tq[i]; wb[3 + i] += fb[i]; }
 }
 
+/* The trunk box's faces against the heightfields (go1_device.h face_scan / face_force; go1.urdf:53-58,
+ * tunnel_fn.py:99-163): once per control step the deepest grid vertex of the floor inside the bottom face's
+ * footprint and of the ceiling inside the top face's, among the 10 x 8 vertices around the trunk centre (the
+ * window's long side along the world axis nearer the trunk's x), depths compared quantised to 1e-5 m, ties to
+ * the lowest window position; every sim step an explicit penalty force at the two vertices along the face
+ * normal (k depth - d vn, depth capped at the box height) with the regularised Coulomb friction of the point
+ * contacts.  The GPU scans its LDS terrain patch (which holds the trunk's footprint), this restatement the tile
+ * (both clamp at the tile's edges). */
+#define FACE_Q 1.0e-5
+static void face_scan(const TerrainView* T, real R[3][3], const real* pos, const real* th, int* sel) {
+  int xl = fabs(R[0][0]) >= fabs(R[1][0]);
+  int ci = (int)floor(fmin(fmax(pos[0] / T->hs, -16000.0), 16000.0)), cj = (int)floor(fmin(fmax(pos[1] / T->hs, -16000.0), 16000.0));
+  for (int hh = 0; hh < 2; ++hh) {
+    int best = -1;
+    for (int v = 0; v < 80; ++v) {
+      int a = v % 10, b = v / 10;
+      int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+      real d[3] = {i * T->hs - pos[0], j * T->hs - pos[1], tile_at(T, hh == 0 ? 1 : 0, i, j) - pos[2]}, c[3];
+      for (int k = 0; k < 3; ++k) c[k] = R[0][k] * d[0] + R[1][k] * d[1] + R[2][k] * d[2];
+      real pen = hh == 0 ? c[2] + th[2] : th[2] - c[2];
+      if (!(fabs(c[0]) <= th[0] && fabs(c[1]) <= th[1] && pen > 0.0)) continue;
+      int q = (int)fmin(pen / FACE_Q, 1e6);
+      int key = (q << 7) | (127 - v);
+      if (key > best) best = key;
+    }
+    if (best < 0) { sel[hh] = -1; continue; }
+    int v = 127 - (best & 127), a = v % 10, b = v / 10;
+    int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+    sel[hh] = ((i + 16384) << 16) | (j + 16384);
+  }
+}
+/* adds the base-frame wrench (moment about the base origin, force) to wb and the world force to Fw */
+static void face_force(const TerrainView* T, const ContactParams* C, real R[3][3], const real* pos, const real* vb,
+                       const real* th, const int* sel, real* wb, real* Fw) {
+  for (int hh = 0; hh < 2; ++hh) {
+    if (sel[hh] < 0) continue;
+    int i = (sel[hh] >> 16) - 16384, j = (sel[hh] & 0xffff) - 16384;
+    real d[3] = {i * T->hs - pos[0], j * T->hs - pos[1], tile_at(T, hh == 0 ? 1 : 0, i, j) - pos[2]}, c[3];
+    for (int k = 0; k < 3; ++k) c[k] = R[0][k] * d[0] + R[1][k] * d[1] + R[2][k] * d[2];
+    real pen = hh == 0 ? c[2] + th[2] : th[2] - c[2];
+    if (!(fabs(c[0]) <= th[0] && fabs(c[1]) <= th[1] && pen > 0.0)) continue;
+    real nz = hh == 0 ? 1.0 : -1.0;
+    real v[3] = {vb[3] + (vb[1] * c[2] - vb[2] * c[1]), vb[4] + (vb[2] * c[0] - vb[0] * c[2]),
+                 vb[5] + (vb[0] * c[1] - vb[1] * c[0])};
+    real depth = fmin(pen, 2.0 * th[2]), vn = v[2] * nz;
+    real fn = C->k * depth - C->d * vn;
+    if (!(fn > 0.0)) continue;
+    real vt = sqrt(v[0] * v[0] + v[1] * v[1]);
+    real ct = (C->kf * vt > C->mu * fn && vt > 1e-9) ? C->mu * fn / vt : C->kf;
+    real F[3] = {-ct * v[0], -ct * v[1], fn * nz}, m[3];
+    cross3(c, F, m);
+    for (int k = 0; k < 3; ++k) { wb[k] += m[k]; wb[3 + k] += F[k]; }
+    for (int k = 0; k < 3; ++k) Fw[k] += R[k][0] * F[0] + R[k][1] * F[1] + R[k][2] * F[2];
+  }
+}
+
 /* One integrator step of length h with torques tau.  Writes net contact forces
  * per reported body (17 x 3, world) into cf (may be NULL). */
 static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, const real* tau, real h,
                          const real* g, real friction, real restitution, real payload, const TerrainView* T,
-                         real* cf) {
+                         real* cf, int face_scan_now) {
   ContactParams C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction,
                      0.5 * (restitution + (real)cfg->terrain_restitution), cfg->bounce_threshold};
   real R[3][3];
@@ -701,35 +763,45 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       memcpy(vp, vj[l][j], sizeof(vp));
     }
   }
-  /* self-collision forces on the thigh / calf / foot spheres and the trunk's reaction wrench */
-  real Fself[24][3], wself[6] = {0, 0, 0, 0, 0, 0};
+  /* self-collision forces on the thigh / calf / foot / hip-capsule spheres and the trunk's reaction wrench */
+  real Fself[32][3], wself[6] = {0, 0, 0, 0, 0, 0};
   memset(Fself, 0, sizeof(Fself));
   if (cfg->self_stiffness > 0.0f) {
-    real SP[24][3], SV[24][3], SR[24];
+    real SP[32][3], SV[32][3], SR[32];
     for (int l = 0; l < 4; ++l)
-      for (int s6 = 0; s6 < 6; ++s6) {
-        int j = s6 < 3 ? 1 : 2;
+      for (int s8 = 0; s8 < 8; ++s8) {
+        int j = s8 < 3 ? 1 : (s8 < 6 ? 2 : 0);
         real lp[3] = {0, 0, 0};
-        if (s6 < 3) lp[2] = THIGH_PTS_Z[s6];
-        else if (s6 < 5) lp[2] = CALF_PTS_Z[s6 - 3];
-        else { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
-        point_kin(Rw_all[l][j], pw_all[l][j], vj[l][j], lp, SP[l * 6 + s6], SV[l * 6 + s6]);
-        SR[l * 6 + s6] = s6 < 3 ? M->thigh_r : (s6 < 5 ? M->calf_r : M->foot_r);
+        if (s8 < 3) lp[2] = THIGH_PTS_Z[s8];
+        else if (s8 < 5) lp[2] = CALF_PTS_Z[s8 - 3];
+        else if (s8 == 5) { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
+        else lp[1] = ((l & 1) ? -1.0 : 1.0) * M->hip_y[s8 - 6];
+        point_kin(Rw_all[l][j], pw_all[l][j], vj[l][j], lp, SP[l * 8 + s8], SV[l * 8 + s8]);
+        SR[l * 8 + s8] = s8 < 3 ? M->thigh_r : (s8 < 5 ? M->calf_r : (s8 == 5 ? M->foot_r : M->hip_r));
       }
     const real ks = cfg->self_stiffness, ds = cfg->self_damping;
+    /* every sphere pair of two different legs (the force computed on the lower leg's sphere) */
     for (int la = 0; la < 4; ++la)
       for (int lb = la + 1; lb < 4; ++lb)
-        for (int a = 0; a < 6; ++a)
-          for (int b = 0; b < 6; ++b) {
-            if (a < 3 && b < 3) continue;
-            int ia = la * 6 + a, ib = lb * 6 + b;
+        for (int a = 0; a < 8; ++a)
+          for (int b = 0; b < 8; ++b) {
+            int ia = la * 8 + a, ib = lb * 8 + b;
             real F[3];
             self_sphere_force(SP[ia], SV[ia], SR[ia], SP[ib], SV[ib], SR[ib], ks, ds, F);
             for (int i = 0; i < 3; ++i) { Fself[ia][i] += F[i]; Fself[ib][i] -= F[i]; }
           }
+    /* the non-adjacent links of one leg: hip capsule vs calf / foot, thigh vs foot (SELF_SAME_A / _B) */
     for (int l = 0; l < 4; ++l)
-      for (int s6 = 3; s6 < 6; ++s6) {
-        int ia = l * 6 + s6;
+      for (int p2 = 0; p2 < SELF_NSAME; ++p2) {
+        int ia = l * 8 + SELF_SAME_A[p2], ib = l * 8 + SELF_SAME_B[p2];
+        real F[3];
+        self_sphere_force(SP[ia], SV[ia], SR[ia], SP[ib], SV[ib], SR[ib], ks, ds, F);
+        for (int i = 0; i < 3; ++i) { Fself[ia][i] += F[i]; Fself[ib][i] -= F[i]; }
+      }
+    /* the thigh, calf and foot spheres against the trunk box (the hip is the trunk's neighbour) */
+    for (int l = 0; l < 4; ++l)
+      for (int s8 = 0; s8 < 6; ++s8) {
+        int ia = l * 8 + s8;
         real F[3];
         real wb[6] = {0, 0, 0, 0, 0, 0};
         self_box_force(SP[ia], SV[ia], SR[ia], R, S->pos, vb, M->trunk_half, ks, ds, F, wb);
@@ -769,6 +841,7 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
           } else {
             sphere_contact(T, &C, pw, vw, M->hip_r, F);
           }
+          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 8 + 6 + p][i];
           point_force(Rw[j], lp, F, fext);
           if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
         }
@@ -783,7 +856,7 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
           } else {
             sphere_contact(T, &C, pw, vw, M->thigh_r, F);
           }
-          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 6 + p][i];
+          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 8 + p][i];
           point_force(Rw[j], lp, F, fext);
           if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
         }
@@ -801,7 +874,7 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
           } else {
             sphere_contact(T, &C, pw, vw, r, F);
           }
-          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 6 + 3 + p][i];
+          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 8 + 3 + p][i];
           point_force(Rw[j], lp, F, fext);
           int bi = p < N_CALF_PTS ? body_idx : body_idx + 1; /* foot body reported separately */
           if (cf) for (int i = 0; i < 3; ++i) cf[bi * 3 + i] += F[i];
@@ -843,6 +916,14 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
         for (int i = 0; i < 6; ++i) pA0[i] += pp2[i];
       }
     }
+  }
+  /* the trunk faces: vertices once per control step, the force every sim step (the tunnel only) */
+  if (T->tile) {
+    real wf[6] = {0, 0, 0, 0, 0, 0}, Ff[3] = {0, 0, 0};
+    if (face_scan_now) face_scan(T, R, S->pos, M->trunk_half, S->face);
+    face_force(T, &C, R, S->pos, vb, M->trunk_half, S->face, wf, Ff);
+    for (int i = 0; i < 6; ++i) pA0[i] -= wf[i];
+    if (cf) for (int i = 0; i < 3; ++i) cf[i] += Ff[i];
   }
   /* base acceleration */
   real a0[6], mp[6];
@@ -966,7 +1047,9 @@ void go1o_physics(const go1_config* cfg, double* pos, double* quat, double* v, d
   for (int i = 0; i < 4; ++i) S.quat[i] = quat[i];
   for (int d = 0; d < NDOF; ++d) { S.q[d] = q[d]; S.qd[d] = qd[d]; tr[d] = tau[d]; }
   TerrainView T = {tile, cfg->hf_nx, cfg->hf_ny, ox, oy, cfg->horizontal_scale};
-  for (int i = 0; i < n_sub; ++i) phys_substep(&M, cfg, &S, tr, (real)h, gr, (real)friction, (real)restitution, (real)payload, &T, cfr);
+  /* the trunk-face vertices chosen every 4 sim steps (a control step of the README configuration) */
+  for (int i = 0; i < n_sub; ++i)
+    phys_substep(&M, cfg, &S, tr, (real)h, gr, (real)friction, (real)restitution, (real)payload, &T, cfr, i % 4 == 0);
   for (int i = 0; i < 3; ++i) { pos[i] = S.pos[i]; v[i] = S.v[i]; w[i] = S.w[i]; }
   for (int i = 0; i < 4; ++i) quat[i] = S.quat[i];
   for (int d = 0; d < NDOF; ++d) { q[d] = S.q[d]; qd[d] = S.qd[d]; }
@@ -1226,7 +1309,8 @@ static void step_env(const go1_config* c, const Model* M, const go1_state* st, c
       TerrainView T = {tile, c->hf_nx, c->hf_ny, 0, 0, c->horizontal_scale};
       real h = (real)c->sim_dt / c->n_internal;
       for (int k = 0; k < c->n_internal; ++k)
-        phys_substep(M, c, &S, tau, h, g, st->friction[e], st->restitution[e], st->payload[e], &T, cfd);
+        phys_substep(M, c, &S, tau, h, g, st->friction[e], st->restitution[e], st->payload[e], &T, cfd,
+                     sub == 0 && k == 0);
       for (int d = 0; d < NDOF; ++d) { dp[d] = (float)S.q[d]; dv[d] = (float)S.qd[d]; }
       for (int i = 0; i < NB * 3; ++i) cf[i] = (float)cfd[i];
     }

@@ -1,8 +1,11 @@
 """Self-collision and restitution on the GPU step against the f64 oracle (CPU invariants of the same
 model in tests/test_self_collision.py).  One-step comparisons with the integrator bounds of
 tests/test_gpu_parity.py (check_integrator_step) on states built to exercise the new terms:
-  * legs in random poses within the joint limits, some with the front feet crossed under the trunk, the base
-    held 1 m above the plane (every reported force is then a self-contact force);
+  * test_self_contact_forces_of_colliding_states: states chosen (numpy kinematics, below) to be in self-contact
+    at the step's only sim step (decimation 1), the base 1 m above the plane: every reported force is a
+    self-contact force, per body against the oracle, with every class of sphere pair hit across the batch;
+  * legs in random poses within the joint limits, some with the front feet crossed under the trunk, stepped
+    through three control steps;
   * the robot dropped onto the plane at up to 2.5 m/s with restitution 0..1, through the rebound.
 """
 import numpy as np
@@ -12,7 +15,7 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-from legged_tracking_amd import config as CF, layout as L, native  # noqa: E402
+from legged_tracking_amd import config as CF, layout as L, native, terrain as T  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from tests.test_gpu_parity import DEV, _dev, _sim_setup, check_integrator_step  # noqa: E402
 
@@ -77,3 +80,212 @@ def test_restitution_step_vs_oracle():
     st["episode_length"][:, 0] = 10
     forces = _run(c, td, ter, st, rng, 4, act_scale=0.5, grav=(0.0, 0.0, 0.0))
     assert (np.abs(forces).max(axis=(0, 2, 3)) > 0).mean() > 0.9
+
+
+# ---- numpy kinematics of the 32 self-collision spheres (trunk frame; shares nothing with the kernel or the oracle)
+def _rx(q):
+    c, s_ = np.cos(q), np.sin(q)
+    o, z = np.ones_like(q), np.zeros_like(q)
+    return np.stack([np.stack([o, z, z], -1), np.stack([z, c, -s_], -1), np.stack([z, s_, c], -1)], -2)
+
+
+def _ry(q):
+    c, s_ = np.cos(q), np.sin(q)
+    o, z = np.ones_like(q), np.zeros_like(q)
+    return np.stack([np.stack([c, z, s_], -1), np.stack([z, o, z], -1), np.stack([-s_, z, c], -1)], -2)
+
+
+def _spheres(q):
+    """(n, 32, 3) centres in the trunk frame, (32,) radii: leg l * 8 + s, s = thigh 0-2, calf 3-4, foot 5,
+    hip-capsule ends 6-7 (go1_device.h self-collision; model.py for the geometry)."""
+    from legged_tracking_amd import model as M
+    n = q.shape[0]
+    P = np.zeros((n, 32, 3))
+    r = np.zeros(32)
+    for l, leg in enumerate(L.LEGS):
+        o = [np.array(v, np.float64) for v in M.joint_origins(leg)]
+        sy = M.LEG_SIGNS[leg][1]
+        R0 = _rx(q[:, 3 * l])
+        p0 = np.broadcast_to(o[0], (n, 3))
+        R1 = R0 @ _ry(q[:, 3 * l + 1])
+        p1 = p0 + R0 @ o[1]
+        R2 = R1 @ _ry(q[:, 3 * l + 2])
+        p2 = p1 + R1 @ o[2]
+        for k in range(3):
+            P[:, 8 * l + k] = p1 + R1 @ np.array([0.0, 0.0, -0.071 * (k + 1)])
+        for k in range(2):
+            P[:, 8 * l + 3 + k] = p2 + R2 @ np.array([0.0, 0.0, -0.071 * (k + 1)])
+        P[:, 8 * l + 5] = p2 + R2 @ np.array(M.FOOT_OFFSET)
+        for k in range(2):
+            P[:, 8 * l + 6 + k] = p0 + R0 @ np.array([0.0, sy * M.HIP_CAPSULE_Y[k], 0.0])
+        r[8 * l:8 * l + 3] = M.THIGH_BOX_HALF_WIDTH
+        r[8 * l + 3:8 * l + 5] = M.CALF_BOX_HALF_WIDTH
+        r[8 * l + 5] = M.FOOT_RADIUS
+        r[8 * l + 6:8 * l + 8] = M.HIP_CAPSULE_RADIUS
+    return P, r
+
+
+SAME = [(6, 3), (6, 4), (6, 5), (7, 3), (7, 4), (7, 5), (0, 5), (1, 5), (2, 5)]
+
+
+def _pair_classes(P, r):
+    """(n, n_classes) overlap flags and the class names: every cross-leg pair (la, lb, a, b), every same-leg pair
+    (l, SAME[p]), every thigh / calf / foot sphere against the trunk box."""
+    from legged_tracking_amd import model as M
+    cols, names = [], []
+    for la in range(4):
+        for lb in range(la + 1, 4):
+            for a in range(8):
+                for b in range(8):
+                    d = P[:, 8 * la + a] - P[:, 8 * lb + b]
+                    cols.append((d * d).sum(-1) < (r[8 * la + a] + r[8 * lb + b]) ** 2)
+                    names.append(("cross", la, lb, a, b))
+    for l in range(4):
+        for a, b in SAME:
+            d = P[:, 8 * l + a] - P[:, 8 * l + b]
+            cols.append((d * d).sum(-1) < (r[8 * l + a] + r[8 * l + b]) ** 2)
+            names.append(("same", l, a, b))
+    th = np.array(M.TRUNK_BOX) / 2
+    for l in range(4):
+        for s in range(6):
+            c = P[:, 8 * l + s]
+            d = c - np.clip(c, -th, th)
+            cols.append((d * d).sum(-1) < r[8 * l + s] ** 2)
+            names.append(("box", l, s))
+    return np.stack(cols, 1), names
+
+
+def test_self_contact_forces_of_colliding_states():
+    """states in self-contact at the step's (only) sim step, GPU per-body contact forces against the
+    f64 oracle.  The pool: 60,000 poses drawn within the joint limits (half with the hips turned inward, which
+    brings the knees and feet under the trunk); the batch: for every pair class some pose hits, one pose that
+    hits it, then poses in contact up to 3/4 of the batch, the rest free.  Requirements: >= 50 % of the envs in
+    self-contact on the GPU, every kind of pair (cross-leg thigh-thigh, with a hip capsule, calf / foot; each of
+    the six leg pairs; the same-leg pairs) hit, and the forces within 1e-3 N + 1e-4 relative of the oracle."""
+    n = 512
+    cfg = CF.readme_config(n_envs=n, terrain="plane", rows=2, cols=4)
+    cfg.control.decimation = 1  # the reported forces are those of the step's only sim step, at the given state
+    c = CF.build_abi_config(cfg)
+    c.camera_zero = 0
+    assert c.self_stiffness > 0
+    td = T.build(cfg, n, np.random.RandomState(11))
+    ter = O.NpTerrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    st = O.NpState(n, cfg=c)
+    O.reset_envs(c, st, ter, np.ones(n, np.uint8), rng_seed=3, rng_step=0)
+    rng = np.random.default_rng(21)
+    lim = np.array([L.JOINT_LIMITS[j % 3] for j in range(12)])
+    pool = rng.uniform(lim[:, 0], lim[:, 1], (60000, 12))
+    inward = rng.random(60000) < 0.5  # hips turned toward the body (FL / RL: q_hip < 0, FR / RR: > 0)
+    sgn = np.array([-1.0, 1.0, -1.0, 1.0])
+    for l in range(4):
+        pool[inward, 3 * l] = sgn[l] * rng.uniform(0.2, 0.8, inward.sum())
+    P, r = _spheres(pool)
+    flags, names = _pair_classes(P, r)
+    anyc = flags.any(1)
+    pick = []
+    for j in range(flags.shape[1]):  # one pose per reachable class
+        idx = np.nonzero(flags[:, j])[0]
+        if len(idx) and not flags[pick, j].any():
+            pick.append(int(idx[0]))
+    assert len(pick) <= n // 2, len(pick)
+    rest = [i for i in np.nonzero(anyc)[0] if i not in set(pick)]
+    pick += rest[:3 * n // 4 - len(pick)]
+    free = np.nonzero(~anyc)[0]
+    pick += list(free[:n - len(pick)])
+    q = pool[pick].astype(np.float32)
+    reach = flags[pick].any(0)
+    kinds = {}
+    for j, nm in enumerate(names):
+        key = nm[0] if nm[0] != "cross" else ("cross-hip" if nm[3] >= 6 or nm[4] >= 6 else
+                                             ("cross-thigh" if nm[3] < 3 and nm[4] < 3 else "cross-calf-foot"))
+        kinds.setdefault(key, []).append(reach[j])
+    print("\npair classes hit per kind: " + ", ".join(f"{k} {sum(v)}/{len(v)}" for k, v in kinds.items()))
+    for key in ("cross-thigh", "cross-hip", "cross-calf-foot"):
+        assert any(kinds[key]), key
+    for lp in range(6):
+        assert any(reach[j] for j, nm in enumerate(names) if nm[0] == "cross" and (nm[1], nm[2]) ==
+                   [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)][lp]), lp
+    st["dof_pos"][:] = q
+    st["dof_vel"][:] = rng.normal(0, 1.0, (n, 12)).astype(np.float32)
+    st["root"][:, 2] = st["root"][:, 2] + 1.0  # 1 m above the plane: every reported force is a self-contact force
+    st["root"][:, 7:13] = rng.normal(0, 0.2, (n, 6)).astype(np.float32)
+    st["episode_length"][:, 0] = 10
+    g = native.Go1Native(c, DEV)
+    g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    g.state.load(st.arrays)
+    gr, gvec = CF.gravity_state([0.0, 0.0, 0.0])
+    scales = np.zeros(c.n_terms, np.float32)
+    a = np.zeros((n, 12), np.float32)
+    g.step(_dev(a), gvec, gr, scales, rng_seed=5, rng_step=300)
+    torch.cuda.synchronize()
+    out = O.step(c, st, ter, a, gvec, gr, scales, rng_seed=5, rng_step=300, debug=False)
+    cf = g.contact_forces.cpu().numpy()
+    ref = out["contact_forces"]
+    touching = np.abs(cf).max(axis=(1, 2)) > 0
+    print(f"envs in self-contact: GPU {touching.mean():.2f}, oracle {(np.abs(ref).max(axis=(1, 2)) > 0).mean():.2f}; "
+          f"max |dF| {np.abs(cf - ref).max():.2e} N of max |F| {np.abs(ref).max():.2e} N")
+    assert touching.mean() >= 0.5
+    # f32 against f64 kinematics (the integrator's hardware sin / cos): ~1e-7 m in a sphere centre, which turns the
+    # normal of a deep overlap (centres ~1 mm apart, up to 100 N) by ~1e-4 -- hence a looser bound on the few
+    # worst elements and a tight one on almost all of them
+    err = np.abs(cf - ref)
+    assert np.percentile(err, 99) <= 1e-3, np.percentile(err, 99)
+    np.testing.assert_allclose(cf, ref, rtol=1e-3, atol=0.05)
+    # internal forces: the per-env sum over the bodies vanishes
+    np.testing.assert_allclose(cf.sum(axis=1), 0.0, atol=2e-3)
+
+
+def test_trunk_face_contacts_step_vs_oracle():
+    """the trunk's top face against ceiling apexes and its bottom face against a floor ridge that
+    lie between the box corners (go1_device.h face_scan / face_force against oracle/go1_oracle.c).  Every tile gets
+    a flat floor and ceiling with three downward ceiling spikes and a raised floor ridge under the trunk; every
+    env's trunk sits over them, level to within 0.1 rad and yawed up to 0.5 rad, at heights that put the spikes and
+    the ridge 0-15 mm into its faces.  README configuration (decimation 4, the specialised kernel), three control
+    steps, each against the f64 oracle from the same state within the integrator bounds of
+    tests/test_gpu_parity.py; the trunk's reported contact force, which only the faces produce here, within
+    1e-3 relative of the oracle's and present in most envs."""
+    n = 256
+    cfg, c, td, ter, st, rng = _sim_setup(n, "single_path")
+    hs = float(c.horizontal_scale)
+    tiles = td.tiles.copy()
+    tiles[:, 1] = 0.0   # floor
+    tiles[:, 0] = 0.5   # ceiling
+    i0, j0 = 40, 20
+    for di, dj in ((0, 0), (3, 0), (-3, 1)):
+        tiles[:, 0, i0 + di, j0 + dj] = 0.395
+    tiles[:, 1, i0 - 1:i0 + 2, j0] = 0.255
+    td.tiles[:] = tiles
+    ter = O.NpTerrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    root = st["root"]
+    root[:, 0] = td.env_terrain_origin[:, 0] + i0 * hs + rng.uniform(-0.02, 0.02, n)
+    root[:, 1] = td.env_terrain_origin[:, 1] + j0 * hs + rng.uniform(-0.02, 0.02, n)
+    root[:, 2] = rng.uniform(0.30, 0.35, n)
+    yaw, pitch, roll = rng.uniform(-0.5, 0.5, n), rng.uniform(-0.1, 0.1, n), rng.uniform(-0.1, 0.1, n)
+    cy, sy, cp, sp, cr, sr = np.cos(yaw / 2), np.sin(yaw / 2), np.cos(pitch / 2), np.sin(pitch / 2), np.cos(roll / 2), np.sin(roll / 2)
+    root[:, 3] = sr * cp * cy - cr * sp * sy
+    root[:, 4] = cr * sp * cy + sr * cp * sy
+    root[:, 5] = cr * cp * sy - sr * sp * cy
+    root[:, 6] = cr * cp * cy + sr * sp * sy
+    root[:, 7:13] = rng.normal(0, 0.1, (n, 6))
+    st["episode_length"][:, 0] = 10
+    g = native.Go1Native(c, DEV)
+    g.set_terrain(td.tiles, td.env_tile, td.env_terrain_origin, td.env_origins)
+    grav, gvec = CF.gravity_state([0.0, 0.0, 0.0])
+    scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
+    hits = []
+    for t in range(3):
+        g.state.load(st.arrays)
+        act = rng.normal(0, 0.3, (n, 12)).astype(np.float32)
+        g.step(_dev(act), gvec, grav, scales, rng_seed=4, rng_step=400 + t)
+        torch.cuda.synchronize()
+        out = O.step(c, st, ter, act, gvec, grav, scales, rng_seed=4, rng_step=400 + t, debug=False)
+        gs = g.state.numpy()
+        cf = g.contact_forces.cpu().numpy()
+        check_integrator_step(gs, st, cf, out["contact_forces"], g.reset.cpu().numpy().astype(bool),
+                              out["reset"].astype(bool))
+        base, base_ref = cf[:, 0], out["contact_forces"][:, 0]
+        np.testing.assert_allclose(base, base_ref, rtol=1e-3, atol=2e-2)
+        hits.append((np.linalg.norm(base_ref, axis=1) > 0).mean())
+        st = O.NpState(n, gs, c)
+    print(f"\nenvs with trunk-face forces per step: {hits}")
+    assert hits[0] > 0.3
