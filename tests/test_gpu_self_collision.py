@@ -208,6 +208,10 @@ def test_self_contact_forces_of_colliding_states():
     st["dof_pos"][:] = q
     st["dof_vel"][:] = rng.normal(0, 1.0, (n, 12)).astype(np.float32)
     st["root"][:, 2] = st["root"][:, 2] + 1.0  # 1 m above the plane: every reported force is a self-contact force
+    # every env at the world origin (they do not interact): on the plane the integrator works in world coordinates,
+    # and at the env origins' 10-60 m an f32 ulp (1-4 um) puts ~1e-5 m into each sphere centre, i.e. 0.02-0.04 N
+    # of the 2000 N/m springs -- physically nothing, but it would hide the narrow phase's own arithmetic here
+    st["root"][:, 0:2] = 0.0
     st["root"][:, 7:13] = rng.normal(0, 0.2, (n, 6)).astype(np.float32)
     st["episode_length"][:, 0] = 10
     g = native.Go1Native(c, DEV)
@@ -225,12 +229,13 @@ def test_self_contact_forces_of_colliding_states():
     print(f"envs in self-contact: GPU {touching.mean():.2f}, oracle {(np.abs(ref).max(axis=(1, 2)) > 0).mean():.2f}; "
           f"max |dF| {np.abs(cf - ref).max():.2e} N of max |F| {np.abs(ref).max():.2e} N")
     assert touching.mean() >= 0.5
-    # f32 against f64 kinematics (the integrator's hardware sin / cos): ~1e-7 m in a sphere centre, which turns the
-    # normal of a deep overlap (centres ~1 mm apart, up to 100 N) by ~1e-4 -- hence a looser bound on the few
-    # worst elements and a tight one on almost all of them
+    # f32 against f64 kinematics (the integrator's hardware sin / cos): ~1e-7 m in a sphere centre, 2e-4 N of a
+    # spring; a deep overlap (centres ~1 mm apart, up to 100 N) turns its normal by ~1e-4 -- hence a looser bound on
+    # the few worst elements and a tight one on almost all of them
     err = np.abs(cf - ref)
+    print(f"force error p99 {np.percentile(err, 99):.2e} N, max {err.max():.2e} N")
     assert np.percentile(err, 99) <= 1e-3, np.percentile(err, 99)
-    np.testing.assert_allclose(cf, ref, rtol=1e-3, atol=0.05)
+    np.testing.assert_allclose(cf, ref, rtol=1e-3, atol=0.02)
     # internal forces: the per-env sum over the bodies vanishes
     np.testing.assert_allclose(cf.sum(axis=1), 0.0, atol=2e-3)
 

@@ -145,3 +145,29 @@ def test_restitution_below_threshold_changes_nothing():
     c = _cfg()
     assert c.bounce_threshold == np.float32(0.5)
     assert not np.array_equal(_drop(c, 0.0)[2], _drop(c, 1.0)[2])
+
+
+def test_restitution_drop_apex_is_pinned():
+    """the restitution model's rebound, pinned.  The trunk dropped upside down from 0.4 m (impact
+    2.60 m/s) on its box corners: rebound / impact speed and the apex the trunk rises to after the first
+    impact, for e = 0, 0.5, 1.  A penalty contact bounces a little by itself (its spring returns part of the
+    stored energy) and e hands back part of the damping, so the rebound ratio goes from 0.26 to 0.34 -- where
+    PhysX's rigid contact would give e itself above the 0.5 m/s threshold (a deliberate deviation,
+    parity with PhysX unpinned)."""
+    c = _cfg()
+    want = {0.0: (0.2568, 0.02864), 0.5: (0.3018, 0.03777), 1.0: (0.3446, 0.04733)}
+    for e, (ratio, rise) in want.items():
+        b = _body(z=0.4)
+        b["quat"] = [1.0, 0.0, 0.0, 0.0]
+        zs, vs = [], []
+        for _ in range(300):
+            O.physics(c, b, np.zeros(12), 1, 0.005, G, 1.0, e, 0.0)
+            zs.append(b["pos"][2])
+            vs.append(b["v"][2])
+        zs, vs = np.array(zs), np.array(vs)
+        k = int(np.argmax(vs > 0))
+        assert k > 0
+        impact, rebound = -vs[:k].min(), vs[k:].max()
+        assert abs(impact - 2.5996) < 1e-3, impact
+        np.testing.assert_allclose(rebound / impact, ratio, rtol=0.01, err_msg=str(e))
+        np.testing.assert_allclose(zs[k:].max() - zs[:k].min(), rise, rtol=0.02, err_msg=str(e))
