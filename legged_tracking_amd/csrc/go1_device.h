@@ -26,7 +26,7 @@ static_assert(GO1_MODEL_CONST_FLOATS == GO1_MODEL_FLOATS, "regenerate go1_model_
 // Diagnostic build only (tools/stamps.py): every marker records (source line, s_memtime)
 // into a buffer of its own, read back by go1_debug_stamps.  Never built into the product.
 #define GO1_STAMP_WAVES 4096
-#define GO1_STAMP_SLOTS 160
+#define GO1_STAMP_SLOTS 320
 __device__ unsigned long long g_go1_stamps[GO1_STAMP_WAVES * GO1_STAMP_SLOTS];
 __shared__ unsigned s_go1_stamp_k;
 __device__ __forceinline__ void go1_stamp(unsigned line) {
@@ -1434,7 +1434,6 @@ struct Phys {
   float pos[3], quat[4];  // base (replicated on the 16 lanes of the env)
   f2 wv[3];               // base angular and linear velocity (world) as (w_i, v_i) pairs
   float q[3], qd[3];                   // this lane's leg
-  int face[2];            // the trunk faces' contact vertices of the control step (face_scan), -1: none
 };
 
 // ---- the trunk box's faces against the heightfields (go1.urdf:53-58, the 0.3762 x 0.0935 x 0.114
@@ -1560,28 +1559,26 @@ __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 // Broad phase in registers: each lane bounds its leg (thigh joint, knee, foot, hip-capsule ends, grown by their
 // radii) by an AABB in the trunk frame, swaps the four legs' boxes over the quad (DPP) and tests the six leg pairs,
 // the trunk box and the leg's own folded links; a wave whose envs have no candidate is done.  Otherwise, per env in
-// LDS: the 32 spheres as (pos, r), (vel, 0); one candidate group at a time (wave-uniform), the env's 16 lanes
-// evaluate the group's pairs (j = k, k + 16, ... for env-local lane k) into the group's force slots, and each
-// sphere's owner sums its slots in a fixed order -- the force on a sphere does not depend on which lane evaluated
-// which pair, and a pair's two spheres get exactly opposite forces.  Sphere owners: role 0 (thigh 0, thigh 1),
-// role 1 (thigh 2, hip end 6), role 2 (calf 0, calf 1), role 3 (foot, hip end 7).  The box pairs are evaluated by
-// the sphere's own lane.
-#define SELF_NSAME 9
-#define SELF_ENV_FLOATS (32 * 8 + 64 * 4 + 48 * 4)  // spheres, one group's pair forces, the same-leg pair forces
-__device__ __forceinline__ constexpr int self_same_a(int p) { return p < 3 ? 6 : (p < 6 ? 7 : p - 6); }
-__device__ __forceinline__ constexpr int self_same_b(int p) { return p < 6 ? 3 + p % 3 : 5; }
+// LDS: the 32 spheres as (pos, r), (vel, 0), and each lane sums the forces on its own two spheres from their
+// candidate partners (self_narrow).  Sphere owners: role 0 (thigh 0, thigh 1), role 1 (thigh 2, hip end 6),
+// role 2 (calf 0, calf 1), role 3 (foot, hip end 7).
+// the 32 spheres (pos, r), (vel, 0); then the trunk faces' two vertices of the control step (face_scan)
+#define SELF_ENV_FLOATS (32 * 8 + 4)
+#define FACE_SEL_OFF (32 * 8)
 // the lane's spheres: x half s0, y half s1
 __device__ __forceinline__ int self_s0(int role) { return role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5)); }
 __device__ __forceinline__ int self_s1(int role) { return role == 0 ? 1 : (role == 1 ? 6 : (role == 2 ? 4 : 7)); }
 
 // force on sphere A (world) of the pair (A, B); zero when apart or when the spring no longer compresses
+// (sg: the normal of coincident centres, +1 when A has the lower sphere index: the pair's two evaluations, A on
+// B and B on A, give exactly opposite forces -- the negated differences square and multiply to the same bits)
 __device__ __forceinline__ void self_sphere_force(const float4 A, const float4 Av, const float4 B, const float4 Bv,
-                                                  float ks, float ds, float* F) {
+                                                  float ks, float ds, float* F, float sg = 1.0f) {
   const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z;
   const float dd = d0 * d0 + d1 * d1 + d2 * d2, rs = A.w + B.w;
   const float inv = dd > 1e-18f ? frsq(dd) : 0.0f;
   const float n0 = dd > 1e-18f ? d0 * inv : 0.0f, n1 = dd > 1e-18f ? d1 * inv : 0.0f,
-              n2 = dd > 1e-18f ? d2 * inv : 1.0f;
+              n2 = dd > 1e-18f ? d2 * inv : sg;
   const float pen = rs - dd * inv;
   const float vn = (Av.x - Bv.x) * n0 + (Av.y - Bv.y) * n1 + (Av.z - Bv.z) * n2;
   float fn = ks * pen - ds * vn;
@@ -1646,110 +1643,97 @@ __device__ __forceinline__ int quad_or(int v) {
 }
 
 // leg pairs lp: (0,1) = 0, (0,2) = 1, (0,3) = 2, (1,2) = 3, (1,3) = 4, (2,3) = 5
-__device__ __forceinline__ constexpr int self_la(int lp) { return lp < 3 ? 0 : (lp < 5 ? 1 : 2); }
-__device__ __forceinline__ constexpr int self_lb(int lp) { return lp < 3 ? lp + 1 : (lp < 5 ? lp - 1 : 3); }
 
 // Narrow phase (a wave whose broad phase found a candidate; inline: out of line, the call's saves and
 // restores of the step kernel's ~500 live registers cost more than the narrow phase itself).  sc: this env's
-// LDS scratch, the spheres already written (self_put).  Fs: the self-contact world forces on the lane's two
-// spheres (x, y halves), wb: the trunk reaction wrench of the lane's box contacts (base frame, summed over the
-// env's lanes by the caller).
+// LDS scratch, the spheres already written (self_put).  Each lane sums the forces on its own two spheres from
+// their partners directly -- for each candidate leg the other leg's 8 spheres in one LDS round trip, the two own
+// spheres in the halves of the tests -- so there are no force slots, no barriers and no dependent LDS trips
+// (the slot form cost ~10 us a step: a barrier and two round trips per leg pair, with one wave per SIMD nothing
+// hides them).  Each pair is evaluated once from each side; the two results are exactly opposite
+// (self_sphere_force), and every sphere's sum runs in a fixed order.  Fs: the self-contact world forces on the
+// lane's two spheres (x, y halves), wb: the trunk reaction wrench of the lane's box contacts (base frame, summed
+// over the env's lanes by the caller).
 __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
                                            const float* R, const float* pos, const float* vb, const float* th,
                                            float Fs[2][3], float* wb) {
   const float ks = cfg->self_stiffness, ds = cfg->self_damping;
-  const int k = 4 * role + leg;
   const int s0 = self_s0(role), s1 = self_s1(role);
+  const int ia0 = leg * 8 + s0, ia1 = leg * 8 + s1;
   float4* P = reinterpret_cast<float4*>(sc);
-  float4* FS = reinterpret_cast<float4*>(sc + 32 * 8);
-  float4* FS2 = reinterpret_cast<float4*>(sc + 32 * 8 + 64 * 4);
+  const float4 A0 = P[2 * ia0], A0v = P[2 * ia0 + 1], A1 = P[2 * ia1], A1v = P[2 * ia1 + 1];
   // the trunk box, by the lane of the sphere (thigh, calf and foot: every x half, the y halves of roles 0 and 2)
   if ((mask >> (6 + leg)) & 1) {
-    self_box_force(P[2 * (leg * 8 + s0)], P[2 * (leg * 8 + s0) + 1], R, pos, vb, th, ks, ds, Fs[0], wb);
-    if ((role & 1) == 0) self_box_force(P[2 * (leg * 8 + s1)], P[2 * (leg * 8 + s1) + 1], R, pos, vb, th, ks, ds, Fs[1], wb);
+    self_box_force(A0, A0v, R, pos, vb, th, ks, ds, Fs[0], wb);
+    if ((role & 1) == 0) self_box_force(A1, A1v, R, pos, vb, th, ks, ds, Fs[1], wb);
   }
-  // the cross-leg groups, one at a time through the group's 64 force slots
+  MARK(self_box_done);
+  // the other legs of candidate leg pairs (leg ^ d, d = 1, 2, 3: mask bits as self_broad sets them)
 #pragma unroll
-  for (int lp = 0; lp < 6; ++lp) {
-    if (!__any((mask >> lp) & 1)) continue;
-    const int la = self_la(lp), lb = self_lb(lp);
+  for (int d = 1; d < 4; ++d) {
+    const int m = leg ^ d;
+    const int lp = d == 1 ? ((leg >> 1) ? 5 : 0) : (d == 2 ? ((leg & 1) ? 4 : 1) : ((leg == 0 || leg == 3) ? 2 : 3));
     const bool on = (mask >> lp) & 1;
-    unsigned act = 0u;  // bit t: this lane's pair k + 16 t overlaps
+    if (!__any(on)) continue;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = k + 16 * t;
-      const float4 A = P[2 * (la * 8 + (j >> 3))], B = P[2 * (lb * 8 + (j & 7))];
-      const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
-      act |= (on && d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << t) : 0u;
+    for (int u = 0; u < 8; ++u) {  // one partner at a time: the narrow phase runs at the kernel's register peak
+      const int ib = m * 8 + u;
+      const float4 B = P[2 * ib];
+      const float a0 = A0.x - B.x, a1 = A0.y - B.y, a2 = A0.z - B.z, ra = A0.w + B.w;
+      const float c0 = A1.x - B.x, c1 = A1.y - B.y, c2 = A1.z - B.z, rc = A1.w + B.w;
+      const bool h0 = on && a0 * a0 + a1 * a1 + a2 * a2 < ra * ra, h1 = on && c0 * c0 + c1 * c1 + c2 * c2 < rc * rc;
+      if (!__any(h0 || h1)) continue;
+      const float4 Bv = P[2 * ib + 1];
+      float f[3] = {0.0f, 0.0f, 0.0f}, g[3] = {0.0f, 0.0f, 0.0f};
+      if (h0) self_sphere_force(A0, A0v, B, Bv, ks, ds, f, ia0 < ib ? 1.0f : -1.0f);
+      if (h1) self_sphere_force(A1, A1v, B, Bv, ks, ds, g, ia1 < ib ? 1.0f : -1.0f);
+      Fs[0][0] += f[0]; Fs[0][1] += f[1]; Fs[0][2] += f[2];
+      Fs[1][0] += g[0]; Fs[1][1] += g[1]; Fs[1][2] += g[2];
     }
-    if (!__any(act != 0u)) continue;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = k + 16 * t;
-      float F[3] = {0.0f, 0.0f, 0.0f};
-      if ((act >> t) & 1u) {
-        const int a = la * 8 + (j >> 3), b = lb * 8 + (j & 7);
-        self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
-      }
-      FS[j] = make_float4(F[0], F[1], F[2], 0.0f);
-    }
-    __syncthreads();
-    if (on && (leg == la || leg == lb)) {
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int s = hh == 0 ? s0 : s1;
-        float x = 0.0f, y = 0.0f, z = 0.0f;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float4 f = leg == la ? FS[8 * s + u] : FS[8 * u + s];
-          x += f.x; y += f.y; z += f.z;
-        }
-        const float sg = leg == la ? 1.0f : -1.0f;
-        Fs[hh][0] += sg * x; Fs[hh][1] += sg * y; Fs[hh][2] += sg * z;
-      }
-    }
-    __syncthreads();  // the slots are rewritten by the next group
   }
-  // the same-leg pairs: 4 legs x 9 over the env's 16 lanes
-  if (__any(((mask >> 10) & 15) != 0)) {
-    unsigned act = 0u;
+  MARK(self_cross_done);
+  // the leg's own links two joints apart (rare: unreachable within the joint limits): each own sphere against
+  // its partners of the oracle's SELF_SAME_A / _B -- hip ends 6, 7: calf 3, 4 and foot 5; calf: hip ends; foot:
+  // hip ends and thigh 0-2; thigh: foot
+  if (__any((mask >> (10 + leg)) & 1)) {
+    const bool on = (mask >> (10 + leg)) & 1;
+    const unsigned pm0 = s0 == 3 ? 0xC0u : (s0 == 5 ? 0xC7u : 0x20u);  // s0: 0, 2, 3 or 5
+    const unsigned pm1 = s1 >= 6 ? 0x38u : (s1 == 4 ? 0xC0u : 0x20u);  // s1: 1, 6, 4 or 7
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int j = k + 16 * t, l2 = j / SELF_NSAME, p = j - SELF_NSAME * l2;
-      if (j < 4 * SELF_NSAME && ((mask >> (10 + l2)) & 1)) {
-        const float4 A = P[2 * (l2 * 8 + self_same_a(p))], B = P[2 * (l2 * 8 + self_same_b(p))];
-        const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z, rs = A.w + B.w;
-        act |= (d0 * d0 + d1 * d1 + d2 * d2 < rs * rs) ? (1u << t) : 0u;
-      }
-    }
-    if (__any(act != 0u)) {
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int j = k + 16 * t, l2 = j / SELF_NSAME, p = j - SELF_NSAME * l2;
-        float F[3] = {0.0f, 0.0f, 0.0f};
-        if ((act >> t) & 1u) {
-          const int a = l2 * 8 + self_same_a(p), b = l2 * 8 + self_same_b(p);
-          self_sphere_force(P[2 * a], P[2 * a + 1], P[2 * b], P[2 * b + 1], ks, ds, F);
-        }
-        if (j < 4 * SELF_NSAME) FS2[j] = make_float4(F[0], F[1], F[2], 0.0f);
-      }
-      __syncthreads();
-      if ((mask >> (10 + leg)) & 1) {
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int s = hh == 0 ? s0 : s1;
-#pragma unroll
-          for (int p = 0; p < SELF_NSAME; ++p) {
-            const float sg = self_same_a(p) == s ? 1.0f : (self_same_b(p) == s ? -1.0f : 0.0f);
-            const float4 f = FS2[SELF_NSAME * leg + p];
-            Fs[hh][0] += sg * f.x; Fs[hh][1] += sg * f.y; Fs[hh][2] += sg * f.z;
-          }
-        }
-      }
-      __syncthreads();
+    for (int u = 0; u < 8; ++u) {
+      const bool h0 = on && ((pm0 >> u) & 1u), h1 = on && ((pm1 >> u) & 1u);
+      if (!__any(h0 || h1)) continue;
+      const int ib = leg * 8 + u;
+      const float4 B = P[2 * ib], Bv = P[2 * ib + 1];
+      float f[3] = {0.0f, 0.0f, 0.0f}, g[3] = {0.0f, 0.0f, 0.0f};
+      if (h0) self_sphere_force(A0, A0v, B, Bv, ks, ds, f, ia0 < ib ? 1.0f : -1.0f);
+      if (h1) self_sphere_force(A1, A1v, B, Bv, ks, ds, g, ia1 < ib ? 1.0f : -1.0f);
+      Fs[0][0] += f[0]; Fs[0][1] += f[1]; Fs[0][2] += f[2];
+      Fs[1][0] += g[0]; Fs[1][1] += g[1]; Fs[1][2] += g[2];
     }
   }
 }
+
+#ifdef GO1_ABL_SELF_NOINLINE  // A/B: the narrow phase out of line (its registers not reserved in the step kernel)
+struct SelfOut {
+  float f[12];
+};
+__device__ __noinline__ SelfOut self_narrow_ool(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
+                                               float R0, float R1, float R2, float R3, float R4, float R5, float R6,
+                                               float R7, float R8, float x0, float x1, float x2, float v0, float v1,
+                                               float v2, float v3, float v4, float v5) {
+  const float R[9] = {R0, R1, R2, R3, R4, R5, R6, R7, R8}, pos[3] = {x0, x1, x2}, vb[6] = {v0, v1, v2, v3, v4, v5};
+  const float* th = GO1_MODEL_F32 + 13 * 10 + 4 * 9 + 3 + 1;
+  float Fs[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}}, wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  self_narrow(cfg, sc, leg, role, mask, R, pos, vb, th, Fs, wb);
+  SelfOut o;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { o.f[i] = Fs[0][i]; o.f[3 + i] = Fs[1][i]; }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) o.f[6 + i] = wb[i];
+  return o;
+}
+#endif
 
 // the lane's spheres into this env's LDS scratch (x half s0, y half s1)
 __device__ __forceinline__ void self_put(float* sc, int leg, int role, const float* p0, const float* v0, float r0,
@@ -1764,13 +1748,14 @@ __device__ __forceinline__ void self_put(float* sc, int leg, int role, const flo
 
 // Broad phase, in registers, in the trunk frame (where the legs keep their places whatever the trunk's
 // pose; world-axis boxes of a yawed trunk overlap every leg): bit lp of the result = leg pair lp's boxes overlap,
-// bit 6 + leg = the leg's thigh and calf box meets the trunk box, bit 10 + leg = the leg's own links two joints
-// apart may touch (the hip capsule's ends against the calf / foot box, the thigh against the foot); the same mask
-// on the env's 16 lanes.  pth, pkn, pft: the thigh joint, knee and foot (world); hc0, hc1: the hip capsule's ends
-// in the trunk frame.
+// bit 6 + leg = one of the lane's own box spheres meets the trunk box (exact), bit 10 + leg = the leg is folded
+// past its joint band (its same-leg pairs are tested); the pair bits on the env's 16 lanes.  pth, pkn, pft: the
+// thigh joint, knee and foot (world); hc0, hc1: the hip capsule's ends in the trunk frame; pw, rr: the lane's two
+// contact spheres (world centres, radii), box_y: the y half is a box sphere (roles 0 and 2); q: the leg's joints.
 __device__ __forceinline__ int self_broad(int leg, const float* pth, const float* pkn, const float* pft, float rmax,
-                                          float rthigh, float rfoot, const float* hc0, const float* hc1, float rhip,
-                                          const float* R, const float* pos, const float* th) {
+                                          const float* hc0, const float* hc1, float rhip,
+                                          const float* R, const float* pos, const float* th, const f2* pw, f2 rr,
+                                          bool box_y, const float* q) {
   float b[3][3];  // the three points in the trunk frame, R^T (p - pos)
   const float* pts[3] = {pth, pkn, pft};
 #pragma unroll
@@ -1779,7 +1764,7 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
 #pragma unroll
     for (int i = 0; i < 3; ++i) b[k][i] = R[i] * w0 + R[3 + i] * w1 + R[6 + i] * w2;
   }
-  bool o1 = true, o2 = true, o3 = true, ob = true, ohc = true, otf = true;
+  bool o1 = true, o2 = true, o3 = true;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float clo = fminf(b[1][i], b[2][i]) - rmax, chi = fmaxf(b[1][i], b[2][i]) + rmax;  // knee .. foot
@@ -1789,16 +1774,32 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
     o1 = o1 && lo <= quad_xor<1>(hi) && quad_xor<1>(lo) <= hi;
     o2 = o2 && lo <= quad_xor<2>(hi) && quad_xor<2>(lo) <= hi;
     o3 = o3 && lo <= quad_xor<3>(hi) && quad_xor<3>(lo) <= hi;
-    ob = ob && tlo <= th[i] && -th[i] <= thi;
-    ohc = ohc && hlo <= chi && clo <= hhi;
-    const float t0 = fminf(b[0][i], b[1][i]) - rthigh, t1 = fmaxf(b[0][i], b[1][i]) + rthigh;  // the thigh
-    otf = otf && t0 <= b[2][i] + rfoot && b[2][i] - rfoot <= t1;
+  }
+  // the leg's own links two joints apart and the trunk box: out of reach while every joint of the leg is within
+  // 0.1 rad of its URDF range (the nearest such contact needs 0.2 rad past a limit, a trunk box contact 0.89;
+  // tests/test_self_collision.py::test_fold_gate_is_sound), so only a leg outside that band is tested -- then the
+  // box exactly on the lane's own thigh, calf and foot spheres (x half; the y half on roles 0 and 2, grown by
+  // 1e-4 against the narrow phase's rounding) and the same-leg pairs in the narrow phase
+  const bool wild = q[0] < -0.9029f || q[0] > 0.9029f || q[1] < -1.1472f || q[1] > 4.2888f || q[2] < -2.7966f ||
+                    q[2] > -0.8163f;
+  int fold = 0;
+  if (__any(wild)) {
+    float bx = 0.0f, by = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float cx = R[i] * (pw[0].x - pos[0]) + R[3 + i] * (pw[1].x - pos[1]) + R[6 + i] * (pw[2].x - pos[2]);
+      const float cy = R[i] * (pw[0].y - pos[0]) + R[3 + i] * (pw[1].y - pos[1]) + R[6 + i] * (pw[2].y - pos[2]);
+      const float dx = cx - fminf(fmaxf(cx, -th[i]), th[i]), dy = cy - fminf(fmaxf(cy, -th[i]), th[i]);
+      bx += dx * dx; by += dy * dy;
+    }
+    const float rbx = rr.x + 1e-4f, rby = rr.y + 1e-4f;
+    const bool ob = bx < rbx * rbx || (box_y && by < rby * rby);
+    fold = wild ? ((ob ? 64 << leg : 0) | (1024 << leg)) : 0;
   }
   const int lp1 = (leg >> 1) ? 5 : 0;                         // (0,1) / (2,3)
   const int lp2 = (leg & 1) ? 4 : 1;                          // (0,2) / (1,3)
   const int lp3 = (leg == 0 || leg == 3) ? 2 : 3;             // (0,3) / (1,2)
-  int mask = (o1 ? 1 << lp1 : 0) | (o2 ? 1 << lp2 : 0) | (o3 ? 1 << lp3 : 0) | (ob ? 64 << leg : 0) |
-             ((ohc || otf) ? 1024 << leg : 0);
+  const int mask = (o1 ? 1 << lp1 : 0) | (o2 ? 1 << lp2 : 0) | (o3 ? 1 << lp3 : 0) | fold;
   return quad_or(mask);
 }
 
@@ -1838,7 +1839,6 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   const float hip_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 2];
   const float hip_y0 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 3], hip_y1 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 4];
   float Fhip[3] = {0.0f, 0.0f, 0.0f};  // the hip capsule's world force (the leg's, on every role)
-  float FhS[3] = {0.0f, 0.0f, 0.0f};   // its self-contact part
   float cs[3][2];
   float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
   f2 cjp[3][3], pAp[3][3];  // c_j and the articulated bias force as (angular, linear) pairs
@@ -1945,11 +1945,14 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     // self-collision while the terrain reads land: world forces on the lane's two spheres, the trunk's
     // reaction wrench of the lane's box pairs into its trunk share
     float Fs[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}}, wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cf_raw[6 + i] = 0.0f;  // the hip's reported force of this sim step, from here
 #ifndef GO1_ABL_NO_SELF  // ablation build only: no self-collision
     if (cfg->self_stiffness > 0.0f) {
 #else
     if (false) {
 #endif
+      MARK(self_begin);
       float pft[3];  // the foot centre (calf frame offset), for the leg's bounding box
 #pragma unroll
       for (int i = 0; i < 3; ++i) pft[i] = pl[1][i] + Rl[1][3 * i] * foot[0] + Rl[1][3 * i + 1] * foot[1] + Rl[1][3 * i + 2] * foot[2];
@@ -1957,8 +1960,9 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       const f2 hy = msy * f2{hip_y0, hip_y1};
       const f2 hcy = origin[1] + cs[0][0] * hy, hcz = origin[2] + cs[0][1] * hy;
       const float hc0[3] = {origin[0], hcy.x, hcz.x}, hc1[3] = {origin[0], hcy.y, hcz.y};
-      const int mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), thigh_r, foot_r, hc0,
-                                  hc1, hip_r, R, S.pos, th);
+      const int mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), hc0,
+                                  hc1, hip_r, R, S.pos, th, pw, rr, (role & 1) == 0, S.q);
+      MARK(self_broad_done);
       if (__any(mask != 0)) {
         // the lane's second sphere: point b of the contact pass, or on roles 1 and 3 an end of the hip capsule
         // (world p = pos + R c, v = R (v_b + w_b x c + qd_hip e_x x (c - hip joint)))
@@ -1980,26 +1984,44 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
         const float p0[3] = {pw[0].x, pw[1].x, pw[2].x}, v0[3] = {vw[0].x, vw[1].x, vw[2].x};
         self_put(self_sc, leg, role, p0, v0, rr.x, p1, v1, odd ? hip_r : rr.y);
         __syncthreads();
-        self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
-        // the hip ends' forces (y halves of roles 1 and 3) on the hip link: hip-frame force f = Rh^T F and
-        // moment (0, y, 0) x f, summed over the leg's rows (every role runs the leg's ABA)
-        float hv[8];
+        MARK(self_put_done);
+#ifdef GO1_ABL_SELF_NOINLINE
         {
-          const float F0 = odd ? Fs[1][0] : 0.0f, F1 = odd ? Fs[1][1] : 0.0f, F2 = odd ? Fs[1][2] : 0.0f;
-          const float r0 = R[0] * F0 + R[3] * F1 + R[6] * F2, r1 = R[1] * F0 + R[4] * F1 + R[7] * F2,
-                      r2 = R[2] * F0 + R[5] * F1 + R[8] * F2;
-          const float fh1 = cs[0][0] * r1 + cs[0][1] * r2, fh2 = cs[0][0] * r2 - cs[0][1] * r1;
-          const float y = role == 1 ? hy.x : hy.y;
-          hv[0] = y * fh2; hv[1] = -(y * r0); hv[2] = r0; hv[3] = fh1; hv[4] = fh2;
-          hv[5] = F0; hv[6] = F1; hv[7] = F2;
-        }
-        rowsum4_n<8>(hv);
-        pAp[0][0] -= f2{hv[0], hv[2]};
-        pAp[0][1] -= f2{0.0f, hv[3]};
-        pAp[0][2] -= f2{hv[1], hv[4]};
+          const SelfOut o = self_narrow_ool(cfg, self_sc, leg, role, mask, R[0], R[1], R[2], R[3], R[4], R[5], R[6],
+                                            R[7], R[8], S.pos[0], S.pos[1], S.pos[2], vb[0], vb[1], vb[2], vb[3],
+                                            vb[4], vb[5]);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) FhS[i] = hv[5 + i];
+          for (int i = 0; i < 3; ++i) { Fs[0][i] = o.f[i]; Fs[1][i] = o.f[3 + i]; }
+#pragma unroll
+          for (int i = 0; i < 6; ++i) wb[i] = o.f[6 + i];
+        }
+#else
+        self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
+#endif
+        MARK(self_narrow_done);
+        // the hip ends' forces (y halves of roles 1 and 3) on the hip link: hip-frame force f = Rh^T F and
+        // moment (0, y, 0) x f, summed over the leg's rows (every role runs the leg's ABA); rare, so only in a
+        // wave that has one
+        if (__any(odd && (Fs[1][0] != 0.0f || Fs[1][1] != 0.0f || Fs[1][2] != 0.0f))) {
+          float hv[8];
+          {
+            const float F0 = odd ? Fs[1][0] : 0.0f, F1 = odd ? Fs[1][1] : 0.0f, F2 = odd ? Fs[1][2] : 0.0f;
+            const float r0 = R[0] * F0 + R[3] * F1 + R[6] * F2, r1 = R[1] * F0 + R[4] * F1 + R[7] * F2,
+                        r2 = R[2] * F0 + R[5] * F1 + R[8] * F2;
+            const float fh1 = cs[0][0] * r1 + cs[0][1] * r2, fh2 = cs[0][0] * r2 - cs[0][1] * r1;
+            const float y = role == 1 ? hy.x : hy.y;
+            hv[0] = y * fh2; hv[1] = -(y * r0); hv[2] = r0; hv[3] = fh1; hv[4] = fh2;
+            hv[5] = F0; hv[6] = F1; hv[7] = F2;
+          }
+          rowsum4_n<8>(hv);
+          pAp[0][0] -= f2{hv[0], hv[2]};
+          pAp[0][1] -= f2{0.0f, hv[3]};
+          pAp[0][2] -= f2{hv[1], hv[4]};
+#pragma unroll
+          for (int i = 0; i < 3; ++i) cf_raw[6 + i] = hv[5 + i];  // the hip's self-contact force (+ Fhip at the end)
+        }
         if (odd) { Fs[1][0] = 0.0f; Fs[1][1] = 0.0f; Fs[1][2] = 0.0f; }  // not the trunk corner's
+        MARK(self_hip_done);
       }
 #pragma unroll
       for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
@@ -2192,8 +2214,15 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   f2 wface[3] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
   float Fface[3] = {0.0f, 0.0f, 0.0f};
   if (T.patch) {  // the tunnel; on the plane the corners are the faces' deepest points
-    if (face_scan_now) face_scan(T, R, S.pos, th, 4 * role + leg, S.face);
-    face_force(T, C, R, S.pos, vb, th, S.face, wface, Fface);
+    // the chosen vertices live in the env's LDS scratch across the control step (not in registers)
+    int* fsel = reinterpret_cast<int*>(self_sc + FACE_SEL_OFF);
+    if (face_scan_now) {
+      int sel[2];
+      face_scan(T, R, S.pos, th, 4 * role + leg, sel);
+      if (role == 0 && leg == 0) { fsel[0] = sel[0]; fsel[1] = sel[1]; }
+    }
+    const int sel[2] = {fsel[0], fsel[1]};
+    face_force(T, C, R, S.pos, vb, th, sel, wface, Fface);
   }
   // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
   const float* bb = model;
@@ -2303,7 +2332,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   for (int i = 0; i < 3; ++i) {
     cf_raw[i] = Fpt[i].x;
     cf_raw[3 + i] = Fpt[i].y;
-    cf_raw[6 + i] = Fhip[i] + FhS[i];
+    cf_raw[6 + i] += Fhip[i];
     cf_raw[9 + i] = Fbs[i] + (role == 0 && leg == 0 ? Fface[i] : 0.0f);  // summed over the env's lanes (cf_sum)
   }
 }

@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 from legged_tracking_amd import config as CF, layout as L, native, terrain as T  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from tests.test_gpu_parity import DEV, _dev, _sim_setup, check_integrator_step  # noqa: E402
+from tests.self_geom import pair_classes as _pair_classes, spheres as _spheres  # noqa: E402
 
 
 def _run(c, td, ter, st, rng, steps, act_scale=1.0, grav=(0.0, 0.0, 0.0), act=None):
@@ -82,86 +83,17 @@ def test_restitution_step_vs_oracle():
     assert (np.abs(forces).max(axis=(0, 2, 3)) > 0).mean() > 0.9
 
 
-# ---- numpy kinematics of the 32 self-collision spheres (trunk frame; shares nothing with the kernel or the oracle)
-def _rx(q):
-    c, s_ = np.cos(q), np.sin(q)
-    o, z = np.ones_like(q), np.zeros_like(q)
-    return np.stack([np.stack([o, z, z], -1), np.stack([z, c, -s_], -1), np.stack([z, s_, c], -1)], -2)
-
-
-def _ry(q):
-    c, s_ = np.cos(q), np.sin(q)
-    o, z = np.ones_like(q), np.zeros_like(q)
-    return np.stack([np.stack([c, z, s_], -1), np.stack([z, o, z], -1), np.stack([-s_, z, c], -1)], -2)
-
-
-def _spheres(q):
-    """(n, 32, 3) centres in the trunk frame, (32,) radii: leg l * 8 + s, s = thigh 0-2, calf 3-4, foot 5,
-    hip-capsule ends 6-7 (go1_device.h self-collision; model.py for the geometry)."""
-    from legged_tracking_amd import model as M
-    n = q.shape[0]
-    P = np.zeros((n, 32, 3))
-    r = np.zeros(32)
-    for l, leg in enumerate(L.LEGS):
-        o = [np.array(v, np.float64) for v in M.joint_origins(leg)]
-        sy = M.LEG_SIGNS[leg][1]
-        R0 = _rx(q[:, 3 * l])
-        p0 = np.broadcast_to(o[0], (n, 3))
-        R1 = R0 @ _ry(q[:, 3 * l + 1])
-        p1 = p0 + R0 @ o[1]
-        R2 = R1 @ _ry(q[:, 3 * l + 2])
-        p2 = p1 + R1 @ o[2]
-        for k in range(3):
-            P[:, 8 * l + k] = p1 + R1 @ np.array([0.0, 0.0, -0.071 * (k + 1)])
-        for k in range(2):
-            P[:, 8 * l + 3 + k] = p2 + R2 @ np.array([0.0, 0.0, -0.071 * (k + 1)])
-        P[:, 8 * l + 5] = p2 + R2 @ np.array(M.FOOT_OFFSET)
-        for k in range(2):
-            P[:, 8 * l + 6 + k] = p0 + R0 @ np.array([0.0, sy * M.HIP_CAPSULE_Y[k], 0.0])
-        r[8 * l:8 * l + 3] = M.THIGH_BOX_HALF_WIDTH
-        r[8 * l + 3:8 * l + 5] = M.CALF_BOX_HALF_WIDTH
-        r[8 * l + 5] = M.FOOT_RADIUS
-        r[8 * l + 6:8 * l + 8] = M.HIP_CAPSULE_RADIUS
-    return P, r
-
-
-SAME = [(6, 3), (6, 4), (6, 5), (7, 3), (7, 4), (7, 5), (0, 5), (1, 5), (2, 5)]
-
-
-def _pair_classes(P, r):
-    """(n, n_classes) overlap flags and the class names: every cross-leg pair (la, lb, a, b), every same-leg pair
-    (l, SAME[p]), every thigh / calf / foot sphere against the trunk box."""
-    from legged_tracking_amd import model as M
-    cols, names = [], []
-    for la in range(4):
-        for lb in range(la + 1, 4):
-            for a in range(8):
-                for b in range(8):
-                    d = P[:, 8 * la + a] - P[:, 8 * lb + b]
-                    cols.append((d * d).sum(-1) < (r[8 * la + a] + r[8 * lb + b]) ** 2)
-                    names.append(("cross", la, lb, a, b))
-    for l in range(4):
-        for a, b in SAME:
-            d = P[:, 8 * l + a] - P[:, 8 * l + b]
-            cols.append((d * d).sum(-1) < (r[8 * l + a] + r[8 * l + b]) ** 2)
-            names.append(("same", l, a, b))
-    th = np.array(M.TRUNK_BOX) / 2
-    for l in range(4):
-        for s in range(6):
-            c = P[:, 8 * l + s]
-            d = c - np.clip(c, -th, th)
-            cols.append((d * d).sum(-1) < r[8 * l + s] ** 2)
-            names.append(("box", l, s))
-    return np.stack(cols, 1), names
-
-
-def test_self_contact_forces_of_colliding_states():
+@pytest.mark.parametrize("pool_kind", ["within_limits", "folded"])
+def test_self_contact_forces_of_colliding_states(pool_kind):
     """states in self-contact at the step's (only) sim step, GPU per-body contact forces against the
-    f64 oracle.  The pool: 60,000 poses drawn within the joint limits (half with the hips turned inward, which
-    brings the knees and feet under the trunk); the batch: for every pair class some pose hits, one pose that
-    hits it, then poses in contact up to 3/4 of the batch, the rest free.  Requirements: >= 50 % of the envs in
-    self-contact on the GPU, every kind of pair (cross-leg thigh-thigh, with a hip capsule, calf / foot; each of
-    the six leg pairs; the same-leg pairs) hit, and the forces within 1e-3 N + 1e-4 relative of the oracle."""
+    f64 oracle.  within_limits: 60,000 poses drawn within the joint limits (half with the hips turned inward, which
+    brings the knees and feet under the trunk); folded: poses up to 1.2 rad past the limits, where the same-leg
+    pairs and the trunk box are reached (the kernel tests those only for a leg past its 0.1 rad band:
+    tests/test_self_collision.py::test_fold_gate_is_sound).  The batch: for every pair class some pose hits, one
+    pose that hits it, then poses in contact up to 3/4 of the batch, the rest free.  Requirements: >= 50 % of the
+    envs in self-contact on the GPU, every kind of pair (within_limits: cross-leg thigh-thigh, with a hip capsule,
+    calf / foot, each of the six leg pairs; folded: the same-leg pairs and the trunk box) hit, and the forces within
+    1e-3 N + 1e-4 relative of the oracle."""
     n = 512
     cfg = CF.readme_config(n_envs=n, terrain="plane", rows=2, cols=4)
     cfg.control.decimation = 1  # the reported forces are those of the step's only sim step, at the given state
@@ -174,11 +106,14 @@ def test_self_contact_forces_of_colliding_states():
     O.reset_envs(c, st, ter, np.ones(n, np.uint8), rng_seed=3, rng_step=0)
     rng = np.random.default_rng(21)
     lim = np.array([L.JOINT_LIMITS[j % 3] for j in range(12)])
-    pool = rng.uniform(lim[:, 0], lim[:, 1], (60000, 12))
-    inward = rng.random(60000) < 0.5  # hips turned toward the body (FL / RL: q_hip < 0, FR / RR: > 0)
-    sgn = np.array([-1.0, 1.0, -1.0, 1.0])
-    for l in range(4):
-        pool[inward, 3 * l] = sgn[l] * rng.uniform(0.2, 0.8, inward.sum())
+    if pool_kind == "within_limits":
+        pool = rng.uniform(lim[:, 0], lim[:, 1], (60000, 12))
+        inward = rng.random(60000) < 0.5  # hips turned toward the body (FL / RL: q_hip < 0, FR / RR: > 0)
+        sgn = np.array([-1.0, 1.0, -1.0, 1.0])
+        for l in range(4):
+            pool[inward, 3 * l] = sgn[l] * rng.uniform(0.2, 0.8, inward.sum())
+    else:
+        pool = rng.uniform(lim[:, 0] - 1.2, lim[:, 1] + 1.2, (60000, 12))
     P, r = _spheres(pool)
     flags, names = _pair_classes(P, r)
     anyc = flags.any(1)
@@ -200,11 +135,15 @@ def test_self_contact_forces_of_colliding_states():
                                              ("cross-thigh" if nm[3] < 3 and nm[4] < 3 else "cross-calf-foot"))
         kinds.setdefault(key, []).append(reach[j])
     print("\npair classes hit per kind: " + ", ".join(f"{k} {sum(v)}/{len(v)}" for k, v in kinds.items()))
-    for key in ("cross-thigh", "cross-hip", "cross-calf-foot"):
-        assert any(kinds[key]), key
-    for lp in range(6):
-        assert any(reach[j] for j, nm in enumerate(names) if nm[0] == "cross" and (nm[1], nm[2]) ==
-                   [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)][lp]), lp
+    if pool_kind == "within_limits":
+        for key in ("cross-thigh", "cross-hip", "cross-calf-foot"):
+            assert any(kinds[key]), key
+        for lp in range(6):
+            assert any(reach[j] for j, nm in enumerate(names) if nm[0] == "cross" and (nm[1], nm[2]) ==
+                       [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)][lp]), lp
+    else:
+        for key in ("same", "box"):
+            assert sum(kinds[key]) >= 4, (key, sum(kinds[key]))
     st["dof_pos"][:] = q
     st["dof_vel"][:] = rng.normal(0, 1.0, (n, 12)).astype(np.float32)
     st["root"][:, 2] = st["root"][:, 2] + 1.0  # 1 m above the plane: every reported force is a self-contact force

@@ -171,3 +171,38 @@ def test_restitution_drop_apex_is_pinned():
         assert abs(impact - 2.5996) < 1e-3, impact
         np.testing.assert_allclose(rebound / impact, ratio, rtol=0.01, err_msg=str(e))
         np.testing.assert_allclose(zs[k:].max() - zs[:k].min(), rise, rtol=0.02, err_msg=str(e))
+
+
+def test_fold_gate_is_sound():
+    """go1_device.h self_broad tests a leg's same-leg pairs and its spheres against the trunk box only while one of
+    its joints is more than 0.1 rad past its URDF range (the oracle always tests them).  Sound if none of those
+    pairs can touch inside the band: on a grid of step h the clearance stays above what a grid cell can close
+    (per joint: the lever arm of the farthest sphere about its axis x h / 2).  The same-leg geometry does not
+    depend on the hip joint (the hip capsule turns with the leg), so that grid is (thigh, knee)."""
+    from legged_tracking_amd import model as M
+    from tests.self_geom import SAME, leg_spheres
+    lim = np.array(L.JOINT_LIMITS)
+    band = np.stack([lim[:, 0] - 0.1001, lim[:, 1] + 0.1001], 1)
+    o = [np.linalg.norm(v) for v in M.joint_origins(L.LEGS[0])]
+    calf = np.linalg.norm(M.FOOT_OFFSET)  # the knee axis to the farthest sphere centre (the foot's)
+    lever = np.array([o[1] + o[2] + calf, o[2] + calf, calf])  # hip, thigh, knee
+    # same-leg pairs, (thigh, knee) grid
+    h = 0.005
+    qt, qk = [np.arange(band[j, 0], band[j, 1] + h, h) for j in (1, 2)]
+    T2, K2 = (a.ravel() for a in np.meshgrid(qt, qk, indexing="ij"))
+    P, r = leg_spheres(np.zeros_like(T2), T2, K2)
+    clear = min(float((np.linalg.norm(P[:, a] - P[:, b], axis=1) - r[a] - r[b]).min()) for a, b in SAME)
+    bound = (lever[1] + lever[2]) * h / 2
+    assert clear > bound, (clear, bound)
+    # trunk box, (hip, thigh, knee) grid, one hip angle at a time
+    h = 0.02
+    th = np.array(M.TRUNK_BOX) / 2
+    qt, qk = [np.arange(band[j, 0], band[j, 1] + h, h) for j in (1, 2)]
+    T2, K2 = (a.ravel() for a in np.meshgrid(qt, qk, indexing="ij"))
+    box = np.inf
+    for qh in np.arange(band[0, 0], band[0, 1] + h, h):
+        P, r = leg_spheres(np.full_like(T2, qh), T2, K2)
+        c = P[:, :6]
+        box = min(box, float((np.linalg.norm(c - np.clip(c, -th, th), axis=2) - r[:6]).min()))
+    bound = lever.sum() * h / 2
+    assert box > bound, (box, bound)

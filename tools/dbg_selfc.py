@@ -4,7 +4,7 @@ import sys, os
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
-import tests.test_gpu_self_collision as TS
+import tests.self_geom as TS
 from legged_tracking_amd import config as CF, layout as L, native, terrain as T
 from oracle import oracle as O
 from tests.test_gpu_parity import DEV, _dev
@@ -23,8 +23,8 @@ inward = rng.random(60000) < 0.5
 sgn = np.array([-1.0, 1.0, -1.0, 1.0])
 for l in range(4):
     pool[inward, 3 * l] = sgn[l] * rng.uniform(0.2, 0.8, inward.sum())
-P, r = TS._spheres(pool)
-flags, names = TS._pair_classes(P, r)
+P, r = TS.spheres(pool)
+flags, names = TS.pair_classes(P, r)
 idx = np.nonzero(flags.any(1))[0][:n]
 q = pool[idx].astype(np.float32)
 for vel in (0.0, 1.0):

@@ -32,7 +32,9 @@ def main():
             cur = m.group(1)
             continue
         t = l.strip()
-        c = counts.setdefault(cur, [0, 0, 0, 0, 0])
+        c = counts.setdefault(cur, [0, 0, 0, 0, 0, 0])
+        if t.startswith("scratch_") or (t.startswith("buffer_") and "off, s[0:3]" in t):
+            c[5] += 1  # register spill traffic
         if t.startswith("v_"):
             c[0] += 1
             if "mfma" in t:
@@ -43,9 +45,9 @@ def main():
             c[3] += 1
         elif t.startswith("s_"):
             c[4] += 1
-    print(f"{'section (code after marker)':32s} {'VALU':>6s} {'MFMA':>5s} {'VMEM':>5s} {'LDS':>5s} {'SALU':>5s}")
-    for k, (v, mf, vm, ld, sa) in counts.items():
-        print(f"{k:32s} {v:6d} {mf:5d} {vm:5d} {ld:5d} {sa:5d}")
+    print(f"{'section (code after marker)':32s} {'VALU':>6s} {'MFMA':>5s} {'VMEM':>5s} {'LDS':>5s} {'SALU':>5s} {'SPILL':>5s}")
+    for k, (v, mf, vm, ld, sa, sp) in counts.items():
+        print(f"{k:32s} {v:6d} {mf:5d} {vm:5d} {ld:5d} {sa:5d} {sp:5d}")
     # f32 arithmetic by class, scalar vs packed (the SQ_INSTS_VALU_{FMA,ADD,MUL}_F32 counters count a
     # v_pk_* instruction once, tools/probes/flop_count.hip): the packed share of each class, for the
     # FP32-roofline FLOP count (profiles/r03/step_counters.json "flops_per_launch")

@@ -19,7 +19,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ["GO1_LIB_OVERRIDE"] = os.path.join(ROOT, "legged_tracking_amd", "_build", "libgo1_var_%s.so" % os.environ.get("GO1_STAMPS_VARIANT", "stamps"))
-WAVES, SLOTS = 4096, 160
+WAVES, SLOTS = 4096, int(os.environ.get("GO1_STAMPS_SLOTS", "320"))
 
 
 def main():
@@ -47,8 +47,13 @@ def main():
     assert lib.go1_debug_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
     g.close()
 
-    src = open(os.path.join(ROOT, "legged_tracking_amd", "csrc", "go1_step.hip")).read().splitlines()
-    name = {i + 1: m.group(1) for i, l in enumerate(src) for m in [re.search(r"MARK\((\w+)\)", l)] if m}
+    name = {}
+    for f in ("go1_step.hip", "go1_device.h"):  # (a line number marked in both files names both)
+        src = open(os.path.join(ROOT, "legged_tracking_amd", "csrc", f)).read().splitlines()
+        for i, l in enumerate(src):
+            m = re.search(r"MARK\((\w+)\)", l)
+            if m:
+                name[i + 1] = name[i + 1] + "|" + m.group(1) if i + 1 in name else m.group(1)
     nw = min(WAVES, n // 4)
     b = buf[: nw * SLOTS].reshape(nw, SLOTS)
     line = (b >> np.uint64(48)).astype(np.int64)
@@ -89,6 +94,17 @@ def main():
     extra = {nm: np.mean([per_wave[i][nm] for i in slow]) - np.mean([per_wave[i][nm] for i in mid]) for nm in secs}
     for nm, v in sorted(extra.items(), key=lambda x: -x[1])[:12]:
         print(f"{nm:28s} {v:+12.0f}")
+    # per-execution cost of the sections in the slowest waves (execs there vs the middle half)
+    cw = []
+    for w in range(nw):
+        k = int(np.count_nonzero(line[w]))
+        c = collections.Counter(name.get(int(line[w, i]), str(line[w, i])) for i in range(max(0, k - 1)))
+        cw.append(c)
+    print(f"\n{'section':28s} {'execs slow':>10s} {'execs mid':>10s} {'cyc/exec slow':>14s} {'cyc/exec mid':>13s}")
+    for nm in sorted(secs, key=lambda x: -extra[x])[:14]:
+        es = np.mean([cw[i][nm] for i in slow]); em = np.mean([cw[i][nm] for i in mid])
+        ts = np.mean([per_wave[i][nm] for i in slow]); tm = np.mean([per_wave[i][nm] for i in mid])
+        print(f"{nm:28s} {es:10.2f} {em:10.2f} {ts / max(es, 1e-9):14.0f} {tm / max(em, 1e-9):13.0f}")
 
 
 if __name__ == "__main__":
