@@ -60,12 +60,12 @@ PATH_BYTES_PER_ENV_STEP = 1696 + 2047
 PREWARM_S = 0.25
 # Algorithmic FLOPs per env-step, SURVEY.md 8(d): actuator MLP 132,144 (exact) + ABA / contact /
 # integration ~40,000 (estimate) + post-physics ~6,000 -> ~1.8e5.  The measured count (PMC VALU / MFMA
-# FLOP counters of the step kernel, profiles/r04/step_counters.json) is reported beside it.
+# FLOP counters of the step kernel, profiles/r05/step_counters.json) is reported beside it.
 SURVEY_FLOPS_PER_ENV_STEP = 1.8e5
 
 # PMC-measured HBM bytes per launch of the step kernel (tools/profile.sh + tools/prof_summary.py;
 # FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  Re-collected whenever the kernel changes.
-TRAFFIC_FILES = [os.path.join(REPO, "profiles", r, "step_counters.json") for r in ("r04", "r03", "r02", "r01")]
+TRAFFIC_FILES = [os.path.join(REPO, "profiles", r, "step_counters.json") for r in ("r05", "r04", "r03", "r02", "r01")]
 
 
 def pmc_counters(n_envs):

@@ -1644,16 +1644,18 @@ __device__ __forceinline__ int quad_or(int v) {
 
 // leg pairs lp: (0,1) = 0, (0,2) = 1, (0,3) = 2, (1,2) = 3, (1,3) = 4, (2,3) = 5
 
-// Narrow phase (a wave whose broad phase found a candidate; inline: out of line, the call's saves and
-// restores of the step kernel's ~500 live registers cost more than the narrow phase itself).  sc: this env's
-// LDS scratch, the spheres already written (self_put).  Each lane sums the forces on its own two spheres from
-// their partners directly -- for each candidate leg the other leg's 8 spheres in one LDS round trip, the two own
-// spheres in the halves of the tests -- so there are no force slots, no barriers and no dependent LDS trips
-// (the slot form cost ~10 us a step: a barrier and two round trips per leg pair, with one wave per SIMD nothing
-// hides them).  Each pair is evaluated once from each side; the two results are exactly opposite
-// (self_sphere_force), and every sphere's sum runs in a fixed order.  Fs: the self-contact world forces on the
-// lane's two spheres (x, y halves), wb: the trunk reaction wrench of the lane's box contacts (base frame, summed
-// over the env's lanes by the caller).
+// Narrow phase (a wave whose broad phase found a candidate).  sc: this env's LDS scratch, the spheres already
+// written (self_put).  Each lane sums the forces on its own two spheres from their partners directly: per
+// candidate partner leg, the leg's 8 spheres in one LDS round trip against both own spheres at once (packed
+// halves), the overlaps into a per-lane work list, then one force per list entry.  Both loops run as often as the
+// busiest lane needs -- with one wave per SIMD the launch lasts as long as its slowest wave, and the slow waves
+// are those with a folded env; a wave-uniform loop over every partner any lane touches (~90 VALU each) made the
+// narrow phase cost ~10 us of the launch, force slots with barriers likewise.  Each pair is evaluated once from
+// each side; the two results are exactly opposite (self_sphere_force), and every sphere's sum runs in a fixed
+// order (the list's bit order).  Fs: the self-contact world forces on the lane's two spheres (x, y halves), wb:
+// the trunk reaction wrench of the lane's box contacts (base frame, summed over the env's lanes by the caller).
+// Measured out of line (a call) and with the actuator net's weights reloaded per sub-step to free registers:
+// neither faster.
 __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
                                            const float* R, const float* pos, const float* vb, const float* th,
                                            float Fs[2][3], float* wb) {
@@ -1661,79 +1663,75 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
   const int s0 = self_s0(role), s1 = self_s1(role);
   const int ia0 = leg * 8 + s0, ia1 = leg * 8 + s1;
   float4* P = reinterpret_cast<float4*>(sc);
-  const float4 A0 = P[2 * ia0], A0v = P[2 * ia0 + 1], A1 = P[2 * ia1], A1v = P[2 * ia1 + 1];
+  // (the own spheres are re-read from LDS where needed: registers are scarce here, and every one freed lets the
+  // test loop keep more partner loads in flight)
   // the trunk box, by the lane of the sphere (thigh, calf and foot: every x half, the y halves of roles 0 and 2)
   if ((mask >> (6 + leg)) & 1) {
-    self_box_force(A0, A0v, R, pos, vb, th, ks, ds, Fs[0], wb);
-    if ((role & 1) == 0) self_box_force(A1, A1v, R, pos, vb, th, ks, ds, Fs[1], wb);
+    self_box_force(P[2 * ia0], P[2 * ia0 + 1], R, pos, vb, th, ks, ds, Fs[0], wb);
+    if ((role & 1) == 0) self_box_force(P[2 * ia1], P[2 * ia1 + 1], R, pos, vb, th, ks, ds, Fs[1], wb);
   }
   MARK(self_box_done);
-  // the other legs of candidate leg pairs (leg ^ d, d = 1, 2, 3: mask bits as self_broad sets them)
+  const float4 A0 = P[2 * ia0], A1 = P[2 * ia1];
+  // Tests first, forces from a per-lane work list: bit 16 d + 2 u + h of ovm = own sphere h overlaps sphere u of
+  // leg ^ d (d = 0: the own leg's pairs two joints apart, SELF_SAME_A / _B of the oracle; d = 1..3: the other
+  // legs of candidate leg pairs, mask bits as self_broad sets them).  The force loop then runs as many times as
+  // the busiest lane has overlaps (a wave-uniform loop over the partners would run every partner any lane
+  // touches, ~90 VALU each, at the pace of the one folded env of the wave).
+  const f2 Ax = f2{A0.x, A1.x}, Ay = f2{A0.y, A1.y}, Az = f2{A0.z, A1.z}, Ar = f2{A0.w, A1.w};
+  unsigned long long ovm = 0ull;
+  // the lane's candidate partner legs (bit d: leg ^ d), walked as a per-lane list like the forces below: the
+  // loop runs as often as the lane with the most candidates needs, not once per leg pair any env of the wave has
+  const int lp1 = (leg >> 1) ? 5 : 0, lp2 = (leg & 1) ? 4 : 1, lp3 = (leg == 0 || leg == 3) ? 2 : 3;
+  unsigned cand = ((mask >> (10 + leg)) & 1) | (((mask >> lp1) & 1) << 1) | (((mask >> lp2) & 1) << 2) |
+                  (((mask >> lp3) & 1) << 3);
+  // d = 0: hip ends 6, 7 against calf 3, 4 and foot 5; calf against the hip ends; foot against the hip ends and
+  // thigh 0-2; thigh against the foot (s0: 0, 2, 3 or 5; s1: 1, 6, 4 or 7)
+  const unsigned sm0 = s0 == 3 ? 0xC0u : (s0 == 5 ? 0xC7u : 0x20u);
+  const unsigned sm1 = s1 >= 6 ? 0x38u : (s1 == 4 ? 0xC0u : 0x20u);
+  while (__any(cand != 0u)) {
+    const bool act = cand != 0u;
+    const int d = act ? __builtin_ctz(cand) : 0;
+    cand &= cand - 1u;
+    const unsigned pm0 = !act ? 0u : (d == 0 ? sm0 : 0xFFu), pm1 = !act ? 0u : (d == 0 ? sm1 : 0xFFu);
+    const float4* Q = P + 16 * (leg ^ d);
+    unsigned bits = 0u;
+    float4 Bs[8];  // all eight partner loads in flight at once (one LDS round trip)
 #pragma unroll
-  for (int d = 1; d < 4; ++d) {
-    const int m = leg ^ d;
-    const int lp = d == 1 ? ((leg >> 1) ? 5 : 0) : (d == 2 ? ((leg & 1) ? 4 : 1) : ((leg == 0 || leg == 3) ? 2 : 3));
-    const bool on = (mask >> lp) & 1;
-    if (!__any(on)) continue;
+    for (int u = 0; u < 8; ++u) Bs[u] = Q[2 * u];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {  // one partner at a time: the narrow phase runs at the kernel's register peak
-      const int ib = m * 8 + u;
-      const float4 B = P[2 * ib];
-      const float a0 = A0.x - B.x, a1 = A0.y - B.y, a2 = A0.z - B.z, ra = A0.w + B.w;
-      const float c0 = A1.x - B.x, c1 = A1.y - B.y, c2 = A1.z - B.z, rc = A1.w + B.w;
-      const bool h0 = on && a0 * a0 + a1 * a1 + a2 * a2 < ra * ra, h1 = on && c0 * c0 + c1 * c1 + c2 * c2 < rc * rc;
-      if (!__any(h0 || h1)) continue;
-      const float4 Bv = P[2 * ib + 1];
-      float f[3] = {0.0f, 0.0f, 0.0f}, g[3] = {0.0f, 0.0f, 0.0f};
-      if (h0) self_sphere_force(A0, A0v, B, Bv, ks, ds, f, ia0 < ib ? 1.0f : -1.0f);
-      if (h1) self_sphere_force(A1, A1v, B, Bv, ks, ds, g, ia1 < ib ? 1.0f : -1.0f);
-      Fs[0][0] += f[0]; Fs[0][1] += f[1]; Fs[0][2] += f[2];
-      Fs[1][0] += g[0]; Fs[1][1] += g[1]; Fs[1][2] += g[2];
+    for (int u = 0; u < 8; ++u) {
+      const float4 B = Bs[u];
+      const f2 e0 = Ax - B.x, e1 = Ay - B.y, e2 = Az - B.z, rs = Ar + B.w;  // both own spheres (packed halves)
+      const f2 dd = e0 * e0 + e1 * e1 + e2 * e2, r2 = rs * rs;
+      bits |= (dd.x < r2.x ? 1u << (2 * u) : 0u) | (dd.y < r2.y ? 2u << (2 * u) : 0u);
+    }
+    // keep the pairs of the partner masks (h = 0: even bits, h = 1: odd bits)
+    unsigned keep = 0u;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) keep |= (((pm0 >> u) & 1u) << (2 * u)) | (((pm1 >> u) & 1u) << (2 * u + 1));
+    ovm |= (unsigned long long)(bits & keep) << (16 * d);
+  }
+  MARK(self_tests_done);
+  while (__any(ovm != 0ull)) {
+    const bool act = ovm != 0ull;
+    const int bit = act ? (int)__builtin_ctzll(ovm) : 0;
+    ovm &= ovm - 1ull;
+    const bool h = (bit & 1) != 0;
+    const int ib = ((leg ^ (bit >> 4)) << 3) + ((bit >> 1) & 7);
+    const float4 B = P[2 * ib], Bv = P[2 * ib + 1];
+    const int ia = h ? ia1 : ia0;
+    const float4 A = P[2 * ia], Av = P[2 * ia + 1];
+    float f[3];
+    self_sphere_force(A, Av, B, Bv, ks, ds, f, ia < ib ? 1.0f : -1.0f);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      Fs[0][i] += (act && !h) ? f[i] : 0.0f;
+      Fs[1][i] += (act && h) ? f[i] : 0.0f;
     }
   }
   MARK(self_cross_done);
-  // the leg's own links two joints apart (rare: unreachable within the joint limits): each own sphere against
-  // its partners of the oracle's SELF_SAME_A / _B -- hip ends 6, 7: calf 3, 4 and foot 5; calf: hip ends; foot:
-  // hip ends and thigh 0-2; thigh: foot
-  if (__any((mask >> (10 + leg)) & 1)) {
-    const bool on = (mask >> (10 + leg)) & 1;
-    const unsigned pm0 = s0 == 3 ? 0xC0u : (s0 == 5 ? 0xC7u : 0x20u);  // s0: 0, 2, 3 or 5
-    const unsigned pm1 = s1 >= 6 ? 0x38u : (s1 == 4 ? 0xC0u : 0x20u);  // s1: 1, 6, 4 or 7
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool h0 = on && ((pm0 >> u) & 1u), h1 = on && ((pm1 >> u) & 1u);
-      if (!__any(h0 || h1)) continue;
-      const int ib = leg * 8 + u;
-      const float4 B = P[2 * ib], Bv = P[2 * ib + 1];
-      float f[3] = {0.0f, 0.0f, 0.0f}, g[3] = {0.0f, 0.0f, 0.0f};
-      if (h0) self_sphere_force(A0, A0v, B, Bv, ks, ds, f, ia0 < ib ? 1.0f : -1.0f);
-      if (h1) self_sphere_force(A1, A1v, B, Bv, ks, ds, g, ia1 < ib ? 1.0f : -1.0f);
-      Fs[0][0] += f[0]; Fs[0][1] += f[1]; Fs[0][2] += f[2];
-      Fs[1][0] += g[0]; Fs[1][1] += g[1]; Fs[1][2] += g[2];
-    }
-  }
 }
-
-#ifdef GO1_ABL_SELF_NOINLINE  // A/B: the narrow phase out of line (its registers not reserved in the step kernel)
-struct SelfOut {
-  float f[12];
-};
-__device__ __noinline__ SelfOut self_narrow_ool(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
-                                               float R0, float R1, float R2, float R3, float R4, float R5, float R6,
-                                               float R7, float R8, float x0, float x1, float x2, float v0, float v1,
-                                               float v2, float v3, float v4, float v5) {
-  const float R[9] = {R0, R1, R2, R3, R4, R5, R6, R7, R8}, pos[3] = {x0, x1, x2}, vb[6] = {v0, v1, v2, v3, v4, v5};
-  const float* th = GO1_MODEL_F32 + 13 * 10 + 4 * 9 + 3 + 1;
-  float Fs[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}}, wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  self_narrow(cfg, sc, leg, role, mask, R, pos, vb, th, Fs, wb);
-  SelfOut o;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) { o.f[i] = Fs[0][i]; o.f[3 + i] = Fs[1][i]; }
-#pragma unroll
-  for (int i = 0; i < 6; ++i) o.f[6 + i] = wb[i];
-  return o;
-}
-#endif
 
 // the lane's spheres into this env's LDS scratch (x half s0, y half s1)
 __device__ __forceinline__ void self_put(float* sc, int leg, int role, const float* p0, const float* v0, float r0,
@@ -1764,6 +1762,7 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
 #pragma unroll
     for (int i = 0; i < 3; ++i) b[k][i] = R[i] * w0 + R[3 + i] * w1 + R[6 + i] * w2;
   }
+  // (bitwise &, |: short-circuit operators around the convergent DPP moves compile to exec-mask branches)
   bool o1 = true, o2 = true, o3 = true;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -1771,17 +1770,19 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
     const float tlo = fminf(b[0][i], clo), thi = fmaxf(b[0][i], chi);                       // + the thigh joint
     const float hlo = fminf(hc0[i], hc1[i]) - rhip, hhi = fmaxf(hc0[i], hc1[i]) + rhip;     // the hip capsule
     const float lo = fminf(tlo, hlo), hi = fmaxf(thi, hhi);
-    o1 = o1 && lo <= quad_xor<1>(hi) && quad_xor<1>(lo) <= hi;
-    o2 = o2 && lo <= quad_xor<2>(hi) && quad_xor<2>(lo) <= hi;
-    o3 = o3 && lo <= quad_xor<3>(hi) && quad_xor<3>(lo) <= hi;
+    const float lo1 = quad_xor<1>(lo), hi1 = quad_xor<1>(hi), lo2 = quad_xor<2>(lo), hi2 = quad_xor<2>(hi);
+    const float lo3 = quad_xor<3>(lo), hi3 = quad_xor<3>(hi);
+    o1 = o1 & (lo <= hi1) & (lo1 <= hi);
+    o2 = o2 & (lo <= hi2) & (lo2 <= hi);
+    o3 = o3 & (lo <= hi3) & (lo3 <= hi);
   }
   // the leg's own links two joints apart and the trunk box: out of reach while every joint of the leg is within
   // 0.1 rad of its URDF range (the nearest such contact needs 0.2 rad past a limit, a trunk box contact 0.89;
   // tests/test_self_collision.py::test_fold_gate_is_sound), so only a leg outside that band is tested -- then the
   // box exactly on the lane's own thigh, calf and foot spheres (x half; the y half on roles 0 and 2, grown by
   // 1e-4 against the narrow phase's rounding) and the same-leg pairs in the narrow phase
-  const bool wild = q[0] < -0.9029f || q[0] > 0.9029f || q[1] < -1.1472f || q[1] > 4.2888f || q[2] < -2.7966f ||
-                    q[2] > -0.8163f;
+  const bool wild = (fabsf(q[0]) > 0.9029f) | (q[1] < -1.1472f) | (q[1] > 4.2888f) | (q[2] < -2.7966f) |
+                    (q[2] > -0.8163f);
   int fold = 0;
   if (__any(wild)) {
     float bx = 0.0f, by = 0.0f;
@@ -1983,21 +1984,12 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
         }
         const float p0[3] = {pw[0].x, pw[1].x, pw[2].x}, v0[3] = {vw[0].x, vw[1].x, vw[2].x};
         self_put(self_sc, leg, role, p0, v0, rr.x, p1, v1, odd ? hip_r : rr.y);
-        __syncthreads();
+        // the block is this one wave (TPB 64): the other lanes' spheres are visible once the wave's own LDS
+        // writes completed -- no s_barrier, and above all no vmcnt(0) drain of the terrain loads in flight
+        static_assert(TPB == 64, "self-collision LDS exchange assumes one wave per block");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         MARK(self_put_done);
-#ifdef GO1_ABL_SELF_NOINLINE
-        {
-          const SelfOut o = self_narrow_ool(cfg, self_sc, leg, role, mask, R[0], R[1], R[2], R[3], R[4], R[5], R[6],
-                                            R[7], R[8], S.pos[0], S.pos[1], S.pos[2], vb[0], vb[1], vb[2], vb[3],
-                                            vb[4], vb[5]);
-#pragma unroll
-          for (int i = 0; i < 3; ++i) { Fs[0][i] = o.f[i]; Fs[1][i] = o.f[3 + i]; }
-#pragma unroll
-          for (int i = 0; i < 6; ++i) wb[i] = o.f[6 + i];
-        }
-#else
         self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
-#endif
         MARK(self_narrow_done);
         // the hip ends' forces (y halves of roles 1 and 3) on the hip link: hip-frame force f = Rh^T F and
         // moment (0, y, 0) x f, summed over the leg's rows (every role runs the leg's ABA); rare, so only in a

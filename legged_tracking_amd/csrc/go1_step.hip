@@ -385,17 +385,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int j = 0; j < 3; ++j) tq[j] = 0.0f * (b0[j] + b1v[j]);  // ablation build only: no actuator net
 #else
-#ifdef GO1_ABL_MLP_RELOAD
-      {
-        const float* W = c_gen->actuator;
-        asm volatile("" : "+s"(W));  // per sub-step: the fragments are not held across the loop
-        MlpFrag Fr;
-        mlp_load(W, lane, Fr);
-        mlp_group3(Fr, b0, b1v, tq);
-      }
-#else
       mlp_group3(F, b0, b1v, tq);
-#endif
 #endif
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll

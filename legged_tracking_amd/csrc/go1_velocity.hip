@@ -293,17 +293,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         b0[j] = sel4(lq, y[0], y[1], y[2], y[3]);
         b1v[j] = sel4(lq, y[4], y[5], 0.0f, 0.0f);
       }
-#ifdef GO1_ABL_MLP_RELOAD
-      {
-        const float* W = c_gen->actuator;
-        asm volatile("" : "+s"(W));  // per sub-step: the fragments are not held across the loop
-        MlpFrag Fr;
-        mlp_load(W, lane, Fr);
-        mlp_group3(Fr, b0, b1v, tq);
-      }
-#else
       mlp_group3(F, b0, b1v, tq);
-#endif
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         eh[1][j] = eh[0][j];
