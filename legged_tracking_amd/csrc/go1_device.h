@@ -48,6 +48,7 @@ __device__ __forceinline__ void go1_stamp(unsigned line) {
 #define NB 17
 #define EPB 16          // envs per block of the reset kernel (4 lanes per env)
 #define TPB 64          // one wave per block
+#define HOLD_N 23       // post-physics inputs parked in LDS across the step kernel's sub-step loop
 // LDS copy of the per-joint config arrays, contiguous in go1_config from default_dof_pos
 // (checked at go1_create): default_dof_pos, dof_pos_limits, torque_limits, hard_limits,
 // height_grid_x, height_grid_y, after the model block

@@ -217,15 +217,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const float friction = st.friction[e], payload = st.payload[e];
   // the env origin a reset needs, with the prologue loads (no memory round trip in the reset path)
-  const float eo_pre[3] = {K.ter.env_origins[(size_t)e * 3], K.ter.env_origins[(size_t)e * 3 + 1],
-                           K.ter.env_origins[(size_t)e * 3 + 2]};
-  const float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
+  float eo_pre[3] = {K.ter.env_origins[(size_t)e * 3], K.ter.env_origins[(size_t)e * 3 + 1],
+                     K.ter.env_origins[(size_t)e * 3 + 2]};
+  float cam_pitch = st.base_rotation[(size_t)e * 3 + 1];  // previous step's pitch (:1939)
   // ---- the post-physics state inputs ride with the prologue loads (one wait for all of
-  // them); they are held across the sub-step loop (AGPRs), so after the physics only the
-  // height-scan gathers make a memory round trip
-  const int ep_in = st.episode_length[e];
-  const int idx_in = st.curr_pose_index[e];
-  const int coll_in = st.collision_count[e];
+  // them); they wait out the sub-step loop in LDS (s_hold, below), so after the physics only
+  // the height-scan gathers make a memory round trip
+  int ep_in = st.episode_length[e];
+  int idx_in = st.curr_pose_index[e];
+  int coll_in = st.collision_count[e];
   const float restitution = st.restitution[e];
   const int TL = CI(traj_length), NT = CI(n_terms), NS = NT + 3;
   float traj_in[6], ldv[3], la[3];
@@ -243,8 +243,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   // reward slot k (Cfg.reward_scales order) belongs to the env's lane sub16 == k: its term id,
   // scale and episode sum; lanes 0..2 also carry total, total_pos, total_neg
-  const int my_id = sub16 < NT ? c_gen->term_ids[sub16] : GO1_T_NONE;
-  const float my_scale = A.reward_scales[sub16];
+  int my_id = sub16 < NT ? c_gen->term_ids[sub16] : GO1_T_NONE;
+  float my_scale = A.reward_scales[sub16];
   float my_sum = sub16 < NT ? st.episode_sums[(size_t)e * NS + sub16] : 0.0f;
   float my_tot = sub16 < 3 ? st.episode_sums[(size_t)e * NS + NT + sub16] : 0.0f;
   Phys P;
@@ -334,6 +334,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   }
   MARK(pro_dma_issued);
+  // The post-physics inputs wait out the sub-step loop in LDS, one column per lane: the loop's register
+  // peak is at the VGPR + AGPR limit, and these 23 values held across it pushed the kernel into scratch
+  // spills (an extra ~1 MB of HBM writes per launch).  hold() re-reads them through an opaque pointer (the
+  // compiler would otherwise forward the parked values and keep them in registers after all).
+  __shared__ float s_hold[HOLD_N][TPB];
+  auto hold = [&](bool park) {
+    float* hp = &s_hold[0][lane];
+    if (!park) asm volatile("" : "+v"(hp));
+    auto f = [&](int k, float& v) { if (park) hp[k * TPB] = v; else v = hp[k * TPB]; };
+    auto i = [&](int k, int& v) { float x = __int_as_float(v); f(k, x); v = __float_as_int(x); };
+#pragma unroll
+    for (int k = 0; k < 6; ++k) f(k, traj_in[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { f(6 + k, ldv[k]); f(9 + k, la[k]); f(12 + k, eo_pre[k]); }
+    f(15, cam_pitch); f(16, my_scale); f(17, my_sum); f(18, my_tot);
+    i(19, ep_in); i(20, idx_in); i(21, coll_in); i(22, my_id);
+  };
+  hold(true);
   asm volatile("" : "+v"(rebind_flag));  // kept in a VGPR: a scalar branch on it would wait early
   if (rebind && sub16 == 0 && rebind_flag) K.prev_extras[e] = rebind_val;
   float scaled[3];
@@ -434,6 +452,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   }
   cf_sum(cf_raw, role, cf_leg, cf_base, cf_hip);
+  hold(false);
   float root[13];
   if (INJ) {
 #pragma unroll
