@@ -961,6 +961,11 @@ struct CkShared {
   int wloaded;                                        // w holds the weights (loaded on first need)
 };
 
+// Workgroup barrier for LDS hand-offs: every exchange between the curriculum's sections goes through LDS, and
+// __syncthreads also waits out every global access in flight -- the sampling's command / observation stores
+// and the rebinding's writes, ~2 k cycles at each phase end for nothing (nothing in the launch reads them back).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // the weights into LDS, once per launch, when a phase first needs them (called by the whole workgroup)
 __device__ void ensure_weights(VCfg* v, const CArgs& K, CkShared& S) {
   if (S.wloaded) return;
@@ -969,9 +974,9 @@ __device__ void ensure_weights(VCfg* v, const CArgs& K, CkShared& S) {
     const int c = i / nb;
     S.w[(size_t)c * GO1_VEL_MAX_BINS + (i - c * nb)] = K.st.curriculum_weights[i];
   }
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) S.wloaded = 1;
-  __syncthreads();
+  lds_barrier();
 }
 
 // The curriculum runs on K.nblk workgroups.  Everything _resample_commands computes for the batch as a whole --
@@ -1031,7 +1036,7 @@ __device__ __forceinline__ void resample_prologue(VCfg* v, const CArgs& K, CkSha
       if (lane + 64 * i < nb) dst[lane + 64 * i] = t[i];
     if (lane == 0) S.pvalid[c] = ok;
   }
-  __syncthreads();
+  lds_barrier();
   VSTAMP(0, 10, t0);
 }
 
@@ -1113,7 +1118,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   }
   if (kindB && K.extras_time_outs)  // this workgroup's share of the rebinding
     for (int e = blk * CK_THREADS + tid; e < n; e += nblk * CK_THREADS) K.extras_time_outs[e] = K.time_out[e];
-  __syncthreads();
+  lds_barrier();
   VSTAMP(ph, 1, t0);
   const int n_list = S.cnt[2];
   // weights: cell j of category c gets +0.2 (clipped) once if it was a success bin and once per success
@@ -1123,7 +1128,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
   if (n_list > 0) {
     ensure_weights(v, K, S);
     for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.inc[i] = 0;
-    __syncthreads();
+    lds_barrier();
     for (int l = tid; l < n_list; l += CK_THREADS) {
       const int cb = S.list[l], cat = cb / nb, b = cb % nb, h = S.hist[cb];
       atomicAdd(&S.inc[cb], 1);  // weights[bin_inds[is_success]] += 0.2 (once per distinct bin)
@@ -1137,7 +1142,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
           if (j[u] >= 0) atomicAdd(&S.inc[cat * nb + j[u]], h);
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) {
       const int k = S.inc[i];
       if (k > 0) {
@@ -1149,7 +1154,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
         S.wchg = 1;
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
   VSTAMP(ph, 2, t0);
   // ---- numpy rng.choice(p = w / w.sum()): cdf = cumsum(p) / cdf[-1], wave c for category c, in LDS
@@ -1201,7 +1206,7 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
 #endif
     }
   }
-  __syncthreads();
+  lds_barrier();
   VSTAMP(ph, 3, t0);
   // ---- new category, cell and command per env (:759-842), this workgroup's envs (list positions
   // blk, blk + nblk, ...; env ids e % nblk == blk beyond the list capacity), 16 lanes per env: lane k < 15
@@ -1221,11 +1226,15 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
       const Rng rng = {U, K.seed, step, e, e + K.env_id_offset, GO1_VEL_U_PER_ENV};
       const RngD rngd = {UD, K.seed, step, e, e + K.env_id_offset};
       const int subc = min(sub, GO1_VEL_NUM_COMMANDS - 1);  // clamped: unconditional loads
-      float cmd = st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + subc];
-      if (sub >= GO1_VEL_NUM_COMMANDS) cmd = 0.0f;
+      // the old command (kept when the category draw fails) is read first and not touched before the draws and
+      // the cdf search are done
+      const float cmd_old = st.commands[(size_t)e * GO1_VEL_NUM_COMMANDS + subc];
+      const double half = v->bin_sizes[subc] / 2.0;
       const int cat = draw_category(rng(ucat));
+      float cmd = 0.0f;
       if (cat >= 0) {
         const double u = rngd(sub < GO1_VEL_NUM_COMMANDS ? dch + 1 + sub : dch);
+        VSTAMP(ph, 5, t0);
         int idx = 0;
         if (sub == 15) {
           idx = cdf_search(S.p + (size_t)cat * GO1_VEL_MAX_BINS, nb, u);
@@ -1235,7 +1244,8 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
           }
         }
         idx = __shfl(idx, 15, 16);
-        const double cen = K.grid[(size_t)subc * nb + idx], half = v->bin_sizes[subc] / 2.0;
+        VSTAMP(ph, 6, t0);
+        const double cen = K.grid[(size_t)subc * nb + idx];
         if (sub < GO1_VEL_NUM_COMMANDS) {
           const double l = cen + half, h = cen - half;
           cmd = (float)(l + (h - l) * u);
@@ -1245,6 +1255,8 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
             else cmd = 0.0f;
           }
         }
+      } else {
+        cmd = sub < GO1_VEL_NUM_COMMANDS ? cmd_old : 0.0f;
       }
       if (v->binary_phases && sub >= 5 && sub < 8) cmd = remainder1(rintf(2.0f * cmd) / 2.0f);
       {
@@ -1266,10 +1278,11 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
       }
     }
   }
+  VSTAMP(ph, 7, t0);
   // ready for the next phase: success counts and the pair list cleared
   for (int i = tid; i < GO1_VEL_N_CATEGORIES * nb; i += CK_THREADS) S.hist[i] = 0;
   if (tid == 0) S.cnt[2] = 0;
-  __syncthreads();
+  lds_barrier();
   VSTAMP(ph, 4, t0);
 }
 
@@ -1278,10 +1291,11 @@ __device__ void resample_phase(VCfg* v, const CArgs& K, bool kindB, CkShared& S)
 // precede its ticket; acquire: the last one sees every other workgroup done before it writes.
 __device__ void resample_commit(VCfg* v, const CArgs& K, CkShared& S) {
   const int tid = threadIdx.x, nb = K.nb;
-  __syncthreads();
+  lds_barrier();
   // every workgroup takes the same decisions: with no weight changed and no cdf recomputed there is nothing
   // to commit, and none of them takes a ticket
   if (!S.wchg && !S.rec_[0] && !S.rec_[1] && !S.rec_[2] && !S.rec_[3]) return;
+  __syncthreads();  // (a commit: every thread's global accesses precede the ticket's release)
 #ifdef GO1_VEL_STAMPS
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif

@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ["GO1_VEL_LIB_OVERRIDE"] = os.environ.get("VEL_STAMPS_LIB") or os.path.join(ROOT, "legged_tracking_amd", "_build", "libgo1_velocity_stamps.so")
 NAMES = {0: "scan (all phases)", 15: "count>0 entry", 1: "success hist", 2: "weights update", 3: "cdf",
-         4: "sampling", 14: "cdf recomputes (count)", 10: "prologue (phase B row: every launch)",
+         4: "sampling (clear + barrier)", 5: "sampling: records, loads, draws", 6: "sampling: cdf search + shfl",
+         7: "sampling: centre, commands, stores", 14: "cdf recomputes (count)", 10: "prologue (phase B row: every launch)",
          11: "commit (phase B row, launches that commit)"}
 
 
@@ -46,7 +47,7 @@ def main():
     for ph, name in ((0, "B (reset envs)"), (1, "A (next interval envs)")):
         ran = max(int(buf[ph, 15] > 0), 1)
         print(f"phase {name}: {calls} launches")
-        for k in (10, 11, 0, 15, 1, 2, 3, 4, 14):
+        for k in (10, 11, 0, 15, 1, 2, 3, 5, 6, 7, 4, 14):
             print(f"  {NAMES[k]:<26} {int(buf[ph, k]):>14}  per launch {buf[ph, k] / calls:10.0f}")
     env.env.close()
 
