@@ -284,7 +284,7 @@ def test_engine_world_n_arithmetic_equals_one_engine_over_the_union(world, n_loc
     gives them):
       * the same learning-rate decisions, after the first mini-batch and after the whole update (5 epochs x 4
         mini-batches); after the first mini-batch the loss sums within rtol 1e-6 (a wrong / world is off by the
-        factor world in the loss sums and the KL mean);
+        factor world in the loss sums and the KL mean) and the weights p99.99 within 1e-5;
       * losses and weights as close to the union's as one engine over the same union with the rows of every
         mini-batch in another order (the floor: the 3xF16 operand scaling is per tensor, so any regrouping of the
         rows rounds differently -- Adam's first step is lr g / (|g| + eps), which turns that into weight
@@ -386,8 +386,10 @@ def test_engine_world_n_arithmetic_equals_one_engine_over_the_union(world, n_loc
               f"(reorder floor {dl_f.max():.2e}); weights max {d_w.max():.2e} p99.99 {np.percentile(d_w, 99.99):.2e} "
               f"(floor {d_f.max():.2e} / {np.percentile(d_f, 99.99):.2e}; the update moved weights by up to "
               f"{dw(s1, base_sd).max():.2e}); lr {r1:.3e}")
-        if loss_rtol:  # one step: the loss sums agree to rounding (a wrong / world is off by the factor world)
+        if loss_rtol:  # one step: the loss sums agree to rounding (a wrong / world is off by the factor world),
+            # and the weights p99.99 within VERDICT r04's 1e-5 (measured 6.9e-7 at world 2, 1.7e-6 at world 8)
             assert (dl_w <= loss_rtol).all(), (when, dl_w)
+            assert np.percentile(d_w, 99.99) <= 1e-5, (when, np.percentile(d_w, 99.99))
         assert (dl_w <= np.maximum(4 * dl_f, 1e-6)).all(), (when, dl_w, dl_f)
         assert np.percentile(d_w, 99.99) <= max(4 * np.percentile(d_f, 99.99), 1e-6), when
         assert d_w.max() <= max(4 * d_f.max(), 1e-5), when
