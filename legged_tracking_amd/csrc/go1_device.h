@@ -1747,14 +1747,12 @@ __device__ __forceinline__ void self_put(float* sc, int leg, int role, const flo
 
 // Broad phase, in registers, in the trunk frame (where the legs keep their places whatever the trunk's
 // pose; world-axis boxes of a yawed trunk overlap every leg): bit lp of the result = leg pair lp's boxes overlap,
-// bit 6 + leg = one of the lane's own box spheres meets the trunk box (exact), bit 10 + leg = the leg is folded
-// past its joint band (its same-leg pairs are tested); the pair bits on the env's 16 lanes.  pth, pkn, pft: the
-// thigh joint, knee and foot (world); hc0, hc1: the hip capsule's ends in the trunk frame; pw, rr: the lane's two
-// contact spheres (world centres, radii), box_y: the y half is a box sphere (roles 0 and 2); q: the leg's joints.
+// bits 6 + leg and 10 + leg = the leg is folded past its joint band (its trunk-box and same-leg pairs are
+// tested); the pair bits on the env's 16 lanes.  pth, pkn, pft: the thigh joint, knee and foot (world); hc0, hc1:
+// the hip capsule's ends in the trunk frame; q: the leg's joints.
 __device__ __forceinline__ int self_broad(int leg, const float* pth, const float* pkn, const float* pft, float rmax,
                                           const float* hc0, const float* hc1, float rhip,
-                                          const float* R, const float* pos, const float* th, const f2* pw, f2 rr,
-                                          bool box_y, const float* q) {
+                                          const float* R, const float* pos, const float* th, const float* q) {
   float b[3][3];  // the three points in the trunk frame, R^T (p - pos)
   const float* pts[3] = {pth, pkn, pft};
 #pragma unroll
@@ -1779,25 +1777,11 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
   }
   // the leg's own links two joints apart and the trunk box: out of reach while every joint of the leg is within
   // 0.1 rad of its URDF range (the nearest such contact needs 0.2 rad past a limit, a trunk box contact 0.89;
-  // tests/test_self_collision.py::test_fold_gate_is_sound), so only a leg outside that band is tested -- then the
-  // box exactly on the lane's own thigh, calf and foot spheres (x half; the y half on roles 0 and 2, grown by
-  // 1e-4 against the narrow phase's rounding) and the same-leg pairs in the narrow phase
+  // tests/test_self_collision.py::test_fold_gate_is_sound), so only a leg outside that band goes to the narrow
+  // phase for them (no branch here: the broad phase shares a basic block with the terrain contacts)
   const bool wild = (fabsf(q[0]) > 0.9029f) | (q[1] < -1.1472f) | (q[1] > 4.2888f) | (q[2] < -2.7966f) |
                     (q[2] > -0.8163f);
-  int fold = 0;
-  if (__any(wild)) {
-    float bx = 0.0f, by = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float cx = R[i] * (pw[0].x - pos[0]) + R[3 + i] * (pw[1].x - pos[1]) + R[6 + i] * (pw[2].x - pos[2]);
-      const float cy = R[i] * (pw[0].y - pos[0]) + R[3 + i] * (pw[1].y - pos[1]) + R[6 + i] * (pw[2].y - pos[2]);
-      const float dx = cx - fminf(fmaxf(cx, -th[i]), th[i]), dy = cy - fminf(fmaxf(cy, -th[i]), th[i]);
-      bx += dx * dx; by += dy * dy;
-    }
-    const float rbx = rr.x + 1e-4f, rby = rr.y + 1e-4f;
-    const bool ob = bx < rbx * rbx || (box_y && by < rby * rby);
-    fold = wild ? ((ob ? 64 << leg : 0) | (1024 << leg)) : 0;
-  }
+  const int fold = wild ? ((64 << leg) | (1024 << leg)) : 0;  // the narrow phase tests them exactly
   const int lp1 = (leg >> 1) ? 5 : 0;                         // (0,1) / (2,3)
   const int lp2 = (leg & 1) ? 4 : 1;                          // (0,2) / (1,3)
   const int lp3 = (leg == 0 || leg == 3) ? 2 : 3;             // (0,3) / (1,2)
@@ -1944,87 +1928,95 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       hq_fetch(T, pw[0].x, pw[1].x, qa);
       hq_fetch(T, pw[0].y, pw[1].y, qb);
     }
-    // self-collision while the terrain reads land: world forces on the lane's two spheres, the trunk's
-    // reaction wrench of the lane's box pairs into its trunk share
+    // self-collision: world forces on the lane's two spheres, the trunk's reaction wrench of the lane's box pairs
+    // into its trunk share.  The broad phase has no branch around it (the off switch is a select), so it sits in
+    // one basic block with the terrain contacts below and the scheduler overlaps its latency chains (trunk-frame
+    // transforms, DPP exchanges) with theirs; the narrow phase follows the contacts.
     float Fs[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}}, wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int i = 0; i < 3; ++i) cf_raw[6 + i] = 0.0f;  // the hip's reported force of this sim step, from here
+    MARK(self_begin);
+    // the hip capsule's ends in the trunk frame: the hip joint + Rx(q_hip) (0, y, 0)
+    const f2 hy = msy * f2{hip_y0, hip_y1};
+    const f2 hcy = origin[1] + cs[0][0] * hy, hcz = origin[2] + cs[0][1] * hy;
+    const float hc0[3] = {origin[0], hcy.x, hcz.x}, hc1[3] = {origin[0], hcy.y, hcz.y};
 #ifndef GO1_ABL_NO_SELF  // ablation build only: no self-collision
-    if (cfg->self_stiffness > 0.0f) {
-#else
-    if (false) {
-#endif
-      MARK(self_begin);
+    const bool self_on = cfg->self_stiffness > 0.0f;
+    int mask;
+    {
       float pft[3];  // the foot centre (calf frame offset), for the leg's bounding box
 #pragma unroll
       for (int i = 0; i < 3; ++i) pft[i] = pl[1][i] + Rl[1][3 * i] * foot[0] + Rl[1][3 * i + 1] * foot[1] + Rl[1][3 * i + 2] * foot[2];
-      // the hip capsule's ends in the trunk frame: the hip joint + Rx(q_hip) (0, y, 0)
-      const f2 hy = msy * f2{hip_y0, hip_y1};
-      const f2 hcy = origin[1] + cs[0][0] * hy, hcz = origin[2] + cs[0][1] * hy;
-      const float hc0[3] = {origin[0], hcy.x, hcz.x}, hc1[3] = {origin[0], hcy.y, hcz.y};
-      const int mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), hc0,
-                                  hc1, hip_r, R, S.pos, th, pw, rr, (role & 1) == 0, S.q);
-      MARK(self_broad_done);
-      if (__any(mask != 0)) {
-        // the lane's second sphere: point b of the contact pass, or on roles 1 and 3 an end of the hip capsule
-        // (world p = pos + R c, v = R (v_b + w_b x c + qd_hip e_x x (c - hip joint)))
-        const bool odd = (role & 1) != 0;
-        const float* hc = role == 1 ? hc0 : hc1;
-        float p1[3], v1[3];
-        {
-          const float rx = hc[1] - origin[1], rz = hc[2] - origin[2];  // e_x x (0, ry, rz) = (0, -rz, ry)
-          const float vh[3] = {vb[3] + (vb[1] * hc[2] - vb[2] * hc[1]), vb[4] + (vb[2] * hc[0] - vb[0] * hc[2]) - S.qd[0] * rz,
-                               vb[5] + (vb[0] * hc[1] - vb[1] * hc[0]) + S.qd[0] * rx};
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const float ph = S.pos[i] + (R[3 * i] * hc[0] + R[3 * i + 1] * hc[1] + R[3 * i + 2] * hc[2]);
-            const float vw_h = R[3 * i] * vh[0] + R[3 * i + 1] * vh[1] + R[3 * i + 2] * vh[2];
-            p1[i] = odd ? ph : pw[i].y;
-            v1[i] = odd ? vw_h : vw[i].y;
-          }
-        }
-        const float p0[3] = {pw[0].x, pw[1].x, pw[2].x}, v0[3] = {vw[0].x, vw[1].x, vw[2].x};
-        self_put(self_sc, leg, role, p0, v0, rr.x, p1, v1, odd ? hip_r : rr.y);
-        // the block is this one wave (TPB 64): the other lanes' spheres are visible once the wave's own LDS
-        // writes completed -- no s_barrier, and above all no vmcnt(0) drain of the terrain loads in flight
-        static_assert(TPB == 64, "self-collision LDS exchange assumes one wave per block");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        MARK(self_put_done);
-        self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
-        MARK(self_narrow_done);
-        // the hip ends' forces (y halves of roles 1 and 3) on the hip link: hip-frame force f = Rh^T F and
-        // moment (0, y, 0) x f, summed over the leg's rows (every role runs the leg's ABA); rare, so only in a
-        // wave that has one
-        if (__any(odd && (Fs[1][0] != 0.0f || Fs[1][1] != 0.0f || Fs[1][2] != 0.0f))) {
-          float hv[8];
-          {
-            const float F0 = odd ? Fs[1][0] : 0.0f, F1 = odd ? Fs[1][1] : 0.0f, F2 = odd ? Fs[1][2] : 0.0f;
-            const float r0 = R[0] * F0 + R[3] * F1 + R[6] * F2, r1 = R[1] * F0 + R[4] * F1 + R[7] * F2,
-                        r2 = R[2] * F0 + R[5] * F1 + R[8] * F2;
-            const float fh1 = cs[0][0] * r1 + cs[0][1] * r2, fh2 = cs[0][0] * r2 - cs[0][1] * r1;
-            const float y = role == 1 ? hy.x : hy.y;
-            hv[0] = y * fh2; hv[1] = -(y * r0); hv[2] = r0; hv[3] = fh1; hv[4] = fh2;
-            hv[5] = F0; hv[6] = F1; hv[7] = F2;
-          }
-          rowsum4_n<8>(hv);
-          pAp[0][0] -= f2{hv[0], hv[2]};
-          pAp[0][1] -= f2{0.0f, hv[3]};
-          pAp[0][2] -= f2{hv[1], hv[4]};
-#pragma unroll
-          for (int i = 0; i < 3; ++i) cf_raw[6 + i] = hv[5 + i];  // the hip's self-contact force (+ Fhip at the end)
-        }
-        if (odd) { Fs[1][0] = 0.0f; Fs[1][1] = 0.0f; Fs[1][2] = 0.0f; }  // not the trunk corner's
-        MARK(self_hip_done);
-      }
-#pragma unroll
-      for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
+      mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), hc0, hc1, hip_r, R, S.pos, th,
+                        S.q);
+      mask = self_on ? mask : 0;
     }
+#else
+    const bool self_on = false;
+    const int mask = 0;
+#endif
+    MARK(self_broad_done);
     float Fa[3], Fb2[3], Ma[6], Mb[6];
     {
       const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
       const float pb[3] = {pw[0].y, pw[1].y, pw[2].y}, vb2[3] = {vw[0].y, vw[1].y, vw[2].y};
       sphere_contact_im(T, qa, C, pa, va, rr.x, h, Fa, Ma);
       sphere_contact_im(T, qb, C, pb, vb2, rr.y, h, Fb2, Mb);
+    }
+    if (__any(mask != 0)) {
+      // the lane's second sphere: point b of the contact pass, or on roles 1 and 3 an end of the hip capsule
+      // (world p = pos + R c, v = R (v_b + w_b x c + qd_hip e_x x (c - hip joint)))
+      const bool odd = (role & 1) != 0;
+      const float* hc = role == 1 ? hc0 : hc1;
+      float p1[3], v1[3];
+      {
+        const float rx = hc[1] - origin[1], rz = hc[2] - origin[2];  // e_x x (0, ry, rz) = (0, -rz, ry)
+        const float vh[3] = {vb[3] + (vb[1] * hc[2] - vb[2] * hc[1]), vb[4] + (vb[2] * hc[0] - vb[0] * hc[2]) - S.qd[0] * rz,
+                             vb[5] + (vb[0] * hc[1] - vb[1] * hc[0]) + S.qd[0] * rx};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const float ph = S.pos[i] + (R[3 * i] * hc[0] + R[3 * i + 1] * hc[1] + R[3 * i + 2] * hc[2]);
+          const float vw_h = R[3 * i] * vh[0] + R[3 * i + 1] * vh[1] + R[3 * i + 2] * vh[2];
+          p1[i] = odd ? ph : pw[i].y;
+          v1[i] = odd ? vw_h : vw[i].y;
+        }
+      }
+      const float p0[3] = {pw[0].x, pw[1].x, pw[2].x}, v0[3] = {vw[0].x, vw[1].x, vw[2].x};
+      self_put(self_sc, leg, role, p0, v0, rr.x, p1, v1, odd ? hip_r : rr.y);
+      // the block is this one wave (TPB 64): the other lanes' spheres are visible once the wave's own LDS
+      // writes completed -- no s_barrier, and above all no vmcnt(0) drain of the terrain loads in flight
+      static_assert(TPB == 64, "self-collision LDS exchange assumes one wave per block");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      MARK(self_put_done);
+      self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
+      MARK(self_narrow_done);
+      // the hip ends' forces (y halves of roles 1 and 3) on the hip link: hip-frame force f = Rh^T F and
+      // moment (0, y, 0) x f, summed over the leg's rows (every role runs the leg's ABA); rare, so only in a
+      // wave that has one
+      if (__any(odd && (Fs[1][0] != 0.0f || Fs[1][1] != 0.0f || Fs[1][2] != 0.0f))) {
+        float hv[8];
+        {
+          const float F0 = odd ? Fs[1][0] : 0.0f, F1 = odd ? Fs[1][1] : 0.0f, F2 = odd ? Fs[1][2] : 0.0f;
+          const float r0 = R[0] * F0 + R[3] * F1 + R[6] * F2, r1 = R[1] * F0 + R[4] * F1 + R[7] * F2,
+                      r2 = R[2] * F0 + R[5] * F1 + R[8] * F2;
+          const float fh1 = cs[0][0] * r1 + cs[0][1] * r2, fh2 = cs[0][0] * r2 - cs[0][1] * r1;
+          const float y = role == 1 ? hy.x : hy.y;
+          hv[0] = y * fh2; hv[1] = -(y * r0); hv[2] = r0; hv[3] = fh1; hv[4] = fh2;
+          hv[5] = F0; hv[6] = F1; hv[7] = F2;
+        }
+        rowsum4_n<8>(hv);
+        pAp[0][0] -= f2{hv[0], hv[2]};
+        pAp[0][1] -= f2{0.0f, hv[3]};
+        pAp[0][2] -= f2{hv[1], hv[4]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) cf_raw[6 + i] = hv[5 + i];  // the hip's self-contact force (+ Fhip at the end)
+      }
+      if (odd) { Fs[1][0] = 0.0f; Fs[1][1] = 0.0f; Fs[1][2] = 0.0f; }  // not the trunk corner's
+      MARK(self_hip_done);
+    }
+    if (self_on) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) { Fa[i] += Fs[0][i]; Fb2[i] += Fs[1][i]; }
