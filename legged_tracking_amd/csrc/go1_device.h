@@ -1687,13 +1687,17 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
                   (((mask >> lp3) & 1) << 3);
   // d = 0: hip ends 6, 7 against calf 3, 4 and foot 5; calf against the hip ends; foot against the hip ends and
   // thigh 0-2; thigh against the foot (s0: 0, 2, 3 or 5; s1: 1, 6, 4 or 7)
+  // as list bits (h = 0: even bits 2 u, h = 1: odd bits 2 u + 1), interleaved once here
   const unsigned sm0 = s0 == 3 ? 0xC0u : (s0 == 5 ? 0xC7u : 0x20u);
   const unsigned sm1 = s1 >= 6 ? 0x38u : (s1 == 4 ? 0xC0u : 0x20u);
+  unsigned keep_same = 0u;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) keep_same |= (((sm0 >> u) & 1u) << (2 * u)) | (((sm1 >> u) & 1u) << (2 * u + 1));
   while (__any(cand != 0u)) {
     const bool act = cand != 0u;
     const int d = act ? __builtin_ctz(cand) : 0;
     cand &= cand - 1u;
-    const unsigned pm0 = !act ? 0u : (d == 0 ? sm0 : 0xFFu), pm1 = !act ? 0u : (d == 0 ? sm1 : 0xFFu);
+    const unsigned keep = !act ? 0u : (d == 0 ? keep_same : 0xFFFFu);
     const float4* Q = P + 16 * (leg ^ d);
     unsigned bits = 0u;
     float4 Bs[8];  // all eight partner loads in flight at once (one LDS round trip)
@@ -1707,10 +1711,6 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
       const f2 dd = e0 * e0 + e1 * e1 + e2 * e2, r2 = rs * rs;
       bits |= (dd.x < r2.x ? 1u << (2 * u) : 0u) | (dd.y < r2.y ? 2u << (2 * u) : 0u);
     }
-    // keep the pairs of the partner masks (h = 0: even bits, h = 1: odd bits)
-    unsigned keep = 0u;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) keep |= (((pm0 >> u) & 1u) << (2 * u)) | (((pm1 >> u) & 1u) << (2 * u + 1));
     ovm |= (unsigned long long)(bits & keep) << (16 * d);
   }
   MARK(self_tests_done);
