@@ -1183,6 +1183,14 @@ int go1_debug_stamps(void* host, size_t bytes) {
   if (bytes > sizeof(g_go1_stamps)) bytes = sizeof(g_go1_stamps);
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_go1_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
+// zero the stamp buffer (before the launch to be read: a wave records only as many slots as it executes
+// markers, so slots of an earlier launch with more markers would otherwise survive behind them)
+int go1_debug_stamps_clear(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_go1_stamps)) != hipSuccess) return 1;
+  if (hipMemset(p, 0, sizeof(g_go1_stamps)) != hipSuccess) return 1;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
 #endif
 
 int go1_abi_version(void) { return GO1_ABI_VERSION; }

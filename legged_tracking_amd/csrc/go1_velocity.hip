@@ -876,6 +876,7 @@ __device__ unsigned long long g_vstamps[2][16];
 #define VSTAMP(ph, k, t0)
 #endif
 #define CK_PRE 1024  // list records prefetched into LDS per phase (one per thread); the rest read from memory
+static_assert(CK_PRE <= CK_THREADS, "the prologue fills one prefetched record per thread (S.rec[ph][tid], tid < CK_THREADS)");
 // the curriculum's record of a selected env: (env, command category, command bin, success of every task over the
 // episode's command sums) -- written by the step kernel (or go1_vel_list_kernel) before the launch
 typedef int4 CkRec;

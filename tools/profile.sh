@@ -18,4 +18,8 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_
 echo sq done
 timeout -k 10 300 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY --output-format csv -d "$OUT/sq2" -o sq2 -- python3 $B > "$OUT/sq2.log" 2>&1 || { echo "sq2 rc=$?"; tail -20 "$OUT/sq2.log"; }
 echo sq2 done
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS --output-format csv -d "$OUT/lds" -o lds -- python3 $B > "$OUT/lds.log" 2>&1 || { echo "lds rc=$?"; tail -20 "$OUT/lds.log"; }
+echo lds done
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 --output-format csv -d "$OUT/flop" -o flop -- python3 $B > "$OUT/flop.log" 2>&1 || { echo "flop rc=$?"; tail -20 "$OUT/flop.log"; }
+echo flop done
 find "$OUT" -name "*.csv" | head -20

@@ -1,5 +1,8 @@
 """Where one step-kernel launch spends its time, per source section (diagnostic build).
 
+The stamp buffer is zeroed before each of the GO1_STAMPS_MEASURE launches read (after
+GO1_STAMPS_STEPS warm-up launches); every statistic is over (launch, wave) records.
+
   local:  bash tools/variants.sh build stamps "-DGO1_STAMPS"
   gpurun: python tools/stamps.py [n_envs]
 
@@ -39,12 +42,20 @@ def main():
     scales = CF.reward_scale_vector(CF.derived(cfg)["reward_scales"])
     grav, gvec = CF.gravity_state(rng.uniform(-1, 1, 3))
     ring = torch.randn((8, n, 12), device=dev)
-    for k in range(int(os.environ.get('GO1_STAMPS_STEPS', '30'))):
-        g.step(ring[k % 8], gvec, grav, scales, rng_seed=11, rng_step=1 + k)
-    torch.cuda.synchronize()
+    warm = int(os.environ.get('GO1_STAMPS_STEPS', '30'))
+    meas = int(os.environ.get('GO1_STAMPS_MEASURE', '8'))
     lib = native.lib()
-    buf = np.zeros(WAVES * SLOTS, np.uint64)
-    assert lib.go1_debug_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
+    bufs = []
+    for k in range(warm + meas):
+        if k >= warm:  # every measured launch starts from a zeroed buffer (stale slots of an earlier launch
+            torch.cuda.synchronize()  # with more markers would otherwise be read as this launch's)
+            assert lib.go1_debug_stamps_clear() == 0
+        g.step(ring[k % 8], gvec, grav, scales, rng_seed=11, rng_step=1 + k)
+        if k >= warm:
+            torch.cuda.synchronize()
+            buf = np.zeros(WAVES * SLOTS, np.uint64)
+            assert lib.go1_debug_stamps(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
+            bufs.append(buf)
     g.close()
 
     name = {}
@@ -55,17 +66,22 @@ def main():
             if m:
                 name[i + 1] = name[i + 1] + "|" + m.group(1) if i + 1 in name else m.group(1)
     nw = min(WAVES, n // 4)
-    b = buf[: nw * SLOTS].reshape(nw, SLOTS)
+    b = np.concatenate([x[: nw * SLOTS].reshape(nw, SLOTS) for x in bufs])  # (launches x waves, slots)
     line = (b >> np.uint64(48)).astype(np.int64)
     t = (b & np.uint64((1 << 48) - 1)).astype(np.int64)
+    nrec = np.count_nonzero(line, 1)
+    # a record is written in slot order: the count of non-zero slots is the number of markers executed
+    assert all(np.count_nonzero(line[w, : nrec[w]]) == nrec[w] for w in range(len(line)))
     tot = collections.Counter()
     cnt = collections.Counter()
     life = []
-    per_wave = []  # per wave: section -> cycles (the tail analysis below)
-    for w in range(nw):
-        k = int(np.count_nonzero(line[w]))
+    per_wave = []  # per (launch, wave): section -> cycles (the tail analysis below)
+    keep = []
+    for w in range(len(line)):
+        k = int(nrec[w])
         if k < 2:
             continue
+        keep.append(w)
         life.append(t[w, k - 1] - t[w, 0])
         pw = collections.Counter()
         for i in range(k - 1):
@@ -74,13 +90,14 @@ def main():
             pw[nm] += int(t[w, i + 1] - t[w, i])
             cnt[nm] += 1
         per_wave.append(pw)
+    assert min(life) > 0, "negative wave lifetime: stale stamps"
     L = float(np.mean(life))
     lf = np.array(life, np.float64)
     print(f"wave lifetime cycles: p50 {np.percentile(lf, 50):.0f}  p90 {np.percentile(lf, 90):.0f}  "
           f"p99 {np.percentile(lf, 99):.0f}  max {lf.max():.0f}  min {lf.min():.0f}")
-    starts = t[:, 0]
-    print(f"waves {len(life)}; mean wave lifetime {L:.0f} cycles (s_memtime); start spread "
-          f"{(starts.max() - starts.min()):.0f} cycles; stamps per wave {int(np.mean(np.count_nonzero(line, 1)))}")
+    print(f"wave records {len(life)} ({len(bufs)} launches x {nw} waves); mean wave lifetime {L:.0f} cycles "
+          f"(s_memtime, per-wave differences only: the counters of different XCDs are not aligned); "
+          f"stamps per wave {np.mean(nrec):.0f}")
     print(f"{'section (after marker)':28s} {'cycles/wave':>12s} {'share':>7s} {'execs':>6s}")
     for nm, v in sorted(tot.items(), key=lambda x: -x[1]):
         print(f"{nm:28s} {v / len(life):12.0f} {v / len(life) / L:7.1%} {cnt[nm] / len(life):6.1f}")
@@ -96,8 +113,8 @@ def main():
         print(f"{nm:28s} {v:+12.0f}")
     # per-execution cost of the sections in the slowest waves (execs there vs the middle half)
     cw = []
-    for w in range(nw):
-        k = int(np.count_nonzero(line[w]))
+    for w in keep:
+        k = int(nrec[w])
         c = collections.Counter(name.get(int(line[w, i]), str(line[w, i])) for i in range(max(0, k - 1)))
         cw.append(c)
     print(f"\n{'section':28s} {'execs slow':>10s} {'execs mid':>10s} {'cyc/exec slow':>14s} {'cyc/exec mid':>13s}")
