@@ -226,6 +226,22 @@ __device__ __forceinline__ void mlp_load(const float* __restrict__ W, int lane, 
   F.b3 = W[1312];
 }
 
+// The fragments wait out each sub-step's physics in LDS (round 6): the loop's register peak (the self-collision narrow
+// phase, the capsule search, the trunk faces) is at the VGPR + AGPR limit, and 45 values held across it made the
+// compiler spill.  mlp_unpark re-reads them through an opaque pointer before each evaluation (48 x 64 floats per wave).
+#define MLP_PARK_FLOATS ((int)(sizeof(MlpFrag) / sizeof(float)))
+__device__ __forceinline__ void mlp_park(const MlpFrag& F, float* s, int lane) {
+  const float* f = reinterpret_cast<const float*>(&F);
+#pragma unroll
+  for (int k = 0; k < MLP_PARK_FLOATS; ++k) s[k * 64 + lane] = f[k];
+}
+__device__ __forceinline__ void mlp_unpark(MlpFrag& F, const float* s, int lane) {
+  asm volatile("" : "+v"(s));  // opaque: no forwarding of the parked values (they would stay live in registers)
+  float* f = reinterpret_cast<float*>(&F);
+#pragma unroll
+  for (int k = 0; k < MLP_PARK_FLOATS; ++k) f[k] = s[k * 64 + lane];
+}
+
 // b0 = X[k = q][item], b1v = X[k = 4 + q][item] (0 for q >= 2).  Returns the torque
 // of item (lane & 15) in all four lanes of the item.  Needs all 64 lanes active.
 __device__ __forceinline__ float mlp_group(const MlpFrag& F, float b0, float b1v) {
@@ -972,40 +988,6 @@ __device__ __forceinline__ float tile_at(const Terr& T, int layer, int i, int j)
   return T.tile[((size_t)layer * T.nx + i) * T.ny + j];
 }
 
-// floor (layer 1) and ceiling (layer 0) heights and gradients at world (x, y), bilinear
-__device__ __forceinline__ void height_query2(const Terr& T, float x, float y, float* hf, float* hc) {
-  if (!T.tile) {
-    hf[0] = 0.0f; hf[1] = 0.0f; hf[2] = 0.0f;
-    hc[0] = 1e9f; hc[1] = 0.0f; hc[2] = 0.0f;
-    return;
-  }
-  // bounded before the float -> int conversions (a diverged pose must not index memory)
-  const float ihs = frcp(T.hs);
-  const float u = fminf(fmaxf(x * ihs, -4.0f), (float)(T.nx + 4));
-  const float v = fminf(fmaxf(y * ihs, -4.0f), (float)(T.ny + 4));
-  const float fu = floorf(u), fv = floorf(v);
-  const int i = (int)fu, j = (int)fv;
-  const float a = u - fu, b = v - fv;
-  float2 c00, c10, c01, c11;
-  const int li = i - T.pi0, lj = j - T.pj0;
-  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
-    const float2* pp = T.patch + li * PSZY + lj;
-    c00 = pp[0]; c01 = pp[1]; c10 = pp[PSZY]; c11 = pp[PSZY + 1];
-  } else {
-    c00 = make_float2(tile_at(T, 1, i, j), tile_at(T, 0, i, j));
-    c10 = make_float2(tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j));
-    c01 = make_float2(tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1));
-    c11 = make_float2(tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1));
-  }
-  const float inv = ihs;
-  hf[0] = (1 - a) * (1 - b) * c00.x + a * (1 - b) * c10.x + (1 - a) * b * c01.x + a * b * c11.x;
-  hf[1] = ((1 - b) * (c10.x - c00.x) + b * (c11.x - c01.x)) * inv;
-  hf[2] = ((1 - a) * (c01.x - c00.x) + a * (c11.x - c10.x)) * inv;
-  hc[0] = (1 - a) * (1 - b) * c00.y + a * (1 - b) * c10.y + (1 - a) * b * c01.y + a * b * c11.y;
-  hc[1] = ((1 - b) * (c10.y - c00.y) + b * (c11.y - c01.y)) * inv;
-  hc[2] = ((1 - a) * (c01.y - c00.y) + a * (c11.y - c10.y)) * inv;
-}
-
 struct CP {
   float k, d, kf, mu;
   float e, vb;  // restitution (the env's and the terrain's, averaged) and the bounce threshold
@@ -1016,84 +998,74 @@ struct CP {
 // carried as the two halves of an f2 all the way from the bilinear patch to the force.
 __device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
 
-// (floor, ceiling) heights and gradients at world (x, y), bilinear, in two halves, so that the
-// corner reads are issued early and land while independent work runs (the articulated-inertia
-// chain of the sub-step): hq_fetch reads the four (floor, ceiling) corners -- the LDS patch stores
-// (floor, ceiling) per cell, i.e. already in f2 layout; the HBM tile outside it -- and hq_finish
-// interpolates.
+// (floor, ceiling) at the four corners of cell (i, j): the LDS patch, or the tile outside it
+__device__ __forceinline__ void cell_fetch(const Terr& T, int i, int j, f2& c00, f2& c10, f2& c01, f2& c11) {
+  const int li = i - T.pi0, lj = j - T.pj0;
+  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
+    const float2* pp = T.patch + li * PSZY + lj;
+    const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];
+    c00 = f2{q00.x, q00.y}; c01 = f2{q01.x, q01.y}; c10 = f2{q10.x, q10.y}; c11 = f2{q11.x, q11.y};
+  } else {
+    c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
+    c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
+    c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
+    c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
+  }
+}
+
+// (floor, ceiling) heights and gradients at world (x, y) in two halves, so that the corner reads are issued early and
+// land while independent work runs: hq_fetch reads the cell's four (floor, ceiling) corners -- the LDS patch stores
+// (floor, ceiling) per cell, i.e. already in f2 layout; the HBM tile outside it -- and hq_finish evaluates the
+// triangle's plane.
 struct HQ {
   f2 c00, c10, c01, c11;
   float a, b;
+  bool up;  // the cell's upper triangle (a < b): (i, j), (i + 1, j + 1), (i, j + 1); else (i, j), (i + 1, j), (i + 1, j + 1)
 };
 __device__ __forceinline__ void hq_fetch(const Terr& T, float x, float y, HQ& q) {
   if (!T.tile) {
     q.c00 = q.c10 = q.c01 = q.c11 = f2{0.0f, 1e9f};
     q.a = q.b = 0.0f;
+    q.up = false;
     return;
   }
   const float ihs = frcp(T.hs);
   const float u = fminf(fmaxf(x * ihs, -4.0f), (float)(T.nx + 4));
   const float v = fminf(fmaxf(y * ihs, -4.0f), (float)(T.ny + 4));
   const float fu = floorf(u), fv = floorf(v);
-  const int i = (int)fu, j = (int)fv;
   q.a = u - fu;
   q.b = v - fv;
-#ifdef GO1_ABL_NO_FALLBACK  // ablation build only: every query from the (clamped) LDS patch
-  const int li = min(max(i - T.pi0, 0), PSZX - 2), lj = min(max(j - T.pj0, 0), PSZY - 2);
-#else
-  const int li = i - T.pi0, lj = j - T.pj0;
-#endif
-  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
-    const float2* pp = T.patch + li * PSZY + lj;
-    const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];
-    q.c00 = f2{q00.x, q00.y}; q.c01 = f2{q01.x, q01.y}; q.c10 = f2{q10.x, q10.y}; q.c11 = f2{q11.x, q11.y};
-  } else {
-    q.c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
-    q.c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
-    q.c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
-    q.c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
-  }
+  q.up = q.a < q.b;
+  cell_fetch(T, (int)fu, (int)fv, q.c00, q.c10, q.c01, q.c11);
 }
+// the cell and triangle of a capsule's deepest point (SEG_CELL, seg_deepest2): a = u - i, b = v - j on that triangle's
+// plane, so at a mesh edge the normal is the one of the triangle the search chose, not whichever side floor() of a
+// rounded coordinate lands on (which the f32 kernel and the f64 oracle would decide differently)
+__device__ __forceinline__ void hq_fetch_cell(const Terr& T, float x, float y, int cell, HQ& q) {
+  if (!T.tile) {
+    q.c00 = q.c10 = q.c01 = q.c11 = f2{0.0f, 1e9f};
+    q.a = q.b = 0.0f;
+    q.up = false;
+    return;
+  }
+  const float ihs = frcp(T.hs);
+  const float u = fminf(fmaxf(x * ihs, -4.0f), (float)(T.nx + 4));
+  const float v = fminf(fmaxf(y * ihs, -4.0f), (float)(T.ny + 4));
+  const int i = (cell >> 16) - 16384, j = (cell & 0x7fff) - 16384;
+  q.a = u - (float)i;
+  q.b = v - (float)j;
+  q.up = (cell >> 15) & 1;
+  cell_fetch(T, i, j, q.c00, q.c10, q.c01, q.c11);
+}
+// height and gradient of (floor, ceiling) on the triangle.  Round 6: the surface is the heightfield's triangle mesh,
+// as the reference collides with it (mesh_type 'trimesh'; tunnel.py:139-147 builds it with isaacgym terrain_utils.
+// convert_heightfield_to_trimesh: every cell split along its (i, j) - (i + 1, j + 1) diagonal); oracle tri_query
 __device__ __forceinline__ void hq_finish(const Terr& T, const HQ& q, f2& h, f2& gx, f2& gy) {
   const float ihs = frcp(T.hs);
-  const float a = q.a, b = q.b, a1 = 1.0f - a, b1 = 1.0f - b;
-  h = (a1 * b1) * q.c00 + (a * b1) * q.c10 + (a1 * b) * q.c01 + (a * b) * q.c11;
-  gx = (b1 * (q.c10 - q.c00) + b * (q.c11 - q.c01)) * ihs;
-  gy = (a1 * (q.c01 - q.c00) + a * (q.c11 - q.c10)) * ihs;
-}
-
-// penalty contact of a sphere (centre p, velocity pv, radius r) with the floor (pushes up)
-// and the ceiling (pushes down), both layers at once; F = floor + ceiling force
-__device__ __forceinline__ void sphere_contact_pk(const Terr& T, const HQ& q, const CP& C, const float* p,
-                                                  const float* pv, float r, float* F) {
-  f2 h, gx, gy;
-  hq_finish(T, q, h, gx, gy);
-  const f2 sg = f2{1.0f, -1.0f};
-  const f2 dv = sg * (h - p[2]) + r;  // floor: h + r - z, ceiling: z + r - h
-  f2 nx = -sg * gx, ny = -sg * gy;
-  f2 inv = nx * nx + ny * ny + 1.0f;
-  inv = f2{frsq(inv.x), frsq(inv.y)};
-  nx = nx * inv;
-  ny = ny * inv;
-  const f2 nz = sg * inv;
-  const f2 depth = dv * inv;
-  const f2 vn = pv[0] * nx + pv[1] * ny + pv[2] * nz;
-  const f2 fn = C.k * depth - C.d * vn;
-  const f2 vtx = pv[0] - vn * nx, vty = pv[1] - vn * ny, vtz = pv[2] - vn * nz;
-  const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
-  const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
-  const f2 vtn = vt2 * ivt;
-  const f2 cf = C.kf * vtn, cm = C.mu * fn;
-  const f2 ft = f2{fminf(cf.x, cm.x), fminf(cf.y, cm.y)};
-  const f2 fti = ft * ivt;
-  // a layer acts only in penetration with a compressive normal force
-  const bool ax = dv.x > 0.0f && fn.x > 0.0f, ay = dv.y > 0.0f && fn.y > 0.0f;
-  const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
-  const f2 sc = f2{(ax && vtn.x > 1e-9f) ? fti.x : 0.0f, (ay && vtn.y > 1e-9f) ? fti.y : 0.0f};
-  const f2 Fx = fa * nx - sc * vtx, Fy = fa * ny - sc * vty, Fz = fa * nz - sc * vtz;
-  F[0] = Fx.x + Fx.y;
-  F[1] = Fy.x + Fy.y;
-  F[2] = Fz.x + Fz.y;
+  const f2 da = q.up ? q.c11 - q.c01 : q.c10 - q.c00, db = q.up ? q.c01 - q.c00 : q.c11 - q.c10;
+  h = q.c00 + q.a * da + q.b * db;
+  gx = da * ihs;
+  gy = db * ihs;
 }
 
 // Restitution.  PhysX bounces a contact whose relative velocity exceeds the bounce threshold with the
@@ -1156,41 +1128,6 @@ __device__ __forceinline__ void sphere_contact_im(const Terr& T, const HQ& q, co
   Mp[3] = myy.x + myy.y; Mp[4] = myz.x + myz.y; Mp[5] = mzz.x + mzz.y;
 }
 
-__device__ __forceinline__ void sphere_contact(const Terr& T, const CP& C, const float* p, const float* pv, float r,
-                                               float* F) {
-  F[0] = F[1] = F[2] = 0.0f;
-  float hq[2][3];
-  height_query2(T, p[0], p[1], hq[1], hq[0]);
-#pragma unroll
-  for (int layer = 1; layer >= 0; --layer) {
-    const float h = hq[layer][0], gx = hq[layer][1], gy = hq[layer][2];
-    float n[3], dv;
-    if (layer == 1) {
-      dv = h + r - p[2];
-      n[0] = -gx; n[1] = -gy; n[2] = 1.0f;
-    } else {
-      dv = p[2] + r - h;
-      n[0] = gx; n[1] = gy; n[2] = -1.0f;
-    }
-    if (dv <= 0.0f) continue;
-    const float inv = frsq(n[0] * n[0] + n[1] * n[1] + 1.0f);
-    n[0] *= inv; n[1] *= inv; n[2] *= inv;
-    const float depth = dv * inv;
-    const float vn = pv[0] * n[0] + pv[1] * n[1] + pv[2] * n[2];
-    const float fn = C.k * depth - C.d * vn;
-    if (fn <= 0.0f) continue;
-    const float vt[3] = {pv[0] - vn * n[0], pv[1] - vn * n[1], pv[2] - vn * n[2]};
-    const float vt2 = vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2];
-    const float ivt = frsq(fmaxf(vt2, 1e-18f));
-    const float vtn = vt2 * ivt;
-    const float ft = fminf(C.kf * vtn, C.mu * fn);
-    const float sc = vtn > 1e-9f ? ft * ivt : 0.0f;
-    F[0] += fn * n[0] - sc * vt[0];
-    F[1] += fn * n[1] - sc * vt[1];
-    F[2] += fn * n[2] - sc * vt[2];
-  }
-}
-
 __device__ __forceinline__ void point_kin(const float* Rb, const float* pb, const float* vb, const float* lp, float* pw,
                                           float* vw) {
   float wl[3], vl[3];
@@ -1202,149 +1139,133 @@ __device__ __forceinline__ void point_kin(const float* Rb, const float* pb, cons
   mat3_vec(Rb, vl, vw);
 }
 
-// Hip capsule contact (model.py HIP_CAPSULE_*: the two ends of the capsule's segment as spheres of its
-// radius on the hip link's y axis, oracle/go1_oracle.c phys_substep j == 0).  Every role lane of a leg
-// evaluates its own leg's hip (redundantly over the four roles, like the leg's ABA: no cross-lane
-// sums), the two spheres in the halves of f2.  A wave whose hip spheres all clear both layers (the
-// contact's own penetration test, evaluated first) skips the force and the added mass, which are then
-// exactly zero (as the oracle computes them): on open ground and with the trunk level the hips never
-// touch, and the skip costs the kinematics and one height query.
-// Adds the added mass to the hip's articulated inertia IA and the force to its bias force pA (hip
-// frame, (angular, linear) pairs); Fw = the world force, the hip's reported contact force.
-__device__ __forceinline__ void hip_contact(const Terr& T, const CP& C, const float* R, const float* pos,
-                                            const f2* vbp, const float* org, float cq, float sq, float qd0,
-                                            f2 yy, float hr, float h, const float* g, int role, SIP& IA, f2* pA,
-                                            float* Fw) {
-  Fw[0] = Fw[1] = Fw[2] = 0.0f;
-  // sphere centres from the hip joint, base frame: Rx(q) (0, y, 0) = (0, c y, s y)
-  const f2 rby = cq * yy, rbz = sq * yy;
-  // base frame: p = org + r, v = v_b + w_b x org + (w_b + qd e_x) x r
-  const float w0 = vbp[0].x, w1 = vbp[1].x, w2 = vbp[2].x, wh0 = w0 + qd0;
-  const float vo0 = vbp[0].y + (w1 * org[2] - w2 * org[1]);
-  const float vo1 = vbp[1].y + (w2 * org[0] - w0 * org[2]);
-  const float vo2 = vbp[2].y + (w0 * org[1] - w1 * org[0]);
-  const f2 pb[3] = {f2s(org[0]), org[1] + rby, org[2] + rbz};
-  const f2 vpb[3] = {vo0 + (w1 * rbz - w2 * rby), vo1 - wh0 * rbz, vo2 + wh0 * rby};
-  f2 pw[3], vw[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    pw[i] = pos[i] + (R[3 * i] * pb[0] + R[3 * i + 1] * pb[1] + R[3 * i + 2] * pb[2]);
-    vw[i] = R[3 * i] * vpb[0] + R[3 * i + 1] * vpb[1] + R[3 * i + 2] * vpb[2];
+// ---- capsules against the heightfield meshes (round 6; oracle/go1_oracle.c seg_deepest is the f64 restatement).  A
+// capsule (segment A -> B, radius r) acts at the deepest point of its segment: the t in [0, 1] that maximises the
+// vertical gap of either layer, floor h_f + r - z and ceiling z + r - h_c.  Both layers are triangle meshes over the
+// grid (hq_finish), so along the segment the gaps are piecewise linear in t and their maximum lies at an end or where
+// the segment's (x, y) projection crosses a mesh edge: a grid line u = k or v = k, or a cell diagonal u - v = k.  The
+// candidates are exactly those (on an edge the height interpolates its two vertices): exact, and no serial walk --
+// every candidate's reads are independent.  A half link of 0.1065 m crosses at most 3 lines of each grid direction
+// and 4 diagonals at 0.05 m cells (go1_create rejects finer grids).  Each candidate carries the cell and triangle on
+// the segment's incoming side of its edge; the contact takes that triangle's plane (hq_fetch_cell).  A candidate's
+// key is its deeper layer's gap quantised to 1e-5 m, ties to the smaller t (the segment's first end; the link halves
+// start at their outer ends, so a link lying flat is carried at both): this f32 search and the oracle's f64 one
+// choose the same point.  On the plane: the lower end (ties: A).  The search runs once per control step; the chosen t
+// is held for the control step's sim steps (phys_substep), as the trunk faces' vertices are.
+#define SEG_QI 1.0e5f  // 1 / SEG_Q of the oracle
+__device__ __forceinline__ int seg_quant(float g) { return (int)floorf(fminf(fmaxf(g, -1.0f), 1.0f) * SEG_QI); }
+// cell (i, j in [-4, n + 4]) and triangle (up: the upper one) packed into a positive int
+#define SEG_CELL(i, j, up) ((((i) + 16384) << 16) | ((up) ? 0x8000 : 0) | ((j) + 16384))
+struct SegBest {
+  int key;   // the best candidate's key: quantised gap (the deeper layer) x 4096 + the earlier t (4095 - 4095 t)
+  float t;   // its t
+  int cell;  // and its cell and triangle
+};
+__device__ __forceinline__ void seg_offer(SegBest& sb, f2 h, float z, float r, float t, int cell, bool valid) {
+  const int q = max(seg_quant((h.x - z) + r), seg_quant((z - h.y) + r));
+  const int key = q * 4096 + (4095 - (int)floorf(t * 4095.0f));
+  const bool up = valid && key > sb.key;  // an equal key (a vertex on several edges) keeps the first offer
+  sb.key = up ? key : sb.key;
+  sb.t = up ? t : sb.t;
+  sb.cell = up ? cell : sb.cell;
+}
+// the two (floor, ceiling) vertices of the mesh edge (i, j) - (i + di, j + dj): the LDS patch, or the tile outside it
+__device__ __forceinline__ void edge_fetch(const Terr& T, int i, int j, int di, int dj, f2& p0, f2& p1) {
+  const int li = i - T.pi0, lj = j - T.pj0;
+  if (T.patch && li >= 0 && li + di < PSZX && lj >= 0 && lj + dj < PSZY) {
+    const float2* pp = T.patch + li * PSZY + lj;
+    const float2 q0 = pp[0], q1 = pp[di * PSZY + dj];
+    p0 = f2{q0.x, q0.y};
+    p1 = f2{q1.x, q1.y};
+  } else {
+    p0 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
+    p1 = f2{tile_at(T, 1, i + di, j + dj), tile_at(T, 0, i + di, j + dj)};
   }
-  HQ qa, qb;
-  hq_fetch(T, pw[0].x, pw[1].x, qa);
-  hq_fetch(T, pw[0].y, pw[1].y, qb);
-  // heights and gradients with the spheres in the halves: layer L = 0 floor (.x of hq_finish), 1 ceiling
-  f2 hl[2], gxl[2], gyl[2];
+}
+// deepest point of one segment (world ends A, B): t and SEG_CELL
+__device__ __forceinline__ float seg_deepest(const Terr& T, const float* A, const float* B, float r, int& cell) {
+  if (!T.tile) {  // the plane: the lower end
+    cell = SEG_CELL(0, 0, false);
+    return seg_quant(r - B[2]) > seg_quant(r - A[2]) ? 1.0f : 0.0f;
+  }
+  const float ihs = frcp(T.hs);
+  const float uA = fminf(fmaxf(A[0] * ihs, -4.0f), (float)(T.nx + 4)), vA = fminf(fmaxf(A[1] * ihs, -4.0f), (float)(T.ny + 4));
+  const float uB = fminf(fmaxf(B[0] * ihs, -4.0f), (float)(T.nx + 4)), vB = fminf(fmaxf(B[1] * ihs, -4.0f), (float)(T.ny + 4));
+  const float du = uB - uA, dv = vB - vA, dw = du - dv, dz = B[2] - A[2], zA = A[2];
+  SegBest sb;
+  sb.key = -2147483647 - 1;
+  sb.t = 0.0f;
+  sb.cell = SEG_CELL(0, 0, false);
+  // the ends
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float u = e ? uB : uA, v = e ? vB : vA;
+    const float fu = floorf(u), fv = floorf(v);
+    HQ q;
+    q.a = u - fu;
+    q.b = v - fv;
+    q.up = q.a < q.b;
+    cell_fetch(T, (int)fu, (int)fv, q.c00, q.c10, q.c01, q.c11);
+    const f2 da = q.up ? q.c11 - q.c01 : q.c10 - q.c00, db = q.up ? q.c01 - q.c00 : q.c11 - q.c10;
+    seg_offer(sb, q.c00 + q.a * da + q.b * db, e ? B[2] : zA, r, (float)e, SEG_CELL((int)fu, (int)fv, q.up), true);
+  }
+  // grid lines u = k (the edge (k, j) - (k, j + 1)), entered from cell k - 1 (du > 0) or k
   {
-    f2 ha, gxa, gya, hb, gxb, gyb;
-    hq_finish(T, qa, ha, gxa, gya);
-    hq_finish(T, qb, hb, gxb, gyb);
-    hl[0] = f2{ha.x, hb.x}; gxl[0] = f2{gxa.x, gxb.x}; gyl[0] = f2{gya.x, gyb.x};
-    hl[1] = f2{ha.y, hb.y}; gxl[1] = f2{gxa.y, gxb.y}; gyl[1] = f2{gya.y, gyb.y};
+    const int k0 = (int)floorf(fminf(uA, uB)) + 1;
+    const float hi = fmaxf(uA, uB), rdu = du != 0.0f ? frcp(du) : 0.0f;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int k = k0 + m;
+      const bool valid = (float)k < hi;
+      const float t = valid ? ((float)k - uA) * rdu : 0.0f, v = vA + dv * t, fv = floorf(v), b = v - fv;
+      const int j = (int)fv, i = du > 0.0f ? k - 1 : k;
+      f2 p0, p1;
+      edge_fetch(T, k, j, 0, 1, p0, p1);
+      seg_offer(sb, p0 + b * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, (float)(k - i) < b), valid);
+    }
   }
-  // the penetration test of sphere_contact_im: floor h + r - z, ceiling z + r - h
-  const f2 dvl[2] = {(hl[0] - pw[2]) + hr, (pw[2] - hl[1]) + hr};
-  if (!__any(dvl[0].x > 0.0f || dvl[0].y > 0.0f || dvl[1].x > 0.0f || dvl[1].y > 0.0f)) return;
-  // The contact of sphere_contact_im (the oracle's sphere_contact_im), evaluated in the hip frame: with
-  // m = Rh^T n the force is sum_L fa m - sc Rh^T vt and the added mass sum_L (cn - cd) m m^T + cd I
-  // (the rotation leaves I alone), so neither Mp nor F needs the 3x3 sandwich into the link frame.
-  float Rh[9];  // hip link rotation (world <- hip): R Rx(q), columns R0, c R1 + s R2, c R2 - s R1
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    Rh[3 * i] = R[3 * i];
-    Rh[3 * i + 1] = cq * R[3 * i + 1] + sq * R[3 * i + 2];
-    Rh[3 * i + 2] = cq * R[3 * i + 2] - sq * R[3 * i + 1];
-  }
-  f2 vh[3];  // sphere velocities, hip frame
-#pragma unroll
-  for (int j = 0; j < 3; ++j) vh[j] = Rh[j] * vw[0] + Rh[3 + j] * vw[1] + Rh[6 + j] * vw[2];
-  float gh[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) gh[j] = Rh[j] * g[0] + Rh[3 + j] * g[1] + Rh[6 + j] * g[2];
-  // The two layers split over the role rows: rows 0 and 2 evaluate the floor (L = 0), rows 1 and 3 the
-  // ceiling (L = 1), both spheres packed; each sum over the layers is the row pair's sum (one permlane16
-  // swap), the same addition in every row (x + y = y + x) as one lane walking both layers.
-  const bool ceil_row = (role & 1) != 0;
-  const float sg = ceil_row ? -1.0f : 1.0f;
-  const f2 gxL = ceil_row ? gxl[1] : gxl[0], gyL = ceil_row ? gyl[1] : gyl[0], dvL = ceil_row ? dvl[1] : dvl[0];
-  f2 Fh[3], M[6], cds, Fwx, Fwy, Fwz;
+  // grid lines v = k (the edge (i, k) - (i + 1, k)), entered from cell k - 1 (dv > 0) or k
   {
-    f2 nx = -sg * gxL, ny = -sg * gyL;
-    f2 inv = nx * nx + ny * ny + 1.0f;
-    inv = f2{frsq(inv.x), frsq(inv.y)};
-    nx = nx * inv;
-    ny = ny * inv;
-    const f2 nz = sg * inv;
-    const f2 depth = dvL * inv;
-    const f2 vn = vw[0] * nx + vw[1] * ny + vw[2] * nz;
-    const f2 fn0 = C.k * depth - C.d * vn;
-    const f2 fn = restitute(C, h, vn, fn0 - (h * C.k) * vn);
-    const float cn = h * (h * C.k + C.d);
-    const f2 vtx = vw[0] - vn * nx, vty = vw[1] - vn * ny, vtz = vw[2] - vn * nz;
-    const f2 vt2 = vtx * vtx + vty * vty + vtz * vtz;
-    const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
-    const f2 vtn = vt2 * ivt;
-    const f2 cm = C.mu * fn0;
-    const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
-                     (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
-    const bool ax = dvL.x > 0.0f && fn0.x > 0.0f, ay = dvL.y > 0.0f && fn0.y > 0.0f;
-    const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
-    const f2 sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
-    Fwx = fa * nx - sc * vtx;  // the reported world force
-    Fwy = fa * ny - sc * vty;
-    Fwz = fa * nz - sc * vtz;
-    f2 m[3];  // the normal in the hip frame
+    const int k0 = (int)floorf(fminf(vA, vB)) + 1;
+    const float hi = fmaxf(vA, vB), rdv = dv != 0.0f ? frcp(dv) : 0.0f;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) m[j] = Rh[j] * nx + Rh[3 + j] * ny + Rh[6 + j] * nz;
-    // F = fa n - sc (v - vn n) = (fa + sc vn) n - sc v
-    const f2 fs = fa + sc * vn;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) Fh[j] = fs * m[j] - sc * vh[j];
-    const f2 cd = h * sc, cnd = f2{ax ? cn : 0.0f, ay ? cn : 0.0f} - cd;
-    cds = cd;
-    const f2 am[3] = {cnd * m[0], cnd * m[1], cnd * m[2]};
-    M[0] = am[0] * m[0]; M[1] = am[0] * m[1]; M[2] = am[0] * m[2];
-    M[3] = am[1] * m[1]; M[4] = am[1] * m[2]; M[5] = am[2] * m[2];
+    for (int m = 0; m < 3; ++m) {
+      const int k = k0 + m;
+      const bool valid = (float)k < hi;
+      const float t = valid ? ((float)k - vA) * rdv : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
+      const int i = (int)fu, j = dv > 0.0f ? k - 1 : k;
+      f2 p0, p1;
+      edge_fetch(T, i, k, 1, 0, p0, p1);
+      seg_offer(sb, p0 + a * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, a < (float)(k - j)), valid);
+    }
   }
+  // cell diagonals u - v = k (the point (i + a, j + a) of cell (i, j), i - j = k), entered from the upper triangle
+  // (dw > 0: u - v grows through k, a < b before) or the lower
   {
-    auto pair = [](f2& v) {
-      auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.x), __float_as_uint(v.x), false, false);
-      auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.y), __float_as_uint(v.y), false, false);
-      v = f2{__uint_as_float(rx[0]), __uint_as_float(ry[0])} + f2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
-    };
+    const float wA = uA - vA, wB = uB - vB;
+    const int k0 = (int)floorf(fminf(wA, wB)) + 1;
+    const float hi = fmaxf(wA, wB), rdw = dw != 0.0f ? frcp(dw) : 0.0f;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) pair(Fh[j]);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) pair(M[k]);
-    pair(cds);
-    pair(Fwx);
-    pair(Fwy);
-    pair(Fwz);
+    for (int m = 0; m < 4; ++m) {
+      const int k = k0 + m;
+      const bool valid = (float)k < hi;
+      const float t = valid ? ((float)k - wA) * rdw : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
+      const int i = (int)fu, j = i - k;
+      f2 p0, p1;
+      edge_fetch(T, i, j, 1, 1, p0, p1);
+      seg_offer(sb, p0 + a * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, dw > 0.0f), valid);
+    }
   }
-  M[0] += cds; M[3] += cds; M[5] += cds;
-  Fw[0] = Fwx.x + Fwx.y; Fw[1] = Fwy.x + Fwy.y; Fw[2] = Fwz.x + Fwz.y;
-  // the force the added mass sees is F - M g (accelerations relative to free fall, as the leg points);
-  // moment lp x f with lp = (0, y, 0): (y fz, 0, -y fx)
-  f2 f[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) f[i] = Fh[i] - (M[s3i(i, 0)] * gh[0] + M[s3i(i, 1)] * gh[1] + M[s3i(i, 2)] * gh[2]);
-  const f2 m0 = yy * f[2], m2 = -(yy * f[0]);
-  pA[0] -= f2{m0.x + m0.y, f[0].x + f[0].y};
-  pA[1] -= f2{0.0f, f[1].x + f[1].y};
-  pA[2] -= f2{m2.x + m2.y, f[2].x + f[2].y};
-  // about the hip origin, S = lp~: S M S^T has (0,0) y^2 M22, (0,2) -y^2 M20, (2,2) y^2 M00 and zeros
-  // elsewhere; S M has rows (y M2., 0, -y M0.); C = M
-  const f2 y2 = yy * yy;
-  const f2 A[6] = {y2 * M[5], f2s(0.0f), -(y2 * M[2]), f2s(0.0f), f2s(0.0f), y2 * M[0]};  // 00 01 02 11 12 22
-#pragma unroll
-  for (int k = 0; k < 6; ++k) IA.ac[k] += f2{A[k].x + A[k].y, M[k].x + M[k].y};
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const f2 b0 = yy * M[s3i(2, j)], b2 = -(yy * M[s3i(0, j)]);
-    IA.b[j] += b0.x + b0.y;
-    IA.b[6 + j] += b2.x + b2.y;
-  }
+  cell = sb.cell;
+  return sb.t;
+}
+// the lane's two segments (x, y halves of the contact pass)
+__device__ __forceinline__ f2 seg_deepest2(const Terr& T, const f2* A, const f2* B, f2 r, int* cell) {
+  const float a0[3] = {A[0].x, A[1].x, A[2].x}, b0[3] = {B[0].x, B[1].x, B[2].x};
+  const float a1[3] = {A[0].y, A[1].y, A[2].y}, b1[3] = {B[0].y, B[1].y, B[2].y};
+  const float tx = seg_deepest(T, a0, b0, r.x, cell[0]);
+  const float ty = seg_deepest(T, a1, b1, r.y, cell[1]);
+  return f2{tx, ty};
 }
 
 __device__ __forceinline__ void point_force(const float* Rb, const float* lp, const float* F, float* fs) {
@@ -1441,12 +1362,17 @@ struct Phys {
 // box; tunnel_fn.py:99-163, the ceiling's downward wedges).  The 8 box corners are contact points of the sub-step
 // (above); a wedge apex or ridge that enters a face between its corners is a grid vertex of the heightfield
 // inside the face's footprint (bilinear cells: a face's deepest point against them is a vertex or on the
-// footprint's boundary).  Once per control step, the env's 16 lanes scan the 10 x 8 vertices around the trunk
-// (5 each, both layers in the halves: floor against the bottom face, ceiling against the top face) and keep, per
-// face, the deepest vertex inside the footprint; depths are compared quantised to 1e-5 m, ties go to the lowest
-// window position, so the choice is a lexicographic maximum (associative: the same in any reduction order, and
-// the oracle's).  Every sim step a penalty force acts at the two chosen vertices (face_force).
+// footprint's boundary).  Once per control step the env's 16 lanes scan the 10 x 10 vertices around the trunk
+// (offsets -4 .. +5 on both axes: they hold the footprint's +-0.166 m at any yaw wherever the centre sits in its
+// cell; 7 per lane, both layers in the halves: floor against the bottom face, ceiling against the top
+// face) and keep, per face, the vertex inside the footprint nearest to (or deepest in) the face -- its signed
+// depth, so a vertex that enters during the control step is already chosen -- compared quantised
+// to 1e-5 m, ties to the lowest window position: a lexicographic maximum (associative: the same in any reduction
+// order, and the oracle's).  Every sim step a penalty force acts at the two chosen vertices where they penetrate
+// (face_force).  Scanning every sim step measured +3.7 k cycles per sim step per wave; the held choice is bounded
+// by tests/test_trunk_faces.py::test_held_face_vertex_matches_every_step_scan.
 #define FACE_Q 1.0e-5f
+#define FACE_W 10
 __device__ __forceinline__ int face_key_max(int v) {  // max over the env's 16 lanes (quad, then the rows)
   v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true));
   v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true));
@@ -1455,19 +1381,19 @@ __device__ __forceinline__ int face_key_max(int v) {  // max over the env's 16 l
   auto b = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
   return max((int)b[0], (int)b[1]);
 }
+#define FACE_SIGNED 0.1f  // signed depths from -0.1 m (a vertex farther from the face cannot reach it in a control step)
 __device__ __forceinline__ void face_scan(const Terr& T, const float* R, const float* pos, const float* th, int sub16,
                                           int* sel) {
   const float ihs = frcp(T.hs);
-  const bool xl = fabsf(R[0]) >= fabsf(R[3]);  // the window's long side along the world axis nearer the trunk's x
   const int ci = (int)floorf(fminf(fmaxf(pos[0] * ihs, -16000.0f), 16000.0f));
   const int cj = (int)floorf(fminf(fmaxf(pos[1] * ihs, -16000.0f), 16000.0f));
   int key[2] = {-1, -1};
 #pragma unroll
-  for (int u = 0; u < 5; ++u) {
-    const int v = sub16 + 16 * u, a = v % 10, b = v / 10;
-    const int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+  for (int u = 0; u < (FACE_W * FACE_W + 15) / 16; ++u) {
+    const int v = sub16 + 16 * u;
+    const int i = ci + v % FACE_W - 4, j = cj + v / FACE_W - 4;
     const int li = i - T.pi0, lj = j - T.pj0;
-    const bool inp = li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
+    const bool inp = v < FACE_W * FACE_W && li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
     const float2 hv = T.patch[min(max(li, 0), PSZX - 1) * PSZY + min(max(lj, 0), PSZY - 1)];
     const float dx = (float)i * T.hs - pos[0], dy = (float)j * T.hs - pos[1];
     const f2 dz = f2{hv.x, hv.y} - pos[2];
@@ -1476,8 +1402,8 @@ __device__ __forceinline__ void face_scan(const Terr& T, const float* R, const f
     const f2 pen = f2{cz.x + th[2], th[2] - cz.y};  // floor vertex above the bottom face / ceiling below the top
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const bool in = inp && fabsf(cx[hh]) <= th[0] && fabsf(cy[hh]) <= th[1] && pen[hh] > 0.0f;
-      const int q = (int)fminf(pen[hh] * (1.0f / FACE_Q), 1.0e6f);
+      const bool in = inp && fabsf(cx[hh]) <= th[0] && fabsf(cy[hh]) <= th[1] && pen[hh] > -FACE_SIGNED;
+      const int q = (int)floorf(fminf(pen[hh] + FACE_SIGNED, 10.0f) * (1.0f / FACE_Q));  // signed depth, offset
       const int k = in ? (q << 7) | (127 - v) : -1;
       key[hh] = max(key[hh], k);
     }
@@ -1485,8 +1411,8 @@ __device__ __forceinline__ void face_scan(const Terr& T, const float* R, const f
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int k = face_key_max(key[hh]);
-    const int v = 127 - (k & 127), a = v % 10, b = v / 10;
-    const int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+    const int v = 127 - (k & 127);
+    const int i = ci + v % FACE_W - 4, j = cj + v / FACE_W - 4;
     sel[hh] = k < 0 ? -1 : ((i + 16384) << 16) | (j + 16384);
   }
 }
@@ -1540,55 +1466,134 @@ __device__ __forceinline__ void face_force(const Terr& T, const CP& C, const flo
 // sum over the 4 roles of a leg (the four 16-lane rows), bitwise identical on every lane
 __device__ __forceinline__ float rsum(float v) { return rowsum4(v); }
 
-// One integrator step of length h for the env of this lane.  Lane layout (16 per
-// env): lane = 16 role + 4 env + leg.  The four roles of a leg compute the leg's
-// kinematics and ABA passes redundantly (base quantities on all 16 lanes), and
-// split the leg's 8 contact points [thigh x3, calf x2, foot, 2 trunk corners]
-// two per lane, so each wave has four envs and the whole grid fills every SIMD.
-// cf_raw: this lane's reported contact forces (its two points; its leg's hip; the trunk's self-collision
-// reaction of the lane's box pairs).
-// `lds` = the model block (GO1_MODEL_FLOATS) followed by the per-joint config arrays (LDS_*), staged
-// in LDS once per block: the lane-dependent (per-leg) constants are re-read every sub-step
-// because the physics keeps every VGPR busy, and LDS answers faster than the caches.
 // ---- self-collision (asset.self_collisions == 0, go1_crawling.py:44: Isaac Gym collides every pair of bodies no
-// joint connects; oracle/go1_oracle.c phys_substep).  Spheres leg * 8 + s (s: thigh 0-2, calf 3-4, foot 5 -- the
-// contact points below -- and the hip capsule's ends 6-7).  Pairs: every sphere of leg la against every sphere of
-// leg lb (la < lb: 64 per leg pair, pair j = 8 a + b of group lp); within a leg the links two joints apart (hip
-// capsule vs calf and foot, thigh vs foot: SELF_SAME_A / _B); the thigh, calf and foot spheres against the trunk
-// box (the hip is the trunk's neighbour).  Explicit penalty springs on the overlap, fn = ks pen - ds vn
-// (compressive only), no friction, no added mass (the bodies sit in different ABA chains, or two joints apart).
+// joint connects; oracle/go1_oracle.c phys_substep).  Round 6: the links as capsules over their full length
+// (the sphere chains of rounds 3-5 had 46-55 mm holes).  Primitive 4 leg + k, owned by the lane of role
+// k: 0 thigh capsule (thigh joint .. knee), 1 hip capsule, 2 calf capsule (knee .. foot), 3 foot sphere.  Pairs:
+// every primitive of leg la against every primitive of leg lb (16 per leg pair); within a leg the links two joints
+// apart (hip vs calf and foot, thigh vs foot); the thigh and calf capsules and the foot against the trunk box (the
+// hip is the trunk's neighbour).  A pair acts at the closest points of its two segments as two spheres of the
+// capsules' radii there (seg_closest), a capsule against the box at its point nearest the box (seg_box_t).
+// Explicit penalty springs on the overlap, fn = ks pen - ds vn (compressive only), no friction, no added mass (the
+// bodies sit in different ABA chains, or two joints apart).
 // Broad phase in registers: each lane bounds its leg (thigh joint, knee, foot, hip-capsule ends, grown by their
 // radii) by an AABB in the trunk frame, swaps the four legs' boxes over the quad (DPP) and tests the six leg pairs,
 // the trunk box and the leg's own folded links; a wave whose envs have no candidate is done.  Otherwise, per env in
-// LDS: the 32 spheres as (pos, r), (vel, 0), and each lane sums the forces on its own two spheres from their
-// candidate partners (self_narrow).  Sphere owners: role 0 (thigh 0, thigh 1), role 1 (thigh 2, hip end 6),
-// role 2 (calf 0, calf 1), role 3 (foot, hip end 7).
-// the 32 spheres (pos, r), (vel, 0); then the trunk faces' two vertices of the control step (face_scan)
-#define SELF_ENV_FLOATS (32 * 8 + 4)
-#define FACE_SEL_OFF (32 * 8)
-// the lane's spheres: x half s0, y half s1
-__device__ __forceinline__ int self_s0(int role) { return role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5)); }
-__device__ __forceinline__ int self_s1(int role) { return role == 0 ? 1 : (role == 1 ? 6 : (role == 2 ? 4 : 7)); }
+// LDS: the 16 primitives as (P0, r), (P1, 0), (V0, 0), (V1, 0) (segment ends and their velocities, world), and each
+// lane sums the forces on its own primitive from its candidate partners (self_narrow).
+#define SELF_ENV_FLOATS (16 * 16 + 4 + 32)
+#define FACE_SEL_OFF (16 * 16)  // then the trunk faces' two vertices of the control step (face_scan)
+#define SEG_T_OFF (16 * 16 + 4)  // then the capsules' deepest-point parameters of the control step, (x, y) per lane
 
-// force on sphere A (world) of the pair (A, B); zero when apart or when the spring no longer compresses
-// (sg: the normal of coincident centres, +1 when A has the lower sphere index: the pair's two evaluations, A on
-// B and B on A, give exactly opposite forces -- the negated differences square and multiply to the same bits)
-__device__ __forceinline__ void self_sphere_force(const float4 A, const float4 Av, const float4 B, const float4 Bv,
-                                                  float ks, float ds, float* F, float sg = 1.0f) {
-  const float d0 = A.x - B.x, d1 = A.y - B.y, d2 = A.z - B.z;
-  const float dd = d0 * d0 + d1 * d1 + d2 * d2, rs = A.w + B.w;
-  const float inv = dd > 1e-18f ? frsq(dd) : 0.0f;
-  const float n0 = dd > 1e-18f ? d0 * inv : 0.0f, n1 = dd > 1e-18f ? d1 * inv : 0.0f,
-              n2 = dd > 1e-18f ? d2 * inv : sg;
-  const float pen = rs - dd * inv;
-  const float vn = (Av.x - Bv.x) * n0 + (Av.y - Bv.y) * n1 + (Av.z - Bv.z) * n2;
-  float fn = ks * pen - ds * vn;
-  fn = (dd < rs * rs && fn > 0.0f) ? fn : 0.0f;
-  F[0] = fn * n0; F[1] = fn * n1; F[2] = fn * n2;
+// the lane's own primitive into this env's LDS scratch; rb: the radius of its bounding sphere about the segment's middle
+// (half the segment plus r), for the narrow phase's first test
+__device__ __forceinline__ void self_put(float* sc, int leg, int role, const float* P0, const float* P1, float r,
+                                         float rb, const float* V0, const float* V1) {
+  float4* Q = reinterpret_cast<float4*>(sc) + 4 * (4 * leg + role);
+  Q[0] = make_float4(P0[0], P0[1], P0[2], r);
+  Q[1] = make_float4(P1[0], P1[1], P1[2], rb);
+  Q[2] = make_float4(V0[0], V0[1], V0[2], 0.0f);
+  Q[3] = make_float4(V1[0], V1[1], V1[2], 0.0f);
 }
 
-// sphere A against the trunk box (half extents th about the base origin): the force on A (world) added to F
-// and the trunk's reaction wrench (base frame, (moment, force) about the base origin) added to wb
+// closest points of the segments P0 + s d1 and Q0 + t d2 (s, t in [0, 1]; a = |d1|^2, e = |d2|^2; a point has a
+// or e = 0): Ericson's clamped construction, branch-free (oracle/go1_oracle.c seg_seg_closest), the lines' s formed
+// without cancellation as (n . (d2 x r)) / (n . n), n = d1 x d2 (for nearly parallel links a e - b^2 cancels to a few
+// ulps and would place the closest points anywhere along them)
+__device__ __forceinline__ void seg_closest(const float* P0, const float* d1, const float* Q0, const float* d2,
+                                            float& s, float& t) {
+  const float r[3] = {P0[0] - Q0[0], P0[1] - Q0[1], P0[2] - Q0[2]};
+  const float a = d1[0] * d1[0] + d1[1] * d1[1] + d1[2] * d1[2], e = d2[0] * d2[0] + d2[1] * d2[1] + d2[2] * d2[2];
+  const float b = d1[0] * d2[0] + d1[1] * d2[1] + d1[2] * d2[2];
+  const float c = d1[0] * r[0] + d1[1] * r[1] + d1[2] * r[2], f = d2[0] * r[0] + d2[1] * r[1] + d2[2] * r[2];
+  float n[3], m[3];
+  cross3(d1, d2, n);
+  cross3(d2, r, m);
+  const float den = n[0] * n[0] + n[1] * n[1] + n[2] * n[2], num = n[0] * m[0] + n[1] * m[1] + n[2] * m[2];
+  const bool pa = a > 1e-12f, pe = e > 1e-12f;
+  const float ia = pa ? frcp(a) : 0.0f, ie = pe ? frcp(e) : 0.0f;
+  float ss = den > 1e-10f * a * e ? clampf(num * frcp(den), 0.0f, 1.0f) : 0.0f;
+  float tt = (b * ss + f) * ie;
+  ss = tt < 0.0f ? clampf(-c * ia, 0.0f, 1.0f) : (tt > 1.0f ? clampf((b - c) * ia, 0.0f, 1.0f) : ss);
+  tt = clampf(tt, 0.0f, 1.0f);
+  s = !pa ? 0.0f : (!pe ? clampf(-c * ia, 0.0f, 1.0f) : ss);
+  t = !pe ? 0.0f : (!pa ? clampf(f * ie, 0.0f, 1.0f) : tt);
+}
+
+// the point of the segment P0 -> P1 (world) nearest the trunk box, deepest inside it: the box's signed distance is
+// convex along the segment, minimised by golden-section search (oracle/go1_oracle.c seg_box_t, SEG_GOLDEN steps)
+__device__ __forceinline__ float box_sdf(const float* c, const float* th) {
+  float o = 0.0f, in = -1e30f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float q = fabsf(c[i]) - th[i];
+    o += q > 0.0f ? q * q : 0.0f;
+    in = fmaxf(in, q);
+  }
+  return o * frsq(fmaxf(o, 1e-30f)) + fminf(in, 0.0f);
+}
+#define SEG_GOLDEN 32
+__device__ __forceinline__ float seg_box_t(const float* P0, const float* P1, const float* R, const float* pos,
+                                           const float* th) {
+  float a0[3], d[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    a0[i] = R[i] * (P0[0] - pos[0]) + R[3 + i] * (P0[1] - pos[1]) + R[6 + i] * (P0[2] - pos[2]);
+    d[i] = R[i] * (P1[0] - P0[0]) + R[3 + i] * (P1[1] - P0[1]) + R[6 + i] * (P1[2] - P0[2]);
+  }
+  const float gr = 0.6180339887498949f;
+  float lo = 0.0f, hi = 1.0f, x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
+  auto f = [&](float x) {
+    const float c[3] = {a0[0] + x * d[0], a0[1] + x * d[1], a0[2] + x * d[2]};
+    return box_sdf(c, th);
+  };
+  float f1 = f(x1), f2v = f(x2);
+  for (int it = 0; it < SEG_GOLDEN; ++it) {
+    const bool left = f1 <= f2v;
+    hi = left ? x2 : hi;
+    lo = left ? lo : x1;
+    const float nx = left ? hi - gr * (hi - lo) : lo + gr * (hi - lo);
+    const float fn = f(nx);
+    const float x1n = left ? nx : x2, x2n = left ? x1 : nx;
+    const float f1n = left ? fn : f2v, f2n = left ? f1 : fn;
+    x1 = x1n; x2 = x2n; f1 = f1n; f2v = f2n;
+  }
+  return 0.5f * (lo + hi);
+}
+
+// The force of a pair on one of its primitives: the pair is evaluated in its canonical order (A = the lower primitive
+// index), spheres of the two radii at the closest points s (on A), t (on B); the force on A, or its negative on B
+// (own_first false), and the own primitive's point (world).  A, B: (P0 r, P1, V0, V1) records in LDS, so the two
+// lanes of a pair compute the same bits and apply exactly opposite forces.
+__device__ __forceinline__ void self_pair_force(const float4* A, const float4* B, bool own_first, float ks, float ds,
+                                                float* F, float* pown) {
+  const float4 a0 = A[0], a1 = A[1], b0 = B[0], b1 = B[1];
+  const float pa0[3] = {a0.x, a0.y, a0.z}, da[3] = {a1.x - a0.x, a1.y - a0.y, a1.z - a0.z};
+  const float pb0[3] = {b0.x, b0.y, b0.z}, db[3] = {b1.x - b0.x, b1.y - b0.y, b1.z - b0.z};
+  float s, t;
+  seg_closest(pa0, da, pb0, db, s, t);
+  const float pa[3] = {pa0[0] + s * da[0], pa0[1] + s * da[1], pa0[2] + s * da[2]};
+  const float pb[3] = {pb0[0] + t * db[0], pb0[1] + t * db[1], pb0[2] + t * db[2]};
+  const float d0 = pa[0] - pb[0], d1 = pa[1] - pb[1], d2 = pa[2] - pb[2];
+  const float dd = d0 * d0 + d1 * d1 + d2 * d2, rs = a0.w + b0.w;
+  const float inv = dd > 1e-18f ? frsq(dd) : 0.0f;
+  const float n0 = dd > 1e-18f ? d0 * inv : 0.0f, n1 = dd > 1e-18f ? d1 * inv : 0.0f, n2 = dd > 1e-18f ? d2 * inv : 1.0f;
+  const float pen = rs - dd * inv;
+  const float4 va0 = A[2], va1 = A[3], vb0 = B[2], vb1 = B[3];
+  const float vr0 = (va0.x + s * (va1.x - va0.x)) - (vb0.x + t * (vb1.x - vb0.x));
+  const float vr1 = (va0.y + s * (va1.y - va0.y)) - (vb0.y + t * (vb1.y - vb0.y));
+  const float vr2 = (va0.z + s * (va1.z - va0.z)) - (vb0.z + t * (vb1.z - vb0.z));
+  const float vn = vr0 * n0 + vr1 * n1 + vr2 * n2;
+  float fn = ks * pen - ds * vn;
+  fn = (dd < rs * rs && fn > 0.0f) ? fn : 0.0f;
+  fn = own_first ? fn : -fn;
+  F[0] = fn * n0; F[1] = fn * n1; F[2] = fn * n2;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) pown[i] = own_first ? pa[i] : pb[i];
+}
+
+// sphere A (centre, radius in w) against the trunk box (half extents th about the base origin): the force on A (world)
+// added to F and the trunk's reaction wrench (base frame, (moment, force) about the base origin) added to wb
 __device__ __forceinline__ void self_box_force(const float4 A, const float4 Av, const float* R, const float* pos,
                                                const float* vb, const float* th, float ks, float ds, float* F,
                                                float* wb) {
@@ -1605,9 +1610,12 @@ __device__ __forceinline__ void self_box_force(const float4 A, const float4 Av, 
 #pragma unroll
     for (int i = 0; i < 3; ++i) nb[i] = d[i] * inv;
     pen = A.w - dd * inv;
-  } else {  // centre inside: out through the nearest face (lowest axis on ties)
+  } else {  // centre inside: out through the nearest face (lowest axis on ties), the depths compared quantised
+    // to 0.1 mm (oracle BOX_Q): a segment's deepest point inside the box often has two faces equally near
     const float m0 = th[0] - fabsf(c[0]), m1 = th[1] - fabsf(c[1]), m2 = th[2] - fabsf(c[2]);
-    const int ax = (m0 <= m1 && m0 <= m2) ? 0 : (m1 <= m2 ? 1 : 2);
+    const int q0 = (int)floorf(fminf(fmaxf(m0, -1.0f), 1.0f) * 1.0e4f), q1 = (int)floorf(fminf(fmaxf(m1, -1.0f), 1.0f) * 1.0e4f),
+              q2 = (int)floorf(fminf(fmaxf(m2, -1.0f), 1.0f) * 1.0e4f);
+    const int ax = (q0 <= q1 && q0 <= q2) ? 0 : (q1 <= q2 ? 1 : 2);
     const float sg = c[ax] >= 0.0f ? 1.0f : -1.0f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) nb[i] = i == ax ? sg : 0.0f;
@@ -1645,104 +1653,94 @@ __device__ __forceinline__ int quad_or(int v) {
 
 // leg pairs lp: (0,1) = 0, (0,2) = 1, (0,3) = 2, (1,2) = 3, (1,3) = 4, (2,3) = 5
 
-// Narrow phase (a wave whose broad phase found a candidate).  sc: this env's LDS scratch, the spheres already
-// written (self_put).  Each lane sums the forces on its own two spheres from their partners directly: per
-// candidate partner leg, the leg's 8 spheres in one LDS round trip against both own spheres at once (packed
-// halves), the overlaps into a per-lane work list, then one force per list entry.  Both loops run as often as the
-// busiest lane needs -- with one wave per SIMD the launch lasts as long as its slowest wave, and the slow waves
-// are those with a folded env; a wave-uniform loop over every partner any lane touches (~90 VALU each) made the
-// narrow phase cost ~10 us of the launch, force slots with barriers likewise.  Each pair is evaluated once from
-// each side; the two results are exactly opposite (self_sphere_force), and every sphere's sum runs in a fixed
-// order (the list's bit order).  Fs: the self-contact world forces on the lane's two spheres (x, y halves), wb:
-// the trunk reaction wrench of the lane's box contacts (base frame, summed over the env's lanes by the caller).
-// Measured out of line (a call) and with the actuator net's weights reloaded per sub-step to free registers:
-// neither faster.
+// Narrow phase (a wave whose broad phase found a candidate).  sc: this env's LDS scratch, the primitives already
+// written (self_put).  Each lane sums the forces on its own primitive from its candidate partners: per candidate
+// partner leg (a per-lane list walked with ctz: the loop runs as often as the lane with the most candidates needs),
+// the leg's four primitives (the own leg's two-joints-apart ones for d = 0), each pair evaluated in its canonical
+// order (the lower primitive index first), so the two lanes of a pair compute the same bits and apply exactly
+// opposite forces, every sum in a fixed order.  Then the trunk box for a folded leg.  Output: the world force Fo on
+// the own primitive and its moment Mo about the own body's origin pb; wb: the trunk reaction of the lane's box
+// contact (base frame).
 __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, int leg, int role, int mask,
                                            const float* R, const float* pos, const float* vb, const float* th,
-                                           float Fs[2][3], float* wb) {
+                                           const float* pb, float* Fo, float* Mo, float* wb) {
   const float ks = cfg->self_stiffness, ds = cfg->self_damping;
-  const int s0 = self_s0(role), s1 = self_s1(role);
-  const int ia0 = leg * 8 + s0, ia1 = leg * 8 + s1;
-  float4* P = reinterpret_cast<float4*>(sc);
-  // (the own spheres are re-read from LDS where needed: registers are scarce here, and every one freed lets the
-  // test loop keep more partner loads in flight)
-  // the trunk box, by the lane of the sphere (thigh, calf and foot: every x half, the y halves of roles 0 and 2)
-  if ((mask >> (6 + leg)) & 1) {
-    self_box_force(P[2 * ia0], P[2 * ia0 + 1], R, pos, vb, th, ks, ds, Fs[0], wb);
-    if ((role & 1) == 0) self_box_force(P[2 * ia1], P[2 * ia1 + 1], R, pos, vb, th, ks, ds, Fs[1], wb);
-  }
-  MARK(self_box_done);
-  const float4 A0 = P[2 * ia0], A1 = P[2 * ia1];
-  // Tests first, forces from a per-lane work list: bit 16 d + 2 u + h of ovm = own sphere h overlaps sphere u of
-  // leg ^ d (d = 0: the own leg's pairs two joints apart, SELF_SAME_A / _B of the oracle; d = 1..3: the other
-  // legs of candidate leg pairs, mask bits as self_broad sets them).  The force loop then runs as many times as
-  // the busiest lane has overlaps (a wave-uniform loop over the partners would run every partner any lane
-  // touches, ~90 VALU each, at the pace of the one folded env of the wave).
-  const f2 Ax = f2{A0.x, A1.x}, Ay = f2{A0.y, A1.y}, Az = f2{A0.z, A1.z}, Ar = f2{A0.w, A1.w};
-  unsigned long long ovm = 0ull;
-  // the lane's candidate partner legs (bit d: leg ^ d), walked as a per-lane list like the forces below: the
-  // loop runs as often as the lane with the most candidates needs, not once per leg pair any env of the wave has
+  const float4* Pr = reinterpret_cast<const float4*>(sc);
+  const int io = 4 * leg + role;
   const int lp1 = (leg >> 1) ? 5 : 0, lp2 = (leg & 1) ? 4 : 1, lp3 = (leg == 0 || leg == 3) ? 2 : 3;
+  // candidate partner legs, bit d: leg ^ d (d = 0: the own leg's links two joints apart, when folded)
   unsigned cand = ((mask >> (10 + leg)) & 1) | (((mask >> lp1) & 1) << 1) | (((mask >> lp2) & 1) << 2) |
                   (((mask >> lp3) & 1) << 3);
-  // d = 0: hip ends 6, 7 against calf 3, 4 and foot 5; calf against the hip ends; foot against the hip ends and
-  // thigh 0-2; thigh against the foot (s0: 0, 2, 3 or 5; s1: 1, 6, 4 or 7)
-  // as list bits (h = 0: even bits 2 u, h = 1: odd bits 2 u + 1), interleaved once here
-  const unsigned sm0 = s0 == 3 ? 0xC0u : (s0 == 5 ? 0xC7u : 0x20u);
-  const unsigned sm1 = s1 >= 6 ? 0x38u : (s1 == 4 ? 0xC0u : 0x20u);
-  unsigned keep_same = 0u;
+  // the own leg's partners of primitive `role`: thigh - foot, hip - calf / foot, calf - hip, foot - thigh / hip
+  const unsigned keep_same = role == 0 ? 0x8u : (role == 1 ? 0xCu : (role == 2 ? 0x2u : 0x3u));
+  auto acc = [&](const float* p, const float* F) {  // force F (world) on the own primitive at p
+    const float p0 = p[0] - pb[0], p1 = p[1] - pb[1], p2 = p[2] - pb[2];
+    Fo[0] += F[0]; Fo[1] += F[1]; Fo[2] += F[2];
+    Mo[0] += p1 * F[2] - p2 * F[1];
+    Mo[1] += p2 * F[0] - p0 * F[2];
+    Mo[2] += p0 * F[1] - p1 * F[0];
+  };
+  // first the bounding boxes (the segment's ends grown by the radius, world axes) of the candidate legs' primitives,
+  // all four partners' loads in one LDS round trip, into a per-lane work list (bit 4 d + m: primitive m of leg ^ d);
+  // then the pairs of the list -- both loops run as often as the busiest lane needs
+  unsigned work = 0u;
+  {
+    const float4 O0 = Pr[4 * io], O1 = Pr[4 * io + 1];
+    const float olx = fminf(O0.x, O1.x) - O0.w, ohx = fmaxf(O0.x, O1.x) + O0.w;
+    const float oly = fminf(O0.y, O1.y) - O0.w, ohy = fmaxf(O0.y, O1.y) + O0.w;
+    const float olz = fminf(O0.z, O1.z) - O0.w, ohz = fmaxf(O0.z, O1.z) + O0.w;
+    while (__any(cand != 0u)) {
+      const bool act = cand != 0u;
+      const int d = act ? __builtin_ctz(cand) : 0;
+      cand &= cand - 1u;
+      const unsigned keep = !act ? 0u : (d == 0 ? keep_same : 0xFu);
+      const float4* Q = Pr + 16 * (leg ^ d);
+      float4 B0[4], B1[4];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) keep_same |= (((sm0 >> u) & 1u) << (2 * u)) | (((sm1 >> u) & 1u) << (2 * u + 1));
-  while (__any(cand != 0u)) {
-    const bool act = cand != 0u;
-    const int d = act ? __builtin_ctz(cand) : 0;
-    cand &= cand - 1u;
-    const unsigned keep = !act ? 0u : (d == 0 ? keep_same : 0xFFFFu);
-    const float4* Q = P + 16 * (leg ^ d);
-    unsigned bits = 0u;
-    float4 Bs[8];  // all eight partner loads in flight at once (one LDS round trip)
+      for (int m = 0; m < 4; ++m) { B0[m] = Q[4 * m]; B1[m] = Q[4 * m + 1]; }
+      __builtin_amdgcn_sched_barrier(0);
+      unsigned bits = 0u;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) Bs[u] = Q[2 * u];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float4 B = Bs[u];
-      const f2 e0 = Ax - B.x, e1 = Ay - B.y, e2 = Az - B.z, rs = Ar + B.w;  // both own spheres (packed halves)
-      const f2 dd = e0 * e0 + e1 * e1 + e2 * e2, r2 = rs * rs;
-      bits |= (dd.x < r2.x ? 1u << (2 * u) : 0u) | (dd.y < r2.y ? 2u << (2 * u) : 0u);
+      for (int m = 0; m < 4; ++m) {
+        const float r = B0[m].w;
+        const bool ox = (fminf(B0[m].x, B1[m].x) - r <= ohx) & (olx <= fmaxf(B0[m].x, B1[m].x) + r);
+        const bool oy = (fminf(B0[m].y, B1[m].y) - r <= ohy) & (oly <= fmaxf(B0[m].y, B1[m].y) + r);
+        const bool oz = (fminf(B0[m].z, B1[m].z) - r <= ohz) & (olz <= fmaxf(B0[m].z, B1[m].z) + r);
+        bits |= (ox & oy & oz) ? 1u << m : 0u;
+      }
+      work |= (bits & keep) << (4 * d);
     }
-    ovm |= (unsigned long long)(bits & keep) << (16 * d);
   }
   MARK(self_tests_done);
-  while (__any(ovm != 0ull)) {
-    const bool act = ovm != 0ull;
-    const int bit = act ? (int)__builtin_ctzll(ovm) : 0;
-    ovm &= ovm - 1ull;
-    const bool h = (bit & 1) != 0;
-    const int ib = ((leg ^ (bit >> 4)) << 3) + ((bit >> 1) & 7);
-    const float4 B = P[2 * ib], Bv = P[2 * ib + 1];
-    const int ia = h ? ia1 : ia0;
-    const float4 A = P[2 * ia], Av = P[2 * ia + 1];
-    float f[3];
-    self_sphere_force(A, Av, B, Bv, ks, ds, f, ia < ib ? 1.0f : -1.0f);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      Fs[0][i] += (act && !h) ? f[i] : 0.0f;
-      Fs[1][i] += (act && h) ? f[i] : 0.0f;
-    }
+  while (__any(work != 0u)) {
+    const bool act = work != 0u;
+    const int bit = act ? __builtin_ctz(work) : 0;
+    work &= work - 1u;
+    const int ip = 4 * (leg ^ (bit >> 2)) + (bit & 3);
+    const bool first = io < ip;
+    float F[3], p[3];
+    self_pair_force(Pr + 4 * min(io, ip), Pr + 4 * max(io, ip), first, ks, ds, F, p);
+    const float Fw[3] = {act ? F[0] : 0.0f, act ? F[1] : 0.0f, act ? F[2] : 0.0f};
+    acc(p, Fw);
   }
-  MARK(self_cross_done);
-}
-
-// the lane's spheres into this env's LDS scratch (x half s0, y half s1)
-__device__ __forceinline__ void self_put(float* sc, int leg, int role, const float* p0, const float* v0, float r0,
-                                         const float* p1, const float* v1, float r1) {
-  float4* P = reinterpret_cast<float4*>(sc);
-  const int a = leg * 8 + self_s0(role), b = leg * 8 + self_s1(role);
-  P[2 * a] = make_float4(p0[0], p0[1], p0[2], r0);
-  P[2 * a + 1] = make_float4(v0[0], v0[1], v0[2], 0.0f);
-  P[2 * b] = make_float4(p1[0], p1[1], p1[2], r1);
-  P[2 * b + 1] = make_float4(v1[0], v1[1], v1[2], 0.0f);
+  MARK(self_pairs_done);
+  // the trunk box, for a folded leg's thigh, calf and foot (the hip is the trunk's neighbour)
+  if (__any(((mask >> (6 + leg)) & 1) && role != 1)) {
+    const bool on = ((mask >> (6 + leg)) & 1) && role != 1;
+    const float4 O0 = Pr[4 * io], O1 = Pr[4 * io + 1], O2 = Pr[4 * io + 2], O3 = Pr[4 * io + 3];
+    const float P0[3] = {O0.x, O0.y, O0.z}, P1[3] = {O1.x, O1.y, O1.z};
+    const float u = role == 3 ? 0.0f : seg_box_t(P0, P1, R, pos, th);
+    const float4 C = make_float4(O0.x + u * (O1.x - O0.x), O0.y + u * (O1.y - O0.y), O0.z + u * (O1.z - O0.z), O0.w);
+    const float4 Cv = make_float4(O2.x + u * (O3.x - O2.x), O2.y + u * (O3.y - O2.y), O2.z + u * (O3.z - O2.z), 0.0f);
+    float F[3] = {0.0f, 0.0f, 0.0f}, w6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    self_box_force(C, Cv, R, pos, vb, th, ks, ds, F, w6);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) wb[i] += on ? w6[i] : 0.0f;
+    const float Fb[3] = {on ? F[0] : 0.0f, on ? F[1] : 0.0f, on ? F[2] : 0.0f};
+    const float pc[3] = {C.x, C.y, C.z};
+    acc(pc, Fb);
+  }
+  MARK(self_box_done);
 }
 
 // Broad phase, in registers, in the trunk frame (where the legs keep their places whatever the trunk's
@@ -1776,7 +1774,7 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
     o3 = o3 & (lo <= hi3) & (lo3 <= hi);
   }
   // the leg's own links two joints apart and the trunk box: out of reach while every joint of the leg is within
-  // 0.1 rad of its URDF range (the nearest such contact needs 0.2 rad past a limit, a trunk box contact 0.89;
+  // 0.1 rad of its URDF range (inside the band the capsules keep 8.6 mm same-leg and 14.8 mm box clearance;
   // tests/test_self_collision.py::test_fold_gate_is_sound), so only a leg outside that band goes to the narrow
   // phase for them (no branch here: the broad phase shares a basic block with the terrain contacts)
   const bool wild = (fabsf(q[0]) > 0.9029f) | (q[1] < -1.1472f) | (q[1] > 4.2888f) | (q[2] < -2.7966f) |
@@ -1789,6 +1787,18 @@ __device__ __forceinline__ int self_broad(int leg, const float* pth, const float
   return quad_or(mask);
 }
 
+// One integrator step of length h for the env of this lane.  Lane layout (16 per env): lane = 16 role + 4 env +
+// leg.  The four roles of a leg compute the leg's kinematics and ABA passes redundantly (base quantities on all 16
+// lanes), and split the leg's contact geometry two per lane (x, y halves of f2), each a capsule segment acting at
+// its deepest point (seg_deepest2; a point is a degenerate segment):
+//   role 0: thigh half at the thigh joint, thigh half at the knee   (body: thigh, thigh)
+//   role 1: hip capsule, trunk corner 2 leg                          (body: hip, trunk)
+//   role 2: calf half at the knee, calf half at the foot             (body: calf, calf)
+//   role 3: foot sphere, trunk corner 2 leg + 1                      (body: calf, trunk)
+// so each wave has four envs and the whole grid fills every SIMD.  The lane's self-collision primitive is its x
+// half's link (thigh, hip, calf, foot).
+// cf_raw: this lane's reported contact forces (x half with the own primitive's self-contact force, y half, the
+// trunk's self-collision reaction of the lane's box contact and, on one lane, the trunk faces').
 __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float* lds, Phys& S, const float* tau,
                                              float h, const float* g, float friction, float restitution,
                                              float payload, const Terr& T, int leg, int role, bool cf_out,
@@ -1816,6 +1826,20 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   for (int i = 0; i < 3; ++i) vbp[i] = R[i] * S.wv[0] + R[3 + i] * S.wv[1] + R[6 + i] * S.wv[2];
   const float vb[6] = {vbp[0].x, vbp[1].x, vbp[2].x, vbp[0].y, vbp[1].y, vbp[2].y};
   const float* th = model + 13 * 10 + 4 * 9 + 3 + 1;  // trunk half extents
+#ifndef GO1_ABL_NO_FACES
+  // the trunk faces' vertices of the control step (face_scan), chosen here where few values are live yet (wave-uniform
+  // condition); one lane stores them for every sim step's face_force below (the same on the env's 16 lanes)
+  if (T.patch && face_scan_now) {
+    int sel[2];
+    face_scan(T, R, S.pos, th, 4 * role + leg, sel);
+    if (role == 0 && leg == 0) {
+      int* fsel = reinterpret_cast<int*>(self_sc + FACE_SEL_OFF);
+      fsel[0] = sel[0];
+      fsel[1] = sel[1];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the env's other lanes read them (face_force)
+  }
+#endif
   // ---- this leg: kinematics, rigid bias forces and gravity (hip -> calf)
   const float* origin = LC + 30;
   const float* foot = model + 13 * 10 + 4 * 9;
@@ -1824,9 +1848,16 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   const float calf_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 1];
   const float hip_r = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 2];
   const float hip_y0 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 3], hip_y1 = model[13 * 10 + 4 * 9 + 3 + 1 + 3 + 4];
-  float Fhip[3] = {0.0f, 0.0f, 0.0f};  // the hip capsule's world force (the leg's, on every role)
   float cs[3][2];
-  float Rl[2][9], pl[2][3], vl[2][6];  // thigh and calf frames for the contacts
+  // the lane's two bodies (x, y halves of the contact pass), selected as the chain passes them: x half thigh (role
+  // 0), hip (1), calf (2, 3); y half thigh (0), calf (2), trunk (odd rows)
+  const bool even = (role & 1) == 0;
+  f2 Rs[9], ps[3], vs[6];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rs[i] = f2{0.0f, R[i]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { ps[i] = f2{0.0f, S.pos[i]}; vs[i] = f2{0.0f, vb[i]}; vs[3 + i] = f2{0.0f, vb[3 + i]}; }
+  float pth[3], pkn[3], pft[3];  // the thigh joint, the knee and the foot centre (world), for the broad phase
   f2 cjp[3][3], pAp[3][3];  // c_j and the articulated bias force as (angular, linear) pairs
   {
     // link frame: rows 0 and 1 of the rotation as pairs over the column (row0_k, row1_k)
@@ -1862,92 +1893,83 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       rE(ax, cn, sn, R2, R2);
       // rigid bias force v x* I v about the link origin (gravity: a base acceleration, below)
       rigid_bias2(LC + 10 * j, vj, pAp[j]);
+      const bool sx = j == 0 ? role == 1 : (j == 1 ? role == 0 : role >= 2);  // this link is the x half's
+      const bool sy = j == 1 ? role == 0 : (j == 2 ? role == 2 : false);      // ... the y half's
       if (j > 0) {
+        (j == 1 ? pth : pkn)[0] = pp01.x; (j == 1 ? pth : pkn)[1] = pp01.y; (j == 1 ? pth : pkn)[2] = pp2;
+      }
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { Rl[j - 1][k] = R01[k].x; Rl[j - 1][3 + k] = R01[k].y; Rl[j - 1][6 + k] = R2[k]; }
-        pl[j - 1][0] = pp01.x; pl[j - 1][1] = pp01.y; pl[j - 1][2] = pp2;
+      for (int k = 0; k < 3; ++k) {
+        const float lr[3] = {R01[k].x, R01[k].y, R2[k]};  // column k of the link rotation
 #pragma unroll
-        for (int i = 0; i < 3; ++i) { vl[j - 1][i] = vj[i].x; vl[j - 1][3 + i] = vj[i].y; }
+        for (int row = 0; row < 3; ++row) {
+          Rs[3 * row + k].x = sx ? lr[row] : Rs[3 * row + k].x;
+          Rs[3 * row + k].y = sy ? lr[row] : Rs[3 * row + k].y;
+        }
+      }
+      const float pv[3] = {pp01.x, pp01.y, pp2};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        ps[i].x = sx ? pv[i] : ps[i].x;
+        ps[i].y = sy ? pv[i] : ps[i].y;
+        vs[i].x = sx ? vj[i].x : vs[i].x;
+        vs[i].y = sy ? vj[i].x : vs[i].y;
+        vs[3 + i].x = sx ? vj[i].y : vs[3 + i].x;
+        vs[3 + i].y = sy ? vj[i].y : vs[3 + i].y;
+      }
+      if (j == 2) {  // the foot centre (world), for the broad phase
+        pft[0] = pp01.x + R01[0].x * foot[0] + R01[1].x * foot[1] + R01[2].x * foot[2];
+        pft[1] = pp01.y + R01[0].y * foot[0] + R01[1].y * foot[1] + R01[2].y * foot[2];
+        pft[2] = pp2 + R2[0] * foot[0] + R2[1] * foot[1] + R2[2] * foot[2];
       }
 #pragma unroll
       for (int i = 0; i < 3; ++i) vp[i] = vj[i];
     }
   }
   MARK(leg_kin_done);
-  // ---- contacts: points 2 role, 2 role + 1 of [thigh0, thigh1, thigh2, calf0, calf1, foot,
-  //      corner 2 leg, corner 2 leg + 1] -- world position / velocity, terrain corners, the explicit
-  //      force (body frame of the point's body) and the added mass of the implicit contact
-  // per lane: the leg's (thigh | calf) share in the row pair of its body and the trunk corner's share
-  float fleg[6] = {0, 0, 0, 0, 0, 0}, fbase[6] = {0, 0, 0, 0, 0, 0};
-  f2 Fpt[3] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};  // world forces of the lane's two points
-  float Fbs[3] = {0.0f, 0.0f, 0.0f};  // world reaction force on the trunk of the lane's self-collision box pairs
-  const bool even = (role & 1) == 0;
-  // the contact inertias of this lane's points as one packed SIP per half (x, y = the two points):
-  // [[S M S^T, S M], [M S^T, M]] with M = Rs^T Mp Rs in the body frame, S = lp~
+  // ---- contacts: the lane's two segments (x, y halves) in the body frame of their link, their deepest points
+  //      against the heightfields, the explicit force there and the added mass of the implicit contact
+  // per lane: the body-frame wrench of the x half's link (thigh, hip or calf) and of the even rows' y half (the
+  // same link), the trunk's share (odd rows' y halves, the box reactions)
+  float fx[6], fy[6], fbase[6];
+  f2 Fpt[3];          // world forces of the lane's two contact points
+  float Fo[3] = {0.0f, 0.0f, 0.0f};  // the own primitive's self-contact force (world)
+  float Fbs[3] = {0.0f, 0.0f, 0.0f};  // world reaction force on the trunk of the lane's self-collision box contact
   SIP cin[2];
 #ifndef GO1_ABL_NO_CONTACT
   {
-    // the lane's two points ride in the halves of f2 (v_pk) from the frame selection to
-    // the body-frame force.  Points p: thigh 0-2, calf 3-4, foot 5 (on the calf), trunk corners
-    // 6-7 (2 leg, 2 leg + 1).  Rows (roles): 0 (thigh0, thigh1), 1 (thigh2, corner 6),
-    // 2 (calf0, calf1), 3 (foot, corner 7) -- x halves and the even rows' y halves belong to the
-    // thigh on rows 0-1 and to the calf on rows 2-3 (one pair reduction, pairsum_rows_n), the odd
-    // rows' y halves to the trunk
-    f2 Rs[9], lp[3], rr, pw[3], vw[3];
-    HQ qa, qb;
+    f2 lpA[3], lpB[3], rr;
     {
-      const bool lo_rows = role <= 1;  // x: thigh on rows 0-1, calf on rows 2-3; y: thigh, base, calf, base
-      f2 ps[3], vs[6];
-#pragma unroll
-      for (int i = 0; i < 9; ++i)
-        Rs[i] = f2{lo_rows ? Rl[0][i] : Rl[1][i], even ? (lo_rows ? Rl[0][i] : Rl[1][i]) : R[i]};
-#pragma unroll
-      for (int i = 0; i < 3; ++i) ps[i] = f2{lo_rows ? pl[0][i] : pl[1][i], even ? (lo_rows ? pl[0][i] : pl[1][i]) : S.pos[i]};
-#pragma unroll
-      for (int i = 0; i < 6; ++i) vs[i] = f2{lo_rows ? vl[0][i] : vl[1][i], even ? (lo_rows ? vl[0][i] : vl[1][i]) : vb[i]};
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int p = hh == 0 ? (role == 0 ? 0 : (role == 1 ? 2 : (role == 2 ? 3 : 5)))
-                              : (role == 0 ? 1 : (role == 1 ? 6 : (role == 2 ? 4 : 7)));
-        const bool on_thigh = p < 3, on_base = p >= 6;
-        const int cx = leg * 2 + (p - 6);
-        const float lz = -0.071f * (float)(on_thigh ? p + 1 : p - 2);
-        lp[0][hh] = on_base ? ((cx & 1) ? th[0] : -th[0]) : (p == 5 ? foot[0] : 0.0f);
-        lp[1][hh] = on_base ? ((cx & 2) ? th[1] : -th[1]) : (p == 5 ? foot[1] : 0.0f);
-        lp[2][hh] = on_base ? ((cx & 4) ? th[2] : -th[2]) : (p == 5 ? foot[2] : lz);
-        rr[hh] = on_base ? 0.0f : (on_thigh ? thigh_r : (p == 5 ? foot_r : calf_r));
-      }
-      // point kinematics: v = R (v_lin + w x lp), p = p_body + R lp
-      const f2 wl[3] = {vs[1] * lp[2] - vs[2] * lp[1], vs[2] * lp[0] - vs[0] * lp[2], vs[0] * lp[1] - vs[1] * lp[0]};
-      const f2 vlin[3] = {vs[3] + wl[0], vs[4] + wl[1], vs[5] + wl[2]};
+      // segment ends in the link frame: halves walked from their outer ends (a link lying flat is carried at both)
+      const float* kn = origin + 6;  // the knee: the calf joint's origin in the thigh frame
+      const int cA = leg * 2, cB = leg * 2 + 1;  // this leg's trunk corners (roles 1, 3)
+      const float crn[2][3] = {{(cA & 1) ? th[0] : -th[0], (cA & 2) ? th[1] : -th[1], (cA & 4) ? th[2] : -th[2]},
+                               {(cB & 1) ? th[0] : -th[0], (cB & 2) ? th[1] : -th[1], (cB & 4) ? th[2] : -th[2]}};
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        pw[i] = ps[i] + Rs[3 * i] * lp[0] + Rs[3 * i + 1] * lp[1] + Rs[3 * i + 2] * lp[2];
-        vw[i] = Rs[3 * i] * vlin[0] + Rs[3 * i + 1] * vlin[1] + Rs[3 * i + 2] * vlin[2];
+        const float hyA = i == 1 ? msy * hip_y0 : 0.0f, hyB = i == 1 ? msy * hip_y1 : 0.0f;
+        const float xa = role == 0 ? 0.0f : (role == 1 ? hyA : (role == 2 ? 0.0f : foot[i]));
+        const float xb = role == 0 ? 0.5f * kn[i] : (role == 1 ? hyB : (role == 2 ? 0.5f * foot[i] : foot[i]));
+        const float ya = role == 0 ? kn[i] : (role == 2 ? foot[i] : crn[role >> 1][i]);
+        const float yb = role == 0 ? 0.5f * kn[i] : (role == 2 ? 0.5f * foot[i] : crn[role >> 1][i]);
+        lpA[i] = f2{xa, ya};
+        lpB[i] = f2{xb, yb};
       }
-      hq_fetch(T, pw[0].x, pw[1].x, qa);
-      hq_fetch(T, pw[0].y, pw[1].y, qb);
+      rr = f2{role == 0 ? thigh_r : (role == 1 ? hip_r : (role == 2 ? calf_r : foot_r)),
+              role == 0 ? thigh_r : (role == 2 ? calf_r : 0.0f)};
     }
-    // self-collision: world forces on the lane's two spheres, the trunk's reaction wrench of the lane's box pairs
-    // into its trunk share.  The broad phase has no branch around it (the off switch is a select), so it sits in
-    // one basic block with the terrain contacts below and the scheduler overlaps its latency chains (trunk-frame
-    // transforms, DPP exchanges) with theirs; the narrow phase follows the contacts.
-    float Fs[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}}, wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) cf_raw[6 + i] = 0.0f;  // the hip's reported force of this sim step, from here
+    // self-collision first (few values live yet): the broad phase, and the narrow phase in a wave with a candidate
+    float wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, Mo[3] = {0.0f, 0.0f, 0.0f};
     MARK(self_begin);
-    // the hip capsule's ends in the trunk frame: the hip joint + Rx(q_hip) (0, y, 0)
-    const f2 hy = msy * f2{hip_y0, hip_y1};
-    const f2 hcy = origin[1] + cs[0][0] * hy, hcz = origin[2] + cs[0][1] * hy;
-    const float hc0[3] = {origin[0], hcy.x, hcz.x}, hc1[3] = {origin[0], hcy.y, hcz.y};
 #ifndef GO1_ABL_NO_SELF  // ablation build only: no self-collision
     const bool self_on = cfg->self_stiffness > 0.0f;
     int mask;
     {
-      float pft[3];  // the foot centre (calf frame offset), for the leg's bounding box
-#pragma unroll
-      for (int i = 0; i < 3; ++i) pft[i] = pl[1][i] + Rl[1][3 * i] * foot[0] + Rl[1][3 * i + 1] * foot[1] + Rl[1][3 * i + 2] * foot[2];
-      mask = self_broad(leg, pl[0], pl[1], pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), hc0, hc1, hip_r, R, S.pos, th,
+      // the hip capsule's ends in the trunk frame: the hip joint + Rx(q) (0, y, 0)
+      const f2 hy = msy * f2{hip_y0, hip_y1};
+      const f2 hcy = origin[1] + cs[0][0] * hy, hcz = origin[2] + cs[0][1] * hy;
+      const float hc0[3] = {origin[0], hcy.x, hcz.x}, hc1[3] = {origin[0], hcy.y, hcz.y};
+      mask = self_broad(leg, pth, pkn, pft, fmaxf(foot_r, fmaxf(thigh_r, calf_r)), hc0, hc1, hip_r, R, S.pos, th,
                         S.q);
       mask = self_on ? mask : 0;
     }
@@ -1956,6 +1978,92 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     const int mask = 0;
 #endif
     MARK(self_broad_done);
+    if (__any(mask != 0)) {
+      // the lane's own primitive (its x half's link): the whole segment, ends and their velocities (world)
+      float P0[3], P1[3], V0[3], V1[3];
+      {
+        const float* kn = origin + 6;
+        f2 e[3];  // (end 0, end 1) in the link frame
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const float hy0 = i == 1 ? msy * hip_y0 : 0.0f, hy1 = i == 1 ? msy * hip_y1 : 0.0f;
+          e[i] = f2{role == 1 ? hy0 : (role == 3 ? foot[i] : 0.0f),
+                    role == 0 ? kn[i] : (role == 1 ? hy1 : foot[i])};
+        }
+        const float w[3] = {vs[0].x, vs[1].x, vs[2].x};
+        const f2 wl[3] = {w[1] * e[2] - w[2] * e[1], w[2] * e[0] - w[0] * e[2], w[0] * e[1] - w[1] * e[0]};
+        const f2 vlin[3] = {vs[3].x + wl[0], vs[4].x + wl[1], vs[5].x + wl[2]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const f2 p = ps[i].x + Rs[3 * i].x * e[0] + Rs[3 * i + 1].x * e[1] + Rs[3 * i + 2].x * e[2];
+          const f2 v = Rs[3 * i].x * vlin[0] + Rs[3 * i + 1].x * vlin[1] + Rs[3 * i + 2].x * vlin[2];
+          P0[i] = p.x; P1[i] = p.y; V0[i] = v.x; V1[i] = v.y;
+        }
+      }
+      // bounding radius: half the link's segment (thigh, calf: half the knee / foot offset; hip: half the capsule's
+      // segment; foot: a point) plus its radius
+      const float half = role == 0 ? 0.5f * fabsf(origin[8]) : (role == 1 ? 0.5f * (hip_y1 - hip_y0) : (role == 2 ? 0.5f * fabsf(foot[2]) : 0.0f));
+      self_put(self_sc, leg, role, P0, P1, rr.x, half + rr.x, V0, V1);
+      // the block is this one wave (TPB 64): the other lanes' primitives are visible once the wave's own LDS
+      // writes completed -- no s_barrier, and above all no vmcnt(0) drain of the terrain loads in flight
+      static_assert(TPB == 64, "self-collision LDS exchange assumes one wave per block");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      MARK(self_put_done);
+      const float pb[3] = {ps[0].x, ps[1].x, ps[2].x};
+      self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, pb, Fo, Mo, wb);
+      // the next sub-step's self_put must not overtake this one's partner reads of other lanes' records
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      MARK(self_narrow_done);
+    }
+    // world positions of the segment ends, the deepest point of each segment, its point kinematics
+    f2 lp[3], pw[3], vw[3];
+    HQ qa, qb;
+    int cell[2];
+    {
+      f2 wA[3], wB[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        wA[i] = ps[i] + Rs[3 * i] * lpA[0] + Rs[3 * i + 1] * lpA[1] + Rs[3 * i + 2] * lpA[2];
+        wB[i] = ps[i] + Rs[3 * i] * lpB[0] + Rs[3 * i + 1] * lpB[1] + Rs[3 * i + 2] * lpB[2];
+      }
+      MARK(seg_begin);
+      // the search once per control step (wave-uniform), its t held in the env's LDS scratch for the other sim steps
+      float2* held = reinterpret_cast<float2*>(self_sc + SEG_T_OFF) + (4 * role + leg);
+      f2 ts;
+      if (face_scan_now) {
+#ifdef GO1_ABL_NO_WALK  // ablation build only: every segment at its first end
+        ts = f2{0.0f, 0.0f} * (wA[0] + wB[0]);
+        cell[0] = SEG_CELL((int)floorf(wA[0].x / T.hs), (int)floorf(wA[1].x / T.hs), false);
+        cell[1] = SEG_CELL((int)floorf(wA[0].y / T.hs), (int)floorf(wA[1].y / T.hs), false);
+#else
+        ts = seg_deepest2(T, wA, wB, rr, cell);
+#endif
+        *held = make_float2(ts.x, ts.y);
+      } else {
+        const float2 hv = *held;
+        ts = f2{hv.x, hv.y};
+      }
+      MARK(seg_done);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) lp[i] = lpA[i] + ts * (lpB[i] - lpA[i]);
+      // point kinematics: v = R (v_lin + w x lp), p = p_body + R lp
+      const f2 wl[3] = {vs[1] * lp[2] - vs[2] * lp[1], vs[2] * lp[0] - vs[0] * lp[2], vs[0] * lp[1] - vs[1] * lp[0]};
+      const f2 vlin[3] = {vs[3] + wl[0], vs[4] + wl[1], vs[5] + wl[2]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pw[i] = ps[i] + Rs[3 * i] * lp[0] + Rs[3 * i + 1] * lp[1] + Rs[3 * i + 2] * lp[2];
+        vw[i] = Rs[3 * i] * vlin[0] + Rs[3 * i + 1] * vlin[1] + Rs[3 * i + 2] * vlin[2];
+      }
+    }
+    // the terrain contacts at the segments' deepest points: on the search step on the triangle the search chose, later
+    // on the triangle under the point
+    if (face_scan_now) {
+      hq_fetch_cell(T, pw[0].x, pw[1].x, cell[0], qa);
+      hq_fetch_cell(T, pw[0].y, pw[1].y, cell[1], qb);
+    } else {
+      hq_fetch(T, pw[0].x, pw[1].x, qa);
+      hq_fetch(T, pw[0].y, pw[1].y, qb);
+    }
     float Fa[3], Fb2[3], Ma[6], Mb[6];
     {
       const float pa[3] = {pw[0].x, pw[1].x, pw[2].x}, va[3] = {vw[0].x, vw[1].x, vw[2].x};
@@ -1963,63 +2071,10 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       sphere_contact_im(T, qa, C, pa, va, rr.x, h, Fa, Ma);
       sphere_contact_im(T, qb, C, pb, vb2, rr.y, h, Fb2, Mb);
     }
-    if (__any(mask != 0)) {
-      // the lane's second sphere: point b of the contact pass, or on roles 1 and 3 an end of the hip capsule
-      // (world p = pos + R c, v = R (v_b + w_b x c + qd_hip e_x x (c - hip joint)))
-      const bool odd = (role & 1) != 0;
-      const float* hc = role == 1 ? hc0 : hc1;
-      float p1[3], v1[3];
-      {
-        const float rx = hc[1] - origin[1], rz = hc[2] - origin[2];  // e_x x (0, ry, rz) = (0, -rz, ry)
-        const float vh[3] = {vb[3] + (vb[1] * hc[2] - vb[2] * hc[1]), vb[4] + (vb[2] * hc[0] - vb[0] * hc[2]) - S.qd[0] * rz,
-                             vb[5] + (vb[0] * hc[1] - vb[1] * hc[0]) + S.qd[0] * rx};
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const float ph = S.pos[i] + (R[3 * i] * hc[0] + R[3 * i + 1] * hc[1] + R[3 * i + 2] * hc[2]);
-          const float vw_h = R[3 * i] * vh[0] + R[3 * i + 1] * vh[1] + R[3 * i + 2] * vh[2];
-          p1[i] = odd ? ph : pw[i].y;
-          v1[i] = odd ? vw_h : vw[i].y;
-        }
-      }
-      const float p0[3] = {pw[0].x, pw[1].x, pw[2].x}, v0[3] = {vw[0].x, vw[1].x, vw[2].x};
-      self_put(self_sc, leg, role, p0, v0, rr.x, p1, v1, odd ? hip_r : rr.y);
-      // the block is this one wave (TPB 64): the other lanes' spheres are visible once the wave's own LDS
-      // writes completed -- no s_barrier, and above all no vmcnt(0) drain of the terrain loads in flight
-      static_assert(TPB == 64, "self-collision LDS exchange assumes one wave per block");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      MARK(self_put_done);
-      self_narrow(cfg, self_sc, leg, role, mask, R, S.pos, vb, th, Fs, wb);
-      MARK(self_narrow_done);
-      // the hip ends' forces (y halves of roles 1 and 3) on the hip link: hip-frame force f = Rh^T F and
-      // moment (0, y, 0) x f, summed over the leg's rows (every role runs the leg's ABA); rare, so only in a
-      // wave that has one
-      if (__any(odd && (Fs[1][0] != 0.0f || Fs[1][1] != 0.0f || Fs[1][2] != 0.0f))) {
-        float hv[8];
-        {
-          const float F0 = odd ? Fs[1][0] : 0.0f, F1 = odd ? Fs[1][1] : 0.0f, F2 = odd ? Fs[1][2] : 0.0f;
-          const float r0 = R[0] * F0 + R[3] * F1 + R[6] * F2, r1 = R[1] * F0 + R[4] * F1 + R[7] * F2,
-                      r2 = R[2] * F0 + R[5] * F1 + R[8] * F2;
-          const float fh1 = cs[0][0] * r1 + cs[0][1] * r2, fh2 = cs[0][0] * r2 - cs[0][1] * r1;
-          const float y = role == 1 ? hy.x : hy.y;
-          hv[0] = y * fh2; hv[1] = -(y * r0); hv[2] = r0; hv[3] = fh1; hv[4] = fh2;
-          hv[5] = F0; hv[6] = F1; hv[7] = F2;
-        }
-        rowsum4_n<8>(hv);
-        pAp[0][0] -= f2{hv[0], hv[2]};
-        pAp[0][1] -= f2{0.0f, hv[3]};
-        pAp[0][2] -= f2{hv[1], hv[4]};
-#pragma unroll
-        for (int i = 0; i < 3; ++i) cf_raw[6 + i] = hv[5 + i];  // the hip's self-contact force (+ Fhip at the end)
-      }
-      if (odd) { Fs[1][0] = 0.0f; Fs[1][1] = 0.0f; Fs[1][2] = 0.0f; }  // not the trunk corner's
-      MARK(self_hip_done);
-    }
     if (self_on) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) Fbs[i] = R[3 * i] * wb[3] + R[3 * i + 1] * wb[4] + R[3 * i + 2] * wb[5];
     }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) { Fa[i] += Fs[0][i]; Fb2[i] += Fs[1][i]; }
     const f2 F[3] = {f2{Fa[0], Fb2[0]}, f2{Fa[1], Fb2[1]}, f2{Fa[2], Fb2[2]}};
     // the ABA below solves for accelerations relative to free fall (gravity as a base
     // acceleration), so the added mass would respond to a - g: the force it sees is F - Mp g
@@ -2028,7 +2083,8 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     for (int i = 0; i < 3; ++i)
       Fd[i] = F[i] - (f2{Ma[s3i(i, 0)], Mb[s3i(i, 0)]} * g[0] + f2{Ma[s3i(i, 1)], Mb[s3i(i, 1)]} * g[1] +
                       f2{Ma[s3i(i, 2)], Mb[s3i(i, 2)]} * g[2]);
-    // body-frame force f = R^T Fd and moment lp x f
+    // body-frame force f = R^T Fd and moment lp x f; the own primitive's self-contact wrench (R^T Fo, R^T Mo) joins
+    // the x half (its link)
     f2 f6[6];
 #pragma unroll
     for (int j = 0; j < 3; ++j) f6[3 + j] = Rs[j] * Fd[0] + Rs[3 + j] * Fd[1] + Rs[6 + j] * Fd[2];
@@ -2036,8 +2092,14 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     f6[1] = lp[2] * f6[3] - lp[0] * f6[5];
     f6[2] = lp[0] * f6[4] - lp[1] * f6[3];
 #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      f6[j].x += Rs[j].x * Mo[0] + Rs[3 + j].x * Mo[1] + Rs[6 + j].x * Mo[2];
+      f6[3 + j].x += Rs[j].x * Fo[0] + Rs[3 + j].x * Fo[1] + Rs[6 + j].x * Fo[2];
+    }
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
-      fleg[i] = f6[i].x + (even ? f6[i].y : 0.0f);
+      fx[i] = f6[i].x;
+      fy[i] = even ? f6[i].y : 0.0f;
       fbase[i] = (even ? 0.0f : f6[i].y) + wb[i];
     }
 #pragma unroll
@@ -2067,7 +2129,6 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       SM[3 + j] = lp[2] * M[j] - lp[0] * M[6 + j];
       SM[6 + j] = lp[0] * M[3 + j] - lp[1] * M[j];
     }
-    // (S M) S^T: element (i, j) = (S M)_i . S_j row, S_j row = (lp x e)_j -> -(row i of SM) x lp
     const int II[6] = {0, 0, 0, 1, 1, 2}, JJ[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -2082,7 +2143,8 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     for (int i = 0; i < 9; ++i) { cin[0].b[i] = SM[i].x; cin[1].b[i] = SM[i].y; }
   }
 #else  // ablation build only: no contacts
-  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)hip_r; (void)hip_y0; (void)hip_y1; (void)C; (void)T; (void)Rl; (void)pl; (void)vl;
+  (void)th; (void)foot_r; (void)thigh_r; (void)calf_r; (void)hip_r; (void)hip_y0; (void)hip_y1; (void)C; (void)T;
+  (void)Rs; (void)ps; (void)vs; (void)pth; (void)pkn; (void)pft;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
 #pragma unroll
@@ -2090,37 +2152,64 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
 #pragma unroll
     for (int i = 0; i < 9; ++i) cin[k].b[i] = 0.0f;
   }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { fx[i] = 0.0f; fy[i] = 0.0f; fbase[i] = 0.0f; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Fpt[i] = f2{0.0f, 0.0f};
 #endif
-  // the lane's contributions per body (thigh, calf, base), then summed over the leg's roles
-  SIP ci_th, ci_ca, ci_bs;
+  // the lane's contributions per body, summed over the leg's roles: thigh (rows 0-1: role 0's halves), calf (rows
+  // 2-3: role 2's halves and role 3's foot) in one pair reduction; hip (role 1's x half) and the trunk (odd rows'
+  // y halves, the box reactions) in a second
+  SIP ci_th, ci_ca, ci_hp, ci_bs;
   {
-    float lg[6 + 21], bs[6 + 21], th6[6 + 21], ca6[6 + 21];
+    const bool hip_lane = role == 1;
+    auto term = [&](int h, int k) -> float {  // value k of the lane's half h: the wrench (6), then the 21 inertia terms
+      if (k < 6) return h == 0 ? fx[k] : fy[k];
+      const int m = k - 6;
+      return m < 12 ? cin[h].ac[m >> 1][m & 1] : cin[h].b[m - 12];
+    };
+    {  // thigh (rows 0-1) and calf (rows 2-3)
+      float lg[6 + 21], th6[6 + 21], ca6[6 + 21];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) { lg[i] = fleg[i]; bs[i] = fbase[i]; }
+      for (int k = 0; k < 27; ++k) lg[k] = (hip_lane ? 0.0f : term(0, k)) + (even ? term(1, k) : 0.0f);
+      pairsum_rows_n<6 + 21>(lg, th6, ca6);
 #pragma unroll
-    for (int k = 0; k < 21; ++k) {
-      const float x = k < 12 ? cin[0].ac[k >> 1][k & 1] : cin[0].b[k - 12];
-      const float y = k < 12 ? cin[1].ac[k >> 1][k & 1] : cin[1].b[k - 12];
-      lg[6 + k] = x + (even ? y : 0.0f);  // thigh on rows 0-1, calf on rows 2-3
-      bs[6 + k] = even ? 0.0f : y;        // this leg's trunk corners
+      for (int i = 0; i < 3; ++i) {
+        pAp[1][i] -= f2{th6[i], th6[3 + i]};
+        pAp[2][i] -= f2{ca6[i], ca6[3 + i]};
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        ci_th.ac[k] = f2{th6[6 + 2 * k], th6[6 + 2 * k + 1]};
+        ci_ca.ac[k] = f2{ca6[6 + 2 * k], ca6[6 + 2 * k + 1]};
+      }
+#pragma unroll
+      for (int i = 0; i < 9; ++i) { ci_th.b[i] = th6[18 + i]; ci_ca.b[i] = ca6[18 + i]; }
     }
-    pairsum_rows_n<6 + 21>(lg, th6, ca6);
-    rowsum4_n<6 + 21>(bs);
+    {  // the hip capsule (row 1's x half): the rows 0-1 sum of a value that only row 1 holds
+      float hp[6 + 21], lo[6 + 21], hi[6 + 21];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      pAp[1][i] -= f2{th6[i], th6[3 + i]};
-      pAp[2][i] -= f2{ca6[i], ca6[3 + i]};
+      for (int k = 0; k < 27; ++k) hp[k] = hip_lane ? term(0, k) : 0.0f;
+      pairsum_rows_n<6 + 21>(hp, lo, hi);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pAp[0][i] -= f2{lo[i], lo[3 + i]};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) ci_hp.ac[k] = f2{lo[6 + 2 * k], lo[6 + 2 * k + 1]};
+#pragma unroll
+      for (int i = 0; i < 9; ++i) ci_hp.b[i] = lo[18 + i];
     }
+    {  // the trunk: this leg's corners (odd rows' y halves) and the box reactions
+      float bs[6 + 21];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) fbase[i] = bs[i];
+      for (int k = 0; k < 27; ++k) bs[k] = k < 6 ? fbase[k] : (even ? 0.0f : term(1, k));
+      rowsum4_n<6 + 21>(bs);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      ci_th.ac[k] = f2{th6[6 + 2 * k], th6[6 + 2 * k + 1]};
-      ci_ca.ac[k] = f2{ca6[6 + 2 * k], ca6[6 + 2 * k + 1]};
-      ci_bs.ac[k] = f2{bs[6 + 2 * k], bs[6 + 2 * k + 1]};
+      for (int i = 0; i < 6; ++i) fbase[i] = bs[i];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) ci_bs.ac[k] = f2{bs[6 + 2 * k], bs[6 + 2 * k + 1]};
+#pragma unroll
+      for (int i = 0; i < 9; ++i) ci_bs.b[i] = bs[18 + i];
     }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) { ci_th.b[i] = th6[18 + i]; ci_ca.b[i] = ca6[18 + i]; ci_bs.b[i] = bs[18 + i]; }
   }
   MARK(leg_kin_contacts_done);
   // ---- backward pass calf -> hip (articulated inertias with the contact added masses, bias
@@ -2173,19 +2262,9 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       if (j > 0) {
         rigid_sip(LC + 10 * (j - 1), 1.0f, IA);
         sip_add(IA, It);
-        if (j == 2) sip_add(IA, ci_th);  // the thigh's contact added masses
+        sip_add(IA, j == 2 ? ci_th : ci_hp);  // the thigh's / the hip capsule's contact added masses
 #pragma unroll
         for (int i = 0; i < 3; ++i) pAp[j - 1][i] += pt[i];
-#ifndef GO1_ABL_NO_CONTACT
-#ifndef GO1_ABL_NO_HIP  // ablation build only: no hip capsules
-        if (j == 1) {  // the hip capsule's contact, on the hip's inertia and bias force
-          MARK(hip_begin);
-          hip_contact(T, C, R, S.pos, vbp, origin, cs[0][0], cs[0][1], S.qd[0], msy * f2{hip_y0, hip_y1}, hip_r, h,
-                      g, role, IA, pAp[0], Fhip);
-          MARK(hip_done);
-        }
-#endif
-#endif
       } else {
         Ip = It;
         sip_add(Ip, ci_bs);  // this leg's trunk corners: summed over the legs with the hips below
@@ -2198,17 +2277,17 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   // ---- the trunk faces (face_scan / face_force): the vertices once per control step, the force every sim step
   f2 wface[3] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
   float Fface[3] = {0.0f, 0.0f, 0.0f};
+#ifdef GO1_ABL_NO_FACES  // ablation build only: no trunk faces
+  if (false) {
+#else
   if (T.patch) {  // the tunnel; on the plane the corners are the faces' deepest points
-    // the chosen vertices live in the env's LDS scratch across the control step (not in registers)
-    int* fsel = reinterpret_cast<int*>(self_sc + FACE_SEL_OFF);
-    if (face_scan_now) {
-      int sel[2];
-      face_scan(T, R, S.pos, th, 4 * role + leg, sel);
-      if (role == 0 && leg == 0) { fsel[0] = sel[0]; fsel[1] = sel[1]; }
-    }
+#endif
+    // the vertices chosen at the control step's first sim step (at the top of phys_substep) from the env's LDS scratch
+    const int* fsel = reinterpret_cast<const int*>(self_sc + FACE_SEL_OFF);
     const int sel[2] = {fsel[0], fsel[1]};
     face_force(T, C, R, S.pos, vb, th, sel, wface, Fface);
   }
+  MARK(faces_done);
   // ---- base: rigid inertia + quad sum of the four legs and the trunk corners
   const float* bb = model;
   const float mscale = (bb[0] + payload) * frcp(bb[0]);
@@ -2315,36 +2394,36 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
   (void)cf_out;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    cf_raw[i] = Fpt[i].x;
+    cf_raw[i] = Fpt[i].x + Fo[i];
     cf_raw[3 + i] = Fpt[i].y;
-    cf_raw[6 + i] += Fhip[i];
-    cf_raw[9 + i] = Fbs[i] + (role == 0 && leg == 0 ? Fface[i] : 0.0f);  // summed over the env's lanes (cf_sum)
+    cf_raw[6 + i] = Fbs[i] + (role == 0 && leg == 0 ? Fface[i] : 0.0f);  // summed over the env's lanes (cf_sum)
   }
 }
 
-// reported contact forces from the last sub-step's per-lane values: thigh, calf, foot of
-// the lane's leg (role sums), the base (role and leg sums) and the leg's hip
+// reported contact forces from the last sub-step's per-lane values: thigh, calf, foot and hip of the lane's leg
+// (role sums), the base (role and leg sums).  cf_raw: world forces of the lane's x half (with its primitive's
+// self-contact force) and y half -- rows 0 (thigh, thigh), 1 (hip, corner), 2 (calf, calf), 3 (foot, corner) --
+// then the trunk's self-collision reaction and faces
+#define CF_RAW 9
 __device__ __forceinline__ void cf_sum(const float* cf_raw, int role, float* cf_leg, float* cf_base, float* cf_hip) {
-  // cf_raw: world forces of the lane's two points (x, y); rows 0 (thigh, thigh), 1 (thigh, corner),
-  // 2 (calf, calf), 3 (foot, corner); then the leg's hip (already whole on every role)
-  float v[12];
+  float v[15];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float x = cf_raw[i], y = cf_raw[3 + i];
-    v[i] = role == 0 ? x + y : (role == 1 ? x : 0.0f);  // thigh
-    v[3 + i] = role == 2 ? x + y : 0.0f;                 // calf
-    v[6 + i] = role == 3 ? x : 0.0f;                     // foot
-    v[9 + i] = ((role & 1) ? y : 0.0f) + cf_raw[9 + i];  // trunk corners, self-collision reactions
+    v[i] = role == 0 ? x + y : 0.0f;                      // thigh
+    v[3 + i] = role == 2 ? x + y : 0.0f;                  // calf
+    v[6 + i] = role == 3 ? x : 0.0f;                      // foot
+    v[9 + i] = role == 1 ? x : 0.0f;                      // hip
+    v[12 + i] = ((role & 1) ? y : 0.0f) + cf_raw[6 + i];  // trunk corners, self-collision reactions, faces
   }
-  rowsum4_n<12>(v);
+  rowsum4_n<15>(v);
 #pragma unroll
   for (int i = 0; i < 9; ++i) cf_leg[i] = v[i];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    cf_base[i] = qsum(v[9 + i]);
-    cf_hip[i] = cf_raw[6 + i];
+    cf_base[i] = qsum(v[12 + i]);
+    cf_hip[i] = v[9 + i];
   }
 }
 
 #pragma clang fp contract(off)
-

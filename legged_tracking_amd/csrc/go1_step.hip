@@ -175,6 +175,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
   MlpFrag F;
   mlp_load(c_gen->actuator, lane, F);  // lane-indexed: generic pointer
+  __shared__ float s_mlp[MLP_PARK_FLOATS * 64];  // the fragments across the sub-step loop (mlp_park)
+  mlp_park(F, s_mlp, lane);
   const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset, CI(u_per_env)};
   // the previous step's extras["time_outs"] rebinding, for this wave's envs (flags of the
   // previous launch are complete now), and the flag the next launch will set is cleared
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // (:973), so sub-step s reads the slot s+1 of the incoming ring and the ring
   // leaves the step as [old4, old5, old6, scaled x 4].
   float torque[3], tgt[3];
-  float cf_raw[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
+  float cf_raw[CF_RAW] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
   for (int sub = 0; sub < dec; ++sub) {
     MARK(sub_begin);
     // _compute_torques (:957-996)
@@ -403,7 +405,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int j = 0; j < 3; ++j) tq[j] = 0.0f * (b0[j] + b1v[j]);  // ablation build only: no actuator net
 #else
-      mlp_group3(F, b0, b1v, tq);
+      {
+        MlpFrag Fs;
+        mlp_unpark(Fs, s_mlp, lane);
+        mlp_group3(Fs, b0, b1v, tq);
+      }
 #endif
 #ifdef GO1_ABL_NO_MLP
 #pragma unroll
@@ -1209,6 +1215,10 @@ int go1_create(const go1_config* cfg, go1_handle** out) {
   if (cfg->n_envs <= 0) return fail(GO1_E_ARG, "go1_create: n_envs must be > 0");
   if (cfg->decimation <= 0 || cfg->n_internal <= 0) return fail(GO1_E_ARG, "go1_create: decimation/n_internal");
   if (cfg->terrain_kind == 1 && (cfg->hf_nx < 2 || cfg->hf_ny < 2)) return fail(GO1_E_ARG, "go1_create: tile shape");
+  // the capsules' deepest-point search (go1_device.h seg_deepest) takes at most 3 grid lines per direction and 4 cell
+  // diagonals per half link (0.1065 m): cells of at least 0.05 m
+  if (cfg->terrain_kind == 1 && !(cfg->horizontal_scale >= 0.0499f))
+    return fail(GO1_E_ARG, "go1_create: horizontal_scale < 0.05 m is not supported by the capsule contact search");
   if (cfg->rand_interval <= 0) return fail(GO1_E_ARG, "go1_create: rand_interval");
   if (cfg->n_envs % EPB != 0)
     return fail(GO1_E_ARG, "go1_create: n_envs must be a multiple of 16 (one wave = 16 envs x 4 legs)");

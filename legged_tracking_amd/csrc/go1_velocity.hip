@@ -197,6 +197,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int e = blockIdx.x * SEPB + el;  // n % 16 == 0 (go1_vel_create)
   MlpFrag F;
   mlp_load(c_gen->actuator, lane, F);
+  __shared__ float s_mlp[MLP_PARK_FLOATS * 64];  // the fragments across the sub-step loop (mlp_park)
+  mlp_park(F, s_mlp, lane);
   const Rng rng = {A.uniforms, A.rng_seed, A.rng_step, e, e + c->env_id_offset, GO1_VEL_U_PER_ENV};
   const size_t d0 = (size_t)e * NDOF + leg * 3;
   const int dec = c->decimation;
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // ---------------- decimation loop (:76-82): lag ring pushed per sim step (:940-942)
   float torque[3], tgt[3];
-  float cf_raw[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
+  float cf_raw[CF_RAW] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, cf_leg[9], cf_base[3], cf_hip[3];
   for (int sub = 0; sub < dec; ++sub) {
     {
       const int m = 6 - sub;
@@ -293,7 +295,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         b0[j] = sel4(lq, y[0], y[1], y[2], y[3]);
         b1v[j] = sel4(lq, y[4], y[5], 0.0f, 0.0f);
       }
-      mlp_group3(F, b0, b1v, tq);
+      {
+        MlpFrag Fs;
+        mlp_unpark(Fs, s_mlp, lane);
+        mlp_group3(Fs, b0, b1v, tq);
+      }
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         eh[1][j] = eh[0][j];

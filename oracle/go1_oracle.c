@@ -24,6 +24,7 @@
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).
  */
 #include <math.h>
+#include <limits.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -370,7 +371,14 @@ static void quat_to_R(const real* q, real R[3][3]) {
   R[2][0] = 2 * (x * z - y * w); R[2][1] = 2 * (y * z + x * w); R[2][2] = 1 - 2 * (x * x + y * y);
 }
 
-/* ---- terrain queries (tile layer 0 ceiling, 1 floor), bilinear at pixel corners */
+/* ---- terrain queries (tile layer 0 ceiling, 1 floor).  Round 6: the surface is the heightfield's triangle mesh, as
+ * the reference collides with it (mesh_type 'trimesh', legged_robot_trajectory_tracking.py:1450-1480; tunnel.py:139-147
+ * builds it with isaacgym terrain_utils.convert_heightfield_to_trimesh): every cell (i, j) split along its
+ * (i, j) - (i + 1, j + 1) diagonal into the triangles (i, j), (i + 1, j), (i + 1, j + 1) ("lower", a >= b) and (i, j),
+ * (i + 1, j + 1), (i, j + 1) ("upper"), a = u - i, b = v - j.  (convert_heightfield_to_trimesh's slope threshold,
+ * which moves vertices sideways under steep steps, is not modelled: the surface stays on the grid.)  Rounds 1-5 used the
+ * bilinear patch; a triangle surface is piecewise linear along any segment, which makes a capsule's deepest point a
+ * finite candidate set (seg_deepest). */
 typedef struct {
   const float* tile; /* (2, nx, ny) or NULL for plane */
   int nx, ny;
@@ -385,22 +393,38 @@ static real tile_at(const TerrainView* T, int layer, int i, int j) {
   return (real)T->tile[((size_t)layer * T->nx + i) * T->ny + j];
 }
 
-/* height and gradient of layer at world (x, y) */
-static void height_query(const TerrainView* T, int layer, real x, real y, real* h, real* gx, real* gy) {
+/* height and gradient of layer at world (x, y) on triangle `up` (0 lower, 1 upper) of cell (ci, cj): the cell and
+ * triangle a capsule's deepest-point search found the point on (seg_deepest), so that at an edge of the mesh (a ridge,
+ * a spike's apex) the normal is the one of the triangle chosen there, not whichever side floor() of a rounded
+ * coordinate lands on; tri_locate gives them for a point query */
+static void tri_query(const TerrainView* T, int layer, real x, real y, int ci, int cj, int up, real* h, real* gx,
+                      real* gy) {
   if (!T->tile) {
     *h = layer == 1 ? 0.0 : 1e9;
     *gx = *gy = 0.0;
     return;
   }
   real u = fmin(fmax((x - T->ox) / T->hs, -4.0), T->nx + 4.0), v = fmin(fmax((y - T->oy) / T->hs, -4.0), T->ny + 4.0);
+  real a = u - ci, b = v - cj;
+  real h00 = tile_at(T, layer, ci, cj), h10 = tile_at(T, layer, ci + 1, cj);
+  real h01 = tile_at(T, layer, ci, cj + 1), h11 = tile_at(T, layer, ci + 1, cj + 1);
+  real da = up ? h11 - h01 : h10 - h00, db = up ? h01 - h00 : h11 - h10;
+  *h = h00 + a * da + b * db;
+  *gx = da / T->hs;
+  *gy = db / T->hs;
+}
+static void tri_locate(const TerrainView* T, real x, real y, int* cell) {
+  real u = fmin(fmax((x - T->ox) / T->hs, -4.0), T->nx + 4.0), v = fmin(fmax((y - T->oy) / T->hs, -4.0), T->ny + 4.0);
   real fu = floor(u), fv = floor(v);
-  int i = (int)fu, j = (int)fv;
-  real a = u - fu, b = v - fv;
-  real h00 = tile_at(T, layer, i, j), h10 = tile_at(T, layer, i + 1, j);
-  real h01 = tile_at(T, layer, i, j + 1), h11 = tile_at(T, layer, i + 1, j + 1);
-  *h = (1 - a) * (1 - b) * h00 + a * (1 - b) * h10 + (1 - a) * b * h01 + a * b * h11;
-  *gx = ((1 - b) * (h10 - h00) + b * (h11 - h01)) / T->hs;
-  *gy = ((1 - a) * (h01 - h00) + a * (h11 - h10)) / T->hs;
+  cell[0] = (int)fu;
+  cell[1] = (int)fv;
+  cell[2] = (u - fu) < (v - fv);
+}
+/* height and gradient of layer at world (x, y): the triangle under the point */
+static void height_query(const TerrainView* T, int layer, real x, real y, real* h, real* gx, real* gy) {
+  int cell[3] = {0, 0, 0};
+  if (T->tile) tri_locate(T, x, y, cell);
+  tri_query(T, layer, x, y, cell[0], cell[1], cell[2], h, gx, gy);
 }
 
 typedef struct {
@@ -422,12 +446,13 @@ void go1o_set_implicit_contact(int on) { g_implicit_contact = on; }
 
 /* penalty contact of a sphere (centre p, velocity pv, radius r) against floor and
  * ceiling; returns world force F (and, implicit option, adds the point's added mass to Mp) */
-static void sphere_contact_im(const TerrainView* T, const ContactParams* C, const real* p, const real* pv, real r,
-                              real* F, real h, real Mp[3][3]) {
+static void sphere_contact_im_cell(const TerrainView* T, const ContactParams* C, const real* p, const real* pv, real r,
+                                   real* F, real h, real Mp[3][3], const int* cell) {
   F[0] = F[1] = F[2] = 0.0;
   for (int layer = 1; layer >= 0; --layer) {
     real hh, gx, gy;
-    height_query(T, layer, p[0], p[1], &hh, &gx, &gy);
+    if (cell) tri_query(T, layer, p[0], p[1], cell[0], cell[1], cell[2], &hh, &gx, &gy);
+    else height_query(T, layer, p[0], p[1], &hh, &gx, &gy);
     real n[3], dv;
     if (layer == 1) {
       dv = hh + r - p[2];
@@ -457,6 +482,10 @@ static void sphere_contact_im(const TerrainView* T, const ContactParams* C, cons
       for (int j = 0; j < 3; ++j) Mp[i][j] += (cn - cd) * n[i] * n[j] + (i == j ? cd : 0.0);
     }
   }
+}
+static void sphere_contact_im(const TerrainView* T, const ContactParams* C, const real* p, const real* pv, real r,
+                              real* F, real h, real Mp[3][3]) {
+  sphere_contact_im_cell(T, C, p, pv, r, F, h, Mp, NULL);
 }
 
 /* the added mass Mp (world, at local point lp of a link with rotation Rb) as a spatial inertia
@@ -522,23 +551,200 @@ static void sphere_contact(const TerrainView* T, const ContactParams* C, const r
   }
 }
 
-/* Contact points per leg, in the frame of their link:
- *   thigh: (0,0,-0.071), (0,0,-0.142), knee (0,0,-0.213)   radius thigh_r
- *   calf : (0,0,-0.071), (0,0,-0.142)                     radius calf_r
- *   foot : foot offset (calf frame)                        radius foot_r
- *   hip  : (0, +-hip_y[0], 0), (0, +-hip_y[1], 0)            radius hip_r (the ends of the hip
- *          capsule's segment, go1.urdf:106-111 as a capsule per replace_cylinder_with_capsule;
- *          the sign is the leg's side)
- * Trunk: the 8 corners of the collision box (radius 0). */
-#define N_THIGH_PTS 3
-#define N_CALF_PTS 2
-static const real THIGH_PTS_Z[N_THIGH_PTS] = {-0.071, -0.142, -0.213};
-static const real CALF_PTS_Z[N_CALF_PTS] = {-0.071, -0.142};
+/* Collision geometry per leg (round 6: capsules over the links' full length, no sphere chains), in the frame of
+ * their link:
+ *   hip  : capsule, segment (0, +-hip_y[0], 0) .. (0, +-hip_y[1], 0), radius hip_r (go1.urdf:106-111 as a capsule per
+ *          replace_cylinder_with_capsule; the sign is the leg's side)
+ *   thigh: capsule, segment (0,0,0) .. the knee (the calf joint's origin, (0,0,-0.213)), radius thigh_r (the
+ *          0.213 x 0.0245 x 0.034 box of go1.urdf:148-153 as the capsule of its narrow half width)
+ *   calf : capsule, segment (0,0,0) .. the foot offset (0,0,-0.213), radius calf_r (go1.urdf:176-181)
+ *   foot : sphere at the foot offset (calf frame), radius foot_r (go1.urdf:201-205)
+ * Trunk: the 8 corners of the collision box (radius 0) and its faces (face_scan).
+ * Against the heightfields every capsule acts at the deepest point of its segment (seg_deepest): the hip capsule
+ * at one point, the thigh and calf at one point per half (each half walked from its outer end, so a link lying
+ * flat is carried at both ends). */
+
+/* The deepest point of the segment A -> B (world) of a capsule of radius r against the floor and ceiling meshes
+ * (go1_device.h seg_deepest2 is the f32 restatement): the t in [0, 1] that maximises the vertical gap of either layer,
+ * floor h_f(x, y) + r - z and ceiling z + r - h_c(x, y).  Both meshes are triangles over the grid (tri_query), so
+ * along the segment the gaps are piecewise linear in t and their maximum lies at an end or where the segment's (x, y)
+ * projection crosses a mesh edge: a grid line u = k, v = k or a cell diagonal u - v = k.  The candidates are exactly
+ * those (on an edge the height is the interpolation of its two vertices), so the search is exact and needs no
+ * walk; each candidate carries the cell and triangle on the segment's incoming side of the edge, whose plane the
+ * contact then uses.  A candidate's key is its deeper layer's gap quantised to SEG_Q, ties to the smaller t (the
+ * segment's first end: the halves of the thigh and calf start at their outer ends, so a link lying flat is carried at
+ * both), so the f32 kernel and this f64 restatement choose the same point.  On the plane the lower end (ties: A).
+ * phys_substep searches once per control step and holds t for the control step's other sim steps (the kernel's
+ * cadence, as for the trunk faces). */
+#define SEG_Q 1.0e-5
+static long seg_quant(real g) { return (long)floor(fmin(fmax(g, -1.0), 1.0) / SEG_Q); }
+typedef struct {
+  long key; /* the best candidate's key: quantised gap (the deeper layer) x 4096 + the earlier t (4095 - 4095 t) */
+  real t;
+  int c[3];
+} SegBest;
+static void seg_offer(SegBest* sb, const real* h, real z, real r, real t, int ci, int cj, int up) {
+  long qf = seg_quant((h[0] - z) + r), qc = seg_quant((z - h[1]) + r);
+  long key = (qf > qc ? qf : qc) * 4096 + (4095 - (long)floor(t * 4095.0));
+  if (key > sb->key) { /* an equal key (a vertex on several edges) keeps the first offer */
+    sb->key = key;
+    sb->t = t;
+    sb->c[0] = ci; sb->c[1] = cj; sb->c[2] = up;
+  }
+}
+static real seg_deepest(const TerrainView* T, const real* A, const real* B, real r, int* cell) {
+  cell[0] = cell[1] = cell[2] = 0;
+  if (!T->tile) return seg_quant(r - B[2]) > seg_quant(r - A[2]) ? 1.0 : 0.0;
+  real uA = fmin(fmax((A[0] - T->ox) / T->hs, -4.0), T->nx + 4.0), vA = fmin(fmax((A[1] - T->oy) / T->hs, -4.0), T->ny + 4.0);
+  real uB = fmin(fmax((B[0] - T->ox) / T->hs, -4.0), T->nx + 4.0), vB = fmin(fmax((B[1] - T->oy) / T->hs, -4.0), T->ny + 4.0);
+  real du = uB - uA, dv = vB - vA, dw = du - dv, dz = B[2] - A[2];
+  SegBest sb = {LONG_MIN, 0.0, {0, 0, 0}};
+  real h[2];
+  /* the ends */
+  for (int e = 0; e < 2; ++e) {
+    const real* P = e ? B : A;
+    int c[3];
+    real gx, gy;
+    tri_locate(T, P[0], P[1], c);
+    tri_query(T, 1, P[0], P[1], c[0], c[1], c[2], &h[0], &gx, &gy);
+    tri_query(T, 0, P[0], P[1], c[0], c[1], c[2], &h[1], &gx, &gy);
+    seg_offer(&sb, h, P[2], r, (real)e, c[0], c[1], c[2]);
+  }
+  /* grid lines u = k */
+  for (int k = (int)floor(fmin(uA, uB)) + 1; k < fmax(uA, uB); ++k) {
+    real t = (k - uA) / du, v = vA + dv * t;
+    int j = (int)floor(v), i = du > 0.0 ? k - 1 : k;
+    real b = v - j;
+    for (int L = 0; L < 2; ++L) {
+      int layer = L == 0 ? 1 : 0;
+      h[L] = tile_at(T, layer, k, j) + b * (tile_at(T, layer, k, j + 1) - tile_at(T, layer, k, j));
+    }
+    seg_offer(&sb, h, A[2] + dz * t, r, t, i, j, (real)(k - i) < b);
+  }
+  /* grid lines v = k */
+  for (int k = (int)floor(fmin(vA, vB)) + 1; k < fmax(vA, vB); ++k) {
+    real t = (k - vA) / dv, u = uA + du * t;
+    int i = (int)floor(u), j = dv > 0.0 ? k - 1 : k;
+    real a = u - i;
+    for (int L = 0; L < 2; ++L) {
+      int layer = L == 0 ? 1 : 0;
+      h[L] = tile_at(T, layer, i, k) + a * (tile_at(T, layer, i + 1, k) - tile_at(T, layer, i, k));
+    }
+    seg_offer(&sb, h, A[2] + dz * t, r, t, i, j, a < (real)(k - j));
+  }
+  /* cell diagonals u - v = k (the point (i + a, j + a) of cell (i, j), i - j = k) */
+  real wA = uA - vA, wB = uB - vB;
+  for (int k = (int)floor(fmin(wA, wB)) + 1; k < fmax(wA, wB); ++k) {
+    real t = (k - wA) / dw, u = uA + du * t;
+    int i = (int)floor(u), j = i - k;
+    real a = u - i;
+    for (int L = 0; L < 2; ++L) {
+      int layer = L == 0 ? 1 : 0;
+      h[L] = tile_at(T, layer, i, j) + a * (tile_at(T, layer, i + 1, j + 1) - tile_at(T, layer, i, j));
+    }
+    seg_offer(&sb, h, A[2] + dz * t, r, t, i, j, dw > 0.0); /* incoming: u - v < k, i.e. a < b: upper */
+  }
+  for (int m = 0; m < 3; ++m) cell[m] = sb.c[m];
+  return sb.t;
+}
+
+/* closest points of the segments P0 -> P1 and Q0 -> Q1: parameters s (on P) and t (on Q) in [0, 1] (Ericson,
+ * Real-Time Collision Detection 5.1.9; a degenerate segment (a point) has s = 0 or t = 0).  The unclamped s of the two
+ * lines, (b f - c e) / (a e - b^2), is formed without cancellation as (n . (d2 x r)) / (n . n), n = d1 x d2 (Lagrange's
+ * identity): for nearly parallel links a e - b^2 cancels to a few f32 ulps, and the f32 kernel would otherwise
+ * place the closest points anywhere along them. */
+static void seg_seg_closest(const real* P0, const real* P1, const real* Q0, const real* Q1, real* s_out, real* t_out) {
+  real d1[3], d2[3], r[3], n[3], m[3];
+  for (int i = 0; i < 3; ++i) { d1[i] = P1[i] - P0[i]; d2[i] = Q1[i] - Q0[i]; r[i] = P0[i] - Q0[i]; }
+  real a = d1[0] * d1[0] + d1[1] * d1[1] + d1[2] * d1[2], e = d2[0] * d2[0] + d2[1] * d2[1] + d2[2] * d2[2];
+  real f = d2[0] * r[0] + d2[1] * r[1] + d2[2] * r[2];
+  real s = 0.0, t = 0.0;
+  if (a <= 1e-12 && e <= 1e-12) {
+    s = t = 0.0;
+  } else if (a <= 1e-12) {
+    t = fmin(fmax(f / e, 0.0), 1.0);
+  } else {
+    real c = d1[0] * r[0] + d1[1] * r[1] + d1[2] * r[2];
+    if (e <= 1e-12) {
+      s = fmin(fmax(-c / a, 0.0), 1.0);
+    } else {
+      real b = d1[0] * d2[0] + d1[1] * d2[1] + d1[2] * d2[2];
+      cross3(d1, d2, n);
+      cross3(d2, r, m);
+      real den = n[0] * n[0] + n[1] * n[1] + n[2] * n[2], num = n[0] * m[0] + n[1] * m[1] + n[2] * m[2];
+      s = den > 1e-10 * a * e ? fmin(fmax(num / den, 0.0), 1.0) : 0.0;
+      t = (b * s + f) / e;
+      if (t < 0.0) { t = 0.0; s = fmin(fmax(-c / a, 0.0), 1.0); }
+      else if (t > 1.0) { t = 1.0; s = fmin(fmax((b - c) / a, 0.0), 1.0); }
+    }
+  }
+  *s_out = s;
+  *t_out = t;
+}
+
+/* exposed for tests/test_capsules.py: the deepest point of a segment against one (2, nx, ny) tile at the origin,
+ * and the closest points of two segments */
+double go1o_seg_deepest(const float* tile, int nx, int ny, double hs, const double* A, const double* B, double r) {
+  TerrainView T = {tile, nx, ny, 0.0, 0.0, (real)hs};
+  real a[3] = {A[0], A[1], A[2]}, b[3] = {B[0], B[1], B[2]};
+  int cell[3];
+  return (double)seg_deepest(&T, a, b, (real)r, cell);
+}
+void go1o_seg_closest(const double* P0, const double* P1, const double* Q0, const double* Q1, double* st) {
+  real p0[3], p1[3], q0[3], q1[3], s, t;
+  for (int i = 0; i < 3; ++i) { p0[i] = P0[i]; p1[i] = P1[i]; q0[i] = Q0[i]; q1[i] = Q1[i]; }
+  seg_seg_closest(p0, p1, q0, q1, &s, &t);
+  st[0] = s;
+  st[1] = t;
+}
+
+/* signed distance of the base-frame point c to the trunk box (half extents th) */
+static real box_sdf(const real* c, const real* th) {
+  real q[3], o = 0.0, in = -1e30;
+  for (int i = 0; i < 3; ++i) {
+    q[i] = fabs(c[i]) - th[i];
+    o += q[i] > 0.0 ? q[i] * q[i] : 0.0;
+    in = fmax(in, q[i]);
+  }
+  return sqrt(o) + fmin(in, 0.0);
+}
+/* the point of the segment P0 -> P1 (world) nearest the trunk box (deepest inside it): the box's signed distance is
+ * convex, so along the segment it is a convex function of t, minimised by golden-section search (SEG_GOLDEN
+ * steps, 0.618^32 of the segment ~ 0.04 um on a 0.213 m link; go1_device.h seg_box_t is the f32 restatement) */
+#define SEG_GOLDEN 32
+#define BOX_Q 1.0e-4
+static long box_quant(real d) { return (long)floor(fmin(fmax(d, -1.0), 1.0) / BOX_Q); }
+static real seg_box_t(const real* P0, const real* P1, real R[3][3], const real* pos, const real* th) {
+  real a0[3], d[3];
+  for (int i = 0; i < 3; ++i) {
+    a0[i] = R[0][i] * (P0[0] - pos[0]) + R[1][i] * (P0[1] - pos[1]) + R[2][i] * (P0[2] - pos[2]);
+    d[i] = R[0][i] * (P1[0] - P0[0]) + R[1][i] * (P1[1] - P0[1]) + R[2][i] * (P1[2] - P0[2]);
+  }
+  const real gr = 0.6180339887498949;
+  real lo = 0.0, hi = 1.0, x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), c[3];
+  for (int i = 0; i < 3; ++i) c[i] = a0[i] + x1 * d[i];
+  real f1 = box_sdf(c, th);
+  for (int i = 0; i < 3; ++i) c[i] = a0[i] + x2 * d[i];
+  real f2 = box_sdf(c, th);
+  for (int it = 0; it < SEG_GOLDEN; ++it) {
+    if (f1 <= f2) {
+      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
+      for (int i = 0; i < 3; ++i) c[i] = a0[i] + x1 * d[i];
+      f1 = box_sdf(c, th);
+    } else {
+      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
+      for (int i = 0; i < 3; ++i) c[i] = a0[i] + x2 * d[i];
+      f2 = box_sdf(c, th);
+    }
+  }
+  return 0.5 * (lo + hi);
+}
 
 typedef struct {
   real pos[3], quat[4], v[3], w[3];
   real q[NDOF], qd[NDOF];
   int face[2]; /* the trunk faces' contact vertices of the control step (face_scan), -1: none */
+  real seg_t[4][5]; /* per leg the capsules' deepest points of the control step (seg_deepest): hip, thigh x2, calf x2 */
 } PhysState;
 
 /* world pose/velocity of a point given body pose (Rb, pb) and body spatial velocity
@@ -563,16 +769,18 @@ static void point_force(real Rb[3][3], const real* lp, const real* F, real* fs) 
 }
 
 /* Self-collision (asset.self_collisions == 0, go1_crawling.py:44: Isaac Gym collides every pair of bodies that
- * no joint connects; go1_device.h self_narrow): spheres leg * 8 + s (s: thigh points 0-2, calf points 3-4, foot 5,
- * hip-capsule ends 6-7, the contact spheres of phys_substep); pairs: every sphere of leg la against every sphere
- * of leg lb (la < lb, 64 per leg pair), within a leg the links two joints apart (hip capsule vs calf and foot,
- * thigh vs foot: SELF_SAME_A / _B), and the thigh / calf / foot spheres against the trunk box (half extents
- * trunk_half about the base origin; the hip is the trunk's neighbour).  Explicit penalty springs
- * fn = ks pen - ds vn on the overlap, compressive only, no friction; the force on the first sphere of a pair is
- * computed, the other gets its negative, the trunk the box pairs' reaction. */
-#define SELF_NSAME 9
-static const int SELF_SAME_A[SELF_NSAME] = {6, 6, 6, 7, 7, 7, 0, 1, 2};
-static const int SELF_SAME_B[SELF_NSAME] = {3, 4, 5, 3, 4, 5, 5, 5, 5};
+ * no joint connects; go1_device.h self_narrow): the primitives 4 leg + k of the legs (k: 0 thigh capsule, 1 hip
+ * capsule, 2 calf capsule, 3 foot sphere; the collision geometry above); pairs: every primitive of leg la against
+ * every primitive of leg lb (la < lb, 16 per leg pair), within a leg the links two joints apart (hip capsule vs calf
+ * capsule and foot, thigh capsule vs foot: SELF_SAME_A / _B), and the thigh / calf capsules and the foot against
+ * the trunk box (half extents trunk_half about the base origin; the hip is the trunk's neighbour).  A pair acts at
+ * the closest points of its two segments (seg_seg_closest) as two spheres of the capsules' radii there; a capsule
+ * against the box at its point nearest the box (seg_box_t).  Explicit penalty springs fn = ks pen - ds vn on the
+ * overlap, compressive only, no friction; the force on the primitive of the lower index is computed, the other
+ * gets its negative at its own closest point, the trunk the box pairs' reaction. */
+#define SELF_NSAME 3
+static const int SELF_SAME_A[SELF_NSAME] = {1, 1, 0};
+static const int SELF_SAME_B[SELF_NSAME] = {2, 3, 3};
 static void self_sphere_force(const real* pa, const real* va, real ra, const real* pb, const real* vb, real rb,
                               real ks, real ds, real* F) {
   real d[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
@@ -602,10 +810,13 @@ static void self_box_force(const real* pa, const real* va, real r, real R[3][3],
     real dist = sqrt(dd);
     for (int i = 0; i < 3; ++i) nb[i] = d[i] / dist;
     pen = r - dist;
-  } else { /* centre inside: out through the nearest face, lowest axis on ties */
+  } else { /* centre inside: out through the nearest face, lowest axis on ties -- compared quantised to BOX_Q: the
+            * deepest point of a segment inside the box is often where two faces are equally near, and there the f32
+            * kernel and this f64 restatement must choose the same face */
     real m[3];
-    for (int i = 0; i < 3; ++i) m[i] = th[i] - fabs(c[i]);
-    int ax = (m[0] <= m[1] && m[0] <= m[2]) ? 0 : (m[1] <= m[2] ? 1 : 2);
+    long mq[3];
+    for (int i = 0; i < 3; ++i) { m[i] = th[i] - fabs(c[i]); mq[i] = box_quant(m[i]); }
+    int ax = (mq[0] <= mq[1] && mq[0] <= mq[2]) ? 0 : (mq[1] <= mq[2] ? 1 : 2);
     real sg = c[ax] >= 0.0 ? 1.0 : -1.0;
     for (int i = 0; i < 3; ++i) nb[i] = i == ax ? sg : 0.0;
     q[ax] = sg * th[ax];
@@ -626,33 +837,34 @@ static void self_box_force(const real* pa, const real* va, real r, real R[3][3],
 }
 
 /* The trunk box's faces against the heightfields (go1_device.h face_scan / face_force; go1.urdf:53-58,
- * tunnel_fn.py:99-163): once per control step the deepest grid vertex of the floor inside the bottom face's
- * footprint and of the ceiling inside the top face's, among the 10 x 8 vertices around the trunk centre (the
- * window's long side along the world axis nearer the trunk's x), depths compared quantised to 1e-5 m, ties to
- * the lowest window position; every sim step an explicit penalty force at the two vertices along the face
+ * tunnel_fn.py:99-163): once per control step, per face the grid vertex inside its footprint nearest to (or deepest
+ * in) the face -- the floor against the bottom face, the ceiling against the top -- among the 10 x 10 vertices around
+ * the trunk centre (offsets -4 .. +5 on both axes: they cover the footprint's +-0.166 m at any yaw, whatever the
+ * centre's position in its cell), signed depths from -FACE_SIGNED compared quantised to 1e-5 m, ties to the lowest
+ * window position; every sim step an explicit penalty force at the two vertices where they penetrate, along the face
  * normal (k depth - d vn, depth capped at the box height) with the regularised Coulomb friction of the point
  * contacts.  The GPU scans its LDS terrain patch (which holds the trunk's footprint), this restatement the tile
  * (both clamp at the tile's edges). */
 #define FACE_Q 1.0e-5
+#define FACE_W 10
+#define FACE_SIGNED 0.1
 static void face_scan(const TerrainView* T, real R[3][3], const real* pos, const real* th, int* sel) {
-  int xl = fabs(R[0][0]) >= fabs(R[1][0]);
   int ci = (int)floor(fmin(fmax(pos[0] / T->hs, -16000.0), 16000.0)), cj = (int)floor(fmin(fmax(pos[1] / T->hs, -16000.0), 16000.0));
   for (int hh = 0; hh < 2; ++hh) {
     int best = -1;
-    for (int v = 0; v < 80; ++v) {
-      int a = v % 10, b = v / 10;
-      int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+    for (int v = 0; v < FACE_W * FACE_W; ++v) {
+      int i = ci + v % FACE_W - 4, j = cj + v / FACE_W - 4;
       real d[3] = {i * T->hs - pos[0], j * T->hs - pos[1], tile_at(T, hh == 0 ? 1 : 0, i, j) - pos[2]}, c[3];
       for (int k = 0; k < 3; ++k) c[k] = R[0][k] * d[0] + R[1][k] * d[1] + R[2][k] * d[2];
       real pen = hh == 0 ? c[2] + th[2] : th[2] - c[2];
-      if (!(fabs(c[0]) <= th[0] && fabs(c[1]) <= th[1] && pen > 0.0)) continue;
-      int q = (int)fmin(pen / FACE_Q, 1e6);
+      if (!(fabs(c[0]) <= th[0] && fabs(c[1]) <= th[1] && pen > -FACE_SIGNED)) continue;
+      int q = (int)floor(fmin(pen + FACE_SIGNED, 10.0) / FACE_Q);
       int key = (q << 7) | (127 - v);
       if (key > best) best = key;
     }
     if (best < 0) { sel[hh] = -1; continue; }
-    int v = 127 - (best & 127), a = v % 10, b = v / 10;
-    int i = ci + (xl ? a - 4 : b - 3), j = cj + (xl ? b - 3 : a - 4);
+    int v = 127 - (best & 127);
+    int i = ci + v % FACE_W - 4, j = cj + v / FACE_W - 4;
     sel[hh] = ((i + 16384) << 16) | (j + 16384);
   }
 }
@@ -763,54 +975,87 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       memcpy(vp, vj[l][j], sizeof(vp));
     }
   }
-  /* self-collision forces on the thigh / calf / foot / hip-capsule spheres and the trunk's reaction wrench */
-  real Fself[32][3], wself[6] = {0, 0, 0, 0, 0, 0};
-  memset(Fself, 0, sizeof(Fself));
+  /* self-collision: body-frame wrenches on the legs' links (wsl[l][j], j = hip, thigh, calf), reported forces per
+   * body (cfs, the cf layout) and the trunk's reaction wrench */
+  real wsl[4][3][6], cfs[NB][3], wself[6] = {0, 0, 0, 0, 0, 0};
+  memset(wsl, 0, sizeof(wsl));
+  memset(cfs, 0, sizeof(cfs));
   if (cfg->self_stiffness > 0.0f) {
-    real SP[32][3], SV[32][3], SR[32];
+    /* primitive 4 l + k: link j, segment ends lp0 -> lp1 in the link frame, world ends P0 / P1, their velocities */
+    real SP[16][2][3], SV[16][2][3], SL[16][2][3], SR[16];
+    int SJ[16], SB[16];
     for (int l = 0; l < 4; ++l)
-      for (int s8 = 0; s8 < 8; ++s8) {
-        int j = s8 < 3 ? 1 : (s8 < 6 ? 2 : 0);
-        real lp[3] = {0, 0, 0};
-        if (s8 < 3) lp[2] = THIGH_PTS_Z[s8];
-        else if (s8 < 5) lp[2] = CALF_PTS_Z[s8 - 3];
-        else if (s8 == 5) { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
-        else lp[1] = ((l & 1) ? -1.0 : 1.0) * M->hip_y[s8 - 6];
-        point_kin(Rw_all[l][j], pw_all[l][j], vj[l][j], lp, SP[l * 8 + s8], SV[l * 8 + s8]);
-        SR[l * 8 + s8] = s8 < 3 ? M->thigh_r : (s8 < 5 ? M->calf_r : (s8 == 5 ? M->foot_r : M->hip_r));
+      for (int k = 0; k < 4; ++k) {
+        int j = k == 0 ? 1 : (k == 1 ? 0 : 2), p = 4 * l + k;
+        real lp[2][3] = {{0, 0, 0}, {0, 0, 0}};
+        const real sy = (l & 1) ? -1.0 : 1.0;
+        if (k == 0) { for (int i = 0; i < 3; ++i) lp[1][i] = M->origin[l][2][i]; }        /* thigh: joint .. knee */
+        else if (k == 1) { lp[0][1] = sy * M->hip_y[0]; lp[1][1] = sy * M->hip_y[1]; }    /* hip capsule */
+        else if (k == 2) { for (int i = 0; i < 3; ++i) lp[1][i] = M->foot[i]; }          /* calf: knee .. foot */
+        else { for (int i = 0; i < 3; ++i) lp[0][i] = lp[1][i] = M->foot[i]; }            /* foot sphere */
+        for (int e = 0; e < 2; ++e) {
+          for (int i = 0; i < 3; ++i) SL[p][e][i] = lp[e][i];
+          point_kin(Rw_all[l][j], pw_all[l][j], vj[l][j], lp[e], SP[p][e], SV[p][e]);
+        }
+        SR[p] = k == 0 ? M->thigh_r : (k == 1 ? M->hip_r : (k == 2 ? M->calf_r : M->foot_r));
+        SJ[p] = j;
+        SB[p] = k == 3 ? 1 + l * 4 + 3 : 1 + l * 4 + j; /* reported body (the foot its own) */
       }
     const real ks = cfg->self_stiffness, ds = cfg->self_damping;
-    /* every sphere pair of two different legs (the force computed on the lower leg's sphere) */
+    /* force F (world) on primitive p at segment parameter s: its link's wrench and its body's reported force */
+#define SELF_APPLY(p, sp, F)                                                                              \
+  do {                                                                                                    \
+    int l_ = (p) / 4;                                                                                     \
+    real lpp[3];                                                                                          \
+    for (int i_ = 0; i_ < 3; ++i_) lpp[i_] = SL[p][0][i_] + (sp) * (SL[p][1][i_] - SL[p][0][i_]);         \
+    point_force(Rw_all[l_][SJ[p]], lpp, (F), wsl[l_][SJ[p]]);                                              \
+    for (int i_ = 0; i_ < 3; ++i_) cfs[SB[p]][i_] += (F)[i_];                                             \
+  } while (0)
+    /* a pair (ia < ib): spheres of the two radii at the segments' closest points */
+#define SELF_PAIR(ia, ib)                                                                                 \
+  do {                                                                                                    \
+    real s_, t_, pa_[3], va_[3], pb_[3], vb_[3], F_[3], G_[3];                                            \
+    seg_seg_closest(SP[ia][0], SP[ia][1], SP[ib][0], SP[ib][1], &s_, &t_);                                \
+    for (int i_ = 0; i_ < 3; ++i_) {                                                                      \
+      pa_[i_] = SP[ia][0][i_] + s_ * (SP[ia][1][i_] - SP[ia][0][i_]);                                     \
+      va_[i_] = SV[ia][0][i_] + s_ * (SV[ia][1][i_] - SV[ia][0][i_]);                                     \
+      pb_[i_] = SP[ib][0][i_] + t_ * (SP[ib][1][i_] - SP[ib][0][i_]);                                     \
+      vb_[i_] = SV[ib][0][i_] + t_ * (SV[ib][1][i_] - SV[ib][0][i_]);                                     \
+    }                                                                                                     \
+    self_sphere_force(pa_, va_, SR[ia], pb_, vb_, SR[ib], ks, ds, F_);                                    \
+    for (int i_ = 0; i_ < 3; ++i_) G_[i_] = -F_[i_];                                                      \
+    SELF_APPLY(ia, s_, F_);                                                                               \
+    SELF_APPLY(ib, t_, G_);                                                                               \
+  } while (0)
+    /* every primitive pair of two different legs */
     for (int la = 0; la < 4; ++la)
       for (int lb = la + 1; lb < 4; ++lb)
-        for (int a = 0; a < 8; ++a)
-          for (int b = 0; b < 8; ++b) {
-            int ia = la * 8 + a, ib = lb * 8 + b;
-            real F[3];
-            self_sphere_force(SP[ia], SV[ia], SR[ia], SP[ib], SV[ib], SR[ib], ks, ds, F);
-            for (int i = 0; i < 3; ++i) { Fself[ia][i] += F[i]; Fself[ib][i] -= F[i]; }
-          }
-    /* the non-adjacent links of one leg: hip capsule vs calf / foot, thigh vs foot (SELF_SAME_A / _B) */
+        for (int a = 0; a < 4; ++a)
+          for (int b = 0; b < 4; ++b) SELF_PAIR(la * 4 + a, lb * 4 + b);
+    /* the non-adjacent links of one leg: hip capsule vs calf capsule / foot, thigh capsule vs foot */
     for (int l = 0; l < 4; ++l)
-      for (int p2 = 0; p2 < SELF_NSAME; ++p2) {
-        int ia = l * 8 + SELF_SAME_A[p2], ib = l * 8 + SELF_SAME_B[p2];
-        real F[3];
-        self_sphere_force(SP[ia], SV[ia], SR[ia], SP[ib], SV[ib], SR[ib], ks, ds, F);
-        for (int i = 0; i < 3; ++i) { Fself[ia][i] += F[i]; Fself[ib][i] -= F[i]; }
-      }
-    /* the thigh, calf and foot spheres against the trunk box (the hip is the trunk's neighbour) */
+      for (int p2 = 0; p2 < SELF_NSAME; ++p2) SELF_PAIR(l * 4 + SELF_SAME_A[p2], l * 4 + SELF_SAME_B[p2]);
+    /* the thigh / calf capsules and the foot against the trunk box (the hip is the trunk's neighbour) */
     for (int l = 0; l < 4; ++l)
-      for (int s8 = 0; s8 < 6; ++s8) {
-        int ia = l * 8 + s8;
-        real F[3];
-        real wb[6] = {0, 0, 0, 0, 0, 0};
-        self_box_force(SP[ia], SV[ia], SR[ia], R, S->pos, vb, M->trunk_half, ks, ds, F, wb);
+      for (int k = 0; k < 4; ++k) {
+        if (k == 1) continue;
+        int p = 4 * l + k;
+        real t = k == 3 ? 0.0 : seg_box_t(SP[p][0], SP[p][1], R, S->pos, M->trunk_half);
+        real pc[3], vc[3], F[3], wb[6] = {0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < 3; ++i) {
+          pc[i] = SP[p][0][i] + t * (SP[p][1][i] - SP[p][0][i]);
+          vc[i] = SV[p][0][i] + t * (SV[p][1][i] - SV[p][0][i]);
+        }
+        self_box_force(pc, vc, SR[p], R, S->pos, vb, M->trunk_half, ks, ds, F, wb);
         for (int i = 0; i < 6; ++i) wself[i] += wb[i];
-        for (int i = 0; i < 3; ++i) Fself[ia][i] += F[i];
+        SELF_APPLY(p, t, F);
         /* the trunk's reported contact force includes the reaction (world frame) */
-        if (cf) for (int i = 0; i < 3; ++i) cf[i] += R[i][0] * wb[3] + R[i][1] * wb[4] + R[i][2] * wb[5];
+        for (int i = 0; i < 3; ++i) cfs[0][i] += R[i][0] * wb[3] + R[i][1] * wb[4] + R[i][2] * wb[5];
       }
+#undef SELF_PAIR
+#undef SELF_APPLY
     for (int i = 0; i < 6; ++i) pA0[i] -= wself[i];
+    if (cf) for (int b2 = 0; b2 < NB; ++b2) for (int i = 0; i < 3; ++i) cf[b2 * 3 + i] += cfs[b2][i];
   }
   for (int l = 0; l < 4; ++l) {
     M6 IA[3];
@@ -827,58 +1072,56 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
       for (int i = 0; i < 3; ++i) gl[i] = Rw[j][0][i] * g[0] + Rw[j][1][i] * g[1] + Rw[j][2][i] * g[2];
       for (int i = 0; i < 3; ++i) fg[i] = B->mass * gl[i];
       cross3(B->com, fg, cg);
-      for (int i = 0; i < 3; ++i) { fext[i] += cg[i]; fext[3 + i] += fg[i]; }
+      for (int i = 0; i < 3; ++i) { fext[i] += cg[i] + wsl[l][j][i]; fext[3 + i] += fg[i] + wsl[l][j][3 + i]; }
       int body_idx = 1 + l * 4 + j; /* hip, thigh, calf */
-      if (j == 0) {
-        const real sy = (l & 1) ? -1.0 : 1.0; /* legs FL, FR, RL, RR */
-        for (int p = 0; p < 2; ++p) {
-          real lp[3] = {0, sy * M->hip_y[p], 0}, pw[3], vw[3], F[3];
-          point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
-          if (g_implicit_contact) {
-            real Mp[3][3] = {{0}};
-            sphere_contact_im(T, &C, pw, vw, M->hip_r, F, h, Mp);
-            point_inertia(Rw[j], lp, Mp, &IA[j]);
-          } else {
-            sphere_contact(T, &C, pw, vw, M->hip_r, F);
-          }
-          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 8 + 6 + p][i];
-          point_force(Rw[j], lp, F, fext);
-          if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
+      /* the link's heightfield contacts: per capsule (half) its deepest point (seg_deepest), the foot sphere */
+      real segs[3][2][3], rads[3];
+      int nseg = 0, foot_seg = -1;
+      const real sy = (l & 1) ? -1.0 : 1.0;
+      memset(segs, 0, sizeof(segs));
+      if (j == 0) { /* hip capsule: one point */
+        segs[0][0][1] = sy * M->hip_y[0]; segs[0][1][1] = sy * M->hip_y[1];
+        rads[0] = M->hip_r;
+        nseg = 1;
+      } else { /* thigh / calf: the halves, each from its outer end to the middle */
+        const real* end = j == 1 ? M->origin[l][2] : M->foot;
+        for (int i = 0; i < 3; ++i) {
+          segs[0][1][i] = 0.5 * end[i];
+          segs[1][0][i] = end[i];
+          segs[1][1][i] = 0.5 * end[i];
         }
-      } else if (j == 1) {
-        for (int p = 0; p < N_THIGH_PTS; ++p) {
-          real lp[3] = {0, 0, THIGH_PTS_Z[p]}, pw[3], vw[3], F[3];
-          point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
-          if (g_implicit_contact) {
-            real Mp[3][3] = {{0}};
-            sphere_contact_im(T, &C, pw, vw, M->thigh_r, F, h, Mp);
-            point_inertia(Rw[j], lp, Mp, &IA[j]);
-          } else {
-            sphere_contact(T, &C, pw, vw, M->thigh_r, F);
-          }
-          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 8 + p][i];
-          point_force(Rw[j], lp, F, fext);
-          if (cf) for (int i = 0; i < 3; ++i) cf[body_idx * 3 + i] += F[i];
+        rads[0] = rads[1] = j == 1 ? M->thigh_r : M->calf_r;
+        nseg = 2;
+        if (j == 2) { /* the foot sphere */
+          for (int i = 0; i < 3; ++i) segs[2][0][i] = segs[2][1][i] = M->foot[i];
+          rads[2] = M->foot_r;
+          foot_seg = 2;
+          nseg = 3;
         }
-      } else if (j == 2) {
-        for (int p = 0; p < N_CALF_PTS + 1; ++p) {
-          real lp[3], r = p < N_CALF_PTS ? M->calf_r : M->foot_r;
-          if (p < N_CALF_PTS) { lp[0] = 0; lp[1] = 0; lp[2] = CALF_PTS_Z[p]; }
-          else { lp[0] = M->foot[0]; lp[1] = M->foot[1]; lp[2] = M->foot[2]; }
-          real pw[3], vw[3], F[3];
-          point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
-          if (g_implicit_contact) {
-            real Mp[3][3] = {{0}};
-            sphere_contact_im(T, &C, pw, vw, r, F, h, Mp);
-            point_inertia(Rw[j], lp, Mp, &IA[j]);
-          } else {
-            sphere_contact(T, &C, pw, vw, r, F);
-          }
-          for (int i = 0; i < 3; ++i) F[i] += Fself[l * 8 + 3 + p][i];
-          point_force(Rw[j], lp, F, fext);
-          int bi = p < N_CALF_PTS ? body_idx : body_idx + 1; /* foot body reported separately */
-          if (cf) for (int i = 0; i < 3; ++i) cf[bi * 3 + i] += F[i];
+      }
+      for (int p = 0; p < nseg; ++p) {
+        real wA[3], wB[3], vA_[3], vB_[3], lp[3], pw[3], vw[3], F[3];
+        point_kin(Rw[j], pw_[j], vj[l][j], segs[p][0], wA, vA_);
+        point_kin(Rw[j], pw_[j], vj[l][j], segs[p][1], wB, vB_);
+        int cell[3];
+        const int slot = j == 0 ? 0 : 2 * j - 1 + p; /* hip; thigh 1, 2; calf 3, 4 */
+        real t = 0.0;
+        if (p != foot_seg) {
+          if (face_scan_now) S->seg_t[l][slot] = seg_deepest(T, wA, wB, rads[p], cell);
+          t = S->seg_t[l][slot];
         }
+        for (int i = 0; i < 3; ++i) lp[i] = segs[p][0][i] + t * (segs[p][1][i] - segs[p][0][i]);
+        point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
+        if (g_implicit_contact) {
+          real Mp[3][3] = {{0}};
+          sphere_contact_im_cell(T, &C, pw, vw, rads[p], F, h, Mp, T->tile && face_scan_now && p != foot_seg ? cell : NULL);
+          point_inertia(Rw[j], lp, Mp, &IA[j]);
+        } else {
+          sphere_contact(T, &C, pw, vw, rads[p], F);
+        }
+        point_force(Rw[j], lp, F, fext);
+        int bi = p == foot_seg ? body_idx + 1 : body_idx; /* foot body reported separately */
+        if (cf) for (int i = 0; i < 3; ++i) cf[bi * 3 + i] += F[i];
       }
       for (int i = 0; i < 6; ++i) pA[j][i] -= fext[i];
     }
@@ -1047,9 +1290,10 @@ void go1o_physics(const go1_config* cfg, double* pos, double* quat, double* v, d
   for (int i = 0; i < 4; ++i) S.quat[i] = quat[i];
   for (int d = 0; d < NDOF; ++d) { S.q[d] = q[d]; S.qd[d] = qd[d]; tr[d] = tau[d]; }
   TerrainView T = {tile, cfg->hf_nx, cfg->hf_ny, ox, oy, cfg->horizontal_scale};
-  /* the trunk-face vertices chosen every 4 sim steps (a control step of the README configuration) */
+  /* the trunk-face vertices chosen once per control step (decimation x n_internal sim steps), as the kernel does */
+  const int scan = cfg->decimation * cfg->n_internal > 0 ? cfg->decimation * cfg->n_internal : 1;
   for (int i = 0; i < n_sub; ++i)
-    phys_substep(&M, cfg, &S, tr, (real)h, gr, (real)friction, (real)restitution, (real)payload, &T, cfr, i % 4 == 0);
+    phys_substep(&M, cfg, &S, tr, (real)h, gr, (real)friction, (real)restitution, (real)payload, &T, cfr, i % scan == 0);
   for (int i = 0; i < 3; ++i) { pos[i] = S.pos[i]; v[i] = S.v[i]; w[i] = S.w[i]; }
   for (int i = 0; i < 4; ++i) quat[i] = S.quat[i];
   for (int d = 0; d < NDOF; ++d) { q[d] = S.q[d]; qd[d] = S.qd[d]; }

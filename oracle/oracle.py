@@ -66,6 +66,27 @@ def physics(cfg, body, tau, n_sub, h, g, friction, restitution, payload, tile=No
     return cf.reshape(17, 3)
 
 
+def seg_deepest(tile, hs, A, B, r):
+    """t in [0, 1] of the deepest point of the segment A -> B (a capsule of radius r) against one (2, nx, ny) tile
+    at the origin (go1_oracle.c seg_deepest)."""
+    tl = np.ascontiguousarray(tile, np.float32)
+    a, b = _d(A, 3), _d(B, 3)
+    f = lib().go1o_seg_deepest
+    f.restype = C.c_double
+    f.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_double]
+    return f(tl.ctypes.data, int(tl.shape[1]), int(tl.shape[2]), hs, a.ctypes.data, b.ctypes.data, r)
+
+
+def seg_closest(P0, P1, Q0, Q1):
+    """(s, t): parameters of the closest points of the segments P0 -> P1 and Q0 -> Q1 (go1_oracle.c)."""
+    st = np.zeros(2)
+    args = [_d(x, 3) for x in (P0, P1, Q0, Q1)]
+    f = lib().go1o_seg_closest
+    f.argtypes = [C.c_void_p] * 5
+    f(*(x.ctypes.data for x in args), st.ctypes.data)
+    return float(st[0]), float(st[1])
+
+
 def energy(cfg, body, g, payload):
     """Kinetic + potential energy of one env's state (dict as `physics`) in the gravity field g."""
     b = {k: _d(body[k], n) for k, n in (("pos", 3), ("quat", 4), ("v", 3), ("w", 3), ("q", 12), ("qd", 12))}

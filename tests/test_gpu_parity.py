@@ -190,13 +190,26 @@ def test_reset_kernel_matches_oracle():
 INTEGRATOR_MAX_ERR = {"dof_pos": 5e-5, "dof_vel": 5e-3, "root": 5e-4}
 
 
-def check_integrator_step(gs, st, cf_gpu, cf_oracle, reset_gpu, reset_oracle):
+def check_integrator_step(gs, st, cf_gpu, cf_oracle, reset_gpu, reset_oracle, st32=None):
+    """st32: the same step through the oracle's f32 build (oracle.step(precision="f32")).  Envs where it is itself
+    out of the bounds against the f64 oracle are ill-conditioned for f32 arithmetic -- since round 6 the capsules'
+    contact points: two nearly parallel links, a deepest point that ties between two places -- and are held to the
+    f32 oracle's own distance instead (at most 2 % of the envs)."""
     flip = ((np.linalg.norm(cf_gpu, axis=2) > 0) != (np.linalg.norm(cf_oracle, axis=2) > 0)).any(axis=1)
     n = flip.size
     assert flip.sum() <= 1 + n // 1000, f"{flip.sum()} envs with a different contact set"
+    sens = np.zeros(n, bool)
+    if st32 is not None:
+        for k, tol in INTEGRATOR_MAX_ERR.items():
+            sens |= (np.abs(st32[k] - st[k]) / np.maximum(1.0, np.abs(st[k]))).max(axis=1) >= tol
+        assert sens.sum() <= 1 + n // 50, f"{sens.sum()} ill-conditioned envs"
     for k, tol in INTEGRATOR_MAX_ERR.items():
         err = (np.abs(gs[k] - st[k]) / np.maximum(1.0, np.abs(st[k]))).max(axis=1)
-        assert err[~flip].max() < tol, (k, err[~flip].max(), int(np.argmax(np.where(flip, 0, err))))
+        ok = ~flip & ~sens
+        assert err[ok].max() < tol, (k, err[ok].max(), int(np.argmax(np.where(ok, err, 0))))
+        if sens.any():  # within 4x of the f32 oracle's own distance from the f64 one
+            e32 = (np.abs(st32[k] - st[k]) / np.maximum(1.0, np.abs(st[k]))).max(axis=1)
+            assert (err[sens & ~flip] <= 4 * e32[sens & ~flip] + tol).all(), (k, err[sens], e32[sens])
     np.testing.assert_array_equal(reset_gpu[~flip], reset_oracle[~flip])
     return int(flip.sum())
 

@@ -3,7 +3,7 @@ model in tests/test_self_collision.py).  One-step comparisons with the integrato
 tests/test_gpu_parity.py (check_integrator_step) on states built to exercise the new terms:
   * test_self_contact_forces_of_colliding_states: states chosen (numpy kinematics, below) to be in self-contact
     at the step's only sim step (decimation 1), the base 1 m above the plane: every reported force is a
-    self-contact force, per body against the oracle, with every class of sphere pair hit across the batch;
+    self-contact force, per body against the oracle, with every class of primitive pair hit across the batch;
   * legs in random poses within the joint limits, some with the front feet crossed under the trunk, stepped
     through three control steps;
   * the robot dropped onto the plane at up to 2.5 m/s with restitution 0..1, through the rebound.
@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 from legged_tracking_amd import config as CF, layout as L, native, terrain as T  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from tests.test_gpu_parity import DEV, _dev, _sim_setup, check_integrator_step  # noqa: E402
-from tests.self_geom import pair_classes as _pair_classes, spheres as _spheres  # noqa: E402
+from tests.self_geom import capsules as _capsules, pair_classes as _pair_classes  # noqa: E402
 
 
 def _run(c, td, ter, st, rng, steps, act_scale=1.0, grav=(0.0, 0.0, 0.0), act=None):
@@ -33,11 +33,13 @@ def _run(c, td, ter, st, rng, steps, act_scale=1.0, grav=(0.0, 0.0, 0.0), act=No
         a = (act_scale * rng.normal(0, 1, (n, 12))).astype(np.float32) if act is None else act.astype(np.float32)
         g.step(_dev(a), gvec, gr, scales, rng_seed=5, rng_step=200 + t)
         torch.cuda.synchronize()
+        s32 = st.copy()
         out = O.step(c, st, ter, a, gvec, gr, scales, rng_seed=5, rng_step=200 + t, debug=False)
+        O.step(c, s32, ter, a, gvec, gr, scales, rng_seed=5, rng_step=200 + t, debug=False, precision="f32")
         gs = g.state.numpy()
         cf = g.contact_forces.cpu().numpy()
         check_integrator_step(gs, st, cf, out["contact_forces"], g.reset.cpu().numpy().astype(bool),
-                              out["reset"].astype(bool))
+                              out["reset"].astype(bool), st32=s32)
         forces.append(cf)
         st = O.NpState(n, gs, c)
     return np.stack(forces)
@@ -114,7 +116,7 @@ def test_self_contact_forces_of_colliding_states(pool_kind):
             pool[inward, 3 * l] = sgn[l] * rng.uniform(0.2, 0.8, inward.sum())
     else:
         pool = rng.uniform(lim[:, 0] - 1.2, lim[:, 1] + 1.2, (60000, 12))
-    P, r = _spheres(pool)
+    P, r = _capsules(pool)
     flags, names = _pair_classes(P, r)
     anyc = flags.any(1)
     pick = []
@@ -131,8 +133,8 @@ def test_self_contact_forces_of_colliding_states(pool_kind):
     reach = flags[pick].any(0)
     kinds = {}
     for j, nm in enumerate(names):
-        key = nm[0] if nm[0] != "cross" else ("cross-hip" if nm[3] >= 6 or nm[4] >= 6 else
-                                             ("cross-thigh" if nm[3] < 3 and nm[4] < 3 else "cross-calf-foot"))
+        key = nm[0] if nm[0] != "cross" else ("cross-hip" if nm[3] == 1 or nm[4] == 1 else
+                                             ("cross-thigh" if nm[3] == 0 and nm[4] == 0 else "cross-calf-foot"))
         kinds.setdefault(key, []).append(reach[j])
     print("\npair classes hit per kind: " + ", ".join(f"{k} {sum(v)}/{len(v)}" for k, v in kinds.items()))
     if pool_kind == "within_limits":
@@ -168,13 +170,15 @@ def test_self_contact_forces_of_colliding_states(pool_kind):
     print(f"envs in self-contact: GPU {touching.mean():.2f}, oracle {(np.abs(ref).max(axis=(1, 2)) > 0).mean():.2f}; "
           f"max |dF| {np.abs(cf - ref).max():.2e} N of max |F| {np.abs(ref).max():.2e} N")
     assert touching.mean() >= 0.5
-    # f32 against f64 kinematics (the integrator's hardware sin / cos): ~1e-7 m in a sphere centre, 2e-4 N of a
+    # f32 against f64 kinematics (the integrator's hardware sin / cos): ~1e-7 m in a closest point, 2e-4 N of a
     # spring; a deep overlap (centres ~1 mm apart, up to 100 N) turns its normal by ~1e-4 -- hence a looser bound on
     # the few worst elements and a tight one on almost all of them
     err = np.abs(cf - ref)
     print(f"force error p99 {np.percentile(err, 99):.2e} N, max {err.max():.2e} N")
     assert np.percentile(err, 99) <= 1e-3, np.percentile(err, 99)
-    np.testing.assert_allclose(cf, ref, rtol=1e-3, atol=0.02)
+    # round 6, capsules: a capsule's point nearest the trunk box comes from a golden-section search, and the f32 build
+    # of the oracle itself lands 0.023 N (folded pool) / 0.042 N (within limits) from the f64 one at worst
+    np.testing.assert_allclose(cf, ref, rtol=1e-3, atol=0.05)
     # internal forces: the per-env sum over the bodies vanishes
     np.testing.assert_allclose(cf.sum(axis=1), 0.0, atol=2e-3)
 
@@ -222,11 +226,13 @@ def test_trunk_face_contacts_step_vs_oracle():
         act = rng.normal(0, 0.3, (n, 12)).astype(np.float32)
         g.step(_dev(act), gvec, grav, scales, rng_seed=4, rng_step=400 + t)
         torch.cuda.synchronize()
+        s32 = st.copy()
         out = O.step(c, st, ter, act, gvec, grav, scales, rng_seed=4, rng_step=400 + t, debug=False)
+        O.step(c, s32, ter, act, gvec, grav, scales, rng_seed=4, rng_step=400 + t, debug=False, precision="f32")
         gs = g.state.numpy()
         cf = g.contact_forces.cpu().numpy()
         check_integrator_step(gs, st, cf, out["contact_forces"], g.reset.cpu().numpy().astype(bool),
-                              out["reset"].astype(bool))
+                              out["reset"].astype(bool), st32=s32)
         base, base_ref = cf[:, 0], out["contact_forces"][:, 0]
         np.testing.assert_allclose(base, base_ref, rtol=1e-3, atol=2e-2)
         hits.append((np.linalg.norm(base_ref, axis=1) > 0).mean())

@@ -15,7 +15,7 @@ O=gpurun_out/$TAG
 mkdir -p "$O"
 R=$PWD
 if [ "${SUITE:-0}" = 1 ]; then
-  timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread ${TESTS:-tests} -m gpu > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|assert" $O/pytest_gpu.log | head -30; exit 1; }
+  timeout -k 10 900 python -u -m pytest ${PYX--x} -v --timeout 300 --timeout-method thread ${TESTS:-tests} -m gpu > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error|assert" $O/pytest_gpu.log | head -30; exit 1; }
   echo "pytest ok: $(tail -1 $O/pytest_gpu.log)"
   timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke.log; exit 1; }
 fi
