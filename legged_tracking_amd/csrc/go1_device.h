@@ -1192,6 +1192,9 @@ __device__ __forceinline__ float seg_deepest(const Terr& T, const float* A, cons
   const float uA = fminf(fmaxf(A[0] * ihs, -4.0f), (float)(T.nx + 4)), vA = fminf(fmaxf(A[1] * ihs, -4.0f), (float)(T.ny + 4));
   const float uB = fminf(fmaxf(B[0] * ihs, -4.0f), (float)(T.nx + 4)), vB = fminf(fmaxf(B[1] * ihs, -4.0f), (float)(T.ny + 4));
   const float du = uB - uA, dv = vB - vA, dw = du - dv, dz = B[2] - A[2], zA = A[2];
+  // an invalid candidate (beyond the segment's crossings) reads A's cell instead of an edge up to 4 cells off, which
+  // could leave the LDS patch and send the whole wave to the HBM tile
+  const int iA = (int)floorf(uA), jA = (int)floorf(vA);
   SegBest sb;
   sb.key = -2147483647 - 1;
   sb.t = 0.0f;
@@ -1220,7 +1223,7 @@ __device__ __forceinline__ float seg_deepest(const Terr& T, const float* A, cons
       const float t = valid ? ((float)k - uA) * rdu : 0.0f, v = vA + dv * t, fv = floorf(v), b = v - fv;
       const int j = (int)fv, i = du > 0.0f ? k - 1 : k;
       f2 p0, p1;
-      edge_fetch(T, k, j, 0, 1, p0, p1);
+      edge_fetch(T, valid ? k : iA, valid ? j : jA, 0, 1, p0, p1);
       seg_offer(sb, p0 + b * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, (float)(k - i) < b), valid);
     }
   }
@@ -1235,7 +1238,7 @@ __device__ __forceinline__ float seg_deepest(const Terr& T, const float* A, cons
       const float t = valid ? ((float)k - vA) * rdv : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
       const int i = (int)fu, j = dv > 0.0f ? k - 1 : k;
       f2 p0, p1;
-      edge_fetch(T, i, k, 1, 0, p0, p1);
+      edge_fetch(T, valid ? i : iA, valid ? k : jA, 1, 0, p0, p1);
       seg_offer(sb, p0 + a * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, a < (float)(k - j)), valid);
     }
   }
@@ -1252,7 +1255,7 @@ __device__ __forceinline__ float seg_deepest(const Terr& T, const float* A, cons
       const float t = valid ? ((float)k - wA) * rdw : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
       const int i = (int)fu, j = i - k;
       f2 p0, p1;
-      edge_fetch(T, i, j, 1, 1, p0, p1);
+      edge_fetch(T, valid ? i : iA, valid ? j : jA, 1, 1, p0, p1);
       seg_offer(sb, p0 + a * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, dw > 0.0f), valid);
     }
   }
@@ -1520,19 +1523,10 @@ __device__ __forceinline__ void seg_closest(const float* P0, const float* d1, co
   t = !pe ? 0.0f : (!pa ? clampf(f * ie, 0.0f, 1.0f) : tt);
 }
 
-// the point of the segment P0 -> P1 (world) nearest the trunk box, deepest inside it: the box's signed distance is
-// convex along the segment, minimised by golden-section search (oracle/go1_oracle.c seg_box_t, SEG_GOLDEN steps)
-__device__ __forceinline__ float box_sdf(const float* c, const float* th) {
-  float o = 0.0f, in = -1e30f;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const float q = fabsf(c[i]) - th[i];
-    o += q > 0.0f ? q * q : 0.0f;
-    in = fmaxf(in, q);
-  }
-  return o * frsq(fmaxf(o, 1e-30f)) + fminf(in, 0.0f);
-}
-#define SEG_GOLDEN 32
+// the point of the segment P0 -> P1 (world) nearest the trunk box, deepest inside it: bisection on the sign of the
+// derivative of the box's signed distance along the segment (convex), SEG_BISECT halvings (oracle/go1_oracle.c
+// seg_box_t, which explains the sign); no square roots, and every midpoint an exact binary fraction
+#define SEG_BISECT 20
 __device__ __forceinline__ float seg_box_t(const float* P0, const float* P1, const float* R, const float* pos,
                                            const float* th) {
   float a0[3], d[3];
@@ -1541,22 +1535,22 @@ __device__ __forceinline__ float seg_box_t(const float* P0, const float* P1, con
     a0[i] = R[i] * (P0[0] - pos[0]) + R[3 + i] * (P0[1] - pos[1]) + R[6 + i] * (P0[2] - pos[2]);
     d[i] = R[i] * (P1[0] - P0[0]) + R[3 + i] * (P1[1] - P0[1]) + R[6 + i] * (P1[2] - P0[2]);
   }
-  const float gr = 0.6180339887498949f;
-  float lo = 0.0f, hi = 1.0f, x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo);
-  auto f = [&](float x) {
-    const float c[3] = {a0[0] + x * d[0], a0[1] + x * d[1], a0[2] + x * d[2]};
-    return box_sdf(c, th);
-  };
-  float f1 = f(x1), f2v = f(x2);
-  for (int it = 0; it < SEG_GOLDEN; ++it) {
-    const bool left = f1 <= f2v;
-    hi = left ? x2 : hi;
-    lo = left ? lo : x1;
-    const float nx = left ? hi - gr * (hi - lo) : lo + gr * (hi - lo);
-    const float fn = f(nx);
-    const float x1n = left ? nx : x2, x2n = left ? x1 : nx;
-    const float f1n = left ? fn : f2v, f2n = left ? f1 : fn;
-    x1 = x1n; x2 = x2n; f1 = f1n; f2v = f2n;
+  float lo = 0.0f, hi = 1.0f;
+  for (int it = 0; it < SEG_BISECT; ++it) {
+    const float m = 0.5f * (lo + hi);
+    float so = 0.0f, qmax = -1e30f, sin = 0.0f;
+    bool out = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float c = a0[i] + m * d[i], sd = c >= 0.0f ? d[i] : -d[i], q = fabsf(c) - th[i];
+      so += q > 0.0f ? q * sd : 0.0f;
+      out = out || q > 0.0f;
+      sin = q > qmax ? sd : sin;
+      qmax = fmaxf(qmax, q);
+    }
+    const float sl = out ? so : sin;
+    lo = sl < 0.0f ? m : lo;
+    hi = sl < 0.0f ? hi : m;
   }
   return 0.5f * (lo + hi);
 }

@@ -698,20 +698,14 @@ void go1o_seg_closest(const double* P0, const double* P1, const double* Q0, cons
   st[1] = t;
 }
 
-/* signed distance of the base-frame point c to the trunk box (half extents th) */
-static real box_sdf(const real* c, const real* th) {
-  real q[3], o = 0.0, in = -1e30;
-  for (int i = 0; i < 3; ++i) {
-    q[i] = fabs(c[i]) - th[i];
-    o += q[i] > 0.0 ? q[i] * q[i] : 0.0;
-    in = fmax(in, q[i]);
-  }
-  return sqrt(o) + fmin(in, 0.0);
-}
-/* the point of the segment P0 -> P1 (world) nearest the trunk box (deepest inside it): the box's signed distance is
- * convex, so along the segment it is a convex function of t, minimised by golden-section search (SEG_GOLDEN
- * steps, 0.618^32 of the segment ~ 0.04 um on a 0.213 m link; go1_device.h seg_box_t is the f32 restatement) */
-#define SEG_GOLDEN 32
+/* the point of the segment P0 -> P1 (world) nearest the trunk box (deepest inside it).  The box's signed distance is
+ * convex, so along the segment it is a convex function of t; its minimum is found by bisection on the sign of the
+ * derivative (SEG_BISECT halvings, 2^-20 of the segment ~ 0.2 um on a 0.213 m link; every midpoint an exact binary
+ * fraction in f32 and f64 alike).  Outside the box the distance |q+| (q_i = |c_i| - th_i) has the derivative's sign
+ * of sum_i q+_i sgn(c_i) d_i; inside, max_i q_i has sgn(c_k) d_k for the deepest axis k (the lowest on ties).  Round
+ * 6's first cut ran a golden-section search on the distance itself (32 evaluations with a square root each), the
+ * slowest waves' largest section.  go1_device.h seg_box_t is the f32 restatement. */
+#define SEG_BISECT 20
 #define BOX_Q 1.0e-4
 static long box_quant(real d) { return (long)floor(fmin(fmax(d, -1.0), 1.0) / BOX_Q); }
 static real seg_box_t(const real* P0, const real* P1, real R[3][3], const real* pos, const real* th) {
@@ -720,22 +714,18 @@ static real seg_box_t(const real* P0, const real* P1, real R[3][3], const real* 
     a0[i] = R[0][i] * (P0[0] - pos[0]) + R[1][i] * (P0[1] - pos[1]) + R[2][i] * (P0[2] - pos[2]);
     d[i] = R[0][i] * (P1[0] - P0[0]) + R[1][i] * (P1[1] - P0[1]) + R[2][i] * (P1[2] - P0[2]);
   }
-  const real gr = 0.6180339887498949;
-  real lo = 0.0, hi = 1.0, x1 = hi - gr * (hi - lo), x2 = lo + gr * (hi - lo), c[3];
-  for (int i = 0; i < 3; ++i) c[i] = a0[i] + x1 * d[i];
-  real f1 = box_sdf(c, th);
-  for (int i = 0; i < 3; ++i) c[i] = a0[i] + x2 * d[i];
-  real f2 = box_sdf(c, th);
-  for (int it = 0; it < SEG_GOLDEN; ++it) {
-    if (f1 <= f2) {
-      hi = x2; x2 = x1; f2 = f1; x1 = hi - gr * (hi - lo);
-      for (int i = 0; i < 3; ++i) c[i] = a0[i] + x1 * d[i];
-      f1 = box_sdf(c, th);
-    } else {
-      lo = x1; x1 = x2; f1 = f2; x2 = lo + gr * (hi - lo);
-      for (int i = 0; i < 3; ++i) c[i] = a0[i] + x2 * d[i];
-      f2 = box_sdf(c, th);
+  real lo = 0.0, hi = 1.0;
+  for (int it = 0; it < SEG_BISECT; ++it) {
+    const real m = 0.5 * (lo + hi);
+    real so = 0.0, qmax = -1e30, sin = 0.0;
+    int out = 0;
+    for (int i = 0; i < 3; ++i) {
+      const real c = a0[i] + m * d[i], sg = c >= 0.0 ? 1.0 : -1.0, q = fabs(c) - th[i];
+      if (q > 0.0) { so += q * sg * d[i]; out = 1; }
+      if (q > qmax) { qmax = q; sin = sg * d[i]; }
     }
+    const real sl = out ? so : sin;
+    if (sl < 0.0) lo = m; else hi = m;
   }
   return 0.5 * (lo + hi);
 }

@@ -122,6 +122,12 @@ def main():
         es = np.mean([cw[i][nm] for i in slow]); em = np.mean([cw[i][nm] for i in mid])
         ts = np.mean([per_wave[i][nm] for i in slow]); tm = np.mean([per_wave[i][nm] for i in mid])
         print(f"{nm:28s} {es:10.2f} {em:10.2f} {ts / max(es, 1e-9):14.0f} {tm / max(em, 1e-9):13.0f}")
+    # the very slowest waves one by one (the launch time is the slowest wave's): their largest extra sections
+    mid_mean = {nm: np.mean([per_wave[i][nm] for i in mid]) for nm in secs}
+    print("\nthe 6 slowest waves: lifetime, then the sections with the most extra cycles over the middle half")
+    for i in order[-6:][::-1]:
+        ex = sorted(((per_wave[i][nm] - mid_mean[nm], nm) for nm in secs), reverse=True)[:5]
+        print(f"  {lf[i]:8.0f}  " + "  ".join(f"{nm} {v:+.0f} ({cw[i][nm]}x)" for v, nm in ex))
 
 
 if __name__ == "__main__":
