@@ -1169,20 +1169,29 @@ __device__ __forceinline__ void seg_offer(SegBest& sb, f2 h, float z, float r, f
   sb.t = up ? t : sb.t;
   sb.cell = up ? cell : sb.cell;
 }
-// the two (floor, ceiling) vertices of the mesh edge (i, j) - (i + di, j + dj): the LDS patch, or the tile outside it
-__device__ __forceinline__ void edge_fetch(const Terr& T, int i, int j, int di, int dj, f2& p0, f2& p1) {
-  const int li = i - T.pi0, lj = j - T.pj0;
-  if (T.patch && li >= 0 && li + di < PSZX && lj >= 0 && lj + dj < PSZY) {
-    const float2* pp = T.patch + li * PSZY + lj;
-    const float2 q0 = pp[0], q1 = pp[di * PSZY + dj];
-    p0 = f2{q0.x, q0.y};
-    p1 = f2{q1.x, q1.y};
-  } else {
-    p0 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
-    p1 = f2{tile_at(T, 1, i + di, j + dj), tile_at(T, 0, i + di, j + dj)};
+// the (floor, ceiling) mesh vertices (vi, vj): the LDS patch in one batch of reads, then the HBM tile for the rare
+// ones outside it (a wave-uniform branch), so the wave waits for the patch once per batch
+template <int N>
+__device__ __forceinline__ void verts_fetch(const Terr& T, const int* vi, const int* vj, f2* h) {
+  unsigned out = T.patch ? 0u : (1u << N) - 1u;
+  if (T.patch) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const int li = vi[n] - T.pi0, lj = vj[n] - T.pj0;
+      const bool in = li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
+      const float2 q = T.patch[min(max(li, 0), PSZX - 1) * PSZY + min(max(lj, 0), PSZY - 1)];
+      h[n] = f2{q.x, q.y};
+      out |= in ? 0u : 1u << n;
+    }
+  }
+  if (__any(out != 0u)) {
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      if ((out >> n) & 1u) h[n] = f2{tile_at(T, 1, vi[n], vj[n]), tile_at(T, 0, vi[n], vj[n])};
   }
 }
-// deepest point of one segment (world ends A, B): t and SEG_CELL
+// deepest point of one segment (world ends A, B): t and SEG_CELL.  Two batches of candidates (the ends and the lines
+// u = k; the lines v = k and the diagonals), each gathering its mesh vertices (verts_fetch) before comparing them
 __device__ __forceinline__ float seg_deepest(const Terr& T, const float* A, const float* B, float r, int& cell) {
   if (!T.tile) {  // the plane: the lower end
     cell = SEG_CELL(0, 0, false);
@@ -1193,70 +1202,103 @@ __device__ __forceinline__ float seg_deepest(const Terr& T, const float* A, cons
   const float uB = fminf(fmaxf(B[0] * ihs, -4.0f), (float)(T.nx + 4)), vB = fminf(fmaxf(B[1] * ihs, -4.0f), (float)(T.ny + 4));
   const float du = uB - uA, dv = vB - vA, dw = du - dv, dz = B[2] - A[2], zA = A[2];
   // an invalid candidate (beyond the segment's crossings) reads A's cell instead of an edge up to 4 cells off, which
-  // could leave the LDS patch and send the whole wave to the HBM tile
+  // could leave the LDS patch
   const int iA = (int)floorf(uA), jA = (int)floorf(vA);
   SegBest sb;
   sb.key = -2147483647 - 1;
   sb.t = 0.0f;
   sb.cell = SEG_CELL(0, 0, false);
-  // the ends
+  {  // the ends (vertices c00, c11 and c01 on the upper triangle / c10) and the grid lines u = k (the edge (k, j) -
+     // (k, j + 1), entered from cell k - 1 (du > 0) or k)
+    int vi[12], vj[12];
+    float ca[5], cb[2], ct[3];
+    int ccell[5];
+    bool cup[2], cval[3];
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const float u = e ? uB : uA, v = e ? vB : vA;
-    const float fu = floorf(u), fv = floorf(v);
-    HQ q;
-    q.a = u - fu;
-    q.b = v - fv;
-    q.up = q.a < q.b;
-    cell_fetch(T, (int)fu, (int)fv, q.c00, q.c10, q.c01, q.c11);
-    const f2 da = q.up ? q.c11 - q.c01 : q.c10 - q.c00, db = q.up ? q.c01 - q.c00 : q.c11 - q.c10;
-    seg_offer(sb, q.c00 + q.a * da + q.b * db, e ? B[2] : zA, r, (float)e, SEG_CELL((int)fu, (int)fv, q.up), true);
-  }
-  // grid lines u = k (the edge (k, j) - (k, j + 1)), entered from cell k - 1 (du > 0) or k
-  {
+    for (int e = 0; e < 2; ++e) {
+      const float u = e ? uB : uA, v = e ? vB : vA;
+      const float fu = floorf(u), fv = floorf(v);
+      const int i = (int)fu, j = (int)fv;
+      ca[e] = u - fu;
+      cb[e] = v - fv;
+      cup[e] = ca[e] < cb[e];
+      ccell[e] = SEG_CELL(i, j, cup[e]);
+      vi[3 * e] = i; vj[3 * e] = j;
+      vi[3 * e + 1] = i + 1; vj[3 * e + 1] = j + 1;
+      vi[3 * e + 2] = cup[e] ? i : i + 1; vj[3 * e + 2] = cup[e] ? j + 1 : j;
+    }
     const int k0 = (int)floorf(fminf(uA, uB)) + 1;
     const float hi = fmaxf(uA, uB), rdu = du != 0.0f ? frcp(du) : 0.0f;
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      const int k = k0 + m;
+      const int k = k0 + m, n = 6 + 2 * m;
       const bool valid = (float)k < hi;
       const float t = valid ? ((float)k - uA) * rdu : 0.0f, v = vA + dv * t, fv = floorf(v), b = v - fv;
       const int j = (int)fv, i = du > 0.0f ? k - 1 : k;
-      f2 p0, p1;
-      edge_fetch(T, valid ? k : iA, valid ? j : jA, 0, 1, p0, p1);
-      seg_offer(sb, p0 + b * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, (float)(k - i) < b), valid);
+      ct[m] = t; ca[2 + m] = b; cval[m] = valid;
+      ccell[2 + m] = SEG_CELL(i, j, (float)(k - i) < b);
+      vi[n] = valid ? k : iA; vj[n] = valid ? j : jA;
+      vi[n + 1] = vi[n]; vj[n + 1] = vj[n] + 1;
     }
-  }
-  // grid lines v = k (the edge (i, k) - (i + 1, k)), entered from cell k - 1 (dv > 0) or k
-  {
-    const int k0 = (int)floorf(fminf(vA, vB)) + 1;
-    const float hi = fmaxf(vA, vB), rdv = dv != 0.0f ? frcp(dv) : 0.0f;
+    f2 h[12];
+    verts_fetch<12>(T, vi, vj, h);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const f2 c00 = h[3 * e], c11 = h[3 * e + 1], cx = h[3 * e + 2];
+      const f2 da = cup[e] ? c11 - cx : cx - c00, db = cup[e] ? cx - c00 : c11 - cx;
+      seg_offer(sb, c00 + ca[e] * da + cb[e] * db, e ? B[2] : zA, r, (float)e, ccell[e], true);
+    }
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      const int k = k0 + m;
-      const bool valid = (float)k < hi;
-      const float t = valid ? ((float)k - vA) * rdv : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
-      const int i = (int)fu, j = dv > 0.0f ? k - 1 : k;
-      f2 p0, p1;
-      edge_fetch(T, valid ? i : iA, valid ? k : jA, 1, 0, p0, p1);
-      seg_offer(sb, p0 + a * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, a < (float)(k - j)), valid);
+      const f2 p0 = h[6 + 2 * m], p1 = h[7 + 2 * m];
+      seg_offer(sb, p0 + ca[2 + m] * (p1 - p0), zA + dz * ct[m], r, ct[m], ccell[2 + m], cval[m]);
     }
   }
-  // cell diagonals u - v = k (the point (i + a, j + a) of cell (i, j), i - j = k), entered from the upper triangle
-  // (dw > 0: u - v grows through k, a < b before) or the lower
-  {
-    const float wA = uA - vA, wB = uB - vB;
-    const int k0 = (int)floorf(fminf(wA, wB)) + 1;
-    const float hi = fmaxf(wA, wB), rdw = dw != 0.0f ? frcp(dw) : 0.0f;
+  __builtin_amdgcn_sched_barrier(0);
+  {  // the grid lines v = k (the edge (i, k) - (i + 1, k), entered from cell k - 1 (dv > 0) or k) and the cell
+     // diagonals u - v = k (the point (i + a, j + a) of cell (i, j), i - j = k, entered from the upper triangle (dw > 0:
+     // u - v grows through k, a < b before) or the lower)
+    int vi[14], vj[14];
+    float ca[7], ct[7];
+    int ccell[7];
+    bool cval[7];
+    {
+      const int k0 = (int)floorf(fminf(vA, vB)) + 1;
+      const float hi = fmaxf(vA, vB), rdv = dv != 0.0f ? frcp(dv) : 0.0f;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int k = k0 + m;
-      const bool valid = (float)k < hi;
-      const float t = valid ? ((float)k - wA) * rdw : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
-      const int i = (int)fu, j = i - k;
-      f2 p0, p1;
-      edge_fetch(T, valid ? i : iA, valid ? j : jA, 1, 1, p0, p1);
-      seg_offer(sb, p0 + a * (p1 - p0), zA + dz * t, r, t, SEG_CELL(i, j, dw > 0.0f), valid);
+      for (int m = 0; m < 3; ++m) {
+        const int k = k0 + m, n = 2 * m;
+        const bool valid = (float)k < hi;
+        const float t = valid ? ((float)k - vA) * rdv : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
+        const int i = (int)fu, j = dv > 0.0f ? k - 1 : k;
+        ct[m] = t; ca[m] = a; cval[m] = valid;
+        ccell[m] = SEG_CELL(i, j, a < (float)(k - j));
+        vi[n] = valid ? i : iA; vj[n] = valid ? k : jA;
+        vi[n + 1] = vi[n] + 1; vj[n + 1] = vj[n];
+      }
+    }
+    {
+      const float wA = uA - vA, wB = uB - vB;
+      const int k0 = (int)floorf(fminf(wA, wB)) + 1;
+      const float hi = fmaxf(wA, wB), rdw = dw != 0.0f ? frcp(dw) : 0.0f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int k = k0 + m, c = 3 + m, n = 2 * c;
+        const bool valid = (float)k < hi;
+        const float t = valid ? ((float)k - wA) * rdw : 0.0f, u = uA + du * t, fu = floorf(u), a = u - fu;
+        const int i = (int)fu, j = i - k;
+        ct[c] = t; ca[c] = a; cval[c] = valid;
+        ccell[c] = SEG_CELL(i, j, dw > 0.0f);
+        vi[n] = valid ? i : iA; vj[n] = valid ? j : jA;
+        vi[n + 1] = vi[n] + 1; vj[n + 1] = vj[n] + 1;
+      }
+    }
+    f2 h[14];
+    verts_fetch<14>(T, vi, vj, h);
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+      const f2 p0 = h[2 * c], p1 = h[2 * c + 1];
+      seg_offer(sb, p0 + ca[c] * (p1 - p0), zA + dz * ct[c], r, ct[c], ccell[c], cval[c]);
     }
   }
   cell = sb.cell;
@@ -1267,6 +1309,7 @@ __device__ __forceinline__ f2 seg_deepest2(const Terr& T, const f2* A, const f2*
   const float a0[3] = {A[0].x, A[1].x, A[2].x}, b0[3] = {B[0].x, B[1].x, B[2].x};
   const float a1[3] = {A[0].y, A[1].y, A[2].y}, b1[3] = {B[0].y, B[1].y, B[2].y};
   const float tx = seg_deepest(T, a0, b0, r.x, cell[0]);
+  __builtin_amdgcn_sched_barrier(0);  // one segment's vertex batch live at a time
   const float ty = seg_deepest(T, a1, b1, r.y, cell[1]);
   return f2{tx, ty};
 }

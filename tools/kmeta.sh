@@ -16,7 +16,7 @@ for l in sys.stdin:
 out.append(cur)
 for b in out:
     if "step_kernel" in b.get("name", ""):
-        print(b["name"][:48], "vgpr", b.get("vgpr_count"), "agpr", b.get("agpr_count"), "spill", b.get("vgpr_spill_count"), "scratch", b.get("private_segment_fixed_size"))
+        print(b["name"][:48], "vgpr", b.get("vgpr_count"), "agpr", b.get("agpr_count"), "spill", b.get("vgpr_spill_count"), "scratch", b.get("private_segment_fixed_size"), "lds", b.get("group_segment_fixed_size"))
 '
 /opt/rocm/lib/llvm/bin/llvm-readelf -S $T/dev.o | grep " .text" | awk '{print "text bytes", strtonum("0x"$6)}'
 rm -rf $T
