@@ -177,8 +177,9 @@ def make_env(n, rank, world, dev):
                                                     world_size=world))
 
 
-def kernel_loop(env, ring, steps, warmup, every=4):
-    """The fused kernel alone (Go1Native.step, no env host code) on the env's own handle."""
+def kernel_loop(env, ring, steps, warmup, every=4, contact_forces=True):
+    """The fused kernel alone (Go1Native.step, no env host code) on the env's own handle; no aux block, and
+    contact_forces=False leaves the contact-force store out as well (the rollout's outputs)."""
     import torch
     base = env.env
     sim = base._sim
@@ -186,12 +187,14 @@ def kernel_loop(env, ring, steps, warmup, every=4):
     scales = base._scale_vector()
     ev = EventPairs((steps + every - 1) // every)
     for k in range(warmup):
-        sim.step(ring[k % len(ring)], gvec, grav, scales, rng_seed=7, rng_step=(1 << 40) + k)
+        sim.step(ring[k % len(ring)], gvec, grav, scales, rng_seed=7, rng_step=(1 << 40) + k,
+                 contact_forces=contact_forces)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
         e = ev.pair(k // every) if k % every == 0 else None
-        sim.step(ring[k % len(ring)], gvec, grav, scales, rng_seed=7, rng_step=(1 << 40) + warmup + k, events=e)
+        sim.step(ring[k % len(ring)], gvec, grav, scales, rng_seed=7, rng_step=(1 << 40) + warmup + k, events=e,
+                 contact_forces=contact_forces)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     kt = [ev.ms(i) for i in range((steps + every - 1) // every)]
@@ -455,6 +458,8 @@ def main():
     ap.add_argument("--sweep", default="", help="comma-separated envs/GPU for an extra size sweep (e.g. 16384,65536)")
     ap.add_argument("--selftest", action="store_true", help="CPU-only launcher test (gloo, no GPU work)")
     ap.add_argument("--kernel-only", action="store_true", help="A/B helper: time only the fused kernel")
+    ap.add_argument("--rollout-outputs", action="store_true",
+                    help="with --kernel-only: the rollout's stores only (no contact forces, no aux block)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -474,7 +479,7 @@ def main():
         env = make_env(args.envs_per_gpu, 0, 1, dev)
         env.reset()
         ring = torch.randn((64, args.envs_per_gpu, 12), device=dev)
-        kdt, kms = kernel_loop(env, ring, args.steps, args.warmup, every=1)
+        kdt, kms = kernel_loop(env, ring, args.steps, args.warmup, every=1, contact_forces=not args.rollout_outputs)
         kt = np.array(kernel_loop.last)
         print(json.dumps({"kernel_ms_mean": kms, "kernel_ms_median": float(np.median(kt)),
                           "kernel_ms_p10": float(np.percentile(kt, 10)), "loop_ms_per_step": kdt / args.steps * 1e3}))

@@ -376,6 +376,8 @@ class LeggedRobot:
         self._elog = EpisodeLogRing(self, n, dev, compact=self._fast and not self._abi_cfg.indefinite_slots)
         self._prepared = {}
         self._aux = torch.zeros((n, abi.GO1_AUX), device=dev)
+        # which per-step outputs the kernel stores beyond obs / rewards / resets (set_output_demand)
+        self._demand = (True, True)
         # envs the native integrator's divergence guard reset, cumulative (extras["diverged"])
         self._diverged = torch.zeros(1, dtype=torch.int64, device=dev)
         # host RNG for the global gravity draws: identical on every rank
@@ -531,29 +533,46 @@ class LeggedRobot:
     def joint_pos_target(self):
         return self._sim.state["joint_pos_target"]
 
+    def set_output_demand(self, contact_forces=True, aux=True):
+        """Whether each step stores the contact forces (n, 17, 3) and the aux block (base velocities, commands,
+        foot positions, torques) -- 204 + 128 B per env-step of HBM writes.  Both default on: the reference
+        refreshes them every step (legged_robot_trajectory_tracking.py:64-112, gym.refresh_net_contact_force_tensor)
+        and the extras read them.  Runner.learn switches both off while it collects rollouts, which read neither
+        (ppo_cse/__init__.py:164-214), and restores them; reading one while it is off raises instead of returning
+        a stale step."""
+        self._demand = (bool(contact_forces), bool(aux))
+
+    def _aux_view(self, a, b):
+        if not self._demand[1]:
+            raise RuntimeError("the aux outputs are not stored while set_output_demand(aux=False) is in effect")
+        return self._aux[:, a:b]
+
     @property
     def contact_forces(self):
+        if not self._demand[0]:
+            raise RuntimeError("contact_forces are not stored while set_output_demand(contact_forces=False) is in "
+                               "effect")
         return self._sim.contact_forces
 
     @property
     def torques(self):
-        return self._aux[:, 20:32]
+        return self._aux_view(20, 32)
 
     @property
     def base_lin_vel(self):
-        return self._aux[:, 0:3]
+        return self._aux_view(0, 3)
 
     @property
     def base_ang_vel(self):
-        return self._aux[:, 3:6]
+        return self._aux_view(3, 6)
 
     @property
     def commands(self):
-        return self._aux[:, 6:8]
+        return self._aux_view(6, 8)
 
     @property
     def foot_positions(self):
-        return self._aux[:, 8:20].view(-1, 4, 3)
+        return self._aux_view(8, 20).view(-1, 4, 3)
 
     @property
     def episode_sums(self):
@@ -591,7 +610,7 @@ class LeggedRobot:
         if self._fast:
             el = self._elog
             log = el.next_slot()
-            key = (s, el.half if el.compact else el.slot + el.R * el.half, self._obs_hist is not None)
+            key = (s, el.half if el.compact else el.slot + el.R * el.half, self._obs_hist is not None, self._demand)
             p = self._prepared.get(key)
             if p is None:
                 p = self._prepared[key] = self._prepare_slot(s, log)
@@ -603,9 +622,11 @@ class LeggedRobot:
             out = dict(obs=self._obs[s], priv=self._priv[s], rew=self._rew[s], reset=self._reset[s],
                        time_out=self._time_out[s])
             hist = self._obs_hist[s] if self._obs_hist is not None else None
+            cf = {} if self._demand[0] else {"contact_forces": False}
             self._sim.step(a, self._gravity_vec, self._sim_gravity, self._scale_vector(), rng_seed=self.seed,
-                           rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(), aux=self._aux,
-                           obs_history=hist, events=events, diverged_count=self._diverged)
+                           rng_step=self._rng_step, out=out, episode_log=self._elog.next_slot(),
+                           aux=self._aux if self._demand[1] else None, obs_history=hist, events=events,
+                           diverged_count=self._diverged, **cf)
         self._last_hist = hist
         self._rng_step += 1
         self._elog.advance()
@@ -626,8 +647,10 @@ class LeggedRobot:
                    time_out=self._time_out[s])
         hist = self._obs_hist[s] if self._obs_hist is not None else None
         el = self._elog
-        args = self._sim.prepare(out, aux=self._aux, obs_history=hist, diverged_count=self._diverged,
-                                 episode_log=log, log_count=el.count[el.half] if el.compact else None)
+        args = self._sim.prepare(out, aux=self._aux if self._demand[1] else None, obs_history=hist,
+                                 diverged_count=self._diverged, episode_log=log,
+                                 log_count=el.count[el.half] if el.compact else None,
+                                 contact_forces=self._demand[0])
         return args, out, hist
 
     def update_curriculum(self):

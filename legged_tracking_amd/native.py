@@ -164,18 +164,19 @@ class Go1Native:
 
     def step(self, actions, gravity_vec, sim_gravity, reward_scales, rng_seed=0, rng_step=0, uniforms=None,
              inj=None, debug=None, events=None, episode_log=None, aux=None, out=None, obs_history=None,
-             diverged_count=None):
+             diverged_count=None, contact_forces=True):
         """One fused LeggedRobot.step on the current stream.  `debug` is an optional dict
         of preallocated tensors (torques, heights, terms, commands, reached); `out` may
-        replace the default output buffers (obs, priv, rew, reset, time_out).
+        replace the default output buffers (obs, priv, rew, reset, time_out); contact_forces=False
+        skips the (n, 17, 3) contact-force store (the kernel writes nothing there).
 
         The go1_step_args struct is kept between calls (the rollout calls this every
         few hundred microseconds); only the fields that change are rewritten."""
         a = self._args
         if a is None:
             a = self._args = abi.Go1StepArgs()
-            a.contact_forces = self.contact_forces.data_ptr()
             a.extras_time_outs = self.extras_time_outs.data_ptr()
+        a.contact_forces = self.contact_forces.data_ptr() if contact_forces else None
         if actions.dtype != torch.float32 or actions.shape != (self.n, 12) or not actions.is_contiguous() or \
                 actions.device != self.device:
             raise NativeError("actions must be a contiguous (n_envs, 12) float32 tensor on the env's device")
@@ -229,13 +230,15 @@ class Go1Native:
         _check(self._lib_step(self.h, C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
 
     # ------------------------------------------------------------------ per-step fast path
-    def prepare(self, out, aux=None, obs_history=None, diverged_count=None, episode_log=None, log_count=None):
+    def prepare(self, out, aux=None, obs_history=None, diverged_count=None, episode_log=None, log_count=None,
+                contact_forces=True):
         """A validated go1_step_args for step_prepared: the env builds one per (output-ring slot,
         episode-log half) once, so the per-step host work is a handful of field writes and the
         ctypes call (the loop is otherwise host-bound at ~60 us per step).  `episode_log` with
-        `log_count` selects the compact log (go1_step_args.episode_log_count)."""
+        `log_count` selects the compact log (go1_step_args.episode_log_count); contact_forces=False
+        leaves the contact-force store out."""
         a = abi.Go1StepArgs()
-        a.contact_forces = self.contact_forces.data_ptr()
+        a.contact_forces = self.contact_forces.data_ptr() if contact_forces else None
         a.extras_time_outs = self.extras_time_outs.data_ptr()
         for k in ("obs", "priv", "rew", "reset", "time_out"):
             v, ref = out[k], getattr(self, k)

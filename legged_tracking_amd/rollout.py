@@ -16,6 +16,7 @@ RCCL), the advantage statistics, the gradients and the KL estimate are
 all-reduced so that every rank follows the same optimisation trajectory as one
 large-batch run.
 """
+import contextlib
 import copy
 import ctypes as C
 import os
@@ -910,6 +911,21 @@ class PPO:
 
 
 # ----------------------------------------------------------------------------- runner
+@contextlib.contextmanager
+def _rollout_outputs(env):
+    """The rollout reads neither the contact forces nor the aux block (ppo_cse/__init__.py:164-214): the step leaves
+    both stores out (LeggedRobot.set_output_demand) while it runs, and they are back on afterwards."""
+    f = getattr(env, "set_output_demand", None)
+    if f is None:
+        yield
+        return
+    f(contact_forces=False, aux=False)
+    try:
+        yield
+    finally:
+        f(contact_forces=True, aux=True)
+
+
 class Runner:
     """Runner (ppo_cse/__init__.py:66-357): rollout of num_steps_per_env env steps per
     iteration, GAE, PPO update, checkpoints (ac_weights.pt + TorchScript adaptation
@@ -969,7 +985,7 @@ class Runner:
                                                              high=int(self.env.max_episode_length))
         for it in range(num_learning_iterations):
             start = time.time()
-            with torch.inference_mode():
+            with torch.inference_mode(), _rollout_outputs(self.env):
                 obs, privileged_obs, obs_history, infos = self.rollout(obs, privileged_obs, obs_history,
                                                                        update_model, eval_expert)
                 if update_model:

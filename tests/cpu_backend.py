@@ -55,7 +55,8 @@ class OracleBackend:
         out["rew"].copy_(torch.from_numpy(o["rew"]))
         out["reset"].copy_(torch.from_numpy(o["reset"].astype(bool)))
         out["time_out"].copy_(torch.from_numpy(o["time_out"].astype(bool)))
-        self.contact_forces.copy_(torch.from_numpy(o["contact_forces"]))
+        if kw.get("contact_forces", True):
+            self.contact_forces.copy_(torch.from_numpy(o["contact_forces"]))
         if o["reset"].any():
             self.extras_time_outs.copy_(torch.from_numpy(o["time_out"].astype(bool)))
         if episode_log is not None:

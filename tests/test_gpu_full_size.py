@@ -162,6 +162,43 @@ def test_env_fast_path_and_compact_log_match_generic_path():
         e.close()
 
 
+def test_output_demand_off_skips_the_stores_and_nothing_else():
+    """LeggedRobot.set_output_demand(False, False) (what Runner.learn sets while it collects rollouts): the step
+    leaves the contact-force and aux buffers untouched (sentinels survive) and everything else is bit-identical to an
+    env that stores them; reading them meanwhile raises; switched back on, the next step writes both and they equal
+    the other env's (4096 envs, prepared-args path)."""
+    from legged_tracking_amd import env as E
+    envs = []
+    for _ in range(2):
+        cfg = CF.readme_config(n_envs=N, terrain="single_path", rows=32, cols=32)
+        env = E.TrajectoryTrackingEnv(sim_device=DEV, cfg=cfg, seed=6)
+        env.reset()
+        envs.append(env)
+    off = envs[1]
+    off.set_output_demand(contact_forces=False, aux=False)
+    off._sim.contact_forces.fill_(float("nan"))
+    off._aux.fill_(float("nan"))
+    ring = torch.randn((8, N, 12), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+    for k in range(24):
+        outs = [e.step(ring[k % 8]) for e in envs]
+        for a, b in zip(outs[0][:3], outs[1][:3]):
+            assert torch.equal(a, b), k
+    for name in ("dof_pos", "dof_vel", "root"):
+        assert torch.equal(envs[0]._sim.state[name], off._sim.state[name]), name
+    torch.cuda.synchronize()
+    assert torch.isnan(off._sim.contact_forces).all() and torch.isnan(off._aux).all()
+    for name in ("contact_forces", "torques", "base_lin_vel", "foot_positions"):
+        with pytest.raises(RuntimeError):
+            getattr(off, name)
+    off.set_output_demand()
+    for e in envs:
+        e.step(ring[0])
+    assert torch.equal(envs[0].contact_forces, off.contact_forces)
+    assert torch.equal(envs[0].torques, off.torques) and torch.equal(envs[0].foot_positions, off.foot_positions)
+    for e in envs:
+        e.close()
+
+
 def test_full_size_height_scan_bit_exact_from_post_physics_pose():
     """The height scan (_get_heights :1918-1965: grid + base xy (+ camera offset), / horizontal_scale,
     .long() truncation, clip to [0, shape - 2], gather of both layers) against a numpy restatement

@@ -104,9 +104,15 @@ def test_runner_learns_and_writes_reference_checkpoints(tmp_path):
     try:
         runner = _runner(tmp_path)
         before = {k: v.clone() for k, v in runner.alg.actor_critic.state_dict().items()}
+        # the rollout steps with the contact-force and aux stores off (it reads neither), restored afterwards
+        inner, demand = runner.env.env, []
+        step = inner.step
+        inner.step = lambda a: (demand.append(inner._demand), step(a))[1]
         runner.learn(2, init_at_random_ep_len=True)
     finally:
         R.RunnerArgs.num_steps_per_env, R.PPO_Args.num_learning_epochs, R.PPO_Args.num_mini_batches = 24, 5, 4
+    assert len(demand) > 0
+    assert set(demand) == {(False, False)} and inner._demand == (True, True)
     after = runner.alg.actor_critic.state_dict()
     assert any(not torch.equal(before[k], after[k]) for k in before)
     ck = tmp_path / "checkpoints"

@@ -40,7 +40,10 @@ if [ "${PMC:-0}" = 1 ]; then
   timeout -k 10 1200 bash tools/profile.sh $TAG > $O/profile_sh.log 2>&1 || { echo "profile.sh failed"; tail -5 $O/profile_sh.log; exit 1; }
   [ -f "$ISA_MIX" ] && cp "$ISA_MIX" $O/step_isa_mix.json  # packed shares for the FLOP count (tools/isa_sections.py)
   python tools/prof_summary.py gpurun_out/prof_$TAG $O step go1_step_kernel > $O/prof_summary.log 2>&1 || { echo "summary failed"; tail -5 $O/prof_summary.log; exit 1; }
-  rm -rf gpurun_out/prof_$TAG  # raw counter CSVs of whole bench runs: far above what gpurun copies back
+  if [ -d gpurun_out/prof_${TAG}_rollout ]; then
+    python tools/prof_summary.py gpurun_out/prof_${TAG}_rollout $O step_rollout go1_step_kernel >> $O/prof_summary.log 2>&1 || { echo "rollout summary failed"; exit 1; }
+  fi
+  rm -rf gpurun_out/prof_$TAG gpurun_out/prof_${TAG}_rollout  # raw counter CSVs of whole bench runs: far above what gpurun copies back
   echo "pmc ok"; tail -8 $O/prof_summary.log
 fi
 if [ "${STAMPS:-0}" = 1 ]; then

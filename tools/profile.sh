@@ -22,4 +22,12 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_
 echo lds done
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 --output-format csv -d "$OUT/flop" -o flop -- python3 $B > "$OUT/flop.log" 2>&1 || { echo "flop rc=$?"; tail -20 "$OUT/flop.log"; }
 echo flop done
+# the rollout's stores (Runner.learn: no contact forces, no aux block): the kernel alone, HBM passes only
+if [ "${ROLLOUT_PASS:-1}" = 1 ]; then
+  R="$ROOT/gpurun_out/prof_${TAG}_rollout"; mkdir -p "$R"
+  K="$ROOT/bench.py --kernel-only --rollout-outputs --steps 300 --warmup 20"
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/fetch" -o fetch -- python3 $K > "$R/fetch.log" 2>&1 || { echo "rollout fetch rc=$?"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/write" -o write -- python3 $K > "$R/write.log" 2>&1 || { echo "rollout write rc=$?"; exit 1; }
+  echo rollout passes ok
+fi
 find "$OUT" -name "*.csv" | head -20
