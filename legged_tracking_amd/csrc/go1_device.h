@@ -1416,7 +1416,7 @@ struct Phys {
 // to 1e-5 m, ties to the lowest window position: a lexicographic maximum (associative: the same in any reduction
 // order, and the oracle's).  Every sim step a penalty force acts at the two chosen vertices where they penetrate
 // (face_force).  Scanning every sim step measured +3.7 k cycles per sim step per wave; the held choice is bounded
-// by tests/test_trunk_faces.py::test_held_face_vertex_matches_every_step_scan.
+// by tests/test_held_contacts.py (held vs every sim step in the f64 oracle).
 #define FACE_Q 1.0e-5f
 #define FACE_W 10
 __device__ __forceinline__ int face_key_max(int v) {  // max over the env's 16 lanes (quad, then the rows)

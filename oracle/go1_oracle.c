@@ -839,12 +839,14 @@ static void self_box_force(const real* pa, const real* va, real r, real R[3][3],
 #define FACE_W 10
 #define FACE_SIGNED 0.1
 static void face_scan(const TerrainView* T, real R[3][3], const real* pos, const real* th, int* sel) {
-  int ci = (int)floor(fmin(fmax(pos[0] / T->hs, -16000.0), 16000.0)), cj = (int)floor(fmin(fmax(pos[1] / T->hs, -16000.0), 16000.0));
+  /* (positions relative to the tile's origin (ox, oy): zero in the step, which integrates in terrain coordinates) */
+  const real px = pos[0] - T->ox, py = pos[1] - T->oy;
+  int ci = (int)floor(fmin(fmax(px / T->hs, -16000.0), 16000.0)), cj = (int)floor(fmin(fmax(py / T->hs, -16000.0), 16000.0));
   for (int hh = 0; hh < 2; ++hh) {
     int best = -1;
     for (int v = 0; v < FACE_W * FACE_W; ++v) {
       int i = ci + v % FACE_W - 4, j = cj + v / FACE_W - 4;
-      real d[3] = {i * T->hs - pos[0], j * T->hs - pos[1], tile_at(T, hh == 0 ? 1 : 0, i, j) - pos[2]}, c[3];
+      real d[3] = {i * T->hs - px, j * T->hs - py, tile_at(T, hh == 0 ? 1 : 0, i, j) - pos[2]}, c[3];
       for (int k = 0; k < 3; ++k) c[k] = R[0][k] * d[0] + R[1][k] * d[1] + R[2][k] * d[2];
       real pen = hh == 0 ? c[2] + th[2] : th[2] - c[2];
       if (!(fabs(c[0]) <= th[0] && fabs(c[1]) <= th[1] && pen > -FACE_SIGNED)) continue;
@@ -864,7 +866,8 @@ static void face_force(const TerrainView* T, const ContactParams* C, real R[3][3
   for (int hh = 0; hh < 2; ++hh) {
     if (sel[hh] < 0) continue;
     int i = (sel[hh] >> 16) - 16384, j = (sel[hh] & 0xffff) - 16384;
-    real d[3] = {i * T->hs - pos[0], j * T->hs - pos[1], tile_at(T, hh == 0 ? 1 : 0, i, j) - pos[2]}, c[3];
+    real d[3] = {i * T->hs - (pos[0] - T->ox), j * T->hs - (pos[1] - T->oy), tile_at(T, hh == 0 ? 1 : 0, i, j) - pos[2]},
+         c[3];
     for (int k = 0; k < 3; ++k) c[k] = R[0][k] * d[0] + R[1][k] * d[1] + R[2][k] * d[2];
     real pen = hh == 0 ? c[2] + th[2] : th[2] - c[2];
     if (!(fabs(c[0]) <= th[0] && fabs(c[1]) <= th[1] && pen > 0.0)) continue;
@@ -885,9 +888,15 @@ static void face_force(const TerrainView* T, const ContactParams* C, real R[3][3
 
 /* One integrator step of length h with torques tau.  Writes net contact forces
  * per reported body (17 x 3, world) into cf (may be NULL). */
+/* tests/test_held_contacts.py: make a held choice every sim step (bit 0: the trunk faces' vertices, bit 1: the
+ * capsules' deepest points), to measure what holding them for a control step changes */
+static int g_rescan_every_step = 0;
+void go1o_set_rescan_every_step(int mask) { g_rescan_every_step = mask; }
 static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, const real* tau, real h,
                          const real* g, real friction, real restitution, real payload, const TerrainView* T,
-                         real* cf, int face_scan_now) {
+                         real* cf, int scan_now) {
+  const int face_scan_now = scan_now || (g_rescan_every_step & 1);
+  const int seg_scan_now = scan_now || (g_rescan_every_step & 2);
   ContactParams C = {cfg->contact_stiffness, cfg->contact_damping, cfg->friction_damping, friction,
                      0.5 * (restitution + (real)cfg->terrain_restitution), cfg->bounce_threshold};
   real R[3][3];
@@ -1097,14 +1106,14 @@ static void phys_substep(const Model* M, const go1_config* cfg, PhysState* S, co
         const int slot = j == 0 ? 0 : 2 * j - 1 + p; /* hip; thigh 1, 2; calf 3, 4 */
         real t = 0.0;
         if (p != foot_seg) {
-          if (face_scan_now) S->seg_t[l][slot] = seg_deepest(T, wA, wB, rads[p], cell);
+          if (seg_scan_now) S->seg_t[l][slot] = seg_deepest(T, wA, wB, rads[p], cell);
           t = S->seg_t[l][slot];
         }
         for (int i = 0; i < 3; ++i) lp[i] = segs[p][0][i] + t * (segs[p][1][i] - segs[p][0][i]);
         point_kin(Rw[j], pw_[j], vj[l][j], lp, pw, vw);
         if (g_implicit_contact) {
           real Mp[3][3] = {{0}};
-          sphere_contact_im_cell(T, &C, pw, vw, rads[p], F, h, Mp, T->tile && face_scan_now && p != foot_seg ? cell : NULL);
+          sphere_contact_im_cell(T, &C, pw, vw, rads[p], F, h, Mp, T->tile && seg_scan_now && p != foot_seg ? cell : NULL);
           point_inertia(Rw[j], lp, Mp, &IA[j]);
         } else {
           sphere_contact(T, &C, pw, vw, rads[p], F);

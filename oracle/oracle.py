@@ -77,6 +77,14 @@ def seg_deepest(tile, hs, A, B, r):
     return f(tl.ctypes.data, int(tl.shape[1]), int(tl.shape[2]), hs, a.ctypes.data, b.ctypes.data, r)
 
 
+def set_rescan_every_step(faces=False, segments=False):
+    """Test knob (tests/test_held_contacts.py): choose the trunk faces' vertices / the capsules' deepest points every
+    sim step instead of once per control step (the kernel's and the oracle's default)."""
+    f = lib().go1o_set_rescan_every_step
+    f.argtypes = [C.c_int]
+    f(int(bool(faces)) | 2 * int(bool(segments)))
+
+
 def seg_closest(P0, P1, Q0, Q1):
     """(s, t): parameters of the closest points of the segments P0 -> P1 and Q0 -> Q1 (go1_oracle.c)."""
     st = np.zeros(2)
