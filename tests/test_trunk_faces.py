@@ -105,3 +105,37 @@ def test_face_contacts_follow_a_yawed_trunk_and_conserve_energy_without_damping_
     b["v"] = [0.0, 0.0, 0.5]
     _step(c, t, b, n=60)
     assert -0.5 < b["v"][2] < 0.0
+
+
+def test_apex_entering_the_face_during_the_control_step_acts_at_once():
+    """the scan at the control step's first sim step keeps the nearest vertex by signed depth, so an apex
+    5 mm above the top face when the trunk starts moving up at 1 m/s (5 mm per sim step) pushes back on the sim step
+    it enters, not a control step later."""
+    c = _cfg()
+    hs = float(c.horizontal_scale)
+    i0, j0 = 40, 20
+    x, y, z = i0 * hs + 0.012, j0 * hs + 0.01, 0.30
+    t = _tile(c)
+    t[0, i0, j0] = z + 0.057 + 0.005
+    forces = []
+    for n in (1, 2, 3, 4):  # n sim steps of one control step (the scan runs on the first)
+        b = _body(x, y, z)
+        b["v"] = [0.0, 0.0, 1.0]
+        forces.append(_step(c, t, b, n=n)[0][2])
+    assert forces[0] == 0.0
+    assert min(forces[2:]) < -20.0, forces
+
+
+def test_the_vertex_window_covers_a_face_end_at_45_degrees():
+    """at a yaw near 45 degrees the footprint reaches 0.166 m along both axes; an apex 10 mm inside the top
+    face near its end, 4 cells from the centre's cell on the short axis (outside a 10 x 8 window), is found."""
+    c = _cfg()
+    hs = float(c.horizontal_scale)
+    i0, j0 = 40, 20
+    yaw = 0.75
+    quat = (0.0, 0.0, np.sin(yaw / 2), np.cos(yaw / 2))
+    x, y, z = i0 * hs, (j0 + 0.9) * hs, 0.30
+    t = _tile(c)
+    t[0, i0 + 2, j0 + 4] = z + 0.057 - 0.010
+    cf = _step(c, t, _body(x, y, z, quat))
+    np.testing.assert_allclose(cf[0], [0.0, 0.0, -K_CONTACT * 0.010], rtol=1e-5, atol=1e-9)
