@@ -65,7 +65,9 @@ SURVEY_FLOPS_PER_ENV_STEP = 1.8e5
 
 # PMC-measured HBM bytes per launch of the step kernel (tools/profile.sh + tools/prof_summary.py;
 # FETCH_SIZE + WRITE_SIZE, separate --pmc passes).  Re-collected whenever the kernel changes.
-TRAFFIC_FILES = [os.path.join(REPO, "profiles", r, "step_counters.json") for r in ("r05", "r04", "r03", "r02", "r01")]
+TRAFFIC_FILES = [os.path.join(REPO, "profiles", r, "step_counters.json") for r in ("r06", "r05", "r04", "r03", "r02", "r01")]
+# the same kernel with the rollout's stores only (no contact forces, no aux block: Runner.learn's output demand)
+ROLLOUT_TRAFFIC_FILE = os.path.join(REPO, "profiles", "r06", "step_rollout_counters.json")
 
 
 def pmc_counters(n_envs):
@@ -87,6 +89,22 @@ def pmc_counters(n_envs):
         except (OSError, KeyError, ValueError, ZeroDivisionError):
             continue
     return dict(traffic=None, traffic_x2=None, written=None, flops=None, valu=None, src=None)
+
+
+def rollout_traffic(n_envs):
+    """HBM bytes per launch of the step kernel with the rollout's stores only (profiles/r06, tools/profile.sh)."""
+    try:
+        with open(ROLLOUT_TRAFFIC_FILE) as f:
+            d = json.load(f)
+        if int(d["resources"]["Grid_Size"]) != 16 * n_envs:
+            return None
+        h = d["hbm_bytes_per_launch"]
+        return {"traffic": h["traffic"], "written": h["write"], "over_algorithmic": h["traffic"] / (3522 * n_envs),
+                "written_per_env_step": h["write"] / n_envs, "source": os.path.relpath(ROLLOUT_TRAFFIC_FILE, REPO),
+                "what": "bench.py --kernel-only --rollout-outputs: the rollout's stores (Runner.learn switches the "
+                        "contact-force and aux stores off, LeggedRobot.set_output_demand)"}
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
 
 
 def hip():
@@ -603,6 +621,7 @@ def main():
                          "traffic_over_algorithmic_fetch_doubled": ratio(pmc["traffic_x2"], alg),
                          "write_traffic_over_algorithmic_writes": ratio(pmc["written"], 1758 * n),
                          "traffic_source": pmc["src"],
+                         "traffic_rollout_outputs": rollout_traffic(n),
                          "algorithmic_bytes_per_launch": alg, "bytes_per_env_step": SURVEY_BYTES_PER_ENV_STEP,
                          "bytes_source": "SURVEY.md 8(d): 3,522 B per env-step",
                          "bytes_written_by_path": {"bytes_per_env_step": PATH_BYTES_PER_ENV_STEP,

@@ -1579,6 +1579,7 @@ __device__ __forceinline__ float seg_box_t(const float* P0, const float* P1, con
     d[i] = R[i] * (P1[0] - P0[0]) + R[3 + i] * (P1[1] - P0[1]) + R[6 + i] * (P1[2] - P0[2]);
   }
   float lo = 0.0f, hi = 1.0f;
+#pragma unroll
   for (int it = 0; it < SEG_BISECT; ++it) {
     const float m = 0.5f * (lo + hi);
     float so = 0.0f, qmax = -1e30f, sin = 0.0f;
@@ -1603,7 +1604,7 @@ __device__ __forceinline__ float seg_box_t(const float* P0, const float* P1, con
 // (own_first false), and the own primitive's point (world).  A, B: (P0 r, P1, V0, V1) records in LDS, so the two
 // lanes of a pair compute the same bits and apply exactly opposite forces.
 __device__ __forceinline__ void self_pair_force(const float4* A, const float4* B, bool own_first, float ks, float ds,
-                                                float* F, float* pown) {
+                                                float* F, float* pown, bool& touch) {
   const float4 a0 = A[0], a1 = A[1], b0 = B[0], b1 = B[1];
   const float pa0[3] = {a0.x, a0.y, a0.z}, da[3] = {a1.x - a0.x, a1.y - a0.y, a1.z - a0.z};
   const float pb0[3] = {b0.x, b0.y, b0.z}, db[3] = {b1.x - b0.x, b1.y - b0.y, b1.z - b0.z};
@@ -1613,6 +1614,12 @@ __device__ __forceinline__ void self_pair_force(const float4* A, const float4* B
   const float pb[3] = {pb0[0] + t * db[0], pb0[1] + t * db[1], pb0[2] + t * db[2]};
   const float d0 = pa[0] - pb[0], d1 = pa[1] - pb[1], d2 = pa[2] - pb[2];
   const float dd = d0 * d0 + d1 * d1 + d2 * d2, rs = a0.w + b0.w;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { pown[i] = own_first ? pa[i] : pb[i]; F[i] = 0.0f; }
+  touch = dd < rs * rs;
+  // the spring only where some lane of the wave has an overlap (most pairs the boxes let through do not touch; a
+  // pair that does not has no force, so skipping it changes nothing)
+  if (!__any(touch)) return;
   const float inv = dd > 1e-18f ? frsq(dd) : 0.0f;
   const float n0 = dd > 1e-18f ? d0 * inv : 0.0f, n1 = dd > 1e-18f ? d1 * inv : 0.0f, n2 = dd > 1e-18f ? d2 * inv : 1.0f;
   const float pen = rs - dd * inv;
@@ -1622,11 +1629,9 @@ __device__ __forceinline__ void self_pair_force(const float4* A, const float4* B
   const float vr2 = (va0.z + s * (va1.z - va0.z)) - (vb0.z + t * (vb1.z - vb0.z));
   const float vn = vr0 * n0 + vr1 * n1 + vr2 * n2;
   float fn = ks * pen - ds * vn;
-  fn = (dd < rs * rs && fn > 0.0f) ? fn : 0.0f;
+  fn = (touch && fn > 0.0f) ? fn : 0.0f;
   fn = own_first ? fn : -fn;
   F[0] = fn * n0; F[1] = fn * n1; F[2] = fn * n2;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) pown[i] = own_first ? pa[i] : pb[i];
 }
 
 // sphere A (centre, radius in w) against the trunk box (half extents th about the base origin): the force on A (world)
@@ -1756,15 +1761,30 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
     const int ip = 4 * (leg ^ (bit >> 2)) + (bit & 3);
     const bool first = io < ip;
     float F[3], p[3];
-    self_pair_force(Pr + 4 * min(io, ip), Pr + 4 * max(io, ip), first, ks, ds, F, p);
-    const float Fw[3] = {act ? F[0] : 0.0f, act ? F[1] : 0.0f, act ? F[2] : 0.0f};
-    acc(p, Fw);
+    bool touch;
+    self_pair_force(Pr + 4 * min(io, ip), Pr + 4 * max(io, ip), first, ks, ds, F, p, touch);
+    if (__any(act && touch)) {
+      const float Fw[3] = {act ? F[0] : 0.0f, act ? F[1] : 0.0f, act ? F[2] : 0.0f};
+      acc(p, Fw);
+    }
   }
   MARK(self_pairs_done);
-  // the trunk box, for a folded leg's thigh, calf and foot (the hip is the trunk's neighbour)
-  if (__any(((mask >> (6 + leg)) & 1) && role != 1)) {
-    const bool on = ((mask >> (6 + leg)) & 1) && role != 1;
-    const float4 O0 = Pr[4 * io], O1 = Pr[4 * io + 1], O2 = Pr[4 * io + 2], O3 = Pr[4 * io + 3];
+  // the trunk box, for a folded leg's thigh, calf and foot (the hip is the trunk's neighbour) whose segment's
+  // trunk-frame AABB, grown by its radius, meets the box (the fold gate is coarse: most folded links are far from
+  // the trunk, and a link that misses the grown box has no force -- skipping it changes nothing)
+  const float4 O0 = Pr[4 * io], O1 = Pr[4 * io + 1];
+  bool on = ((mask >> (6 + leg)) & 1) && role != 1;
+  {
+    const float w0[3] = {O0.x - pos[0], O0.y - pos[1], O0.z - pos[2]}, w1[3] = {O1.x - pos[0], O1.y - pos[1], O1.z - pos[2]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float c0 = R[i] * w0[0] + R[3 + i] * w0[1] + R[6 + i] * w0[2];
+      const float c1 = R[i] * w1[0] + R[3 + i] * w1[1] + R[6 + i] * w1[2];
+      on = on && fminf(c0, c1) - O0.w <= th[i] && fmaxf(c0, c1) + O0.w >= -th[i];
+    }
+  }
+  if (__any(on)) {
+    const float4 O2 = Pr[4 * io + 2], O3 = Pr[4 * io + 3];
     const float P0[3] = {O0.x, O0.y, O0.z}, P1[3] = {O1.x, O1.y, O1.z};
     const float u = role == 3 ? 0.0f : seg_box_t(P0, P1, R, pos, th);
     const float4 C = make_float4(O0.x + u * (O1.x - O0.x), O0.y + u * (O1.y - O0.y), O0.z + u * (O1.z - O0.z), O0.w);
