@@ -2035,7 +2035,11 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
     const int mask = 0;
 #endif
     MARK(self_broad_done);
+#ifdef GO1_ABL_NO_NARROW  // ablation build only: the broad phase runs, the narrow phase never does
+    if (__any(mask != 0) && mask == 12345) {
+#else
     if (__any(mask != 0)) {
+#endif
       // the lane's own primitive (its x half's link): the whole segment, ends and their velocities (world)
       float P0[3], P1[3], V0[3], V1[3];
       {
