@@ -176,7 +176,7 @@ def test_self_contact_forces_of_colliding_states(pool_kind):
     err = np.abs(cf - ref)
     print(f"force error p99 {np.percentile(err, 99):.2e} N, max {err.max():.2e} N")
     assert np.percentile(err, 99) <= 1e-3, np.percentile(err, 99)
-    # round 6, capsules: a capsule's point nearest the trunk box comes from a golden-section search, and the f32 build
+    # round 6, capsules: a capsule's point nearest the trunk box comes from a bisection on its slope, and the f32 build
     # of the oracle itself lands 0.023 N (folded pool) / 0.042 N (within limits) from the f64 one at worst
     np.testing.assert_allclose(cf, ref, rtol=1e-3, atol=0.05)
     # internal forces: the per-env sum over the bodies vanishes
