@@ -1162,7 +1162,7 @@ struct SegBest {
   int cell;  // and its cell and triangle
 };
 __device__ __forceinline__ void seg_offer(SegBest& sb, f2 h, float z, float r, float t, int cell, bool valid) {
-  const int q = max(seg_quant((h.x - z) + r), seg_quant((z - h.y) + r));
+  const int q = seg_quant(fmaxf((h.x - z) + r, (z - h.y) + r));  // (the quantisation is monotone: = the max of both)
   const int key = q * 4096 + (4095 - (int)floorf(t * 4095.0f));
   const bool up = valid && key > sb.key;  // an equal key (a vertex on several edges) keeps the first offer
   sb.key = up ? key : sb.key;
@@ -1177,9 +1177,10 @@ __device__ __forceinline__ void verts_fetch(const Terr& T, const int* vi, const 
   if (T.patch) {
 #pragma unroll
     for (int n = 0; n < N; ++n) {
-      const int li = vi[n] - T.pi0, lj = vj[n] - T.pj0;
-      const bool in = li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
-      const float2 q = T.patch[min(max(li, 0), PSZX - 1) * PSZY + min(max(lj, 0), PSZY - 1)];
+      // (unsigned: a negative offset is out of range too; outside the patch read cell 0, replaced below)
+      const unsigned li = (unsigned)(vi[n] - T.pi0), lj = (unsigned)(vj[n] - T.pj0);
+      const bool in = li < (unsigned)PSZX && lj < (unsigned)PSZY;
+      const float2 q = T.patch[in ? (int)(li * PSZY + lj) : 0];
       h[n] = f2{q.x, q.y};
       out |= in ? 0u : 1u << n;
     }
