@@ -1732,6 +1732,9 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
     const float olx = fminf(O0.x, O1.x) - O0.w, ohx = fmaxf(O0.x, O1.x) + O0.w;
     const float oly = fminf(O0.y, O1.y) - O0.w, ohy = fmaxf(O0.y, O1.y) + O0.w;
     const float olz = fminf(O0.z, O1.z) - O0.w, ohz = fmaxf(O0.z, O1.z) + O0.w;
+#ifdef GO1_ABL_NO_TESTLOOP  // ablation build only: no partner tests (and so no pairs)
+    cand = 0u;
+#endif
     while (__any(cand != 0u)) {
       const bool act = cand != 0u;
       const int d = act ? __builtin_ctz(cand) : 0;
@@ -1755,6 +1758,9 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
     }
   }
   MARK(self_tests_done);
+#ifdef GO1_ABL_NO_PAIRLOOP  // ablation build only: the pairs tested but never evaluated
+  work = 0u;
+#endif
   while (__any(work != 0u)) {
     const bool act = work != 0u;
     const int bit = act ? __builtin_ctz(work) : 0;
@@ -1774,7 +1780,11 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
   // trunk-frame AABB, grown by its radius, meets the box (the fold gate is coarse: most folded links are far from
   // the trunk, and a link that misses the grown box has no force -- skipping it changes nothing)
   const float4 O0 = Pr[4 * io], O1 = Pr[4 * io + 1];
+#ifdef GO1_ABL_NO_BOXPHASE  // ablation build only: no capsule-box pairs
+  bool on = false;
+#else
   bool on = ((mask >> (6 + leg)) & 1) && role != 1;
+#endif
   {
     const float w0[3] = {O0.x - pos[0], O0.y - pos[1], O0.z - pos[2]}, w1[3] = {O1.x - pos[0], O1.y - pos[1], O1.z - pos[2]};
 #pragma unroll
