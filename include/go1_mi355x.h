@@ -152,7 +152,7 @@ typedef struct go1_config {
   float hip_scale_reduction;   /* 0.5 */
   float clip_actions;          /* 10 (train.py:241) */
   float clip_obs;              /* 100 */
-  float horizontal_scale;      /* 0.05 */
+  float horizontal_scale;      /* 0.05 (>= 0.05 required with terrain_kind 1) */
   float max_episode_length;    /* ceil(episode_length_s / dt) = 500 */
   float terminal_body_height;  /* 0.0 */
   float switch_dist;           /* 0.3 (train.py:169) */
@@ -314,6 +314,9 @@ int go1_abi_version(void);
  * lets a foreign binding (ctypes / cgo / JNI) verify its struct mirrors. */
 void go1_abi_sizes(int64_t out[4]);
 const char* go1_last_error(void);
+/* Checks the config (GO1_E_ARG with go1_last_error for anything the kernels do not implement; among them a
+ * heightfield finer than horizontal_scale = 0.05 m, where a capsule half-link could cross more grid lines than
+ * the terrain search's candidates cover) and allocates the handle. */
 int go1_create(const go1_config* cfg, go1_handle** out);
 /* Binds the caller's state planes (never copied, allocated or freed).  planes: GO1_STATE_PLANES
  * descriptors, go1_state order, required. */
