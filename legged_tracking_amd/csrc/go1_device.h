@@ -1735,6 +1735,9 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
 #ifdef GO1_ABL_NO_TESTLOOP  // ablation build only: no partner tests (and so no pairs)
     cand = 0u;
 #endif
+#ifdef GO1_ABL_RT_NO_TESTLOOP  // ablation build only: the same, decided at run time (the code stays)
+    cand = cfg->self_stiffness > 1e30f ? cand : 0u;
+#endif
     while (__any(cand != 0u)) {
       const bool act = cand != 0u;
       const int d = act ? __builtin_ctz(cand) : 0;
@@ -1760,6 +1763,9 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
   MARK(self_tests_done);
 #ifdef GO1_ABL_NO_PAIRLOOP  // ablation build only: the pairs tested but never evaluated
   work = 0u;
+#endif
+#ifdef GO1_ABL_RT_NO_PAIRLOOP  // ablation build only: the same, decided at run time (the code stays)
+  work = cfg->self_stiffness > 1e30f ? work : 0u;
 #endif
   while (__any(work != 0u)) {
     const bool act = work != 0u;
