@@ -995,7 +995,7 @@ struct CP {
 
 // ---- packed (v_pk_*_f32) contact: one wave issues a v_pk_fma_f32 (two FMAs) as fast as a
 // v_fma_f32 (tools/probes/pk_rate.hip), so the floor and ceiling layers of a point are
-// carried as the two halves of an f2 all the way from the bilinear patch to the force.
+// carried as the two halves of an f2 all the way from the mesh triangle to the force.
 __device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
 
 // (floor, ceiling) at the four corners of cell (i, j): the LDS patch, or the tile outside it
@@ -1408,7 +1408,7 @@ struct Phys {
 // ---- the trunk box's faces against the heightfields (go1.urdf:53-58, the 0.3762 x 0.0935 x 0.114
 // box; tunnel_fn.py:99-163, the ceiling's downward wedges).  The 8 box corners are contact points of the sub-step
 // (above); a wedge apex or ridge that enters a face between its corners is a grid vertex of the heightfield
-// inside the face's footprint (bilinear cells: a face's deepest point against them is a vertex or on the
+// inside the face's footprint (mesh triangles: a face's deepest point against them is a vertex or on the
 // footprint's boundary).  Once per control step the env's 16 lanes scan the 10 x 10 vertices around the trunk
 // (offsets -4 .. +5 on both axes: they hold the footprint's +-0.166 m at any yaw wherever the centre sits in its
 // cell; 7 per lane, both layers in the halves: floor against the bottom face, ceiling against the top
