@@ -1559,12 +1559,15 @@ __device__ __forceinline__ void seg_closest(const float* P0, const float* d1, co
   const float den = n[0] * n[0] + n[1] * n[1] + n[2] * n[2], num = n[0] * m[0] + n[1] * m[1] + n[2] * m[2];
   const bool pa = a > 1e-12f, pe = e > 1e-12f;
   const float ia = pa ? frcp(a) : 0.0f, ie = pe ? frcp(e) : 0.0f;
-  float ss = den > 1e-10f * a * e ? clampf(num * frcp(den), 0.0f, 1.0f) : 0.0f;
-  float tt = (b * ss + f) * ie;
-  ss = tt < 0.0f ? clampf(-c * ia, 0.0f, 1.0f) : (tt > 1.0f ? clampf((b - c) * ia, 0.0f, 1.0f) : ss);
-  tt = clampf(tt, 0.0f, 1.0f);
-  s = !pa ? 0.0f : (!pe ? clampf(-c * ia, 0.0f, 1.0f) : ss);
-  t = !pe ? 0.0f : (!pa ? clampf(f * ie, 0.0f, 1.0f) : tt);
+  // every candidate computed, then selected (v_med3 clamps): as ternaries around the clamps the compiler had
+  // made exec-mask branches of them, one wave paying each arm plus the hazard nops
+  const float s0 = den > 1e-10f * a * e ? __builtin_amdgcn_fmed3f(num * frcp(den), 0.0f, 1.0f) : 0.0f;
+  const float tt = (b * s0 + f) * ie;
+  const float s_lo = __builtin_amdgcn_fmed3f(-c * ia, 0.0f, 1.0f), s_hi = __builtin_amdgcn_fmed3f((b - c) * ia, 0.0f, 1.0f);
+  const float ss = tt < 0.0f ? s_lo : (tt > 1.0f ? s_hi : s0);
+  const float t_pt = __builtin_amdgcn_fmed3f(f * ie, 0.0f, 1.0f);
+  s = !pa ? 0.0f : (!pe ? s_lo : ss);
+  t = !pe ? 0.0f : (!pa ? t_pt : __builtin_amdgcn_fmed3f(tt, 0.0f, 1.0f));
 }
 
 // the point of the segment P0 -> P1 (world) nearest the trunk box, deepest inside it: bisection on the sign of the
