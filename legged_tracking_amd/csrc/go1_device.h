@@ -1718,7 +1718,7 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
   unsigned cand = ((mask >> (10 + leg)) & 1) | (((mask >> lp1) & 1) << 1) | (((mask >> lp2) & 1) << 2) |
                   (((mask >> lp3) & 1) << 3);
   // the own leg's partners of primitive `role`: thigh - foot, hip - calf / foot, calf - hip, foot - thigh / hip
-  const unsigned keep_same = role == 0 ? 0x8u : (role == 1 ? 0xCu : (role == 2 ? 0x2u : 0x3u));
+  const unsigned keep_same = (0x32C8u >> (4 * role)) & 0xFu;  // role 0: 0x8, 1: 0xC, 2: 0x2, 3: 0x3
   auto acc = [&](const float* p, const float* F) {  // force F (world) on the own primitive at p
     const float p0 = p[0] - pb[0], p1 = p[1] - pb[1], p2 = p[2] - pb[2];
     Fo[0] += F[0]; Fo[1] += F[1]; Fo[2] += F[2];
@@ -2025,15 +2025,15 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const float hyA = i == 1 ? msy * hip_y0 : 0.0f, hyB = i == 1 ? msy * hip_y1 : 0.0f;
-        const float xa = role == 0 ? 0.0f : (role == 1 ? hyA : (role == 2 ? 0.0f : foot[i]));
-        const float xb = role == 0 ? 0.5f * kn[i] : (role == 1 ? hyB : (role == 2 ? 0.5f * foot[i] : foot[i]));
-        const float ya = role == 0 ? kn[i] : (role == 2 ? foot[i] : crn[role >> 1][i]);
-        const float yb = role == 0 ? 0.5f * kn[i] : (role == 2 ? 0.5f * foot[i] : crn[role >> 1][i]);
+        // (sel4: bit-test selects; equality chains on role compile to divergent branches)
+        const float xa = sel4(role, 0.0f, hyA, 0.0f, foot[i]);
+        const float xb = sel4(role, 0.5f * kn[i], hyB, 0.5f * foot[i], foot[i]);
+        const float ya = sel4(role, kn[i], crn[0][i], foot[i], crn[1][i]);
+        const float yb = sel4(role, 0.5f * kn[i], crn[0][i], 0.5f * foot[i], crn[1][i]);
         lpA[i] = f2{xa, ya};
         lpB[i] = f2{xb, yb};
       }
-      rr = f2{role == 0 ? thigh_r : (role == 1 ? hip_r : (role == 2 ? calf_r : foot_r)),
-              role == 0 ? thigh_r : (role == 2 ? calf_r : 0.0f)};
+      rr = f2{sel4(role, thigh_r, hip_r, calf_r, foot_r), sel4(role, thigh_r, 0.0f, calf_r, 0.0f)};
     }
     // self-collision first (few values live yet): the broad phase, and the narrow phase in a wave with a candidate
     float wb[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, Mo[3] = {0.0f, 0.0f, 0.0f};
@@ -2068,8 +2068,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           const float hy0 = i == 1 ? msy * hip_y0 : 0.0f, hy1 = i == 1 ? msy * hip_y1 : 0.0f;
-          e[i] = f2{role == 1 ? hy0 : (role == 3 ? foot[i] : 0.0f),
-                    role == 0 ? kn[i] : (role == 1 ? hy1 : foot[i])};
+          e[i] = f2{sel4(role, 0.0f, hy0, 0.0f, foot[i]), sel4(role, kn[i], hy1, foot[i], foot[i])};
         }
         const float w[3] = {vs[0].x, vs[1].x, vs[2].x};
         const f2 wl[3] = {w[1] * e[2] - w[2] * e[1], w[2] * e[0] - w[0] * e[2], w[0] * e[1] - w[1] * e[0]};
@@ -2083,7 +2082,7 @@ __device__ __forceinline__ void phys_substep(CCfg* __restrict__ cfg, const float
       }
       // bounding radius: half the link's segment (thigh, calf: half the knee / foot offset; hip: half the capsule's
       // segment; foot: a point) plus its radius
-      const float half = role == 0 ? 0.5f * fabsf(origin[8]) : (role == 1 ? 0.5f * (hip_y1 - hip_y0) : (role == 2 ? 0.5f * fabsf(foot[2]) : 0.0f));
+      const float half = sel4(role, 0.5f * fabsf(origin[8]), 0.5f * (hip_y1 - hip_y0), 0.5f * fabsf(foot[2]), 0.0f);
       self_put(self_sc, leg, role, P0, P1, rr.x, half + rr.x, V0, V1);
       // the block is this one wave (TPB 64): the other lanes' primitives are visible once the wave's own LDS
       // writes completed -- no s_barrier, and above all no vmcnt(0) drain of the terrain loads in flight
