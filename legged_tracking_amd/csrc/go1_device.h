@@ -999,17 +999,23 @@ struct CP {
 __device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
 
 // (floor, ceiling) at the four corners of cell (i, j): the LDS patch, or the tile outside it
+// (the patch read unconditionally, the tile only in a wave with a lane outside the patch: as an if / else per lane
+// the two paths were exec-mask branches every call)
 __device__ __forceinline__ void cell_fetch(const Terr& T, int i, int j, f2& c00, f2& c10, f2& c01, f2& c11) {
-  const int li = i - T.pi0, lj = j - T.pj0;
-  if (T.patch && li >= 0 && li < PSZX - 1 && lj >= 0 && lj < PSZY - 1) {
-    const float2* pp = T.patch + li * PSZY + lj;
+  const unsigned li = (unsigned)(i - T.pi0), lj = (unsigned)(j - T.pj0);
+  const bool in = T.patch && li < (unsigned)(PSZX - 1) && lj < (unsigned)(PSZY - 1);
+  if (T.patch) {
+    const float2* pp = T.patch + (in ? (int)(li * PSZY + lj) : 0);
     const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];
     c00 = f2{q00.x, q00.y}; c01 = f2{q01.x, q01.y}; c10 = f2{q10.x, q10.y}; c11 = f2{q11.x, q11.y};
-  } else {
-    c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
-    c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
-    c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
-    c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
+  }
+  if (__any(!in)) {
+    if (!in) {
+      c00 = f2{tile_at(T, 1, i, j), tile_at(T, 0, i, j)};
+      c10 = f2{tile_at(T, 1, i + 1, j), tile_at(T, 0, i + 1, j)};
+      c01 = f2{tile_at(T, 1, i, j + 1), tile_at(T, 0, i, j + 1)};
+      c11 = f2{tile_at(T, 1, i + 1, j + 1), tile_at(T, 0, i + 1, j + 1)};
+    }
   }
 }
 
