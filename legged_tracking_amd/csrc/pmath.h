@@ -58,35 +58,28 @@ PM_FN void pm_sincosf(float x, float* s, float* c) {
 PM_FN float pm_sinf(float x) { float s, c; pm_sincosf(x, &s, &c); return s; }
 PM_FN float pm_cosf(float x) { float s, c; pm_sincosf(x, &s, &c); return c; }
 
+/* asin / atan / atan2 with every case computed and the result selected: as if / else on the argument's range the
+ * cases were exec-mask branches, one wave paying each arm (and its IEEE division) in turn.  The arithmetic of each
+ * case is unchanged (atan's third case divides by 1.0, which is exact), so the results are bit for bit those of the
+ * branching form and of oracle/portable_math.h. */
 PM_FN float pm_asinf(float x) {
-  float a = fabsf(x), z, s;
-  int big = a > 0.5f;
-  if (big) {
-    z = 0.5f * (1.0f - a);
-    s = sqrtf(z);
-  } else {
-    z = a * a;
-    s = a;
-  }
+  const float a = fabsf(x);
+  const bool big = a > 0.5f;
+  const float zb = 0.5f * (1.0f - a);
+  const float z = big ? zb : a * a, s = big ? sqrtf(zb) : a;
   float p = fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
                       7.4953002686e-2f), z, 1.6666752422e-1f);
   float r = fmaf(p * z, s, s);
-  if (big) r = PM_PIO2 - (r + r);
+  r = big ? PM_PIO2 - (r + r) : r;
   return copysignf(r, x);
 }
 
 PM_FN float pm_atanf(float x) {
-  float a = fabsf(x), y0, t;
-  if (a > 2.414213562373095f) {
-    y0 = PM_PIO2;
-    t = -1.0f / a;
-  } else if (a > 0.4142135623730950f) {
-    y0 = PM_PIO4;
-    t = (a - 1.0f) / (a + 1.0f);
-  } else {
-    y0 = 0.0f;
-    t = a;
-  }
+  const float a = fabsf(x);
+  const bool big = a > 2.414213562373095f, mid = a > 0.4142135623730950f;
+  const float y0 = big ? PM_PIO2 : (mid ? PM_PIO4 : 0.0f);
+  const float num = big ? -1.0f : (mid ? a - 1.0f : a), den = big ? a : (mid ? a + 1.0f : 1.0f);
+  const float t = num / den;
   float z = t * t;
   float p = fmaf(fmaf(fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f), z,
                  -3.33329491539e-1f);
@@ -95,13 +88,11 @@ PM_FN float pm_atanf(float x) {
 }
 
 PM_FN float pm_atan2f(float y, float x) {
-  if (x == 0.0f) {
-    if (y == 0.0f) return __builtin_signbit(x) ? copysignf(PM_PI, y) : copysignf(0.0f, y);
-    return copysignf(PM_PIO2, y);
-  }
-  float r = pm_atanf(y / x);
-  if (x < 0.0f) r = (y < 0.0f || (y == 0.0f && __builtin_signbit(y))) ? r - PM_PI : r + PM_PI;
-  return r;
+  const float r0 = pm_atanf(y / x);  // (x = 0: inf or NaN, selected away below)
+  const bool yneg = y < 0.0f || (y == 0.0f && __builtin_signbit(y));
+  const float r1 = x < 0.0f ? (yneg ? r0 - PM_PI : r0 + PM_PI) : r0;
+  const float rz = y == 0.0f ? (__builtin_signbit(x) ? copysignf(PM_PI, y) : copysignf(0.0f, y)) : copysignf(PM_PIO2, y);
+  return x == 0.0f ? rz : r1;
 }
 
 /* ---- softsign x / (|x| + 1) of the actuator net, bit-identical to the IEEE quotient for
