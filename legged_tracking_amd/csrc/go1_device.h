@@ -1084,7 +1084,7 @@ __device__ __forceinline__ void hq_finish(const Terr& T, const HQ& q, f2& h, f2&
 // e = 0 leaves the force bit for bit as before.
 __device__ __forceinline__ f2 restitute(const CP& C, float h, f2 vn, f2 fn) {
   const float cr = (h * C.k + C.d) * C.e;
-  return f2{(C.e > 0.0f && vn.x > C.vb) ? fn.x + cr * vn.x : fn.x, (C.e > 0.0f && vn.y > C.vb) ? fn.y + cr * vn.y : fn.y};
+  return f2{(C.e > 0.0f & vn.x > C.vb) ? fn.x + cr * vn.x : fn.x, (C.e > 0.0f & vn.y > C.vb) ? fn.y + cr * vn.y : fn.y};
 }
 
 // The same contact, linearly implicit in the point velocity (the integrator's scheme: one 5 ms step
@@ -1117,9 +1117,9 @@ __device__ __forceinline__ void sphere_contact_im(const Terr& T, const HQ& q, co
   const f2 vtn = vt2 * ivt;
   const f2 cm = C.mu * fn0;
   // c_t = min(kf, mu fn0 / |vt|); kf in the viscous limit |vt| -> 0
-  const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
-                   (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
-  const bool ax = dv.x > 0.0f && fn0.x > 0.0f, ay = dv.y > 0.0f && fn0.y > 0.0f;
+  const f2 ct = f2{(C.kf * vtn.x > cm.x & vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
+                   (C.kf * vtn.y > cm.y & vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
+  const bool ax = dv.x > 0.0f & fn0.x > 0.0f, ay = dv.y > 0.0f & fn0.y > 0.0f;
   const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f};
   const f2 sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
   const f2 Fx = fa * nx - sc * vtx, Fy = fa * ny - sc * vty, Fz = fa * nz - sc * vtz;
@@ -1455,7 +1455,7 @@ __device__ __forceinline__ void face_scan(const Terr& T, const float* R, const f
     const f2 pen = f2{cz.x + th[2], th[2] - cz.y};  // floor vertex above the bottom face / ceiling below the top
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const bool in = inp && fabsf(cx[hh]) <= th[0] && fabsf(cy[hh]) <= th[1] && pen[hh] > -FACE_SIGNED;
+      const bool in = inp & fabsf(cx[hh]) <= th[0] & fabsf(cy[hh]) <= th[1] & pen[hh] > -FACE_SIGNED;
       const int q = (int)floorf(fminf(pen[hh] + FACE_SIGNED, 10.0f) * (1.0f / FACE_Q));  // signed depth, offset
       const int k = in ? (q << 7) | (127 - v) : -1;
       key[hh] = max(key[hh], k);
@@ -1481,7 +1481,7 @@ __device__ __forceinline__ void face_force(const Terr& T, const CP& C, const flo
   for (int hh = 0; hh < 2; ++hh) {
     const int i = (sel[hh] >> 16) - 16384, j = (sel[hh] & 0xffff) - 16384;
     const int li = i - T.pi0, lj = j - T.pj0;
-    ok[hh] = sel[hh] >= 0 && li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
+    ok[hh] = sel[hh] >= 0 & li >= 0 & li < PSZX & lj >= 0 & lj < PSZY;
     const float2 hv = T.patch[min(max(li, 0), PSZX - 1) * PSZY + min(max(lj, 0), PSZY - 1)];
     const float dx = (float)i * T.hs - pos[0], dy = (float)j * T.hs - pos[1], dz = (hh == 0 ? hv.x : hv.y) - pos[2];
     cx[hh] = (R[0] * dx + R[3] * dy) + R[6] * dz;
@@ -1491,7 +1491,7 @@ __device__ __forceinline__ void face_force(const Terr& T, const CP& C, const flo
   const f2 pen = f2{cz.x + th[2], th[2] - cz.y};
   bool act[2];
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) act[hh] = ok[hh] && fabsf(cx[hh]) <= th[0] && fabsf(cy[hh]) <= th[1] && pen[hh] > 0.0f;
+  for (int hh = 0; hh < 2; ++hh) act[hh] = ok[hh] & fabsf(cx[hh]) <= th[0] & fabsf(cy[hh]) <= th[1] & pen[hh] > 0.0f;
   if (!__any(act[0] || act[1])) return;
   const f2 nz = f2{1.0f, -1.0f};
   // the trunk's velocity at the vertex, base frame: v + w x c
@@ -1502,9 +1502,9 @@ __device__ __forceinline__ void face_force(const Terr& T, const CP& C, const flo
   const f2 vt2 = vx * vx + vy * vy;
   const f2 ivt = f2{frsq(fmaxf(vt2.x, 1e-18f)), frsq(fmaxf(vt2.y, 1e-18f))};
   const f2 vtn = vt2 * ivt, cm = C.mu * fn;
-  const f2 ct = f2{(C.kf * vtn.x > cm.x && vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
-                   (C.kf * vtn.y > cm.y && vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
-  const bool ax = act[0] && fn.x > 0.0f, ay = act[1] && fn.y > 0.0f;
+  const f2 ct = f2{(C.kf * vtn.x > cm.x & vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
+                   (C.kf * vtn.y > cm.y & vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
+  const bool ax = act[0] & fn.x > 0.0f, ay = act[1] & fn.y > 0.0f;
   const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f}, sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
   const f2 Fx = -(sc * vx), Fy = -(sc * vy), Fz = fa * nz;
   const f2 mx = cy * Fz - cz * Fy, my = cz * Fx - cx * Fz, mz = cx * Fy - cy * Fx;
@@ -1639,7 +1639,7 @@ __device__ __forceinline__ void self_pair_force(const float4* A, const float4* B
   const float vr2 = (va0.z + s * (va1.z - va0.z)) - (vb0.z + t * (vb1.z - vb0.z));
   const float vn = vr0 * n0 + vr1 * n1 + vr2 * n2;
   float fn = ks * pen - ds * vn;
-  fn = (touch && fn > 0.0f) ? fn : 0.0f;
+  fn = (touch & fn > 0.0f) ? fn : 0.0f;
   fn = own_first ? fn : -fn;
   F[0] = fn * n0; F[1] = fn * n1; F[2] = fn * n2;
 }
@@ -1683,7 +1683,7 @@ __device__ __forceinline__ void self_box_force(const float4 A, const float4 Av, 
   for (int i = 0; i < 3; ++i) va[i] = R[i] * Av.x + R[3 + i] * Av.y + R[6 + i] * Av.z;
   const float vn = (va[0] - vq0) * nb[0] + (va[1] - vq1) * nb[1] + (va[2] - vq2) * nb[2];
   float fn = ks * pen - ds * vn;
-  fn = (dd < A.w * A.w && fn > 0.0f) ? fn : 0.0f;
+  fn = (dd < A.w * A.w & fn > 0.0f) ? fn : 0.0f;
 #pragma unroll
   for (int i = 0; i < 3; ++i) F[i] += fn * (R[3 * i] * nb[0] + R[3 * i + 1] * nb[1] + R[3 * i + 2] * nb[2]);
   const float f0 = -fn * nb[0], f1 = -fn * nb[1], f2v = -fn * nb[2];
