@@ -602,9 +602,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // an output (zero reward, post-reset observations, see below)
     bool finite = true;
 #pragma unroll
-    for (int i = 0; i < 13; ++i) finite = finite && fabsf(root[i]) < GO1_DIVERGED;
+    for (int i = 0; i < 13; ++i) finite = finite & (fabsf(root[i]) < GO1_DIVERGED);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) finite = finite && fabsf(q[j]) < GO1_DIVERGED && fabsf(qd[j]) < GO1_DIVERGED;
+    for (int j = 0; j < 3; ++j) finite = finite & (fabsf(q[j]) < GO1_DIVERGED) & (fabsf(qd[j]) < GO1_DIVERGED);
     diverged = qsum(finite ? 0.0f : 1.0f) != 0.0f;
     if (diverged) reset = true;
     if (diverged && sub16 == 0 && A.diverged_count) atomicAdd((unsigned long long*)A.diverged_count, 1ull);

@@ -389,7 +389,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   {
     const float ph = cmd[5], off = cmd[6], bnd = cmd[7];
     const float f0 = ((gait + ph) + off) + bnd, f1 = gait + off, f2_ = gait + bnd, f3 = gait + ph;
-    fi_raw = leg == 0 ? f0 : (leg == 1 ? f1 : (leg == 2 ? f2_ : f3));
+    fi_raw = sel4(leg, f0, f1, f2_, f3);  // (bit-test selects: an equality chain on leg compiles to a switch)
   }
   const float foot_idx = remainder_f(fi_raw, 1.0f);  // self.foot_indices
   float fiw = fi_raw;
@@ -439,9 +439,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (!INJ) {  // native-integrator divergence guard (go1_step.hip): the env is reset, its rewards zeroed
     bool finite = true;
 #pragma unroll
-    for (int i = 0; i < 13; ++i) finite = finite && fabsf(root[i]) < GO1_DIVERGED;
+    for (int i = 0; i < 13; ++i) finite = finite & (fabsf(root[i]) < GO1_DIVERGED);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) finite = finite && fabsf(q[j]) < GO1_DIVERGED && fabsf(qd[j]) < GO1_DIVERGED;
+    for (int j = 0; j < 3; ++j) finite = finite & (fabsf(q[j]) < GO1_DIVERGED) & (fabsf(qd[j]) < GO1_DIVERGED);
     diverged = qsum(finite ? 0.0f : 1.0f) != 0.0f;
     if (diverged) reset = true;
   }
