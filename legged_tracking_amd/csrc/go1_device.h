@@ -236,7 +236,9 @@ __device__ __forceinline__ void mlp_park(const MlpFrag& F, float* s, int lane) {
   for (int k = 0; k < MLP_PARK_FLOATS; ++k) s[k * 64 + lane] = f[k];
 }
 __device__ __forceinline__ void mlp_unpark(MlpFrag& F, const float* s, int lane) {
-  asm volatile("" : "+v"(s));  // opaque: no forwarding of the parked values (they would stay live in registers)
+  // an opaque lane index: no forwarding of the parked values (they would stay live in registers).  (An opaque
+  // pointer would hide that s is LDS: the reads then compile to flat loads, with their longer latency.)
+  asm volatile("" : "+v"(lane));
   float* f = reinterpret_cast<float*>(&F);
 #pragma unroll
   for (int k = 0; k < MLP_PARK_FLOATS; ++k) f[k] = s[k * 64 + lane];
@@ -1003,7 +1005,7 @@ __device__ __forceinline__ f2 f2s(float v) { return f2{v, v}; }
 // the two paths were exec-mask branches every call)
 __device__ __forceinline__ void cell_fetch(const Terr& T, int i, int j, f2& c00, f2& c10, f2& c01, f2& c11) {
   const unsigned li = (unsigned)(i - T.pi0), lj = (unsigned)(j - T.pj0);
-  const bool in = T.patch && li < (unsigned)(PSZX - 1) && lj < (unsigned)(PSZY - 1);
+  const bool in = (T.patch != nullptr) & (li < (unsigned)(PSZX - 1)) & (lj < (unsigned)(PSZY - 1));
   if (T.patch) {
     const float2* pp = T.patch + (in ? (int)(li * PSZY + lj) : 0);
     const float2 q00 = pp[0], q01 = pp[1], q10 = pp[PSZY], q11 = pp[PSZY + 1];
@@ -1170,7 +1172,7 @@ struct SegBest {
 __device__ __forceinline__ void seg_offer(SegBest& sb, f2 h, float z, float r, float t, int cell, bool valid) {
   const int q = seg_quant(fmaxf((h.x - z) + r, (z - h.y) + r));  // (the quantisation is monotone: = the max of both)
   const int key = q * 4096 + (4095 - (int)floorf(t * 4095.0f));
-  const bool up = valid && key > sb.key;  // an equal key (a vertex on several edges) keeps the first offer
+  const bool up = valid & (key > sb.key);  // an equal key (a vertex on several edges) keeps the first offer
   sb.key = up ? key : sb.key;
   sb.t = up ? t : sb.t;
   sb.cell = up ? cell : sb.cell;
@@ -1185,7 +1187,7 @@ __device__ __forceinline__ void verts_fetch(const Terr& T, const int* vi, const 
     for (int n = 0; n < N; ++n) {
       // (unsigned: a negative offset is out of range too; outside the patch read cell 0, replaced below)
       const unsigned li = (unsigned)(vi[n] - T.pi0), lj = (unsigned)(vj[n] - T.pj0);
-      const bool in = li < (unsigned)PSZX && lj < (unsigned)PSZY;
+      const bool in = (li < (unsigned)PSZX) & (lj < (unsigned)PSZY);
       const float2 q = T.patch[in ? (int)(li * PSZY + lj) : 0];
       h[n] = f2{q.x, q.y};
       out |= in ? 0u : 1u << n;
@@ -1446,7 +1448,7 @@ __device__ __forceinline__ void face_scan(const Terr& T, const float* R, const f
     const int v = sub16 + 16 * u;
     const int i = ci + v % FACE_W - 4, j = cj + v / FACE_W - 4;
     const int li = i - T.pi0, lj = j - T.pj0;
-    const bool inp = v < FACE_W * FACE_W && li >= 0 && li < PSZX && lj >= 0 && lj < PSZY;
+    const bool inp = (v < FACE_W * FACE_W) & (li >= 0) & (li < PSZX) & (lj >= 0) & (lj < PSZY);
     const float2 hv = T.patch[min(max(li, 0), PSZX - 1) * PSZY + min(max(lj, 0), PSZY - 1)];
     const float dx = (float)i * T.hs - pos[0], dy = (float)j * T.hs - pos[1];
     const f2 dz = f2{hv.x, hv.y} - pos[2];
@@ -1455,7 +1457,7 @@ __device__ __forceinline__ void face_scan(const Terr& T, const float* R, const f
     const f2 pen = f2{cz.x + th[2], th[2] - cz.y};  // floor vertex above the bottom face / ceiling below the top
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const bool in = inp & fabsf(cx[hh]) <= th[0] & fabsf(cy[hh]) <= th[1] & pen[hh] > -FACE_SIGNED;
+      const bool in = inp & (fabsf(cx[hh]) <= th[0]) & (fabsf(cy[hh]) <= th[1]) & (pen[hh] > -FACE_SIGNED);
       const int q = (int)floorf(fminf(pen[hh] + FACE_SIGNED, 10.0f) * (1.0f / FACE_Q));  // signed depth, offset
       const int k = in ? (q << 7) | (127 - v) : -1;
       key[hh] = max(key[hh], k);
@@ -1491,7 +1493,7 @@ __device__ __forceinline__ void face_force(const Terr& T, const CP& C, const flo
   const f2 pen = f2{cz.x + th[2], th[2] - cz.y};
   bool act[2];
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) act[hh] = ok[hh] & fabsf(cx[hh]) <= th[0] & fabsf(cy[hh]) <= th[1] & pen[hh] > 0.0f;
+  for (int hh = 0; hh < 2; ++hh) act[hh] = ok[hh] & (fabsf(cx[hh]) <= th[0]) & (fabsf(cy[hh]) <= th[1]) & (pen[hh] > 0.0f);
   if (!__any(act[0] || act[1])) return;
   const f2 nz = f2{1.0f, -1.0f};
   // the trunk's velocity at the vertex, base frame: v + w x c
@@ -1504,7 +1506,7 @@ __device__ __forceinline__ void face_force(const Terr& T, const CP& C, const flo
   const f2 vtn = vt2 * ivt, cm = C.mu * fn;
   const f2 ct = f2{(C.kf * vtn.x > cm.x & vtn.x > 1e-9f) ? cm.x * ivt.x : C.kf,
                    (C.kf * vtn.y > cm.y & vtn.y > 1e-9f) ? cm.y * ivt.y : C.kf};
-  const bool ax = act[0] & fn.x > 0.0f, ay = act[1] & fn.y > 0.0f;
+  const bool ax = act[0] & (fn.x > 0.0f), ay = act[1] & (fn.y > 0.0f);
   const f2 fa = f2{ax ? fn.x : 0.0f, ay ? fn.y : 0.0f}, sc = f2{ax ? ct.x : 0.0f, ay ? ct.y : 0.0f};
   const f2 Fx = -(sc * vx), Fy = -(sc * vy), Fz = fa * nz;
   const f2 mx = cy * Fz - cz * Fy, my = cz * Fx - cx * Fz, mz = cx * Fy - cy * Fx;
@@ -1639,7 +1641,7 @@ __device__ __forceinline__ void self_pair_force(const float4* A, const float4* B
   const float vr2 = (va0.z + s * (va1.z - va0.z)) - (vb0.z + t * (vb1.z - vb0.z));
   const float vn = vr0 * n0 + vr1 * n1 + vr2 * n2;
   float fn = ks * pen - ds * vn;
-  fn = (touch & fn > 0.0f) ? fn : 0.0f;
+  fn = (touch & (fn > 0.0f)) ? fn : 0.0f;
   fn = own_first ? fn : -fn;
   F[0] = fn * n0; F[1] = fn * n1; F[2] = fn * n2;
 }
@@ -1667,7 +1669,7 @@ __device__ __forceinline__ void self_box_force(const float4 A, const float4 Av, 
     const float m0 = th[0] - fabsf(c[0]), m1 = th[1] - fabsf(c[1]), m2 = th[2] - fabsf(c[2]);
     const int q0 = (int)floorf(fminf(fmaxf(m0, -1.0f), 1.0f) * 1.0e4f), q1 = (int)floorf(fminf(fmaxf(m1, -1.0f), 1.0f) * 1.0e4f),
               q2 = (int)floorf(fminf(fmaxf(m2, -1.0f), 1.0f) * 1.0e4f);
-    const int ax = (q0 <= q1 && q0 <= q2) ? 0 : (q1 <= q2 ? 1 : 2);
+    const int ax = ((q0 <= q1) & (q0 <= q2)) ? 0 : (q1 <= q2 ? 1 : 2);
     const float sg = c[ax] >= 0.0f ? 1.0f : -1.0f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) nb[i] = i == ax ? sg : 0.0f;
@@ -1683,7 +1685,7 @@ __device__ __forceinline__ void self_box_force(const float4 A, const float4 Av, 
   for (int i = 0; i < 3; ++i) va[i] = R[i] * Av.x + R[3 + i] * Av.y + R[6 + i] * Av.z;
   const float vn = (va[0] - vq0) * nb[0] + (va[1] - vq1) * nb[1] + (va[2] - vq2) * nb[2];
   float fn = ks * pen - ds * vn;
-  fn = (dd < A.w * A.w & fn > 0.0f) ? fn : 0.0f;
+  fn = ((dd < A.w * A.w) & (fn > 0.0f)) ? fn : 0.0f;
 #pragma unroll
   for (int i = 0; i < 3; ++i) F[i] += fn * (R[3 * i] * nb[0] + R[3 * i + 1] * nb[1] + R[3 * i + 2] * nb[2]);
   const float f0 = -fn * nb[0], f1 = -fn * nb[1], f2v = -fn * nb[2];
@@ -1785,7 +1787,7 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
     float F[3], p[3];
     bool touch;
     self_pair_force(Pr + 4 * min(io, ip), Pr + 4 * max(io, ip), first, ks, ds, F, p, touch);
-    if (__any(act && touch)) {
+    if (__any(act & touch)) {
       const float Fw[3] = {act ? F[0] : 0.0f, act ? F[1] : 0.0f, act ? F[2] : 0.0f};
       acc(p, Fw);
     }
@@ -1798,7 +1800,7 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
 #ifdef GO1_ABL_NO_BOXPHASE  // ablation build only: no capsule-box pairs
   bool on = false;
 #else
-  bool on = ((mask >> (6 + leg)) & 1) && role != 1;
+  bool on = ((mask >> (6 + leg)) & 1) & (role != 1);
 #endif
   {
     const float w0[3] = {O0.x - pos[0], O0.y - pos[1], O0.z - pos[2]}, w1[3] = {O1.x - pos[0], O1.y - pos[1], O1.z - pos[2]};
@@ -1806,7 +1808,7 @@ __device__ __forceinline__ void self_narrow(CCfg* __restrict__ cfg, float* sc, i
     for (int i = 0; i < 3; ++i) {
       const float c0 = R[i] * w0[0] + R[3 + i] * w0[1] + R[6 + i] * w0[2];
       const float c1 = R[i] * w1[0] + R[3 + i] * w1[1] + R[6 + i] * w1[2];
-      on = on && fminf(c0, c1) - O0.w <= th[i] && fmaxf(c0, c1) + O0.w >= -th[i];
+      on = on & (fminf(c0, c1) - O0.w <= th[i]) & (fmaxf(c0, c1) + O0.w >= -th[i]);  // (&: && branches)
     }
   }
   if (__any(on)) {

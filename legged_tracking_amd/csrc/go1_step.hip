@@ -342,8 +342,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // compiler would otherwise forward the parked values and keep them in registers after all).
   __shared__ float s_hold[HOLD_N][TPB];
   auto hold = [&](bool park) {
-    float* hp = &s_hold[0][lane];
-    if (!park) asm volatile("" : "+v"(hp));
+    int hl = lane;
+    if (!park) asm volatile("" : "+v"(hl));  // opaque index, not pointer: the reads stay ds_read (not flat)
+    float* hp = &s_hold[0][hl];
     auto f = [&](int k, float& v) { if (park) hp[k * TPB] = v; else v = hp[k * TPB]; };
     auto i = [&](int k, int& v) { float x = __int_as_float(v); f(k, x); v = __float_as_int(x); };
 #pragma unroll
